@@ -1,0 +1,171 @@
+"""bench.py -- AES-256-GCM seal+unseal GiB/s on device-resident packet batches (BASELINE.json).
+
+Workload per rank (BASELINE config 2, the single-GPU headline): 2^20 packets x 1350 B, one key
+(NewAES("AES256Key-32Characters1234567890", salt 00..1f)), AAD = 4-B private IP, explicit seeded
+nonces, slots laid out as Payload.Raw records of 1392 B.  One step = seal every packet, then
+unseal every packet (crypto/aes.go Encrypt then Decrypt), the reference's BenchmarkAES loop body
+(crypto/crypto_test.go:103-131) over a batch.  Multi-GPU: one process per GPU, each sealing its
+own shard (packets are independent: no data-path collective), weak scaling.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from quantum_amd import batch  # noqa: E402
+from quantum_amd.crypto import Context, derive_key  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, MI355X_MICROARCH.md "Chip-level parameters"
+SECRET = b"AES256Key-32Characters1234567890"
+SALT = bytes(range(32))
+AAD = bytes([10, 99, 0, 1])
+
+
+def parse() -> argparse.Namespace:
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--packets", type=int, default=1 << 20, help="packets per GPU")
+    p.add_argument("--len", type=int, default=1350, help="payload bytes per packet")
+    p.add_argument("--stride", type=int, default=0, help="slot stride (0 = smallest 16-B multiple)")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
+    return p.parse_args()
+
+
+def cpu_baseline(key: bytes, L: int, threads: int) -> dict:
+    """OpenSSL EVP AES-256-GCM with crypto/aes.go semantics (oracle/ossl_check.c), host cores."""
+    from oracle import oracle as O
+
+    # calibrate one thread, then size the all-thread sample to ~1.5 s wall (~threads*1.5 s CPU work)
+    n1 = 20000
+    t1 = O.ossl_cpu_baseline(key, 1, n1, L)
+    rate1 = 2 * n1 * L / t1 / 2**30
+    per_thread = max(20000, int(n1 / t1 * 1.5))
+    tN = O.ossl_cpu_baseline(key, threads, per_thread, L)
+    rateN = 2 * threads * per_thread * L / tN / 2**30
+    return {"value": round(rateN, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "sample": (f"{threads} threads x {per_thread} packets x {L} B seal+open, crypto/aes.go semantics "
+                       f"(getrandom nonce/packet, in place, 4-B AAD) on OpenSSL EVP aes-256-gcm; "
+                       f"1 thread: {rate1:.3f} GiB/s over {n1} packets")}
+
+
+def main() -> None:
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", init_method="env://")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    N, L = args.packets, args.len
+    stride = args.stride or batch.slot_stride(L)
+    ctx = Context(device=local, max_keys=16)
+    key = derive_key(SECRET, SALT)  # crypto/aes.go:66, host, once
+    ctx.set_key(0, key)
+
+    arena = torch.zeros(N * stride, dtype=torch.uint8, device=dev)
+    nonces = torch.zeros(12 * N, dtype=torch.uint8, device=dev)
+    status = torch.zeros(N, dtype=torch.uint8, device=dev)
+    aad_word = int.from_bytes(AAD, "little")
+    batch.fill_uniform(arena, stride, N, L, aad_word, 0x5EED0001 + rank, nonces, 0x5EED0002 + rank)
+    stream = torch.cuda.current_stream()
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        batch.seal_uniform(ctx, arena, stride, N, L, 0, nonces, status=None, stream=stream)
+        if ev is not None:
+            ev[1].record(stream)
+        batch.open_uniform(ctx, arena, stride, N, L + 28, 0, status=status, stream=stream)
+        if ev is not None:
+            ev[2].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    ok = int(status.sum().item()) == N
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(evs[k])
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        okt = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+        ok = bool(okt.item())
+
+    seal_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
+    open_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
+    ms_step = elapsed * 1e3 / args.steps
+    total_bytes = world * 2 * N * L  # each payload byte counted once sealed and once unsealed
+    value = total_bytes / (elapsed / args.steps) / 2**30
+
+    # dominant kernel roofline: algorithmic bytes per launch: seal 2L+44, open 2L+32
+    if seal_ms >= open_ms:
+        kname, kms, per_pkt = "seal", seal_ms, 2 * L + 44
+    else:
+        kname, kms, per_pkt = "open", open_ms, 2 * L + 32
+    achieved = N * per_pkt / (kms * 1e-3) / 1e9
+
+    if rank == 0:
+        line = {
+            "metric": "AES-256-GCM seal+unseal GiB/s (device-resident packets) at 1/2/4/8 MI355X",
+            "value": round(value, 2),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (seeded splitmix64 payloads and nonces, one PBKDF2-derived key)",
+            "config": {"workload": f"config2: {N} x {L} B packets per GPU, seal then unseal, 1 key, AAD 4 B",
+                       "packets_per_gpu": N, "payload_len": L, "slot_stride": stride,
+                       "parallelism": f"replicas/shards x{world}, no collectives"},
+            "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "bytes_per_packet": per_pkt, "kernel_ms": round(kms, 4)},
+            "kernels_ms": {"seal": round(seal_ms, 4), "open": round(open_ms, 4)},
+            "status_ok": ok,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+            line["cpu_baseline"] = cpu_baseline(key, L, threads)
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,139 @@
+/*
+ * qgcm.h -- C ABI of the MI355X-native AES-256-GCM packet sealer (libqgcm.so).
+ *
+ * This is the drop-in boundary for quantum's Encryption plugin path.  Every entry point
+ * names the reference interface it replaces (paths relative to the quantum tree):
+ *
+ *   crypto/aes.go:22-26   type AES {block, aead, salt}        -> qgcm_ctx + key slot (key_idx)
+ *   crypto/aes.go:65-83   NewAES(secret, salt)                -> qgcm_derive_key + qgcm_set_key
+ *   crypto/aes.go:41-52   (*AES).Encrypt(data, length, aad)   -> qgcm_seal_one / qgcm_seal_batch
+ *   crypto/aes.go:57-62   (*AES).Decrypt(data, aad)           -> qgcm_open_one / qgcm_open_batch
+ *   crypto/aes.go:29-36   EncryptedSize / DecryptedSize       -> QGCM_OVERHEAD (= 16 + 12)
+ *   crypto/ecdh.go:13-31  GenerateECKeyPair / GenerateSharedSecret -> qgcm_x25519*
+ *   plugin/encryption.go:16-40 Encryption.Apply calls Encrypt/Decrypt per packet; the batch
+ *                         entry points are what a coalescing Apply shim drives.
+ *
+ * Error convention follows the reference's own cgo layer (crypto/dtls.go:37-40, dtls.h:43-48):
+ * constructors return NULL and fill a caller-supplied error buffer; everything else returns
+ * a negative QGCM_E* code (see qgcm_strerror) or, for the per-packet calls, -1 exactly where the
+ * Go method returns an error.  All functions are thread-safe unless stated otherwise.
+ *
+ * Packet slot layout (common/payload.go:7-45, common/common.go:16-38): a slot is one
+ * common.Payload.Raw buffer: [0:4) sender private IPv4 = the GCM additional data,
+ * [4:4+L) payload.  Sealing writes ct over the payload, then tag (16 B) and nonce (12 B):
+ * [4:4+L) ct, [4+L:4+L+16) tag, [4+L+16:4+L+28) nonce -- exactly crypto/aes.go:49-51.
+ * Slot offsets must be multiples of 4; slots need capacity 4+L+28 bytes.
+ *
+ * Device pointers are HIP device pointers on the context's device; `stream` is a hipStream_t
+ * (NULL = the null stream).  Batch calls are asynchronous with respect to the host.
+ */
+#ifndef QGCM_H
+#define QGCM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define QGCM_KEY_BYTES 32    /* crypto/crypto.go:7 keyLength */
+#define QGCM_SALT_BYTES 32   /* crypto/aes.go:17 SaltLength */
+#define QGCM_NONCE_BYTES 12  /* cipher.NewGCM standard nonce */
+#define QGCM_TAG_BYTES 16    /* cipher.NewGCM standard tag (aead.Overhead()) */
+#define QGCM_OVERHEAD 28     /* EncryptedSize - len = Overhead + NonceSize, crypto/aes.go:29-36 */
+#define QGCM_PBKDF2_ITERS 10000 /* crypto/aes.go:18 */
+#define QGCM_ERRLEN 120      /* crypto/dtls.go:23 errorLen */
+
+/* status codes */
+#define QGCM_OK 0
+#define QGCM_E_ARG -1       /* bad argument / size */
+#define QGCM_E_HIP -2       /* HIP runtime error */
+#define QGCM_E_KEY -3       /* key index not set or out of range */
+#define QGCM_E_AUTH -4      /* message authentication failed (errOpen) */
+#define QGCM_E_NOMEM -5
+
+typedef struct qgcm_ctx qgcm_ctx;
+
+/* One packet descriptor of a device batch.  For seal, len = payload length L
+ * (Encrypt's `length`); for open, len = sealed length L+28 (len(Payload.Packet) as
+ * passed to Decrypt).  offset = byte offset of the slot (the Raw buffer) in the arena. */
+typedef struct qgcm_desc {
+    uint64_t offset;
+    uint32_t len;
+    uint32_t key_idx;
+} qgcm_desc;
+
+/* ---- context (replaces the per-process Go AEAD objects) ---- */
+qgcm_ctx *qgcm_create(int device, uint32_t max_keys, char *err, int errlen);
+void qgcm_destroy(qgcm_ctx *ctx);
+const char *qgcm_strerror(int code);
+const char *qgcm_version(void);
+
+/* ---- key setup: crypto/aes.go:65-83 NewAES, common/mapping.go:90-99 ---- */
+/* key = PBKDF2-HMAC-SHA512(secret, salt, 10000, 32)  (crypto/aes.go:66) -- host */
+int qgcm_derive_key(const uint8_t *secret, size_t secret_len, const uint8_t *salt, size_t salt_len,
+                    uint8_t key[QGCM_KEY_BYTES]);
+/* Batched: keys[i] = PBKDF2(secrets[i], salts[i]) for count peers, multithreaded host. */
+int qgcm_derive_keys(const uint8_t *secrets, const uint8_t *salts, uint32_t count, uint8_t *keys);
+/* aes.NewCipher + cipher.NewGCM (crypto/aes.go:68-76): expands round keys and the GHASH
+ * tables on the device for slot key_idx.  Synchronous. */
+int qgcm_set_key(qgcm_ctx *ctx, uint32_t key_idx, const uint8_t key[QGCM_KEY_BYTES]);
+int qgcm_set_keys(qgcm_ctx *ctx, uint32_t first_idx, uint32_t count, const uint8_t *keys);
+/* X25519 (crypto/ecdh.go:13-31): pub = X25519(priv, 9); secret = X25519(priv, peer_pub). */
+int qgcm_x25519_base(uint8_t pub[32], const uint8_t priv[32]);
+int qgcm_x25519(uint8_t secret[32], const uint8_t priv[32], const uint8_t peer_pub[32]);
+
+/* ---- device batches (the throughput path) ---- */
+/* Seal n packets in place.  nonces: device array of n*12 bytes (nonce i for packet i, written
+ * into the slot like crypto/aes.go:50), or NULL to use the nonce already present at
+ * [4+L+16, 4+L+28) of each slot.  aad_len: 0 (nil additional) or 4 (the Payload IP header).
+ * status (device, n bytes, may be NULL): 1 = sealed, 0 = rejected (bad key index). */
+int qgcm_seal_batch(qgcm_ctx *ctx, uint8_t *d_arena, const qgcm_desc *d_descs, uint32_t n,
+                    const uint8_t *d_nonces, uint32_t aad_len, uint8_t *d_status, void *stream);
+/* Open n packets in place.  status[i] = 1 if authentic (plaintext at [4, 4+len-28)),
+ * 0 on errOpen (tag mismatch: plaintext region zeroed as Go 1.9 gcm.Open does;
+ * len < 28: slot untouched). */
+int qgcm_open_batch(qgcm_ctx *ctx, uint8_t *d_arena, const qgcm_desc *d_descs, uint32_t n,
+                    uint32_t aad_len, uint8_t *d_status, void *stream);
+/* Uniform batches: slot i at i*stride, same length and key for all packets (no descriptor
+ * traffic).  seal: len = L; open: len = L + 28. */
+int qgcm_seal_uniform(qgcm_ctx *ctx, uint8_t *d_arena, uint64_t stride, uint32_t n, uint32_t len,
+                      uint32_t key_idx, const uint8_t *d_nonces, uint32_t aad_len,
+                      uint8_t *d_status, void *stream);
+int qgcm_open_uniform(qgcm_ctx *ctx, uint8_t *d_arena, uint64_t stride, uint32_t n, uint32_t len,
+                      uint32_t key_idx, uint32_t aad_len, uint8_t *d_status, void *stream);
+
+/* ---- per-packet host calls, the exact Encrypt/Decrypt contract ---- */
+/* crypto/aes.go:41-52: seals data[0:length] in place, appends tag and nonce; data must have
+ * capacity length+28.  nonce NULL -> 12 fresh bytes from getrandom(2) as crypto/rand does.
+ * aad may be NULL (aad_len 0).  Returns length+28, or -1. */
+long qgcm_seal_one(qgcm_ctx *ctx, uint32_t key_idx, uint8_t *data, long length, const uint8_t *aad,
+                   uint32_t aad_len, const uint8_t *nonce);
+/* crypto/aes.go:57-62: opens data[0:len] in place.  Returns len-28, or -1 (errOpen; data[0:len-28]
+ * zeroed on tag mismatch; len < 28 leaves data untouched -- the reference panics below 12). */
+long qgcm_open_one(qgcm_ctx *ctx, uint32_t key_idx, uint8_t *data, long len, const uint8_t *aad,
+                   uint32_t aad_len);
+
+/* ---- host batches through pinned staging (end-to-end incl. PCIe) ---- */
+/* Slots in host memory at i*stride; copies in, runs the device batch, copies back.  Returns
+ * the number of packets that failed (0 = all ok) or a negative error.  status may be NULL. */
+int qgcm_seal_host(qgcm_ctx *ctx, uint8_t *h_arena, uint64_t stride, uint32_t n, uint32_t len,
+                   uint32_t key_idx, const uint8_t *h_nonces, uint32_t aad_len, uint8_t *h_status);
+int qgcm_open_host(qgcm_ctx *ctx, uint8_t *h_arena, uint64_t stride, uint32_t n, uint32_t len,
+                   uint32_t key_idx, uint32_t aad_len, uint8_t *h_status);
+
+/* ---- nonce source for production seals (crypto/aes.go:42-47 draws per packet) ---- */
+/* Fills n*12 bytes of host memory from getrandom(2). */
+int qgcm_random_nonces(uint8_t *h_out, uint32_t n);
+
+/* ---- synthetic workload generator (bench/tests; BASELINE.json configs) ---- */
+/* Slot i at i*stride: [aad_word LE][payload L bytes of the splitmix64(seed_payload) stream at
+ * byte offset i*L]; nonces[i*12..] = splitmix64(seed_nonce) stream at byte offset i*12. */
+int qgcm_fill_uniform(uint8_t *d_arena, uint64_t stride, uint32_t n, uint32_t len, uint32_t aad_word,
+                      uint64_t seed_payload, uint8_t *d_nonces, uint64_t seed_nonce, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* QGCM_H */

@@ -1,0 +1,285 @@
+/*
+ * oracle/gcm_oracle.c -- TEST INFRASTRUCTURE ONLY (the parity checker).
+ *
+ * Plain-C CPU restatement of quantum's per-packet encryption path:
+ *   crypto/aes.go:41-52   AES.Encrypt  (seal in place, ct||tag||nonce framing)
+ *   crypto/aes.go:57-62   AES.Decrypt  (open in place, nonce = last 12 B)
+ *   crypto/aes.go:29-36   EncryptedSize / DecryptedSize (+28 / -28)
+ *   crypto/aes.go:68-76   aes.NewCipher + cipher.NewGCM (AES-256, 12-B nonce, 16-B tag)
+ * The arithmetic underneath lives in the Go 1.9 standard library (crypto/aes,
+ * crypto/cipher gcm.go; Go version pinned by dist/docker/Dockerfile.builder:6),
+ * which is NOT under /root/reference.  It implements FIPS-197 AES and
+ * NIST SP 800-38D GCM; this file restates those published algorithms directly:
+ * byte-oriented AES (FIPS-197 s5.1-5.3), bit-serial GF(2^128) multiply
+ * (SP 800-38D Algorithm 1), GHASH/GCTR (Algorithms 2-4).
+ *
+ * Parity pinning (see tests/test_oracle.py): NIST GCM spec test cases 13-16
+ * (the AES-256 cases of McGrew & Viega's GCM submission) and an independent
+ * OpenSSL EVP_aes_256_gcm implementation (oracle/ossl_check.c).
+ *
+ * Go-specific semantics restated here (Go 1.9 crypto/cipher/gcm.go Open):
+ *   - on tag mismatch the plaintext region data[0:L] is ZEROED and errOpen returned;
+ *   - a ciphertext shorter than the tag -> errOpen, buffer untouched;
+ *   - len(data) < 12 panics in the reference (negative slice, crypto/aes.go:58-59);
+ *     here it returns -1 (documented divergence).
+ *
+ * Must never be linked into or called by the product path (quantum_amd/).
+ */
+#include <stdint.h>
+#include <stddef.h>
+#include <string.h>
+
+/* ---------------- FIPS-197 AES-256 (byte oriented) ---------------- */
+
+static uint8_t SBOX[256];
+static int sbox_ready = 0;
+
+static uint8_t gf8_mul(uint8_t a, uint8_t b) {
+    uint8_t p = 0;
+    for (int i = 0; i < 8; i++) {
+        if (b & 1) p ^= a;
+        uint8_t hi = a & 0x80;
+        a <<= 1;
+        if (hi) a ^= 0x1b;
+        b >>= 1;
+    }
+    return p;
+}
+
+static uint8_t rotl8(uint8_t x, int s) { return (uint8_t)((x << s) | (x >> (8 - s))); }
+
+/* S-box from its definition (FIPS-197 s5.1.1): multiplicative inverse then affine map. */
+static void build_sbox(void) {
+    if (sbox_ready) return;
+    for (int x = 0; x < 256; x++) {
+        uint8_t inv = 0;
+        if (x) {
+            /* x^254 = x^-1 in GF(2^8) */
+            uint8_t r = 1, b = (uint8_t)x;
+            int e = 254;
+            while (e) {
+                if (e & 1) r = gf8_mul(r, b);
+                b = gf8_mul(b, b);
+                e >>= 1;
+            }
+            inv = r;
+        }
+        SBOX[x] = inv ^ rotl8(inv, 1) ^ rotl8(inv, 2) ^ rotl8(inv, 3) ^ rotl8(inv, 4) ^ 0x63;
+    }
+    sbox_ready = 1;
+}
+
+/* KeyExpansion, Nk = 8, Nr = 14 -> 240 bytes of round keys (FIPS-197 s5.2). */
+void oracle_aes256_expand(const uint8_t key[32], uint8_t rk[240]) {
+    build_sbox();
+    memcpy(rk, key, 32);
+    uint8_t rcon = 1;
+    for (int i = 8; i < 60; i++) {
+        uint8_t t[4];
+        memcpy(t, rk + 4 * (i - 1), 4);
+        if (i % 8 == 0) {
+            uint8_t t0 = t[0];
+            t[0] = SBOX[t[1]] ^ rcon;
+            t[1] = SBOX[t[2]];
+            t[2] = SBOX[t[3]];
+            t[3] = SBOX[t0];
+            rcon = gf8_mul(rcon, 2);
+        } else if (i % 8 == 4) {
+            for (int j = 0; j < 4; j++) t[j] = SBOX[t[j]];
+        }
+        for (int j = 0; j < 4; j++) rk[4 * i + j] = rk[4 * (i - 8) + j] ^ t[j];
+    }
+}
+
+/* Cipher (FIPS-197 s5.1); state byte (r,c) at index r + 4c. */
+void oracle_aes256_encrypt_block(const uint8_t rk[240], const uint8_t in[16], uint8_t out[16]) {
+    uint8_t s[16], t[16];
+    build_sbox();
+    for (int i = 0; i < 16; i++) s[i] = in[i] ^ rk[i];
+    for (int round = 1; round <= 14; round++) {
+        /* SubBytes + ShiftRows: new(r,c) = S(old(r, c+r mod 4)) */
+        for (int c = 0; c < 4; c++)
+            for (int r = 0; r < 4; r++) t[r + 4 * c] = SBOX[s[r + 4 * ((c + r) & 3)]];
+        if (round != 14) {
+            for (int c = 0; c < 4; c++) {
+                uint8_t a0 = t[4 * c], a1 = t[4 * c + 1], a2 = t[4 * c + 2], a3 = t[4 * c + 3];
+                s[4 * c + 0] = gf8_mul(a0, 2) ^ gf8_mul(a1, 3) ^ a2 ^ a3;
+                s[4 * c + 1] = a0 ^ gf8_mul(a1, 2) ^ gf8_mul(a2, 3) ^ a3;
+                s[4 * c + 2] = a0 ^ a1 ^ gf8_mul(a2, 2) ^ gf8_mul(a3, 3);
+                s[4 * c + 3] = gf8_mul(a0, 3) ^ a1 ^ a2 ^ gf8_mul(a3, 2);
+            }
+        } else {
+            memcpy(s, t, 16);
+        }
+        for (int i = 0; i < 16; i++) s[i] ^= rk[16 * round + i];
+    }
+    memcpy(out, s, 16);
+}
+
+/* ---------------- SP 800-38D GHASH / GCTR ---------------- */
+
+/* Algorithm 1: Z = X * Y in GF(2^128), bit 0 = MSB of byte 0, R = 11100001 || 0^120. */
+void oracle_gf128_mul(const uint8_t X[16], const uint8_t Y[16], uint8_t Z[16]) {
+    uint8_t z[16] = {0}, v[16];
+    memcpy(v, Y, 16);
+    for (int i = 0; i < 128; i++) {
+        if ((X[i >> 3] >> (7 - (i & 7))) & 1)
+            for (int j = 0; j < 16; j++) z[j] ^= v[j];
+        int lsb = v[15] & 1;
+        for (int j = 15; j > 0; j--) v[j] = (uint8_t)((v[j] >> 1) | (v[j - 1] << 7));
+        v[0] >>= 1;
+        if (lsb) v[0] ^= 0xe1;
+    }
+    memcpy(Z, z, 16);
+}
+
+static void ghash_update(const uint8_t H[16], uint8_t Y[16], const uint8_t *data, size_t len) {
+    while (len) {
+        uint8_t blk[16] = {0};
+        size_t n = len < 16 ? len : 16;
+        memcpy(blk, data, n);
+        for (int j = 0; j < 16; j++) Y[j] ^= blk[j];
+        oracle_gf128_mul(Y, H, Y);
+        data += n;
+        len -= n;
+    }
+}
+
+/* Algorithm 2 over A || pad || C || pad || [len(A)]_64 || [len(C)]_64 */
+void oracle_ghash(const uint8_t H[16], const uint8_t *aad, size_t aad_len,
+                  const uint8_t *c, size_t c_len, uint8_t S[16]) {
+    uint8_t Y[16] = {0}, L[16];
+    ghash_update(H, Y, aad, aad_len);
+    ghash_update(H, Y, c, c_len);
+    uint64_t abits = (uint64_t)aad_len * 8, cbits = (uint64_t)c_len * 8;
+    for (int j = 0; j < 8; j++) {
+        L[j] = (uint8_t)(abits >> (56 - 8 * j));
+        L[8 + j] = (uint8_t)(cbits >> (56 - 8 * j));
+    }
+    ghash_update(H, Y, L, 16);
+    memcpy(S, Y, 16);
+}
+
+static void inc32(uint8_t cb[16]) {
+    for (int j = 15; j >= 12; j--)
+        if (++cb[j]) break;
+}
+
+/* Algorithm 3 (GCTR), in place allowed. */
+static void gctr(const uint8_t rk[240], const uint8_t icb[16], const uint8_t *in, uint8_t *out, size_t len) {
+    uint8_t cb[16], ks[16];
+    memcpy(cb, icb, 16);
+    while (len) {
+        size_t n = len < 16 ? len : 16;
+        oracle_aes256_encrypt_block(rk, cb, ks);
+        for (size_t j = 0; j < n; j++) out[j] = in[j] ^ ks[j];
+        inc32(cb);
+        in += n;
+        out += n;
+        len -= n;
+    }
+}
+
+/* Algorithm 4 (GCM-AE) with a 96-bit IV: J0 = IV || 0^31 || 1. */
+void oracle_gcm_seal(const uint8_t key[32], const uint8_t iv[12], const uint8_t *aad, size_t aad_len,
+                     const uint8_t *pt, size_t len, uint8_t *ct, uint8_t tag[16]) {
+    uint8_t rk[240], H[16] = {0}, J0[16], icb[16], S[16], EJ0[16];
+    oracle_aes256_expand(key, rk);
+    oracle_aes256_encrypt_block(rk, H, H);
+    memcpy(J0, iv, 12);
+    J0[12] = J0[13] = J0[14] = 0;
+    J0[15] = 1;
+    memcpy(icb, J0, 16);
+    inc32(icb);
+    gctr(rk, icb, pt, ct, len);
+    oracle_ghash(H, aad, aad_len, ct, len, S);
+    oracle_aes256_encrypt_block(rk, J0, EJ0);
+    for (int j = 0; j < 16; j++) tag[j] = EJ0[j] ^ S[j];
+}
+
+/* Algorithm 5 (GCM-AD). Returns 0 on success, -1 on FAIL (pt untouched here). */
+int oracle_gcm_open(const uint8_t key[32], const uint8_t iv[12], const uint8_t *aad, size_t aad_len,
+                    const uint8_t *ct, size_t len, const uint8_t tag[16], uint8_t *pt) {
+    uint8_t rk[240], H[16] = {0}, J0[16], icb[16], S[16], EJ0[16];
+    oracle_aes256_expand(key, rk);
+    oracle_aes256_encrypt_block(rk, H, H);
+    memcpy(J0, iv, 12);
+    J0[12] = J0[13] = J0[14] = 0;
+    J0[15] = 1;
+    oracle_ghash(H, aad, aad_len, ct, len, S);
+    oracle_aes256_encrypt_block(rk, J0, EJ0);
+    uint8_t diff = 0;
+    for (int j = 0; j < 16; j++) diff |= (uint8_t)(EJ0[j] ^ S[j] ^ tag[j]);
+    if (diff) return -1;
+    memcpy(icb, J0, 16);
+    inc32(icb);
+    gctr(rk, icb, ct, pt, len);
+    return 0;
+}
+
+/* ---------------- crypto/aes.go framing ---------------- */
+
+/* crypto/aes.go:41-52 AES.Encrypt with the nonce injected (the reference draws it
+ * from crypto/rand at :42-47).  data must hold length + 28 bytes.
+ * Returns EncryptedSize = length + 16 + 12 (crypto/aes.go:29-31). */
+long oracle_aesgo_encrypt(const uint8_t key[32], uint8_t *data, long length,
+                          const uint8_t *aad, long aad_len, const uint8_t nonce[12]) {
+    uint8_t tag[16], n[12];
+    if (length < 0) return -1;
+    memcpy(n, nonce, 12);                      /* nonce may alias data */
+    oracle_gcm_seal(key, n, aad, (size_t)aad_len, data, (size_t)length, data, tag); /* :49 Seal(data[:0],...) */
+    memcpy(data + length, tag, 16);            /* tag appended by Seal */
+    memcpy(data + length + 16, n, 12);         /* :50 copy(data[length+Overhead:], nonce) */
+    return length + 28;                        /* :51 */
+}
+
+/* crypto/aes.go:57-62 AES.Decrypt: nonce = data[len-12:], tag = the 16 B before it.
+ * Returns DecryptedSize = len - 28 on success, -1 on error (errOpen).
+ * Go 1.9 gcm Open zeroes the would-be plaintext data[0:len-28] on tag mismatch. */
+long oracle_aesgo_decrypt(const uint8_t key[32], uint8_t *data, long len,
+                          const uint8_t *aad, long aad_len) {
+    if (len < 12) return -1;                   /* reference panics here (negative slice) */
+    long length = len - 12;                    /* :58 */
+    const uint8_t *nonce = data + length;      /* :59 */
+    if (length < 16) return -1;                /* Open: ciphertext shorter than tag -> errOpen */
+    long L = length - 16;
+    uint8_t n[12], tag[16];
+    memcpy(n, nonce, 12);
+    memcpy(tag, data + L, 16);
+    if (oracle_gcm_open(key, n, aad, (size_t)aad_len, data, (size_t)L, tag, data) != 0) {
+        memset(data, 0, (size_t)L);            /* Go 1.9 gcm.go Open: zero out on mismatch */
+        return -1;
+    }
+    return L;                                  /* :61 DecryptedSize */
+}
+
+/* ---------------- synthetic batch generator (BASELINE configs) ---------------- */
+
+/* splitmix64 output k for a seed (random access form): the k-th output of the
+ * sequential generator started at `seed`. */
+uint64_t oracle_splitmix64_at(uint64_t seed, uint64_t k) {
+    uint64_t z = seed + (k + 1) * 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+/* Byte b of the little-endian splitmix64 stream. */
+static inline uint8_t stream_byte(uint64_t seed, uint64_t b) {
+    return (uint8_t)(oracle_splitmix64_at(seed, b >> 3) >> (8 * (b & 7)));
+}
+
+void oracle_fill_stream(uint64_t seed, uint64_t byte_offset, uint8_t *dst, size_t n) {
+    for (size_t i = 0; i < n; i++) dst[i] = stream_byte(seed, byte_offset + i);
+}
+
+/* Seal a uniform batch laid out as common.Payload.Raw slots (common/payload.go:22-32):
+ * slot i at arena + i*stride: [aad (aad_len B)] [payload L] [tag 16] [nonce 12].
+ * nonces: n*12 bytes.  Used to cross-check the device path on small batches. */
+void oracle_seal_uniform(const uint8_t key[32], uint8_t *arena, size_t stride, long n, long L,
+                         long aad_len, const uint8_t *nonces) {
+    for (long i = 0; i < n; i++) {
+        uint8_t *raw = arena + (size_t)i * stride;
+        oracle_aesgo_encrypt(key, raw + 4, L, aad_len ? raw : NULL, aad_len, nonces + 12 * i);
+    }
+}

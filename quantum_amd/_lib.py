@@ -1,0 +1,97 @@
+"""ctypes binding of libqgcm.so (include/qgcm.h).
+
+The library is the product: every packet is sealed/opened by the gfx950 kernels inside it.
+There is no Python or CPU fallback -- if the shared object is missing or no gfx950 device is
+present, loading/creating a context raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libqgcm.so")
+
+# Every symbol include/qgcm.h declares (checked by tests/test_abi.py).
+EXPORTS = (
+    "qgcm_create", "qgcm_destroy", "qgcm_strerror", "qgcm_version",
+    "qgcm_derive_key", "qgcm_derive_keys", "qgcm_set_key", "qgcm_set_keys",
+    "qgcm_x25519_base", "qgcm_x25519",
+    "qgcm_seal_batch", "qgcm_open_batch", "qgcm_seal_uniform", "qgcm_open_uniform",
+    "qgcm_seal_one", "qgcm_open_one", "qgcm_seal_host", "qgcm_open_host",
+    "qgcm_random_nonces", "qgcm_fill_uniform",
+)
+
+QGCM_OK = 0
+QGCM_E_ARG = -1
+QGCM_E_HIP = -2
+QGCM_E_KEY = -3
+QGCM_E_AUTH = -4
+QGCM_E_NOMEM = -5
+OVERHEAD = 28
+ERRLEN = 120
+
+
+class QgcmError(RuntimeError):
+    pass
+
+
+class Desc(C.Structure):
+    """qgcm_desc: {offset u64, len u32, key_idx u32} -- 16 bytes."""
+
+    _fields_ = [("offset", C.c_uint64), ("len", C.c_uint32), ("key_idx", C.c_uint32)]
+
+
+_lib: C.CDLL | None = None
+
+
+def _bind(L: C.CDLL) -> None:
+    vp, u8p, sz, u32, u64, i32, lng = C.c_void_p, C.c_char_p, C.c_size_t, C.c_uint32, C.c_uint64, C.c_int, C.c_long
+    L.qgcm_create.argtypes = [i32, u32, C.c_char_p, i32]
+    L.qgcm_create.restype = vp
+    L.qgcm_destroy.argtypes = [vp]
+    L.qgcm_destroy.restype = None
+    L.qgcm_strerror.argtypes = [i32]
+    L.qgcm_strerror.restype = C.c_char_p
+    L.qgcm_version.restype = C.c_char_p
+    L.qgcm_derive_key.argtypes = [u8p, sz, u8p, sz, u8p]
+    L.qgcm_derive_keys.argtypes = [u8p, u8p, u32, u8p]
+    L.qgcm_set_key.argtypes = [vp, u32, u8p]
+    L.qgcm_set_keys.argtypes = [vp, u32, u32, u8p]
+    L.qgcm_x25519_base.argtypes = [u8p, u8p]
+    L.qgcm_x25519.argtypes = [u8p, u8p, u8p]
+    L.qgcm_seal_batch.argtypes = [vp, vp, vp, u32, vp, u32, vp, vp]
+    L.qgcm_open_batch.argtypes = [vp, vp, vp, u32, u32, vp, vp]
+    L.qgcm_seal_uniform.argtypes = [vp, vp, u64, u32, u32, u32, vp, u32, vp, vp]
+    L.qgcm_open_uniform.argtypes = [vp, vp, u64, u32, u32, u32, u32, vp, vp]
+    L.qgcm_seal_one.argtypes = [vp, u32, vp, lng, vp, u32, vp]
+    L.qgcm_seal_one.restype = lng
+    L.qgcm_open_one.argtypes = [vp, u32, vp, lng, vp, u32]
+    L.qgcm_open_one.restype = lng
+    L.qgcm_seal_host.argtypes = [vp, vp, u64, u32, u32, u32, vp, u32, vp]
+    L.qgcm_open_host.argtypes = [vp, vp, u64, u32, u32, u32, u32, vp]
+    L.qgcm_random_nonces.argtypes = [vp, u32]
+    L.qgcm_fill_uniform.argtypes = [vp, u64, u32, u32, u32, u64, vp, u64, vp]
+
+
+def lib() -> C.CDLL:
+    """Load libqgcm.so (built in-tree by __graft_entry__.build())."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise QgcmError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+        # Share torch's HIP runtime (same SONAME libamdhip64.so.7) when torch is present: import it first.
+        try:
+            import torch  # noqa: F401
+        except Exception:  # pragma: no cover - torch is plumbing only
+            pass
+        L = C.CDLL(LIB_PATH)
+        _bind(L)
+        _lib = L
+    return _lib
+
+
+def check(rc: int, what: str) -> int:
+    if rc < 0:
+        raise QgcmError(f"{what}: {lib().qgcm_strerror(rc).decode()} ({rc})")
+    return rc

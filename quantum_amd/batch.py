@@ -1,0 +1,78 @@
+"""Device-resident packet batches: the throughput path behind a coalescing Encryption.Apply.
+
+Slots are common.Payload.Raw buffers laid end to end in one HBM arena (include/qgcm.h).  Torch
+is used only as the device allocator and for stream handles; the work is done by libqgcm.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from . import _lib
+from .crypto import Context
+
+AAD_LEN = 4  # the Payload IP header is the additional data (plugin/encryption.go:22,31)
+
+
+def _stream_handle(stream: torch.cuda.Stream | None) -> int:
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return int(s.cuda_stream)
+
+
+def _ptr(t: torch.Tensor | None) -> int | None:
+    return None if t is None else int(t.data_ptr())
+
+
+def slot_stride(max_len: int) -> int:
+    """Smallest 16-byte multiple holding [aad 4][payload][tag 16][nonce 12]."""
+    return (4 + max_len + _lib.OVERHEAD + 15) & ~15
+
+
+def seal_uniform(ctx: Context, arena: torch.Tensor, stride: int, n: int, length: int, key_idx: int,
+                 nonces: torch.Tensor | None = None, aad_len: int = AAD_LEN, status: torch.Tensor | None = None,
+                 stream: torch.cuda.Stream | None = None) -> None:
+    _lib.check(_lib.lib().qgcm_seal_uniform(ctx.handle, _ptr(arena), stride, n, length, key_idx, _ptr(nonces),
+                                            aad_len, _ptr(status), _stream_handle(stream)), "qgcm_seal_uniform")
+
+
+def open_uniform(ctx: Context, arena: torch.Tensor, stride: int, n: int, sealed_len: int, key_idx: int,
+                 aad_len: int = AAD_LEN, status: torch.Tensor | None = None,
+                 stream: torch.cuda.Stream | None = None) -> None:
+    _lib.check(_lib.lib().qgcm_open_uniform(ctx.handle, _ptr(arena), stride, n, sealed_len, key_idx, aad_len,
+                                            _ptr(status), _stream_handle(stream)), "qgcm_open_uniform")
+
+
+def make_descs(offsets, lengths, keys, device) -> torch.Tensor:
+    """Pack qgcm_desc records ({u64 offset, u32 len, u32 key_idx}) into a device uint8 tensor."""
+    off = torch.as_tensor(offsets, dtype=torch.int64).reshape(-1, 1)
+    ln = torch.as_tensor(lengths, dtype=torch.int64).reshape(-1, 1)
+    ky = torch.as_tensor(keys, dtype=torch.int64).reshape(-1, 1)
+    words = torch.cat([off & 0xFFFFFFFF, off >> 32, ln, ky], dim=1).to(torch.int64)
+    words = torch.where(words >= 2**31, words - 2**32, words).to(torch.int32)
+    return words.contiguous().view(torch.uint8).reshape(-1).to(device)
+
+
+def seal_batch(ctx: Context, arena: torch.Tensor, descs: torch.Tensor, n: int, nonces: torch.Tensor | None = None,
+               aad_len: int = AAD_LEN, status: torch.Tensor | None = None,
+               stream: torch.cuda.Stream | None = None) -> None:
+    _lib.check(_lib.lib().qgcm_seal_batch(ctx.handle, _ptr(arena), _ptr(descs), n, _ptr(nonces), aad_len,
+                                          _ptr(status), _stream_handle(stream)), "qgcm_seal_batch")
+
+
+def open_batch(ctx: Context, arena: torch.Tensor, descs: torch.Tensor, n: int, aad_len: int = AAD_LEN,
+               status: torch.Tensor | None = None, stream: torch.cuda.Stream | None = None) -> None:
+    _lib.check(_lib.lib().qgcm_open_batch(ctx.handle, _ptr(arena), _ptr(descs), n, aad_len, _ptr(status),
+                                          _stream_handle(stream)), "qgcm_open_batch")
+
+
+def fill_uniform(arena: torch.Tensor, stride: int, n: int, length: int, aad_word: int, seed_payload: int,
+                 nonces: torch.Tensor | None, seed_nonce: int, stream: torch.cuda.Stream | None = None) -> None:
+    """Synthetic slots: payload = splitmix64(seed_payload) stream bytes [i*L, (i+1)*L)."""
+    _lib.check(_lib.lib().qgcm_fill_uniform(_ptr(arena), stride, n, length, aad_word, seed_payload, _ptr(nonces),
+                                            seed_nonce, _stream_handle(stream)), "qgcm_fill_uniform")
+
+
+def host_ptr(buf: bytearray) -> tuple[int, object]:
+    arr = (C.c_uint8 * len(buf)).from_buffer(buf)
+    return C.addressof(arr), arr

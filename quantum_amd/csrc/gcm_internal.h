@@ -1,0 +1,54 @@
+// Internal interface between the C ABI (qgcm_api.cpp) and the gfx950 kernels (gcm_kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/qgcm.h"
+
+namespace qgcm {
+
+// Workgroup shape of the packet kernels: 8 wave64s, one workgroup per CU (LDS-bound design,
+// see DESIGN.md "Kernel").
+constexpr int kWaves = 8;
+constexpr int kThreads = kWaves * 64;
+// LDS: Te0/Te1 replicated 32x, rows of 256 B (x<<8 | lane*4, Te1 at +128) = 64 KiB,
+// then one 8 KiB GHASH comb table per wave.
+constexpr uint32_t kTeBytes = 65536;
+constexpr uint32_t kGhBytes = 8192;
+constexpr uint32_t kLdsBytes = kTeBytes + kWaves * kGhBytes;
+// Device key slot: 60 round-key words (+4 pad), their rot16 copies, and the 4-bit comb table of
+// H (512 x 16 B).
+constexpr uint32_t kRkWords = 128;  // [0,64): rk words, [64,128): rot16(rk)
+constexpr uint32_t kGhEntries = 512;
+
+struct Batch {
+    uint8_t *arena;
+    const qgcm_desc *descs;     // NULL -> uniform
+    const uint32_t *worklist;   // NULL -> identity; else n_items entries, 0xffffffff = padding
+    const uint8_t *nonces;      // seal only; NULL -> nonce already in slot
+    uint8_t *status;            // may be NULL
+    const uint32_t *rk_table;   // [max_keys][kRkWords]
+    const uint4 *gh_table;      // [max_keys][kGhEntries]
+    const uint32_t *te;         // [512] Te0 then Te1
+    uint64_t stride;
+    uint32_t uniform_len;
+    uint32_t uniform_key;
+    uint32_t n;
+    uint32_t n_items;           // multiple of 64
+    uint32_t aad_len;           // 0 or 4
+    uint32_t max_keys;
+};
+
+hipError_t init_kernels();
+hipError_t launch_seal(const Batch &b, int grid, hipStream_t s);
+hipError_t launch_open(const Batch &b, int grid, hipStream_t s);
+hipError_t launch_key_setup(const uint8_t *d_keys, uint32_t first, uint32_t count, uint32_t *rk_table,
+                            uint4 *gh_table, const uint8_t *d_sbox, hipStream_t s);
+// Groups descriptor batches into key-uniform 64-packet tiles (counting sort by key_idx).
+hipError_t launch_build_worklist(const qgcm_desc *descs, uint32_t n, uint32_t max_keys, uint32_t *counts,
+                                 uint32_t *cursors, uint32_t *worklist, uint32_t n_items_cap,
+                                 hipStream_t s);
+hipError_t launch_fill_uniform(uint8_t *arena, uint64_t stride, uint32_t n, uint32_t len, uint32_t aad_word,
+                               uint64_t seed_payload, uint8_t *nonces, uint64_t seed_nonce, hipStream_t s);
+
+}  // namespace qgcm

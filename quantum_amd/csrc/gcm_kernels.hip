@@ -1,0 +1,622 @@
+// gcm_kernels.hip -- AES-256-GCM seal/open of packet batches for gfx950 (MI355X, CDNA4).
+//
+// Replaces, per packet, crypto/aes.go:41-52 (Encrypt: cipher.AEAD.Seal in place, tag, nonce)
+// and crypto/aes.go:57-62 (Decrypt: cipher.AEAD.Open in place), the calls that
+// plugin/encryption.go:22-37 makes for every tunnelled payload.
+//
+// Design (DESIGN.md has the numbers):
+//  * one lane = one packet = one GCM instance; a wave64 owns 64 packets that share a key
+//    (key-uniform tiles), so round keys sit in SGPRs and the GHASH multiplier H is uniform;
+//  * AES-256 by T-tables in LDS: Te0/Te1 replicated 32x so a ds_read_b32 is bank-conflict free;
+//    the lookup address (x<<8 | lane*4) is ONE v_perm_b32; Te2/Te3 = rot16(Te0/Te1) folded
+//    into the column XOR;
+//  * CTR caching: counters of a packet differ only in the low byte for 256 consecutive blocks,
+//    so rounds 1-2 collapse to 5 lookups per block (197 instead of 224 lookups per block);
+//  * GHASH by a 4-bit comb of the uniform H: 32 tables x 16 entries x 16 B = one 256-B bank row
+//    per table, so 64 lanes reading arbitrary nibbles via ds_read_b128 never conflict;
+//    the address is again one v_perm_b32;
+//  * the kernel is persistent: one 512-thread workgroup per CU fills the LDS tables once.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "gcm_internal.h"
+
+namespace qgcm {
+
+// The packet kernels use dynamic LDS only, so it starts at LDS address 0 and every table address
+// below is absolute: LDS pointers are formed straight from the integer (no base add per lookup).
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) u32x4 lds_u128;
+
+struct __attribute__((aligned(4))) W4 {
+    uint32_t x, y, z, w;
+};
+
+__device__ __forceinline__ uint32_t perm(uint32_t s0, uint32_t s1, uint32_t sel) {
+    return __builtin_amdgcn_perm(s0, s1, sel);
+}
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // v_bitop3_b32, truth table of a^b^c
+}
+__device__ __forceinline__ uint32_t rot16(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 16); }
+__device__ __forceinline__ uint32_t bswap(uint32_t x) { return __builtin_bswap32(x); }
+
+__device__ __forceinline__ uint32_t lds32(uint32_t addr) { return *(const lds_u32 *)(size_t)addr; }
+__device__ __forceinline__ uint4 lds128(uint32_t addr) {
+    const u32x4 v = *(const lds_u128 *)(size_t)addr;
+    return uint4{v.x, v.y, v.z, v.w};
+}
+__device__ __forceinline__ void lds_st32(uint32_t addr, uint32_t v) { *(lds_u32 *)(size_t)addr = v; }
+__device__ __forceinline__ void lds_st128(uint32_t addr, uint4 v) {
+    *(lds_u128 *)(size_t)addr = u32x4{v.x, v.y, v.z, v.w};
+}
+
+// Te0[byte k of s] / Te1[byte k of s] from this lane's replica.
+// v_perm: result byte0 = lb.byte0 (lane*4), byte1 = s.byte k, bytes 2,3 = 0.
+#define TA(s, k) perm((s), lb, 0x0c0c0400u + ((k) << 8))
+#define TE0(s, k) lds32(TA(s, k))
+#define TE1(s, k) lds32(TA(s, k) + 128u)
+
+struct Ctr {
+    uint32_t K0, x3;          // round-1 column 0 without the varying term; rk0 word3 byte3
+    uint32_t U0, U1, U2, U3;  // round-2 columns without the term that depends on column 0
+};
+
+// Round keys of one key slot: rk[0..59] (FIPS-197 words as LE column words) and
+// rr[0..59] = rot16(rk) so that  a ^ rot16(b) ^ rk  =  a ^ rot16(b ^ rr)  costs two v_bitop3.
+struct Keys {
+    const uint32_t *rk;
+    const uint32_t *rr;
+};
+
+// One full AES round (SubBytes, ShiftRows, MixColumns, AddRoundKey) on LE column words:
+// column c = Te0[s_c.b0] ^ Te1[s_c+1.b1] ^ rot16(Te0[s_c+2.b2] ^ Te1[s_c+3.b3]) ^ rk_c.
+__device__ __forceinline__ void round_full(uint32_t &s0, uint32_t &s1, uint32_t &s2, uint32_t &s3, const Keys &k,
+                                           int r, uint32_t lb) {
+    const uint32_t b0 = xor3(TE0(s2, 2), TE1(s3, 3), k.rr[4 * r + 0]);
+    const uint32_t b1 = xor3(TE0(s3, 2), TE1(s0, 3), k.rr[4 * r + 1]);
+    const uint32_t b2 = xor3(TE0(s0, 2), TE1(s1, 3), k.rr[4 * r + 2]);
+    const uint32_t b3 = xor3(TE0(s1, 2), TE1(s2, 3), k.rr[4 * r + 3]);
+    const uint32_t o0 = xor3(TE0(s0, 0), TE1(s1, 1), rot16(b0));
+    const uint32_t o1 = xor3(TE0(s1, 0), TE1(s2, 1), rot16(b1));
+    const uint32_t o2 = xor3(TE0(s2, 0), TE1(s3, 1), rot16(b2));
+    const uint32_t o3 = xor3(TE0(s3, 0), TE1(s0, 1), rot16(b3));
+    s0 = o0;
+    s1 = o1;
+    s2 = o2;
+    s3 = o3;
+}
+
+// Final round (no MixColumns): S-box bytes are byte1/byte2 of Te0 and byte3 of Te1.
+__device__ __forceinline__ void round_last(uint32_t &s0, uint32_t &s1, uint32_t &s2, uint32_t &s3, const Keys &k,
+                                           uint32_t lb) {
+    const uint32_t *rk = k.rk + 56;
+    const uint32_t o0 = xor3(perm(TE0(s1, 1), TE0(s0, 0), 0x0c0c0501u), perm(TE1(s3, 3), TE0(s2, 2), 0x07020c0cu), rk[0]);
+    const uint32_t o1 = xor3(perm(TE0(s2, 1), TE0(s1, 0), 0x0c0c0501u), perm(TE1(s0, 3), TE0(s3, 2), 0x07020c0cu), rk[1]);
+    const uint32_t o2 = xor3(perm(TE0(s3, 1), TE0(s2, 0), 0x0c0c0501u), perm(TE1(s1, 3), TE0(s0, 2), 0x07020c0cu), rk[2]);
+    const uint32_t o3 = xor3(perm(TE0(s0, 1), TE0(s3, 0), 0x0c0c0501u), perm(TE1(s2, 3), TE0(s1, 2), 0x07020c0cu), rk[3]);
+    s0 = o0;
+    s1 = o1;
+    s2 = o2;
+    s3 = o3;
+}
+
+// Precompute rounds 1-2 for counter blocks nonce || (ctr_hi << 8 | low byte).  Round 1: only
+// column 0 sees the varying byte (s3.b3, via Te3); round 2: each column sees exactly one byte
+// of that column 0.
+__device__ __forceinline__ void ctr_setup(Ctr &c, uint32_t n0, uint32_t n1, uint32_t n2, uint32_t ctr_hi,
+                                          const Keys &k, uint32_t lb) {
+    const uint32_t *rk = k.rk;
+    const uint32_t s0 = n0 ^ rk[0], s1 = n1 ^ rk[1], s2 = n2 ^ rk[2];
+    const uint32_t s3 = bswap(ctr_hi << 8) ^ rk[3];  // byte3 varies per block; unused below
+    c.x3 = rk[3] >> 24;
+    c.K0 = xor3(TE0(s0, 0), TE1(s1, 1), rot16(TE0(s2, 2))) ^ rk[4];
+    const uint32_t t1 = xor3(TE0(s1, 0), TE1(s2, 1), rot16(xor3(TE0(s3, 2), TE1(s0, 3), k.rr[5])));
+    const uint32_t t2 = xor3(TE0(s2, 0), TE1(s3, 1), rot16(xor3(TE0(s0, 2), TE1(s1, 3), k.rr[6])));
+    const uint32_t t3 = xor3(TE0(s3, 0), TE1(s0, 1), rot16(xor3(TE0(s1, 2), TE1(s2, 3), k.rr[7])));
+    c.U0 = TE1(t1, 1) ^ rot16(xor3(TE0(t2, 2), TE1(t3, 3), k.rr[8]));
+    c.U1 = xor3(TE0(t1, 0), TE1(t2, 1), rot16(TE0(t3, 2))) ^ rk[9];
+    c.U2 = xor3(TE0(t2, 0), TE1(t3, 1), rot16(TE1(t1, 3))) ^ rk[10];
+    c.U3 = TE0(t3, 0) ^ rot16(xor3(TE0(t1, 2), TE1(t2, 3), k.rr[11]));
+}
+
+// E_K(nonce || ctr) for a counter whose high 24 bits match the cache; lo = ctr & 0xff.
+__device__ __forceinline__ void ctr_block(const Ctr &c, uint32_t lo, const Keys &k, uint32_t lb, uint32_t &s0,
+                                          uint32_t &s1, uint32_t &s2, uint32_t &s3) {
+    const uint32_t x = lo ^ c.x3;
+    const uint32_t t0 = c.K0 ^ rot16(lds32(((x << 8) | lb) + 128u));  // Te3[x]
+    s0 = c.U0 ^ TE0(t0, 0);
+    s1 = c.U1 ^ rot16(TE1(t0, 3));  // Te3[t0.b3]
+    s2 = c.U2 ^ rot16(TE0(t0, 2));  // Te2[t0.b2]
+    s3 = c.U3 ^ TE1(t0, 1);
+#pragma unroll
+    for (int r = 3; r < 14; ++r) round_full(s0, s1, s2, s3, k, r, lb);
+    round_last(s0, s1, s2, s3, k, lb);
+}
+
+// Y <- Y * H in GF(2^128) via the 4-bit comb in this wave's LDS table at gb (byte1/2 of gb hold
+// its base; byte0 is 0).  Entry (p, v) at gb + p*256 + v*16, p = nibble position (2*byte for the
+// high nibble, 2*byte+1 for the low one), v = nibble value.
+__device__ __forceinline__ void ghash_mul(uint32_t &y0, uint32_t &y1, uint32_t &y2, uint32_t &y3, uint32_t gb) {
+    uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+    const uint32_t yw[4] = {y0, y1, y2, y3};
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        const uint32_t hi = yw[w] & 0xf0f0f0f0u;
+        const uint32_t lo = (yw[w] << 4) & 0xf0f0f0f0u;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int j = 4 * w + k;
+            const uint4 th = lds128(perm(gb, hi, 0x0c060500u | k) + (2 * j) * 256);
+            const uint4 tl = lds128(perm(gb, lo, 0x0c060500u | k) + (2 * j + 1) * 256);
+            a0 = xor3(a0, th.x, tl.x);
+            a1 = xor3(a1, th.y, tl.y);
+            a2 = xor3(a2, th.z, tl.z);
+            a3 = xor3(a3, th.w, tl.w);
+        }
+    }
+    y0 = a0;
+    y1 = a1;
+    y2 = a2;
+    y3 = a3;
+}
+
+__device__ __forceinline__ uint32_t sel4(uint32_t q, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    return q == 0 ? a : (q == 1 ? b : (q == 2 ? c : d));
+}
+__device__ __forceinline__ uint32_t lowmask(uint32_t s) { return s ? (0xffffffffu >> (32 - 8 * s)) : 0u; }
+__device__ __forceinline__ void store_bytes(uint8_t *p, uint32_t v, uint32_t nbytes) {
+    if (nbytes > 0) p[0] = (uint8_t)v;
+    if (nbytes > 1) p[1] = (uint8_t)(v >> 8);
+    if (nbytes > 2) p[2] = (uint8_t)(v >> 16);
+}
+__device__ __forceinline__ uint32_t load_bytes(const uint8_t *p, uint32_t nbytes) {
+    uint32_t v = 0;
+    if (nbytes > 0) v |= p[0];
+    if (nbytes > 1) v |= (uint32_t)p[1] << 8;
+    if (nbytes > 2) v |= (uint32_t)p[2] << 16;
+    return v;
+}
+
+// Reads the 28-byte tag||nonce that starts at byte L of data (any alignment; data 4-aligned).
+// Out: tn[0..3] = tag words, tn[4..6] = nonce words (LE), and the s = L%4 bytes before it.
+struct Tail {
+    uint32_t t0, t1, t2, t3, n0, n1, n2;  // tag words, nonce words (LE)
+};
+
+__device__ __forceinline__ void read_tail(const uint8_t *data, uint32_t L, Tail &tn, uint32_t &prefix) {
+    const uint32_t s = L & 3u;
+    const uint32_t *t = reinterpret_cast<const uint32_t *>(data + (L & ~3u));
+    uint32_t W[8];
+#pragma unroll
+    for (int j = 0; j < 7; ++j) W[j] = t[j];
+    W[7] = load_bytes(data + (L & ~3u) + 28, s);
+    tn.t0 = __builtin_amdgcn_alignbyte(W[1], W[0], s);
+    tn.t1 = __builtin_amdgcn_alignbyte(W[2], W[1], s);
+    tn.t2 = __builtin_amdgcn_alignbyte(W[3], W[2], s);
+    tn.t3 = __builtin_amdgcn_alignbyte(W[4], W[3], s);
+    tn.n0 = __builtin_amdgcn_alignbyte(W[5], W[4], s);
+    tn.n1 = __builtin_amdgcn_alignbyte(W[6], W[5], s);
+    tn.n2 = __builtin_amdgcn_alignbyte(W[7], W[6], s);
+    prefix = W[0] & lowmask(s);
+}
+
+// Writes prefix (s = L%4 bytes, the end of the payload) followed by tag||nonce (tn[0..6]) at
+// data + (L & ~3): 7 dwords + s bytes, never touching bytes past L+28.
+__device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t sh) {
+    return (uint32_t)((((uint64_t)hi << 32) | lo) >> sh);  // sh in [8, 32]
+}
+__device__ __forceinline__ void write_tail(uint8_t *data, uint32_t L, const Tail &tn, uint32_t prefix) {
+    const uint32_t s = L & 3u;
+    uint32_t *t = reinterpret_cast<uint32_t *>(data + (L & ~3u));
+    const uint32_t sh = 32 - 8 * s;  // 32 when s == 0
+    t[0] = (uint32_t)((((uint64_t)tn.t0 << 32) | ((uint64_t)prefix << sh)) >> sh);
+    t[1] = funnel(tn.t1, tn.t0, sh);
+    t[2] = funnel(tn.t2, tn.t1, sh);
+    t[3] = funnel(tn.t3, tn.t2, sh);
+    t[4] = funnel(tn.n0, tn.t3, sh);
+    t[5] = funnel(tn.n1, tn.n0, sh);
+    t[6] = funnel(tn.n2, tn.n1, sh);
+    if (s) store_bytes(data + (L & ~3u) + 28, tn.n2 >> sh, s);
+}
+
+template <bool kSeal>
+__global__ void __launch_bounds__(kThreads) gcm_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = threadIdx.x >> 6;
+
+    // Fill the replicated T-tables: dword i = row x = i/64, slot i%64 (<32: Te0, else Te1).
+    for (uint32_t i = threadIdx.x; i < kTeBytes / 4; i += kThreads) {
+        const uint32_t x = i >> 6, slot = i & 63u;
+        lds_st32(4 * i, b.te[(slot >> 5) * 256u + x]);
+    }
+    __syncthreads();
+
+    const uint32_t lb = (lane & 31u) << 2;
+    const uint32_t gb = kTeBytes + wave * kGhBytes;
+    uint32_t cur_key = 0xffffffffu;
+    const uint32_t ntiles = b.n_items >> 6;
+
+    for (uint32_t tile = blockIdx.x * kWaves + wave; tile < ntiles; tile += gridDim.x * kWaves) {
+        const uint32_t item = tile * 64u + lane;
+        const uint32_t pkt = b.worklist ? b.worklist[item] : item;
+        bool valid = pkt < b.n;
+        uint64_t off = 0;
+        uint32_t len = 0, key = 0;
+        if (valid) {
+            if (b.descs) {
+                const qgcm_desc d = b.descs[pkt];
+                off = d.offset;
+                len = d.len;
+                key = d.key_idx;
+            } else {
+                off = (uint64_t)pkt * b.stride;
+                len = b.uniform_len;
+                key = b.uniform_key;
+            }
+        }
+        const uint64_t vmask = __ballot(valid);
+        if (vmask == 0) continue;
+        const int first = __ffsll((unsigned long long)vmask) - 1;
+        const uint32_t wkey = __builtin_amdgcn_readfirstlane(__shfl(key, first));
+        if (wkey != cur_key) {
+            const uint4 *src = b.gh_table + (size_t)wkey * kGhEntries;
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                const uint32_t e = r * 64 + lane;
+                lds_st128(gb + e * 16, src[e]);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            cur_key = wkey;
+        }
+        const Keys kk = {rk_table + (size_t)wkey * kRkWords, rk_table + (size_t)wkey * kRkWords + 64};
+
+        // Per-lane framing (crypto/aes.go:41-62).
+        uint32_t L;
+        if (kSeal) {
+            L = len;
+        } else {
+            valid = valid && len >= (uint32_t)QGCM_OVERHEAD;  // Open: ciphertext shorter than tag
+            L = len - QGCM_OVERHEAD;
+        }
+        if (!valid) {
+            if (!kSeal && b.status && pkt < b.n) b.status[pkt] = 0;
+            continue;
+        }
+        uint8_t *raw = b.arena + off;
+        uint8_t *data = raw + 4;  // common.PacketStart
+
+        Tail tn;
+        uint32_t prefix;
+        if (kSeal && b.nonces) {
+            const uint32_t *np = reinterpret_cast<const uint32_t *>(b.nonces + 12ull * pkt);
+            tn.n0 = np[0];
+            tn.n1 = np[1];
+            tn.n2 = np[2];
+        } else {
+            read_tail(data, L, tn, prefix);
+        }
+        const uint32_t n0 = tn.n0, n1 = tn.n1, n2 = tn.n2;
+
+        // GHASH(A): the additional data is the 4-B private-IP header Raw[0:4].
+        uint32_t y0 = 0, y1 = 0, y2 = 0, y3 = 0;
+        if (b.aad_len) {
+            y0 = *reinterpret_cast<const uint32_t *>(raw) & (b.aad_len >= 4 ? 0xffffffffu : lowmask(b.aad_len));
+            ghash_mul(y0, y1, y2, y3, gb);
+        }
+
+        Ctr cc;
+        ctr_setup(cc, n0, n1, n2, 0, kk, lb);
+        uint32_t e0, e1, e2, e3;  // E_K(J0), J0 = nonce || 0^31 || 1
+        ctr_block(cc, 1, kk, lb, e0, e1, e2, e3);
+
+        const uint32_t nfull = L >> 4;
+        for (uint32_t i = 0; i < nfull; ++i) {
+            const uint32_t ctr = i + 2;  // inc32(J0) + i
+            if ((ctr & 0xffu) == 0) ctr_setup(cc, n0, n1, n2, ctr >> 8, kk, lb);
+            uint32_t k0, k1, k2, k3;
+            ctr_block(cc, ctr & 0xffu, kk, lb, k0, k1, k2, k3);
+            W4 *p = reinterpret_cast<W4 *>(data + 16u * i);
+            const W4 in = *p;
+            const W4 out = {in.x ^ k0, in.y ^ k1, in.z ^ k2, in.w ^ k3};
+            *p = out;
+            const W4 &c = kSeal ? out : in;
+            y0 ^= c.x;
+            y1 ^= c.y;
+            y2 ^= c.z;
+            y3 ^= c.w;
+            ghash_mul(y0, y1, y2, y3, gb);
+        }
+        const uint32_t r = L & 15u;
+        prefix = 0;
+        if (r) {
+            const uint32_t ctr = nfull + 2;
+            if ((ctr & 0xffu) == 0) ctr_setup(cc, n0, n1, n2, ctr >> 8, kk, lb);
+            uint32_t k0, k1, k2, k3;
+            ctr_block(cc, ctr & 0xffu, kk, lb, k0, k1, k2, k3);
+            uint8_t *blk = data + 16u * nfull;
+            const W4 in = *reinterpret_cast<const W4 *>(blk);  // reads into tag area: inside the slot
+            const uint32_t q = r >> 2, s = r & 3u;
+            const uint32_t m0 = q > 0 ? 0xffffffffu : (q == 0 ? lowmask(s) : 0u);
+            const uint32_t m1 = q > 1 ? 0xffffffffu : (q == 1 ? lowmask(s) : 0u);
+            const uint32_t m2 = q > 2 ? 0xffffffffu : (q == 2 ? lowmask(s) : 0u);
+            const uint32_t m3 = q == 3 ? lowmask(s) : 0u;
+            const uint32_t o0 = in.x ^ k0, o1 = in.y ^ k1, o2 = in.z ^ k2, o3 = in.w ^ k3;
+            uint32_t *bw = reinterpret_cast<uint32_t *>(blk);
+            if (q > 0) bw[0] = o0;
+            if (q > 1) bw[1] = o1;
+            if (q > 2) bw[2] = o2;
+            const uint32_t oq = sel4(q, o0, o1, o2, o3) & lowmask(s);
+            if (kSeal) {
+                prefix = oq;  // written by write_tail together with tag||nonce
+                y0 ^= o0 & m0;
+                y1 ^= o1 & m1;
+                y2 ^= o2 & m2;
+                y3 ^= o3 & m3;
+            } else {
+                store_bytes(blk + 4 * q, oq, s);
+                y0 ^= in.x & m0;
+                y1 ^= in.y & m1;
+                y2 ^= in.z & m2;
+                y3 ^= in.w & m3;
+            }
+            ghash_mul(y0, y1, y2, y3, gb);
+        }
+        // [len(A)]_64 || [len(C)]_64 in bits, big endian.
+        y1 ^= bswap(b.aad_len * 8u);
+        y3 ^= bswap(L * 8u);
+        ghash_mul(y0, y1, y2, y3, gb);
+        const uint32_t t0 = y0 ^ e0, t1 = y1 ^ e1, t2 = y2 ^ e2, t3 = y3 ^ e3;
+
+        if (kSeal) {
+            tn.t0 = t0;
+            tn.t1 = t1;
+            tn.t2 = t2;
+            tn.t3 = t3;
+            write_tail(data, L, tn, prefix);
+            if (b.status) b.status[pkt] = 1;
+        } else {
+            const bool ok = ((t0 ^ tn.t0) | (t1 ^ tn.t1) | (t2 ^ tn.t2) | (t3 ^ tn.t3)) == 0;
+            if (!ok) {
+                // Go 1.9 crypto/cipher gcm Open: zero the would-be plaintext on tag mismatch.
+                uint32_t *dw = reinterpret_cast<uint32_t *>(data);
+                for (uint32_t i = 0; i < (L >> 2); ++i) dw[i] = 0;
+                store_bytes(data + (L & ~3u), 0, L & 3u);
+            }
+            if (b.status) b.status[pkt] = ok ? 1 : 0;
+        }
+    }
+}
+
+hipError_t init_kernels() {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&gcm_kernel<true>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+    if (e != hipSuccess) return e;
+    return hipFuncSetAttribute(reinterpret_cast<const void *>(&gcm_kernel<false>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+}
+
+hipError_t launch_seal(const Batch &b, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(gcm_kernel<true>, dim3(grid), dim3(kThreads), kLdsBytes, s, b, b.rk_table);
+    return hipGetLastError();
+}
+
+hipError_t launch_open(const Batch &b, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(gcm_kernel<false>, dim3(grid), dim3(kThreads), kLdsBytes, s, b, b.rk_table);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// Key setup: crypto/aes.go:68-76 (aes.NewCipher + cipher.NewGCM).  One 256-thread workgroup per
+// key: FIPS-197 key expansion, H = E_K(0^128), x^i * H for i < 128, then the 4-bit comb
+// T_p[v] = sum over set bits of v (MSB = x^0) of x^(4p+k) * H.
+__device__ __forceinline__ uint8_t xt(uint8_t a) { return (uint8_t)((a << 1) ^ ((a & 0x80) ? 0x1b : 0)); }
+
+__global__ void __launch_bounds__(256) key_setup_kernel(const uint8_t *keys, uint32_t first, uint32_t *rk_table,
+                                                        uint4 *gh_table, const uint8_t *sbox_g) {
+    __shared__ uint8_t sbox[256];
+    __shared__ uint8_t rkb[240];
+    __shared__ uint4 pw[128];
+    const uint32_t kidx = blockIdx.x;
+    const uint8_t *key = keys + 32u * kidx;
+    sbox[threadIdx.x] = sbox_g[threadIdx.x];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int i = 0; i < 32; ++i) rkb[i] = key[i];
+        uint8_t rcon = 1;
+        for (int i = 8; i < 60; ++i) {
+            uint8_t t[4] = {rkb[4 * i - 4], rkb[4 * i - 3], rkb[4 * i - 2], rkb[4 * i - 1]};
+            if (i % 8 == 0) {
+                const uint8_t t0 = t[0];
+                t[0] = sbox[t[1]] ^ rcon;
+                t[1] = sbox[t[2]];
+                t[2] = sbox[t[3]];
+                t[3] = sbox[t0];
+                rcon = xt(rcon);
+            } else if (i % 8 == 4) {
+                for (int j = 0; j < 4; ++j) t[j] = sbox[t[j]];
+            }
+            for (int j = 0; j < 4; ++j) rkb[4 * i + j] = rkb[4 * i - 32 + j] ^ t[j];
+        }
+        // H = E_K(0)
+        uint8_t s[16], u[16];
+        for (int i = 0; i < 16; ++i) s[i] = rkb[i];
+        for (int round = 1; round <= 14; ++round) {
+            for (int c = 0; c < 4; ++c)
+                for (int r = 0; r < 4; ++r) u[r + 4 * c] = sbox[s[r + 4 * ((c + r) & 3)]];
+            if (round != 14) {
+                for (int c = 0; c < 4; ++c) {
+                    const uint8_t a0 = u[4 * c], a1 = u[4 * c + 1], a2 = u[4 * c + 2], a3 = u[4 * c + 3];
+                    const uint8_t all = a0 ^ a1 ^ a2 ^ a3;
+                    s[4 * c + 0] = a0 ^ all ^ xt(a0 ^ a1);
+                    s[4 * c + 1] = a1 ^ all ^ xt(a1 ^ a2);
+                    s[4 * c + 2] = a2 ^ all ^ xt(a2 ^ a3);
+                    s[4 * c + 3] = a3 ^ all ^ xt(a3 ^ a0);
+                }
+            } else {
+                for (int i = 0; i < 16; ++i) s[i] = u[i];
+            }
+            for (int i = 0; i < 16; ++i) s[i] ^= rkb[16 * round + i];
+        }
+        // x^i * H: multiply by x = shift toward higher bit index (right shift of the byte string),
+        // reduce with R = 0xe1 || 0^120 (SP 800-38D Algorithm 1).
+        uint8_t v[16];
+        for (int i = 0; i < 16; ++i) v[i] = s[i];
+        for (int i = 0; i < 128; ++i) {
+            uint4 w;
+            w.x = v[0] | v[1] << 8 | v[2] << 16 | (uint32_t)v[3] << 24;
+            w.y = v[4] | v[5] << 8 | v[6] << 16 | (uint32_t)v[7] << 24;
+            w.z = v[8] | v[9] << 8 | v[10] << 16 | (uint32_t)v[11] << 24;
+            w.w = v[12] | v[13] << 8 | v[14] << 16 | (uint32_t)v[15] << 24;
+            pw[i] = w;
+            const int lsb = v[15] & 1;
+            for (int j = 15; j > 0; --j) v[j] = (uint8_t)((v[j] >> 1) | (v[j - 1] << 7));
+            v[0] >>= 1;
+            if (lsb) v[0] ^= 0xe1;
+        }
+    }
+    __syncthreads();
+    const uint32_t slot = first + kidx;
+    if (threadIdx.x < 64) {
+        const int i = threadIdx.x;
+        const uint32_t w = i < 60 ? (rkb[4 * i] | rkb[4 * i + 1] << 8 | rkb[4 * i + 2] << 16 |
+                                     (uint32_t)rkb[4 * i + 3] << 24)
+                                  : 0u;
+        rk_table[(size_t)slot * kRkWords + i] = w;
+        rk_table[(size_t)slot * kRkWords + 64 + i] = (w << 16) | (w >> 16);
+    }
+    for (uint32_t e = threadIdx.x; e < kGhEntries; e += 256) {
+        const uint32_t p = e >> 4, v = e & 15u;
+        uint4 acc = {0, 0, 0, 0};
+        for (int k = 0; k < 4; ++k) {
+            if ((v >> (3 - k)) & 1u) {
+                const uint4 t = pw[4 * p + k];
+                acc.x ^= t.x;
+                acc.y ^= t.y;
+                acc.z ^= t.z;
+                acc.w ^= t.w;
+            }
+        }
+        gh_table[(size_t)slot * kGhEntries + e] = acc;
+    }
+}
+
+hipError_t launch_key_setup(const uint8_t *d_keys, uint32_t first, uint32_t count, uint32_t *rk_table,
+                            uint4 *gh_table, const uint8_t *d_sbox, hipStream_t s) {
+    if (count == 0) return hipSuccess;
+    hipLaunchKernelGGL(key_setup_kernel, dim3(count), dim3(256), 0, s, d_keys, first, rk_table, gh_table, d_sbox);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// Worklist: counting sort of descriptor batches by key_idx into 64-aligned key groups, so every
+// wave64 tile is key-uniform.  Packets with key_idx >= max_keys are dropped (status stays 0).
+__global__ void wl_hist_kernel(const qgcm_desc *descs, uint32_t n, uint32_t max_keys, uint32_t *counts) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        const uint32_t k = descs[i].key_idx;
+        if (k < max_keys) atomicAdd(&counts[k], 1u);
+    }
+}
+
+// Single workgroup: counts[k] -> padded exclusive offsets (in place), cursors zeroed by memset.
+__global__ void __launch_bounds__(1024) wl_scan_kernel(uint32_t *counts, uint32_t max_keys) {
+    __shared__ uint32_t partial[1024];
+    const uint32_t t = threadIdx.x;
+    const uint32_t per = (max_keys + 1023) / 1024;
+    const uint32_t lo = t * per, hi = min(lo + per, max_keys);
+    uint32_t sum = 0;
+    for (uint32_t k = lo; k < hi; ++k) sum += (counts[k] + 63u) & ~63u;
+    partial[t] = sum;
+    __syncthreads();
+    for (uint32_t d = 1; d < 1024; d <<= 1) {
+        const uint32_t v = t >= d ? partial[t - d] : 0;
+        __syncthreads();
+        partial[t] += v;
+        __syncthreads();
+    }
+    uint32_t run = partial[t] - sum;
+    for (uint32_t k = lo; k < hi; ++k) {
+        const uint32_t c = (counts[k] + 63u) & ~63u;
+        counts[k] = run;
+        run += c;
+    }
+}
+
+__global__ void wl_scatter_kernel(const qgcm_desc *descs, uint32_t n, uint32_t max_keys, const uint32_t *offs,
+                                  uint32_t *cursors, uint32_t *worklist) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        const uint32_t k = descs[i].key_idx;
+        if (k < max_keys) worklist[offs[k] + atomicAdd(&cursors[k], 1u)] = i;
+    }
+}
+
+hipError_t launch_build_worklist(const qgcm_desc *descs, uint32_t n, uint32_t max_keys, uint32_t *counts,
+                                 uint32_t *cursors, uint32_t *worklist, uint32_t n_items_cap, hipStream_t s) {
+    hipError_t e;
+    if ((e = hipMemsetAsync(counts, 0, sizeof(uint32_t) * max_keys, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(cursors, 0, sizeof(uint32_t) * max_keys, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(worklist, 0xff, sizeof(uint32_t) * n_items_cap, s)) != hipSuccess) return e;
+    const int bs = 256, g = (int)((n + bs - 1) / bs);
+    if (n) hipLaunchKernelGGL(wl_hist_kernel, dim3(g), dim3(bs), 0, s, descs, n, max_keys, counts);
+    hipLaunchKernelGGL(wl_scan_kernel, dim3(1), dim3(1024), 0, s, counts, max_keys);
+    if (n) hipLaunchKernelGGL(wl_scatter_kernel, dim3(g), dim3(bs), 0, s, descs, n, max_keys, counts, cursors, worklist);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// Synthetic workload (BASELINE configs): splitmix64 stream bytes, random-access form.
+__device__ __forceinline__ uint64_t splitmix_at(uint64_t seed, uint64_t k) {
+    uint64_t z = seed + (k + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__device__ __forceinline__ uint8_t stream_byte(uint64_t seed, uint64_t b) {
+    return (uint8_t)(splitmix_at(seed, b >> 3) >> (8 * (b & 7)));
+}
+
+// One thread per (slot, 4-byte group of the slot's first 4+L bytes).
+__global__ void fill_uniform_kernel(uint8_t *arena, uint64_t stride, uint32_t n, uint32_t len, uint32_t aad_word,
+                                    uint64_t seed_payload, uint8_t *nonces, uint64_t seed_nonce) {
+    const uint32_t groups = (4 + len + 3) / 4 + 3;  // +3 groups for the 12-byte nonce
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (uint64_t)n * groups) return;
+    const uint32_t slot = (uint32_t)(t / groups), g = (uint32_t)(t % groups);
+    uint8_t *raw = arena + (uint64_t)slot * stride;
+    const uint32_t dgroups = groups - 3;
+    if (g < dgroups) {
+        for (uint32_t j = 0; j < 4; ++j) {
+            const uint32_t pos = 4 * g + j;
+            if (pos < 4) {
+                raw[pos] = (uint8_t)(aad_word >> (8 * pos));
+            } else if (pos < 4 + len) {
+                raw[pos] = stream_byte(seed_payload, (uint64_t)slot * len + (pos - 4));
+            }
+        }
+    } else if (nonces) {
+        const uint32_t ng = g - dgroups;
+        for (uint32_t j = 0; j < 4; ++j) {
+            const uint64_t pos = 12ull * slot + 4 * ng + j;
+            nonces[pos] = stream_byte(seed_nonce, pos);
+        }
+    }
+}
+
+hipError_t launch_fill_uniform(uint8_t *arena, uint64_t stride, uint32_t n, uint32_t len, uint32_t aad_word,
+                               uint64_t seed_payload, uint8_t *nonces, uint64_t seed_nonce, hipStream_t s) {
+    const uint32_t groups = (4 + len + 3) / 4 + 3;
+    const uint64_t total = (uint64_t)n * groups;
+    if (total == 0) return hipSuccess;
+    const int bs = 256;
+    const uint64_t g = (total + bs - 1) / bs;
+    hipLaunchKernelGGL(fill_uniform_kernel, dim3((uint32_t)g), dim3(bs), 0, s, arena, stride, n, len, aad_word,
+                       seed_payload, nonces, seed_nonce);
+    return hipGetLastError();
+}
+
+}  // namespace qgcm

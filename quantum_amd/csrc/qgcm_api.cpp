@@ -1,0 +1,455 @@
+// qgcm_api.cpp -- the C ABI of include/qgcm.h over the gfx950 kernels in gcm_kernels.hip.
+//
+// Host responsibilities only: argument checks (the Go methods' error contract), device key
+// tables, stream plumbing and pinned staging.  All cryptographic work on packets runs on the
+// GPU; there is no CPU fallback -- without a usable HIP device qgcm_create returns NULL.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+#include <sys/random.h>
+
+#include <mutex>
+#include <vector>
+
+#include "../../include/qgcm.h"
+#include "gcm_internal.h"
+
+using namespace qgcm;
+
+struct qgcm_ctx {
+    int device = 0;
+    int num_cus = 0;
+    uint32_t max_keys = 0;
+    uint32_t *d_rk = nullptr;
+    uint4 *d_gh = nullptr;
+    uint32_t *d_te = nullptr;
+    uint8_t *d_sbox = nullptr;
+    std::vector<uint8_t> key_set;  // host view of which slots are populated
+    std::mutex key_mu;
+
+    // descriptor-batch workspace (worklist), guarded by ws_mu for the whole enqueue
+    std::mutex ws_mu;
+    uint32_t *d_counts = nullptr, *d_cursors = nullptr, *d_worklist = nullptr;
+    size_t wl_cap = 0;
+
+    // per-packet and host-batch staging, guarded by io_mu
+    std::mutex io_mu;
+    hipStream_t io_stream = nullptr;
+    uint8_t *d_io = nullptr;
+    size_t io_cap = 0;
+    uint8_t *h_pin = nullptr;
+    size_t pin_cap = 0;
+};
+
+namespace {
+
+thread_local bool tl_dummy;
+
+uint8_t gf8_mul(uint8_t a, uint8_t b) {
+    uint8_t p = 0;
+    for (int i = 0; i < 8; ++i) {
+        if (b & 1) p ^= a;
+        const uint8_t hi = a & 0x80;
+        a <<= 1;
+        if (hi) a ^= 0x1b;
+        b >>= 1;
+    }
+    return p;
+}
+
+// FIPS-197 S-box from its definition; Te0[x] = (2S, S, S, 3S) as a little-endian word,
+// Te1 = rotl8(Te0).
+void build_tables(uint8_t sbox[256], uint32_t te[512]) {
+    for (int x = 0; x < 256; ++x) {
+        uint8_t inv = 0;
+        if (x) {
+            uint8_t r = 1, b = (uint8_t)x;
+            for (int e = 254; e; e >>= 1) {
+                if (e & 1) r = gf8_mul(r, b);
+                b = gf8_mul(b, b);
+            }
+            inv = r;
+        }
+        auto rl = [](uint8_t v, int s) { return (uint8_t)((v << s) | (v >> (8 - s))); };
+        sbox[x] = inv ^ rl(inv, 1) ^ rl(inv, 2) ^ rl(inv, 3) ^ rl(inv, 4) ^ 0x63;
+    }
+    for (int x = 0; x < 256; ++x) {
+        const uint32_t s = sbox[x], s2 = gf8_mul((uint8_t)s, 2), s3 = s2 ^ s;
+        const uint32_t t0 = s2 | (s << 8) | (s << 16) | (s3 << 24);
+        te[x] = t0;
+        te[256 + x] = (t0 << 8) | (t0 >> 24);
+    }
+}
+
+void set_err(char *err, int errlen, const char *msg) {
+    if (err && errlen > 0) snprintf(err, (size_t)errlen, "%s", msg);
+}
+
+int hip_fail(hipError_t e) { return e == hipSuccess ? QGCM_OK : QGCM_E_HIP; }
+
+int grid_for(const qgcm_ctx *ctx, uint32_t n_items) {
+    const uint32_t tiles = n_items / 64;
+    const uint32_t wgs = (tiles + kWaves - 1) / kWaves;
+    const uint32_t cap = (uint32_t)ctx->num_cus;  // one 128-KiB-LDS workgroup per CU
+    return (int)(wgs < cap ? (wgs ? wgs : 1) : cap);
+}
+
+Batch base_batch(const qgcm_ctx *ctx) {
+    Batch b{};
+    b.rk_table = ctx->d_rk;
+    b.gh_table = ctx->d_gh;
+    b.te = ctx->d_te;
+    b.max_keys = ctx->max_keys;
+    return b;
+}
+
+bool key_ok(qgcm_ctx *ctx, uint32_t k) {
+    if (k >= ctx->max_keys) return false;
+    std::lock_guard<std::mutex> g(ctx->key_mu);
+    return ctx->key_set[k] != 0;
+}
+
+int run_uniform(qgcm_ctx *ctx, bool seal, uint8_t *arena, uint64_t stride, uint32_t n, uint32_t len,
+                uint32_t key_idx, const uint8_t *nonces, uint32_t aad_len, uint8_t *status, hipStream_t s) {
+    if (!ctx || (!arena && n) || aad_len > 4) return QGCM_E_ARG;
+    if (((uintptr_t)arena & 3) || (stride & 3) || (nonces && ((uintptr_t)nonces & 3))) return QGCM_E_ARG;
+    if (n && stride < (uint64_t)len + 4 + (seal ? QGCM_OVERHEAD : 0)) return QGCM_E_ARG;
+    if (!key_ok(ctx, key_idx)) return QGCM_E_KEY;
+    if (n == 0) return QGCM_OK;
+    if (hipSetDevice(ctx->device) != hipSuccess) return QGCM_E_HIP;
+    Batch b = base_batch(ctx);
+    b.arena = arena;
+    b.nonces = seal ? nonces : nullptr;
+    b.status = status;
+    b.stride = stride;
+    b.uniform_len = len;
+    b.uniform_key = key_idx;
+    b.n = n;
+    b.n_items = (uint32_t)(((uint64_t)n + 63) & ~63ull);
+    b.aad_len = aad_len;
+    const int grid = grid_for(ctx, b.n_items);
+    return hip_fail(seal ? launch_seal(b, grid, s) : launch_open(b, grid, s));
+}
+
+int run_descs(qgcm_ctx *ctx, bool seal, uint8_t *arena, const qgcm_desc *descs, uint32_t n, const uint8_t *nonces,
+              uint32_t aad_len, uint8_t *status, hipStream_t s) {
+    if (!ctx || (n && (!arena || !descs)) || aad_len > 4) return QGCM_E_ARG;
+    if (((uintptr_t)arena & 3) || (nonces && ((uintptr_t)nonces & 3))) return QGCM_E_ARG;
+    if (n == 0) return QGCM_OK;
+    if (hipSetDevice(ctx->device) != hipSuccess) return QGCM_E_HIP;
+    if (status && hipMemsetAsync(status, 0, n, s) != hipSuccess) return QGCM_E_HIP;
+    const uint64_t cap = (uint64_t)n + 64ull * (n < ctx->max_keys ? n : ctx->max_keys);
+    std::lock_guard<std::mutex> g(ctx->ws_mu);
+    if (cap > ctx->wl_cap) {
+        if (ctx->d_worklist) hipFree(ctx->d_worklist);
+        ctx->d_worklist = nullptr;
+        if (hipMalloc(&ctx->d_worklist, cap * sizeof(uint32_t)) != hipSuccess) {
+            ctx->wl_cap = 0;
+            return QGCM_E_NOMEM;
+        }
+        ctx->wl_cap = cap;
+    }
+    const uint32_t items = (uint32_t)((cap + 63) & ~63ull);
+    if (items > ctx->wl_cap) {
+        hipFree(ctx->d_worklist);
+        if (hipMalloc(&ctx->d_worklist, (size_t)items * sizeof(uint32_t)) != hipSuccess) {
+            ctx->d_worklist = nullptr;
+            ctx->wl_cap = 0;
+            return QGCM_E_NOMEM;
+        }
+        ctx->wl_cap = items;
+    }
+    hipError_t e = launch_build_worklist(descs, n, ctx->max_keys, ctx->d_counts, ctx->d_cursors, ctx->d_worklist,
+                                         items, s);
+    if (e != hipSuccess) return QGCM_E_HIP;
+    Batch b = base_batch(ctx);
+    b.arena = arena;
+    b.descs = descs;
+    b.worklist = ctx->d_worklist;
+    b.nonces = seal ? nonces : nullptr;
+    b.status = status;
+    b.n = n;
+    b.n_items = items;
+    b.aad_len = aad_len;
+    const int grid = grid_for(ctx, b.n_items);
+    return hip_fail(seal ? launch_seal(b, grid, s) : launch_open(b, grid, s));
+}
+
+int ensure_io(qgcm_ctx *ctx, size_t bytes) {
+    if (bytes <= ctx->io_cap && bytes <= ctx->pin_cap) return QGCM_OK;
+    size_t want = 1;
+    while (want < bytes) want <<= 1;
+    if (want < 4096) want = 4096;
+    if (ctx->d_io) hipFree(ctx->d_io);
+    if (ctx->h_pin) hipHostFree(ctx->h_pin);
+    ctx->d_io = nullptr;
+    ctx->h_pin = nullptr;
+    ctx->io_cap = ctx->pin_cap = 0;
+    if (hipMalloc(&ctx->d_io, want) != hipSuccess) return QGCM_E_NOMEM;
+    if (hipHostMalloc(&ctx->h_pin, want, hipHostMallocDefault) != hipSuccess) return QGCM_E_NOMEM;
+    ctx->io_cap = ctx->pin_cap = want;
+    return QGCM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *qgcm_version(void) { return "qgcm 0.1.0 (gfx950)"; }
+
+const char *qgcm_strerror(int code) {
+    switch (code) {
+        case QGCM_OK: return "ok";
+        case QGCM_E_ARG: return "invalid argument";
+        case QGCM_E_HIP: return "HIP runtime error";
+        case QGCM_E_KEY: return "key index not set or out of range";
+        case QGCM_E_AUTH: return "message authentication failed";
+        case QGCM_E_NOMEM: return "out of device or pinned memory";
+        default: return "unknown error";
+    }
+}
+
+qgcm_ctx *qgcm_create(int device, uint32_t max_keys, char *err, int errlen) {
+    (void)tl_dummy;
+    if (max_keys == 0 || max_keys > (1u << 20)) {
+        set_err(err, errlen, "max_keys must be in [1, 2^20]");
+        return nullptr;
+    }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) {
+        set_err(err, errlen, "no such HIP device");
+        return nullptr;
+    }
+    if (hipSetDevice(device) != hipSuccess) {
+        set_err(err, errlen, "hipSetDevice failed");
+        return nullptr;
+    }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) {
+        set_err(err, errlen, "hipGetDeviceProperties failed");
+        return nullptr;
+    }
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        char m[QGCM_ERRLEN];
+        snprintf(m, sizeof m, "device %d is %s; libqgcm is built for gfx950 only", device, prop.gcnArchName);
+        set_err(err, errlen, m);
+        return nullptr;
+    }
+    auto *ctx = new qgcm_ctx();
+    ctx->device = device;
+    ctx->num_cus = prop.multiProcessorCount;
+    ctx->max_keys = max_keys;
+    ctx->key_set.assign(max_keys, 0);
+    uint8_t sbox[256];
+    uint32_t te[512];
+    build_tables(sbox, te);
+    bool ok = hipMalloc(&ctx->d_rk, (size_t)max_keys * kRkWords * 4) == hipSuccess &&
+              hipMalloc(&ctx->d_gh, (size_t)max_keys * kGhEntries * 16) == hipSuccess &&
+              hipMalloc(&ctx->d_te, sizeof te) == hipSuccess && hipMalloc(&ctx->d_sbox, sizeof sbox) == hipSuccess &&
+              hipMalloc(&ctx->d_counts, (size_t)max_keys * 4) == hipSuccess &&
+              hipMalloc(&ctx->d_cursors, (size_t)max_keys * 4) == hipSuccess &&
+              hipMemcpy(ctx->d_te, te, sizeof te, hipMemcpyHostToDevice) == hipSuccess &&
+              hipMemcpy(ctx->d_sbox, sbox, sizeof sbox, hipMemcpyHostToDevice) == hipSuccess &&
+              hipStreamCreateWithFlags(&ctx->io_stream, hipStreamNonBlocking) == hipSuccess &&
+              init_kernels() == hipSuccess;
+    if (!ok) {
+        set_err(err, errlen, "device allocation / kernel setup failed");
+        qgcm_destroy(ctx);
+        return nullptr;
+    }
+    return ctx;
+}
+
+void qgcm_destroy(qgcm_ctx *ctx) {
+    if (!ctx) return;
+    hipSetDevice(ctx->device);
+    hipDeviceSynchronize();
+    hipFree(ctx->d_rk);
+    hipFree(ctx->d_gh);
+    hipFree(ctx->d_te);
+    hipFree(ctx->d_sbox);
+    hipFree(ctx->d_counts);
+    hipFree(ctx->d_cursors);
+    hipFree(ctx->d_worklist);
+    hipFree(ctx->d_io);
+    if (ctx->h_pin) hipHostFree(ctx->h_pin);
+    if (ctx->io_stream) hipStreamDestroy(ctx->io_stream);
+    delete ctx;
+}
+
+int qgcm_set_keys(qgcm_ctx *ctx, uint32_t first_idx, uint32_t count, const uint8_t *keys) {
+    if (!ctx || (count && !keys)) return QGCM_E_ARG;
+    if ((uint64_t)first_idx + count > ctx->max_keys) return QGCM_E_KEY;
+    if (count == 0) return QGCM_OK;
+    if (hipSetDevice(ctx->device) != hipSuccess) return QGCM_E_HIP;
+    uint8_t *d_keys = nullptr;
+    if (hipMalloc(&d_keys, (size_t)count * 32) != hipSuccess) return QGCM_E_NOMEM;
+    hipStream_t s = nullptr;
+    int rc = QGCM_OK;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess ||
+        hipMemcpyAsync(d_keys, keys, (size_t)count * 32, hipMemcpyHostToDevice, s) != hipSuccess ||
+        launch_key_setup(d_keys, first_idx, count, ctx->d_rk, ctx->d_gh, ctx->d_sbox, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        rc = QGCM_E_HIP;
+    if (s) hipStreamDestroy(s);
+    hipFree(d_keys);
+    if (rc == QGCM_OK) {
+        std::lock_guard<std::mutex> g(ctx->key_mu);
+        for (uint32_t i = 0; i < count; ++i) ctx->key_set[first_idx + i] = 1;
+    }
+    return rc;
+}
+
+int qgcm_set_key(qgcm_ctx *ctx, uint32_t key_idx, const uint8_t key[QGCM_KEY_BYTES]) {
+    return qgcm_set_keys(ctx, key_idx, 1, key);
+}
+
+int qgcm_seal_batch(qgcm_ctx *ctx, uint8_t *d_arena, const qgcm_desc *d_descs, uint32_t n, const uint8_t *d_nonces,
+                    uint32_t aad_len, uint8_t *d_status, void *stream) {
+    return run_descs(ctx, true, d_arena, d_descs, n, d_nonces, aad_len, d_status, (hipStream_t)stream);
+}
+
+int qgcm_open_batch(qgcm_ctx *ctx, uint8_t *d_arena, const qgcm_desc *d_descs, uint32_t n, uint32_t aad_len,
+                    uint8_t *d_status, void *stream) {
+    return run_descs(ctx, false, d_arena, d_descs, n, nullptr, aad_len, d_status, (hipStream_t)stream);
+}
+
+int qgcm_seal_uniform(qgcm_ctx *ctx, uint8_t *d_arena, uint64_t stride, uint32_t n, uint32_t len, uint32_t key_idx,
+                      const uint8_t *d_nonces, uint32_t aad_len, uint8_t *d_status, void *stream) {
+    return run_uniform(ctx, true, d_arena, stride, n, len, key_idx, d_nonces, aad_len, d_status, (hipStream_t)stream);
+}
+
+int qgcm_open_uniform(qgcm_ctx *ctx, uint8_t *d_arena, uint64_t stride, uint32_t n, uint32_t len, uint32_t key_idx,
+                      uint32_t aad_len, uint8_t *d_status, void *stream) {
+    if (len < QGCM_OVERHEAD && n) {
+        // every packet fails Open; the slots stay untouched (ciphertext shorter than the tag)
+        if (!ctx) return QGCM_E_ARG;
+        if (d_status) {
+            if (hipSetDevice(ctx->device) != hipSuccess) return QGCM_E_HIP;
+            return hip_fail(hipMemsetAsync(d_status, 0, n, (hipStream_t)stream));
+        }
+        return QGCM_OK;
+    }
+    return run_uniform(ctx, false, d_arena, stride, n, len, key_idx, nullptr, aad_len, d_status, (hipStream_t)stream);
+}
+
+long qgcm_seal_one(qgcm_ctx *ctx, uint32_t key_idx, uint8_t *data, long length, const uint8_t *aad, uint32_t aad_len,
+                   const uint8_t *nonce) {
+    if (!ctx || !data || length < 0 || length > (1l << 30) || aad_len > 4 || (aad_len && !aad)) return -1;
+    if (!key_ok(ctx, key_idx)) return -1;
+    uint8_t nb[12];
+    if (nonce) {
+        memcpy(nb, nonce, 12);
+    } else if (getrandom(nb, 12, 0) != 12) {  // crypto/aes.go:44 rand.Read(nonce)
+        return -1;
+    }
+    std::lock_guard<std::mutex> g(ctx->io_mu);
+    if (hipSetDevice(ctx->device) != hipSuccess) return -1;
+    const uint64_t stride = ((uint64_t)length + 4 + QGCM_OVERHEAD + 15) & ~15ull;
+    if (ensure_io(ctx, stride + 16) != QGCM_OK) return -1;
+    uint8_t *h = ctx->h_pin;
+    memset(h, 0, stride);
+    if (aad_len) memcpy(h, aad, aad_len);
+    memcpy(h + 4, data, (size_t)length);
+    memcpy(h + 4 + length + 16, nb, 12);
+    hipStream_t s = ctx->io_stream;
+    uint8_t *d_status = ctx->d_io + stride;
+    if (hipMemcpyAsync(ctx->d_io, h, stride, hipMemcpyHostToDevice, s) != hipSuccess) return -1;
+    if (run_uniform(ctx, true, ctx->d_io, stride, 1, (uint32_t)length, key_idx, nullptr, aad_len, d_status, s) != QGCM_OK)
+        return -1;
+    if (hipMemcpyAsync(h, ctx->d_io, stride + 1, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return -1;
+    if (h[stride] != 1) return -1;
+    memcpy(data, h + 4, (size_t)length + QGCM_OVERHEAD);
+    return length + QGCM_OVERHEAD;
+}
+
+long qgcm_open_one(qgcm_ctx *ctx, uint32_t key_idx, uint8_t *data, long len, const uint8_t *aad, uint32_t aad_len) {
+    if (!ctx || (!data && len) || len < 0 || len > (1l << 30) || aad_len > 4 || (aad_len && !aad)) return -1;
+    if (len < QGCM_OVERHEAD) return -1;  // crypto/aes.go:58-60: errOpen (the reference panics below 12)
+    if (!key_ok(ctx, key_idx)) return -1;
+    std::lock_guard<std::mutex> g(ctx->io_mu);
+    if (hipSetDevice(ctx->device) != hipSuccess) return -1;
+    const uint64_t stride = ((uint64_t)len + 4 + 15) & ~15ull;
+    if (ensure_io(ctx, stride + 16) != QGCM_OK) return -1;
+    uint8_t *h = ctx->h_pin;
+    memset(h, 0, stride);
+    if (aad_len) memcpy(h, aad, aad_len);
+    memcpy(h + 4, data, (size_t)len);
+    hipStream_t s = ctx->io_stream;
+    uint8_t *d_status = ctx->d_io + stride;
+    if (hipMemcpyAsync(ctx->d_io, h, stride, hipMemcpyHostToDevice, s) != hipSuccess) return -1;
+    if (run_uniform(ctx, false, ctx->d_io, stride, 1, (uint32_t)len, key_idx, nullptr, aad_len, d_status, s) != QGCM_OK)
+        return -1;
+    if (hipMemcpyAsync(h, ctx->d_io, stride + 1, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return -1;
+    memcpy(data, h + 4, (size_t)len - QGCM_OVERHEAD);  // plaintext, or zeros on auth failure
+    return h[stride] == 1 ? len - QGCM_OVERHEAD : -1;
+}
+
+static int run_host(qgcm_ctx *ctx, bool seal, uint8_t *h_arena, uint64_t stride, uint32_t n, uint32_t len,
+                    uint32_t key_idx, const uint8_t *h_nonces, uint32_t aad_len, uint8_t *h_status) {
+    if (!ctx || (n && !h_arena)) return QGCM_E_ARG;
+    if (n == 0) return 0;
+    std::lock_guard<std::mutex> g(ctx->io_mu);
+    if (hipSetDevice(ctx->device) != hipSuccess) return QGCM_E_HIP;
+    const uint64_t bytes = stride * n;
+    const uint64_t nb = seal && h_nonces ? 12ull * n : 0;
+    const uint64_t need = ((bytes + 15) & ~15ull) + ((nb + 15) & ~15ull) + n;
+    int rc = ensure_io(ctx, need);
+    if (rc != QGCM_OK) return rc;
+    uint8_t *d_arena = ctx->d_io, *d_non = ctx->d_io + ((bytes + 15) & ~15ull);
+    uint8_t *d_stat = d_non + ((nb + 15) & ~15ull);
+    hipStream_t s = ctx->io_stream;
+    if (hipMemcpyAsync(d_arena, h_arena, bytes, hipMemcpyHostToDevice, s) != hipSuccess) return QGCM_E_HIP;
+    if (nb && hipMemcpyAsync(d_non, h_nonces, nb, hipMemcpyHostToDevice, s) != hipSuccess) return QGCM_E_HIP;
+    rc = seal ? run_uniform(ctx, true, d_arena, stride, n, len, key_idx, nb ? d_non : nullptr, aad_len, d_stat, s)
+              : (len < QGCM_OVERHEAD ? hip_fail(hipMemsetAsync(d_stat, 0, n, s))
+                                     : run_uniform(ctx, false, d_arena, stride, n, len, key_idx, nullptr, aad_len,
+                                                   d_stat, s));
+    if (rc != QGCM_OK) return rc;
+    if (hipMemcpyAsync(h_arena, d_arena, bytes, hipMemcpyDeviceToHost, s) != hipSuccess) return QGCM_E_HIP;
+    std::vector<uint8_t> st(n);
+    if (hipMemcpyAsync(st.data(), d_stat, n, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return QGCM_E_HIP;
+    int bad = 0;
+    for (uint32_t i = 0; i < n; ++i) bad += st[i] != 1;
+    if (h_status) memcpy(h_status, st.data(), n);
+    return bad;
+}
+
+int qgcm_seal_host(qgcm_ctx *ctx, uint8_t *h_arena, uint64_t stride, uint32_t n, uint32_t len, uint32_t key_idx,
+                   const uint8_t *h_nonces, uint32_t aad_len, uint8_t *h_status) {
+    return run_host(ctx, true, h_arena, stride, n, len, key_idx, h_nonces, aad_len, h_status);
+}
+
+int qgcm_open_host(qgcm_ctx *ctx, uint8_t *h_arena, uint64_t stride, uint32_t n, uint32_t len, uint32_t key_idx,
+                   uint32_t aad_len, uint8_t *h_status) {
+    return run_host(ctx, false, h_arena, stride, n, len, key_idx, nullptr, aad_len, h_status);
+}
+
+int qgcm_random_nonces(uint8_t *h_out, uint32_t n) {
+    if (!h_out && n) return QGCM_E_ARG;
+    size_t left = 12ull * n;
+    uint8_t *p = h_out;
+    while (left) {
+        const ssize_t r = getrandom(p, left > 33554431 ? 33554431 : left, 0);
+        if (r <= 0) return QGCM_E_ARG;
+        p += r;
+        left -= (size_t)r;
+    }
+    return QGCM_OK;
+}
+
+int qgcm_fill_uniform(uint8_t *d_arena, uint64_t stride, uint32_t n, uint32_t len, uint32_t aad_word,
+                      uint64_t seed_payload, uint8_t *d_nonces, uint64_t seed_nonce, void *stream) {
+    if ((n && !d_arena) || (n && stride < (uint64_t)len + 4)) return QGCM_E_ARG;
+    return hip_fail(launch_fill_uniform(d_arena, stride, n, len, aad_word, seed_payload, d_nonces, seed_nonce,
+                                        (hipStream_t)stream));
+}
+
+}  // extern "C"
