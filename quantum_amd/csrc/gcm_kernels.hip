@@ -181,44 +181,46 @@ __device__ __forceinline__ uint32_t load_bytes(const uint8_t *p, uint32_t nbytes
 
 // Reads the 28-byte tag||nonce that starts at byte L of data (any alignment; data 4-aligned).
 // Out: tn[0..3] = tag words, tn[4..6] = nonce words (LE), and the s = L%4 bytes before it.
-struct Tail {
-    uint32_t t0, t1, t2, t3, n0, n1, n2;  // tag words, nonce words (LE)
-};
+// NOTE: the packet kernels address LDS absolutely from 0, so they must own NO static LDS: the
+// build passes -disable-promote-alloca-to-lds, tail values are plain scalars (no private arrays
+// or structs left for the compiler to spill), and init_kernels() refuses a kernel whose static
+// LDS size is not 0.
 
-__device__ __forceinline__ void read_tail(const uint8_t *data, uint32_t L, Tail &tn, uint32_t &prefix) {
+// Reads the 28-byte tag||nonce that starts at byte L of data (any alignment; data 4-aligned):
+// tag words g0..g3, nonce words n0..n2 (LE), and the s = L%4 payload bytes before it (prefix).
+__device__ __forceinline__ void read_tail(const uint8_t *data, uint32_t L, uint32_t &g0, uint32_t &g1, uint32_t &g2,
+                                          uint32_t &g3, uint32_t &n0, uint32_t &n1, uint32_t &n2) {
     const uint32_t s = L & 3u;
     const uint32_t *t = reinterpret_cast<const uint32_t *>(data + (L & ~3u));
-    uint32_t W[8];
-#pragma unroll
-    for (int j = 0; j < 7; ++j) W[j] = t[j];
-    W[7] = load_bytes(data + (L & ~3u) + 28, s);
-    tn.t0 = __builtin_amdgcn_alignbyte(W[1], W[0], s);
-    tn.t1 = __builtin_amdgcn_alignbyte(W[2], W[1], s);
-    tn.t2 = __builtin_amdgcn_alignbyte(W[3], W[2], s);
-    tn.t3 = __builtin_amdgcn_alignbyte(W[4], W[3], s);
-    tn.n0 = __builtin_amdgcn_alignbyte(W[5], W[4], s);
-    tn.n1 = __builtin_amdgcn_alignbyte(W[6], W[5], s);
-    tn.n2 = __builtin_amdgcn_alignbyte(W[7], W[6], s);
-    prefix = W[0] & lowmask(s);
+    const uint32_t w0 = t[0], w1 = t[1], w2 = t[2], w3 = t[3], w4 = t[4], w5 = t[5], w6 = t[6];
+    const uint32_t w7 = load_bytes(data + (L & ~3u) + 28, s);
+    g0 = __builtin_amdgcn_alignbyte(w1, w0, s);
+    g1 = __builtin_amdgcn_alignbyte(w2, w1, s);
+    g2 = __builtin_amdgcn_alignbyte(w3, w2, s);
+    g3 = __builtin_amdgcn_alignbyte(w4, w3, s);
+    n0 = __builtin_amdgcn_alignbyte(w5, w4, s);
+    n1 = __builtin_amdgcn_alignbyte(w6, w5, s);
+    n2 = __builtin_amdgcn_alignbyte(w7, w6, s);
 }
 
-// Writes prefix (s = L%4 bytes, the end of the payload) followed by tag||nonce (tn[0..6]) at
+// Writes prefix (s = L%4 bytes, the end of the payload) followed by tag||nonce at
 // data + (L & ~3): 7 dwords + s bytes, never touching bytes past L+28.
 __device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t sh) {
     return (uint32_t)((((uint64_t)hi << 32) | lo) >> sh);  // sh in [8, 32]
 }
-__device__ __forceinline__ void write_tail(uint8_t *data, uint32_t L, const Tail &tn, uint32_t prefix) {
+__device__ __forceinline__ void write_tail(uint8_t *data, uint32_t L, uint32_t g0, uint32_t g1, uint32_t g2,
+                                           uint32_t g3, uint32_t n0, uint32_t n1, uint32_t n2, uint32_t prefix) {
     const uint32_t s = L & 3u;
     uint32_t *t = reinterpret_cast<uint32_t *>(data + (L & ~3u));
     const uint32_t sh = 32 - 8 * s;  // 32 when s == 0
-    t[0] = (uint32_t)((((uint64_t)tn.t0 << 32) | ((uint64_t)prefix << sh)) >> sh);
-    t[1] = funnel(tn.t1, tn.t0, sh);
-    t[2] = funnel(tn.t2, tn.t1, sh);
-    t[3] = funnel(tn.t3, tn.t2, sh);
-    t[4] = funnel(tn.n0, tn.t3, sh);
-    t[5] = funnel(tn.n1, tn.n0, sh);
-    t[6] = funnel(tn.n2, tn.n1, sh);
-    if (s) store_bytes(data + (L & ~3u) + 28, tn.n2 >> sh, s);
+    t[0] = (uint32_t)((((uint64_t)g0 << 32) | ((uint64_t)prefix << sh)) >> sh);
+    t[1] = funnel(g1, g0, sh);
+    t[2] = funnel(g2, g1, sh);
+    t[3] = funnel(g3, g2, sh);
+    t[4] = funnel(n0, g3, sh);
+    t[5] = funnel(n1, n0, sh);
+    t[6] = funnel(n2, n1, sh);
+    if (s) store_bytes(data + (L & ~3u) + 28, n2 >> sh, s);
 }
 
 template <bool kSeal>
@@ -289,17 +291,15 @@ __global__ void __launch_bounds__(kThreads) gcm_kernel(Batch b, const uint32_t *
         uint8_t *raw = b.arena + off;
         uint8_t *data = raw + 4;  // common.PacketStart
 
-        Tail tn;
-        uint32_t prefix;
+        uint32_t g0 = 0, g1 = 0, g2 = 0, g3 = 0, n0, n1, n2;
         if (kSeal && b.nonces) {
             const uint32_t *np = reinterpret_cast<const uint32_t *>(b.nonces + 12ull * pkt);
-            tn.n0 = np[0];
-            tn.n1 = np[1];
-            tn.n2 = np[2];
+            n0 = np[0];
+            n1 = np[1];
+            n2 = np[2];
         } else {
-            read_tail(data, L, tn, prefix);
+            read_tail(data, L, g0, g1, g2, g3, n0, n1, n2);
         }
-        const uint32_t n0 = tn.n0, n1 = tn.n1, n2 = tn.n2;
 
         // GHASH(A): the additional data is the 4-B private-IP header Raw[0:4].
         uint32_t y0 = 0, y1 = 0, y2 = 0, y3 = 0;
@@ -331,7 +331,7 @@ __global__ void __launch_bounds__(kThreads) gcm_kernel(Batch b, const uint32_t *
             ghash_mul(y0, y1, y2, y3, gb);
         }
         const uint32_t r = L & 15u;
-        prefix = 0;
+        uint32_t prefix = 0;
         if (r) {
             const uint32_t ctr = nfull + 2;
             if ((ctr & 0xffu) == 0) ctr_setup(cc, n0, n1, n2, ctr >> 8, kk, lb);
@@ -372,14 +372,10 @@ __global__ void __launch_bounds__(kThreads) gcm_kernel(Batch b, const uint32_t *
         const uint32_t t0 = y0 ^ e0, t1 = y1 ^ e1, t2 = y2 ^ e2, t3 = y3 ^ e3;
 
         if (kSeal) {
-            tn.t0 = t0;
-            tn.t1 = t1;
-            tn.t2 = t2;
-            tn.t3 = t3;
-            write_tail(data, L, tn, prefix);
+            write_tail(data, L, t0, t1, t2, t3, n0, n1, n2, prefix);
             if (b.status) b.status[pkt] = 1;
         } else {
-            const bool ok = ((t0 ^ tn.t0) | (t1 ^ tn.t1) | (t2 ^ tn.t2) | (t3 ^ tn.t3)) == 0;
+            const bool ok = ((t0 ^ g0) | (t1 ^ g1) | (t2 ^ g2) | (t3 ^ g3)) == 0;
             if (!ok) {
                 // Go 1.9 crypto/cipher gcm Open: zero the would-be plaintext on tag mismatch.
                 uint32_t *dw = reinterpret_cast<uint32_t *>(data);
@@ -392,11 +388,18 @@ __global__ void __launch_bounds__(kThreads) gcm_kernel(Batch b, const uint32_t *
 }
 
 hipError_t init_kernels() {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&gcm_kernel<true>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
-    if (e != hipSuccess) return e;
-    return hipFuncSetAttribute(reinterpret_cast<const void *>(&gcm_kernel<false>),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+    const void *ks[2] = {reinterpret_cast<const void *>(&gcm_kernel<true>),
+                         reinterpret_cast<const void *>(&gcm_kernel<false>)};
+    for (const void *k : ks) {
+        hipFuncAttributes a;
+        hipError_t e = hipFuncGetAttributes(&a, k);
+        if (e != hipSuccess) return e;
+        // absolute LDS addressing from 0 requires no static LDS in the packet kernels
+        if (a.sharedSizeBytes != 0) return hipErrorInvalidKernelFile;
+        e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 hipError_t launch_seal(const Batch &b, int grid, hipStream_t s) {
