@@ -135,6 +135,28 @@ __device__ __forceinline__ void ctr_block(const Ctr &c, uint32_t lo, const Keys 
     round_last(s0, s1, s2, s3, k, lb);
 }
 
+// N consecutive counter blocks lo, lo+1, ... (same 256-block segment) in lockstep: N independent
+// dependency chains per lane, so a wave keeps N x 16 LDS lookups in flight per round.
+template <int N>
+__device__ __forceinline__ void ctr_blocks(const Ctr &c, uint32_t lo, const Keys &k, uint32_t lb, uint32_t (&s)[N][4]) {
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        const uint32_t x = (lo + j) ^ c.x3;
+        const uint32_t t0 = c.K0 ^ rot16(lds32(((x << 8) | lb) + 128u));
+        s[j][0] = c.U0 ^ TE0(t0, 0);
+        s[j][1] = c.U1 ^ rot16(TE1(t0, 3));
+        s[j][2] = c.U2 ^ rot16(TE0(t0, 2));
+        s[j][3] = c.U3 ^ TE1(t0, 1);
+    }
+#pragma unroll
+    for (int r = 3; r < 14; ++r) {
+#pragma unroll
+        for (int j = 0; j < N; ++j) round_full(s[j][0], s[j][1], s[j][2], s[j][3], k, r, lb);
+    }
+#pragma unroll
+    for (int j = 0; j < N; ++j) round_last(s[j][0], s[j][1], s[j][2], s[j][3], k, lb);
+}
+
 // Y <- Y * H in GF(2^128) via the 4-bit comb in this wave's LDS table at gb (byte1/2 of gb hold
 // its base; byte0 is 0).  Entry (p, v) at gb + p*256 + v*16, p = nibble position (2*byte for the
 // high nibble, 2*byte+1 for the low one), v = nibble value.
@@ -224,7 +246,7 @@ __device__ __forceinline__ void write_tail(uint8_t *data, uint32_t L, uint32_t g
 }
 
 template <bool kSeal>
-__global__ void __launch_bounds__(kThreads) gcm_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) gcm_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = threadIdx.x >> 6;
 
@@ -314,7 +336,39 @@ __global__ void __launch_bounds__(kThreads) gcm_kernel(Batch b, const uint32_t *
         ctr_block(cc, 1, kk, lb, e0, e1, e2, e3);
 
         const uint32_t nfull = L >> 4;
-        for (uint32_t i = 0; i < nfull; ++i) {
+        uint32_t i = 0;
+        // Groups of 4 full blocks: counters i+2 .. i+5.  Groups start at low byte 2 mod 4, so only
+        // a group starting at 254 crosses a 256-block segment; it takes the per-block route.
+        for (; i + 4 <= nfull; i += 4) {
+            const uint32_t ctr = i + 2, lo = ctr & 0xffu;
+            uint32_t ks[4][4];
+            if (lo <= 252u) {
+                ctr_blocks<4>(cc, lo, kk, lb, ks);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint32_t cj = ctr + j;
+                    if ((cj & 0xffu) == 0) ctr_setup(cc, n0, n1, n2, cj >> 8, kk, lb);
+                    ctr_block(cc, cj & 0xffu, kk, lb, ks[j][0], ks[j][1], ks[j][2], ks[j][3]);
+                }
+            }
+            W4 *p = reinterpret_cast<W4 *>(data + 16u * i);
+            W4 in[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) in[j] = p[j];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const W4 out = {in[j].x ^ ks[j][0], in[j].y ^ ks[j][1], in[j].z ^ ks[j][2], in[j].w ^ ks[j][3]};
+                p[j] = out;
+                const W4 &c = kSeal ? out : in[j];
+                y0 ^= c.x;
+                y1 ^= c.y;
+                y2 ^= c.z;
+                y3 ^= c.w;
+                ghash_mul(y0, y1, y2, y3, gb);
+            }
+        }
+        for (; i < nfull; ++i) {
             const uint32_t ctr = i + 2;  // inc32(J0) + i
             if ((ctr & 0xffu) == 0) ctr_setup(cc, n0, n1, n2, ctr >> 8, kk, lb);
             uint32_t k0, k1, k2, k3;
