@@ -2,7 +2,7 @@
 
 Workload per rank (BASELINE config 2, the single-GPU headline): 2^20 packets x 1350 B, one key
 (NewAES("AES256Key-32Characters1234567890", salt 00..1f)), AAD = 4-B private IP, explicit seeded
-nonces, slots laid out as Payload.Raw records of 1392 B.  One step = seal every packet, then
+nonces, slots laid out as Payload.Raw records of 1408 B with 64-B aligned payloads.  One step = seal every packet, then
 unseal every packet (crypto/aes.go Encrypt then Decrypt), the reference's BenchmarkAES loop body
 (crypto/crypto_test.go:103-131) over a batch.  Multi-GPU: one process per GPU, each sealing its
 own shard (packets are independent: no data-path collective), weak scaling.
@@ -39,7 +39,7 @@ def parse() -> argparse.Namespace:
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--packets", type=int, default=1 << 20, help="packets per GPU")
     p.add_argument("--len", type=int, default=1350, help="payload bytes per packet")
-    p.add_argument("--stride", type=int, default=0, help="slot stride (0 = smallest 16-B multiple)")
+    p.add_argument("--stride", type=int, default=0, help="slot stride (0 = smallest 64-B multiple)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
     return p.parse_args()
@@ -76,12 +76,15 @@ def main() -> None:
     dev = torch.device("cuda", local)
 
     N, L = args.packets, args.len
-    stride = args.stride or batch.slot_stride(L)
+    stride = args.stride or batch.slot_stride(L, align=64)
     ctx = Context(device=local, max_keys=16)
     key = derive_key(SECRET, SALT)  # crypto/aes.go:66, host, once
     ctx.set_key(0, key)
 
-    arena = torch.zeros(N * stride, dtype=torch.uint8, device=dev)
+    # Slots are Payload.Raw records; the arena starts 60 B into a 64-B aligned allocation so every
+    # payload (Raw[4:]) is 64-B aligned and each quad of lanes moves whole 64-B granules.
+    arena_alloc = torch.zeros(N * stride + 64, dtype=torch.uint8, device=dev)
+    arena = arena_alloc[60:]
     nonces = torch.zeros(12 * N, dtype=torch.uint8, device=dev)
     status = torch.zeros(N, dtype=torch.uint8, device=dev)
     aad_word = int.from_bytes(AAD, "little")
@@ -150,7 +153,7 @@ def main() -> None:
             "dtype": "u8",
             "data": "synthetic (seeded splitmix64 payloads and nonces, one PBKDF2-derived key)",
             "config": {"workload": f"config2: {N} x {L} B packets per GPU, seal then unseal, 1 key, AAD 4 B",
-                       "packets_per_gpu": N, "payload_len": L, "slot_stride": stride,
+                       "packets_per_gpu": N, "payload_len": L, "slot_stride": stride, "payload_align": 64,
                        "parallelism": f"replicas/shards x{world}, no collectives"},
             "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,

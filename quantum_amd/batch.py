@@ -24,9 +24,9 @@ def _ptr(t: torch.Tensor | None) -> int | None:
     return None if t is None else int(t.data_ptr())
 
 
-def slot_stride(max_len: int) -> int:
-    """Smallest 16-byte multiple holding [aad 4][payload][tag 16][nonce 12]."""
-    return (4 + max_len + _lib.OVERHEAD + 15) & ~15
+def slot_stride(max_len: int, align: int = 16) -> int:
+    """Smallest multiple of `align` holding [aad 4][payload][tag 16][nonce 12]."""
+    return (4 + max_len + _lib.OVERHEAD + align - 1) // align * align
 
 
 def seal_uniform(ctx: Context, arena: torch.Tensor, stride: int, n: int, length: int, key_idx: int,

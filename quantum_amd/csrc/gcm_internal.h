@@ -7,19 +7,15 @@
 
 namespace qgcm {
 
-// Workgroup shape of the packet kernels: 8 wave64s, one workgroup per CU (LDS-bound design,
-// see DESIGN.md "Kernel").
-constexpr int kWaves = 8;
-constexpr int kThreads = kWaves * 64;
-// LDS: Te0/Te1 replicated 32x, rows of 256 B (x<<8 | lane*4, Te1 at +128) = 64 KiB,
-// then one 8 KiB GHASH comb table per wave.
+// LDS: Te0/Te1 replicated 32x, rows of 256 B (x<<8 | lane*4, Te1 at +128) = 64 KiB, then
+// 8 KiB GHASH comb tables (one per wave, or one per workgroup for single-key batches).
+// One workgroup per CU (DESIGN.md "Kernel").
 constexpr uint32_t kTeBytes = 65536;
 constexpr uint32_t kGhBytes = 8192;
-constexpr uint32_t kLdsBytes = kTeBytes + kWaves * kGhBytes;
-// Device key slot: 60 round-key words (+4 pad), their rot16 copies, and the 4-bit comb table of
-// H (512 x 16 B).
+// Device key slot: 60 round-key words (+4 pad), their rot16 copies, and the 4-bit comb tables of
+// H and H^4 (2 x 512 x 16 B).
 constexpr uint32_t kRkWords = 128;  // [0,64): rk words, [64,128): rot16(rk)
-constexpr uint32_t kGhEntries = 512;
+constexpr uint32_t kGhEntries = 1024;  // [0,512): comb of H, [512,1024): comb of H^4
 
 struct Batch {
     uint8_t *arena;
@@ -39,9 +35,13 @@ struct Batch {
     uint32_t max_keys;
 };
 
+constexpr int kNumVariants = 4;
+constexpr int kVariantGeneral = 0;   // per-wave GHASH tables, any key mix
+constexpr int kVariantUniform = 1;   // default for single-key (uniform) batches: the quad kernel
 hipError_t init_kernels();
-hipError_t launch_seal(const Batch &b, int grid, hipStream_t s);
-hipError_t launch_open(const Batch &b, int grid, hipStream_t s);
+int variant_waves(int variant);
+bool variant_quad(int variant);
+hipError_t launch_packets(bool seal, int variant, const Batch &b, int grid, hipStream_t s);
 hipError_t launch_key_setup(const uint8_t *d_keys, uint32_t first, uint32_t count, uint32_t *rk_table,
                             uint4 *gh_table, const uint8_t *d_sbox, hipStream_t s);
 // Groups descriptor batches into key-uniform 64-packet tiles (counting sort by key_idx).

@@ -163,6 +163,8 @@ __device__ __forceinline__ void ctr_blocks(const Ctr &c, uint32_t lo, const Keys
 __device__ __forceinline__ void ghash_mul(uint32_t &y0, uint32_t &y1, uint32_t &y2, uint32_t &y3, uint32_t gb) {
     uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
     const uint32_t yw[4] = {y0, y1, y2, y3};
+    // Four chunks of 8 lookups (one input word each): at most 8 x 16 B of results live, which is all
+    // the LDS queue can overlap anyway (lgkmcnt tracks 15 in flight per wave).
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
         const uint32_t hi = yw[w] & 0xf0f0f0f0u;
@@ -177,6 +179,7 @@ __device__ __forceinline__ void ghash_mul(uint32_t &y0, uint32_t &y1, uint32_t &
             a2 = xor3(a2, th.z, tl.z);
             a3 = xor3(a3, th.w, tl.w);
         }
+        asm volatile("" ::: "memory");  // hard fence for the LDS loads of the next chunk
     }
     y0 = a0;
     y1 = a1;
@@ -245,24 +248,39 @@ __device__ __forceinline__ void write_tail(uint8_t *data, uint32_t L, uint32_t g
     if (s) store_bytes(data + (L & ~3u) + 28, n2 >> sh, s);
 }
 
-template <bool kSeal>
-__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) gcm_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
+// Kernel variants.  kW waves per workgroup (one workgroup per CU); kShared: one GHASH table for
+// the whole workgroup (uniform single-key batches) instead of one per wave; kIlp counter blocks
+// per lane per iteration.
+template <int kW, bool kShared>
+constexpr uint32_t lds_bytes() {
+    return kTeBytes + (kShared ? 1u : (uint32_t)kW) * kGhBytes;
+}
+
+template <bool kSeal, int kW, bool kShared, int kIlp>
+__global__ void __launch_bounds__(kW * 64) __attribute__((amdgpu_waves_per_eu(kW / 4, kW / 4)))
+gcm_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
+    constexpr uint32_t kT = kW * 64;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = threadIdx.x >> 6;
 
     // Fill the replicated T-tables: dword i = row x = i/64, slot i%64 (<32: Te0, else Te1).
-    for (uint32_t i = threadIdx.x; i < kTeBytes / 4; i += kThreads) {
+    for (uint32_t i = threadIdx.x; i < kTeBytes / 4; i += kT) {
         const uint32_t x = i >> 6, slot = i & 63u;
         lds_st32(4 * i, b.te[(slot >> 5) * 256u + x]);
+    }
+    const uint32_t gb = kTeBytes + (kShared ? 0u : wave) * kGhBytes;
+    uint32_t cur_key = 0xffffffffu;
+    if (kShared) {
+        const uint4 *src = b.gh_table + (size_t)b.uniform_key * kGhEntries;
+        for (uint32_t e = threadIdx.x; e < 512u; e += kT) lds_st128(kTeBytes + e * 16, src[e]);  // H only
+        cur_key = b.uniform_key;
     }
     __syncthreads();
 
     const uint32_t lb = (lane & 31u) << 2;
-    const uint32_t gb = kTeBytes + wave * kGhBytes;
-    uint32_t cur_key = 0xffffffffu;
     const uint32_t ntiles = b.n_items >> 6;
 
-    for (uint32_t tile = blockIdx.x * kWaves + wave; tile < ntiles; tile += gridDim.x * kWaves) {
+    for (uint32_t tile = blockIdx.x * kW + wave; tile < ntiles; tile += gridDim.x * kW) {
         const uint32_t item = tile * 64u + lane;
         const uint32_t pkt = b.worklist ? b.worklist[item] : item;
         bool valid = pkt < b.n;
@@ -283,8 +301,8 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2
         const uint64_t vmask = __ballot(valid);
         if (vmask == 0) continue;
         const int first = __ffsll((unsigned long long)vmask) - 1;
-        const uint32_t wkey = __builtin_amdgcn_readfirstlane(__shfl(key, first));
-        if (wkey != cur_key) {
+        const uint32_t wkey = kShared ? b.uniform_key : __builtin_amdgcn_readfirstlane(__shfl(key, first));
+        if (!kShared && wkey != cur_key) {
             const uint4 *src = b.gh_table + (size_t)wkey * kGhEntries;
 #pragma unroll
             for (int r = 0; r < 8; ++r) {
@@ -337,43 +355,13 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2
 
         const uint32_t nfull = L >> 4;
         uint32_t i = 0;
-        // Groups of 4 full blocks: counters i+2 .. i+5.  Groups start at low byte 2 mod 4, so only
-        // a group starting at 254 crosses a 256-block segment; it takes the per-block route.
-        for (; i + 4 <= nfull; i += 4) {
-            const uint32_t ctr = i + 2, lo = ctr & 0xffu;
-            uint32_t ks[4][4];
-            if (lo <= 252u) {
-                ctr_blocks<4>(cc, lo, kk, lb, ks);
-            } else {
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const uint32_t cj = ctr + j;
-                    if ((cj & 0xffu) == 0) ctr_setup(cc, n0, n1, n2, cj >> 8, kk, lb);
-                    ctr_block(cc, cj & 0xffu, kk, lb, ks[j][0], ks[j][1], ks[j][2], ks[j][3]);
-                }
-            }
-            W4 *p = reinterpret_cast<W4 *>(data + 16u * i);
-            W4 in[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) in[j] = p[j];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const W4 out = {in[j].x ^ ks[j][0], in[j].y ^ ks[j][1], in[j].z ^ ks[j][2], in[j].w ^ ks[j][3]};
-                p[j] = out;
-                const W4 &c = kSeal ? out : in[j];
-                y0 ^= c.x;
-                y1 ^= c.y;
-                y2 ^= c.z;
-                y3 ^= c.w;
-                ghash_mul(y0, y1, y2, y3, gb);
-            }
-        }
-        for (; i < nfull; ++i) {
-            const uint32_t ctr = i + 2;  // inc32(J0) + i
+        // One block through the counter cache (re-derived at each 256-block segment).
+        auto single = [&](uint32_t bi) {
+            const uint32_t ctr = bi + 2;  // inc32(J0) + bi
             if ((ctr & 0xffu) == 0) ctr_setup(cc, n0, n1, n2, ctr >> 8, kk, lb);
             uint32_t k0, k1, k2, k3;
             ctr_block(cc, ctr & 0xffu, kk, lb, k0, k1, k2, k3);
-            W4 *p = reinterpret_cast<W4 *>(data + 16u * i);
+            W4 *p = reinterpret_cast<W4 *>(data + 16u * bi);
             const W4 in = *p;
             const W4 out = {in.x ^ k0, in.y ^ k1, in.z ^ k2, in.w ^ k3};
             *p = out;
@@ -383,7 +371,40 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2
             y2 ^= c.z;
             y3 ^= c.w;
             ghash_mul(y0, y1, y2, y3, gb);
+        };
+        if constexpr (kIlp > 1) {
+            for (; i + kIlp <= nfull; i += kIlp) {
+                const uint32_t ctr = i + 2, lo = ctr & 0xffu;
+                uint32_t ks[kIlp][4];
+                if (lo == 0) ctr_setup(cc, n0, n1, n2, ctr >> 8, kk, lb);
+                if (lo + (kIlp - 1) <= 255u) {
+                    ctr_blocks<kIlp>(cc, lo, kk, lb, ks);
+                } else {
+#pragma unroll
+                    for (int j = 0; j < kIlp; ++j) {
+                        const uint32_t cj = ctr + j;
+                        if ((cj & 0xffu) == 0) ctr_setup(cc, n0, n1, n2, cj >> 8, kk, lb);
+                        ctr_block(cc, cj & 0xffu, kk, lb, ks[j][0], ks[j][1], ks[j][2], ks[j][3]);
+                    }
+                }
+                W4 *p = reinterpret_cast<W4 *>(data + 16u * i);
+                W4 in[kIlp];
+#pragma unroll
+                for (int j = 0; j < kIlp; ++j) in[j] = p[j];
+#pragma unroll
+                for (int j = 0; j < kIlp; ++j) {
+                    const W4 out = {in[j].x ^ ks[j][0], in[j].y ^ ks[j][1], in[j].z ^ ks[j][2], in[j].w ^ ks[j][3]};
+                    p[j] = out;
+                    const W4 &c = kSeal ? out : in[j];
+                    y0 ^= c.x;
+                    y1 ^= c.y;
+                    y2 ^= c.z;
+                    y3 ^= c.w;
+                    ghash_mul(y0, y1, y2, y3, gb);
+                }
+            }
         }
+        for (; i < nfull; ++i) single(i);
         const uint32_t r = L & 15u;
         uint32_t prefix = 0;
         if (r) {
@@ -441,29 +462,290 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Quad kernel (single-key batches): FOUR lanes per packet.  Lane m of a quad owns the packet's
+// 16-B blocks b = m, m+4, m+8, ... so every wave instruction moves 16 contiguous 64-B granules
+// (one per packet) -- full-granule HBM traffic, and only 16 packets in flight per wave, which keeps
+// 16 waves per CU within the caches.  GHASH runs as four interleaved Horner chains
+// Z_m <- Z_m * H^4 ^ C_b (comb table of H^4), recombined once per packet:
+//   Y = ( sum_m Z_m * H^(e_m - 1)  ^  [len(A)]||[len(C)] ) * H,   e_m = d + 1 - b_last(m),
+// with the additional data A folded in as block -1 of lane 3 (SP 800-38D GHASH, restated for a
+// 4-way interleave; checked against the oracle in tests).  E_K(J0) is computed by lane d % 4 in the
+// slot where it has no data block.
+constexpr uint32_t kQuadLds = kTeBytes + 2 * kGhBytes;
+
+__device__ __forceinline__ uint32_t quad_xor(uint32_t v) {
+    v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xf, 0xf, false);  // quad_perm [1,0,3,2]
+    v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xf, 0xf, false);  // quad_perm [2,3,0,1]
+    return v;
+}
+
+template <bool kSeal, int kW, bool kFold>
+__global__ void __launch_bounds__(kW * 64) __attribute__((amdgpu_waves_per_eu(kW / 4, kW / 4)))
+gcm_quad_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
+    constexpr uint32_t kT = kW * 64;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = threadIdx.x >> 6;
+    const uint32_t m = lane & 3u;          // block residue owned by this lane
+    const uint32_t qd = lane >> 2;         // packet slot within the wave tile (16 per wave)
+
+    for (uint32_t i = threadIdx.x; i < kTeBytes / 4; i += kT) {
+        const uint32_t x = i >> 6, slot = i & 63u;
+        lds_st32(4 * i, b.te[(slot >> 5) * 256u + x]);
+    }
+    {
+        const uint4 *src = b.gh_table + (size_t)b.uniform_key * kGhEntries;  // H then H^4
+        for (uint32_t e = threadIdx.x; e < kGhEntries; e += kT) lds_st128(kTeBytes + e * 16, src[e]);
+    }
+    __syncthreads();
+
+    const uint32_t lb = (lane & 31u) << 2;
+    constexpr uint32_t gH = kTeBytes, gH4 = kTeBytes + kGhBytes;
+    const Keys kk = {rk_table + (size_t)b.uniform_key * kRkWords, rk_table + (size_t)b.uniform_key * kRkWords + 64};
+    const uint32_t ntiles = (b.n + 15) >> 4;
+
+    for (uint32_t tile = blockIdx.x * kW + wave; tile < ntiles; tile += gridDim.x * kW) {
+        const uint32_t pkt = tile * 16u + qd;
+        uint32_t L = b.uniform_len;
+        // Opaque per tile: stops LICM from hoisting dozens of L-derived values (masks, selectors)
+        // out of the tile loop, which would hold them in registers for the whole kernel.
+        asm volatile("" : "+s"(L));
+        bool valid = pkt < b.n;
+        if (!kSeal) {
+            if (L < (uint32_t)QGCM_OVERHEAD) valid = false;
+            L -= QGCM_OVERHEAD;
+        }
+        if (!valid) {
+            if (!kSeal && b.status && pkt < b.n && m == 0) b.status[pkt] = 0;
+            continue;  // the whole quad leaves together
+        }
+        uint8_t *raw = b.arena + (uint64_t)pkt * b.stride;
+        uint8_t *data = raw + 4;  // common.PacketStart
+
+        uint32_t g0 = 0, g1 = 0, g2 = 0, g3 = 0, n0, n1, n2;
+        if (kSeal && b.nonces) {
+            const uint32_t *np = reinterpret_cast<const uint32_t *>(b.nonces + 12ull * pkt);
+            n0 = np[0];
+            n1 = np[1];
+            n2 = np[2];
+        } else {
+            read_tail(data, L, g0, g1, g2, g3, n0, n1, n2);
+        }
+        const uint32_t nfull = L >> 4, r = L & 15u;
+        const uint32_t d = nfull + (r ? 1u : 0u);  // data blocks incl. the partial one
+
+        // lane 3 starts its chain with the additional data block (block -1)
+        uint32_t z0 = 0, z1 = 0, z2 = 0, z3 = 0;
+        if (m == 3 && b.aad_len)
+            z0 = *reinterpret_cast<const uint32_t *>(raw) & (b.aad_len >= 4 ? 0xffffffffu : lowmask(b.aad_len));
+        int blast = -1;
+
+        uint32_t e0 = 0, e1 = 0, e2 = 0, e3 = 0;  // E_K(J0)
+        uint32_t prefix = 0;
+        if constexpr (kFold) {
+        Ctr cc;
+        uint32_t hi = 0;
+        ctr_setup(cc, n0, n1, n2, 0, kk, lb);
+        // Lane m walks blocks m, m+4, ... < d, then (lane d % 4 only) the virtual block d = E_K(J0):
+        // one AES instance per step, and J0 fills the slot of the lane with the fewest data blocks.
+        for (uint32_t bi = m; bi <= d; bi += 4) {
+            const bool j0 = bi == d;
+            const uint32_t ctr = j0 ? 1u : bi + 2;  // J0, or inc32(J0) + bi
+            if ((ctr >> 8) != hi) {
+                hi = ctr >> 8;
+                ctr_setup(cc, n0, n1, n2, hi, kk, lb);
+            }
+            uint32_t k0, k1, k2, k3;
+            ctr_block(cc, ctr & 0xffu, kk, lb, k0, k1, k2, k3);
+            if (j0) {
+                e0 = k0;
+                e1 = k1;
+                e2 = k2;
+                e3 = k3;
+                break;
+            }
+            W4 *p = reinterpret_cast<W4 *>(data + 16u * bi);
+            const W4 in = *p;  // a partial block reads into the tag area: inside the slot
+            const W4 out = {in.x ^ k0, in.y ^ k1, in.z ^ k2, in.w ^ k3};
+            W4 c = kSeal ? out : in;
+            if (bi < nfull) {
+                *p = out;
+            } else {  // the partial last block (r bytes)
+                const uint32_t q = r >> 2, sb = r & 3u;
+                uint32_t *bw = reinterpret_cast<uint32_t *>(p);
+                if (q > 0) bw[0] = out.x;
+                if (q > 1) bw[1] = out.y;
+                if (q > 2) bw[2] = out.z;
+                const uint32_t oq = sel4(q, out.x, out.y, out.z, out.w) & lowmask(sb);
+                if (kSeal)
+                    prefix = oq;  // written with tag||nonce by write_tail
+                else
+                    store_bytes(reinterpret_cast<uint8_t *>(p) + 4 * q, oq, sb);
+                c.x &= q > 0 ? 0xffffffffu : lowmask(sb);
+                c.y &= q > 1 ? 0xffffffffu : (q == 1 ? lowmask(sb) : 0u);
+                c.z &= q > 2 ? 0xffffffffu : (q == 2 ? lowmask(sb) : 0u);
+                c.w &= q == 3 ? lowmask(sb) : 0u;
+            }
+            ghash_mul(z0, z1, z2, z3, gH4);
+            z0 ^= c.x;
+            z1 ^= c.y;
+            z2 ^= c.z;
+            z3 ^= c.w;
+            blast = (int)bi;
+        }
+        } else {
+        Ctr cc;
+        uint32_t hi = 0;
+        ctr_setup(cc, n0, n1, n2, 0, kk, lb);
+        for (uint32_t bi = m; bi < nfull; bi += 4) {
+            const uint32_t ctr = bi + 2;  // inc32(J0) + bi
+            if ((ctr >> 8) != hi) {
+                hi = ctr >> 8;
+                ctr_setup(cc, n0, n1, n2, hi, kk, lb);
+            }
+            uint32_t k0, k1, k2, k3;
+            ctr_block(cc, ctr & 0xffu, kk, lb, k0, k1, k2, k3);
+            W4 *p = reinterpret_cast<W4 *>(data + 16u * bi);
+            const W4 in = *p;
+            const W4 out = {in.x ^ k0, in.y ^ k1, in.z ^ k2, in.w ^ k3};
+            *p = out;
+            const W4 &c = kSeal ? out : in;
+            ghash_mul(z0, z1, z2, z3, gH4);
+            z0 ^= c.x;
+            z1 ^= c.y;
+            z2 ^= c.z;
+            z3 ^= c.w;
+            blast = (int)bi;
+        }
+        if (r && (nfull & 3u) == m) {  // the partial last block
+            const uint32_t ctr = nfull + 2;
+            if ((ctr >> 8) != hi) {
+                hi = ctr >> 8;
+                ctr_setup(cc, n0, n1, n2, hi, kk, lb);
+            }
+            uint32_t k0, k1, k2, k3;
+            ctr_block(cc, ctr & 0xffu, kk, lb, k0, k1, k2, k3);
+            uint8_t *blk = data + 16u * nfull;
+            const W4 in = *reinterpret_cast<const W4 *>(blk);  // reads into tag area: inside the slot
+            const uint32_t q = r >> 2, sb = r & 3u;
+            const uint32_t o0 = in.x ^ k0, o1 = in.y ^ k1, o2 = in.z ^ k2, o3 = in.w ^ k3;
+            uint32_t *bw = reinterpret_cast<uint32_t *>(blk);
+            if (q > 0) bw[0] = o0;
+            if (q > 1) bw[1] = o1;
+            if (q > 2) bw[2] = o2;
+            const uint32_t oq = sel4(q, o0, o1, o2, o3) & lowmask(sb);
+            W4 c = kSeal ? W4{o0, o1, o2, o3} : in;
+            if (kSeal)
+                prefix = oq;  // written with tag||nonce by write_tail
+            else
+                store_bytes(blk + 4 * q, oq, sb);
+            c.x &= q > 0 ? 0xffffffffu : lowmask(sb);
+            c.y &= q > 1 ? 0xffffffffu : (q == 1 ? lowmask(sb) : 0u);
+            c.z &= q > 2 ? 0xffffffffu : (q == 2 ? lowmask(sb) : 0u);
+            c.w &= q == 3 ? lowmask(sb) : 0u;
+            ghash_mul(z0, z1, z2, z3, gH4);
+            z0 ^= c.x;
+            z1 ^= c.y;
+            z2 ^= c.z;
+            z3 ^= c.w;
+            blast = (int)nfull;
+        }
+        // E_K(J0) in lane d % 4 (the lane with the fewest data blocks)
+        if (m == (d & 3u)) {
+            if (hi != 0) ctr_setup(cc, n0, n1, n2, 0, kk, lb);
+            ctr_block(cc, 1, kk, lb, e0, e1, e2, e3);
+        }
+        }
+        // Z_m * H^(e_m - 1), e_m = d + 1 - b_last(m)
+        for (int t = (int)d - blast; t > 0; --t) ghash_mul(z0, z1, z2, z3, gH);
+        z0 = quad_xor(z0);
+        z1 = quad_xor(z1);
+        z2 = quad_xor(z2);
+        z3 = quad_xor(z3);
+        e0 = quad_xor(e0);
+        e1 = quad_xor(e1);
+        e2 = quad_xor(e2);
+        e3 = quad_xor(e3);
+        z1 ^= bswap(b.aad_len * 8u);  // [len(A)]_64 || [len(C)]_64, big endian
+        z3 ^= bswap(L * 8u);
+        ghash_mul(z0, z1, z2, z3, gH);
+        const uint32_t t0 = z0 ^ e0, t1 = z1 ^ e1, t2 = z2 ^ e2, t3 = z3 ^ e3;
+        // the lane owning the partial block (or lane 0) writes the tail
+        const uint32_t owner = r ? (nfull & 3u) : 0u;
+        if (kSeal) {
+            if (m == owner) {
+                write_tail(data, L, t0, t1, t2, t3, n0, n1, n2, prefix);
+                if (b.status) b.status[pkt] = 1;
+            }
+        } else {
+            const bool ok = ((t0 ^ g0) | (t1 ^ g1) | (t2 ^ g2) | (t3 ^ g3)) == 0;
+            if (!ok) {
+                // Go 1.9 crypto/cipher gcm Open: zero the would-be plaintext on tag mismatch.
+                for (uint32_t bi = m; bi < nfull; bi += 4) {
+                    const W4 zz = {0, 0, 0, 0};
+                    *reinterpret_cast<W4 *>(data + 16u * bi) = zz;
+                }
+                if (r && m == owner) {
+                    uint32_t *bw = reinterpret_cast<uint32_t *>(data + 16u * nfull);
+                    for (uint32_t w = 0; w < (r >> 2); ++w) bw[w] = 0;
+                    store_bytes(data + 16u * nfull + (r & ~3u), 0, r & 3u);
+                }
+            }
+            if (b.status && m == 0) b.status[pkt] = ok ? 1 : 0;
+        }
+    }
+}
+
+// Variant table: index = QGCM variant id (Batch-independent), see qgcm_api.cpp.
+struct Variant {
+    const void *seal, *open;
+    int waves;
+    uint32_t lds;
+    bool quad;  // 16 packets per wave tile instead of 64
+};
+
+template <int kW, bool kShared, int kIlp>
+Variant make_variant() {
+    return Variant{reinterpret_cast<const void *>(&gcm_kernel<true, kW, kShared, kIlp>),
+                   reinterpret_cast<const void *>(&gcm_kernel<false, kW, kShared, kIlp>), kW,
+                   lds_bytes<kW, kShared>(), false};
+}
+
+template <int kW, bool kFold>
+Variant make_quad() {
+    return Variant{reinterpret_cast<const void *>(&gcm_quad_kernel<true, kW, kFold>),
+                   reinterpret_cast<const void *>(&gcm_quad_kernel<false, kW, kFold>), kW, kQuadLds, true};
+}
+
+static Variant g_variants[kNumVariants];
+
 hipError_t init_kernels() {
-    const void *ks[2] = {reinterpret_cast<const void *>(&gcm_kernel<true>),
-                         reinterpret_cast<const void *>(&gcm_kernel<false>)};
-    for (const void *k : ks) {
-        hipFuncAttributes a;
-        hipError_t e = hipFuncGetAttributes(&a, k);
-        if (e != hipSuccess) return e;
-        // absolute LDS addressing from 0 requires no static LDS in the packet kernels
-        if (a.sharedSizeBytes != 0) return hipErrorInvalidKernelFile;
-        e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
-        if (e != hipSuccess) return e;
+    g_variants[0] = make_variant<8, false, 4>();  // general: lane per packet, per-wave GHASH tables
+    g_variants[1] = make_quad<16, false>();        // single key: 4 lanes per packet, 16 waves/CU
+    g_variants[2] = make_quad<16, true>();         // same, partial block and J0 folded into the loop
+    g_variants[3] = make_variant<8, true, 4>();    // single key, lane per packet, shared GHASH table
+    for (const Variant &v : g_variants) {
+        for (const void *k : {v.seal, v.open}) {
+            hipFuncAttributes a;
+            hipError_t e = hipFuncGetAttributes(&a, k);
+            if (e != hipSuccess) return e;
+            // absolute LDS addressing from 0 requires no static LDS in the packet kernels
+            if (a.sharedSizeBytes != 0) return hipErrorInvalidKernelFile;
+            e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, v.lds);
+            if (e != hipSuccess) return e;
+        }
     }
     return hipSuccess;
 }
 
-hipError_t launch_seal(const Batch &b, int grid, hipStream_t s) {
-    hipLaunchKernelGGL(gcm_kernel<true>, dim3(grid), dim3(kThreads), kLdsBytes, s, b, b.rk_table);
-    return hipGetLastError();
-}
+int variant_waves(int v) { return g_variants[v].waves; }
+bool variant_quad(int v) { return g_variants[v].quad; }
 
-hipError_t launch_open(const Batch &b, int grid, hipStream_t s) {
-    hipLaunchKernelGGL(gcm_kernel<false>, dim3(grid), dim3(kThreads), kLdsBytes, s, b, b.rk_table);
-    return hipGetLastError();
+hipError_t launch_packets(bool seal, int variant, const Batch &b, int grid, hipStream_t s) {
+    if (variant < 0 || variant >= kNumVariants) return hipErrorInvalidValue;
+    const Variant &v = g_variants[variant];
+    void *args[] = {const_cast<Batch *>(&b), const_cast<uint32_t **>(&b.rk_table)};
+    return hipLaunchKernel(seal ? v.seal : v.open, dim3(grid), dim3(v.waves * 64), args, v.lds, s);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -472,11 +754,38 @@ hipError_t launch_open(const Batch &b, int grid, hipStream_t s) {
 // T_p[v] = sum over set bits of v (MSB = x^0) of x^(4p+k) * H.
 __device__ __forceinline__ uint8_t xt(uint8_t a) { return (uint8_t)((a << 1) ^ ((a & 0x80) ? 0x1b : 0)); }
 
+__device__ inline void shift_x(uint8_t v[16]) {
+    const int lsb = v[15] & 1;
+    for (int j = 15; j > 0; --j) v[j] = (uint8_t)((v[j] >> 1) | (v[j - 1] << 7));
+    v[0] >>= 1;
+    if (lsb) v[0] ^= 0xe1;
+}
+__device__ inline uint4 pack16(const uint8_t v[16]) {
+    uint4 w;
+    w.x = v[0] | v[1] << 8 | v[2] << 16 | (uint32_t)v[3] << 24;
+    w.y = v[4] | v[5] << 8 | v[6] << 16 | (uint32_t)v[7] << 24;
+    w.z = v[8] | v[9] << 8 | v[10] << 16 | (uint32_t)v[11] << 24;
+    w.w = v[12] | v[13] << 8 | v[14] << 16 | (uint32_t)v[15] << 24;
+    return w;
+}
+// SP 800-38D Algorithm 1 on byte strings (key setup only).
+__device__ inline void gf128_mul_bytes(const uint8_t X[16], const uint8_t Y[16], uint8_t Z[16]) {
+    uint8_t z[16] = {0}, v[16];
+    for (int i = 0; i < 16; ++i) v[i] = Y[i];
+    for (int i = 0; i < 128; ++i) {
+        if ((X[i >> 3] >> (7 - (i & 7))) & 1)
+            for (int j = 0; j < 16; ++j) z[j] ^= v[j];
+        shift_x(v);
+    }
+    for (int i = 0; i < 16; ++i) Z[i] = z[i];
+}
+
 __global__ void __launch_bounds__(256) key_setup_kernel(const uint8_t *keys, uint32_t first, uint32_t *rk_table,
                                                         uint4 *gh_table, const uint8_t *sbox_g) {
     __shared__ uint8_t sbox[256];
     __shared__ uint8_t rkb[240];
     __shared__ uint4 pw[128];
+    __shared__ uint4 pw4[128];
     const uint32_t kidx = blockIdx.x;
     const uint8_t *key = keys + 32u * kidx;
     sbox[threadIdx.x] = sbox_g[threadIdx.x];
@@ -518,21 +827,22 @@ __global__ void __launch_bounds__(256) key_setup_kernel(const uint8_t *keys, uin
             }
             for (int i = 0; i < 16; ++i) s[i] ^= rkb[16 * round + i];
         }
-        // x^i * H: multiply by x = shift toward higher bit index (right shift of the byte string),
-        // reduce with R = 0xe1 || 0^120 (SP 800-38D Algorithm 1).
-        uint8_t v[16];
-        for (int i = 0; i < 16; ++i) v[i] = s[i];
+        // H^4 = (H^2)^2 by SP 800-38D Algorithm 1 (bit-serial; setup only).
+        uint8_t h2[16], h4[16];
+        gf128_mul_bytes(s, s, h2);
+        gf128_mul_bytes(h2, h2, h4);
+        // x^i * H and x^i * H^4: multiply by x = shift toward higher bit index (right shift of the
+        // byte string), reduce with R = 0xe1 || 0^120 (SP 800-38D Algorithm 1).
+        uint8_t v[16], v4[16];
+        for (int i = 0; i < 16; ++i) {
+            v[i] = s[i];
+            v4[i] = h4[i];
+        }
         for (int i = 0; i < 128; ++i) {
-            uint4 w;
-            w.x = v[0] | v[1] << 8 | v[2] << 16 | (uint32_t)v[3] << 24;
-            w.y = v[4] | v[5] << 8 | v[6] << 16 | (uint32_t)v[7] << 24;
-            w.z = v[8] | v[9] << 8 | v[10] << 16 | (uint32_t)v[11] << 24;
-            w.w = v[12] | v[13] << 8 | v[14] << 16 | (uint32_t)v[15] << 24;
-            pw[i] = w;
-            const int lsb = v[15] & 1;
-            for (int j = 15; j > 0; --j) v[j] = (uint8_t)((v[j] >> 1) | (v[j - 1] << 7));
-            v[0] >>= 1;
-            if (lsb) v[0] ^= 0xe1;
+            pw[i] = pack16(v);
+            pw4[i] = pack16(v4);
+            shift_x(v);
+            shift_x(v4);
         }
     }
     __syncthreads();
@@ -545,12 +855,14 @@ __global__ void __launch_bounds__(256) key_setup_kernel(const uint8_t *keys, uin
         rk_table[(size_t)slot * kRkWords + i] = w;
         rk_table[(size_t)slot * kRkWords + 64 + i] = (w << 16) | (w >> 16);
     }
+    // entries [0, 512): comb table of H; [512, 1024): comb table of H^4
     for (uint32_t e = threadIdx.x; e < kGhEntries; e += 256) {
-        const uint32_t p = e >> 4, v = e & 15u;
+        const uint32_t p = (e & 511u) >> 4, v = e & 15u;
+        const uint4 *src = e < 512 ? pw : pw4;
         uint4 acc = {0, 0, 0, 0};
         for (int k = 0; k < 4; ++k) {
             if ((v >> (3 - k)) & 1u) {
-                const uint4 t = pw[4 * p + k];
+                const uint4 t = src[4 * p + k];
                 acc.x ^= t.x;
                 acc.y ^= t.y;
                 acc.z ^= t.z;

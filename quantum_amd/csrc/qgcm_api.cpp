@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 #include <sys/random.h>
 
@@ -21,6 +22,7 @@ struct qgcm_ctx {
     int device = 0;
     int num_cus = 0;
     uint32_t max_keys = 0;
+    int uniform_variant = kVariantUniform;  // kernel variant for single-key batches (QGCM_VARIANT)
     uint32_t *d_rk = nullptr;
     uint4 *d_gh = nullptr;
     uint32_t *d_te = nullptr;
@@ -88,10 +90,11 @@ void set_err(char *err, int errlen, const char *msg) {
 
 int hip_fail(hipError_t e) { return e == hipSuccess ? QGCM_OK : QGCM_E_HIP; }
 
-int grid_for(const qgcm_ctx *ctx, uint32_t n_items) {
-    const uint32_t tiles = n_items / 64;
-    const uint32_t wgs = (tiles + kWaves - 1) / kWaves;
-    const uint32_t cap = (uint32_t)ctx->num_cus;  // one 128-KiB-LDS workgroup per CU
+int grid_for(const qgcm_ctx *ctx, uint32_t n_items, int variant) {
+    const uint32_t waves = (uint32_t)variant_waves(variant);
+    const uint32_t tiles = variant_quad(variant) ? (n_items + 15) / 16 : n_items / 64;
+    const uint32_t wgs = (tiles + waves - 1) / waves;
+    const uint32_t cap = (uint32_t)ctx->num_cus;  // persistent: one LDS-filling workgroup per CU
     return (int)(wgs < cap ? (wgs ? wgs : 1) : cap);
 }
 
@@ -128,8 +131,8 @@ int run_uniform(qgcm_ctx *ctx, bool seal, uint8_t *arena, uint64_t stride, uint3
     b.n = n;
     b.n_items = (uint32_t)(((uint64_t)n + 63) & ~63ull);
     b.aad_len = aad_len;
-    const int grid = grid_for(ctx, b.n_items);
-    return hip_fail(seal ? launch_seal(b, grid, s) : launch_open(b, grid, s));
+    const int v = ctx->uniform_variant;
+    return hip_fail(launch_packets(seal, v, b, grid_for(ctx, b.n_items, v), s));
 }
 
 int run_descs(qgcm_ctx *ctx, bool seal, uint8_t *arena, const qgcm_desc *descs, uint32_t n, const uint8_t *nonces,
@@ -172,8 +175,7 @@ int run_descs(qgcm_ctx *ctx, bool seal, uint8_t *arena, const qgcm_desc *descs, 
     b.n = n;
     b.n_items = items;
     b.aad_len = aad_len;
-    const int grid = grid_for(ctx, b.n_items);
-    return hip_fail(seal ? launch_seal(b, grid, s) : launch_open(b, grid, s));
+    return hip_fail(launch_packets(seal, kVariantGeneral, b, grid_for(ctx, b.n_items, kVariantGeneral), s));
 }
 
 int ensure_io(qgcm_ctx *ctx, size_t bytes) {
@@ -241,6 +243,10 @@ qgcm_ctx *qgcm_create(int device, uint32_t max_keys, char *err, int errlen) {
     ctx->num_cus = prop.multiProcessorCount;
     ctx->max_keys = max_keys;
     ctx->key_set.assign(max_keys, 0);
+    if (const char *v = getenv("QGCM_VARIANT")) {
+        const int iv = atoi(v);
+        if (iv >= 0 && iv < kNumVariants) ctx->uniform_variant = iv;
+    }
     uint8_t sbox[256];
     uint32_t te[512];
     build_tables(sbox, te);
