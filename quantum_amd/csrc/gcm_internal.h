@@ -35,12 +35,13 @@ struct Batch {
     uint32_t max_keys;
 };
 
-constexpr int kNumVariants = 4;
+constexpr int kNumVariants = 7;
 constexpr int kVariantGeneral = 0;   // per-wave GHASH tables, any key mix
-constexpr int kVariantUniform = 1;   // default for single-key (uniform) batches: the quad kernel
+constexpr int kVariantUniform = 5;   // default for single-key (uniform) batches: quad kernel, 32 waves/CU
 hipError_t init_kernels();
 int variant_waves(int variant);
 bool variant_quad(int variant);
+int variant_wgs_per_cu(int variant);
 hipError_t launch_packets(bool seal, int variant, const Batch &b, int grid, hipStream_t s);
 hipError_t launch_key_setup(const uint8_t *d_keys, uint32_t first, uint32_t count, uint32_t *rk_table,
                             uint4 *gh_table, const uint8_t *d_sbox, hipStream_t s);

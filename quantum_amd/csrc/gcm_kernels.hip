@@ -179,7 +179,9 @@ __device__ __forceinline__ void ghash_mul(uint32_t &y0, uint32_t &y1, uint32_t &
             a2 = xor3(a2, th.z, tl.z);
             a3 = xor3(a3, th.w, tl.w);
         }
-        asm volatile("" ::: "memory");  // hard fence for the LDS loads of the next chunk
+        // chunk fence: the accumulators are consumed here and the next chunk's LDS loads cannot be
+        // hoisted above it, so at most 8 x 16 B of table rows are live at once
+        asm volatile("" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3)::"memory");
     }
     y0 = a0;
     y1 = a1;
@@ -480,8 +482,8 @@ __device__ __forceinline__ uint32_t quad_xor(uint32_t v) {
     return v;
 }
 
-template <bool kSeal, int kW, bool kFold>
-__global__ void __launch_bounds__(kW * 64) __attribute__((amdgpu_waves_per_eu(kW / 4, kW / 4)))
+template <bool kSeal, int kW, bool kFold, int kWpe = kW / 4>
+__global__ void __launch_bounds__(kW * 64) __attribute__((amdgpu_waves_per_eu(kWpe, kWpe)))
 gcm_quad_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
     constexpr uint32_t kT = kW * 64;
     const uint32_t lane = threadIdx.x & 63u;
@@ -701,20 +703,22 @@ struct Variant {
     const void *seal, *open;
     int waves;
     uint32_t lds;
-    bool quad;  // 16 packets per wave tile instead of 64
+    bool quad;       // 16 packets per wave tile instead of 64
+    int wgs_per_cu;  // resident workgroups per CU the persistent grid is sized for
 };
 
 template <int kW, bool kShared, int kIlp>
 Variant make_variant() {
     return Variant{reinterpret_cast<const void *>(&gcm_kernel<true, kW, kShared, kIlp>),
                    reinterpret_cast<const void *>(&gcm_kernel<false, kW, kShared, kIlp>), kW,
-                   lds_bytes<kW, kShared>(), false};
+                   lds_bytes<kW, kShared>(), false, 1};
 }
 
-template <int kW, bool kFold>
+template <int kW, bool kFold, int kWpe = kW / 4>
 Variant make_quad() {
-    return Variant{reinterpret_cast<const void *>(&gcm_quad_kernel<true, kW, kFold>),
-                   reinterpret_cast<const void *>(&gcm_quad_kernel<false, kW, kFold>), kW, kQuadLds, true};
+    return Variant{reinterpret_cast<const void *>(&gcm_quad_kernel<true, kW, kFold, kWpe>),
+                   reinterpret_cast<const void *>(&gcm_quad_kernel<false, kW, kFold, kWpe>), kW, kQuadLds, true,
+                   kWpe * 4 / kW};
 }
 
 static Variant g_variants[kNumVariants];
@@ -724,6 +728,9 @@ hipError_t init_kernels() {
     g_variants[1] = make_quad<16, false>();        // single key: 4 lanes per packet, 16 waves/CU
     g_variants[2] = make_quad<16, true>();         // same, partial block and J0 folded into the loop
     g_variants[3] = make_variant<8, true, 4>();    // single key, lane per packet, shared GHASH table
+    g_variants[4] = make_quad<12, false, 6>();     // quad, 12-wave workgroups, two per CU (24 waves/CU)
+    g_variants[5] = make_quad<16, false, 8>();     // quad, 16-wave workgroups, two per CU (32 waves/CU)
+    g_variants[6] = make_quad<8, false, 4>();      // quad, 8-wave workgroups, two per CU (16 waves/CU)
     for (const Variant &v : g_variants) {
         for (const void *k : {v.seal, v.open}) {
             hipFuncAttributes a;
@@ -740,6 +747,7 @@ hipError_t init_kernels() {
 
 int variant_waves(int v) { return g_variants[v].waves; }
 bool variant_quad(int v) { return g_variants[v].quad; }
+int variant_wgs_per_cu(int v) { return g_variants[v].wgs_per_cu; }
 
 hipError_t launch_packets(bool seal, int variant, const Batch &b, int grid, hipStream_t s) {
     if (variant < 0 || variant >= kNumVariants) return hipErrorInvalidValue;

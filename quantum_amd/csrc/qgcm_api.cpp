@@ -94,7 +94,8 @@ int grid_for(const qgcm_ctx *ctx, uint32_t n_items, int variant) {
     const uint32_t waves = (uint32_t)variant_waves(variant);
     const uint32_t tiles = variant_quad(variant) ? (n_items + 15) / 16 : n_items / 64;
     const uint32_t wgs = (tiles + waves - 1) / waves;
-    const uint32_t cap = (uint32_t)ctx->num_cus;  // persistent: one LDS-filling workgroup per CU
+    // persistent grid: the resident workgroups (each fills its own LDS tables once)
+    const uint32_t cap = (uint32_t)ctx->num_cus * (uint32_t)variant_wgs_per_cu(variant);
     return (int)(wgs < cap ? (wgs ? wgs : 1) : cap);
 }
 
