@@ -1,0 +1,120 @@
+"""Secondary BASELINE configs (bench.py measures the headline config 2):
+
+  config3  2^20 packets, lengths ~ U{64..9000}, 1024 per-peer keys derived as common/mapping.go:90-99
+           (X25519 twice + PBKDF2-HMAC-SHA512 x10000), key_idx ~ U[0,1024), AAD = the peer IP;
+           device-resident descriptor batches (qgcm_seal_batch / qgcm_open_batch).
+  e2e      config 2 from HOST memory: pinned staging + H2D + kernels + D2H (qgcm_seal_host /
+           qgcm_open_host), the PCIe-inclusive rate DESIGN.md reports (never bench.py's value).
+
+Prints one JSON line per config.  Usage: python tools/bench_configs.py [config3] [e2e]
+"""
+from __future__ import annotations
+
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from quantum_amd import _lib, batch  # noqa: E402
+from quantum_amd.crypto import Context, derive_key, derive_keys, x25519, x25519_base  # noqa: E402
+
+
+def config3(reps: int = 5) -> dict:
+    N, NK = 1 << 20, 1024
+    rng = np.random.default_rng(0x5EED0003)
+    # per-peer keys: secret = X25519(peer.pub, my.priv), salt = X25519(peer.pubsalt, my.privsalt)
+    t0 = time.perf_counter()
+    me_priv, me_salt = rng.bytes(32), rng.bytes(32)
+    secrets, salts = bytearray(), bytearray()
+    for _ in range(NK):
+        secrets += x25519(me_priv, x25519_base(rng.bytes(32)))
+        salts += x25519(me_salt, x25519_base(rng.bytes(32)))
+    keys = derive_keys(bytes(secrets), bytes(salts))
+    t_keys = time.perf_counter() - t0
+    ctx = Context(device=0, max_keys=NK)
+    t0 = time.perf_counter()
+    ctx.set_keys(0, keys)
+    t_set = time.perf_counter() - t0
+
+    lens = rng.integers(64, 9001, size=N, dtype=np.int64)
+    kidx = rng.integers(0, NK, size=N, dtype=np.int64)
+    slot = (4 + lens + 28 + 3) & ~3
+    offs = np.zeros(N, dtype=np.int64)
+    offs[1:] = np.cumsum(slot)[:-1]
+    total = int(offs[-1] + slot[-1])
+    arena = torch.randint(0, 256, (total + 64,), dtype=torch.uint8, device="cuda")
+    nonces = torch.randint(0, 256, (12 * N,), dtype=torch.uint8, device="cuda")
+    status = torch.zeros(N, dtype=torch.uint8, device="cuda")
+    d_seal = batch.make_descs(offs, lens, kidx, "cuda")
+    d_open = batch.make_descs(offs, lens + 28, kidx, "cuda")
+    for _ in range(2):
+        batch.seal_batch(ctx, arena, d_seal, N, nonces, status=status)
+        batch.open_batch(ctx, arena, d_open, N, status=status)
+    torch.cuda.synchronize()
+    ok = int(status.sum()) == N
+    ts, to = [], []
+    for _ in range(reps):
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        e[0].record()
+        batch.seal_batch(ctx, arena, d_seal, N, nonces, status=status)
+        e[1].record()
+        batch.open_batch(ctx, arena, d_open, N, status=status)
+        e[2].record()
+        torch.cuda.synchronize()
+        ts.append(e[0].elapsed_time(e[1]))
+        to.append(e[1].elapsed_time(e[2]))
+    ok = ok and int(status.sum()) == N
+    seal_ms, open_ms = float(np.median(ts)), float(np.median(to))
+    payload = int(lens.sum())
+    ctx.close()
+    return {"config": "config3", "packets": N, "keys": NK, "payload_bytes": payload,
+            "value": round(2 * payload / ((seal_ms + open_ms) * 1e-3) / 2**30, 2), "unit": "GiB/s",
+            "seal_ms": round(seal_ms, 3), "open_ms": round(open_ms, 3), "status_ok": ok,
+            "key_setup_s": {"x25519_pbkdf2_host": round(t_keys, 3), "device_expand": round(t_set, 4)}}
+
+
+def e2e(reps: int = 3) -> dict:
+    N, L = 1 << 20, 1350
+    stride = batch.slot_stride(L, align=64)
+    ctx = Context(device=0, max_keys=4)
+    key = derive_key(b"AES256Key-32Characters1234567890", bytes(range(32)))
+    ctx.set_key(0, key)
+    host = bytearray(N * stride)
+    dev = torch.zeros(N * stride, dtype=torch.uint8, device="cuda")
+    non_d = torch.zeros(12 * N, dtype=torch.uint8, device="cuda")
+    batch.fill_uniform(dev, stride, N, L, 0x0100630a, 0x5EED0001, non_d, 0x5EED0002)
+    host[:] = dev.cpu().numpy().tobytes()
+    nonces = bytearray(non_d.cpu().numpy().tobytes())
+    a_ptr, ka = batch.host_ptr(host)
+    n_ptr, kn = batch.host_ptr(nonces)
+    L_ = _lib.lib()
+    rc = L_.qgcm_seal_host(ctx.handle, a_ptr, stride, N, L, 0, n_ptr, 4, None)
+    rc |= L_.qgcm_open_host(ctx.handle, a_ptr, stride, N, L + 28, 0, 4, None)
+    ts, to = [], []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        rc |= L_.qgcm_seal_host(ctx.handle, a_ptr, stride, N, L, 0, n_ptr, 4, None)
+        t1 = time.perf_counter()
+        rc |= L_.qgcm_open_host(ctx.handle, a_ptr, stride, N, L + 28, 0, 4, None)
+        t2 = time.perf_counter()
+        ts.append(t1 - t0)
+        to.append(t2 - t1)
+    del ka, kn
+    s, o = float(np.median(ts)), float(np.median(to))
+    ctx.close()
+    return {"config": "e2e_config2_host_memory", "packets": N, "payload_len": L, "stride": stride,
+            "value": round(2 * N * L / (s + o) / 2**30, 2), "unit": "GiB/s", "seal_s": round(s, 4),
+            "open_s": round(o, 4), "bytes_each_way_per_call": N * stride, "status_ok": rc == 0}
+
+
+if __name__ == "__main__":
+    which = sys.argv[1:] or ["config3", "e2e"]
+    for w in which:
+        print(json.dumps({"config3": config3, "e2e": e2e}[w]()), flush=True)
