@@ -23,7 +23,7 @@ import torch
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from quantum_amd import batch  # noqa: E402
+from quantum_amd import batch, shard  # noqa: E402
 from quantum_amd.crypto import Context, derive_key  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, MI355X_MICROARCH.md "Chip-level parameters"
@@ -117,13 +117,8 @@ def main() -> None:
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        okt = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
-        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
-        ok = bool(okt.item())
+    # max over ranks, AND of the per-rank status (the only cross-rank traffic; no data collective)
+    elapsed, ok = shard.reduce_step_time(elapsed, ok, dist, dev)
 
     seal_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
     open_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
