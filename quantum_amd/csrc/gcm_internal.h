@@ -33,15 +33,23 @@ struct Batch {
     uint32_t n_items;           // multiple of 64
     uint32_t aad_len;           // 0 or 4
     uint32_t max_keys;
+    uint32_t *tile_counter;     // descriptor quad kernels: dynamic tile index (zeroed per launch)
 };
 
-constexpr int kNumVariants = 7;
-constexpr int kVariantGeneral = 0;   // per-wave GHASH tables, any key mix
+constexpr int kNumVariants = 9;
+constexpr int kVariantGeneral = 0;   // lane per packet, per-wave GHASH tables, any key mix
+constexpr int kVariantDescQuad = 7;  // default for descriptor batches: sorted quad tiles
 constexpr int kVariantUniform = 5;   // default for single-key (uniform) batches: quad kernel, 32 waves/CU
 hipError_t init_kernels();
 int variant_waves(int variant);
 bool variant_quad(int variant);
 int variant_wgs_per_cu(int variant);
+bool variant_desc(int variant);
+// sorted, 16-packet key-uniform worklist for the descriptor quad kernels (worklist.hip)
+size_t quad_worklist_bytes(uint32_t n, uint32_t max_keys, uint32_t *n_items_out);
+hipError_t launch_quad_worklist(const qgcm_desc *descs, uint32_t n, uint32_t max_keys, bool seal, void *ws,
+                                size_t ws_bytes, uint32_t **worklist_out, uint32_t **counter_out,
+                                uint32_t *n_items_out, hipStream_t s);
 hipError_t launch_packets(bool seal, int variant, const Batch &b, int grid, hipStream_t s);
 hipError_t launch_key_setup(const uint8_t *d_keys, uint32_t first, uint32_t count, uint32_t *rk_table,
                             uint4 *gh_table, const uint8_t *d_sbox, hipStream_t s);

@@ -189,6 +189,36 @@ __device__ __forceinline__ void ghash_mul(uint32_t &y0, uint32_t &y1, uint32_t &
     y3 = a3;
 }
 
+// Y <- Y * H with the comb table read from global memory (L2/L1-resident, wave-uniform table):
+// used for the few per-packet multiplies by H in the descriptor quad kernel, whose LDS holds only
+// each wave's H^4 table.
+__device__ __forceinline__ void ghash_mul_global(uint32_t &y0, uint32_t &y1, uint32_t &y2, uint32_t &y3,
+                                                 const uint4 *__restrict__ T) {
+    uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+    const uint32_t yw[4] = {y0, y1, y2, y3};
+    const char *base = reinterpret_cast<const char *>(T);
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int j = 4 * w + k;
+            const uint32_t oh = (yw[w] >> (8 * k)) & 0xf0u;
+            const uint32_t ol = ((yw[w] >> (8 * k)) & 0x0fu) << 4;
+            const uint4 th = *reinterpret_cast<const uint4 *>(base + (2 * j) * 256 + oh);
+            const uint4 tl = *reinterpret_cast<const uint4 *>(base + (2 * j + 1) * 256 + ol);
+            a0 = xor3(a0, th.x, tl.x);
+            a1 = xor3(a1, th.y, tl.y);
+            a2 = xor3(a2, th.z, tl.z);
+            a3 = xor3(a3, th.w, tl.w);
+        }
+        asm volatile("" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3)::"memory");
+    }
+    y0 = a0;
+    y1 = a1;
+    y2 = a2;
+    y3 = a3;
+}
+
 __device__ __forceinline__ uint32_t sel4(uint32_t q, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
     return q == 0 ? a : (q == 1 ? b : (q == 2 ? c : d));
 }
@@ -482,7 +512,7 @@ __device__ __forceinline__ uint32_t quad_xor(uint32_t v) {
     return v;
 }
 
-template <bool kSeal, int kW, bool kFold, int kWpe = kW / 4>
+template <bool kSeal, int kW, bool kFold, int kWpe = kW / 4, bool kDesc = false>
 __global__ void __launch_bounds__(kW * 64) __attribute__((amdgpu_waves_per_eu(kWpe, kWpe)))
 gcm_quad_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
     constexpr uint32_t kT = kW * 64;
@@ -495,33 +525,85 @@ gcm_quad_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
         const uint32_t x = i >> 6, slot = i & 63u;
         lds_st32(4 * i, b.te[(slot >> 5) * 256u + x]);
     }
-    {
+    if constexpr (!kDesc) {
         const uint4 *src = b.gh_table + (size_t)b.uniform_key * kGhEntries;  // H then H^4
         for (uint32_t e = threadIdx.x; e < kGhEntries; e += kT) lds_st128(kTeBytes + e * 16, src[e]);
     }
     __syncthreads();
 
     const uint32_t lb = (lane & 31u) << 2;
-    constexpr uint32_t gH = kTeBytes, gH4 = kTeBytes + kGhBytes;
-    const Keys kk = {rk_table + (size_t)b.uniform_key * kRkWords, rk_table + (size_t)b.uniform_key * kRkWords + 64};
-    const uint32_t ntiles = (b.n + 15) >> 4;
+    // single key: H and H^4 tables shared by the workgroup; descriptors: one H^4 table per wave in
+    // LDS (reloaded when the wave's key changes), H read from the L2-resident key table
+    const uint32_t gH = kTeBytes;
+    const uint32_t gH4 = kDesc ? kTeBytes + wave * kGhBytes : kTeBytes + kGhBytes;
+    uint32_t cur_key = kDesc ? 0xffffffffu : b.uniform_key;
+    const uint32_t ntiles = kDesc ? (b.n_items >> 4) : ((b.n + 15) >> 4);
 
-    for (uint32_t tile = blockIdx.x * kW + wave; tile < ntiles; tile += gridDim.x * kW) {
-        const uint32_t pkt = tile * 16u + qd;
-        uint32_t L = b.uniform_len;
-        // Opaque per tile: stops LICM from hoisting dozens of L-derived values (masks, selectors)
-        // out of the tile loop, which would hold them in registers for the whole kernel.
-        asm volatile("" : "+s"(L));
-        bool valid = pkt < b.n;
-        if (!kSeal) {
-            if (L < (uint32_t)QGCM_OVERHEAD) valid = false;
-            L -= QGCM_OVERHEAD;
+    uint32_t tile = blockIdx.x * kW + wave;
+    if constexpr (kDesc) {  // dynamic tiles: lengths vary by 100x between tiles
+        uint32_t t = 0;
+        if (lane == 0) t = atomicAdd(b.tile_counter, 1u);
+        tile = __builtin_amdgcn_readfirstlane(__shfl(t, 0));
+    }
+    for (; tile < ntiles;) {
+        uint32_t pkt, L;
+        bool valid;
+        uint64_t off;
+        uint32_t wkey = cur_key;
+        if constexpr (kDesc) {
+            pkt = b.worklist[tile * 16u + qd];
+            valid = pkt != 0xffffffffu;
+            qgcm_desc dsc = {0, 0, 0};
+            if (valid) dsc = b.descs[pkt];
+            off = dsc.offset;
+            L = kSeal ? dsc.len : dsc.len - QGCM_OVERHEAD;  // open descriptors with len < 28 never get here
+            const uint64_t vmask = __ballot(valid);
+            if (vmask != 0) {
+                wkey = __builtin_amdgcn_readfirstlane(__shfl(dsc.key_idx, __ffsll((unsigned long long)vmask) - 1));
+                if (wkey != cur_key) {
+                    const uint4 *src = b.gh_table + (size_t)wkey * kGhEntries + 512;  // H^4
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) {
+                        const uint32_t e = r * 64 + lane;
+                        lds_st128(gH4 + e * 16, src[e]);
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    cur_key = wkey;
+                }
+            }
+            // next tile (wave-uniform), fetched before this one's work
+            uint32_t t = 0;
+            if (lane == 0) t = atomicAdd(b.tile_counter, 1u);
+            const uint32_t next = __builtin_amdgcn_readfirstlane(__shfl(t, 0));
+            asm volatile("" : "+v"(L));
+            if (!valid) {
+                tile = next;
+                continue;
+            }
+            tile = next;
+        } else {
+            pkt = tile * 16u + qd;
+            L = b.uniform_len;
+            // Opaque per tile: stops LICM from hoisting dozens of L-derived values (masks, selectors)
+            // out of the tile loop, which would hold them in registers for the whole kernel.
+            asm volatile("" : "+s"(L));
+            valid = pkt < b.n;
+            if (!kSeal) {
+                if (L < (uint32_t)QGCM_OVERHEAD) valid = false;
+                L -= QGCM_OVERHEAD;
+            }
+            off = (uint64_t)pkt * b.stride;
+            tile += gridDim.x * kW;
+            if (!valid) {
+                if (!kSeal && b.status && pkt < b.n && m == 0) b.status[pkt] = 0;
+                continue;  // the whole quad leaves together
+            }
         }
-        if (!valid) {
-            if (!kSeal && b.status && pkt < b.n && m == 0) b.status[pkt] = 0;
-            continue;  // the whole quad leaves together
-        }
-        uint8_t *raw = b.arena + (uint64_t)pkt * b.stride;
+        const Keys kk = {rk_table + (size_t)wkey * kRkWords, rk_table + (size_t)wkey * kRkWords + 64};
+        const uint4 *Hg = b.gh_table + (size_t)wkey * kGhEntries;  // comb table of H (global)
+        uint8_t *raw = b.arena + off;
         uint8_t *data = raw + 4;  // common.PacketStart
 
         uint32_t g0 = 0, g1 = 0, g2 = 0, g3 = 0, n0, n1, n2;
@@ -659,7 +741,12 @@ gcm_quad_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
         }
         }
         // Z_m * H^(e_m - 1), e_m = d + 1 - b_last(m)
-        for (int t = (int)d - blast; t > 0; --t) ghash_mul(z0, z1, z2, z3, gH);
+        for (int t = (int)d - blast; t > 0; --t) {
+            if constexpr (kDesc)
+                ghash_mul_global(z0, z1, z2, z3, Hg);
+            else
+                ghash_mul(z0, z1, z2, z3, gH);
+        }
         z0 = quad_xor(z0);
         z1 = quad_xor(z1);
         z2 = quad_xor(z2);
@@ -670,7 +757,10 @@ gcm_quad_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
         e3 = quad_xor(e3);
         z1 ^= bswap(b.aad_len * 8u);  // [len(A)]_64 || [len(C)]_64, big endian
         z3 ^= bswap(L * 8u);
-        ghash_mul(z0, z1, z2, z3, gH);
+        if constexpr (kDesc)
+            ghash_mul_global(z0, z1, z2, z3, Hg);
+        else
+            ghash_mul(z0, z1, z2, z3, gH);
         const uint32_t t0 = z0 ^ e0, t1 = z1 ^ e1, t2 = z2 ^ e2, t3 = z3 ^ e3;
         // the lane owning the partial block (or lane 0) writes the tail
         const uint32_t owner = r ? (nfull & 3u) : 0u;
@@ -705,20 +795,29 @@ struct Variant {
     uint32_t lds;
     bool quad;       // 16 packets per wave tile instead of 64
     int wgs_per_cu;  // resident workgroups per CU the persistent grid is sized for
+    bool desc;       // consumes the sorted 16-packet worklist (launch_quad_worklist)
 };
 
 template <int kW, bool kShared, int kIlp>
 Variant make_variant() {
     return Variant{reinterpret_cast<const void *>(&gcm_kernel<true, kW, kShared, kIlp>),
                    reinterpret_cast<const void *>(&gcm_kernel<false, kW, kShared, kIlp>), kW,
-                   lds_bytes<kW, kShared>(), false, 1};
+                   lds_bytes<kW, kShared>(), false, 1, false};
 }
 
 template <int kW, bool kFold, int kWpe = kW / 4>
 Variant make_quad() {
     return Variant{reinterpret_cast<const void *>(&gcm_quad_kernel<true, kW, kFold, kWpe>),
                    reinterpret_cast<const void *>(&gcm_quad_kernel<false, kW, kFold, kWpe>), kW, kQuadLds, true,
-                   kWpe * 4 / kW};
+                   kWpe * 4 / kW, false};
+}
+
+// descriptor batches: per-wave H^4 table, so LDS = Te + one 8 KiB table per wave
+template <int kW, int kWpe>
+Variant make_quad_desc() {
+    return Variant{reinterpret_cast<const void *>(&gcm_quad_kernel<true, kW, false, kWpe, true>),
+                   reinterpret_cast<const void *>(&gcm_quad_kernel<false, kW, false, kWpe, true>), kW,
+                   kTeBytes + (uint32_t)kW * kGhBytes, true, 1, true};
 }
 
 static Variant g_variants[kNumVariants];
@@ -731,6 +830,8 @@ hipError_t init_kernels() {
     g_variants[4] = make_quad<12, false, 6>();     // quad, 12-wave workgroups, two per CU (24 waves/CU)
     g_variants[5] = make_quad<16, false, 8>();     // quad, 16-wave workgroups, two per CU (32 waves/CU)
     g_variants[6] = make_quad<8, false, 4>();      // quad, 8-wave workgroups, two per CU (16 waves/CU)
+    g_variants[7] = make_quad_desc<12, 3>();       // descriptors: quad, 12 waves/CU, per-wave H^4 tables
+    g_variants[8] = make_quad_desc<8, 2>();        // descriptors: quad, 8 waves/CU
     for (const Variant &v : g_variants) {
         for (const void *k : {v.seal, v.open}) {
             hipFuncAttributes a;
@@ -748,6 +849,7 @@ hipError_t init_kernels() {
 int variant_waves(int v) { return g_variants[v].waves; }
 bool variant_quad(int v) { return g_variants[v].quad; }
 int variant_wgs_per_cu(int v) { return g_variants[v].wgs_per_cu; }
+bool variant_desc(int v) { return g_variants[v].desc; }
 
 hipError_t launch_packets(bool seal, int variant, const Batch &b, int grid, hipStream_t s) {
     if (variant < 0 || variant >= kNumVariants) return hipErrorInvalidValue;

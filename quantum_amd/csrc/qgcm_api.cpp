@@ -23,6 +23,7 @@ struct qgcm_ctx {
     int num_cus = 0;
     uint32_t max_keys = 0;
     int uniform_variant = kVariantUniform;  // kernel variant for single-key batches (QGCM_VARIANT)
+    int desc_variant = kVariantDescQuad;    // kernel variant for descriptor batches (QGCM_DESC_VARIANT)
     uint32_t *d_rk = nullptr;
     uint4 *d_gh = nullptr;
     uint32_t *d_te = nullptr;
@@ -34,6 +35,8 @@ struct qgcm_ctx {
     std::mutex ws_mu;
     uint32_t *d_counts = nullptr, *d_cursors = nullptr, *d_worklist = nullptr;
     size_t wl_cap = 0;
+    void *d_qws = nullptr;  // sorted quad worklist workspace
+    size_t qws_cap = 0;
 
     // per-packet and host-batch staging, guarded by io_mu
     std::mutex io_mu;
@@ -143,40 +146,50 @@ int run_descs(qgcm_ctx *ctx, bool seal, uint8_t *arena, const qgcm_desc *descs, 
     if (n == 0) return QGCM_OK;
     if (hipSetDevice(ctx->device) != hipSuccess) return QGCM_E_HIP;
     if (status && hipMemsetAsync(status, 0, n, s) != hipSuccess) return QGCM_E_HIP;
-    const uint64_t cap = (uint64_t)n + 64ull * (n < ctx->max_keys ? n : ctx->max_keys);
+    // The workspace is reused by the next call on any stream: serialize descriptor batches per ctx.
     std::lock_guard<std::mutex> g(ctx->ws_mu);
-    if (cap > ctx->wl_cap) {
-        if (ctx->d_worklist) hipFree(ctx->d_worklist);
-        ctx->d_worklist = nullptr;
-        if (hipMalloc(&ctx->d_worklist, cap * sizeof(uint32_t)) != hipSuccess) {
-            ctx->wl_cap = 0;
-            return QGCM_E_NOMEM;
+    Batch b = base_batch(ctx);
+    b.arena = arena;
+    b.descs = descs;
+    b.nonces = seal ? nonces : nullptr;
+    b.status = status;
+    b.n = n;
+    b.aad_len = aad_len;
+    const int v = ctx->desc_variant;
+    if (variant_desc(v)) {
+        uint32_t items = 0;
+        const size_t need = quad_worklist_bytes(n, ctx->max_keys, &items);
+        if (need > ctx->qws_cap) {
+            if (ctx->d_qws) hipFree(ctx->d_qws);
+            ctx->d_qws = nullptr;
+            ctx->qws_cap = 0;
+            if (hipMalloc(&ctx->d_qws, need) != hipSuccess) return QGCM_E_NOMEM;
+            ctx->qws_cap = need;
         }
-        ctx->wl_cap = cap;
+        uint32_t *wl = nullptr, *counter = nullptr;
+        if (launch_quad_worklist(descs, n, ctx->max_keys, seal, ctx->d_qws, ctx->qws_cap, &wl, &counter, &items, s) !=
+            hipSuccess)
+            return QGCM_E_HIP;
+        b.worklist = wl;
+        b.tile_counter = counter;
+        b.n_items = items;
+        return hip_fail(launch_packets(seal, v, b, grid_for(ctx, b.n_items, v), s));
     }
+    const uint64_t cap = (uint64_t)n + 64ull * (n < ctx->max_keys ? n : ctx->max_keys);
     const uint32_t items = (uint32_t)((cap + 63) & ~63ull);
     if (items > ctx->wl_cap) {
-        hipFree(ctx->d_worklist);
-        if (hipMalloc(&ctx->d_worklist, (size_t)items * sizeof(uint32_t)) != hipSuccess) {
-            ctx->d_worklist = nullptr;
-            ctx->wl_cap = 0;
-            return QGCM_E_NOMEM;
-        }
+        if (ctx->d_worklist) hipFree(ctx->d_worklist);
+        ctx->d_worklist = nullptr;
+        ctx->wl_cap = 0;
+        if (hipMalloc(&ctx->d_worklist, (size_t)items * sizeof(uint32_t)) != hipSuccess) return QGCM_E_NOMEM;
         ctx->wl_cap = items;
     }
     hipError_t e = launch_build_worklist(descs, n, ctx->max_keys, ctx->d_counts, ctx->d_cursors, ctx->d_worklist,
                                          items, s);
     if (e != hipSuccess) return QGCM_E_HIP;
-    Batch b = base_batch(ctx);
-    b.arena = arena;
-    b.descs = descs;
     b.worklist = ctx->d_worklist;
-    b.nonces = seal ? nonces : nullptr;
-    b.status = status;
-    b.n = n;
     b.n_items = items;
-    b.aad_len = aad_len;
-    return hip_fail(launch_packets(seal, kVariantGeneral, b, grid_for(ctx, b.n_items, kVariantGeneral), s));
+    return hip_fail(launch_packets(seal, v, b, grid_for(ctx, b.n_items, v), s));
 }
 
 int ensure_io(qgcm_ctx *ctx, size_t bytes) {
@@ -244,9 +257,13 @@ qgcm_ctx *qgcm_create(int device, uint32_t max_keys, char *err, int errlen) {
     ctx->num_cus = prop.multiProcessorCount;
     ctx->max_keys = max_keys;
     ctx->key_set.assign(max_keys, 0);
-    if (const char *v = getenv("QGCM_VARIANT")) {
+    if (const char *v = getenv("QGCM_VARIANT")) {  // kernel variant overrides (tuning and tests)
         const int iv = atoi(v);
         if (iv >= 0 && iv < kNumVariants) ctx->uniform_variant = iv;
+    }
+    if (const char *v = getenv("QGCM_DESC_VARIANT")) {
+        const int iv = atoi(v);
+        if (iv == kVariantGeneral || (iv >= 0 && iv < kNumVariants && variant_desc(iv))) ctx->desc_variant = iv;
     }
     uint8_t sbox[256];
     uint32_t te[512];
@@ -279,6 +296,7 @@ void qgcm_destroy(qgcm_ctx *ctx) {
     hipFree(ctx->d_counts);
     hipFree(ctx->d_cursors);
     hipFree(ctx->d_worklist);
+    hipFree(ctx->d_qws);
     hipFree(ctx->d_io);
     if (ctx->h_pin) hipHostFree(ctx->h_pin);
     if (ctx->io_stream) hipStreamDestroy(ctx->io_stream);

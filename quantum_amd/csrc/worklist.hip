@@ -1,0 +1,126 @@
+// worklist.hip -- descriptor batches -> key-uniform 16-packet tiles for the quad kernel.
+//
+// A batch of qgcm_desc (any key mix, any lengths; BASELINE config 3) is ordered by
+// (key_idx, length descending) with a device radix sort, then each key's run is padded to a multiple
+// of 16 entries so that every 16-packet wave tile uses ONE key (round keys in SGPRs, one GHASH table
+// per wave) and holds packets of similar length (the 4-lane quads of a wave finish together).
+// Packets that cannot be processed (key index out of range, open with len < 28) are left out: their
+// status stays 0 and their slot is untouched.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+#include <stdint.h>
+
+#include "gcm_internal.h"
+
+namespace qgcm {
+
+constexpr uint32_t kLenBits = 12;  // length rank bits of the sort key; key index in the top 20 bits
+
+__global__ void qwl_keys_kernel(const qgcm_desc *descs, uint32_t n, uint32_t max_keys, bool seal, uint32_t *sort_keys,
+                                uint32_t *vals, uint32_t *counts) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const qgcm_desc d = descs[i];
+    uint32_t sk = 0xffffffffu;
+    const bool ok = d.key_idx < max_keys && (seal || d.len >= (uint32_t)QGCM_OVERHEAD);
+    if (ok) {
+        const uint32_t L = seal ? d.len : d.len - QGCM_OVERHEAD;
+        const uint32_t nb = min((L + 15u) >> 4, (1u << kLenBits) - 1u);
+        sk = (d.key_idx << kLenBits) | ((1u << kLenBits) - 1u - nb);  // longest first within a key
+        atomicAdd(&counts[d.key_idx], 1u);
+    }
+    sort_keys[i] = sk;
+    vals[i] = i;
+}
+
+// Single workgroup: counts -> start (unpadded, sorted order) and pstart (padded to 16, worklist).
+__global__ void __launch_bounds__(1024) qwl_scan_kernel(const uint32_t *counts, uint32_t max_keys, uint32_t *start,
+                                                        uint32_t *pstart) {
+    __shared__ uint32_t pu[1024], pp[1024];
+    const uint32_t t = threadIdx.x;
+    const uint32_t per = (max_keys + 1023) / 1024;
+    const uint32_t lo = t * per, hi = min(lo + per, max_keys);
+    uint32_t su = 0, sp = 0;
+    for (uint32_t k = lo; k < hi; ++k) {
+        su += counts[k];
+        sp += (counts[k] + 15u) & ~15u;
+    }
+    pu[t] = su;
+    pp[t] = sp;
+    __syncthreads();
+    for (uint32_t d = 1; d < 1024; d <<= 1) {
+        const uint32_t a = t >= d ? pu[t - d] : 0, b = t >= d ? pp[t - d] : 0;
+        __syncthreads();
+        pu[t] += a;
+        pp[t] += b;
+        __syncthreads();
+    }
+    uint32_t ru = pu[t] - su, rp = pp[t] - sp;
+    for (uint32_t k = lo; k < hi; ++k) {
+        start[k] = ru;
+        pstart[k] = rp;
+        ru += counts[k];
+        rp += (counts[k] + 15u) & ~15u;
+    }
+}
+
+__global__ void qwl_scatter_kernel(const uint32_t *sorted_keys, const uint32_t *sorted_vals, uint32_t n,
+                                   const uint32_t *start, const uint32_t *pstart, uint32_t *worklist) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    const uint32_t sk = sorted_keys[j];
+    if (sk == 0xffffffffu) return;
+    const uint32_t k = sk >> kLenBits;
+    worklist[pstart[k] + (j - start[k])] = sorted_vals[j];
+}
+
+size_t quad_worklist_bytes(uint32_t n, uint32_t max_keys, uint32_t *n_items_out) {
+    const uint64_t cap = (uint64_t)n + 16ull * (n < max_keys ? n : max_keys);
+    const uint32_t items = (uint32_t)((cap + 15) & ~15ull);
+    size_t cub = 0;
+    hipcub::DeviceRadixSort::SortPairs(nullptr, cub, (uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                       (uint32_t *)nullptr, (int)n);
+    if (n_items_out) *n_items_out = items;
+    // keys in/out, vals in/out, counts, start, pstart, worklist, tile counter, cub temp (16-B aligned pieces)
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    return 4 * al(4ull * n) + 3 * al(4ull * max_keys) + al(4ull * items) + al(16) + al(cub);
+}
+
+hipError_t launch_quad_worklist(const qgcm_desc *descs, uint32_t n, uint32_t max_keys, bool seal, void *ws,
+                                size_t ws_bytes, uint32_t **worklist_out, uint32_t **counter_out,
+                                uint32_t *n_items_out, hipStream_t s) {
+    uint32_t items = 0;
+    const size_t need = quad_worklist_bytes(n, max_keys, &items);
+    if (ws_bytes < need) return hipErrorInvalidValue;
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    char *p = static_cast<char *>(ws);
+    uint32_t *k_in = (uint32_t *)p;  p += al(4ull * n);
+    uint32_t *k_out = (uint32_t *)p; p += al(4ull * n);
+    uint32_t *v_in = (uint32_t *)p;  p += al(4ull * n);
+    uint32_t *v_out = (uint32_t *)p; p += al(4ull * n);
+    uint32_t *counts = (uint32_t *)p; p += al(4ull * max_keys);
+    uint32_t *start = (uint32_t *)p;  p += al(4ull * max_keys);
+    uint32_t *pstart = (uint32_t *)p; p += al(4ull * max_keys);
+    uint32_t *worklist = (uint32_t *)p; p += al(4ull * items);
+    uint32_t *counter = (uint32_t *)p;  p += al(16);
+    void *cub_tmp = p;
+    size_t cub_bytes = need - (size_t)(p - static_cast<char *>(ws));
+    hipError_t e;
+    if ((e = hipMemsetAsync(counts, 0, 4ull * max_keys, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(worklist, 0xff, 4ull * items, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(counter, 0, 16, s)) != hipSuccess) return e;
+    const int bs = 256, g = (int)((n + bs - 1) / bs);
+    if (n) hipLaunchKernelGGL(qwl_keys_kernel, dim3(g), dim3(bs), 0, s, descs, n, max_keys, seal, k_in, v_in, counts);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = hipcub::DeviceRadixSort::SortPairs(cub_tmp, cub_bytes, k_in, k_out, v_in, v_out, (int)n, 0, 32, s)) !=
+        hipSuccess)
+        return e;
+    hipLaunchKernelGGL(qwl_scan_kernel, dim3(1), dim3(1024), 0, s, counts, max_keys, start, pstart);
+    if (n) hipLaunchKernelGGL(qwl_scatter_kernel, dim3(g), dim3(bs), 0, s, k_out, v_out, n, start, pstart, worklist);
+    *worklist_out = worklist;
+    *counter_out = counter;
+    *n_items_out = items;
+    return hipGetLastError();
+}
+
+}  // namespace qgcm
