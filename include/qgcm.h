@@ -43,6 +43,7 @@ extern "C" {
 #define QGCM_TAG_BYTES 16    /* cipher.NewGCM standard tag (aead.Overhead()) */
 #define QGCM_OVERHEAD 28     /* EncryptedSize - len = Overhead + NonceSize, crypto/aes.go:29-36 */
 #define QGCM_PBKDF2_ITERS 10000 /* crypto/aes.go:18 */
+#define QGCM_MAX_PAYLOAD (1u << 28) /* largest plaintext per packet (GCM allows 2^36-32; packets are <= 9000) */
 #define QGCM_ERRLEN 120      /* crypto/dtls.go:23 errorLen */
 
 /* status codes */
@@ -115,13 +116,21 @@ long qgcm_seal_one(qgcm_ctx *ctx, uint32_t key_idx, uint8_t *data, long length, 
 long qgcm_open_one(qgcm_ctx *ctx, uint32_t key_idx, uint8_t *data, long len, const uint8_t *aad,
                    uint32_t aad_len);
 
-/* ---- host batches through pinned staging (end-to-end incl. PCIe) ---- */
-/* Slots in host memory at i*stride; copies in, runs the device batch, copies back.  Returns
- * the number of packets that failed (0 = all ok) or a negative error.  status may be NULL. */
+/* ---- host batches (end-to-end incl. PCIe) ---- */
+/* Slots in host memory at i*stride; copies in, runs the device batch, copies back, synchronously.
+ * Pipelined in ~32 MiB chunks over 3 streams (H2D of chunk c+1 || kernel c || D2H of chunk c-1);
+ * h_arena from qgcm_host_alloc (pinned) is DMA'd in place, pageable memory is staged by HIP.
+ * Returns the number of packets that failed (0 = all ok) or a negative error.  status may be NULL.
+ * Replaces the per-packet Apply loop of worker/outgoing.go:55-93 / worker/incoming.go:54-92 for a
+ * coalesced batch. */
 int qgcm_seal_host(qgcm_ctx *ctx, uint8_t *h_arena, uint64_t stride, uint32_t n, uint32_t len,
                    uint32_t key_idx, const uint8_t *h_nonces, uint32_t aad_len, uint8_t *h_status);
 int qgcm_open_host(qgcm_ctx *ctx, uint8_t *h_arena, uint64_t stride, uint32_t n, uint32_t len,
                    uint32_t key_idx, uint32_t aad_len, uint8_t *h_status);
+
+/* Pinned (page-locked) host memory for arenas handed to the *_host calls; NULL on failure. */
+void *qgcm_host_alloc(size_t bytes);
+void qgcm_host_free(void *p);
 
 /* ---- nonce source for production seals (crypto/aes.go:42-47 draws per packet) ---- */
 /* Fills n*12 bytes of host memory from getrandom(2). */

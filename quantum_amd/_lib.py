@@ -19,7 +19,7 @@ EXPORTS = (
     "qgcm_x25519_base", "qgcm_x25519",
     "qgcm_seal_batch", "qgcm_open_batch", "qgcm_seal_uniform", "qgcm_open_uniform",
     "qgcm_seal_one", "qgcm_open_one", "qgcm_seal_host", "qgcm_open_host",
-    "qgcm_random_nonces", "qgcm_fill_uniform",
+    "qgcm_random_nonces", "qgcm_fill_uniform", "qgcm_host_alloc", "qgcm_host_free",
 )
 
 QGCM_OK = 0
@@ -71,6 +71,10 @@ def _bind(L: C.CDLL) -> None:
     L.qgcm_seal_host.argtypes = [vp, vp, u64, u32, u32, u32, vp, u32, vp]
     L.qgcm_open_host.argtypes = [vp, vp, u64, u32, u32, u32, u32, vp]
     L.qgcm_random_nonces.argtypes = [vp, u32]
+    L.qgcm_host_alloc.argtypes = [C.c_size_t]
+    L.qgcm_host_alloc.restype = vp
+    L.qgcm_host_free.argtypes = [vp]
+    L.qgcm_host_free.restype = None
     L.qgcm_fill_uniform.argtypes = [vp, u64, u32, u32, u32, u64, vp, u64, vp]
 
 

@@ -15,7 +15,10 @@ constexpr uint32_t kGhBytes = 8192;
 // Device key slot: 60 round-key words (+4 pad), their rot16 copies, and the 4-bit comb tables of
 // H and H^4 (2 x 512 x 16 B).
 constexpr uint32_t kRkWords = 128;  // [0,64): rk words, [64,128): rot16(rk)
-constexpr uint32_t kGhEntries = 1024;  // [0,512): comb of H, [512,1024): comb of H^4
+// Per key: five 4-bit comb tables of 512 x 16 B: H, H^4 (the Horner step of the quad kernel), then
+// H^2, H^3, H^5 (the once-per-packet recombination multiplies, read from global memory).
+constexpr uint32_t kGhEntries = 2560;
+constexpr uint32_t kGhH = 0, kGhH4 = 512, kGhH2 = 1024, kGhH3 = 1536, kGhH5 = 2048;
 
 struct Batch {
     uint8_t *arena;
@@ -36,7 +39,7 @@ struct Batch {
     uint32_t *tile_counter;     // descriptor quad kernels: dynamic tile index (zeroed per launch)
 };
 
-constexpr int kNumVariants = 9;
+constexpr int kNumVariants = 11;
 constexpr int kVariantGeneral = 0;   // lane per packet, per-wave GHASH tables, any key mix
 constexpr int kVariantDescQuad = 7;  // default for descriptor batches: sorted quad tiles
 constexpr int kVariantUniform = 5;   // default for single-key (uniform) batches: quad kernel, 32 waves/CU

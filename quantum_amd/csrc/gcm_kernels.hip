@@ -219,6 +219,30 @@ __device__ __forceinline__ void ghash_mul_global(uint32_t &y0, uint32_t &y1, uin
     y3 = a3;
 }
 
+// [len(A)]_64 || [len(C)]_64 times H from the global comb table of H: only the table rows of the
+// nonzero bytes are read (word 1 holds len(A) <= 32 bits in its top byte, word 3 holds len(C)).
+__device__ __forceinline__ void ghash_lenblock_global(uint32_t aad_len, uint32_t L, const uint4 *__restrict__ T,
+                                                      uint32_t &y0, uint32_t &y1, uint32_t &y2, uint32_t &y3) {
+    const char *base = reinterpret_cast<const char *>(T);
+    const uint32_t w1 = bswap(aad_len * 8u), w3 = bswap(L * 8u);
+    const uint32_t v[5] = {w1 >> 24, w3, w3 >> 8, w3 >> 16, w3 >> 24};
+    const int j[5] = {7, 12, 13, 14, 15};  // comb table pair of word w, byte k: 4 w + k
+    uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        const uint4 th = *reinterpret_cast<const uint4 *>(base + (2 * j[i]) * 256 + (v[i] & 0xf0u));
+        const uint4 tl = *reinterpret_cast<const uint4 *>(base + (2 * j[i] + 1) * 256 + ((v[i] & 0x0fu) << 4));
+        a0 = xor3(a0, th.x, tl.x);
+        a1 = xor3(a1, th.y, tl.y);
+        a2 = xor3(a2, th.z, tl.z);
+        a3 = xor3(a3, th.w, tl.w);
+    }
+    y0 = a0;
+    y1 = a1;
+    y2 = a2;
+    y3 = a3;
+}
+
 __device__ __forceinline__ uint32_t sel4(uint32_t q, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
     return q == 0 ? a : (q == 1 ? b : (q == 2 ? c : d));
 }
@@ -356,6 +380,7 @@ gcm_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
             valid = valid && len >= (uint32_t)QGCM_OVERHEAD;  // Open: ciphertext shorter than tag
             L = len - QGCM_OVERHEAD;
         }
+        valid = valid && L < QGCM_MAX_PAYLOAD;
         if (!valid) {
             if (!kSeal && b.status && pkt < b.n) b.status[pkt] = 0;
             continue;
@@ -504,7 +529,7 @@ gcm_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
 // with the additional data A folded in as block -1 of lane 3 (SP 800-38D GHASH, restated for a
 // 4-way interleave; checked against the oracle in tests).  E_K(J0) is computed by lane d % 4 in the
 // slot where it has no data block.
-constexpr uint32_t kQuadLds = kTeBytes + 2 * kGhBytes;
+constexpr uint32_t kQuadLds = kTeBytes + kGhBytes;  // T-tables + the comb table of H^4
 
 __device__ __forceinline__ uint32_t quad_xor(uint32_t v) {
     v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xf, 0xf, false);  // quad_perm [1,0,3,2]
@@ -512,7 +537,10 @@ __device__ __forceinline__ uint32_t quad_xor(uint32_t v) {
     return v;
 }
 
-template <bool kSeal, int kW, bool kFold, int kWpe = kW / 4, bool kDesc = false>
+// kGFin: the once-per-packet recombination multiplies by H^2..H^5 come from the global key table
+// (one multiply per lane); otherwise by repeated multiplies by H (comb table of H in LDS for single
+// key batches, global for descriptor batches).
+template <bool kSeal, int kW, bool kFold, int kWpe = kW / 4, bool kDesc = false, bool kGFin = true>
 __global__ void __launch_bounds__(kW * 64) __attribute__((amdgpu_waves_per_eu(kWpe, kWpe)))
 gcm_quad_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
     constexpr uint32_t kT = kW * 64;
@@ -526,16 +554,21 @@ gcm_quad_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
         lds_st32(4 * i, b.te[(slot >> 5) * 256u + x]);
     }
     if constexpr (!kDesc) {
-        const uint4 *src = b.gh_table + (size_t)b.uniform_key * kGhEntries;  // H then H^4
-        for (uint32_t e = threadIdx.x; e < kGhEntries; e += kT) lds_st128(kTeBytes + e * 16, src[e]);
+        const uint4 *src = b.gh_table + (size_t)b.uniform_key * kGhEntries + kGhH4;
+        for (uint32_t e = threadIdx.x; e < 512u; e += kT) lds_st128(kTeBytes + e * 16, src[e]);
+        if constexpr (!kGFin) {
+            const uint4 *srcH = b.gh_table + (size_t)b.uniform_key * kGhEntries + kGhH;
+            for (uint32_t e = threadIdx.x; e < 512u; e += kT) lds_st128(kTeBytes + kGhBytes + e * 16, srcH[e]);
+        }
     }
     __syncthreads();
 
     const uint32_t lb = (lane & 31u) << 2;
-    // single key: H and H^4 tables shared by the workgroup; descriptors: one H^4 table per wave in
-    // LDS (reloaded when the wave's key changes), H read from the L2-resident key table
-    const uint32_t gH = kTeBytes;
-    const uint32_t gH4 = kDesc ? kTeBytes + wave * kGhBytes : kTeBytes + kGhBytes;
+    // single key: the H^4 table shared by the workgroup; descriptors: one H^4 table per wave
+    // (reloaded when the wave's key changes).  The once-per-packet multiplies by H^2..H^5 read the
+    // L2-resident key table from global memory, off the LDS pipe that bounds the kernel.
+    const uint32_t gH4 = kDesc ? kTeBytes + wave * kGhBytes : kTeBytes;
+    const uint32_t gH = kTeBytes + kGhBytes;  // comb table of H in LDS (single key, !kGFin)
     uint32_t cur_key = kDesc ? 0xffffffffu : b.uniform_key;
     const uint32_t ntiles = kDesc ? (b.n_items >> 4) : ((b.n + 15) >> 4);
 
@@ -561,7 +594,7 @@ gcm_quad_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
             if (vmask != 0) {
                 wkey = __builtin_amdgcn_readfirstlane(__shfl(dsc.key_idx, __ffsll((unsigned long long)vmask) - 1));
                 if (wkey != cur_key) {
-                    const uint4 *src = b.gh_table + (size_t)wkey * kGhEntries + 512;  // H^4
+                    const uint4 *src = b.gh_table + (size_t)wkey * kGhEntries + kGhH4;
 #pragma unroll
                     for (int r = 0; r < 8; ++r) {
                         const uint32_t e = r * 64 + lane;
@@ -602,7 +635,7 @@ gcm_quad_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
             }
         }
         const Keys kk = {rk_table + (size_t)wkey * kRkWords, rk_table + (size_t)wkey * kRkWords + 64};
-        const uint4 *Hg = b.gh_table + (size_t)wkey * kGhEntries;  // comb table of H (global)
+        const uint4 *Hg = b.gh_table + (size_t)wkey * kGhEntries;  // comb tables of H^k (global)
         uint8_t *raw = b.arena + off;
         uint8_t *data = raw + 4;  // common.PacketStart
 
@@ -701,66 +734,82 @@ gcm_quad_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
             z3 ^= c.w;
             blast = (int)bi;
         }
-        if (r && (nfull & 3u) == m) {  // the partial last block
-            const uint32_t ctr = nfull + 2;
+        // One more slot: the partial last block (lane nfull % 4) and E_K(J0) (lane d % 4, the lane
+        // with the fewest data blocks) share one AES pass.
+        const bool part = r && (nfull & 3u) == m;
+        if (part || m == (d & 3u)) {
+            const uint32_t ctr = part ? nfull + 2 : 1u;  // inc32(J0) + nfull, or J0
             if ((ctr >> 8) != hi) {
                 hi = ctr >> 8;
                 ctr_setup(cc, n0, n1, n2, hi, kk, lb);
             }
             uint32_t k0, k1, k2, k3;
             ctr_block(cc, ctr & 0xffu, kk, lb, k0, k1, k2, k3);
-            uint8_t *blk = data + 16u * nfull;
-            const W4 in = *reinterpret_cast<const W4 *>(blk);  // reads into tag area: inside the slot
-            const uint32_t q = r >> 2, sb = r & 3u;
-            const uint32_t o0 = in.x ^ k0, o1 = in.y ^ k1, o2 = in.z ^ k2, o3 = in.w ^ k3;
-            uint32_t *bw = reinterpret_cast<uint32_t *>(blk);
-            if (q > 0) bw[0] = o0;
-            if (q > 1) bw[1] = o1;
-            if (q > 2) bw[2] = o2;
-            const uint32_t oq = sel4(q, o0, o1, o2, o3) & lowmask(sb);
-            W4 c = kSeal ? W4{o0, o1, o2, o3} : in;
-            if (kSeal)
-                prefix = oq;  // written with tag||nonce by write_tail
-            else
-                store_bytes(blk + 4 * q, oq, sb);
-            c.x &= q > 0 ? 0xffffffffu : lowmask(sb);
-            c.y &= q > 1 ? 0xffffffffu : (q == 1 ? lowmask(sb) : 0u);
-            c.z &= q > 2 ? 0xffffffffu : (q == 2 ? lowmask(sb) : 0u);
-            c.w &= q == 3 ? lowmask(sb) : 0u;
-            ghash_mul(z0, z1, z2, z3, gH4);
-            z0 ^= c.x;
-            z1 ^= c.y;
-            z2 ^= c.z;
-            z3 ^= c.w;
-            blast = (int)nfull;
+            if (part) {
+                uint8_t *blk = data + 16u * nfull;
+                const W4 in = *reinterpret_cast<const W4 *>(blk);  // reads into tag area: inside the slot
+                const uint32_t q = r >> 2, sb = r & 3u;
+                const uint32_t o0 = in.x ^ k0, o1 = in.y ^ k1, o2 = in.z ^ k2, o3 = in.w ^ k3;
+                uint32_t *bw = reinterpret_cast<uint32_t *>(blk);
+                if (q > 0) bw[0] = o0;
+                if (q > 1) bw[1] = o1;
+                if (q > 2) bw[2] = o2;
+                const uint32_t oq = sel4(q, o0, o1, o2, o3) & lowmask(sb);
+                W4 c = kSeal ? W4{o0, o1, o2, o3} : in;
+                if (kSeal)
+                    prefix = oq;  // written with tag||nonce by write_tail
+                else
+                    store_bytes(blk + 4 * q, oq, sb);
+                c.x &= q > 0 ? 0xffffffffu : lowmask(sb);
+                c.y &= q > 1 ? 0xffffffffu : (q == 1 ? lowmask(sb) : 0u);
+                c.z &= q > 2 ? 0xffffffffu : (q == 2 ? lowmask(sb) : 0u);
+                c.w &= q == 3 ? lowmask(sb) : 0u;
+                ghash_mul(z0, z1, z2, z3, gH4);
+                z0 ^= c.x;
+                z1 ^= c.y;
+                z2 ^= c.z;
+                z3 ^= c.w;
+                blast = (int)nfull;
+            } else {
+                e0 = k0;
+                e1 = k1;
+                e2 = k2;
+                e3 = k3;
+            }
         }
-        // E_K(J0) in lane d % 4 (the lane with the fewest data blocks)
-        if (m == (d & 3u)) {
-            if (hi != 0) ctr_setup(cc, n0, n1, n2, 0, kk, lb);
-            ctr_block(cc, 1, kk, lb, e0, e1, e2, e3);
         }
-        }
-        // Z_m * H^(e_m - 1), e_m = d + 1 - b_last(m)
-        for (int t = (int)d - blast; t > 0; --t) {
+        // Y = sum_m Z_m * H^(e_m)  ^  ([len(A)]||[len(C)]) * H,  e_m = d + 1 - b_last(m) in [2, 5]
+        // (a lane without blocks has Z_m = 0 or only the AAD block, b_last = -1, d <= 3).
+        if constexpr (kGFin) {
+            const uint32_t em = d + 1u - (uint32_t)blast;
+            const uint32_t tsel = em == 2 ? kGhH2 : em == 3 ? kGhH3 : em == 4 ? kGhH4 : kGhH5;
+            ghash_mul_global(z0, z1, z2, z3, Hg + tsel);
+            uint32_t l0, l1, l2, l3;
+            ghash_lenblock_global(b.aad_len, L, Hg, l0, l1, l2, l3);
+            z0 = quad_xor(z0) ^ l0;
+            z1 = quad_xor(z1) ^ l1;
+            z2 = quad_xor(z2) ^ l2;
+            z3 = quad_xor(z3) ^ l3;
+        } else {
+            for (int t = (int)d - blast; t > 0; --t) {
+                if constexpr (kDesc)
+                    ghash_mul_global(z0, z1, z2, z3, Hg);
+                else
+                    ghash_mul(z0, z1, z2, z3, gH);
+            }
+            z0 = quad_xor(z0);
+            z1 = quad_xor(z1) ^ bswap(b.aad_len * 8u);  // [len(A)]_64 || [len(C)]_64, big endian
+            z2 = quad_xor(z2);
+            z3 = quad_xor(z3) ^ bswap(L * 8u);
             if constexpr (kDesc)
                 ghash_mul_global(z0, z1, z2, z3, Hg);
             else
                 ghash_mul(z0, z1, z2, z3, gH);
         }
-        z0 = quad_xor(z0);
-        z1 = quad_xor(z1);
-        z2 = quad_xor(z2);
-        z3 = quad_xor(z3);
         e0 = quad_xor(e0);
         e1 = quad_xor(e1);
         e2 = quad_xor(e2);
         e3 = quad_xor(e3);
-        z1 ^= bswap(b.aad_len * 8u);  // [len(A)]_64 || [len(C)]_64, big endian
-        z3 ^= bswap(L * 8u);
-        if constexpr (kDesc)
-            ghash_mul_global(z0, z1, z2, z3, Hg);
-        else
-            ghash_mul(z0, z1, z2, z3, gH);
         const uint32_t t0 = z0 ^ e0, t1 = z1 ^ e1, t2 = z2 ^ e2, t3 = z3 ^ e3;
         // the lane owning the partial block (or lane 0) writes the tail
         const uint32_t owner = r ? (nfull & 3u) : 0u;
@@ -805,18 +854,18 @@ Variant make_variant() {
                    lds_bytes<kW, kShared>(), false, 1, false};
 }
 
-template <int kW, bool kFold, int kWpe = kW / 4>
+template <int kW, bool kFold, int kWpe = kW / 4, bool kGFin = true>
 Variant make_quad() {
-    return Variant{reinterpret_cast<const void *>(&gcm_quad_kernel<true, kW, kFold, kWpe>),
-                   reinterpret_cast<const void *>(&gcm_quad_kernel<false, kW, kFold, kWpe>), kW, kQuadLds, true,
-                   kWpe * 4 / kW, false};
+    return Variant{reinterpret_cast<const void *>(&gcm_quad_kernel<true, kW, kFold, kWpe, false, kGFin>),
+                   reinterpret_cast<const void *>(&gcm_quad_kernel<false, kW, kFold, kWpe, false, kGFin>), kW,
+                   kQuadLds + (kGFin ? 0u : kGhBytes), true, kWpe * 4 / kW, false};
 }
 
 // descriptor batches: per-wave H^4 table, so LDS = Te + one 8 KiB table per wave
-template <int kW, int kWpe>
+template <int kW, int kWpe, bool kGFin = true>
 Variant make_quad_desc() {
-    return Variant{reinterpret_cast<const void *>(&gcm_quad_kernel<true, kW, false, kWpe, true>),
-                   reinterpret_cast<const void *>(&gcm_quad_kernel<false, kW, false, kWpe, true>), kW,
+    return Variant{reinterpret_cast<const void *>(&gcm_quad_kernel<true, kW, false, kWpe, true, kGFin>),
+                   reinterpret_cast<const void *>(&gcm_quad_kernel<false, kW, false, kWpe, true, kGFin>), kW,
                    kTeBytes + (uint32_t)kW * kGhBytes, true, 1, true};
 }
 
@@ -832,6 +881,8 @@ hipError_t init_kernels() {
     g_variants[6] = make_quad<8, false, 4>();      // quad, 8-wave workgroups, two per CU (16 waves/CU)
     g_variants[7] = make_quad_desc<12, 3>();       // descriptors: quad, 12 waves/CU, per-wave H^4 tables
     g_variants[8] = make_quad_desc<8, 2>();        // descriptors: quad, 8 waves/CU
+    g_variants[9] = make_quad<16, false, 8, false>();   // as 5, recombination by repeated H (LDS)
+    g_variants[10] = make_quad_desc<12, 3, false>();    // as 7, recombination by repeated H (global)
     for (const Variant &v : g_variants) {
         for (const void *k : {v.seal, v.open}) {
             hipFuncAttributes a;
@@ -894,8 +945,8 @@ __global__ void __launch_bounds__(256) key_setup_kernel(const uint8_t *keys, uin
                                                         uint4 *gh_table, const uint8_t *sbox_g) {
     __shared__ uint8_t sbox[256];
     __shared__ uint8_t rkb[240];
-    __shared__ uint4 pw[128];
-    __shared__ uint4 pw4[128];
+    __shared__ uint8_t hp[5][16];  // H, H^4, H^2, H^3, H^5 (the order of the comb tables)
+    __shared__ uint4 pw[5][128];   // x^i * hp[t]
     const uint32_t kidx = blockIdx.x;
     const uint8_t *key = keys + 32u * kidx;
     sbox[threadIdx.x] = sbox_g[threadIdx.x];
@@ -937,22 +988,22 @@ __global__ void __launch_bounds__(256) key_setup_kernel(const uint8_t *keys, uin
             }
             for (int i = 0; i < 16; ++i) s[i] ^= rkb[16 * round + i];
         }
-        // H^4 = (H^2)^2 by SP 800-38D Algorithm 1 (bit-serial; setup only).
-        uint8_t h2[16], h4[16];
-        gf128_mul_bytes(s, s, h2);
-        gf128_mul_bytes(h2, h2, h4);
-        // x^i * H and x^i * H^4: multiply by x = shift toward higher bit index (right shift of the
-        // byte string), reduce with R = 0xe1 || 0^120 (SP 800-38D Algorithm 1).
-        uint8_t v[16], v4[16];
-        for (int i = 0; i < 16; ++i) {
-            v[i] = s[i];
-            v4[i] = h4[i];
-        }
+        // powers of H by SP 800-38D Algorithm 1 (bit-serial; setup only)
+        for (int i = 0; i < 16; ++i) hp[0][i] = s[i];
+        gf128_mul_bytes(s, s, hp[2]);            // H^2
+        gf128_mul_bytes(hp[2], s, hp[3]);        // H^3
+        gf128_mul_bytes(hp[2], hp[2], hp[1]);    // H^4
+        gf128_mul_bytes(hp[1], s, hp[4]);        // H^5
+    }
+    __syncthreads();
+    // x^i * H^k: multiply by x = shift toward higher bit index (right shift of the byte string),
+    // reduce with R = 0xe1 || 0^120 (SP 800-38D Algorithm 1).
+    if (threadIdx.x < 5) {
+        uint8_t v[16];
+        for (int i = 0; i < 16; ++i) v[i] = hp[threadIdx.x][i];
         for (int i = 0; i < 128; ++i) {
-            pw[i] = pack16(v);
-            pw4[i] = pack16(v4);
+            pw[threadIdx.x][i] = pack16(v);
             shift_x(v);
-            shift_x(v4);
         }
     }
     __syncthreads();
@@ -965,10 +1016,10 @@ __global__ void __launch_bounds__(256) key_setup_kernel(const uint8_t *keys, uin
         rk_table[(size_t)slot * kRkWords + i] = w;
         rk_table[(size_t)slot * kRkWords + 64 + i] = (w << 16) | (w >> 16);
     }
-    // entries [0, 512): comb table of H; [512, 1024): comb table of H^4
+    // entries [512 t, 512 t + 512): comb table of hp[t]
     for (uint32_t e = threadIdx.x; e < kGhEntries; e += 256) {
         const uint32_t p = (e & 511u) >> 4, v = e & 15u;
-        const uint4 *src = e < 512 ? pw : pw4;
+        const uint4 *src = pw[e >> 9];
         uint4 acc = {0, 0, 0, 0};
         for (int k = 0; k < 4; ++k) {
             if ((v >> (3 - k)) & 1u) {

@@ -18,6 +18,9 @@
 
 using namespace qgcm;
 
+constexpr int kPipeStreams = 3;         // H2D / kernel / D2H of consecutive chunks overlap
+constexpr uint64_t kPipeChunk = 32ull << 20;  // bytes of slots per pipeline chunk
+
 struct qgcm_ctx {
     int device = 0;
     int num_cus = 0;
@@ -45,6 +48,17 @@ struct qgcm_ctx {
     size_t io_cap = 0;
     uint8_t *h_pin = nullptr;
     size_t pin_cap = 0;
+
+    // host-batch pipeline (qgcm_seal_host / qgcm_open_host), guarded by io_mu
+    hipStream_t pipe[kPipeStreams] = {};
+    uint8_t *d_ring = nullptr;  // kPipeStreams chunk slots, one per stream
+    size_t ring_cap = 0;
+    uint8_t *h_stat = nullptr;  // pinned status bytes of the whole host batch
+    size_t hstat_cap = 0;
+
+    // orders reuse of the descriptor workspace across streams (guarded by ws_mu)
+    hipEvent_t ws_done = nullptr;
+    bool ws_pending = false;
 };
 
 namespace {
@@ -122,6 +136,8 @@ int run_uniform(qgcm_ctx *ctx, bool seal, uint8_t *arena, uint64_t stride, uint3
     if (!ctx || (!arena && n) || aad_len > 4) return QGCM_E_ARG;
     if (((uintptr_t)arena & 3) || (stride & 3) || (nonces && ((uintptr_t)nonces & 3))) return QGCM_E_ARG;
     if (n && stride < (uint64_t)len + 4 + (seal ? QGCM_OVERHEAD : 0)) return QGCM_E_ARG;
+    if ((seal || len >= QGCM_OVERHEAD) && len - (seal ? 0u : (uint32_t)QGCM_OVERHEAD) >= QGCM_MAX_PAYLOAD)
+        return QGCM_E_ARG;
     if (!key_ok(ctx, key_idx)) return QGCM_E_KEY;
     if (n == 0) return QGCM_OK;
     if (hipSetDevice(ctx->device) != hipSuccess) return QGCM_E_HIP;
@@ -139,6 +155,9 @@ int run_uniform(qgcm_ctx *ctx, bool seal, uint8_t *arena, uint64_t stride, uint3
     return hip_fail(launch_packets(seal, v, b, grid_for(ctx, b.n_items, v), s));
 }
 
+int run_descs_locked(qgcm_ctx *ctx, bool seal, const qgcm_desc *descs, uint32_t n, hipStream_t s, Batch b,
+                     uint8_t *arena, const uint8_t *nonces, uint32_t aad_len, uint8_t *status);
+
 int run_descs(qgcm_ctx *ctx, bool seal, uint8_t *arena, const qgcm_desc *descs, uint32_t n, const uint8_t *nonces,
               uint32_t aad_len, uint8_t *status, hipStream_t s) {
     if (!ctx || (n && (!arena || !descs)) || aad_len > 4) return QGCM_E_ARG;
@@ -148,7 +167,19 @@ int run_descs(qgcm_ctx *ctx, bool seal, uint8_t *arena, const qgcm_desc *descs, 
     if (status && hipMemsetAsync(status, 0, n, s) != hipSuccess) return QGCM_E_HIP;
     // The workspace is reused by the next call on any stream: serialize descriptor batches per ctx.
     std::lock_guard<std::mutex> g(ctx->ws_mu);
-    Batch b = base_batch(ctx);
+    // ...and on the device: this batch's worklist build must not start before the previous batch's
+    // kernel (possibly on another stream) has finished reading the workspace.
+    if (ctx->ws_pending && hipStreamWaitEvent(s, ctx->ws_done, 0) != hipSuccess) return QGCM_E_HIP;
+    const int rc = run_descs_locked(ctx, seal, descs, n, s, base_batch(ctx), arena, nonces, aad_len, status);
+    if (rc == QGCM_OK) {
+        if (hipEventRecord(ctx->ws_done, s) != hipSuccess) return QGCM_E_HIP;
+        ctx->ws_pending = true;
+    }
+    return rc;
+}
+
+int run_descs_locked(qgcm_ctx *ctx, bool seal, const qgcm_desc *descs, uint32_t n, hipStream_t s, Batch b,
+                     uint8_t *arena, const uint8_t *nonces, uint32_t aad_len, uint8_t *status) {
     b.arena = arena;
     b.descs = descs;
     b.nonces = seal ? nonces : nullptr;
@@ -276,7 +307,10 @@ qgcm_ctx *qgcm_create(int device, uint32_t max_keys, char *err, int errlen) {
               hipMemcpy(ctx->d_te, te, sizeof te, hipMemcpyHostToDevice) == hipSuccess &&
               hipMemcpy(ctx->d_sbox, sbox, sizeof sbox, hipMemcpyHostToDevice) == hipSuccess &&
               hipStreamCreateWithFlags(&ctx->io_stream, hipStreamNonBlocking) == hipSuccess &&
+              hipEventCreateWithFlags(&ctx->ws_done, hipEventDisableTiming) == hipSuccess &&
               init_kernels() == hipSuccess;
+    for (int k = 0; ok && k < kPipeStreams; ++k)
+        ok = hipStreamCreateWithFlags(&ctx->pipe[k], hipStreamNonBlocking) == hipSuccess;
     if (!ok) {
         set_err(err, errlen, "device allocation / kernel setup failed");
         qgcm_destroy(ctx);
@@ -300,6 +334,11 @@ void qgcm_destroy(qgcm_ctx *ctx) {
     hipFree(ctx->d_io);
     if (ctx->h_pin) hipHostFree(ctx->h_pin);
     if (ctx->io_stream) hipStreamDestroy(ctx->io_stream);
+    hipFree(ctx->d_ring);
+    if (ctx->h_stat) hipHostFree(ctx->h_stat);
+    for (hipStream_t p : ctx->pipe)
+        if (p) hipStreamDestroy(p);
+    if (ctx->ws_done) hipEventDestroy(ctx->ws_done);
     delete ctx;
 }
 
@@ -361,7 +400,7 @@ int qgcm_open_uniform(qgcm_ctx *ctx, uint8_t *d_arena, uint64_t stride, uint32_t
 
 long qgcm_seal_one(qgcm_ctx *ctx, uint32_t key_idx, uint8_t *data, long length, const uint8_t *aad, uint32_t aad_len,
                    const uint8_t *nonce) {
-    if (!ctx || !data || length < 0 || length > (1l << 30) || aad_len > 4 || (aad_len && !aad)) return -1;
+    if (!ctx || !data || length < 0 || length >= (long)QGCM_MAX_PAYLOAD || aad_len > 4 || (aad_len && !aad)) return -1;
     if (!key_ok(ctx, key_idx)) return -1;
     uint8_t nb[12];
     if (nonce) {
@@ -392,7 +431,7 @@ long qgcm_seal_one(qgcm_ctx *ctx, uint32_t key_idx, uint8_t *data, long length, 
 }
 
 long qgcm_open_one(qgcm_ctx *ctx, uint32_t key_idx, uint8_t *data, long len, const uint8_t *aad, uint32_t aad_len) {
-    if (!ctx || (!data && len) || len < 0 || len > (1l << 30) || aad_len > 4 || (aad_len && !aad)) return -1;
+    if (!ctx || (!data && len) || len < 0 || len - QGCM_OVERHEAD >= (long)QGCM_MAX_PAYLOAD || aad_len > 4 || (aad_len && !aad)) return -1;
     if (len < QGCM_OVERHEAD) return -1;  // crypto/aes.go:58-60: errOpen (the reference panics below 12)
     if (!key_ok(ctx, key_idx)) return -1;
     std::lock_guard<std::mutex> g(ctx->io_mu);
@@ -415,36 +454,81 @@ long qgcm_open_one(qgcm_ctx *ctx, uint32_t key_idx, uint8_t *data, long len, con
     return h[stride] == 1 ? len - QGCM_OVERHEAD : -1;
 }
 
+// Host batches, pipelined: the batch is cut into ~32 MiB chunks; chunk c runs H2D -> kernel -> D2H on
+// stream c % 3 in its own device slot, so the copy-in of chunk c+1, the kernel of chunk c and the
+// copy-out of chunk c-1 overlap (both PCIe directions busy at once).  Pinned caller memory
+// (qgcm_host_alloc, hipHostMalloc/Register) is DMA'd in place; pageable memory still works but HIP
+// stages it, which serializes the copies.
 static int run_host(qgcm_ctx *ctx, bool seal, uint8_t *h_arena, uint64_t stride, uint32_t n, uint32_t len,
                     uint32_t key_idx, const uint8_t *h_nonces, uint32_t aad_len, uint8_t *h_status) {
-    if (!ctx || (n && !h_arena)) return QGCM_E_ARG;
+    if (!ctx || (n && !h_arena) || aad_len > 4 || (stride & 3)) return QGCM_E_ARG;
+    if (n && stride < (uint64_t)len + 4 + (seal ? QGCM_OVERHEAD : 0)) return QGCM_E_ARG;
+    if ((seal || len >= QGCM_OVERHEAD) && len - (seal ? 0u : (uint32_t)QGCM_OVERHEAD) >= QGCM_MAX_PAYLOAD)
+        return QGCM_E_ARG;
+    if (!key_ok(ctx, key_idx)) return QGCM_E_KEY;
     if (n == 0) return 0;
     std::lock_guard<std::mutex> g(ctx->io_mu);
     if (hipSetDevice(ctx->device) != hipSuccess) return QGCM_E_HIP;
-    const uint64_t bytes = stride * n;
-    const uint64_t nb = seal && h_nonces ? 12ull * n : 0;
-    const uint64_t need = ((bytes + 15) & ~15ull) + ((nb + 15) & ~15ull) + n;
-    int rc = ensure_io(ctx, need);
+    auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
+    uint64_t cpk = (kPipeChunk / stride) & ~63ull;  // packets per chunk, whole 64-packet tiles
+    if (cpk < 64) cpk = 64;
+    if (cpk > n) cpk = n;
+    const uint64_t nchunks = (n + cpk - 1) / cpk;
+    const bool non = seal && h_nonces;
+    const uint64_t off_non = al(cpk * stride), off_st = off_non + (non ? al(12 * cpk) : 0);
+    const uint64_t slot = off_st + al(cpk);
+    const int nslots = nchunks < (uint64_t)kPipeStreams ? (int)nchunks : kPipeStreams;
+    if (slot * nslots > ctx->ring_cap) {
+        if (ctx->d_ring) hipFree(ctx->d_ring);
+        ctx->d_ring = nullptr;
+        ctx->ring_cap = 0;
+        if (hipMalloc(&ctx->d_ring, slot * nslots) != hipSuccess) return QGCM_E_NOMEM;
+        ctx->ring_cap = slot * nslots;
+    }
+    if (n > ctx->hstat_cap) {
+        if (ctx->h_stat) hipHostFree(ctx->h_stat);
+        ctx->h_stat = nullptr;
+        ctx->hstat_cap = 0;
+        if (hipHostMalloc(&ctx->h_stat, n, hipHostMallocDefault) != hipSuccess) return QGCM_E_NOMEM;
+        ctx->hstat_cap = n;
+    }
+    int rc = QGCM_OK;
+    for (uint64_t c = 0; c < nchunks && rc == QGCM_OK; ++c) {
+        const int k = (int)(c % nslots);
+        hipStream_t s = ctx->pipe[k];
+        uint8_t *d = ctx->d_ring + k * slot, *d_non = d + off_non, *d_st = d + off_st;
+        const uint64_t c0 = c * cpk, cn = (n - c0) < cpk ? (n - c0) : cpk;
+        uint8_t *h = h_arena + c0 * stride;
+        if (hipMemcpyAsync(d, h, cn * stride, hipMemcpyHostToDevice, s) != hipSuccess ||
+            (non && hipMemcpyAsync(d_non, h_nonces + 12 * c0, 12 * cn, hipMemcpyHostToDevice, s) != hipSuccess)) {
+            rc = QGCM_E_HIP;
+            break;
+        }
+        if (!seal && len < QGCM_OVERHEAD)
+            rc = hip_fail(hipMemsetAsync(d_st, 0, cn, s));
+        else
+            rc = run_uniform(ctx, seal, d, stride, (uint32_t)cn, len, key_idx, non ? d_non : nullptr, aad_len, d_st, s);
+        if (rc == QGCM_OK && (hipMemcpyAsync(h, d, cn * stride, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                              hipMemcpyAsync(ctx->h_stat + c0, d_st, cn, hipMemcpyDeviceToHost, s) != hipSuccess))
+            rc = QGCM_E_HIP;
+    }
+    for (int k = 0; k < nslots; ++k)
+        if (hipStreamSynchronize(ctx->pipe[k]) != hipSuccess) rc = QGCM_E_HIP;
     if (rc != QGCM_OK) return rc;
-    uint8_t *d_arena = ctx->d_io, *d_non = ctx->d_io + ((bytes + 15) & ~15ull);
-    uint8_t *d_stat = d_non + ((nb + 15) & ~15ull);
-    hipStream_t s = ctx->io_stream;
-    if (hipMemcpyAsync(d_arena, h_arena, bytes, hipMemcpyHostToDevice, s) != hipSuccess) return QGCM_E_HIP;
-    if (nb && hipMemcpyAsync(d_non, h_nonces, nb, hipMemcpyHostToDevice, s) != hipSuccess) return QGCM_E_HIP;
-    rc = seal ? run_uniform(ctx, true, d_arena, stride, n, len, key_idx, nb ? d_non : nullptr, aad_len, d_stat, s)
-              : (len < QGCM_OVERHEAD ? hip_fail(hipMemsetAsync(d_stat, 0, n, s))
-                                     : run_uniform(ctx, false, d_arena, stride, n, len, key_idx, nullptr, aad_len,
-                                                   d_stat, s));
-    if (rc != QGCM_OK) return rc;
-    if (hipMemcpyAsync(h_arena, d_arena, bytes, hipMemcpyDeviceToHost, s) != hipSuccess) return QGCM_E_HIP;
-    std::vector<uint8_t> st(n);
-    if (hipMemcpyAsync(st.data(), d_stat, n, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipStreamSynchronize(s) != hipSuccess)
-        return QGCM_E_HIP;
     int bad = 0;
-    for (uint32_t i = 0; i < n; ++i) bad += st[i] != 1;
-    if (h_status) memcpy(h_status, st.data(), n);
+    for (uint32_t i = 0; i < n; ++i) bad += ctx->h_stat[i] != 1;
+    if (h_status) memcpy(h_status, ctx->h_stat, n);
     return bad;
+}
+
+void *qgcm_host_alloc(size_t bytes) {
+    void *p = nullptr;
+    if (bytes == 0 || hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) return nullptr;
+    return p;
+}
+
+void qgcm_host_free(void *p) {
+    if (p) hipHostFree(p);
 }
 
 int qgcm_seal_host(qgcm_ctx *ctx, uint8_t *h_arena, uint64_t stride, uint32_t n, uint32_t len, uint32_t key_idx,

@@ -4,7 +4,8 @@
 // (key_idx, length descending) with a device radix sort, then each key's run is padded to a multiple
 // of 16 entries so that every 16-packet wave tile uses ONE key (round keys in SGPRs, one GHASH table
 // per wave) and holds packets of similar length (the 4-lane quads of a wave finish together).
-// Packets that cannot be processed (key index out of range, open with len < 28) are left out: their
+// Packets that cannot be processed (key index out of range, open with len < 28, payload of
+// QGCM_MAX_PAYLOAD or more) are left out: their
 // status stays 0 and their slot is untouched.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
@@ -22,7 +23,8 @@ __global__ void qwl_keys_kernel(const qgcm_desc *descs, uint32_t n, uint32_t max
     if (i >= n) return;
     const qgcm_desc d = descs[i];
     uint32_t sk = 0xffffffffu;
-    const bool ok = d.key_idx < max_keys && (seal || d.len >= (uint32_t)QGCM_OVERHEAD);
+    const bool ok = d.key_idx < max_keys && (seal || d.len >= (uint32_t)QGCM_OVERHEAD) &&
+                    d.len - (seal ? 0u : (uint32_t)QGCM_OVERHEAD) < QGCM_MAX_PAYLOAD;
     if (ok) {
         const uint32_t L = seal ? d.len : d.len - QGCM_OVERHEAD;
         const uint32_t nb = min((L + 15u) >> 4, (1u << kLenBits) - 1u);

@@ -1,0 +1,69 @@
+"""A/B the descriptor-batch kernel variants on the config-3 workload in ONE process, interleaved.
+
+Each variant is its own qgcm context (QGCM_DESC_VARIANT is read at qgcm_create) with the same 1024
+keys.  Correctness: every variant's sealed arena must equal the first variant's byte for byte.
+Usage: python tools/ab_desc.py 7,10,8 [rounds]
+"""
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from quantum_amd import batch  # noqa: E402
+from quantum_amd.crypto import Context  # noqa: E402
+
+variants = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "7,10").split(",")]
+rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+N, NK = 1 << 20, 1024
+rng = np.random.default_rng(0x5EED0003)
+keys = rng.bytes(32 * NK)
+ctxs = {}
+for v in variants:
+    os.environ["QGCM_DESC_VARIANT"] = str(v)
+    c = Context(device=0, max_keys=NK)
+    c.set_keys(0, keys)
+    ctxs[v] = c
+lens = rng.integers(64, 9001, size=N, dtype=np.int64)
+kidx = rng.integers(0, NK, size=N, dtype=np.int64)
+slot = (4 + lens + 28 + 3) & ~3
+offs = np.zeros(N, dtype=np.int64)
+offs[1:] = np.cumsum(slot)[:-1]
+total = int(offs[-1] + slot[-1])
+plain = torch.randint(0, 256, (total + 64,), dtype=torch.uint8, device="cuda")
+arena = plain.clone()
+nonces = torch.randint(0, 256, (12 * N,), dtype=torch.uint8, device="cuda")
+status = torch.zeros(N, dtype=torch.uint8, device="cuda")
+d_seal = batch.make_descs(offs, lens, kidx, "cuda")
+d_open = batch.make_descs(offs, lens + 28, kidx, "cuda")
+ref = None
+for v, c in ctxs.items():
+    arena.copy_(plain)
+    batch.seal_batch(c, arena, d_seal, N, nonces, status=status)
+    ok = int(status.sum()) == N
+    if ref is None:
+        ref = arena.clone()
+    same = bool(torch.equal(arena, ref))
+    batch.open_batch(c, arena, d_open, N, status=status)
+    rt = int(status.sum()) == N and bool(torch.equal(arena[:64], plain[:64]))
+    print(f"variant {v}: status_ok={ok} same_as_first={same} roundtrip_ok={rt}", flush=True)
+payload = int(lens.sum())
+res = {v: ([], []) for v in variants}
+for r in range(rounds + 1):
+    for v, c in ctxs.items():
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        e[0].record()
+        batch.seal_batch(c, arena, d_seal, N, nonces, status=status)
+        e[1].record()
+        batch.open_batch(c, arena, d_open, N, status=status)
+        e[2].record()
+        torch.cuda.synchronize()
+        if r > 0:
+            res[v][0].append(e[0].elapsed_time(e[1]))
+            res[v][1].append(e[1].elapsed_time(e[2]))
+for v in variants:
+    s, o = statistics.median(res[v][0]), statistics.median(res[v][1])
+    print(f"variant {v}: seal {s:.3f} ms  open {o:.3f} ms  -> {2 * payload / ((s + o) * 1e-3) / 2**30:.1f} GiB/s",
+          flush=True)
