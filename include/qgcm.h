@@ -128,6 +128,22 @@ int qgcm_seal_host(qgcm_ctx *ctx, uint8_t *h_arena, uint64_t stride, uint32_t n,
 int qgcm_open_host(qgcm_ctx *ctx, uint8_t *h_arena, uint64_t stride, uint32_t n, uint32_t len,
                    uint32_t key_idx, uint32_t aad_len, uint8_t *h_status);
 
+/* ---- coalescer: per-packet calls from many threads, batched on the device ---- */
+/* The exact Encrypt/Decrypt contract of crypto/aes.go:41-62 (blocking, in place, L+28 / len-28 or
+ * -1, plaintext zeroed on auth failure), for the 2 x NumWorkers goroutines that call plugin.Apply
+ * (worker/outgoing.go:55-93, worker/incoming.go:54-92): concurrent calls share one device batch,
+ * flushed at max_batch packets or after max_wait_us.  Seal nonces come from one getrandom(2) per
+ * batch.  Calls whose aad_len differs from the coalescer's go through qgcm_seal_one/open_one.
+ * Thread-safe; destroy only when no call is in flight.  NULL + err on failure. */
+typedef struct qgcm_coalescer qgcm_coalescer;
+qgcm_coalescer *qgcm_coalescer_create(qgcm_ctx *ctx, uint32_t max_batch, uint32_t max_wait_us,
+                                      uint32_t max_packet, uint32_t aad_len, char *err, size_t errlen);
+void qgcm_coalescer_destroy(qgcm_coalescer *c);
+long qgcm_coalescer_seal(qgcm_coalescer *c, uint32_t key_idx, uint8_t *data, long length,
+                         const uint8_t *aad, uint32_t aad_len);
+long qgcm_coalescer_open(qgcm_coalescer *c, uint32_t key_idx, uint8_t *data, long len,
+                         const uint8_t *aad, uint32_t aad_len);
+
 /* Pinned (page-locked) host memory for arenas handed to the *_host calls; NULL on failure. */
 void *qgcm_host_alloc(size_t bytes);
 void qgcm_host_free(void *p);

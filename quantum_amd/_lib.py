@@ -20,6 +20,7 @@ EXPORTS = (
     "qgcm_seal_batch", "qgcm_open_batch", "qgcm_seal_uniform", "qgcm_open_uniform",
     "qgcm_seal_one", "qgcm_open_one", "qgcm_seal_host", "qgcm_open_host",
     "qgcm_random_nonces", "qgcm_fill_uniform", "qgcm_host_alloc", "qgcm_host_free",
+    "qgcm_coalescer_create", "qgcm_coalescer_destroy", "qgcm_coalescer_seal", "qgcm_coalescer_open",
 )
 
 QGCM_OK = 0
@@ -75,6 +76,14 @@ def _bind(L: C.CDLL) -> None:
     L.qgcm_host_alloc.restype = vp
     L.qgcm_host_free.argtypes = [vp]
     L.qgcm_host_free.restype = None
+    L.qgcm_coalescer_create.argtypes = [vp, u32, u32, u32, u32, C.c_char_p, C.c_size_t]
+    L.qgcm_coalescer_create.restype = vp
+    L.qgcm_coalescer_destroy.argtypes = [vp]
+    L.qgcm_coalescer_destroy.restype = None
+    L.qgcm_coalescer_seal.argtypes = [vp, u32, vp, lng, vp, u32]
+    L.qgcm_coalescer_seal.restype = lng
+    L.qgcm_coalescer_open.argtypes = [vp, u32, vp, lng, vp, u32]
+    L.qgcm_coalescer_open.restype = lng
     L.qgcm_fill_uniform.argtypes = [vp, u64, u32, u32, u32, u64, vp, u64, vp]
 
 

@@ -125,11 +125,13 @@ def _addr(data, offset: int = 0) -> tuple[int, int, object]:
 class AES:
     """crypto/aes.go:22-26 -- an AES-256-GCM AEAD bound to a device key slot."""
 
-    def __init__(self, key: bytes, salt: bytes | None = None, ctx: Context | None = None):
+    def __init__(self, key: bytes, salt: bytes | None = None, ctx: Context | None = None, coalescer=None):
         self.ctx = ctx or default_context()
         self.slot = self.ctx.alloc_slot()
         self.ctx.set_key(self.slot, key)
         self.salt = salt
+        # quantum_amd.coalescer.Coalescer: concurrent Encrypt/Decrypt calls share device batches
+        self.coalescer = coalescer
 
     def NonceSize(self) -> int:
         return NonceSize
@@ -152,7 +154,10 @@ class AES:
         if length < 0 or length + Overhead + NonceSize > cap:
             raise IndexError("slice bounds out of range")  # Go would panic in Seal/copy
         aad = bytes(additional) if additional is not None else b""
-        n = _lib.lib().qgcm_seal_one(self.ctx.handle, self.slot, addr, length, aad or None, len(aad), nonce)
+        if self.coalescer is not None and nonce is None:
+            n = _lib.lib().qgcm_coalescer_seal(self.coalescer.handle, self.slot, addr, length, aad or None, len(aad))
+        else:
+            n = _lib.lib().qgcm_seal_one(self.ctx.handle, self.slot, addr, length, aad or None, len(aad), nonce)
         del keep
         if n < 0:
             return -1, RuntimeError("qgcm_seal_one failed")
@@ -164,7 +169,10 @@ class AES:
         if length < NonceSize:
             raise IndexError("slice bounds out of range")  # the reference panics (negative slice)
         aad = bytes(additional) if additional is not None else b""
-        n = _lib.lib().qgcm_open_one(self.ctx.handle, self.slot, addr, length, aad or None, len(aad))
+        if self.coalescer is not None:
+            n = _lib.lib().qgcm_coalescer_open(self.coalescer.handle, self.slot, addr, length, aad or None, len(aad))
+        else:
+            n = _lib.lib().qgcm_open_one(self.ctx.handle, self.slot, addr, length, aad or None, len(aad))
         del keep
         return self.DecryptedSize(data) if n >= 0 else length - Overhead - NonceSize, (None if n >= 0 else ErrOpen())
 

@@ -54,6 +54,9 @@ hipError_t launch_quad_worklist(const qgcm_desc *descs, uint32_t n, uint32_t max
                                 size_t ws_bytes, uint32_t **worklist_out, uint32_t **counter_out,
                                 uint32_t *n_items_out, hipStream_t s);
 hipError_t launch_packets(bool seal, int variant, const Batch &b, int grid, hipStream_t s);
+// context accessors for the coalescer (coalescer.cpp), defined in qgcm_api.cpp
+int ctx_device(const qgcm_ctx *ctx);
+bool ctx_key_ready(qgcm_ctx *ctx, uint32_t key_idx);
 hipError_t launch_key_setup(const uint8_t *d_keys, uint32_t first, uint32_t count, uint32_t *rk_table,
                             uint4 *gh_table, const uint8_t *d_sbox, hipStream_t s);
 // Groups descriptor batches into key-uniform 64-packet tiles (counting sort by key_idx).

@@ -416,10 +416,11 @@ gcm_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
         auto single = [&](uint32_t bi) {
             const uint32_t ctr = bi + 2;  // inc32(J0) + bi
             if ((ctr & 0xffu) == 0) ctr_setup(cc, n0, n1, n2, ctr >> 8, kk, lb);
-            uint32_t k0, k1, k2, k3;
-            ctr_block(cc, ctr & 0xffu, kk, lb, k0, k1, k2, k3);
+            // the data load is issued before the AES rounds so its latency hides behind them
             W4 *p = reinterpret_cast<W4 *>(data + 16u * bi);
             const W4 in = *p;
+            uint32_t k0, k1, k2, k3;
+            ctr_block(cc, ctr & 0xffu, kk, lb, k0, k1, k2, k3);
             const W4 out = {in.x ^ k0, in.y ^ k1, in.z ^ k2, in.w ^ k3};
             *p = out;
             const W4 &c = kSeal ? out : in;
@@ -720,10 +721,11 @@ gcm_quad_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
                 hi = ctr >> 8;
                 ctr_setup(cc, n0, n1, n2, hi, kk, lb);
             }
-            uint32_t k0, k1, k2, k3;
-            ctr_block(cc, ctr & 0xffu, kk, lb, k0, k1, k2, k3);
+            // the data load is issued before the AES rounds so its latency hides behind them
             W4 *p = reinterpret_cast<W4 *>(data + 16u * bi);
             const W4 in = *p;
+            uint32_t k0, k1, k2, k3;
+            ctr_block(cc, ctr & 0xffu, kk, lb, k0, k1, k2, k3);
             const W4 out = {in.x ^ k0, in.y ^ k1, in.z ^ k2, in.w ^ k3};
             *p = out;
             const W4 &c = kSeal ? out : in;

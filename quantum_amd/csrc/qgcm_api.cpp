@@ -131,6 +131,13 @@ bool key_ok(qgcm_ctx *ctx, uint32_t k) {
     return ctx->key_set[k] != 0;
 }
 
+}  // namespace
+
+int qgcm::ctx_device(const qgcm_ctx *ctx) { return ctx->device; }
+bool qgcm::ctx_key_ready(qgcm_ctx *ctx, uint32_t key_idx) { return key_ok(ctx, key_idx); }
+
+namespace {
+
 int run_uniform(qgcm_ctx *ctx, bool seal, uint8_t *arena, uint64_t stride, uint32_t n, uint32_t len,
                 uint32_t key_idx, const uint8_t *nonces, uint32_t aad_len, uint8_t *status, hipStream_t s) {
     if (!ctx || (!arena && n) || aad_len > 4) return QGCM_E_ARG;

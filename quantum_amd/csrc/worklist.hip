@@ -18,7 +18,7 @@ namespace qgcm {
 constexpr uint32_t kLenBits = 12;  // length rank bits of the sort key; key index in the top 20 bits
 
 __global__ void qwl_keys_kernel(const qgcm_desc *descs, uint32_t n, uint32_t max_keys, bool seal, uint32_t *sort_keys,
-                                uint32_t *vals, uint32_t *counts) {
+                                uint32_t *vals) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const qgcm_desc d = descs[i];
@@ -29,10 +29,26 @@ __global__ void qwl_keys_kernel(const qgcm_desc *descs, uint32_t n, uint32_t max
         const uint32_t L = seal ? d.len : d.len - QGCM_OVERHEAD;
         const uint32_t nb = min((L + 15u) >> 4, (1u << kLenBits) - 1u);
         sk = (d.key_idx << kLenBits) | ((1u << kLenBits) - 1u - nb);  // longest first within a key
-        atomicAdd(&counts[d.key_idx], 1u);
     }
     sort_keys[i] = sk;
     vals[i] = i;
+}
+
+// Per-key packet counts from the sorted keys (no atomics: 1M packets on 1024 keys made a
+// histogram kernel contention-bound at ~0.2 ms): the first entry of a key run records its start,
+// the last one its count.
+__global__ void qwl_first_kernel(const uint32_t *sk, uint32_t n, uint32_t *first) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n || sk[j] == 0xffffffffu) return;
+    const uint32_t k = sk[j] >> kLenBits;
+    if (j == 0 || (sk[j - 1] >> kLenBits) != k) first[k] = j;
+}
+
+__global__ void qwl_count_kernel(const uint32_t *sk, uint32_t n, const uint32_t *first, uint32_t *counts) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n || sk[j] == 0xffffffffu) return;
+    const uint32_t k = sk[j] >> kLenBits;
+    if (j == n - 1 || sk[j + 1] == 0xffffffffu || (sk[j + 1] >> kLenBits) != k) counts[k] = j + 1 - first[k];
 }
 
 // Single workgroup: counts -> start (unpadded, sorted order) and pstart (padded to 16, worklist).
@@ -112,11 +128,18 @@ hipError_t launch_quad_worklist(const qgcm_desc *descs, uint32_t n, uint32_t max
     if ((e = hipMemsetAsync(worklist, 0xff, 4ull * items, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(counter, 0, 16, s)) != hipSuccess) return e;
     const int bs = 256, g = (int)((n + bs - 1) / bs);
-    if (n) hipLaunchKernelGGL(qwl_keys_kernel, dim3(g), dim3(bs), 0, s, descs, n, max_keys, seal, k_in, v_in, counts);
+    if (n) hipLaunchKernelGGL(qwl_keys_kernel, dim3(g), dim3(bs), 0, s, descs, n, max_keys, seal, k_in, v_in);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    if ((e = hipcub::DeviceRadixSort::SortPairs(cub_tmp, cub_bytes, k_in, k_out, v_in, v_out, (int)n, 0, 32, s)) !=
-        hipSuccess)
+    // only the bits a valid key can use, plus one so that excluded entries (all ones) sort last
+    int end_bit = kLenBits + 1;
+    while (end_bit < 32 && (1ull << (end_bit - kLenBits - 1)) < max_keys) ++end_bit;
+    if ((e = hipcub::DeviceRadixSort::SortPairs(cub_tmp, cub_bytes, k_in, k_out, v_in, v_out, (int)n, 0, end_bit,
+                                                s)) != hipSuccess)
         return e;
+    if (n) {
+        hipLaunchKernelGGL(qwl_first_kernel, dim3(g), dim3(bs), 0, s, k_out, n, start);
+        hipLaunchKernelGGL(qwl_count_kernel, dim3(g), dim3(bs), 0, s, k_out, n, start, counts);
+    }
     hipLaunchKernelGGL(qwl_scan_kernel, dim3(1), dim3(1024), 0, s, counts, max_keys, start, pstart);
     if (n) hipLaunchKernelGGL(qwl_scatter_kernel, dim3(g), dim3(bs), 0, s, k_out, v_out, n, start, pstart, worklist);
     *worklist_out = worklist;

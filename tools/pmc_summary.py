@@ -6,7 +6,7 @@ for f in glob.glob(os.path.join(root, "*", "**", "*counter_collection.csv"), rec
     v = tag.split("_")[0]
     acc = collections.defaultdict(list)
     for r in csv.DictReader(open(f)):
-        if "gcm_kernel" not in r["Kernel_Name"]: continue
+        if "gcm_" not in r["Kernel_Name"] or "kernel<" not in r["Kernel_Name"]: continue
         kind = "seal" if "<true" in r["Kernel_Name"] else "open"
         acc[(kind, r["Counter_Name"])].append(float(r["Counter_Value"]))
     for (kind, c), vals in acc.items():
