@@ -78,32 +78,34 @@ struct Keys {
 // column c = Te0[s_c.b0] ^ Te1[s_c+1.b1] ^ rot16(Te0[s_c+2.b2] ^ Te1[s_c+3.b3]) ^ rk_c.
 __device__ __forceinline__ void round_full(uint32_t &s0, uint32_t &s1, uint32_t &s2, uint32_t &s3, const Keys &k,
                                            int r, uint32_t lb) {
-    const uint32_t b0 = xor3(TE0(s2, 2), TE1(s3, 3), k.rr[4 * r + 0]);
-    const uint32_t b1 = xor3(TE0(s3, 2), TE1(s0, 3), k.rr[4 * r + 1]);
-    const uint32_t b2 = xor3(TE0(s0, 2), TE1(s1, 3), k.rr[4 * r + 2]);
-    const uint32_t b3 = xor3(TE0(s1, 2), TE1(s2, 3), k.rr[4 * r + 3]);
-    const uint32_t o0 = xor3(TE0(s0, 0), TE1(s1, 1), rot16(b0));
-    const uint32_t o1 = xor3(TE0(s1, 0), TE1(s2, 1), rot16(b1));
-    const uint32_t o2 = xor3(TE0(s2, 0), TE1(s3, 1), rot16(b2));
-    const uint32_t o3 = xor3(TE0(s3, 0), TE1(s0, 1), rot16(b3));
-    s0 = o0;
-    s1 = o1;
-    s2 = o2;
-    s3 = o3;
+    // All 16 lookups of the round are issued before the first combine (the asm is a scheduling
+    // fence): up to 16 LDS reads in flight per wave instead of 1-2 under the 64-VGPR budget.
+    // +2.9% on config 2 in an in-process A/B.
+    const uint32_t a0 = TE0(s2, 2), a1 = TE1(s3, 3), a2 = TE0(s3, 2), a3 = TE1(s0, 3);
+    const uint32_t a4 = TE0(s0, 2), a5 = TE1(s1, 3), a6 = TE0(s1, 2), a7 = TE1(s2, 3);
+    const uint32_t c0 = TE0(s0, 0), c1 = TE1(s1, 1), c2 = TE0(s1, 0), c3 = TE1(s2, 1);
+    const uint32_t c4 = TE0(s2, 0), c5 = TE1(s3, 1), c6 = TE0(s3, 0), c7 = TE1(s0, 1);
+    asm volatile("" ::: "memory");
+    s0 = xor3(c0, c1, rot16(xor3(a0, a1, k.rr[4 * r + 0])));
+    s1 = xor3(c2, c3, rot16(xor3(a2, a3, k.rr[4 * r + 1])));
+    s2 = xor3(c4, c5, rot16(xor3(a4, a5, k.rr[4 * r + 2])));
+    s3 = xor3(c6, c7, rot16(xor3(a6, a7, k.rr[4 * r + 3])));
 }
 
 // Final round (no MixColumns): S-box bytes are byte1/byte2 of Te0 and byte3 of Te1.
 __device__ __forceinline__ void round_last(uint32_t &s0, uint32_t &s1, uint32_t &s2, uint32_t &s3, const Keys &k,
                                            uint32_t lb) {
     const uint32_t *rk = k.rk + 56;
-    const uint32_t o0 = xor3(perm(TE0(s1, 1), TE0(s0, 0), 0x0c0c0501u), perm(TE1(s3, 3), TE0(s2, 2), 0x07020c0cu), rk[0]);
-    const uint32_t o1 = xor3(perm(TE0(s2, 1), TE0(s1, 0), 0x0c0c0501u), perm(TE1(s0, 3), TE0(s3, 2), 0x07020c0cu), rk[1]);
-    const uint32_t o2 = xor3(perm(TE0(s3, 1), TE0(s2, 0), 0x0c0c0501u), perm(TE1(s1, 3), TE0(s0, 2), 0x07020c0cu), rk[2]);
-    const uint32_t o3 = xor3(perm(TE0(s0, 1), TE0(s3, 0), 0x0c0c0501u), perm(TE1(s2, 3), TE0(s1, 2), 0x07020c0cu), rk[3]);
-    s0 = o0;
-    s1 = o1;
-    s2 = o2;
-    s3 = o3;
+    // 16 lookups in flight, then combine (as round_full; +1.1% in an in-process A/B)
+    const uint32_t a0 = TE0(s1, 1), a1 = TE0(s0, 0), a2 = TE1(s3, 3), a3 = TE0(s2, 2);
+    const uint32_t b0 = TE0(s2, 1), b1 = TE0(s1, 0), b2 = TE1(s0, 3), b3 = TE0(s3, 2);
+    const uint32_t c0 = TE0(s3, 1), c1 = TE0(s2, 0), c2 = TE1(s1, 3), c3 = TE0(s0, 2);
+    const uint32_t d0 = TE0(s0, 1), d1 = TE0(s3, 0), d2 = TE1(s2, 3), d3 = TE0(s1, 2);
+    asm volatile("" ::: "memory");
+    s0 = xor3(perm(a0, a1, 0x0c0c0501u), perm(a2, a3, 0x07020c0cu), rk[0]);
+    s1 = xor3(perm(b0, b1, 0x0c0c0501u), perm(b2, b3, 0x07020c0cu), rk[1]);
+    s2 = xor3(perm(c0, c1, 0x0c0c0501u), perm(c2, c3, 0x07020c0cu), rk[2]);
+    s3 = xor3(perm(d0, d1, 0x0c0c0501u), perm(d2, d3, 0x07020c0cu), rk[3]);
 }
 
 // Precompute rounds 1-2 for counter blocks nonce || (ctr_hi << 8 | low byte).  Round 1: only
@@ -286,6 +288,28 @@ __device__ __forceinline__ void read_tail(const uint8_t *data, uint32_t L, uint3
     n0 = __builtin_amdgcn_alignbyte(w5, w4, s);
     n1 = __builtin_amdgcn_alignbyte(w6, w5, s);
     n2 = __builtin_amdgcn_alignbyte(w7, w6, s);
+}
+
+// The two halves of read_tail: the quad kernel reads the nonce when the packet starts and the
+// received tag only when it compares it (4 fewer VGPRs live across the block loop).
+__device__ __forceinline__ void read_nonce(const uint8_t *data, uint32_t L, uint32_t &n0, uint32_t &n1, uint32_t &n2) {
+    const uint32_t s = L & 3u;
+    const uint32_t *t = reinterpret_cast<const uint32_t *>(data + (L & ~3u));
+    const uint32_t w4 = t[4], w5 = t[5], w6 = t[6];
+    const uint32_t w7 = load_bytes(data + (L & ~3u) + 28, s);
+    n0 = __builtin_amdgcn_alignbyte(w5, w4, s);
+    n1 = __builtin_amdgcn_alignbyte(w6, w5, s);
+    n2 = __builtin_amdgcn_alignbyte(w7, w6, s);
+}
+__device__ __forceinline__ void read_tag(const uint8_t *data, uint32_t L, uint32_t &g0, uint32_t &g1, uint32_t &g2,
+                                         uint32_t &g3) {
+    const uint32_t s = L & 3u;
+    const uint32_t *t = reinterpret_cast<const uint32_t *>(data + (L & ~3u));
+    const uint32_t w0 = t[0], w1 = t[1], w2 = t[2], w3 = t[3], w4 = t[4];
+    g0 = __builtin_amdgcn_alignbyte(w1, w0, s);
+    g1 = __builtin_amdgcn_alignbyte(w2, w1, s);
+    g2 = __builtin_amdgcn_alignbyte(w3, w2, s);
+    g3 = __builtin_amdgcn_alignbyte(w4, w3, s);
 }
 
 // Writes prefix (s = L%4 bytes, the end of the payload) followed by tag||nonce at
@@ -651,7 +675,7 @@ gcm_quad_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
             n1 = np[1];
             n2 = np[2];
         } else {
-            read_tail(data, L, g0, g1, g2, g3, n0, n1, n2);
+            read_nonce(data, L, n0, n1, n2);
         }
         const uint32_t nfull = L >> 4, r = L & 15u;
         const uint32_t d = nfull + (r ? 1u : 0u);  // data blocks incl. the partial one
@@ -825,6 +849,7 @@ gcm_quad_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
                 if (b.status) b.status[pkt] = 1;
             }
         } else {
+            read_tag(data, L, g0, g1, g2, g3);  // the tag is never written by Open
             const bool ok = ((t0 ^ g0) | (t1 ^ g1) | (t2 ^ g2) | (t3 ^ g3)) == 0;
             if (!ok) {
                 // Go 1.9 crypto/cipher gcm Open: zero the would-be plaintext on tag mismatch.
