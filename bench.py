@@ -27,6 +27,7 @@ from quantum_amd import batch, shard  # noqa: E402
 from quantum_amd.crypto import Context, derive_key  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, MI355X_MICROARCH.md "Chip-level parameters"
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r1_final", "traffic.json")  # tools/pmc_traffic.py
 SECRET = b"AES256Key-32Characters1234567890"
 SALT = bytes(range(32))
 AAD = bytes([10, 99, 0, 1])
@@ -60,6 +61,36 @@ def cpu_baseline(key: bytes, L: int, threads: int) -> dict:
             "sample": (f"{threads} threads x {per_thread} packets x {L} B seal+open, crypto/aes.go semantics "
                        f"(getrandom nonce/packet, in place, 4-B AAD) on OpenSSL EVP aes-256-gcm; "
                        f"1 thread: {rate1:.3f} GiB/s over {n1} packets")}
+
+
+def stream_copy_gbs(ctx, nbytes: int, dev, stream, reps: int = 5) -> float:
+    """Achievable HBM copy rate (read + write bytes / s) with libqgcm's in-repo stream kernel."""
+    from quantum_amd import _lib
+
+    nbytes &= ~15
+    src = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    dst = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    h = stream.cuda_stream
+    _lib.check(_lib.lib().qgcm_stream_copy(ctx.handle, dst.data_ptr(), src.data_ptr(), nbytes, h), "stream_copy")
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        _lib.lib().qgcm_stream_copy(ctx.handle, dst.data_ptr(), src.data_ptr(), nbytes, h)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    return 2 * nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
+
+
+def pmc_traffic(kind: str, N: int, L: int, stride: int):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC passes of this
+    command (profiles/r1_final/traffic.json), or None when they are absent or for another workload."""
+    try:
+        t = json.load(open(TRAFFIC_JSON))
+    except (OSError, ValueError):
+        return None, None
+    if t.get("workload") != {"packets": N, "payload_len": L, "slot_stride": stride} or kind not in t["kernels"]:
+        return None, None
+    return t["kernels"][kind]["hbm_bytes"], os.path.relpath(TRAFFIC_JSON, ROOT)
 
 
 def main() -> None:
@@ -132,6 +163,10 @@ def main() -> None:
     else:
         kname, kms, per_pkt = "open", open_ms, 2 * L + 32
     achieved = N * per_pkt / (kms * 1e-3) / 1e9
+    read_pkt = L + 16 if kname == "seal" else L + 32  # the HBM-read-only variant
+    achieved_read = N * read_pkt / (kms * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic(kname, N, L, stride)
+    copy_gbs = stream_copy_gbs(ctx, N * stride, dev, stream)  # after the timed region
 
     if rank == 0:
         line = {
@@ -151,8 +186,14 @@ def main() -> None:
                        "packets_per_gpu": N, "payload_len": L, "slot_stride": stride, "payload_align": 64,
                        "parallelism": f"replicas/shards x{world}, no collectives"},
             "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                         "bytes_per_packet": per_pkt, "kernel_ms": round(kms, 4)},
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic, "traffic_source": traffic_src,
+                         "traffic_over_algorithmic": round(traffic / (N * per_pkt), 3) if traffic else None,
+                         "bytes_per_packet": per_pkt, "kernel_ms": round(kms, 4),
+                         "achieved_read_only": round(achieved_read, 1),
+                         "copy_achievable": round(copy_gbs, 1),
+                         "frac_of_copy": round(achieved / copy_gbs, 4),
+                         "compute_bound_note": "LDS-bound T-table AES + comb GHASH (DESIGN.md 4.1)"},
             "kernels_ms": {"seal": round(seal_ms, 4), "open": round(open_ms, 4)},
             "status_ok": ok,
         }

@@ -152,6 +152,10 @@ void qgcm_host_free(void *p);
 /* Fills n*12 bytes of host memory from getrandom(2). */
 int qgcm_random_nonces(uint8_t *h_out, uint32_t n);
 
+/* ---- measurement: achievable HBM copy rate (reads + writes bytes) for the roofline ---- */
+/* 16-B aligned device buffers, bytes a multiple of 16.  Asynchronous on stream. */
+int qgcm_stream_copy(qgcm_ctx *ctx, void *d_dst, const void *d_src, uint64_t bytes, void *stream);
+
 /* ---- synthetic workload generator (bench/tests; BASELINE.json configs) ---- */
 /* Slot i at i*stride: [aad_word LE][payload L bytes of the splitmix64(seed_payload) stream at
  * byte offset i*L]; nonces[i*12..] = splitmix64(seed_nonce) stream at byte offset i*12. */

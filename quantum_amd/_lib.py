@@ -21,6 +21,7 @@ EXPORTS = (
     "qgcm_seal_one", "qgcm_open_one", "qgcm_seal_host", "qgcm_open_host",
     "qgcm_random_nonces", "qgcm_fill_uniform", "qgcm_host_alloc", "qgcm_host_free",
     "qgcm_coalescer_create", "qgcm_coalescer_destroy", "qgcm_coalescer_seal", "qgcm_coalescer_open",
+    "qgcm_stream_copy",
 )
 
 QGCM_OK = 0
@@ -84,6 +85,7 @@ def _bind(L: C.CDLL) -> None:
     L.qgcm_coalescer_seal.restype = lng
     L.qgcm_coalescer_open.argtypes = [vp, u32, vp, lng, vp, u32]
     L.qgcm_coalescer_open.restype = lng
+    L.qgcm_stream_copy.argtypes = [vp, vp, vp, u64, vp]
     L.qgcm_fill_uniform.argtypes = [vp, u64, u32, u32, u32, u64, vp, u64, vp]
 
 

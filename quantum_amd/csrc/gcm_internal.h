@@ -54,6 +54,7 @@ hipError_t launch_quad_worklist(const qgcm_desc *descs, uint32_t n, uint32_t max
                                 size_t ws_bytes, uint32_t **worklist_out, uint32_t **counter_out,
                                 uint32_t *n_items_out, hipStream_t s);
 hipError_t launch_packets(bool seal, int variant, const Batch &b, int grid, hipStream_t s);
+hipError_t launch_stream_copy(void *dst, const void *src, uint64_t bytes, int num_cus, hipStream_t s);
 // context accessors for the coalescer (coalescer.cpp), defined in qgcm_api.cpp
 int ctx_device(const qgcm_ctx *ctx);
 bool ctx_key_ready(qgcm_ctx *ctx, uint32_t key_idx);

@@ -1168,6 +1168,32 @@ __global__ void fill_uniform_kernel(uint8_t *arena, uint64_t stride, uint32_t n,
     }
 }
 
+// Streaming copy, 16 B per lane, grid-stride: the achievable-HBM reference the roofline is also
+// quoted against (SURVEY.md §8d "measure the achievable copy bandwidth with an in-repo stream kernel").
+__global__ void __launch_bounds__(256) stream_copy_kernel(uint4 *__restrict__ dst, const uint4 *__restrict__ src,
+                                                          uint64_t n16) {
+    const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + 3 * step < n16; i += 4 * step) {  // four 16-B loads in flight per lane
+        const uint4 a = src[i], b = src[i + step], c = src[i + 2 * step], d = src[i + 3 * step];
+        dst[i] = a;
+        dst[i + step] = b;
+        dst[i + 2 * step] = c;
+        dst[i + 3 * step] = d;
+    }
+    for (; i < n16; i += step) dst[i] = src[i];
+}
+
+hipError_t launch_stream_copy(void *dst, const void *src, uint64_t bytes, int num_cus, hipStream_t s) {
+    const uint64_t n16 = bytes / 16;
+    if (n16 == 0) return hipSuccess;
+    const uint64_t want = (n16 + 255) / 256;
+    const uint32_t g = (uint32_t)(want < (uint64_t)num_cus * 8 ? want : (uint64_t)num_cus * 8);
+    hipLaunchKernelGGL(stream_copy_kernel, dim3(g), dim3(256), 0, s, static_cast<uint4 *>(dst),
+                       static_cast<const uint4 *>(src), n16);
+    return hipGetLastError();
+}
+
 hipError_t launch_fill_uniform(uint8_t *arena, uint64_t stride, uint32_t n, uint32_t len, uint32_t aad_word,
                                uint64_t seed_payload, uint8_t *nonces, uint64_t seed_nonce, hipStream_t s) {
     const uint32_t groups = (4 + len + 3) / 4 + 3;

@@ -568,4 +568,11 @@ int qgcm_fill_uniform(uint8_t *d_arena, uint64_t stride, uint32_t n, uint32_t le
                                         (hipStream_t)stream));
 }
 
+int qgcm_stream_copy(qgcm_ctx *ctx, void *d_dst, const void *d_src, uint64_t bytes, void *stream) {
+    if (!ctx || (bytes && (!d_dst || !d_src)) || (bytes & 15) || ((uintptr_t)d_dst & 15) || ((uintptr_t)d_src & 15))
+        return QGCM_E_ARG;
+    if (hipSetDevice(ctx->device) != hipSuccess) return QGCM_E_HIP;
+    return hip_fail(launch_stream_copy(d_dst, d_src, bytes, ctx->num_cus, (hipStream_t)stream));
+}
+
 }  // extern "C"

@@ -3,7 +3,7 @@
 # run, never combined with other trace domains).  Usage: bash tools/profile.sh <tag> [bench args]
 set -u
 TAG=${1:-r1}; shift || true
-ARGS=${*:-"--steps 5 --warmup 2 --no-cpu-baseline"}
+ARGS=${*:-"--steps 20 --warmup 3 --no-cpu-baseline"}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
