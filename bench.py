@@ -43,6 +43,9 @@ def parse() -> argparse.Namespace:
     p.add_argument("--stride", type=int, default=0, help="slot stride (0 = smallest 64-B multiple)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
+    p.add_argument("--dist-backend", default="nccl", help="nccl (RCCL, default) or gloo (rehearsal)")
+    p.add_argument("--one-device", action="store_true",
+                   help="every rank on cuda:0 (multi-rank rehearsal on a 1-GPU box, gloo only)")
     return p.parse_args()
 
 
@@ -99,12 +102,18 @@ def main() -> None:
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    if args.one_device and args.dist_backend == "nccl" and world > 1:
+        raise SystemExit("--one-device needs --dist-backend gloo (RCCL allows one rank per GPU)")
+    local = 0 if args.one_device else local
+    torch.cuda.set_device(local)  # before the process group, so RCCL binds each rank to its GPU
+    dev = torch.device("cuda", local)
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", init_method="env://")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", init_method="env://", device_id=dev)
+        else:
+            dist.init_process_group(args.dist_backend, init_method="env://")
 
     N, L = args.packets, args.len
     stride = args.stride or batch.slot_stride(L, align=64)
@@ -149,7 +158,7 @@ def main() -> None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     # max over ranks, AND of the per-rank status (the only cross-rank traffic; no data collective)
-    elapsed, ok = shard.reduce_step_time(elapsed, ok, dist, dev)
+    elapsed, ok = shard.reduce_step_time(elapsed, ok, dist, dev if args.dist_backend == "nccl" else None)
 
     seal_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
     open_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps

@@ -152,6 +152,21 @@ void qgcm_host_free(void *p);
 /* Fills n*12 bytes of host memory from getrandom(2). */
 int qgcm_random_nonces(uint8_t *h_out, uint32_t n);
 
+/* ---- snappy block format: the compression plugin (plugin/compression.go) ---- */
+/* Host codec (C++, from the published format; golang/snappy is not in the reference).  Encode output
+ * is a valid snappy stream (not golang/snappy's exact bytes); Decode accepts every valid stream and
+ * returns -1 on malformed input (compression.go:22-25 decode error). */
+size_t qgcm_snappy_max_compressed_length(size_t n);
+long qgcm_snappy_compress(const uint8_t *src, size_t n, uint8_t *dst, size_t cap);
+long qgcm_snappy_uncompressed_length(const uint8_t *src, size_t n);
+long qgcm_snappy_uncompress(const uint8_t *src, size_t n, uint8_t *dst, size_t cap);
+/* Payload.Raw slots at i*stride: packet i = lens[i] bytes at slot+4, (de)compressed in place,
+ * lens[i] updated (compression.go Apply, Outgoing / Incoming), `threads` host workers.  Returns the
+ * number of packets that failed (untouched; status[i] = 0) or -1. */
+int qgcm_snappy_compress_slots(uint8_t *arena, uint64_t stride, uint32_t n, uint32_t *lens, int threads);
+int qgcm_snappy_uncompress_slots(uint8_t *arena, uint64_t stride, uint32_t n, uint32_t *lens,
+                                 uint8_t *status, int threads);
+
 /* ---- measurement: achievable HBM copy rate (reads + writes bytes) for the roofline ---- */
 /* 16-B aligned device buffers, bytes a multiple of 16.  Asynchronous on stream. */
 int qgcm_stream_copy(qgcm_ctx *ctx, void *d_dst, const void *d_src, uint64_t bytes, void *stream);

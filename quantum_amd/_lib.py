@@ -22,6 +22,8 @@ EXPORTS = (
     "qgcm_random_nonces", "qgcm_fill_uniform", "qgcm_host_alloc", "qgcm_host_free",
     "qgcm_coalescer_create", "qgcm_coalescer_destroy", "qgcm_coalescer_seal", "qgcm_coalescer_open",
     "qgcm_stream_copy",
+    "qgcm_snappy_max_compressed_length", "qgcm_snappy_compress", "qgcm_snappy_uncompressed_length",
+    "qgcm_snappy_uncompress", "qgcm_snappy_compress_slots", "qgcm_snappy_uncompress_slots",
 )
 
 QGCM_OK = 0
@@ -86,6 +88,17 @@ def _bind(L: C.CDLL) -> None:
     L.qgcm_coalescer_open.argtypes = [vp, u32, vp, lng, vp, u32]
     L.qgcm_coalescer_open.restype = lng
     L.qgcm_stream_copy.argtypes = [vp, vp, vp, u64, vp]
+    sz = C.c_size_t
+    L.qgcm_snappy_max_compressed_length.argtypes = [sz]
+    L.qgcm_snappy_max_compressed_length.restype = sz
+    L.qgcm_snappy_compress.argtypes = [vp, sz, vp, sz]
+    L.qgcm_snappy_compress.restype = lng
+    L.qgcm_snappy_uncompressed_length.argtypes = [vp, sz]
+    L.qgcm_snappy_uncompressed_length.restype = lng
+    L.qgcm_snappy_uncompress.argtypes = [vp, sz, vp, sz]
+    L.qgcm_snappy_uncompress.restype = lng
+    L.qgcm_snappy_compress_slots.argtypes = [vp, u64, u32, vp, C.c_int]
+    L.qgcm_snappy_uncompress_slots.argtypes = [vp, u64, u32, vp, vp, C.c_int]
     L.qgcm_fill_uniform.argtypes = [vp, u64, u32, u32, u32, u64, vp, u64, vp]
 
 

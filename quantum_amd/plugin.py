@@ -7,6 +7,7 @@ plugin/plugin.go:60-81   Plugins / Sorter (sort by Order)
 plugin/plugin.go:84-94   New(pluginType, cfg)
 plugin/encryption.go     Encryption.Apply (per packet) -- here backed by the gfx950 kernels
 plugin/mock.go           Mock (identity)
+plugin/compression.go    Compression.Apply (per packet) -- snappy block format, libqgcm host codec
 
 Apply keeps Go's contract: returns (payload, mapping, ok); ok=False means "drop the packet".
 """
@@ -79,6 +80,54 @@ class Encryption(Plugin):
         return EncryptionPluginOrder
 
 
+def _snappy(fn: str, data: bytes, cap: int) -> bytes | None:
+    import ctypes as C
+
+    from . import _lib
+
+    src = C.create_string_buffer(data, len(data)) if data else None
+    dst = C.create_string_buffer(max(cap, 1))
+    n = getattr(_lib.lib(), fn)(src, len(data), dst, cap)
+    return None if n < 0 else dst.raw[:n]
+
+
+class Compression(Plugin):
+    """plugin/compression.go:11-70 (snappy Encode/Decode of Payload.Packet, copied into Raw[4:])."""
+
+    def __init__(self, cfg=None):
+        self.cfg = cfg
+
+    def Apply(self, direction: int, payload: common.Payload, mapping: common.Mapping):
+        from . import _lib
+
+        if not common.StringInSlice(CompressionPlugin, mapping.SupportedPlugins):  # :31-33
+            return payload, mapping, True
+        packet = bytes(payload.Packet)
+        if direction == Incoming:  # :36-43 decompress; a decode error drops the packet
+            n = _lib.lib().qgcm_snappy_uncompressed_length(packet, len(packet)) if packet else -1
+            out = _snappy("qgcm_snappy_uncompress", packet, n) if n >= 0 else None
+        elif direction == Outgoing:  # :44-51 compress
+            out = _snappy("qgcm_snappy_compress", packet, _lib.lib().qgcm_snappy_max_compressed_length(len(packet)))
+        else:
+            return payload, mapping, True
+        if out is None:
+            return payload, mapping, False
+        room = len(payload.Raw) - common.PacketStart
+        payload.Raw[common.PacketStart:common.PacketStart + min(len(out), room)] = out[:room]  # Go copy()
+        payload.Packet = common._View(payload.Raw, common.PacketStart, common.PacketStart + len(out))
+        payload.Length = common.HeaderSize + len(out)
+        return payload, mapping, True
+
+    def Close(self):
+        return None
+
+    def Name(self) -> str:
+        return CompressionPlugin
+
+    def Order(self) -> int:
+        return CompressionPluginOrder
+
+
 class Mock(Plugin):
     """plugin/mock.go:11-36."""
 
@@ -110,5 +159,5 @@ def New(pluginType: str, cfg=None):
     if pluginType == MockPlugin:
         return Mock(cfg), None
     if pluginType == CompressionPlugin:
-        return None, ValueError("compression plugin is outside this build's scope (SURVEY.md s8f rank 3)")
+        return Compression(cfg), None
     return None, ValueError("specified plugin is not supported")
