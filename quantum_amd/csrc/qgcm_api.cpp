@@ -27,6 +27,7 @@ struct qgcm_ctx {
     uint32_t max_keys = 0;
     int uniform_variant = kVariantUniform;  // kernel variant for single-key batches (QGCM_VARIANT)
     int desc_variant = kVariantDescQuad;    // kernel variant for descriptor batches (QGCM_DESC_VARIANT)
+    int wgs_per_cu_override = 0;            // persistent-grid workgroups per CU (QGCM_WGS_PER_CU, tuning)
     uint32_t *d_rk = nullptr;
     uint4 *d_gh = nullptr;
     uint32_t *d_te = nullptr;
@@ -112,7 +113,9 @@ int grid_for(const qgcm_ctx *ctx, uint32_t n_items, int variant) {
     const uint32_t tiles = variant_quad(variant) ? (n_items + 15) / 16 : n_items / 64;
     const uint32_t wgs = (tiles + waves - 1) / waves;
     // persistent grid: the resident workgroups (each fills its own LDS tables once)
-    const uint32_t cap = (uint32_t)ctx->num_cus * (uint32_t)variant_wgs_per_cu(variant);
+    const uint32_t per_cu = ctx->wgs_per_cu_override > 0 ? (uint32_t)ctx->wgs_per_cu_override
+                                                         : (uint32_t)variant_wgs_per_cu(variant);
+    const uint32_t cap = (uint32_t)ctx->num_cus * per_cu;
     return (int)(wgs < cap ? (wgs ? wgs : 1) : cap);
 }
 
@@ -299,6 +302,7 @@ qgcm_ctx *qgcm_create(int device, uint32_t max_keys, char *err, int errlen) {
         const int iv = atoi(v);
         if (iv >= 0 && iv < kNumVariants) ctx->uniform_variant = iv;
     }
+    if (const char *v = getenv("QGCM_WGS_PER_CU")) ctx->wgs_per_cu_override = atoi(v);
     if (const char *v = getenv("QGCM_DESC_VARIANT")) {
         const int iv = atoi(v);
         if (iv == kVariantGeneral || (iv >= 0 && iv < kNumVariants && variant_desc(iv))) ctx->desc_variant = iv;
