@@ -164,8 +164,26 @@ long qgcm_snappy_uncompress(const uint8_t *src, size_t n, uint8_t *dst, size_t c
  * lens[i] updated (compression.go Apply, Outgoing / Incoming), `threads` host workers.  Returns the
  * number of packets that failed (untouched; status[i] = 0) or -1. */
 int qgcm_snappy_compress_slots(uint8_t *arena, uint64_t stride, uint32_t n, uint32_t *lens, int threads);
+/* As qgcm_snappy_compress_slots, but a packet also fails when its compressed form exceeds `limit`
+ * bytes (room left for the seal's tag and nonce); status[i] = 1 ok / 0 failed (may be NULL). */
+int qgcm_snappy_compress_slots_limit(uint8_t *arena, uint64_t stride, uint32_t n, uint32_t *lens, uint64_t limit,
+                                     uint8_t *status, int threads);
 int qgcm_snappy_uncompress_slots(uint8_t *arena, uint64_t stride, uint32_t n, uint32_t *lens,
                                  uint8_t *status, int threads);
+
+/* ---- Compression + Encryption chain (BASELINE config 5) ---- */
+/* Host batches in the order main.go:50-51 sorts the plugins: outgoing compression.go then
+ * encryption.go Apply, incoming the reverse.  Slot i at i*stride holds [aad 4][packet lens[i] B].
+ * compress_seal: snappy-compress each packet in place, then seal it (lens[i] <- compressed + 28).
+ * open_uncompress: open each sealed packet, then uncompress (lens[i] <- plaintext length).
+ * Chunks pipeline the host codec (`threads` workers) with PCIe copies and the device kernels.
+ * Returns the number of failed packets (status 0: codec error, no room for the tag and nonce, or
+ * failed authentication -- plaintext zeroed as in qgcm_open_batch), or a negative error. */
+int qgcm_compress_seal_host(qgcm_ctx *ctx, uint8_t *h_arena, uint64_t stride, uint32_t n, uint32_t *lens,
+                            uint32_t key_idx, const uint8_t *h_nonces, uint32_t aad_len, int threads,
+                            uint8_t *h_status);
+int qgcm_open_uncompress_host(qgcm_ctx *ctx, uint8_t *h_arena, uint64_t stride, uint32_t n, uint32_t *lens,
+                              uint32_t key_idx, uint32_t aad_len, int threads, uint8_t *h_status);
 
 /* ---- measurement: achievable HBM copy rate (reads + writes bytes) for the roofline ---- */
 /* 16-B aligned device buffers, bytes a multiple of 16.  Asynchronous on stream. */

@@ -24,6 +24,7 @@ EXPORTS = (
     "qgcm_stream_copy",
     "qgcm_snappy_max_compressed_length", "qgcm_snappy_compress", "qgcm_snappy_uncompressed_length",
     "qgcm_snappy_uncompress", "qgcm_snappy_compress_slots", "qgcm_snappy_uncompress_slots",
+    "qgcm_snappy_compress_slots_limit", "qgcm_compress_seal_host", "qgcm_open_uncompress_host",
 )
 
 QGCM_OK = 0
@@ -100,6 +101,9 @@ def _bind(L: C.CDLL) -> None:
     L.qgcm_snappy_compress_slots.argtypes = [vp, u64, u32, vp, C.c_int]
     L.qgcm_snappy_uncompress_slots.argtypes = [vp, u64, u32, vp, vp, C.c_int]
     L.qgcm_fill_uniform.argtypes = [vp, u64, u32, u32, u32, u64, vp, u64, vp]
+    L.qgcm_snappy_compress_slots_limit.argtypes = [vp, u64, u32, vp, u64, vp, C.c_int]
+    L.qgcm_compress_seal_host.argtypes = [vp, vp, u64, u32, vp, u32, vp, u32, C.c_int, vp]
+    L.qgcm_open_uncompress_host.argtypes = [vp, vp, u64, u32, vp, u32, u32, C.c_int, vp]
 
 
 def lib() -> C.CDLL:

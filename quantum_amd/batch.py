@@ -76,3 +76,21 @@ def fill_uniform(arena: torch.Tensor, stride: int, n: int, length: int, aad_word
 def host_ptr(buf: bytearray) -> tuple[int, object]:
     arr = (C.c_uint8 * len(buf)).from_buffer(buf)
     return C.addressof(arr), arr
+
+
+def compress_seal_host(ctx: Context, arena_ptr: int, stride: int, n: int, lens, key_idx: int, nonces_ptr: int | None,
+                       aad_len: int = AAD_LEN, threads: int = 16, status_ptr: int | None = None) -> int:
+    """Outgoing plugin chain on host slots (main.go:50-51 order): snappy-compress then seal, pipelined
+    with the device.  `lens` is a numpy uint32 array, updated in place to the sealed lengths.
+    Returns the number of packets that failed (status 0)."""
+    return _lib.check(_lib.lib().qgcm_compress_seal_host(ctx.handle, arena_ptr, stride, n, lens.ctypes.data, key_idx,
+                                                         nonces_ptr, aad_len, threads, status_ptr),
+                      "qgcm_compress_seal_host")
+
+
+def open_uncompress_host(ctx: Context, arena_ptr: int, stride: int, n: int, lens, key_idx: int,
+                         aad_len: int = AAD_LEN, threads: int = 16, status_ptr: int | None = None) -> int:
+    """Incoming plugin chain on host slots: open then snappy-uncompress; `lens` updated in place."""
+    return _lib.check(_lib.lib().qgcm_open_uncompress_host(ctx.handle, arena_ptr, stride, n, lens.ctypes.data, key_idx,
+                                                           aad_len, threads, status_ptr),
+                      "qgcm_open_uncompress_host")

@@ -57,15 +57,22 @@ class Context:
             self._next += 1
             return k
 
+    def _reserve(self, end: int) -> None:
+        """Slots set explicitly are never handed out again by alloc_slot."""
+        with self._mu:
+            self._next = max(self._next, end)
+
     def set_key(self, slot: int, key: bytes) -> None:
         if len(key) != keyLength:
             raise ValueError("AES-256 key must be 32 bytes")
         _lib.check(_lib.lib().qgcm_set_key(self.handle, slot, key), "qgcm_set_key")
+        self._reserve(slot + 1)
 
     def set_keys(self, first: int, keys: bytes) -> None:
         if len(keys) % keyLength:
             raise ValueError("keys must be a multiple of 32 bytes")
         _lib.check(_lib.lib().qgcm_set_keys(self.handle, first, len(keys) // keyLength, keys), "qgcm_set_keys")
+        self._reserve(first + len(keys) // keyLength)
 
     def close(self) -> None:
         if self.handle:

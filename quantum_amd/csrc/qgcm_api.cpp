@@ -10,6 +10,10 @@
 #include <string.h>
 #include <sys/random.h>
 
+#include <atomic>
+#include <memory>
+#include <thread>
+#include <algorithm>
 #include <mutex>
 #include <vector>
 
@@ -56,6 +60,8 @@ struct qgcm_ctx {
     size_t ring_cap = 0;
     uint8_t *h_stat = nullptr;  // pinned status bytes of the whole host batch
     size_t hstat_cap = 0;
+    qgcm_desc *h_desc = nullptr;  // pinned descriptor staging of the chained (snappy + GCM) path
+    size_t hdesc_cap = 0;
 
     // orders reuse of the descriptor workspace across streams (guarded by ws_mu)
     hipEvent_t ws_done = nullptr;
@@ -347,6 +353,7 @@ void qgcm_destroy(qgcm_ctx *ctx) {
     if (ctx->io_stream) hipStreamDestroy(ctx->io_stream);
     hipFree(ctx->d_ring);
     if (ctx->h_stat) hipHostFree(ctx->h_stat);
+    if (ctx->h_desc) hipHostFree(ctx->h_desc);
     for (hipStream_t p : ctx->pipe)
         if (p) hipStreamDestroy(p);
     if (ctx->ws_done) hipEventDestroy(ctx->ws_done);
@@ -530,6 +537,199 @@ static int run_host(qgcm_ctx *ctx, bool seal, uint8_t *h_arena, uint64_t stride,
     for (uint32_t i = 0; i < n; ++i) bad += ctx->h_stat[i] != 1;
     if (h_status) memcpy(h_status, ctx->h_stat, n);
     return bad;
+}
+
+// Compression + Encryption chain over host batches (BASELINE config 5; plugin order main.go:50-51:
+// outgoing compression.go then encryption.go, incoming the reverse).  Chunks of ~32 MiB of slots go
+// through three streams as in run_host.  A pool of `threads` codec workers runs for the whole call,
+// taking 256-packet items in chunk order: on seal it compresses ahead and the main thread enqueues a
+// chunk (H2D, seal, D2H) as soon as its items are done; on open the main thread releases a chunk to
+// the workers once its D2H has landed.  Codec, PCIe and the device overlap.  Packet lengths differ
+// after compression, so each chunk is a descriptor batch (one key).
+namespace {
+
+struct CodecPool {
+    static constexpr uint32_t kItem = 256;  // packets per work item
+    std::atomic<uint64_t> next{0};          // next item to claim
+    std::atomic<uint64_t> limit{0};         // items released to the workers (open)
+    std::atomic<bool> stop{false};
+    std::unique_ptr<std::atomic<uint32_t>[]> done;  // finished items per chunk
+    std::vector<std::thread> workers;
+
+    void wait_chunk(uint64_t c, uint32_t items) const {
+        while (done[c].load(std::memory_order_acquire) < items) std::this_thread::yield();
+    }
+    void join() {
+        stop = true;
+        for (auto &t : workers) t.join();
+        workers.clear();
+    }
+    ~CodecPool() {
+        if (!workers.empty()) join();
+    }
+};
+
+}  // namespace
+
+static int run_host_chain(qgcm_ctx *ctx, bool seal, uint8_t *h_arena, uint64_t stride, uint32_t n, uint32_t *lens,
+                          uint32_t key_idx, const uint8_t *h_nonces, uint32_t aad_len, int threads,
+                          uint8_t *h_status) {
+    if (!ctx || (n && (!h_arena || !lens)) || aad_len > 4 || (stride & 3) || stride < 4 + QGCM_OVERHEAD)
+        return QGCM_E_ARG;
+    if (!key_ok(ctx, key_idx)) return QGCM_E_KEY;
+    if (n == 0) return 0;
+    std::lock_guard<std::mutex> g(ctx->io_mu);
+    if (hipSetDevice(ctx->device) != hipSuccess) return QGCM_E_HIP;
+    auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
+    uint64_t cpk = (kPipeChunk / stride) & ~255ull;  // whole codec items per chunk
+    if (cpk < 256) cpk = 256;
+    if (cpk > n) cpk = n;
+    const uint64_t nchunks = (n + cpk - 1) / cpk;
+    const bool non = seal && h_nonces;
+    const uint64_t off_non = al(cpk * stride), off_st = off_non + (non ? al(12 * cpk) : 0);
+    const uint64_t off_desc = off_st + al(cpk), slot = off_desc + al(16 * cpk);
+    const int nslots = nchunks < (uint64_t)kPipeStreams ? (int)nchunks : kPipeStreams;
+    if (slot * nslots > ctx->ring_cap) {
+        if (ctx->d_ring) hipFree(ctx->d_ring);
+        ctx->d_ring = nullptr;
+        ctx->ring_cap = 0;
+        if (hipMalloc(&ctx->d_ring, slot * nslots) != hipSuccess) return QGCM_E_NOMEM;
+        ctx->ring_cap = slot * nslots;
+    }
+    if (n > ctx->hstat_cap) {
+        if (ctx->h_stat) hipHostFree(ctx->h_stat);
+        ctx->h_stat = nullptr;
+        ctx->hstat_cap = 0;
+        if (hipHostMalloc(&ctx->h_stat, n, hipHostMallocDefault) != hipSuccess) return QGCM_E_NOMEM;
+        ctx->hstat_cap = n;
+    }
+    if (cpk * nslots > ctx->hdesc_cap) {
+        if (ctx->h_desc) hipHostFree(ctx->h_desc);
+        ctx->h_desc = nullptr;
+        ctx->hdesc_cap = 0;
+        if (hipHostMalloc(reinterpret_cast<void **>(&ctx->h_desc), cpk * nslots * sizeof(qgcm_desc),
+                          hipHostMallocDefault) != hipSuccess)
+            return QGCM_E_NOMEM;
+        ctx->hdesc_cap = cpk * nslots;
+    }
+    std::vector<uint8_t> codec(n, 1);  // host codec status per packet (device status: ctx->h_stat)
+    const uint32_t max_plain = (uint32_t)(stride - 4 - QGCM_OVERHEAD);
+    const uint32_t per_chunk = (uint32_t)((cpk + CodecPool::kItem - 1) / CodecPool::kItem);
+    const uint64_t total_items = (n + CodecPool::kItem - 1) / CodecPool::kItem;
+    auto items_in = [&](uint64_t c) {
+        const uint64_t c0 = c * cpk, cn = (n - c0) < cpk ? (n - c0) : cpk;
+        return (uint32_t)((cn + CodecPool::kItem - 1) / CodecPool::kItem);
+    };
+    CodecPool pool;
+    pool.done.reset(new std::atomic<uint32_t>[nchunks]);
+    for (uint64_t c = 0; c < nchunks; ++c) pool.done[c] = 0;
+    if (seal) pool.limit = total_items;
+    auto work = [&] {
+        std::vector<uint8_t> tmp(std::max<uint64_t>(stride, qgcm_snappy_max_compressed_length(stride)));
+        for (;;) {
+            uint64_t it = pool.next.load();
+            for (;;) {
+                if (it >= total_items || pool.stop) return;
+                if (it < pool.limit.load(std::memory_order_acquire)) {
+                    if (pool.next.compare_exchange_weak(it, it + 1)) break;
+                } else {
+                    std::this_thread::yield();
+                    it = pool.next.load();
+                }
+            }
+            const uint64_t i0 = it * CodecPool::kItem, i1 = std::min<uint64_t>(n, i0 + CodecPool::kItem);
+            for (uint64_t i = i0; i < i1; ++i) {
+                uint8_t *pkt = h_arena + i * stride + 4;
+                if (seal) {
+                    // compression.go:44-51; a packet whose compressed form leaves no room for the
+                    // tag and nonce fails, untouched
+                    const long c = lens[i] <= max_plain ? qgcm_snappy_compress(pkt, lens[i], tmp.data(), tmp.size())
+                                                        : -1;
+                    if (c < 0 || (uint64_t)c > max_plain) {
+                        codec[i] = 0;
+                    } else {
+                        memcpy(pkt, tmp.data(), (size_t)c);
+                        lens[i] = (uint32_t)c;
+                    }
+                } else if (ctx->h_stat[i] == 1) {  // compression.go:35-43, on authentic packets only
+                    const uint32_t sl = lens[i] - QGCM_OVERHEAD;
+                    const long u = qgcm_snappy_uncompress(pkt, sl, tmp.data(), stride - 4);
+                    if (u < 0) {
+                        codec[i] = 0;
+                        lens[i] = sl;
+                    } else {
+                        memcpy(pkt, tmp.data(), (size_t)u);
+                        lens[i] = (uint32_t)u;
+                    }
+                }
+            }
+            pool.done[it / per_chunk].fetch_add(1, std::memory_order_release);
+        }
+    };
+    const int nt = std::max(1, std::min(threads, 256));
+    for (int t = 0; t < nt; ++t) pool.workers.emplace_back(work);
+    int rc = QGCM_OK;
+    for (uint64_t c = 0; c < nchunks && rc == QGCM_OK; ++c) {
+        const int k = (int)(c % nslots);
+        hipStream_t s = ctx->pipe[k];
+        uint8_t *d = ctx->d_ring + k * slot, *d_non = d + off_non, *d_st = d + off_st;
+        qgcm_desc *d_desc = reinterpret_cast<qgcm_desc *>(d + off_desc);
+        qgcm_desc *hd = ctx->h_desc + k * cpk;
+        const uint64_t c0 = c * cpk, cn = (n - c0) < cpk ? (n - c0) : cpk;
+        uint8_t *h = h_arena + c0 * stride;
+        // chunk c - nslots used this stream's staging: wait for it to land (open: then its packets
+        // can be decompressed)
+        if (c >= (uint64_t)nslots) {
+            if (hipStreamSynchronize(s) != hipSuccess) {
+                rc = QGCM_E_HIP;
+                break;
+            }
+            if (!seal) pool.limit.store((c - nslots + 1) * per_chunk, std::memory_order_release);
+        }
+        if (seal) pool.wait_chunk(c, items_in(c));
+        for (uint64_t i = 0; i < cn; ++i) {
+            const bool ok = !seal || codec[c0 + i];
+            hd[i] = qgcm_desc{i * stride, ok ? lens[c0 + i] : QGCM_MAX_PAYLOAD, key_idx};
+        }
+        if (hipMemcpyAsync(d, h, cn * stride, hipMemcpyHostToDevice, s) != hipSuccess ||
+            hipMemcpyAsync(d_desc, hd, cn * sizeof(qgcm_desc), hipMemcpyHostToDevice, s) != hipSuccess ||
+            (non && hipMemcpyAsync(d_non, h_nonces + 12 * c0, 12 * cn, hipMemcpyHostToDevice, s) != hipSuccess)) {
+            rc = QGCM_E_HIP;
+            break;
+        }
+        rc = run_descs(ctx, seal, d, d_desc, (uint32_t)cn, non ? d_non : nullptr, aad_len, d_st, s);
+        if (rc == QGCM_OK && (hipMemcpyAsync(h, d, cn * stride, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                              hipMemcpyAsync(ctx->h_stat + c0, d_st, cn, hipMemcpyDeviceToHost, s) != hipSuccess))
+            rc = QGCM_E_HIP;
+    }
+    for (int k = 0; k < nslots; ++k)
+        if (hipStreamSynchronize(ctx->pipe[k]) != hipSuccess) rc = QGCM_E_HIP;
+    if (rc != QGCM_OK) {
+        pool.join();
+        return rc;
+    }
+    if (!seal) pool.limit.store(total_items, std::memory_order_release);
+    for (uint64_t c = 0; c < nchunks; ++c) pool.wait_chunk(c, items_in(c));
+    pool.join();
+    int bad = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const bool ok = ctx->h_stat[i] == 1 && codec[i];
+        if (seal && ok) lens[i] += QGCM_OVERHEAD;
+        bad += !ok;
+        if (h_status) h_status[i] = ok ? 1 : 0;
+    }
+    return bad;
+}
+
+int qgcm_compress_seal_host(qgcm_ctx *ctx, uint8_t *h_arena, uint64_t stride, uint32_t n, uint32_t *lens,
+                            uint32_t key_idx, const uint8_t *h_nonces, uint32_t aad_len, int threads,
+                            uint8_t *h_status) {
+    return run_host_chain(ctx, true, h_arena, stride, n, lens, key_idx, h_nonces, aad_len, threads, h_status);
+}
+
+int qgcm_open_uncompress_host(qgcm_ctx *ctx, uint8_t *h_arena, uint64_t stride, uint32_t n, uint32_t *lens,
+                              uint32_t key_idx, uint32_t aad_len, int threads, uint8_t *h_status) {
+    return run_host_chain(ctx, false, h_arena, stride, n, lens, key_idx, nullptr, aad_len, threads, h_status);
 }
 
 void *qgcm_host_alloc(size_t bytes) {

@@ -196,8 +196,10 @@ long qgcm_snappy_uncompress(const uint8_t *src, size_t n, uint8_t *dst, size_t c
 // at slot+4) in place, lens[i] <- compressed length (plugin/compression.go:39-47).  `threads`
 // workers over the batch.  Returns the number of packets that did not fit their slot (left as is,
 // lens[i] unchanged) or -1.
-int qgcm_snappy_compress_slots(uint8_t *arena, uint64_t stride, uint32_t n, uint32_t *lens, int threads) {
+int qgcm_snappy_compress_slots_limit(uint8_t *arena, uint64_t stride, uint32_t n, uint32_t *lens, uint64_t limit,
+                                     uint8_t *status, int threads) {
     if ((n && (!arena || !lens)) || stride < 4) return -1;
+    if (limit > stride - 4) limit = stride - 4;
     std::atomic<uint32_t> next{0};
     std::atomic<int> bad{0};
     auto work = [&] {
@@ -208,18 +210,20 @@ int qgcm_snappy_compress_slots(uint8_t *arena, uint64_t stride, uint32_t n, uint
             for (uint32_t i = i0; i < std::min(n, i0 + 256); ++i) {
                 uint8_t *pkt = arena + (uint64_t)i * stride + 4;
                 const size_t L = lens[i];
+                if (status) status[i] = 0;
                 if (L + 4 > stride) {
                     ++bad;
                     continue;
                 }
                 tmp.resize(qgcm_snappy_max_compressed_length(L));
                 const long c = qgcm_snappy_compress(pkt, L, tmp.data(), tmp.size());
-                if (c < 0 || (uint64_t)c + 4 > stride) {
+                if (c < 0 || (uint64_t)c > limit) {
                     ++bad;
                     continue;
                 }
                 memcpy(pkt, tmp.data(), (size_t)c);
                 lens[i] = (uint32_t)c;
+                if (status) status[i] = 1;
             }
         }
     };
@@ -229,6 +233,10 @@ int qgcm_snappy_compress_slots(uint8_t *arena, uint64_t stride, uint32_t n, uint
     work();
     for (auto &th : pool) th.join();
     return bad.load();
+}
+
+int qgcm_snappy_compress_slots(uint8_t *arena, uint64_t stride, uint32_t n, uint32_t *lens, int threads) {
+    return qgcm_snappy_compress_slots_limit(arena, stride, n, lens, stride, nullptr, threads);
 }
 
 // Inverse of qgcm_snappy_compress_slots (plugin/compression.go:35-38,41-47 Incoming): a packet that

@@ -5,6 +5,10 @@
            device-resident descriptor batches (qgcm_seal_batch / qgcm_open_batch).
   e2e      config 2 from HOST memory: pinned staging + H2D + kernels + D2H (qgcm_seal_host /
            qgcm_open_host), the PCIe-inclusive rate DESIGN.md reports (never bench.py's value).
+  config5  compression + encryption chain on 2^20 x 1350 B host packets (compressible mix: each
+           packet's first half seeded random bytes, second half a repeated 48-B HTTP request line):
+           snappy (host C++ codec, `threads` workers) -> seal, then open -> uncompress, pipelined
+           with PCIe copies and the device (qgcm_compress_seal_host / qgcm_open_uncompress_host).
 
 Prints one JSON line per config.  Usage: python tools/bench_configs.py [config3] [e2e]
 """
@@ -134,8 +138,62 @@ def e2e(reps: int = 3, pinned: bool = True) -> dict:
             "matches_device_path": same, "status_ok": rc == 0}
 
 
+def config5(reps: int = 3, threads: int = 16) -> dict:
+    N, L, stride = 1 << 20, 1350, 1472  # stride = common.MaxPacketLength (the Payload.Raw buffer)
+    ctx = Context(device=0, max_keys=4)
+    key = derive_key(b"AES256Key-32Characters1234567890", bytes(range(32)))
+    ctx.set_key(0, key)
+    L_ = _lib.lib()
+    a_ptr, n_ptr = L_.qgcm_host_alloc(N * stride), L_.qgcm_host_alloc(12 * N)
+    host = np.frombuffer((C.c_uint8 * (N * stride)).from_address(a_ptr), np.uint8).reshape(N, stride)
+    nonces = np.frombuffer((C.c_uint8 * (12 * N)).from_address(n_ptr), np.uint8)
+    rng = np.random.default_rng(0x5EED0005)
+    host[:, :4] = np.frombuffer(bytes([10, 99, 0, 1]), np.uint8)
+    half = L // 2
+    host[:, 4:4 + half] = rng.integers(0, 256, (N, half), dtype=np.uint8)
+    line = np.frombuffer(b"GET /quantum/v1/peers HTTP/1.1\r\nHost: 10.99.0.1\r\n", np.uint8)
+    host[:, 4 + half:4 + L] = np.tile(line, (L - half) // len(line) + 1)[:L - half]
+    nonces[:] = rng.integers(0, 256, 12 * N, dtype=np.uint8)
+    plain = host[:, :4 + L].copy()
+    lens = np.full(N, L, np.uint32)
+    # codec alone on the host (the same workers), for the bottleneck breakdown
+    tmp = host.copy()
+    tl = np.full(N, L, np.uint32)
+    c0 = time.perf_counter()
+    L_.qgcm_snappy_compress_slots(tmp.ctypes.data, stride, N, tl.ctypes.data, threads)
+    c1 = time.perf_counter()
+    ratio = float(tl.sum()) / (N * L)
+    L_.qgcm_snappy_uncompress_slots(tmp.ctypes.data, stride, N, tl.ctypes.data, None, threads)
+    c2 = time.perf_counter()
+    codec_ok = bool(np.array_equal(tmp[:, :4 + L], plain))
+    del tmp
+    ts, to, bad = [], [], 0
+    for _ in range(reps):
+        lens[:] = L
+        t0 = time.perf_counter()
+        bad += batch.compress_seal_host(ctx, a_ptr, stride, N, lens, 0, n_ptr, threads=threads)
+        t1 = time.perf_counter()
+        sealed = int(lens.sum())
+        bad += batch.open_uncompress_host(ctx, a_ptr, stride, N, lens, 0, threads=threads)
+        t3 = time.perf_counter()
+        ts.append(t1 - t0)
+        to.append(t3 - t1)
+    restored = bool(np.array_equal(host[:, :4 + L], plain)) and bool((lens == L).all())
+    s, o = float(np.median(ts)), float(np.median(to))
+    del host, nonces, plain
+    L_.qgcm_host_free(a_ptr)
+    L_.qgcm_host_free(n_ptr)
+    ctx.close()
+    return {"config": "config5_snappy_then_gcm_host", "packets": N, "payload_len": L, "stride": stride,
+            "threads": threads, "compressed_over_plain": round(ratio, 4), "sealed_bytes": sealed,
+            "value": round(2 * N * L / (s + o) / 2**30, 2), "unit": "GiB/s (of uncompressed payload)",
+            "compress_seal_s": round(s, 4), "open_uncompress_s": round(o, 4),
+            "host_codec_only_s": {"compress": round(c1 - c0, 4), "uncompress": round(c2 - c1, 4)},
+            "status_ok": bad == 0, "restored": restored, "codec_roundtrip_ok": codec_ok}
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["config3", "e2e", "e2e_pageable"]
-    runs = {"config3": config3, "e2e": e2e, "e2e_pageable": lambda: e2e(pinned=False)}
+    which = sys.argv[1:] or ["config3", "e2e", "e2e_pageable", "config5"]
+    runs = {"config3": config3, "e2e": e2e, "e2e_pageable": lambda: e2e(pinned=False), "config5": config5}
     for w in which:
         print(json.dumps(runs[w]()), flush=True)

@@ -145,4 +145,4 @@ def run(x):
         env[d]=eval(e,{},env)&1
     return sum((env[f"s{i}"]&1)<<(7-i) for i in range(8))
 bad=[x for x in range(256) if run(x)!=SB[x]]
-print("mismatches",len(bad), "gates", len(lines))
+
