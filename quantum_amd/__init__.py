@@ -7,11 +7,12 @@ Layout:
   quantum_amd/plugin.py     plugin.Plugin / Encryption / Mock / Sorter mirror (plugin/*.go)
   quantum_amd/common.py     common.Payload and constants mirror (common/payload.go, common.go)
   quantum_amd/batch.py      device-resident batch entry points (throughput path)
+  quantum_amd/worker.py     worker.Outgoing / Incoming pipeline mirror (worker/outgoing.go, incoming.go)
 """
-from . import common, plugin  # noqa: F401
+from . import common, plugin, worker  # noqa: F401
 from ._lib import QgcmError, lib  # noqa: F401
 
-__all__ = ["common", "plugin", "crypto", "batch", "lib", "QgcmError"]
+__all__ = ["common", "plugin", "worker", "crypto", "batch", "lib", "QgcmError"]
 
 
 def __getattr__(name):

@@ -215,3 +215,15 @@ def GenerateSharedSecret(pubkey: bytes, privkey: bytes) -> bytes:
     pub = (bytes(pubkey) + bytes(32))[:32]
     priv = (bytes(privkey) + bytes(32))[:32]
     return x25519(priv, pub)
+
+
+def MappingAES(public_key: bytes | None, public_salt: bytes | None, private_key: bytes, private_salt: bytes,
+               ctx: Context | None = None):
+    """common/mapping.go:94-103 (ParseMapping): a peer's AES from its public key and salt and this
+    node's private ones -> (*AES or None, error).  None when the peer published no keys (the
+    reference then leaves mapping.AES nil)."""
+    if public_key is None or public_salt is None:
+        return None, None
+    secret = GenerateSharedSecret(public_key, private_key)
+    salt = GenerateSharedSecret(public_salt, private_salt)
+    return NewAES(secret, salt, ctx)
