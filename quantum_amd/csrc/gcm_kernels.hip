@@ -566,6 +566,215 @@ __device__ __forceinline__ uint32_t quad_xor(uint32_t v) {
     return v;
 }
 
+// One packet of a quad tile (4 lanes, lane m owns blocks b = m mod 4): CTR + GHASH + tag, in place.
+template <bool kSeal, bool kFold, bool kDesc, bool kGFin>
+__device__ __forceinline__ void quad_packet(const Batch &b, const uint32_t *__restrict__ rk_table, uint32_t pkt,
+                                            uint64_t off, uint32_t L, uint32_t wkey, uint32_t m, uint32_t lb,
+                                            uint32_t gH4, uint32_t gH) {
+    const Keys kk = {rk_table + (size_t)wkey * kRkWords, rk_table + (size_t)wkey * kRkWords + 64};
+    const uint4 *Hg = b.gh_table + (size_t)wkey * kGhEntries;  // comb tables of H^k (global)
+    uint8_t *raw = b.arena + off;
+    uint8_t *data = raw + 4;  // common.PacketStart
+
+    uint32_t g0 = 0, g1 = 0, g2 = 0, g3 = 0, n0, n1, n2;
+    if (kSeal && b.nonces) {
+        const uint32_t *np = reinterpret_cast<const uint32_t *>(b.nonces + 12ull * pkt);
+        n0 = np[0];
+        n1 = np[1];
+        n2 = np[2];
+    } else {
+        read_nonce(data, L, n0, n1, n2);
+    }
+    const uint32_t nfull = L >> 4, r = L & 15u;
+    const uint32_t d = nfull + (r ? 1u : 0u);  // data blocks incl. the partial one
+
+    // lane 3 starts its chain with the additional data block (block -1)
+    uint32_t z0 = 0, z1 = 0, z2 = 0, z3 = 0;
+    if (m == 3 && b.aad_len)
+        z0 = *reinterpret_cast<const uint32_t *>(raw) & (b.aad_len >= 4 ? 0xffffffffu : lowmask(b.aad_len));
+    int blast = -1;
+
+    uint32_t e0 = 0, e1 = 0, e2 = 0, e3 = 0;  // E_K(J0)
+    uint32_t prefix = 0;
+    if constexpr (kFold) {
+    Ctr cc;
+    uint32_t hi = 0;
+    ctr_setup(cc, n0, n1, n2, 0, kk, lb);
+    // Lane m walks blocks m, m+4, ... < d, then (lane d % 4 only) the virtual block d = E_K(J0):
+    // one AES instance per step, and J0 fills the slot of the lane with the fewest data blocks.
+    for (uint32_t bi = m; bi <= d; bi += 4) {
+        const bool j0 = bi == d;
+        const uint32_t ctr = j0 ? 1u : bi + 2;  // J0, or inc32(J0) + bi
+        if ((ctr >> 8) != hi) {
+            hi = ctr >> 8;
+            ctr_setup(cc, n0, n1, n2, hi, kk, lb);
+        }
+        uint32_t k0, k1, k2, k3;
+        ctr_block(cc, ctr & 0xffu, kk, lb, k0, k1, k2, k3);
+        if (j0) {
+            e0 = k0;
+            e1 = k1;
+            e2 = k2;
+            e3 = k3;
+            break;
+        }
+        W4 *p = reinterpret_cast<W4 *>(data + 16u * bi);
+        const W4 in = *p;  // a partial block reads into the tag area: inside the slot
+        const W4 out = {in.x ^ k0, in.y ^ k1, in.z ^ k2, in.w ^ k3};
+        W4 c = kSeal ? out : in;
+        if (bi < nfull) {
+            *p = out;
+        } else {  // the partial last block (r bytes)
+            const uint32_t q = r >> 2, sb = r & 3u;
+            uint32_t *bw = reinterpret_cast<uint32_t *>(p);
+            if (q > 0) bw[0] = out.x;
+            if (q > 1) bw[1] = out.y;
+            if (q > 2) bw[2] = out.z;
+            const uint32_t oq = sel4(q, out.x, out.y, out.z, out.w) & lowmask(sb);
+            if (kSeal)
+                prefix = oq;  // written with tag||nonce by write_tail
+            else
+                store_bytes(reinterpret_cast<uint8_t *>(p) + 4 * q, oq, sb);
+            c.x &= q > 0 ? 0xffffffffu : lowmask(sb);
+            c.y &= q > 1 ? 0xffffffffu : (q == 1 ? lowmask(sb) : 0u);
+            c.z &= q > 2 ? 0xffffffffu : (q == 2 ? lowmask(sb) : 0u);
+            c.w &= q == 3 ? lowmask(sb) : 0u;
+        }
+        ghash_mul(z0, z1, z2, z3, gH4);
+        z0 ^= c.x;
+        z1 ^= c.y;
+        z2 ^= c.z;
+        z3 ^= c.w;
+        blast = (int)bi;
+    }
+    } else {
+    Ctr cc;
+    uint32_t hi = 0;
+    ctr_setup(cc, n0, n1, n2, 0, kk, lb);
+    for (uint32_t bi = m; bi < nfull; bi += 4) {
+        const uint32_t ctr = bi + 2;  // inc32(J0) + bi
+        if ((ctr >> 8) != hi) {
+            hi = ctr >> 8;
+            ctr_setup(cc, n0, n1, n2, hi, kk, lb);
+        }
+        // the data load is issued before the AES rounds so its latency hides behind them
+        W4 *p = reinterpret_cast<W4 *>(data + 16u * bi);
+        const W4 in = load_block(p);
+        uint32_t k0, k1, k2, k3;
+        ctr_block(cc, ctr & 0xffu, kk, lb, k0, k1, k2, k3);
+        const W4 out = {in.x ^ k0, in.y ^ k1, in.z ^ k2, in.w ^ k3};
+        *p = out;
+        const W4 &c = kSeal ? out : in;
+        ghash_mul(z0, z1, z2, z3, gH4);
+        z0 ^= c.x;
+        z1 ^= c.y;
+        z2 ^= c.z;
+        z3 ^= c.w;
+        blast = (int)bi;
+    }
+    // One more slot: the partial last block (lane nfull % 4) and E_K(J0) (lane d % 4, the lane
+    // with the fewest data blocks) share one AES pass.
+    const bool part = r && (nfull & 3u) == m;
+    if (part || m == (d & 3u)) {
+        const uint32_t ctr = part ? nfull + 2 : 1u;  // inc32(J0) + nfull, or J0
+        if ((ctr >> 8) != hi) {
+            hi = ctr >> 8;
+            ctr_setup(cc, n0, n1, n2, hi, kk, lb);
+        }
+        uint32_t k0, k1, k2, k3;
+        ctr_block(cc, ctr & 0xffu, kk, lb, k0, k1, k2, k3);
+        if (part) {
+            uint8_t *blk = data + 16u * nfull;
+            const W4 in = *reinterpret_cast<const W4 *>(blk);  // reads into tag area: inside the slot
+            const uint32_t q = r >> 2, sb = r & 3u;
+            const uint32_t o0 = in.x ^ k0, o1 = in.y ^ k1, o2 = in.z ^ k2, o3 = in.w ^ k3;
+            uint32_t *bw = reinterpret_cast<uint32_t *>(blk);
+            if (q > 0) bw[0] = o0;
+            if (q > 1) bw[1] = o1;
+            if (q > 2) bw[2] = o2;
+            const uint32_t oq = sel4(q, o0, o1, o2, o3) & lowmask(sb);
+            W4 c = kSeal ? W4{o0, o1, o2, o3} : in;
+            if (kSeal)
+                prefix = oq;  // written with tag||nonce by write_tail
+            else
+                store_bytes(blk + 4 * q, oq, sb);
+            c.x &= q > 0 ? 0xffffffffu : lowmask(sb);
+            c.y &= q > 1 ? 0xffffffffu : (q == 1 ? lowmask(sb) : 0u);
+            c.z &= q > 2 ? 0xffffffffu : (q == 2 ? lowmask(sb) : 0u);
+            c.w &= q == 3 ? lowmask(sb) : 0u;
+            ghash_mul(z0, z1, z2, z3, gH4);
+            z0 ^= c.x;
+            z1 ^= c.y;
+            z2 ^= c.z;
+            z3 ^= c.w;
+            blast = (int)nfull;
+        } else {
+            e0 = k0;
+            e1 = k1;
+            e2 = k2;
+            e3 = k3;
+        }
+    }
+    }
+    // Y = sum_m Z_m * H^(e_m)  ^  ([len(A)]||[len(C)]) * H,  e_m = d + 1 - b_last(m) in [2, 5]
+    // (a lane without blocks has Z_m = 0 or only the AAD block, b_last = -1, d <= 3).
+    if constexpr (kGFin) {
+        const uint32_t em = d + 1u - (uint32_t)blast;
+        const uint32_t tsel = em == 2 ? kGhH2 : em == 3 ? kGhH3 : em == 4 ? kGhH4 : kGhH5;
+        ghash_mul_global(z0, z1, z2, z3, Hg + tsel);
+        uint32_t l0, l1, l2, l3;
+        ghash_lenblock_global(b.aad_len, L, Hg, l0, l1, l2, l3);
+        z0 = quad_xor(z0) ^ l0;
+        z1 = quad_xor(z1) ^ l1;
+        z2 = quad_xor(z2) ^ l2;
+        z3 = quad_xor(z3) ^ l3;
+    } else {
+        for (int t = (int)d - blast; t > 0; --t) {
+            if constexpr (kDesc)
+                ghash_mul_global(z0, z1, z2, z3, Hg);
+            else
+                ghash_mul(z0, z1, z2, z3, gH);
+        }
+        z0 = quad_xor(z0);
+        z1 = quad_xor(z1) ^ bswap(b.aad_len * 8u);  // [len(A)]_64 || [len(C)]_64, big endian
+        z2 = quad_xor(z2);
+        z3 = quad_xor(z3) ^ bswap(L * 8u);
+        if constexpr (kDesc)
+            ghash_mul_global(z0, z1, z2, z3, Hg);
+        else
+            ghash_mul(z0, z1, z2, z3, gH);
+    }
+    e0 = quad_xor(e0);
+    e1 = quad_xor(e1);
+    e2 = quad_xor(e2);
+    e3 = quad_xor(e3);
+    const uint32_t t0 = z0 ^ e0, t1 = z1 ^ e1, t2 = z2 ^ e2, t3 = z3 ^ e3;
+    // the lane owning the partial block (or lane 0) writes the tail
+    const uint32_t owner = r ? (nfull & 3u) : 0u;
+    if (kSeal) {
+        if (m == owner) {
+            write_tail(data, L, t0, t1, t2, t3, n0, n1, n2, prefix);
+            if (b.status) b.status[pkt] = 1;
+        }
+    } else {
+        read_tag(data, L, g0, g1, g2, g3);  // the tag is never written by Open
+        const bool ok = ((t0 ^ g0) | (t1 ^ g1) | (t2 ^ g2) | (t3 ^ g3)) == 0;
+        if (!ok) {
+            // Go 1.9 crypto/cipher gcm Open: zero the would-be plaintext on tag mismatch.
+            for (uint32_t bi = m; bi < nfull; bi += 4) {
+                const W4 zz = {0, 0, 0, 0};
+                *reinterpret_cast<W4 *>(data + 16u * bi) = zz;
+            }
+            if (r && m == owner) {
+                uint32_t *bw = reinterpret_cast<uint32_t *>(data + 16u * nfull);
+                for (uint32_t w = 0; w < (r >> 2); ++w) bw[w] = 0;
+                store_bytes(data + 16u * nfull + (r & ~3u), 0, r & 3u);
+            }
+        }
+        if (b.status && m == 0) b.status[pkt] = ok ? 1 : 0;
+    }
+}
+
 // kGFin: the once-per-packet recombination multiplies by H^2..H^5 come from the global key table
 // (one multiply per lane); otherwise by repeated multiplies by H (comb table of H in LDS for single
 // key batches, global for descriptor batches).
@@ -663,208 +872,7 @@ gcm_quad_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
                 continue;  // the whole quad leaves together
             }
         }
-        const Keys kk = {rk_table + (size_t)wkey * kRkWords, rk_table + (size_t)wkey * kRkWords + 64};
-        const uint4 *Hg = b.gh_table + (size_t)wkey * kGhEntries;  // comb tables of H^k (global)
-        uint8_t *raw = b.arena + off;
-        uint8_t *data = raw + 4;  // common.PacketStart
-
-        uint32_t g0 = 0, g1 = 0, g2 = 0, g3 = 0, n0, n1, n2;
-        if (kSeal && b.nonces) {
-            const uint32_t *np = reinterpret_cast<const uint32_t *>(b.nonces + 12ull * pkt);
-            n0 = np[0];
-            n1 = np[1];
-            n2 = np[2];
-        } else {
-            read_nonce(data, L, n0, n1, n2);
-        }
-        const uint32_t nfull = L >> 4, r = L & 15u;
-        const uint32_t d = nfull + (r ? 1u : 0u);  // data blocks incl. the partial one
-
-        // lane 3 starts its chain with the additional data block (block -1)
-        uint32_t z0 = 0, z1 = 0, z2 = 0, z3 = 0;
-        if (m == 3 && b.aad_len)
-            z0 = *reinterpret_cast<const uint32_t *>(raw) & (b.aad_len >= 4 ? 0xffffffffu : lowmask(b.aad_len));
-        int blast = -1;
-
-        uint32_t e0 = 0, e1 = 0, e2 = 0, e3 = 0;  // E_K(J0)
-        uint32_t prefix = 0;
-        if constexpr (kFold) {
-        Ctr cc;
-        uint32_t hi = 0;
-        ctr_setup(cc, n0, n1, n2, 0, kk, lb);
-        // Lane m walks blocks m, m+4, ... < d, then (lane d % 4 only) the virtual block d = E_K(J0):
-        // one AES instance per step, and J0 fills the slot of the lane with the fewest data blocks.
-        for (uint32_t bi = m; bi <= d; bi += 4) {
-            const bool j0 = bi == d;
-            const uint32_t ctr = j0 ? 1u : bi + 2;  // J0, or inc32(J0) + bi
-            if ((ctr >> 8) != hi) {
-                hi = ctr >> 8;
-                ctr_setup(cc, n0, n1, n2, hi, kk, lb);
-            }
-            uint32_t k0, k1, k2, k3;
-            ctr_block(cc, ctr & 0xffu, kk, lb, k0, k1, k2, k3);
-            if (j0) {
-                e0 = k0;
-                e1 = k1;
-                e2 = k2;
-                e3 = k3;
-                break;
-            }
-            W4 *p = reinterpret_cast<W4 *>(data + 16u * bi);
-            const W4 in = *p;  // a partial block reads into the tag area: inside the slot
-            const W4 out = {in.x ^ k0, in.y ^ k1, in.z ^ k2, in.w ^ k3};
-            W4 c = kSeal ? out : in;
-            if (bi < nfull) {
-                *p = out;
-            } else {  // the partial last block (r bytes)
-                const uint32_t q = r >> 2, sb = r & 3u;
-                uint32_t *bw = reinterpret_cast<uint32_t *>(p);
-                if (q > 0) bw[0] = out.x;
-                if (q > 1) bw[1] = out.y;
-                if (q > 2) bw[2] = out.z;
-                const uint32_t oq = sel4(q, out.x, out.y, out.z, out.w) & lowmask(sb);
-                if (kSeal)
-                    prefix = oq;  // written with tag||nonce by write_tail
-                else
-                    store_bytes(reinterpret_cast<uint8_t *>(p) + 4 * q, oq, sb);
-                c.x &= q > 0 ? 0xffffffffu : lowmask(sb);
-                c.y &= q > 1 ? 0xffffffffu : (q == 1 ? lowmask(sb) : 0u);
-                c.z &= q > 2 ? 0xffffffffu : (q == 2 ? lowmask(sb) : 0u);
-                c.w &= q == 3 ? lowmask(sb) : 0u;
-            }
-            ghash_mul(z0, z1, z2, z3, gH4);
-            z0 ^= c.x;
-            z1 ^= c.y;
-            z2 ^= c.z;
-            z3 ^= c.w;
-            blast = (int)bi;
-        }
-        } else {
-        Ctr cc;
-        uint32_t hi = 0;
-        ctr_setup(cc, n0, n1, n2, 0, kk, lb);
-        for (uint32_t bi = m; bi < nfull; bi += 4) {
-            const uint32_t ctr = bi + 2;  // inc32(J0) + bi
-            if ((ctr >> 8) != hi) {
-                hi = ctr >> 8;
-                ctr_setup(cc, n0, n1, n2, hi, kk, lb);
-            }
-            // the data load is issued before the AES rounds so its latency hides behind them
-            W4 *p = reinterpret_cast<W4 *>(data + 16u * bi);
-            const W4 in = load_block(p);
-            uint32_t k0, k1, k2, k3;
-            ctr_block(cc, ctr & 0xffu, kk, lb, k0, k1, k2, k3);
-            const W4 out = {in.x ^ k0, in.y ^ k1, in.z ^ k2, in.w ^ k3};
-            *p = out;
-            const W4 &c = kSeal ? out : in;
-            ghash_mul(z0, z1, z2, z3, gH4);
-            z0 ^= c.x;
-            z1 ^= c.y;
-            z2 ^= c.z;
-            z3 ^= c.w;
-            blast = (int)bi;
-        }
-        // One more slot: the partial last block (lane nfull % 4) and E_K(J0) (lane d % 4, the lane
-        // with the fewest data blocks) share one AES pass.
-        const bool part = r && (nfull & 3u) == m;
-        if (part || m == (d & 3u)) {
-            const uint32_t ctr = part ? nfull + 2 : 1u;  // inc32(J0) + nfull, or J0
-            if ((ctr >> 8) != hi) {
-                hi = ctr >> 8;
-                ctr_setup(cc, n0, n1, n2, hi, kk, lb);
-            }
-            uint32_t k0, k1, k2, k3;
-            ctr_block(cc, ctr & 0xffu, kk, lb, k0, k1, k2, k3);
-            if (part) {
-                uint8_t *blk = data + 16u * nfull;
-                const W4 in = *reinterpret_cast<const W4 *>(blk);  // reads into tag area: inside the slot
-                const uint32_t q = r >> 2, sb = r & 3u;
-                const uint32_t o0 = in.x ^ k0, o1 = in.y ^ k1, o2 = in.z ^ k2, o3 = in.w ^ k3;
-                uint32_t *bw = reinterpret_cast<uint32_t *>(blk);
-                if (q > 0) bw[0] = o0;
-                if (q > 1) bw[1] = o1;
-                if (q > 2) bw[2] = o2;
-                const uint32_t oq = sel4(q, o0, o1, o2, o3) & lowmask(sb);
-                W4 c = kSeal ? W4{o0, o1, o2, o3} : in;
-                if (kSeal)
-                    prefix = oq;  // written with tag||nonce by write_tail
-                else
-                    store_bytes(blk + 4 * q, oq, sb);
-                c.x &= q > 0 ? 0xffffffffu : lowmask(sb);
-                c.y &= q > 1 ? 0xffffffffu : (q == 1 ? lowmask(sb) : 0u);
-                c.z &= q > 2 ? 0xffffffffu : (q == 2 ? lowmask(sb) : 0u);
-                c.w &= q == 3 ? lowmask(sb) : 0u;
-                ghash_mul(z0, z1, z2, z3, gH4);
-                z0 ^= c.x;
-                z1 ^= c.y;
-                z2 ^= c.z;
-                z3 ^= c.w;
-                blast = (int)nfull;
-            } else {
-                e0 = k0;
-                e1 = k1;
-                e2 = k2;
-                e3 = k3;
-            }
-        }
-        }
-        // Y = sum_m Z_m * H^(e_m)  ^  ([len(A)]||[len(C)]) * H,  e_m = d + 1 - b_last(m) in [2, 5]
-        // (a lane without blocks has Z_m = 0 or only the AAD block, b_last = -1, d <= 3).
-        if constexpr (kGFin) {
-            const uint32_t em = d + 1u - (uint32_t)blast;
-            const uint32_t tsel = em == 2 ? kGhH2 : em == 3 ? kGhH3 : em == 4 ? kGhH4 : kGhH5;
-            ghash_mul_global(z0, z1, z2, z3, Hg + tsel);
-            uint32_t l0, l1, l2, l3;
-            ghash_lenblock_global(b.aad_len, L, Hg, l0, l1, l2, l3);
-            z0 = quad_xor(z0) ^ l0;
-            z1 = quad_xor(z1) ^ l1;
-            z2 = quad_xor(z2) ^ l2;
-            z3 = quad_xor(z3) ^ l3;
-        } else {
-            for (int t = (int)d - blast; t > 0; --t) {
-                if constexpr (kDesc)
-                    ghash_mul_global(z0, z1, z2, z3, Hg);
-                else
-                    ghash_mul(z0, z1, z2, z3, gH);
-            }
-            z0 = quad_xor(z0);
-            z1 = quad_xor(z1) ^ bswap(b.aad_len * 8u);  // [len(A)]_64 || [len(C)]_64, big endian
-            z2 = quad_xor(z2);
-            z3 = quad_xor(z3) ^ bswap(L * 8u);
-            if constexpr (kDesc)
-                ghash_mul_global(z0, z1, z2, z3, Hg);
-            else
-                ghash_mul(z0, z1, z2, z3, gH);
-        }
-        e0 = quad_xor(e0);
-        e1 = quad_xor(e1);
-        e2 = quad_xor(e2);
-        e3 = quad_xor(e3);
-        const uint32_t t0 = z0 ^ e0, t1 = z1 ^ e1, t2 = z2 ^ e2, t3 = z3 ^ e3;
-        // the lane owning the partial block (or lane 0) writes the tail
-        const uint32_t owner = r ? (nfull & 3u) : 0u;
-        if (kSeal) {
-            if (m == owner) {
-                write_tail(data, L, t0, t1, t2, t3, n0, n1, n2, prefix);
-                if (b.status) b.status[pkt] = 1;
-            }
-        } else {
-            read_tag(data, L, g0, g1, g2, g3);  // the tag is never written by Open
-            const bool ok = ((t0 ^ g0) | (t1 ^ g1) | (t2 ^ g2) | (t3 ^ g3)) == 0;
-            if (!ok) {
-                // Go 1.9 crypto/cipher gcm Open: zero the would-be plaintext on tag mismatch.
-                for (uint32_t bi = m; bi < nfull; bi += 4) {
-                    const W4 zz = {0, 0, 0, 0};
-                    *reinterpret_cast<W4 *>(data + 16u * bi) = zz;
-                }
-                if (r && m == owner) {
-                    uint32_t *bw = reinterpret_cast<uint32_t *>(data + 16u * nfull);
-                    for (uint32_t w = 0; w < (r >> 2); ++w) bw[w] = 0;
-                    store_bytes(data + 16u * nfull + (r & ~3u), 0, r & 3u);
-                }
-            }
-            if (b.status && m == 0) b.status[pkt] = ok ? 1 : 0;
-        }
+        quad_packet<kSeal, kFold, kDesc, kGFin>(b, rk_table, pkt, off, L, wkey, m, lb, gH4, gH);
     }
 }
 
