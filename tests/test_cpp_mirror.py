@@ -1,0 +1,34 @@
+"""The C++ host mirror of the reference's Go API (include/quantum.hpp, quantum_amd/csrc/quantum_host.cpp)
+through tests/cpp/mirror_test.cpp, a C++ restatement of crypto/crypto_test.go and
+plugin/plugin_test.go (built by __graft_entry__.build()).  The device-free tests run on CPU; the
+ones that seal/open run on the GPU, all in ONE child process."""
+import os
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+BIN = os.path.join(ROOT, "tests", "cpp", "mirror_test")
+CPU_TESTS = ["TestEcdh", "TestSorter", "TestCompression", "TestMock", "TestPayload"]
+GPU_TESTS = ["TestAES", "TestEncryption", "TestMulti", "TestEncryptionTamper", "TestMappingAES"]
+
+
+def run(names, timeout=120):
+    if not os.path.exists(BIN):
+        pytest.fail(f"{BIN} is missing: build it with __graft_entry__.build()")
+    r = subprocess.run([BIN, *names], capture_output=True, text=True, timeout=timeout)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out
+    for n in names:
+        assert f"--- PASS: {n}" in out, out
+
+
+@pytest.mark.parametrize("name", CPU_TESTS)
+def test_cpp_mirror_cpu(name):
+    run([name])
+
+
+@pytest.mark.gpu
+def test_cpp_mirror_gpu():
+    run(GPU_TESTS)
