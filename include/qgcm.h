@@ -185,6 +185,20 @@ int qgcm_compress_seal_host(qgcm_ctx *ctx, uint8_t *h_arena, uint64_t stride, ui
 int qgcm_open_uncompress_host(qgcm_ctx *ctx, uint8_t *h_arena, uint64_t stride, uint32_t n, uint32_t *lens,
                               uint32_t key_idx, uint32_t aad_len, int threads, uint8_t *h_status);
 
+/* ---- batched UDP I/O (socket/udp.go:35-70, one syscall per batch) ---- */
+/* Datagram i is slot i's Raw[:lens[i]] (wire format [4-B IP][packet]), moved with recvmmsg/sendmmsg
+ * straight into / out of a host arena (pinned from qgcm_host_alloc: then also the DMA source of
+ * qgcm_*_host).  qgcm_udp_socket binds ip:port (port 0: any; bufbytes > 0 sizes SO_RCVBUF/SNDBUF)
+ * and returns the fd or -1.  recv waits up to timeout_ms (-1 forever) for the first datagram and then
+ * takes what is queued, up to max_n; returns the count (0 on timeout) or -1.  send returns the
+ * number of datagrams sent or -1. */
+int qgcm_udp_socket(const char *ip, int port, int bufbytes);
+int qgcm_udp_port(int fd);
+int qgcm_udp_close(int fd);
+int qgcm_udp_recv_slots(int fd, uint8_t *arena, uint64_t stride, uint32_t max_n, uint32_t *lens, int timeout_ms);
+int qgcm_udp_send_slots(int fd, const uint8_t *arena, uint64_t stride, uint32_t n, const uint32_t *lens,
+                        const char *ip, int port);
+
 /* ---- measurement: achievable HBM copy rate (reads + writes bytes) for the roofline ---- */
 /* 16-B aligned device buffers, bytes a multiple of 16.  Asynchronous on stream. */
 int qgcm_stream_copy(qgcm_ctx *ctx, void *d_dst, const void *d_src, uint64_t bytes, void *stream);
