@@ -55,6 +55,30 @@ __device__ __forceinline__ void lds_st32(uint32_t addr, uint32_t v) { *(lds_u32 
 __device__ __forceinline__ void lds_st128(uint32_t addr, uint4 v) {
     *(lds_u128 *)(size_t)addr = u32x4{v.x, v.y, v.z, v.w};
 }
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) u32x2 lds_u64;
+// volatile: keeps the two halves as two ds_read_b64 (the load/store optimizer would otherwise pair
+// them into ds_read2_b64, two 4 x 16-lane accesses: 8 LDS cycles instead of 2 x 2)
+__device__ __forceinline__ u32x2 lds64(uint32_t addr) { return *(const volatile lds_u64 *)(size_t)addr; }
+
+// GHASH comb tables in LDS, two layouts.  kB64: entry e = 16 p + v (nibble position p, value v) is
+// split into two 8-B halves, words 0-1 at base + 256 p + 8 v and words 2-3 at +128, read by two
+// ds_read_b64 (2 x 32-lane groups; the 16 entries of a half-row sit in 16 distinct bank pairs, so
+// any 32 nibbles are conflict-free).  Otherwise entry e is 16 B at base + 16 e, read by one
+// ds_read_b128 (4 x 16-lane groups).  Same LDS-array cycles per multiply (2 x 2 vs 4), but at 32
+// waves/CU the b64 form mixes better with the ds_read_b32 T-table stream
+// (tools/microbench/lds_mix.hip +6%; config 2 +2.1% in an in-process A/B) while at 12 waves/CU
+// (descriptor kernel) it is 1.2% slower: the single-key kernel uses kB64, the others do not.
+template <bool kB64>
+__device__ __forceinline__ void lds_st_comb(uint32_t base, uint32_t e, uint4 v) {
+    if constexpr (kB64) {
+        const uint32_t a = base + (e >> 4) * 256u + (e & 15u) * 8u;
+        *(lds_u64 *)(size_t)a = u32x2{v.x, v.y};
+        *(lds_u64 *)(size_t)(a + 128u) = u32x2{v.z, v.w};
+    } else {
+        lds_st128(base + e * 16u, v);
+    }
+}
 
 // Te0[byte k of s] / Te1[byte k of s] from this lane's replica.
 // v_perm: result byte0 = lb.byte0 (lane*4), byte1 = s.byte k, bytes 2,3 = 0.
@@ -166,6 +190,7 @@ __device__ __forceinline__ void ctr_blocks(const Ctr &c, uint32_t lo, const Keys
 // Y <- Y * H in GF(2^128) via the 4-bit comb in this wave's LDS table at gb (byte1/2 of gb hold
 // its base; byte0 is 0).  Entry (p, v) at gb + p*256 + v*16, p = nibble position (2*byte for the
 // high nibble, 2*byte+1 for the low one), v = nibble value.
+template <bool kB64 = false>
 __device__ __forceinline__ void ghash_mul(uint32_t &y0, uint32_t &y1, uint32_t &y2, uint32_t &y3, uint32_t gb) {
     uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
     const uint32_t yw[4] = {y0, y1, y2, y3};
@@ -173,6 +198,21 @@ __device__ __forceinline__ void ghash_mul(uint32_t &y0, uint32_t &y1, uint32_t &
     // the LDS queue can overlap anyway (lgkmcnt tracks 15 in flight per wave).
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
+        if constexpr (kB64) {
+        const uint32_t hi = (yw[w] >> 1) & 0x78787878u;  // 8 x high nibble of each byte
+        const uint32_t lo = (yw[w] << 3) & 0x78787878u;  // 8 x low nibble
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int j = 4 * w + k;
+            const uint32_t ah = perm(gb, hi, 0x0c060500u | k) + (2 * j) * 256;
+            const uint32_t al = perm(gb, lo, 0x0c060500u | k) + (2 * j + 1) * 256;
+            const u32x2 h0 = lds64(ah), h1 = lds64(ah + 128u), l0 = lds64(al), l1 = lds64(al + 128u);
+            a0 = xor3(a0, h0.x, l0.x);
+            a1 = xor3(a1, h0.y, l0.y);
+            a2 = xor3(a2, h1.x, l1.x);
+            a3 = xor3(a3, h1.y, l1.y);
+        }
+        } else {
         const uint32_t hi = yw[w] & 0xf0f0f0f0u;
         const uint32_t lo = (yw[w] << 4) & 0xf0f0f0f0u;
 #pragma unroll
@@ -184,6 +224,7 @@ __device__ __forceinline__ void ghash_mul(uint32_t &y0, uint32_t &y1, uint32_t &
             a1 = xor3(a1, th.y, tl.y);
             a2 = xor3(a2, th.z, tl.z);
             a3 = xor3(a3, th.w, tl.w);
+        }
         }
         // chunk fence: the accumulators are consumed here and the next chunk's LDS loads cannot be
         // hoisted above it, so at most 8 x 16 B of table rows are live at once
@@ -356,7 +397,7 @@ gcm_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
     uint32_t cur_key = 0xffffffffu;
     if (kShared) {
         const uint4 *src = b.gh_table + (size_t)b.uniform_key * kGhEntries;
-        for (uint32_t e = threadIdx.x; e < 512u; e += kT) lds_st128(kTeBytes + e * 16, src[e]);  // H only
+        for (uint32_t e = threadIdx.x; e < 512u; e += kT) lds_st_comb<false>(kTeBytes, e, src[e]);  // H only
         cur_key = b.uniform_key;
     }
     __syncthreads();
@@ -391,7 +432,7 @@ gcm_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
 #pragma unroll
             for (int r = 0; r < 8; ++r) {
                 const uint32_t e = r * 64 + lane;
-                lds_st128(gb + e * 16, src[e]);
+                lds_st_comb<false>(gb, e, src[e]);
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -640,7 +681,7 @@ __device__ __forceinline__ void quad_packet(const Batch &b, const uint32_t *__re
             c.z &= q > 2 ? 0xffffffffu : (q == 2 ? lowmask(sb) : 0u);
             c.w &= q == 3 ? lowmask(sb) : 0u;
         }
-        ghash_mul(z0, z1, z2, z3, gH4);
+        ghash_mul<!kDesc>(z0, z1, z2, z3, gH4);
         z0 ^= c.x;
         z1 ^= c.y;
         z2 ^= c.z;
@@ -665,7 +706,7 @@ __device__ __forceinline__ void quad_packet(const Batch &b, const uint32_t *__re
         const W4 out = {in.x ^ k0, in.y ^ k1, in.z ^ k2, in.w ^ k3};
         *p = out;
         const W4 &c = kSeal ? out : in;
-        ghash_mul(z0, z1, z2, z3, gH4);
+        ghash_mul<!kDesc>(z0, z1, z2, z3, gH4);
         z0 ^= c.x;
         z1 ^= c.y;
         z2 ^= c.z;
@@ -702,7 +743,7 @@ __device__ __forceinline__ void quad_packet(const Batch &b, const uint32_t *__re
             c.y &= q > 1 ? 0xffffffffu : (q == 1 ? lowmask(sb) : 0u);
             c.z &= q > 2 ? 0xffffffffu : (q == 2 ? lowmask(sb) : 0u);
             c.w &= q == 3 ? lowmask(sb) : 0u;
-            ghash_mul(z0, z1, z2, z3, gH4);
+            ghash_mul<!kDesc>(z0, z1, z2, z3, gH4);
             z0 ^= c.x;
             z1 ^= c.y;
             z2 ^= c.z;
@@ -733,7 +774,7 @@ __device__ __forceinline__ void quad_packet(const Batch &b, const uint32_t *__re
             if constexpr (kDesc)
                 ghash_mul_global(z0, z1, z2, z3, Hg);
             else
-                ghash_mul(z0, z1, z2, z3, gH);
+                ghash_mul<!kDesc>(z0, z1, z2, z3, gH);
         }
         z0 = quad_xor(z0);
         z1 = quad_xor(z1) ^ bswap(b.aad_len * 8u);  // [len(A)]_64 || [len(C)]_64, big endian
@@ -742,7 +783,7 @@ __device__ __forceinline__ void quad_packet(const Batch &b, const uint32_t *__re
         if constexpr (kDesc)
             ghash_mul_global(z0, z1, z2, z3, Hg);
         else
-            ghash_mul(z0, z1, z2, z3, gH);
+            ghash_mul<!kDesc>(z0, z1, z2, z3, gH);
     }
     e0 = quad_xor(e0);
     e1 = quad_xor(e1);
@@ -793,10 +834,10 @@ gcm_quad_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
     }
     if constexpr (!kDesc) {
         const uint4 *src = b.gh_table + (size_t)b.uniform_key * kGhEntries + kGhH4;
-        for (uint32_t e = threadIdx.x; e < 512u; e += kT) lds_st128(kTeBytes + e * 16, src[e]);
+        for (uint32_t e = threadIdx.x; e < 512u; e += kT) lds_st_comb<!kDesc>(kTeBytes, e, src[e]);
         if constexpr (!kGFin) {
             const uint4 *srcH = b.gh_table + (size_t)b.uniform_key * kGhEntries + kGhH;
-            for (uint32_t e = threadIdx.x; e < 512u; e += kT) lds_st128(kTeBytes + kGhBytes + e * 16, srcH[e]);
+            for (uint32_t e = threadIdx.x; e < 512u; e += kT) lds_st_comb<!kDesc>(kTeBytes + kGhBytes, e, srcH[e]);
         }
     }
     __syncthreads();
@@ -836,7 +877,7 @@ gcm_quad_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
 #pragma unroll
                     for (int r = 0; r < 8; ++r) {
                         const uint32_t e = r * 64 + lane;
-                        lds_st128(gH4 + e * 16, src[e]);
+                        lds_st_comb<!kDesc>(gH4, e, src[e]);
                     }
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                     __builtin_amdgcn_wave_barrier();
