@@ -27,7 +27,7 @@ from quantum_amd import batch, shard  # noqa: E402
 from quantum_amd.crypto import Context, derive_key  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, MI355X_MICROARCH.md "Chip-level parameters"
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r1_final", "traffic.json")  # tools/pmc_traffic.py
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r1_s3", "traffic.json")  # tools/pmc_traffic.py
 SECRET = b"AES256Key-32Characters1234567890"
 SALT = bytes(range(32))
 AAD = bytes([10, 99, 0, 1])

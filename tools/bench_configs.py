@@ -10,7 +10,9 @@
            snappy (host C++ codec, `threads` workers) -> seal, then open -> uncompress, pipelined
            with PCIe copies and the device (qgcm_compress_seal_host / qgcm_open_uncompress_host).
 
-Prints one JSON line per config.  Usage: python tools/bench_configs.py [config3] [e2e]
+  config4_shard  one GPU's 8 x 2^20-packet shard of config 4 (64 x 2^20 x 1350 B over 8 GPUs).
+
+Prints one JSON line per config.  Usage: python tools/bench_configs.py [config3] [e2e] [config4_shard] ...
 """
 from __future__ import annotations
 
@@ -192,8 +194,56 @@ def config5(reps: int = 3, threads: int = 16) -> dict:
             "status_ok": bad == 0, "restored": restored, "codec_roundtrip_ok": codec_ok}
 
 
+def config4_shard(reps: int = 5, world: int = 8, rank: int = 0) -> dict:
+    """One GPU's shard of config 4: 64 x 2^20 x 1350 B packets split over `world` GPUs by the
+    contiguous single-key partition (quantum_amd.shard.packet_range), i.e. 8 x 2^20 packets
+    (11.8 GB of slots) resident on this GPU.  The 8-GPU aggregate is the driver's N=8 bench run;
+    this measures the per-GPU rate at config 4's per-GPU size, against which its efficiency is read.
+    Parity at this size: sealed -> opened round trip of every packet (status) plus a spot check of
+    the first 4096 slots against a 4096-packet reference batch sealed separately."""
+    from quantum_amd import shard
+
+    total, L = 64 << 20, 1350
+    lo, hi = shard.packet_range(total, world, rank)
+    N = hi - lo
+    stride = batch.slot_stride(L, align=64)
+    ctx = Context(device=0, max_keys=4)
+    key = derive_key(b"AES256Key-32Characters1234567890", bytes(range(32)))
+    ctx.set_key(0, key)
+    alloc = torch.zeros(N * stride + 64, dtype=torch.uint8, device="cuda")
+    arena = alloc[60:]
+    nonces = torch.zeros(12 * N, dtype=torch.uint8, device="cuda")
+    status = torch.zeros(N, dtype=torch.uint8, device="cuda")
+    batch.fill_uniform(arena, stride, N, L, 0x0100630a, 0x5EED0001 + rank, nonces, 0x5EED0002 + rank)
+    head = arena[:4096 * stride].clone()
+    batch.seal_uniform(ctx, head, stride, 4096, L, 0, nonces[:12 * 4096])
+    ts, to = [], []
+    ok = True
+    for r in range(reps + 1):
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        e[0].record()
+        batch.seal_uniform(ctx, arena, stride, N, L, 0, nonces)
+        e[1].record()
+        if r == 0:
+            ok &= bool(torch.equal(arena[:4096 * stride], head))
+        batch.open_uniform(ctx, arena, stride, N, L + 28, 0, status=status)
+        e[2].record()
+        torch.cuda.synchronize()
+        ok &= int(status.sum()) == N
+        if r > 0:
+            ts.append(e[0].elapsed_time(e[1]))
+            to.append(e[1].elapsed_time(e[2]))
+    s, o = float(np.median(ts)), float(np.median(to))
+    ctx.close()
+    return {"config": "config4_per_gpu_shard", "world": world, "rank": rank, "packets_total": total,
+            "packets_this_gpu": N, "payload_len": L, "slot_stride": stride,
+            "arena_GB": round(N * stride / 1e9, 2), "value": round(2 * N * L / ((s + o) * 1e-3) / 2**30, 2),
+            "unit": "GiB/s (this GPU)", "seal_ms": round(s, 3), "open_ms": round(o, 3), "status_ok": ok}
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["config3", "e2e", "e2e_pageable", "config5"]
-    runs = {"config3": config3, "e2e": e2e, "e2e_pageable": lambda: e2e(pinned=False), "config5": config5}
+    which = sys.argv[1:] or ["config3", "e2e", "e2e_pageable", "config5", "config4_shard"]
+    runs = {"config3": config3, "e2e": e2e, "e2e_pageable": lambda: e2e(pinned=False), "config5": config5,
+            "config4_shard": config4_shard}
     for w in which:
         print(json.dumps(runs[w]()), flush=True)
