@@ -22,8 +22,10 @@
 
 using namespace qgcm;
 
-constexpr int kPipeStreams = 3;         // H2D / kernel / D2H of consecutive chunks overlap
-constexpr uint64_t kPipeChunk = 32ull << 20;  // bytes of slots per pipeline chunk
+constexpr int kPipeStreams = 3;         // copy-in / kernel / copy-out stages
+constexpr uint64_t kPipeChunk = 32ull << 20;  // bytes of slots per pipeline chunk (chained path)
+constexpr uint64_t kHostChunk = 64ull << 20;  // run_host: bytes of slots per chunk
+constexpr uint64_t kHostRing = 4ull << 30;    // run_host: device staging budget (HBM is 288 GB)
 
 struct qgcm_ctx {
     int device = 0;
@@ -56,10 +58,14 @@ struct qgcm_ctx {
 
     // host-batch pipeline (qgcm_seal_host / qgcm_open_host), guarded by io_mu
     hipStream_t pipe[kPipeStreams] = {};
-    uint8_t *d_ring = nullptr;  // kPipeStreams chunk slots, one per stream
+    std::vector<hipEvent_t> ev_in, ev_kern, ev_out;  // run_host: per device chunk slot
+    uint64_t host_chunk = kHostChunk, host_ring = kHostRing;  // QGCM_PIPE_CHUNK_MB / QGCM_PIPE_RING_MB
+    uint8_t *d_ring = nullptr;  // chunk slots (run_host: up to host_ring bytes; chained path: one per stream)
     size_t ring_cap = 0;
     uint8_t *h_stat = nullptr;  // pinned status bytes of the whole host batch
     size_t hstat_cap = 0;
+    uint8_t *d_side = nullptr;  // run_host: nonces (12 n) and status (n) of the whole batch
+    size_t side_cap = 0;
     qgcm_desc *h_desc = nullptr;  // pinned descriptor staging of the chained (snappy + GCM) path
     size_t hdesc_cap = 0;
 
@@ -309,6 +315,8 @@ qgcm_ctx *qgcm_create(int device, uint32_t max_keys, char *err, int errlen) {
         if (iv >= 0 && iv < kNumVariants) ctx->uniform_variant = iv;
     }
     if (const char *v = getenv("QGCM_WGS_PER_CU")) ctx->wgs_per_cu_override = atoi(v);
+    if (const char *v = getenv("QGCM_PIPE_CHUNK_MB")) ctx->host_chunk = (uint64_t)std::max(1, atoi(v)) << 20;
+    if (const char *v = getenv("QGCM_PIPE_RING_MB")) ctx->host_ring = (uint64_t)std::max(1, atoi(v)) << 20;
     if (const char *v = getenv("QGCM_DESC_VARIANT")) {
         const int iv = atoi(v);
         if (iv == kVariantGeneral || (iv >= 0 && iv < kNumVariants && variant_desc(iv))) ctx->desc_variant = iv;
@@ -352,11 +360,14 @@ void qgcm_destroy(qgcm_ctx *ctx) {
     if (ctx->h_pin) hipHostFree(ctx->h_pin);
     if (ctx->io_stream) hipStreamDestroy(ctx->io_stream);
     hipFree(ctx->d_ring);
+    hipFree(ctx->d_side);
     if (ctx->h_stat) hipHostFree(ctx->h_stat);
     if (ctx->h_desc) hipHostFree(ctx->h_desc);
     for (hipStream_t p : ctx->pipe)
         if (p) hipStreamDestroy(p);
     if (ctx->ws_done) hipEventDestroy(ctx->ws_done);
+    for (auto *v : {&ctx->ev_in, &ctx->ev_kern, &ctx->ev_out})
+        for (hipEvent_t e : *v) hipEventDestroy(e);
     delete ctx;
 }
 
@@ -472,11 +483,15 @@ long qgcm_open_one(qgcm_ctx *ctx, uint32_t key_idx, uint8_t *data, long len, con
     return h[stride] == 1 ? len - QGCM_OVERHEAD : -1;
 }
 
-// Host batches, pipelined: the batch is cut into ~32 MiB chunks; chunk c runs H2D -> kernel -> D2H on
-// stream c % 3 in its own device slot, so the copy-in of chunk c+1, the kernel of chunk c and the
-// copy-out of chunk c-1 overlap (both PCIe directions busy at once).  Pinned caller memory
-// (qgcm_host_alloc, hipHostMalloc/Register) is DMA'd in place; pageable memory still works but HIP
-// stages it, which serializes the copies.
+// Host batches, pipelined: the batch is cut into ~64 MiB chunks, each with its own device slot while
+// the batch fits the staging budget (4 GiB of the 288 GB HBM; larger batches rotate through the
+// slots).  One stream per stage -- copy-in, kernel, copy-out -- ordered by per-slot events: chunk c's
+// kernel waits for its copy-in, its copy-out for its kernel, and (only when slots rotate) the copy-in
+// of chunk c + nslots for chunk c's copy-out.  Each PCIe direction thus sees an uninterrupted queue
+// of copies (a stream per chunk doing H2D -> kernel -> D2H in order made the next copy-in of that
+// stream wait behind its copy-out: 30.5 GiB/s; per-stage streams with 4 rotating 32 MiB slots: 35.6).
+// Pinned caller memory (qgcm_host_alloc, hipHostMalloc/Register) is DMA'd in place; pageable memory
+// still works but HIP stages it, which serializes the copies.
 static int run_host(qgcm_ctx *ctx, bool seal, uint8_t *h_arena, uint64_t stride, uint32_t n, uint32_t len,
                     uint32_t key_idx, const uint8_t *h_nonces, uint32_t aad_len, uint8_t *h_status) {
     if (!ctx || (n && !h_arena) || aad_len > 4 || (stride & 3)) return QGCM_E_ARG;
@@ -487,15 +502,22 @@ static int run_host(qgcm_ctx *ctx, bool seal, uint8_t *h_arena, uint64_t stride,
     if (n == 0) return 0;
     std::lock_guard<std::mutex> g(ctx->io_mu);
     if (hipSetDevice(ctx->device) != hipSuccess) return QGCM_E_HIP;
-    auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
-    uint64_t cpk = (kPipeChunk / stride) & ~63ull;  // packets per chunk, whole 64-packet tiles
+    uint64_t cpk = (ctx->host_chunk / stride) & ~63ull;  // packets per chunk, whole 64-packet tiles
     if (cpk < 64) cpk = 64;
     if (cpk > n) cpk = n;
     const uint64_t nchunks = (n + cpk - 1) / cpk;
     const bool non = seal && h_nonces;
-    const uint64_t off_non = al(cpk * stride), off_st = off_non + (non ? al(12 * cpk) : 0);
-    const uint64_t slot = off_st + al(cpk);
-    const int nslots = nchunks < (uint64_t)kPipeStreams ? (int)nchunks : kPipeStreams;
+    const uint64_t slot = (cpk * stride + 255) & ~255ull;
+    const uint64_t fit = std::max<uint64_t>(2, ctx->host_ring / slot);
+    const int nslots = (int)std::min<uint64_t>(nchunks, fit);
+    while (ctx->ev_in.size() < (size_t)nslots) {
+        hipEvent_t e[3] = {};
+        for (hipEvent_t &x : e)
+            if (hipEventCreateWithFlags(&x, hipEventDisableTiming) != hipSuccess) return QGCM_E_HIP;
+        ctx->ev_in.push_back(e[0]);
+        ctx->ev_kern.push_back(e[1]);
+        ctx->ev_out.push_back(e[2]);
+    }
     if (slot * nslots > ctx->ring_cap) {
         if (ctx->d_ring) hipFree(ctx->d_ring);
         ctx->d_ring = nullptr;
@@ -503,6 +525,18 @@ static int run_host(qgcm_ctx *ctx, bool seal, uint8_t *h_arena, uint64_t stride,
         if (hipMalloc(&ctx->d_ring, slot * nslots) != hipSuccess) return QGCM_E_NOMEM;
         ctx->ring_cap = slot * nslots;
     }
+    // nonces and status of the whole batch travel in one copy each (per-chunk side copies cost a
+    // DMA setup each: 2 per chunk)
+    const uint64_t non_bytes = non ? (12ull * n + 255) & ~255ull : 0;  // nonces first: 4-B aligned words
+    const uint64_t side = non_bytes + n;
+    if (side > ctx->side_cap) {
+        if (ctx->d_side) hipFree(ctx->d_side);
+        ctx->d_side = nullptr;
+        ctx->side_cap = 0;
+        if (hipMalloc(&ctx->d_side, side) != hipSuccess) return QGCM_E_NOMEM;
+        ctx->side_cap = side;
+    }
+    uint8_t *d_non_all = ctx->d_side, *d_stat_all = ctx->d_side + non_bytes;
     if (n > ctx->hstat_cap) {
         if (ctx->h_stat) hipHostFree(ctx->h_stat);
         ctx->h_stat = nullptr;
@@ -510,28 +544,39 @@ static int run_host(qgcm_ctx *ctx, bool seal, uint8_t *h_arena, uint64_t stride,
         if (hipHostMalloc(&ctx->h_stat, n, hipHostMallocDefault) != hipSuccess) return QGCM_E_NOMEM;
         ctx->hstat_cap = n;
     }
+    // one copy-in stream: alternating two (two SDMA queues) measured 27.3 vs 38.0 GiB/s
+    hipStream_t s_in = ctx->pipe[0], s_k = ctx->pipe[1], s_out = ctx->pipe[2];
     int rc = QGCM_OK;
+    if (non && hipMemcpyAsync(d_non_all, h_nonces, 12ull * n, hipMemcpyHostToDevice, s_in) != hipSuccess)
+        rc = QGCM_E_HIP;
     for (uint64_t c = 0; c < nchunks && rc == QGCM_OK; ++c) {
         const int k = (int)(c % nslots);
-        hipStream_t s = ctx->pipe[k];
-        uint8_t *d = ctx->d_ring + k * slot, *d_non = d + off_non, *d_st = d + off_st;
+        uint8_t *d = ctx->d_ring + k * slot;
         const uint64_t c0 = c * cpk, cn = (n - c0) < cpk ? (n - c0) : cpk;
         uint8_t *h = h_arena + c0 * stride;
-        if (hipMemcpyAsync(d, h, cn * stride, hipMemcpyHostToDevice, s) != hipSuccess ||
-            (non && hipMemcpyAsync(d_non, h_nonces + 12 * c0, 12 * cn, hipMemcpyHostToDevice, s) != hipSuccess)) {
+        // slot k is free once the copy-out of chunk c - nslots has landed
+        if ((c >= (uint64_t)nslots && hipStreamWaitEvent(s_in, ctx->ev_out[k], 0) != hipSuccess) ||
+            hipMemcpyAsync(d, h, cn * stride, hipMemcpyHostToDevice, s_in) != hipSuccess ||
+            hipEventRecord(ctx->ev_in[k], s_in) != hipSuccess || hipStreamWaitEvent(s_k, ctx->ev_in[k], 0) != hipSuccess) {
             rc = QGCM_E_HIP;
             break;
         }
         if (!seal && len < QGCM_OVERHEAD)
-            rc = hip_fail(hipMemsetAsync(d_st, 0, cn, s));
+            rc = hip_fail(hipMemsetAsync(d_stat_all + c0, 0, cn, s_k));
         else
-            rc = run_uniform(ctx, seal, d, stride, (uint32_t)cn, len, key_idx, non ? d_non : nullptr, aad_len, d_st, s);
-        if (rc == QGCM_OK && (hipMemcpyAsync(h, d, cn * stride, hipMemcpyDeviceToHost, s) != hipSuccess ||
-                              hipMemcpyAsync(ctx->h_stat + c0, d_st, cn, hipMemcpyDeviceToHost, s) != hipSuccess))
+            rc = run_uniform(ctx, seal, d, stride, (uint32_t)cn, len, key_idx, non ? d_non_all + 12 * c0 : nullptr,
+                             aad_len, d_stat_all + c0, s_k);
+        if (rc == QGCM_OK &&
+            (hipEventRecord(ctx->ev_kern[k], s_k) != hipSuccess || hipStreamWaitEvent(s_out, ctx->ev_kern[k], 0) != hipSuccess ||
+             hipMemcpyAsync(h, d, cn * stride, hipMemcpyDeviceToHost, s_out) != hipSuccess ||
+             hipEventRecord(ctx->ev_out[k], s_out) != hipSuccess))
             rc = QGCM_E_HIP;
     }
-    for (int k = 0; k < nslots; ++k)
-        if (hipStreamSynchronize(ctx->pipe[k]) != hipSuccess) rc = QGCM_E_HIP;
+    if (rc == QGCM_OK && (hipStreamWaitEvent(s_out, ctx->ev_kern[(nchunks - 1) % nslots], 0) != hipSuccess ||
+                          hipMemcpyAsync(ctx->h_stat, d_stat_all, n, hipMemcpyDeviceToHost, s_out) != hipSuccess))
+        rc = QGCM_E_HIP;
+    for (hipStream_t p : {s_in, s_k, s_out})
+        if (hipStreamSynchronize(p) != hipSuccess) rc = QGCM_E_HIP;
     if (rc != QGCM_OK) return rc;
     int bad = 0;
     for (uint32_t i = 0; i < n; ++i) bad += ctx->h_stat[i] != 1;

@@ -1,0 +1,52 @@
+"""PCIe copy ceiling on the GPU box: pinned host <-> HBM hipMemcpyAsync rates, one direction at a time
+and both directions at once (two streams), for the chunk sizes qgcm_seal_host pipelines with.
+The e2e rows of DESIGN.md section 5 are read against these numbers.
+Usage: python tools/microbench/pcie.py
+"""
+import json
+
+import torch
+
+TOTAL = 1 << 30  # 1 GiB per direction per measurement
+
+
+def rate(chunk: int, h2d: bool, d2h: bool, reps: int = 3, stream_host: bool = False) -> dict:
+    """stream_host: walk a 1 GiB pinned host buffer chunk by chunk (as qgcm_seal_host walks the
+    arena) instead of re-copying one chunk-sized buffer."""
+    n = TOTAL // chunk
+    hsz = TOTAL if stream_host else chunk
+    hs = [torch.empty(hsz, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
+    ds = [torch.empty(chunk, dtype=torch.uint8, device="cuda") for _ in range(2)]
+    s_in, s_out = torch.cuda.Stream(), torch.cuda.Stream()
+    best = None
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        s_in.wait_event(e0)
+        s_out.wait_event(e0)
+        for i in range(n):
+            o = i * chunk if stream_host else 0
+            if h2d:
+                with torch.cuda.stream(s_in):
+                    ds[0].copy_(hs[0][o:o + chunk], non_blocking=True)
+            if d2h:
+                with torch.cuda.stream(s_out):
+                    hs[1][o:o + chunk].copy_(ds[1], non_blocking=True)
+        torch.cuda.current_stream().wait_stream(s_in)
+        torch.cuda.current_stream().wait_stream(s_out)
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1)
+        best = ms if best is None else min(best, ms)
+    gbs = n * chunk / (best * 1e-3) / 1e9
+    return {"chunk_MiB": chunk >> 20, "h2d": h2d, "d2h": d2h, "host_walk_GiB": hsz >> 30,
+            "GB_per_s_each_direction": round(gbs, 1)}
+
+
+if __name__ == "__main__":
+    for chunk in (8 << 20, 32 << 20, 128 << 20):
+        for h2d, d2h in ((True, False), (False, True), (True, True)):
+            print(json.dumps(rate(chunk, h2d, d2h)), flush=True)
+    for chunk in (32 << 20, 64 << 20):
+        print(json.dumps(rate(chunk, True, True, stream_host=True)), flush=True)
