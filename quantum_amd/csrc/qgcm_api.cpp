@@ -513,7 +513,11 @@ static int run_host(qgcm_ctx *ctx, bool seal, uint8_t *h_arena, uint64_t stride,
     while (ctx->ev_in.size() < (size_t)nslots) {
         hipEvent_t e[3] = {};
         for (hipEvent_t &x : e)
-            if (hipEventCreateWithFlags(&x, hipEventDisableTiming) != hipSuccess) return QGCM_E_HIP;
+            if (hipEventCreateWithFlags(&x, hipEventDisableTiming) != hipSuccess) {
+                for (hipEvent_t y : e)
+                    if (y) hipEventDestroy(y);
+                return QGCM_E_HIP;
+            }
         ctx->ev_in.push_back(e[0]);
         ctx->ev_kern.push_back(e[1]);
         ctx->ev_out.push_back(e[2]);
