@@ -1,0 +1,37 @@
+"""bench.py's multi-rank path on real hardware: two ranks launched the way the driver launches N GPUs
+(python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N), each sealing and opening
+its own shard with no data-path collective; barrier + max-over-ranks timing; rank 0 prints the one
+JSON line.  A 1-GPU box cannot host two RCCL ranks, so this rehearsal puts both ranks on cuda:0 over
+gloo (--one-device --dist-backend gloo); the RCCL variant is the same code with device_id per rank.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_bench_two_ranks_one_device():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", "29533", os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "3", "--warmup", "1", "--packets", "65536", "--dist-backend", "gloo",
+           "--one-device"]
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout  # rank 0 only
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["status_ok"] is True and line["steps"] == 3
+    assert line["scaling"] == "weak" and line["config"]["packets_per_gpu"] == 65536
+    assert "cpu_baseline" not in line  # rank 0 at N=1 only
+    assert line["value"] > 0
