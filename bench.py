@@ -36,8 +36,8 @@ AAD = bytes([10, 99, 0, 1])
 def parse() -> argparse.Namespace:
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--steps", type=int, default=100)  # ~0.35 s timed: the clocks ramp for ~70 ms after an idle gap
+    p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--packets", type=int, default=1 << 20, help="packets per GPU")
     p.add_argument("--len", type=int, default=1350, help="payload bytes per packet")
     p.add_argument("--stride", type=int, default=0, help="slot stride (0 = smallest 64-B multiple)")
