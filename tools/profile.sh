@@ -3,7 +3,7 @@
 # run, never combined with other trace domains).  Usage: bash tools/profile.sh <tag> [bench args]
 set -u
 TAG=${1:-r1}; shift || true
-ARGS=${*:-"--steps 20 --warmup 3 --no-cpu-baseline"}
+ARGS=${*:-"--no-cpu-baseline"}  # bench.py defaults: 100 timed steps after 10 warmup
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp

@@ -3,7 +3,7 @@
 Prints, per kernel, calls / mean / min duration (from <prof>/trace/*kernel_stats.csv) and, for the
 packet kernels, the mean over the last `timed` launches in <prof>/trace/*kernel_trace.csv (bench.py
 runs `warmup` untimed steps first) -- the figure bench.py's HIP-event kernel_ms must agree with.
-Usage: python tools/trace_summary.py <prof_dir> [timed=20] > <prof_dir>/kernel_stats_summary.txt
+Usage: python tools/trace_summary.py <prof_dir> [timed=100] > <prof_dir>/kernel_stats_summary.txt
 """
 import csv
 import glob
@@ -14,7 +14,7 @@ import sys
 
 def main() -> None:
     prof = sys.argv[1]
-    timed = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+    timed = int(sys.argv[2]) if len(sys.argv) > 2 else 100
     stats = glob.glob(os.path.join(prof, "trace", "*kernel_stats.csv"))[0]
     trace = glob.glob(os.path.join(prof, "trace", "*kernel_trace.csv"))[0]
     print(f"rocprofv3 --kernel-trace --stats -- python3 bench.py (tools/profile.sh), {prof}")
