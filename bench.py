@@ -85,15 +85,17 @@ def stream_copy_gbs(ctx, nbytes: int, dev, stream, reps: int = 5) -> float:
 
 
 def pmc_traffic(kind: str, N: int, L: int, stride: int):
-    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC passes of this
-    command (profiles/r1_final/traffic.json), or None when they are absent or for another workload."""
+    """HBM bytes per launch and LDS-array busy fraction of the dominant kernel from the committed
+    rocprofv3 PMC passes of this command (profiles/r1_s3/traffic.json), or None when they are absent or
+    for another workload."""
     try:
         t = json.load(open(TRAFFIC_JSON))
     except (OSError, ValueError):
-        return None, None
+        return None, None, None
     if t.get("workload") != {"packets": N, "payload_len": L, "slot_stride": stride} or kind not in t["kernels"]:
-        return None, None
-    return t["kernels"][kind]["hbm_bytes"], os.path.relpath(TRAFFIC_JSON, ROOT)
+        return None, None, None
+    k = t["kernels"][kind]
+    return k["hbm_bytes"], k.get("lds_array_busy"), os.path.relpath(TRAFFIC_JSON, ROOT)
 
 
 def main() -> None:
@@ -174,7 +176,7 @@ def main() -> None:
     achieved = N * per_pkt / (kms * 1e-3) / 1e9
     read_pkt = L + 16 if kname == "seal" else L + 32  # the HBM-read-only variant
     achieved_read = N * read_pkt / (kms * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic(kname, N, L, stride)
+    traffic, lds_busy, traffic_src = pmc_traffic(kname, N, L, stride)
     copy_gbs = stream_copy_gbs(ctx, N * stride, dev, stream)  # after the timed region
 
     if rank == 0:
@@ -202,7 +204,8 @@ def main() -> None:
                          "achieved_read_only": round(achieved_read, 1),
                          "copy_achievable": round(copy_gbs, 1),
                          "frac_of_copy": round(achieved / copy_gbs, 4),
-                         "compute_bound_note": "LDS-bound T-table AES + comb GHASH (DESIGN.md 4.1)"},
+                         "binding_unit": "LDS (T-table AES + comb GHASH lookups, DESIGN.md 4.1)",
+                         "lds_array_busy": lds_busy},
             "kernels_ms": {"seal": round(seal_ms, 4), "open": round(open_ms, 4)},
             "status_ok": ok,
         }

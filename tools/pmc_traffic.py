@@ -30,9 +30,13 @@ def per_kernel(prof: str, counter: str) -> dict:
 def main() -> None:
     prof, n, L, stride = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])
     fetch, write = per_kernel(prof, "FETCH_SIZE"), per_kernel(prof, "WRITE_SIZE")
+    # per_kernel scales by 1024 (KiB counters); these two are plain counts
+    lds_idx = {k: [x / 1024.0 for x in v] for k, v in per_kernel(prof, "SQ_LDS_IDX_ACTIVE").items()}
+    grbm = {k: [x / 1024.0 for x in v] for k, v in per_kernel(prof, "GRBM_GUI_ACTIVE").items()}
     res = {"workload": {"packets": n, "payload_len": L, "slot_stride": stride},
            "source": f"{prof}: rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE passes (separate runs) of "
-                     "bench.py; FETCH_SIZE x2 (gfx950 16-B/lane read correction), KiB -> bytes",
+                     "bench.py; FETCH_SIZE x2 (gfx950 16-B/lane read correction), KiB -> bytes; "
+                     "lds_array_busy from the SQ_LDS_IDX_ACTIVE / GRBM_GUI_ACTIVE pass",
            "kernels": {}}
     for (kind, name), vals in fetch.items():
         w = write.get((kind, name), [])
@@ -45,6 +49,12 @@ def main() -> None:
                                 "write_bytes": round(wb), "hbm_bytes": round(fb + wb),
                                 "fetch_over_algorithmic": round(fb / alg_r, 3),
                                 "write_over_algorithmic": round(wb / alg_w, 3)}
+        # the binding unit: LDS-array busy = SQ_LDS_IDX_ACTIVE per CU over the kernel's
+        # cycles per XCD (GRBM_GUI_ACTIVE is summed over the 8 XCDs, SQ_LDS_IDX_ACTIVE over the 256 CUs)
+        lds, gui = lds_idx.get((kind, name)), grbm.get((kind, name))
+        if lds and gui:
+            res["kernels"][kind]["lds_array_busy"] = round((statistics.median(lds) / 256) /
+                                                           (statistics.median(gui) / 8), 3)
     json.dump(res, open(os.path.join(prof, "traffic.json"), "w"), indent=1)
     print(json.dumps(res, indent=1))
 
