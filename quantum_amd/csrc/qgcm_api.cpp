@@ -301,6 +301,16 @@ qgcm_ctx *qgcm_create(int device, uint32_t max_keys, char *err, int errlen) {
         set_err(err, errlen, m);
         return nullptr;
     }
+    {
+        // the kernel variant table (and each kernel's LDS limit) before the variant overrides below
+        // consult it; serialized for contexts created from several threads
+        static std::mutex init_mu;
+        std::lock_guard<std::mutex> g(init_mu);
+        if (init_kernels() != hipSuccess) {
+            set_err(err, errlen, "kernel setup failed");
+            return nullptr;
+        }
+    }
     auto *ctx = new qgcm_ctx();
     ctx->device = device;
     ctx->num_cus = prop.multiProcessorCount;
@@ -308,7 +318,7 @@ qgcm_ctx *qgcm_create(int device, uint32_t max_keys, char *err, int errlen) {
     ctx->key_set.assign(max_keys, 0);
     if (const char *v = getenv("QGCM_VARIANT")) {  // kernel variant overrides (tuning and tests)
         const int iv = atoi(v);
-        if (iv >= 0 && iv < kNumVariants) ctx->uniform_variant = iv;
+        if (iv >= 0 && iv < kNumVariants && !variant_desc(iv)) ctx->uniform_variant = iv;
     }
     if (const char *v = getenv("QGCM_WGS_PER_CU")) ctx->wgs_per_cu_override = atoi(v);
     if (const char *v = getenv("QGCM_PIPE_CHUNK_MB")) ctx->host_chunk = (uint64_t)std::max(1, atoi(v)) << 20;
@@ -328,8 +338,7 @@ qgcm_ctx *qgcm_create(int device, uint32_t max_keys, char *err, int errlen) {
               hipMemcpy(ctx->d_te, te, sizeof te, hipMemcpyHostToDevice) == hipSuccess &&
               hipMemcpy(ctx->d_sbox, sbox, sizeof sbox, hipMemcpyHostToDevice) == hipSuccess &&
               hipStreamCreateWithFlags(&ctx->io_stream, hipStreamNonBlocking) == hipSuccess &&
-              hipEventCreateWithFlags(&ctx->ws_done, hipEventDisableTiming) == hipSuccess &&
-              init_kernels() == hipSuccess;
+              hipEventCreateWithFlags(&ctx->ws_done, hipEventDisableTiming) == hipSuccess;
     for (int k = 0; ok && k < kPipeStreams; ++k)
         ok = hipStreamCreateWithFlags(&ctx->pipe[k], hipStreamNonBlocking) == hipSuccess;
     if (!ok) {
