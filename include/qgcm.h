@@ -45,6 +45,7 @@ extern "C" {
 #define QGCM_PBKDF2_ITERS 10000 /* crypto/aes.go:18 */
 #define QGCM_MAX_PAYLOAD (1u << 28) /* largest plaintext per packet (GCM allows 2^36-32; packets are <= 9000) */
 #define QGCM_ERRLEN 120      /* crypto/dtls.go:23 errorLen */
+#define QGCM_MAX_BATCH (1u << 31) /* packets per batch call (tile indices stay 32-bit); more -> QGCM_E_ARG */
 
 /* status codes */
 #define QGCM_OK 0

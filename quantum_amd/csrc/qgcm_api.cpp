@@ -153,7 +153,7 @@ namespace {
 
 int run_uniform(qgcm_ctx *ctx, bool seal, uint8_t *arena, uint64_t stride, uint32_t n, uint32_t len,
                 uint32_t key_idx, const uint8_t *nonces, uint32_t aad_len, uint8_t *status, hipStream_t s) {
-    if (!ctx || (!arena && n) || aad_len > 4) return QGCM_E_ARG;
+    if (!ctx || (!arena && n) || aad_len > 4 || n > QGCM_MAX_BATCH) return QGCM_E_ARG;
     if (((uintptr_t)arena & 3) || (stride & 3) || (nonces && ((uintptr_t)nonces & 3))) return QGCM_E_ARG;
     if (n && stride < (uint64_t)len + 4 + (seal ? QGCM_OVERHEAD : 0)) return QGCM_E_ARG;
     if ((seal || len >= QGCM_OVERHEAD) && len - (seal ? 0u : (uint32_t)QGCM_OVERHEAD) >= QGCM_MAX_PAYLOAD)
@@ -180,7 +180,7 @@ int run_descs_locked(qgcm_ctx *ctx, bool seal, const qgcm_desc *descs, uint32_t 
 
 int run_descs(qgcm_ctx *ctx, bool seal, uint8_t *arena, const qgcm_desc *descs, uint32_t n, const uint8_t *nonces,
               uint32_t aad_len, uint8_t *status, hipStream_t s) {
-    if (!ctx || (n && (!arena || !descs)) || aad_len > 4) return QGCM_E_ARG;
+    if (!ctx || (n && (!arena || !descs)) || aad_len > 4 || n > QGCM_MAX_BATCH) return QGCM_E_ARG;
     if (((uintptr_t)arena & 3) || (nonces && ((uintptr_t)nonces & 3))) return QGCM_E_ARG;
     if (n == 0) return QGCM_OK;
     if (hipSetDevice(ctx->device) != hipSuccess) return QGCM_E_HIP;
@@ -419,6 +419,7 @@ int qgcm_seal_uniform(qgcm_ctx *ctx, uint8_t *d_arena, uint64_t stride, uint32_t
 
 int qgcm_open_uniform(qgcm_ctx *ctx, uint8_t *d_arena, uint64_t stride, uint32_t n, uint32_t len, uint32_t key_idx,
                       uint32_t aad_len, uint8_t *d_status, void *stream) {
+    if (n > QGCM_MAX_BATCH) return QGCM_E_ARG;
     if (len < QGCM_OVERHEAD && n) {
         // every packet fails Open; the slots stay untouched (ciphertext shorter than the tag)
         if (!ctx) return QGCM_E_ARG;
