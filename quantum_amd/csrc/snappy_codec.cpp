@@ -111,8 +111,23 @@ long qgcm_snappy_compress(const uint8_t *src, size_t n, uint8_t *dst, size_t cap
                 table[h] = (uint16_t)i;
                 if (cand < i && load32(in + cand) == cur) {
                     if (i > emit) op = emit_literal(op, in + emit, i - emit);
+                    // extend the match 8 bytes at a time (the first differing byte from the XOR's
+                    // trailing zeros), then bytewise for the last < 8
                     size_t m = 4;
-                    while (i + m < len && in[cand + m] == in[i + m]) ++m;
+                    for (;;) {
+                        if (i + m + 8 > len) {
+                            while (i + m < len && in[cand + m] == in[i + m]) ++m;
+                            break;
+                        }
+                        uint64_t a, b;
+                        memcpy(&a, in + cand + m, 8);
+                        memcpy(&b, in + i + m, 8);
+                        if (a != b) {
+                            m += (size_t)__builtin_ctzll(a ^ b) >> 3;
+                            break;
+                        }
+                        m += 8;
+                    }
                     op = emit_copy(op, i - cand, m);
                     i += m;
                     emit = i;
