@@ -194,6 +194,9 @@ int qgcm_open_uncompress_host(qgcm_ctx *ctx, uint8_t *h_arena, uint64_t stride, 
  * takes what is queued, up to max_n; returns the count (0 on timeout) or -1.  send returns the
  * number of datagrams sent or -1. */
 int qgcm_udp_socket(const char *ip, int port, int bufbytes);
+/* One queue of a multi-queue socket (socket/udp.go:55-70: one per worker on the same address):
+ * SO_REUSEPORT, so the kernel spreads incoming flows over the queues of the group. */
+int qgcm_udp_queue(const char *ip, int port, int bufbytes);
 int qgcm_udp_port(int fd);
 int qgcm_udp_close(int fd);
 int qgcm_udp_recv_slots(int fd, uint8_t *arena, uint64_t stride, uint32_t max_n, uint32_t *lens, int timeout_ms);

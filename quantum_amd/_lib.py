@@ -25,7 +25,8 @@ EXPORTS = (
     "qgcm_snappy_max_compressed_length", "qgcm_snappy_compress", "qgcm_snappy_uncompressed_length",
     "qgcm_snappy_uncompress", "qgcm_snappy_compress_slots", "qgcm_snappy_uncompress_slots",
     "qgcm_snappy_compress_slots_limit", "qgcm_compress_seal_host", "qgcm_open_uncompress_host",
-    "qgcm_udp_socket", "qgcm_udp_port", "qgcm_udp_close", "qgcm_udp_recv_slots", "qgcm_udp_send_slots",
+    "qgcm_udp_socket", "qgcm_udp_queue", "qgcm_udp_port", "qgcm_udp_close", "qgcm_udp_recv_slots",
+    "qgcm_udp_send_slots",
 )
 
 QGCM_OK = 0
@@ -106,6 +107,7 @@ def _bind(L: C.CDLL) -> None:
     L.qgcm_compress_seal_host.argtypes = [vp, vp, u64, u32, vp, u32, vp, u32, C.c_int, vp]
     L.qgcm_open_uncompress_host.argtypes = [vp, vp, u64, u32, vp, u32, u32, C.c_int, vp]
     L.qgcm_udp_socket.argtypes = [C.c_char_p, C.c_int, C.c_int]
+    L.qgcm_udp_queue.argtypes = [C.c_char_p, C.c_int, C.c_int]
     L.qgcm_udp_port.argtypes = [C.c_int]
     L.qgcm_udp_close.argtypes = [C.c_int]
     L.qgcm_udp_recv_slots.argtypes = [C.c_int, vp, u64, u32, vp, C.c_int]

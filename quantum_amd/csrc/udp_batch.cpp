@@ -55,6 +55,34 @@ int qgcm_udp_socket(const char *ip, int port, int bufbytes) {
     return fd;
 }
 
+// One queue of a multi-queue UDP socket: socket/udp.go:55-70 (newUDP) opens cfg.NumWorkers sockets on
+// the same ListenAddr, one per worker (socket.go:52-77 sets SO_REUSEADDR).  On Linux only SO_REUSEPORT
+// spreads the incoming datagrams over such a group -- by a hash of the sender's address and port, so
+// each flow stays on one queue and in order -- which is what the per-worker queues are for.  Every
+// queue of a group must be opened by the same user; a port of 0 is resolved by the first queue
+// (qgcm_udp_port) and passed to the others.
+int qgcm_udp_queue(const char *ip, int port, int bufbytes) {
+    sockaddr_in a;
+    if (!ip || !make_addr(ip, port, &a)) return -1;
+    const int fd = socket(AF_INET, SOCK_DGRAM | SOCK_CLOEXEC, 0);
+    if (fd < 0) return -1;
+    const int one = 1;
+    if (setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one) != 0 ||
+        setsockopt(fd, SOL_SOCKET, SO_REUSEPORT, &one, sizeof one) != 0) {
+        close(fd);
+        return -1;
+    }
+    if (bufbytes > 0) {
+        setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &bufbytes, sizeof bufbytes);
+        setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &bufbytes, sizeof bufbytes);
+    }
+    if (bind(fd, reinterpret_cast<sockaddr *>(&a), sizeof a) != 0) {
+        close(fd);
+        return -1;
+    }
+    return fd;
+}
+
 int qgcm_udp_port(int fd) {
     sockaddr_in a;
     socklen_t n = sizeof a;

@@ -72,3 +72,45 @@ def test_timeout_truncation_and_bad_args(pair):
     assert L.qgcm_udp_socket(b"not-an-ip", 0, 0) == -1
     assert L.qgcm_udp_send_slots(a, buf.ctypes.data, STRIDE, 1, ln.ctypes.data, b"127.0.0.1", 70000) == -1
     assert L.qgcm_udp_recv_slots(-1, buf.ctypes.data, STRIDE, 1, ln.ctypes.data, 0) == -1
+
+
+def test_multi_queue_spreads_flows():
+    """socket/udp.go:55-70: NumWorkers queues on one address.  Four SO_REUSEPORT queues share a port;
+    eight senders (distinct source ports = distinct flows) each send a numbered run; every datagram
+    arrives exactly once, each flow on a single queue and in order, and more than one queue is used."""
+    L = _lib.lib()
+    q0 = L.qgcm_udp_queue(b"127.0.0.1", 0, 1 << 22)
+    assert q0 >= 0
+    port = L.qgcm_udp_port(q0)
+    queues = [q0] + [L.qgcm_udp_queue(b"127.0.0.1", port, 1 << 22) for _ in range(3)]
+    senders = [L.qgcm_udp_socket(b"127.0.0.1", 0, 1 << 22) for _ in range(8)]
+    try:
+        assert all(q >= 0 for q in queues) and all(s >= 0 for s in senders)
+        per = 24  # per flow: stays inside the default receive buffer
+        for f, s in enumerate(senders):
+            buf = np.zeros(per * STRIDE, np.uint8)
+            lens = np.full(per, 8, np.uint32)
+            for i in range(per):
+                buf[i * STRIDE:i * STRIDE + 8] = np.frombuffer(bytes([f, i]) + bytes(6), np.uint8)
+            assert L.qgcm_udp_send_slots(s, buf.ctypes.data, STRIDE, per, lens.ctypes.data, b"127.0.0.1", port) == per
+        seen = {}  # flow -> (queue, [seq...])
+        total = 0
+        for qi, q in enumerate(queues):
+            dst = np.zeros(256 * STRIDE, np.uint8)
+            ln = np.zeros(256, np.uint32)
+            while True:
+                r = L.qgcm_udp_recv_slots(q, dst.ctypes.data, STRIDE, 256, ln.ctypes.data, 200)
+                if r <= 0:
+                    break
+                for i in range(r):
+                    f, seq = int(dst[i * STRIDE]), int(dst[i * STRIDE + 1])
+                    qq, seqs = seen.setdefault(f, (qi, []))
+                    assert qq == qi  # a flow stays on one queue
+                    seqs.append(seq)
+                total += r
+        assert total == 8 * per
+        assert all(seqs == list(range(per)) for _, seqs in seen.values())
+        assert len({q for q, _ in seen.values()}) > 1
+    finally:
+        for fd in queues + senders:
+            L.qgcm_udp_close(fd)
