@@ -18,7 +18,6 @@
 // fills while one is on the device and callers of the previous one copy out.
 #include <hip/hip_runtime.h>
 #include <string.h>
-#include <sys/random.h>
 
 #include <algorithm>
 #include <chrono>
@@ -114,7 +113,8 @@ void flusher(qgcm_coalescer *c, Lane *ln) {
 
         int rc = QGCM_OK;
         hipStream_t s = ln->stream;
-        if (ln->seal && getrandom(B.h_nonces, 12ull * n, 0) != (ssize_t)(12ull * n)) rc = QGCM_E_ARG;
+        // one draw for the batch (qgcm_random_nonces: getrandom, resumed after partial reads and EINTR)
+        if (ln->seal && qgcm_random_nonces(B.h_nonces, n) != QGCM_OK) rc = QGCM_E_ARG;
         if (rc == QGCM_OK &&
             (hipMemcpyAsync(B.d_arena, B.h_arena, used, hipMemcpyHostToDevice, s) != hipSuccess ||
              hipMemcpyAsync(B.d_descs, B.h_descs, sizeof(qgcm_desc) * n, hipMemcpyHostToDevice, s) != hipSuccess ||

@@ -4,6 +4,7 @@
 // tables, stream plumbing and pinned staging.  All cryptographic work on packets runs on the
 // GPU; there is no CPU fallback -- without a usable HIP device qgcm_create returns NULL.
 #include <hip/hip_runtime.h>
+#include <errno.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -818,6 +819,7 @@ int qgcm_random_nonces(uint8_t *h_out, uint32_t n) {
     uint8_t *p = h_out;
     while (left) {
         const ssize_t r = getrandom(p, left > 33554431 ? 33554431 : left, 0);
+        if (r < 0 && errno == EINTR) continue;  // large requests can be interrupted by a signal
         if (r <= 0) return QGCM_E_ARG;
         p += r;
         left -= (size_t)r;

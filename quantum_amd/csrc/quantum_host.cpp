@@ -2,6 +2,7 @@
 // over the C ABI (include/qgcm.h).  Each function cites the Go it restates.
 #include "../../include/quantum.hpp"
 
+#include <errno.h>
 #include <sys/random.h>
 
 #include <algorithm>
@@ -98,9 +99,12 @@ std::pair<std::shared_ptr<AES>, Error> NewAES(const std::shared_ptr<GPUContext> 
 std::pair<std::vector<uint8_t>, std::vector<uint8_t>> GenerateECKeyPair() {
     std::vector<uint8_t> pub(keyLength), priv(keyLength);
     size_t got = 0;
-    while (got < priv.size()) {
+    while (got < priv.size()) {  // rand.Read: its error is ignored by the reference (ecdh.go:16)
         const ssize_t r = getrandom(priv.data() + got, priv.size() - got, 0);
-        if (r > 0) got += (size_t)r;
+        if (r > 0)
+            got += (size_t)r;
+        else if (r < 0 && errno != EINTR)
+            break;
     }
     qgcm_x25519_base(pub.data(), priv.data());
     return {pub, priv};
