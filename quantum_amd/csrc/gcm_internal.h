@@ -54,6 +54,10 @@ hipError_t launch_quad_worklist(const qgcm_desc *descs, uint32_t n, uint32_t max
                                 size_t ws_bytes, uint32_t **worklist_out, uint32_t **counter_out,
                                 uint32_t *n_items_out, hipStream_t s);
 hipError_t launch_packets(bool seal, int variant, const Batch &b, int grid, hipStream_t s);
+// One packet, one 256-thread workgroup (qgcm_seal_one / qgcm_open_one): the slot (b.stride bytes,
+// a multiple of 16, at most kOneCap - 16) is staged in LDS; b.n must be 1.
+constexpr uint32_t kOneCap = 65536;
+hipError_t launch_one(bool seal, const Batch &b, hipStream_t s);
 hipError_t launch_stream_copy(void *dst, const void *src, uint64_t bytes, int num_cus, hipStream_t s);
 // context accessors for the coalescer (coalescer.cpp), defined in qgcm_api.cpp
 int ctx_device(const qgcm_ctx *ctx);

@@ -917,6 +917,213 @@ gcm_quad_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Latency kernel for ONE packet (qgcm_seal_one / qgcm_open_one, the per-call form of
+// crypto/aes.go:41-62 behind plugin/encryption.go:22-37).  The batch kernels give a packet 1-4
+// lanes and stream it from memory block by block; for a lone packet on pinned host memory that
+// means ~85 serial PCIe round trips and 22-85 serial AES+GHASH steps per MTU packet (55 us of
+// kernel at 1350 B).  Here one 256-thread workgroup
+//  1. stages the whole slot [aad|data|tag|nonce] into LDS with one coalesced wave of 16-B loads
+//     (one PCIe round trip) while it fills the T-tables and the comb table of H^4;
+//  2. runs every counter block on its own thread (block j on thread j mod 256; block d = E_K(J0));
+//  3. runs GHASH as the quad kernel's four interleaved Horner chains (lanes 0-3 of wave 0, comb
+//     table of H^4 in LDS, recombined by H^2..H^5 from the key table);
+//  4. writes the slot back with one wave of 16-B stores.
+// Open computes GHASH over the staged ciphertext first and decrypts only when the tag matches
+// (zeroed plaintext otherwise, as Go 1.9 Open).
+// LDS: [0, 64K) Te, [64K, 72K) comb of H^4, [72K, 72K + kOneCap) the slot at +12 (payload
+// 16-B aligned), then 64 B of scratch (E_K(J0), the GHASH value, the verdict).
+constexpr uint32_t kOneThreads = 256;
+constexpr uint32_t kOneBuf = kTeBytes + kGhBytes;
+constexpr uint32_t kOneScratch = kOneBuf + kOneCap;
+constexpr uint32_t kOneLds = kOneScratch + 64;
+static_assert(kOneLds <= 160u * 1024u, "gfx950 LDS is 160 KiB per workgroup");
+
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+__device__ __forceinline__ uint32_t lds8(uint32_t addr) { return *(const lds_u8 *)(size_t)addr; }
+__device__ __forceinline__ void lds_st8(uint32_t addr, uint32_t v) { *(lds_u8 *)(size_t)addr = (uint8_t)v; }
+// little-endian word at any LDS byte address
+__device__ __forceinline__ uint32_t lds32u(uint32_t a) {
+    return lds8(a) | lds8(a + 1) << 8 | lds8(a + 2) << 16 | lds8(a + 3) << 24;
+}
+__device__ __forceinline__ void lds_st32u(uint32_t a, uint32_t v) {
+    lds_st8(a, v);
+    lds_st8(a + 1, v >> 8);
+    lds_st8(a + 2, v >> 16);
+    lds_st8(a + 3, v >> 24);
+}
+// byte mask of the first r (< 16) bytes of a block, as four LE words
+__device__ __forceinline__ void block_mask(uint32_t r, uint32_t &m0, uint32_t &m1, uint32_t &m2, uint32_t &m3) {
+    const uint32_t q = r >> 2, sb = r & 3u;
+    m0 = q > 0 ? 0xffffffffu : lowmask(sb);
+    m1 = q > 1 ? 0xffffffffu : (q == 1 ? lowmask(sb) : 0u);
+    m2 = q > 2 ? 0xffffffffu : (q == 2 ? lowmask(sb) : 0u);
+    m3 = q == 3 ? lowmask(sb) : 0u;
+}
+
+// b.arena = the slot (16-B aligned), b.uniform_len = L (seal) or L + 28 (open), b.stride = the
+// slot bytes staged (multiple of 16, >= 4 + L + 28, <= kOneCap - 16), b.status[0] = verdict.
+template <bool kSeal>
+__global__ void __launch_bounds__(kOneThreads) gcm_one_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63u;
+    const uint32_t L = kSeal ? b.uniform_len : b.uniform_len - QGCM_OVERHEAD;
+    const uint32_t A = kOneBuf + 12u, P = kOneBuf + 16u;  // slot base (AAD), payload base
+    const uint32_t n16 = (uint32_t)(b.stride >> 4);
+    const uint4 *gslot = reinterpret_cast<const uint4 *>(b.arena);
+    // 1. stage the slot: every load issued before the table fill, so the PCIe round trip overlaps it
+    uint4 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t i = tid + k * kOneThreads;
+        if (i < n16) v[k] = gslot[i];
+    }
+    for (uint32_t i = tid; i < kTeBytes / 16; i += kOneThreads) {  // Te0/Te1, 32 replicas per row
+        const uint32_t x = i >> 4, half = (i >> 3) & 1u;
+        const uint32_t t = b.te[half * 256u + x];
+        lds_st128(16 * i, uint4{t, t, t, t});
+    }
+    const uint4 *gh = b.gh_table + (size_t)b.uniform_key * kGhEntries;
+    for (uint32_t e = tid; e < 512u; e += kOneThreads) lds_st_comb<false>(kTeBytes, e, gh[kGhH4 + e]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t i = tid + k * kOneThreads;
+        if (i < n16) {
+            const uint32_t a = A + 16 * i;
+            lds_st32(a, v[k].x);
+            lds_st32(a + 4, v[k].y);
+            lds_st32(a + 8, v[k].z);
+            lds_st32(a + 12, v[k].w);
+        }
+    }
+    for (uint32_t i = tid + 4 * kOneThreads; i < n16; i += kOneThreads) {  // slots over 16 KiB
+        const uint4 w = gslot[i];
+        const uint32_t a = A + 16 * i;
+        lds_st32(a, w.x);
+        lds_st32(a + 4, w.y);
+        lds_st32(a + 8, w.z);
+        lds_st32(a + 12, w.w);
+    }
+    __syncthreads();
+
+    const Keys kk = {rk_table + (size_t)b.uniform_key * kRkWords, rk_table + (size_t)b.uniform_key * kRkWords + 64};
+    const uint32_t lb = (lane & 31u) << 2;
+    const uint32_t nfull = L >> 4, r = L & 15u;
+    const uint32_t d = nfull + (r ? 1u : 0u);
+    const uint32_t n0 = lds32u(P + L + 16), n1 = lds32u(P + L + 20), n2 = lds32u(P + L + 24);
+    uint32_t m0, m1, m2, m3;
+    block_mask(r, m0, m1, m2, m3);
+
+    // 2. counter blocks: block j < d XORs its keystream into the staged payload; block d is E_K(J0)
+    // mode 0: payload blocks and J0; 1: payload blocks only; 2: J0 only (thread 64, wave 1)
+    auto ctr_pass = [&](int mode) {
+        const uint32_t j_first = mode == 2 ? (tid == 64 ? d : d + 1) : tid;
+        const uint32_t j_end = mode == 1 ? d : d + 1;
+        for (uint32_t j = j_first; j < j_end; j += kOneThreads) {
+            const uint32_t ctr = j == d ? 1u : j + 2u;  // J0, or inc32(J0) + j
+            Ctr cc;
+            ctr_setup(cc, n0, n1, n2, ctr >> 8, kk, lb);
+            uint32_t k0, k1, k2, k3;
+            ctr_block(cc, ctr & 0xffu, kk, lb, k0, k1, k2, k3);
+            if (j == d) {
+                lds_st128(kOneScratch, uint4{k0, k1, k2, k3});
+            } else {
+                if (j == nfull) {  // partial block: the bytes past L (tag area) stay as they are
+                    k0 &= m0;
+                    k1 &= m1;
+                    k2 &= m2;
+                    k3 &= m3;
+                }
+                const uint4 in = lds128(P + 16 * j);
+                lds_st128(P + 16 * j, uint4{in.x ^ k0, in.y ^ k1, in.z ^ k2, in.w ^ k3});
+            }
+        }
+    };
+    // 3. GHASH over the staged ciphertext (lanes 0-3 of wave 0), tag into scratch + 16
+    auto ghash = [&]() {
+        if (tid < 4) {
+            const uint32_t m = tid;
+            uint32_t z0 = 0, z1 = 0, z2 = 0, z3 = 0;
+            if (m == 3 && b.aad_len) z0 = lds32(A) & (b.aad_len >= 4 ? 0xffffffffu : lowmask(b.aad_len));
+            int blast = -1;
+            for (uint32_t bi = m; bi < d; bi += 4) {
+                uint4 c = lds128(P + 16 * bi);
+                if (bi == nfull) {
+                    c.x &= m0;
+                    c.y &= m1;
+                    c.z &= m2;
+                    c.w &= m3;
+                }
+                ghash_mul<false>(z0, z1, z2, z3, kTeBytes);
+                z0 ^= c.x;
+                z1 ^= c.y;
+                z2 ^= c.z;
+                z3 ^= c.w;
+                blast = (int)bi;
+            }
+            const uint32_t em = d + 1u - (uint32_t)blast;  // in [2, 5], as quad_packet
+            const uint32_t tsel = em == 2 ? kGhH2 : em == 3 ? kGhH3 : em == 4 ? kGhH4 : kGhH5;
+            ghash_mul_global(z0, z1, z2, z3, gh + tsel);
+            uint32_t l0, l1, l2, l3;
+            ghash_lenblock_global(b.aad_len, L, gh, l0, l1, l2, l3);
+            z0 = quad_xor(z0) ^ l0;
+            z1 = quad_xor(z1) ^ l1;
+            z2 = quad_xor(z2) ^ l2;
+            z3 = quad_xor(z3) ^ l3;
+            if (m == 0) lds_st128(kOneScratch + 16, uint4{z0, z1, z2, z3});
+        }
+    };
+
+    if (kSeal) {
+        ctr_pass(0);
+        __syncthreads();
+        ghash();
+        __syncthreads();
+        if (tid == 0) {
+            const uint4 e = lds128(kOneScratch), y = lds128(kOneScratch + 16);
+            lds_st32u(P + L, e.x ^ y.x);
+            lds_st32u(P + L + 4, e.y ^ y.y);
+            lds_st32u(P + L + 8, e.z ^ y.z);
+            lds_st32u(P + L + 12, e.w ^ y.w);
+            if (b.status) b.status[0] = 1;
+        }
+    } else {
+        ghash();
+        ctr_pass(2);  // E_K(J0) on wave 1 while wave 0 hashes
+        __syncthreads();
+        const uint4 e = lds128(kOneScratch), y = lds128(kOneScratch + 16);
+        const bool ok = ((e.x ^ y.x ^ lds32u(P + L)) | (e.y ^ y.y ^ lds32u(P + L + 4)) |
+                         (e.z ^ y.z ^ lds32u(P + L + 8)) | (e.w ^ y.w ^ lds32u(P + L + 12))) == 0;
+        if (ok) {
+            ctr_pass(1);
+        } else {  // Go 1.9 crypto/cipher gcm Open: zero the would-be plaintext on tag mismatch
+            for (uint32_t j = tid; j < d; j += kOneThreads) {
+                const uint4 in = lds128(P + 16 * j);
+                const uint4 z = j == nfull ? uint4{in.x & ~m0, in.y & ~m1, in.z & ~m2, in.w & ~m3} : uint4{0, 0, 0, 0};
+                lds_st128(P + 16 * j, z);
+            }
+        }
+        if (tid == 0 && b.status) b.status[0] = ok ? 1 : 0;
+    }
+    __syncthreads();
+    // 4. write the slot back (the bytes outside the payload/tag are rewritten unchanged)
+    uint4 *oslot = reinterpret_cast<uint4 *>(b.arena);
+    for (uint32_t i = tid; i < n16; i += kOneThreads) {
+        const uint32_t a = A + 16 * i;
+        oslot[i] = uint4{lds32(a), lds32(a + 4), lds32(a + 8), lds32(a + 12)};
+    }
+}
+
+hipError_t launch_one(bool seal, const Batch &b, hipStream_t s) {
+    if (b.n != 1 || (b.stride & 15) || b.stride > kOneCap - 16 || ((uintptr_t)b.arena & 15)) return hipErrorInvalidValue;
+    const uint32_t L = seal ? b.uniform_len : b.uniform_len - QGCM_OVERHEAD;
+    if ((!seal && b.uniform_len < QGCM_OVERHEAD) || b.stride < 4ull + L + QGCM_OVERHEAD) return hipErrorInvalidValue;
+    void *args[] = {const_cast<Batch *>(&b), const_cast<uint32_t **>(&b.rk_table)};
+    const void *k = seal ? reinterpret_cast<const void *>(&gcm_one_kernel<true>)
+                         : reinterpret_cast<const void *>(&gcm_one_kernel<false>);
+    return hipLaunchKernel(k, dim3(1), dim3(kOneThreads), args, kOneLds, s);
+}
+
 // Variant table: index = QGCM variant id (Batch-independent), see qgcm_api.cpp.
 struct Variant {
     const void *seal, *open;
@@ -973,6 +1180,15 @@ hipError_t init_kernels() {
             e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, v.lds);
             if (e != hipSuccess) return e;
         }
+    }
+    for (const void *k : {reinterpret_cast<const void *>(&gcm_one_kernel<true>),
+                          reinterpret_cast<const void *>(&gcm_one_kernel<false>)}) {
+        hipFuncAttributes a;
+        hipError_t e = hipFuncGetAttributes(&a, k);
+        if (e != hipSuccess) return e;
+        if (a.sharedSizeBytes != 0) return hipErrorInvalidKernelFile;
+        e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kOneLds);
+        if (e != hipSuccess) return e;
     }
     return hipSuccess;
 }

@@ -35,6 +35,7 @@ struct qgcm_ctx {
     int uniform_variant = kVariantUniform;  // kernel variant for single-key batches (QGCM_VARIANT)
     int desc_variant = kVariantDescQuad;    // kernel variant for descriptor batches (QGCM_DESC_VARIANT)
     int wgs_per_cu_override = 0;            // persistent-grid workgroups per CU (QGCM_WGS_PER_CU, tuning)
+    bool one_kernel = true;                 // seal_one/open_one use the latency kernel (QGCM_ONE_KERNEL)
     uint32_t *d_rk = nullptr;
     uint4 *d_gh = nullptr;
     uint32_t *d_te = nullptr;
@@ -137,6 +138,28 @@ Batch base_batch(const qgcm_ctx *ctx) {
     b.te = ctx->d_te;
     b.max_keys = ctx->max_keys;
     return b;
+}
+
+int run_uniform(qgcm_ctx *ctx, bool seal, uint8_t *arena, uint64_t stride, uint32_t n, uint32_t len,
+                uint32_t key_idx, const uint8_t *nonces, uint32_t aad_len, uint8_t *status, hipStream_t s);
+
+// seal_one / open_one: the latency kernel when the slot fits its LDS staging area, else the batch
+// kernel on a batch of one (QGCM_ONE_KERNEL=0 forces the latter, for A/B runs).
+int run_one(qgcm_ctx *ctx, bool seal, uint8_t *slot, uint64_t stride, uint32_t len, uint32_t key_idx,
+            uint32_t aad_len, uint8_t *status, hipStream_t s) {
+    if (ctx->one_kernel && stride <= kOneCap - 16 && !(stride & 15) && !((uintptr_t)slot & 15)) {
+        Batch b = base_batch(ctx);
+        b.arena = slot;
+        b.status = status;
+        b.stride = stride;
+        b.uniform_len = len;
+        b.uniform_key = key_idx;
+        b.n = 1;
+        b.n_items = 64;
+        b.aad_len = aad_len;
+        return hip_fail(launch_one(seal, b, s));
+    }
+    return run_uniform(ctx, seal, slot, stride, 1, len, key_idx, nullptr, aad_len, status, s);
 }
 
 bool key_ok(qgcm_ctx *ctx, uint32_t k) {
@@ -322,6 +345,7 @@ qgcm_ctx *qgcm_create(int device, uint32_t max_keys, char *err, int errlen) {
         if (iv >= 0 && iv < kNumVariants && !variant_desc(iv)) ctx->uniform_variant = iv;
     }
     if (const char *v = getenv("QGCM_WGS_PER_CU")) ctx->wgs_per_cu_override = atoi(v);
+    if (const char *v = getenv("QGCM_ONE_KERNEL")) ctx->one_kernel = atoi(v) != 0;
     if (const char *v = getenv("QGCM_PIPE_CHUNK_MB")) ctx->host_chunk = (uint64_t)std::max(1, atoi(v)) << 20;
     if (const char *v = getenv("QGCM_PIPE_RING_MB")) ctx->host_ring = (uint64_t)std::max(1, atoi(v)) << 20;
     if (const char *v = getenv("QGCM_DESC_VARIANT")) {
@@ -456,7 +480,7 @@ long qgcm_seal_one(qgcm_ctx *ctx, uint32_t key_idx, uint8_t *data, long length, 
     // setups; the copy-in / copy-out form took ~3x longer per call)
     hipStream_t s = ctx->io_stream;
     h[stride] = 0;
-    if (run_uniform(ctx, true, h, stride, 1, (uint32_t)length, key_idx, nullptr, aad_len, h + stride, s) != QGCM_OK ||
+    if (run_one(ctx, true, h, stride, (uint32_t)length, key_idx, aad_len, h + stride, s) != QGCM_OK ||
         hipStreamSynchronize(s) != hipSuccess)
         return -1;
     if (h[stride] != 1) return -1;
@@ -478,7 +502,7 @@ long qgcm_open_one(qgcm_ctx *ctx, uint32_t key_idx, uint8_t *data, long len, con
     memcpy(h + 4, data, (size_t)len);
     hipStream_t s = ctx->io_stream;  // zero-copy on the pinned staging slot, as qgcm_seal_one
     h[stride] = 0;
-    if (run_uniform(ctx, false, h, stride, 1, (uint32_t)len, key_idx, nullptr, aad_len, h + stride, s) != QGCM_OK ||
+    if (run_one(ctx, false, h, stride, (uint32_t)len, key_idx, aad_len, h + stride, s) != QGCM_OK ||
         hipStreamSynchronize(s) != hipSuccess)
         return -1;
     memcpy(data, h + 4, (size_t)len - QGCM_OVERHEAD);  // plaintext, or zeros on auth failure
