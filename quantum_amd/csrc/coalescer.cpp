@@ -66,6 +66,7 @@ struct qgcm_coalescer {
     qgcm_ctx *ctx = nullptr;
     int device = 0;
     uint32_t max_batch = 0, max_packet = 0, aad_len = 4;
+    bool one_kernel = false;  // small batches through the latency kernel (slots fit its LDS staging)
     std::chrono::microseconds max_wait{0}, quiet{0};
     uint64_t cap_bytes = 0;
     bool stop = false;
@@ -115,18 +116,25 @@ void flusher(qgcm_coalescer *c, Lane *ln) {
         hipStream_t s = ln->stream;
         // one draw for the batch (qgcm_random_nonces: getrandom, resumed after partial reads and EINTR)
         if (ln->seal && qgcm_random_nonces(B.h_nonces, n) != QGCM_OK) rc = QGCM_E_ARG;
-        if (rc == QGCM_OK &&
-            (hipMemcpyAsync(B.d_arena, B.h_arena, used, hipMemcpyHostToDevice, s) != hipSuccess ||
-             hipMemcpyAsync(B.d_descs, B.h_descs, sizeof(qgcm_desc) * n, hipMemcpyHostToDevice, s) != hipSuccess ||
-             (ln->seal && hipMemcpyAsync(B.d_nonces, B.h_nonces, 12ull * n, hipMemcpyHostToDevice, s) != hipSuccess)))
-            rc = QGCM_E_HIP;
-        if (rc == QGCM_OK)
-            rc = ln->seal ? qgcm_seal_batch(c->ctx, B.d_arena, B.d_descs, n, B.d_nonces, c->aad_len, B.d_status, s)
-                          : qgcm_open_batch(c->ctx, B.d_arena, B.d_descs, n, c->aad_len, B.d_status, s);
-        if (rc == QGCM_OK &&
-            (hipMemcpyAsync(B.h_arena, B.d_arena, used, hipMemcpyDeviceToHost, s) != hipSuccess ||
-             hipMemcpyAsync(B.h_status, B.d_status, n, hipMemcpyDeviceToHost, s) != hipSuccess))
-            rc = QGCM_E_HIP;
+        const bool one = c->one_kernel && n <= qgcm::kOneBatchMax;
+        if (rc == QGCM_OK && one) {
+            // small batch: one latency-kernel workgroup per packet, zero-copy on the pinned batch
+            // (one launch instead of H2D copies + worklist build + batch kernel + D2H copies)
+            rc = qgcm::run_one_descs(c->ctx, ln->seal, B.h_arena, B.h_descs, n, ln->seal ? B.h_nonces : nullptr,
+                                     c->aad_len, B.h_status, s);
+        } else if (rc == QGCM_OK) {
+            if (hipMemcpyAsync(B.d_arena, B.h_arena, used, hipMemcpyHostToDevice, s) != hipSuccess ||
+                hipMemcpyAsync(B.d_descs, B.h_descs, sizeof(qgcm_desc) * n, hipMemcpyHostToDevice, s) != hipSuccess ||
+                (ln->seal && hipMemcpyAsync(B.d_nonces, B.h_nonces, 12ull * n, hipMemcpyHostToDevice, s) != hipSuccess))
+                rc = QGCM_E_HIP;
+            if (rc == QGCM_OK)
+                rc = ln->seal ? qgcm_seal_batch(c->ctx, B.d_arena, B.d_descs, n, B.d_nonces, c->aad_len, B.d_status, s)
+                              : qgcm_open_batch(c->ctx, B.d_arena, B.d_descs, n, c->aad_len, B.d_status, s);
+            if (rc == QGCM_OK &&
+                (hipMemcpyAsync(B.h_arena, B.d_arena, used, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                 hipMemcpyAsync(B.h_status, B.d_status, n, hipMemcpyDeviceToHost, s) != hipSuccess))
+                rc = QGCM_E_HIP;
+        }
         if (hipStreamSynchronize(s) != hipSuccess) rc = QGCM_E_HIP;
 
         lk.lock();
@@ -244,6 +252,7 @@ qgcm_coalescer *qgcm_coalescer_create(qgcm_ctx *ctx, uint32_t max_batch, uint32_
     c->max_wait = std::chrono::microseconds(max_wait_us);
     c->quiet = std::chrono::microseconds(max_wait_us / 8 > 5 ? max_wait_us / 8 : 5);
     c->cap_bytes = (uint64_t)max_batch * slot_bytes(true, max_packet);
+    c->one_kernel = qgcm::ctx_one_kernel(ctx) && slot_bytes(true, max_packet) <= qgcm::kOneCap - 16;
     bool ok = hipSetDevice(c->device) == hipSuccess;
     for (int d = 0; d < 2 && ok; ++d) {
         Lane &ln = c->lanes[d];

@@ -15,10 +15,12 @@ constexpr uint32_t kGhBytes = 8192;
 // Device key slot: 60 round-key words (+4 pad), their rot16 copies, and the 4-bit comb tables of
 // H and H^4 (2 x 512 x 16 B).
 constexpr uint32_t kRkWords = 128;  // [0,64): rk words, [64,128): rot16(rk)
-// Per key: five 4-bit comb tables of 512 x 16 B: H, H^4 (the Horner step of the quad kernel), then
-// H^2, H^3, H^5 (the once-per-packet recombination multiplies, read from global memory).
-constexpr uint32_t kGhEntries = 2560;
+// Per key: nine 4-bit comb tables of 512 x 16 B: H, H^4 (the Horner step of the quad kernel), then
+// H^2, H^3, H^5 (the once-per-packet recombination multiplies, read from global memory), then
+// H^8, H^16, H^32, H^64 (the latency kernel's 64-way GHASH; the batch kernels never read them).
+constexpr uint32_t kGhEntries = 4608;
 constexpr uint32_t kGhH = 0, kGhH4 = 512, kGhH2 = 1024, kGhH3 = 1536, kGhH5 = 2048;
+constexpr uint32_t kGhH8 = 2560, kGhH16 = 3072, kGhH32 = 3584, kGhH64 = 4096;
 
 struct Batch {
     uint8_t *arena;
@@ -56,8 +58,14 @@ hipError_t launch_quad_worklist(const qgcm_desc *descs, uint32_t n, uint32_t max
 hipError_t launch_packets(bool seal, int variant, const Batch &b, int grid, hipStream_t s);
 // One packet, one 256-thread workgroup (qgcm_seal_one / qgcm_open_one): the slot (b.stride bytes,
 // a multiple of 16, at most kOneCap - 16) is staged in LDS; b.n must be 1.
-constexpr uint32_t kOneCap = 65536;
+constexpr uint32_t kOneCap = 32768;
 hipError_t launch_one(bool seal, const Batch &b, hipStream_t s);
+// Small descriptor batches through the latency kernel, one workgroup per packet, straight on the
+// caller's (pinned host or device) arena/descriptors/nonces/status -- the coalescer's flush path.
+constexpr uint32_t kOneBatchMax = 1024;
+int run_one_descs(qgcm_ctx *ctx, bool seal, uint8_t *arena, const qgcm_desc *descs, uint32_t n,
+                  const uint8_t *nonces, uint32_t aad_len, uint8_t *status, hipStream_t s);
+bool ctx_one_kernel(const qgcm_ctx *ctx);
 hipError_t launch_stream_copy(void *dst, const void *src, uint64_t bytes, int num_cus, hipStream_t s);
 // context accessors for the coalescer (coalescer.cpp), defined in qgcm_api.cpp
 int ctx_device(const qgcm_ctx *ctx);

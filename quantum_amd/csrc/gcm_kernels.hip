@@ -190,7 +190,8 @@ __device__ __forceinline__ void ctr_blocks(const Ctr &c, uint32_t lo, const Keys
 // Y <- Y * H in GF(2^128) via the 4-bit comb in this wave's LDS table at gb (byte1/2 of gb hold
 // its base; byte0 is 0).  Entry (p, v) at gb + p*256 + v*16, p = nibble position (2*byte for the
 // high nibble, 2*byte+1 for the low one), v = nibble value.
-template <bool kB64 = false>
+// kFence = false (latency kernel, one wave): no chunk fences, so all 32 lookups can be in flight.
+template <bool kB64 = false, bool kFence = true>
 __device__ __forceinline__ void ghash_mul(uint32_t &y0, uint32_t &y1, uint32_t &y2, uint32_t &y3, uint32_t gb) {
     uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
     const uint32_t yw[4] = {y0, y1, y2, y3};
@@ -228,7 +229,7 @@ __device__ __forceinline__ void ghash_mul(uint32_t &y0, uint32_t &y1, uint32_t &
         }
         // chunk fence: the accumulators are consumed here and the next chunk's LDS loads cannot be
         // hoisted above it, so at most 8 x 16 B of table rows are live at once
-        asm volatile("" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3)::"memory");
+        if constexpr (kFence) asm volatile("" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3)::"memory");
     }
     y0 = a0;
     y1 = a1;
@@ -926,15 +927,20 @@ gcm_quad_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
 //  1. stages the whole slot [aad|data|tag|nonce] into LDS with one coalesced wave of 16-B loads
 //     (one PCIe round trip) while it fills the T-tables and the comb table of H^4;
 //  2. runs every counter block on its own thread (block j on thread j mod 256; block d = E_K(J0));
-//  3. runs GHASH as the quad kernel's four interleaved Horner chains (lanes 0-3 of wave 0, comb
-//     table of H^4 in LDS, recombined by H^2..H^5 from the key table);
+//  3. runs GHASH on the 64 lanes of wave 0: lane m owns the blocks whose exponent in
+//     Y = sum_i B_i H^(N+1-i) is m + 2 mod 64 (the AAD block included), a Horner chain by H^64,
+//     then sum_m Z_m H^m by six radix-2 Estrin levels (multiply by H^(2^l), add the partner lane's
+//     value), then Y = S H^2 + [len(A)]||[len(C)] H -- 2 + 7 serial multiplies at 1350 B where the
+//     quad chains took 23, 16 at 9000 B where they took 142.  The seven comb tables (H^(2^l),
+//     l = 0..6) sit in LDS;
 //  4. writes the slot back with one wave of 16-B stores.
 // Open computes GHASH over the staged ciphertext first and decrypts only when the tag matches
 // (zeroed plaintext otherwise, as Go 1.9 Open).
-// LDS: [0, 64K) Te, [64K, 72K) comb of H^4, [72K, 72K + kOneCap) the slot at +12 (payload
-// 16-B aligned), then 64 B of scratch (E_K(J0), the GHASH value, the verdict).
+// LDS: [0, 64K) Te, [64K, 120K) comb tables of H^(2^l), [120K, 120K + kOneCap) the slot at +12
+// (payload 16-B aligned), then 64 B of scratch (E_K(J0), the GHASH value).
 constexpr uint32_t kOneThreads = 256;
-constexpr uint32_t kOneBuf = kTeBytes + kGhBytes;
+constexpr uint32_t kOneTabs = 7;
+constexpr uint32_t kOneBuf = kTeBytes + kOneTabs * kGhBytes;
 constexpr uint32_t kOneScratch = kOneBuf + kOneCap;
 constexpr uint32_t kOneLds = kOneScratch + 64;
 static_assert(kOneLds <= 160u * 1024u, "gfx950 LDS is 160 KiB per workgroup");
@@ -961,16 +967,36 @@ __device__ __forceinline__ void block_mask(uint32_t r, uint32_t &m0, uint32_t &m
     m3 = q == 3 ? lowmask(sb) : 0u;
 }
 
-// b.arena = the slot (16-B aligned), b.uniform_len = L (seal) or L + 28 (open), b.stride = the
-// slot bytes staged (multiple of 16, >= 4 + L + 28, <= kOneCap - 16), b.status[0] = verdict.
+// One workgroup per packet.  Uniform form (b.descs == NULL, b.n == 1): b.arena = the slot,
+// b.uniform_len = L (seal) or L + 28 (open), b.uniform_key.  Descriptor form (the coalescer's small
+// batches): packet blockIdx.x is b.descs[blockIdx.x] in b.arena.  Slots are 16-B aligned and
+// (4 + len (+ 28 for seal) + 15) & ~15 bytes long, at most kOneCap - 16; seal nonces come from
+// b.nonces (12 B per packet) when it is set, else from the slot.  b.status[packet] = verdict.
 template <bool kSeal>
 __global__ void __launch_bounds__(kOneThreads) gcm_one_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
-    const uint32_t L = kSeal ? b.uniform_len : b.uniform_len - QGCM_OVERHEAD;
+    const uint32_t pkt = blockIdx.x;
+    uint64_t off = 0;
+    uint32_t Lin = b.uniform_len, key = b.uniform_key;
+    if (b.descs) {
+        const qgcm_desc dsc = b.descs[pkt];
+        off = dsc.offset;
+        Lin = dsc.len;
+        key = dsc.key_idx;
+    }
+    const uint32_t n16 = (uint32_t)((4ull + Lin + (kSeal ? QGCM_OVERHEAD : 0) + 15) >> 4);
+    // as the batch kernels: a key index out of range or an open shorter than 28 B fails the packet
+    // (slot untouched); so does a slot past the LDS staging area or misaligned (the host never sends one)
+    if (key >= b.max_keys || (!kSeal && Lin < (uint32_t)QGCM_OVERHEAD) || Lin >= kOneCap || n16 * 16u > kOneCap - 16u ||
+        (off & 15u)) {
+        if (tid == 0 && b.status) b.status[pkt] = 0;
+        return;
+    }
+    const uint32_t L = kSeal ? Lin : Lin - QGCM_OVERHEAD;
     const uint32_t A = kOneBuf + 12u, P = kOneBuf + 16u;  // slot base (AAD), payload base
-    const uint32_t n16 = (uint32_t)(b.stride >> 4);
-    const uint4 *gslot = reinterpret_cast<const uint4 *>(b.arena);
+    uint8_t *slot = b.arena + off;
+    const uint4 *gslot = reinterpret_cast<const uint4 *>(slot);
     // 1. stage the slot: every load issued before the table fill, so the PCIe round trip overlaps it
     uint4 v[4];
 #pragma unroll
@@ -983,8 +1009,18 @@ __global__ void __launch_bounds__(kOneThreads) gcm_one_kernel(Batch b, const uin
         const uint32_t t = b.te[half * 256u + x];
         lds_st128(16 * i, uint4{t, t, t, t});
     }
-    const uint4 *gh = b.gh_table + (size_t)b.uniform_key * kGhEntries;
-    for (uint32_t e = tid; e < 512u; e += kOneThreads) lds_st_comb<false>(kTeBytes, e, gh[kGhH4 + e]);
+    const uint4 *gh = b.gh_table + (size_t)key * kGhEntries;
+    // table l = comb of H^(2^l); only the ones this packet's GHASH reads (H and H^2 always, the
+    // Estrin levels up to bit-length(min(d, 63)), H^64 once a lane owns two blocks)
+    const uint32_t dd = (L + 15u) >> 4;
+    const uint32_t dtop = dd < 63u ? dd : 63u;
+    const uint32_t ntabs = dd >= 64u ? kOneTabs : (dtop > 3u ? 32u - __builtin_clz(dtop) : 2u);
+    for (uint32_t i = tid; i < kOneTabs * 512u; i += kOneThreads) {
+        const uint32_t l = i >> 9, e = i & 511u;
+        if (l >= ntabs) break;
+        const uint32_t src = l == 0 ? kGhH : l == 1 ? kGhH2 : l == 2 ? kGhH4 : kGhH8 + (l - 3) * 512u;
+        lds_st_comb<false>(kTeBytes + l * kGhBytes, e, gh[src + e]);
+    }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const uint32_t i = tid + k * kOneThreads;
@@ -1006,11 +1042,21 @@ __global__ void __launch_bounds__(kOneThreads) gcm_one_kernel(Batch b, const uin
     }
     __syncthreads();
 
-    const Keys kk = {rk_table + (size_t)b.uniform_key * kRkWords, rk_table + (size_t)b.uniform_key * kRkWords + 64};
+    const Keys kk = {rk_table + (size_t)key * kRkWords, rk_table + (size_t)key * kRkWords + 64};
     const uint32_t lb = (lane & 31u) << 2;
     const uint32_t nfull = L >> 4, r = L & 15u;
     const uint32_t d = nfull + (r ? 1u : 0u);
-    const uint32_t n0 = lds32u(P + L + 16), n1 = lds32u(P + L + 20), n2 = lds32u(P + L + 24);
+    uint32_t n0, n1, n2;
+    if (kSeal && b.nonces) {  // the nonce goes into the slot with the tag
+        const uint32_t *np = reinterpret_cast<const uint32_t *>(b.nonces + 12ull * pkt);
+        n0 = np[0];
+        n1 = np[1];
+        n2 = np[2];
+    } else {
+        n0 = lds32u(P + L + 16);
+        n1 = lds32u(P + L + 20);
+        n2 = lds32u(P + L + 24);
+    }
     uint32_t m0, m1, m2, m3;
     block_mask(r, m0, m1, m2, m3);
 
@@ -1039,37 +1085,54 @@ __global__ void __launch_bounds__(kOneThreads) gcm_one_kernel(Batch b, const uin
             }
         }
     };
-    // 3. GHASH over the staged ciphertext (lanes 0-3 of wave 0), tag into scratch + 16
+    // 3. GHASH over the staged ciphertext (wave 0), the hash into scratch + 16
     auto ghash = [&]() {
-        if (tid < 4) {
-            const uint32_t m = tid;
+        if (tid < 64) {
+            const uint32_t m = lane;
             uint32_t z0 = 0, z1 = 0, z2 = 0, z3 = 0;
-            if (m == 3 && b.aad_len) z0 = lds32(A) & (b.aad_len >= 4 ? 0xffffffffu : lowmask(b.aad_len));
-            int blast = -1;
-            for (uint32_t bi = m; bi < d; bi += 4) {
+            const bool aad_lane = m == (d & 63u) && b.aad_len;
+            if (aad_lane) z0 = lds32(A) & (b.aad_len >= 4 ? 0xffffffffu : lowmask(b.aad_len));
+            // blocks bi = d-1-m-64k >= 0, in increasing order: exponent d+1-bi = m+2 (mod 64) at the end
+            const uint32_t first = (d - 1u - m) & 63u;
+            for (uint32_t bi = first; bi < d && m < d; bi += 64) {
                 uint4 c = lds128(P + 16 * bi);
+                // (a chain's first step multiplies Z = 0, or the AAD block when it owns both)
                 if (bi == nfull) {
                     c.x &= m0;
                     c.y &= m1;
                     c.z &= m2;
                     c.w &= m3;
                 }
-                ghash_mul<false>(z0, z1, z2, z3, kTeBytes);
+                if (bi >= 64u || aad_lane) ghash_mul<false, false>(z0, z1, z2, z3, kTeBytes + 6 * kGhBytes);  // H^64
                 z0 ^= c.x;
                 z1 ^= c.y;
                 z2 ^= c.z;
                 z3 ^= c.w;
-                blast = (int)bi;
             }
-            const uint32_t em = d + 1u - (uint32_t)blast;  // in [2, 5], as quad_packet
-            const uint32_t tsel = em == 2 ? kGhH2 : em == 3 ? kGhH3 : em == 4 ? kGhH4 : kGhH5;
-            ghash_mul_global(z0, z1, z2, z3, gh + tsel);
-            uint32_t l0, l1, l2, l3;
-            ghash_lenblock_global(b.aad_len, L, gh, l0, l1, l2, l3);
-            z0 = quad_xor(z0) ^ l0;
-            z1 = quad_xor(z1) ^ l1;
-            z2 = quad_xor(z2) ^ l2;
-            z3 = quad_xor(z3) ^ l3;
+            // S = sum_m Z_m H^m: level l adds lane m + 2^l's value times H^(2^l) into lane m
+            // (only lanes m <= min(d, 63) hold nonzero Z: levels with 2^l > that are skipped)
+            const uint32_t top = d < 63u ? d : 63u;
+            const int levels = top ? 32 - __builtin_clz(top) : 0;
+            for (int l = 0; l < levels; ++l) {
+                uint32_t p0 = z0, p1 = z1, p2 = z2, p3 = z3;
+                ghash_mul<false, false>(p0, p1, p2, p3, kTeBytes + l * kGhBytes);
+                z0 ^= __shfl_down(p0, 1u << l, 64);
+                z1 ^= __shfl_down(p1, 1u << l, 64);
+                z2 ^= __shfl_down(p2, 1u << l, 64);
+                z3 ^= __shfl_down(p3, 1u << l, 64);
+            }
+            // Y = S H^2 (lane 0) + [len(A)]_64 || [len(C)]_64 H (lane 1), in one multiply step
+            if (m == 1) {
+                z0 = 0;
+                z1 = bswap(b.aad_len * 8u);
+                z2 = 0;
+                z3 = bswap(L * 8u);
+            }
+            ghash_mul<false, false>(z0, z1, z2, z3, kTeBytes + (m == 0 ? kGhBytes : 0u));
+            z0 ^= __shfl_down(z0, 1u, 64);
+            z1 ^= __shfl_down(z1, 1u, 64);
+            z2 ^= __shfl_down(z2, 1u, 64);
+            z3 ^= __shfl_down(z3, 1u, 64);
             if (m == 0) lds_st128(kOneScratch + 16, uint4{z0, z1, z2, z3});
         }
     };
@@ -1085,7 +1148,12 @@ __global__ void __launch_bounds__(kOneThreads) gcm_one_kernel(Batch b, const uin
             lds_st32u(P + L + 4, e.y ^ y.y);
             lds_st32u(P + L + 8, e.z ^ y.z);
             lds_st32u(P + L + 12, e.w ^ y.w);
-            if (b.status) b.status[0] = 1;
+            if (b.nonces) {
+                lds_st32u(P + L + 16, n0);
+                lds_st32u(P + L + 20, n1);
+                lds_st32u(P + L + 24, n2);
+            }
+            if (b.status) b.status[pkt] = 1;
         }
     } else {
         ghash();
@@ -1103,11 +1171,11 @@ __global__ void __launch_bounds__(kOneThreads) gcm_one_kernel(Batch b, const uin
                 lds_st128(P + 16 * j, z);
             }
         }
-        if (tid == 0 && b.status) b.status[0] = ok ? 1 : 0;
+        if (tid == 0 && b.status) b.status[pkt] = ok ? 1 : 0;
     }
     __syncthreads();
     // 4. write the slot back (the bytes outside the payload/tag are rewritten unchanged)
-    uint4 *oslot = reinterpret_cast<uint4 *>(b.arena);
+    uint4 *oslot = reinterpret_cast<uint4 *>(slot);
     for (uint32_t i = tid; i < n16; i += kOneThreads) {
         const uint32_t a = A + 16 * i;
         oslot[i] = uint4{lds32(a), lds32(a + 4), lds32(a + 8), lds32(a + 12)};
@@ -1115,13 +1183,15 @@ __global__ void __launch_bounds__(kOneThreads) gcm_one_kernel(Batch b, const uin
 }
 
 hipError_t launch_one(bool seal, const Batch &b, hipStream_t s) {
-    if (b.n != 1 || (b.stride & 15) || b.stride > kOneCap - 16 || ((uintptr_t)b.arena & 15)) return hipErrorInvalidValue;
-    const uint32_t L = seal ? b.uniform_len : b.uniform_len - QGCM_OVERHEAD;
-    if ((!seal && b.uniform_len < QGCM_OVERHEAD) || b.stride < 4ull + L + QGCM_OVERHEAD) return hipErrorInvalidValue;
+    if (b.n == 0 || ((uintptr_t)b.arena & 15)) return hipErrorInvalidValue;
+    if (!b.descs) {  // uniform: one packet whose slot fits the staging area
+        const uint64_t stage = (4ull + b.uniform_len + (seal ? QGCM_OVERHEAD : 0) + 15) & ~15ull;
+        if (b.n != 1 || stage > kOneCap - 16 || (!seal && b.uniform_len < QGCM_OVERHEAD)) return hipErrorInvalidValue;
+    }
     void *args[] = {const_cast<Batch *>(&b), const_cast<uint32_t **>(&b.rk_table)};
     const void *k = seal ? reinterpret_cast<const void *>(&gcm_one_kernel<true>)
                          : reinterpret_cast<const void *>(&gcm_one_kernel<false>);
-    return hipLaunchKernel(k, dim3(1), dim3(kOneThreads), args, kOneLds, s);
+    return hipLaunchKernel(k, dim3(b.n), dim3(kOneThreads), args, kOneLds, s);
 }
 
 // Variant table: index = QGCM variant id (Batch-independent), see qgcm_api.cpp.
@@ -1241,8 +1311,9 @@ __global__ void __launch_bounds__(256) key_setup_kernel(const uint8_t *keys, uin
                                                         uint4 *gh_table, const uint8_t *sbox_g) {
     __shared__ uint8_t sbox[256];
     __shared__ uint8_t rkb[240];
-    __shared__ uint8_t hp[5][16];  // H, H^4, H^2, H^3, H^5 (the order of the comb tables)
-    __shared__ uint4 pw[5][128];   // x^i * hp[t]
+    constexpr int kT = kGhEntries / 512;
+    __shared__ uint8_t hp[kT][16];  // H, H^4, H^2, H^3, H^5, H^8, H^16, H^32, H^64 (comb table order)
+    __shared__ uint4 pw[kT][128];   // x^i * hp[t]
     const uint32_t kidx = blockIdx.x;
     const uint8_t *key = keys + 32u * kidx;
     sbox[threadIdx.x] = sbox_g[threadIdx.x];
@@ -1290,11 +1361,12 @@ __global__ void __launch_bounds__(256) key_setup_kernel(const uint8_t *keys, uin
         gf128_mul_bytes(hp[2], s, hp[3]);        // H^3
         gf128_mul_bytes(hp[2], hp[2], hp[1]);    // H^4
         gf128_mul_bytes(hp[1], s, hp[4]);        // H^5
+        for (int t = 5; t < kT; ++t) gf128_mul_bytes(hp[t == 5 ? 1 : t - 1], hp[t == 5 ? 1 : t - 1], hp[t]);  // H^(2^(t-2))
     }
     __syncthreads();
     // x^i * H^k: multiply by x = shift toward higher bit index (right shift of the byte string),
     // reduce with R = 0xe1 || 0^120 (SP 800-38D Algorithm 1).
-    if (threadIdx.x < 5) {
+    if (threadIdx.x < kT) {
         uint8_t v[16];
         for (int i = 0; i < 16; ++i) v[i] = hp[threadIdx.x][i];
         for (int i = 0; i < 128; ++i) {
