@@ -203,6 +203,20 @@ int qgcm_udp_recv_slots(int fd, uint8_t *arena, uint64_t stride, uint32_t max_n,
 int qgcm_udp_send_slots(int fd, const uint8_t *arena, uint64_t stride, uint32_t n, const uint32_t *lens,
                         const char *ip, int port);
 
+/* ---- batched TUN I/O (device/tun.go:51-118) ---- */
+/* qgcm_tun_open: device/tun.go:97-118 (createTUN) for `queues` queues of one multi-queue TUN device
+ * (IFF_TUN | IFF_NO_PI | IFF_MULTI_QUEUE), fds[i] = queue i; the kernel's device name goes to
+ * ifname_out.  qgcm_tun_up: device/tun.go:121-150 (initTun): up, MTU, address/prefix.  Both return 0
+ * or -errno.  read_slots: device/tun.go:51-57 batched -- waits up to timeout_ms for the first packet,
+ * then drains what the queue holds (up to max_n) into Raw[4:] of slots 0, 1, ... (lens[i] = packet
+ * length); returns the count (0 on timeout) or -1.  write_slots: device/tun.go:60-63 batched --
+ * writes Raw[4 : 4 + lens[i]]; returns the number written or -1. */
+int qgcm_tun_open(const char *name, int queues, int *fds, char *ifname_out, size_t ifname_len);
+int qgcm_tun_up(const char *ifname, const char *ip, int prefix, int mtu);
+int qgcm_tun_read_slots(int fd, uint8_t *arena, uint64_t stride, uint32_t max_n, uint32_t *lens, int timeout_ms);
+int qgcm_tun_write_slots(int fd, const uint8_t *arena, uint64_t stride, uint32_t n, const uint32_t *lens);
+int qgcm_tun_close(int fd);
+
 /* ---- measurement: achievable HBM copy rate (reads + writes bytes) for the roofline ---- */
 /* 16-B aligned device buffers, bytes a multiple of 16.  Asynchronous on stream. */
 int qgcm_stream_copy(qgcm_ctx *ctx, void *d_dst, const void *d_src, uint64_t bytes, void *stream);

@@ -27,6 +27,7 @@ EXPORTS = (
     "qgcm_snappy_compress_slots_limit", "qgcm_compress_seal_host", "qgcm_open_uncompress_host",
     "qgcm_udp_socket", "qgcm_udp_queue", "qgcm_udp_port", "qgcm_udp_close", "qgcm_udp_recv_slots",
     "qgcm_udp_send_slots",
+    "qgcm_tun_open", "qgcm_tun_up", "qgcm_tun_read_slots", "qgcm_tun_write_slots", "qgcm_tun_close",
 )
 
 QGCM_OK = 0
@@ -112,6 +113,11 @@ def _bind(L: C.CDLL) -> None:
     L.qgcm_udp_close.argtypes = [C.c_int]
     L.qgcm_udp_recv_slots.argtypes = [C.c_int, vp, u64, u32, vp, C.c_int]
     L.qgcm_udp_send_slots.argtypes = [C.c_int, vp, u64, u32, vp, C.c_char_p, C.c_int]
+    L.qgcm_tun_open.argtypes = [C.c_char_p, C.c_int, vp, C.c_char_p, sz]
+    L.qgcm_tun_up.argtypes = [C.c_char_p, C.c_char_p, C.c_int, C.c_int]
+    L.qgcm_tun_read_slots.argtypes = [C.c_int, vp, u64, u32, vp, C.c_int]
+    L.qgcm_tun_write_slots.argtypes = [C.c_int, vp, u64, u32, vp]
+    L.qgcm_tun_close.argtypes = [C.c_int]
 
 
 def lib() -> C.CDLL:
