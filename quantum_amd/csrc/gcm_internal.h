@@ -39,6 +39,8 @@ struct Batch {
     uint32_t aad_len;           // 0 or 4
     uint32_t max_keys;
     uint32_t *tile_counter;     // descriptor quad kernels: dynamic tile index (zeroed per launch)
+    uint8_t *done;              // gcm_one_kernel, uniform form: set to 1 after the slot is written
+                                // back and made system-visible (the host polls it instead of the stream)
 };
 
 constexpr int kNumVariants = 11;

@@ -1180,6 +1180,14 @@ __global__ void __launch_bounds__(kOneThreads) gcm_one_kernel(Batch b, const uin
         const uint32_t a = A + 16 * i;
         oslot[i] = uint4{lds32(a), lds32(a + 4), lds32(a + 8), lds32(a + 12)};
     }
+    if (b.done) {  // completion flag: every thread's stores reach the system before thread 0 sets it
+        __threadfence_system();
+        __syncthreads();
+        if (tid == 0) {
+            __threadfence_system();
+            *reinterpret_cast<volatile uint8_t *>(b.done) = 1;
+        }
+    }
 }
 
 hipError_t launch_one(bool seal, const Batch &b, hipStream_t s) {

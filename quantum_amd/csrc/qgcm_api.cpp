@@ -12,9 +12,13 @@
 #include <sys/random.h>
 
 #include <atomic>
+#include <chrono>
 #include <memory>
 #include <thread>
 #include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <chrono>
 #include <mutex>
 #include <vector>
 
@@ -145,10 +149,16 @@ int run_uniform(qgcm_ctx *ctx, bool seal, uint8_t *arena, uint64_t stride, uint3
 
 // seal_one / open_one: the latency kernel when the slot fits its LDS staging area, else the batch
 // kernel on a batch of one (QGCM_ONE_KERNEL=0 forces the latter, for A/B runs).
+// With the latency kernel the call completes on its flag (status[1], written last by the kernel,
+// after a system-scope fence) instead of hipStreamSynchronize: the host spins on pinned memory for
+// up to 1 s, then falls back to the stream (which also reports a failed launch or a fault).
 int run_one(qgcm_ctx *ctx, bool seal, uint8_t *slot, uint64_t stride, uint32_t len, uint32_t key_idx,
             uint32_t aad_len, uint8_t *status, hipStream_t s) {
     if (ctx->one_kernel && stride <= kOneCap - 16 && !(stride & 15) && !((uintptr_t)slot & 15)) {
+        volatile uint8_t *done = status + 1;
+        *done = 0;
         Batch b = base_batch(ctx);
+        b.done = status + 1;
         b.arena = slot;
         b.status = status;
         b.stride = stride;
@@ -157,9 +167,18 @@ int run_one(qgcm_ctx *ctx, bool seal, uint8_t *slot, uint64_t stride, uint32_t l
         b.n = 1;
         b.n_items = 64;
         b.aad_len = aad_len;
-        return hip_fail(launch_one(seal, b, s));
+        if (launch_one(seal, b, s) != hipSuccess) return QGCM_E_HIP;
+        const auto t0 = std::chrono::steady_clock::now();
+        for (uint32_t spins = 0; *done == 0; ++spins) {
+            __builtin_ia32_pause();
+            if ((spins & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(1)) break;
+        }
+        if (*done == 0) return hip_fail(hipStreamSynchronize(s));
+        std::atomic_thread_fence(std::memory_order_acquire);
+        return QGCM_OK;
     }
-    return run_uniform(ctx, seal, slot, stride, 1, len, key_idx, nullptr, aad_len, status, s);
+    const int rc = run_uniform(ctx, seal, slot, stride, 1, len, key_idx, nullptr, aad_len, status, s);
+    return rc == QGCM_OK ? hip_fail(hipStreamSynchronize(s)) : rc;
 }
 
 bool key_ok(qgcm_ctx *ctx, uint32_t k) {
@@ -497,9 +516,7 @@ long qgcm_seal_one(qgcm_ctx *ctx, uint32_t key_idx, uint8_t *data, long length, 
     // setups; the copy-in / copy-out form took ~3x longer per call)
     hipStream_t s = ctx->io_stream;
     h[stride] = 0;
-    if (run_one(ctx, true, h, stride, (uint32_t)length, key_idx, aad_len, h + stride, s) != QGCM_OK ||
-        hipStreamSynchronize(s) != hipSuccess)
-        return -1;
+    if (run_one(ctx, true, h, stride, (uint32_t)length, key_idx, aad_len, h + stride, s) != QGCM_OK) return -1;
     if (h[stride] != 1) return -1;
     memcpy(data, h + 4, (size_t)length + QGCM_OVERHEAD);
     return length + QGCM_OVERHEAD;
@@ -519,9 +536,7 @@ long qgcm_open_one(qgcm_ctx *ctx, uint32_t key_idx, uint8_t *data, long len, con
     memcpy(h + 4, data, (size_t)len);
     hipStream_t s = ctx->io_stream;  // zero-copy on the pinned staging slot, as qgcm_seal_one
     h[stride] = 0;
-    if (run_one(ctx, false, h, stride, (uint32_t)len, key_idx, aad_len, h + stride, s) != QGCM_OK ||
-        hipStreamSynchronize(s) != hipSuccess)
-        return -1;
+    if (run_one(ctx, false, h, stride, (uint32_t)len, key_idx, aad_len, h + stride, s) != QGCM_OK) return -1;
     memcpy(data, h + 4, (size_t)len - QGCM_OVERHEAD);  // plaintext, or zeros on auth failure
     return h[stride] == 1 ? len - QGCM_OVERHEAD : -1;
 }
