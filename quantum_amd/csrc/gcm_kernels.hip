@@ -1004,22 +1004,38 @@ __global__ void __launch_bounds__(kOneThreads) gcm_one_kernel(Batch b, const uin
         const uint32_t i = tid + k * kOneThreads;
         if (i < n16) v[k] = gslot[i];
     }
-    for (uint32_t i = tid; i < kTeBytes / 16; i += kOneThreads) {  // Te0/Te1, 32 replicas per row
-        const uint32_t x = i >> 4, half = (i >> 3) & 1u;
-        const uint32_t t = b.te[half * 256u + x];
-        lds_st128(16 * i, uint4{t, t, t, t});
-    }
+    // The table fills load everything first and store after (one memory latency, not one per
+    // iteration): Te0/Te1 words for 32 replicas per row, then the comb tables of H^(2^l) -- only the
+    // ones this packet's GHASH reads (H and H^2 always, the Estrin levels up to
+    // bit-length(min(d, 63)), H^64 once a lane owns two blocks).
+    constexpr int kTeIt = kTeBytes / 16 / kOneThreads;       // 16
+    constexpr int kGhIt = kOneTabs * 512 / kOneThreads;      // 14
     const uint4 *gh = b.gh_table + (size_t)key * kGhEntries;
-    // table l = comb of H^(2^l); only the ones this packet's GHASH reads (H and H^2 always, the
-    // Estrin levels up to bit-length(min(d, 63)), H^64 once a lane owns two blocks)
     const uint32_t dd = (L + 15u) >> 4;
     const uint32_t dtop = dd < 63u ? dd : 63u;
     const uint32_t ntabs = dd >= 64u ? kOneTabs : (dtop > 3u ? 32u - __builtin_clz(dtop) : 2u);
-    for (uint32_t i = tid; i < kOneTabs * 512u; i += kOneThreads) {
-        const uint32_t l = i >> 9, e = i & 511u;
-        if (l >= ntabs) break;
+    uint32_t tv[kTeIt];
+    uint4 gv[kGhIt];
+#pragma unroll
+    for (int k = 0; k < kTeIt; ++k) {
+        const uint32_t i = tid + k * kOneThreads;
+        tv[k] = b.te[((i >> 3) & 1u) * 256u + (i >> 4)];
+    }
+#pragma unroll
+    for (int k = 0; k < kGhIt; ++k) {
+        const uint32_t i = tid + k * kOneThreads, l = i >> 9;
         const uint32_t src = l == 0 ? kGhH : l == 1 ? kGhH2 : l == 2 ? kGhH4 : kGhH8 + (l - 3) * 512u;
-        lds_st_comb<false>(kTeBytes + l * kGhBytes, e, gh[src + e]);
+        if (l < ntabs) gv[k] = gh[src + (i & 511u)];
+    }
+#pragma unroll
+    for (int k = 0; k < kTeIt; ++k) {
+        const uint32_t i = tid + k * kOneThreads;
+        lds_st128(16 * i, uint4{tv[k], tv[k], tv[k], tv[k]});
+    }
+#pragma unroll
+    for (int k = 0; k < kGhIt; ++k) {
+        const uint32_t i = tid + k * kOneThreads, l = i >> 9;
+        if (l < ntabs) lds_st_comb<false>(kTeBytes + l * kGhBytes, i & 511u, gv[k]);
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
