@@ -113,11 +113,12 @@ def _bind(L: C.CDLL) -> None:
     L.qgcm_udp_close.argtypes = [C.c_int]
     L.qgcm_udp_recv_slots.argtypes = [C.c_int, vp, u64, u32, vp, C.c_int]
     L.qgcm_udp_send_slots.argtypes = [C.c_int, vp, u64, u32, vp, C.c_char_p, C.c_int]
-    L.qgcm_tun_open.argtypes = [C.c_char_p, C.c_int, vp, C.c_char_p, sz]
-    L.qgcm_tun_up.argtypes = [C.c_char_p, C.c_char_p, C.c_int, C.c_int]
-    L.qgcm_tun_read_slots.argtypes = [C.c_int, vp, u64, u32, vp, C.c_int]
-    L.qgcm_tun_write_slots.argtypes = [C.c_int, vp, u64, u32, vp]
-    L.qgcm_tun_close.argtypes = [C.c_int]
+    if hasattr(L, "qgcm_tun_open"):  # (older builds loaded by the A/B tools lack the TUN calls)
+        L.qgcm_tun_open.argtypes = [C.c_char_p, C.c_int, vp, C.c_char_p, sz]
+        L.qgcm_tun_up.argtypes = [C.c_char_p, C.c_char_p, C.c_int, C.c_int]
+        L.qgcm_tun_read_slots.argtypes = [C.c_int, vp, u64, u32, vp, C.c_int]
+        L.qgcm_tun_write_slots.argtypes = [C.c_int, vp, u64, u32, vp]
+        L.qgcm_tun_close.argtypes = [C.c_int]
 
 
 def lib() -> C.CDLL:
