@@ -967,7 +967,7 @@ __device__ __forceinline__ void block_mask(uint32_t r, uint32_t &m0, uint32_t &m
     m3 = q == 3 ? lowmask(sb) : 0u;
 }
 
-// One workgroup per packet.  Uniform form (b.descs == NULL, b.n == 1): b.arena = the slot,
+// One workgroup per packet.  Uniform form (b.descs == NULL): slot i at b.arena + i * b.stride,
 // b.uniform_len = L (seal) or L + 28 (open), b.uniform_key.  Descriptor form (the coalescer's small
 // batches): packet blockIdx.x is b.descs[blockIdx.x] in b.arena.  Slots are 16-B aligned and
 // (4 + len (+ 28 for seal) + 15) & ~15 bytes long, at most kOneCap - 16; seal nonces come from
@@ -977,7 +977,7 @@ __global__ void __launch_bounds__(kOneThreads) gcm_one_kernel(Batch b, const uin
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
     const uint32_t pkt = blockIdx.x;
-    uint64_t off = 0;
+    uint64_t off = (uint64_t)pkt * b.stride;  // uniform form: slot pkt of the batch
     uint32_t Lin = b.uniform_len, key = b.uniform_key;
     if (b.descs) {
         const qgcm_desc dsc = b.descs[pkt];
@@ -1208,9 +1208,11 @@ __global__ void __launch_bounds__(kOneThreads) gcm_one_kernel(Batch b, const uin
 
 hipError_t launch_one(bool seal, const Batch &b, hipStream_t s) {
     if (b.n == 0 || ((uintptr_t)b.arena & 15)) return hipErrorInvalidValue;
-    if (!b.descs) {  // uniform: one packet whose slot fits the staging area
+    if (!b.descs) {  // uniform: slots that hold the 16-B-rounded staging area and fit it in LDS
         const uint64_t stage = (4ull + b.uniform_len + (seal ? QGCM_OVERHEAD : 0) + 15) & ~15ull;
-        if (b.n != 1 || stage > kOneCap - 16 || (!seal && b.uniform_len < QGCM_OVERHEAD)) return hipErrorInvalidValue;
+        if ((b.n > 1 && (b.stride < stage || (b.stride & 15))) || stage > kOneCap - 16 ||
+            (!seal && b.uniform_len < QGCM_OVERHEAD))
+            return hipErrorInvalidValue;
     }
     void *args[] = {const_cast<Batch *>(&b), const_cast<uint32_t **>(&b.rk_table)};
     const void *k = seal ? reinterpret_cast<const void *>(&gcm_one_kernel<true>)

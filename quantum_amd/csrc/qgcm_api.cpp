@@ -40,6 +40,9 @@ struct qgcm_ctx {
     int desc_variant = kVariantDescQuad;    // kernel variant for descriptor batches (QGCM_DESC_VARIANT)
     int wgs_per_cu_override = 0;            // persistent-grid workgroups per CU (QGCM_WGS_PER_CU, tuning)
     bool one_kernel = true;                 // seal_one/open_one use the latency kernel (QGCM_ONE_KERNEL)
+    bool variant_forced = false;            // QGCM_VARIANT given: uniform batches always run that variant
+    uint32_t one_uniform_max = kOneUniformMax;  // uniform batches up to this many packets take the
+                                                // latency kernel (QGCM_ONE_UNIFORM_MAX, tuning)
     uint32_t *d_rk = nullptr;
     uint4 *d_gh = nullptr;
     uint32_t *d_te = nullptr;
@@ -231,6 +234,12 @@ int run_uniform(qgcm_ctx *ctx, bool seal, uint8_t *arena, uint64_t stride, uint3
     b.n = n;
     b.n_items = (uint32_t)(((uint64_t)n + 63) & ~63ull);
     b.aad_len = aad_len;
+    // Small batches (one workgroup wave: n <= kOneUniformMax) take the latency kernel, one
+    // workgroup per packet, when the slots allow it and no kernel variant is forced (QGCM_VARIANT).
+    const uint64_t stage = (4ull + len + (seal ? QGCM_OVERHEAD : 0) + 15) & ~15ull;
+    if (ctx->one_kernel && !ctx->variant_forced && n <= ctx->one_uniform_max && !(stride & 15) &&
+        !((uintptr_t)arena & 15) && stage <= stride && stage <= kOneCap - 16)
+        return hip_fail(launch_one(seal, b, s));
     const int v = ctx->uniform_variant;
     return hip_fail(launch_packets(seal, v, b, grid_for(ctx, b.n_items, v), s));
 }
@@ -378,10 +387,14 @@ qgcm_ctx *qgcm_create(int device, uint32_t max_keys, char *err, int errlen) {
     ctx->key_set.assign(max_keys, 0);
     if (const char *v = getenv("QGCM_VARIANT")) {  // kernel variant overrides (tuning and tests)
         const int iv = atoi(v);
-        if (iv >= 0 && iv < kNumVariants && !variant_desc(iv)) ctx->uniform_variant = iv;
+        if (iv >= 0 && iv < kNumVariants && !variant_desc(iv)) {
+            ctx->uniform_variant = iv;
+            ctx->variant_forced = true;
+        }
     }
     if (const char *v = getenv("QGCM_WGS_PER_CU")) ctx->wgs_per_cu_override = atoi(v);
     if (const char *v = getenv("QGCM_ONE_KERNEL")) ctx->one_kernel = atoi(v) != 0;
+    if (const char *v = getenv("QGCM_ONE_UNIFORM_MAX")) ctx->one_uniform_max = (uint32_t)std::max(0, atoi(v));
     if (const char *v = getenv("QGCM_PIPE_CHUNK_MB")) ctx->host_chunk = (uint64_t)std::max(1, atoi(v)) << 20;
     if (const char *v = getenv("QGCM_PIPE_RING_MB")) ctx->host_ring = (uint64_t)std::max(1, atoi(v)) << 20;
     if (const char *v = getenv("QGCM_DESC_VARIANT")) {
