@@ -59,9 +59,18 @@ struct qgcm_ctx {
 
     // per-packet and host-batch staging, guarded by io_mu
     std::mutex io_mu;
-    hipStream_t io_stream = nullptr;
-    uint8_t *h_pin = nullptr;
-    size_t pin_cap = 0;
+    // per-packet calls (qgcm_seal_one / qgcm_open_one): a pool of pinned staging slots, each with
+    // its own stream and lock, so concurrent callers (quantum's worker goroutines) run their
+    // one-workgroup kernels side by side instead of queueing on one slot
+    struct OneSlot {
+        std::mutex mu;
+        hipStream_t stream = nullptr;
+        uint8_t *h = nullptr;
+        size_t cap = 0;
+    };
+    static constexpr int kOneSlots = 8;
+    OneSlot one[kOneSlots];
+    std::atomic<uint32_t> one_rr{0};
 
     // host-batch pipeline (qgcm_seal_host / qgcm_open_host), guarded by io_mu
     hipStream_t pipe[kPipeStreams] = {};
@@ -312,18 +321,38 @@ int run_descs_locked(qgcm_ctx *ctx, bool seal, const qgcm_desc *descs, uint32_t 
     return hip_fail(launch_packets(seal, v, b, grid_for(ctx, b.n_items, v), s));
 }
 
-// Pinned staging slot of the per-packet calls (the kernel works on it in place, zero-copy).
-int ensure_io(qgcm_ctx *ctx, size_t bytes) {
-    if (bytes <= ctx->pin_cap) return QGCM_OK;
-    size_t want = 1;
-    while (want < bytes) want <<= 1;
-    if (want < 4096) want = 4096;
-    if (ctx->h_pin) hipHostFree(ctx->h_pin);
-    ctx->h_pin = nullptr;
-    ctx->pin_cap = 0;
-    if (hipHostMalloc(&ctx->h_pin, want, hipHostMallocDefault) != hipSuccess) return QGCM_E_NOMEM;
-    ctx->pin_cap = want;
-    return QGCM_OK;
+// Takes a free per-packet staging slot (the first one whose lock is free, starting round-robin; all
+// busy: waits on one) and makes its pinned buffer hold `bytes` (the kernel works on it in place,
+// zero-copy).  Returns nullptr on allocation failure.
+qgcm_ctx::OneSlot *acquire_one(qgcm_ctx *ctx, size_t bytes, std::unique_lock<std::mutex> &lk) {
+    const uint32_t start = ctx->one_rr.fetch_add(1, std::memory_order_relaxed);
+    qgcm_ctx::OneSlot *sl = nullptr;
+    for (int i = 0; i < qgcm_ctx::kOneSlots && !sl; ++i) {
+        qgcm_ctx::OneSlot &c = ctx->one[(start + i) % qgcm_ctx::kOneSlots];
+        std::unique_lock<std::mutex> l(c.mu, std::try_to_lock);
+        if (l.owns_lock()) {
+            lk = std::move(l);
+            sl = &c;
+        }
+    }
+    if (!sl) {
+        sl = &ctx->one[start % qgcm_ctx::kOneSlots];
+        lk = std::unique_lock<std::mutex>(sl->mu);
+    }
+    if (!sl->stream && hipStreamCreateWithFlags(&sl->stream, hipStreamNonBlocking) != hipSuccess) {
+        sl->stream = nullptr;
+        return nullptr;
+    }
+    if (bytes > sl->cap) {
+        size_t want = 4096;
+        while (want < bytes) want <<= 1;
+        if (sl->h) hipHostFree(sl->h);
+        sl->h = nullptr;
+        sl->cap = 0;
+        if (hipHostMalloc(&sl->h, want, hipHostMallocDefault) != hipSuccess) return nullptr;
+        sl->cap = want;
+    }
+    return sl;
 }
 
 }  // namespace
@@ -411,7 +440,6 @@ qgcm_ctx *qgcm_create(int device, uint32_t max_keys, char *err, int errlen) {
               hipMalloc(&ctx->d_cursors, (size_t)max_keys * 4) == hipSuccess &&
               hipMemcpy(ctx->d_te, te, sizeof te, hipMemcpyHostToDevice) == hipSuccess &&
               hipMemcpy(ctx->d_sbox, sbox, sizeof sbox, hipMemcpyHostToDevice) == hipSuccess &&
-              hipStreamCreateWithFlags(&ctx->io_stream, hipStreamNonBlocking) == hipSuccess &&
               hipEventCreateWithFlags(&ctx->ws_done, hipEventDisableTiming) == hipSuccess;
     for (int k = 0; ok && k < kPipeStreams; ++k)
         ok = hipStreamCreateWithFlags(&ctx->pipe[k], hipStreamNonBlocking) == hipSuccess;
@@ -435,8 +463,10 @@ void qgcm_destroy(qgcm_ctx *ctx) {
     hipFree(ctx->d_cursors);
     hipFree(ctx->d_worklist);
     hipFree(ctx->d_qws);
-    if (ctx->h_pin) hipHostFree(ctx->h_pin);
-    if (ctx->io_stream) hipStreamDestroy(ctx->io_stream);
+    for (auto &sl : ctx->one) {
+        if (sl.h) hipHostFree(sl.h);
+        if (sl.stream) hipStreamDestroy(sl.stream);
+    }
     hipFree(ctx->d_ring);
     hipFree(ctx->d_side);
     if (ctx->h_stat) hipHostFree(ctx->h_stat);
@@ -516,18 +546,19 @@ long qgcm_seal_one(qgcm_ctx *ctx, uint32_t key_idx, uint8_t *data, long length, 
     } else if (getrandom(nb, 12, 0) != 12) {  // crypto/aes.go:44 rand.Read(nonce)
         return -1;
     }
-    std::lock_guard<std::mutex> g(ctx->io_mu);
     if (hipSetDevice(ctx->device) != hipSuccess) return -1;
     const uint64_t stride = ((uint64_t)length + 4 + QGCM_OVERHEAD + 15) & ~15ull;
-    if (ensure_io(ctx, stride + 16) != QGCM_OK) return -1;
-    uint8_t *h = ctx->h_pin;
+    std::unique_lock<std::mutex> lk;
+    qgcm_ctx::OneSlot *sl = acquire_one(ctx, stride + 16, lk);
+    if (!sl) return -1;
+    uint8_t *h = sl->h;
     memset(h, 0, stride);
     if (aad_len) memcpy(h, aad, aad_len);
     memcpy(h + 4, data, (size_t)length);
     memcpy(h + 4 + length + 16, nb, 12);
     // Zero-copy: the kernel seals the pinned staging slot in place over PCIe (one packet: no DMA
     // setups; the copy-in / copy-out form took ~3x longer per call)
-    hipStream_t s = ctx->io_stream;
+    hipStream_t s = sl->stream;
     h[stride] = 0;
     if (run_one(ctx, true, h, stride, (uint32_t)length, key_idx, aad_len, h + stride, s) != QGCM_OK) return -1;
     if (h[stride] != 1) return -1;
@@ -539,15 +570,16 @@ long qgcm_open_one(qgcm_ctx *ctx, uint32_t key_idx, uint8_t *data, long len, con
     if (!ctx || (!data && len) || len < 0 || len - QGCM_OVERHEAD >= (long)QGCM_MAX_PAYLOAD || aad_len > 4 || (aad_len && !aad)) return -1;
     if (len < QGCM_OVERHEAD) return -1;  // crypto/aes.go:58-60: errOpen (the reference panics below 12)
     if (!key_ok(ctx, key_idx)) return -1;
-    std::lock_guard<std::mutex> g(ctx->io_mu);
     if (hipSetDevice(ctx->device) != hipSuccess) return -1;
     const uint64_t stride = ((uint64_t)len + 4 + 15) & ~15ull;
-    if (ensure_io(ctx, stride + 16) != QGCM_OK) return -1;
-    uint8_t *h = ctx->h_pin;
+    std::unique_lock<std::mutex> lk;
+    qgcm_ctx::OneSlot *sl = acquire_one(ctx, stride + 16, lk);
+    if (!sl) return -1;
+    uint8_t *h = sl->h;
     memset(h, 0, stride);
     if (aad_len) memcpy(h, aad, aad_len);
     memcpy(h + 4, data, (size_t)len);
-    hipStream_t s = ctx->io_stream;  // zero-copy on the pinned staging slot, as qgcm_seal_one
+    hipStream_t s = sl->stream;  // zero-copy on the pinned staging slot, as qgcm_seal_one
     h[stride] = 0;
     if (run_one(ctx, false, h, stride, (uint32_t)len, key_idx, aad_len, h + stride, s) != QGCM_OK) return -1;
     memcpy(data, h + 4, (size_t)len - QGCM_OVERHEAD);  // plaintext, or zeros on auth failure
