@@ -1,11 +1,16 @@
 """bench.py -- AES-256-GCM seal+unseal GiB/s on device-resident packet batches (BASELINE.json).
 
-Workload per rank (BASELINE config 2, the single-GPU headline): 2^20 packets x 1350 B, one key
+Workload (BASELINE.json configs): at N = 1 GPU, config 2 -- 2^20 packets x 1350 B, one key
 (NewAES("AES256Key-32Characters1234567890", salt 00..1f)), AAD = 4-B private IP, explicit seeded
-nonces, slots laid out as Payload.Raw records of 1408 B with 64-B aligned payloads.  One step = seal every packet, then
-unseal every packet (crypto/aes.go Encrypt then Decrypt), the reference's BenchmarkAES loop body
-(crypto/crypto_test.go:103-131) over a batch.  Multi-GPU: one process per GPU, each sealing its
-own shard (packets are independent: no data-path collective), weak scaling.
+nonces, slots laid out as Payload.Raw records of 1408 B with 64-B aligned payloads.  At N > 1, config
+4 -- 64 x 2^20 packets x 1350 B sharded over the N GPUs (one process per GPU, each owning its
+contiguous shard: packets are independent, no data-path collective), so the total work is fixed
+("strong"); --workload config2 keeps 2^20 packets per GPU instead ("weak").  One step = seal every
+packet, then unseal every packet (crypto/aes.go Encrypt then Decrypt), the reference's BenchmarkAES
+loop body (crypto/crypto_test.go:103-131) over a batch.
+
+Before the W warmup steps the GPU runs the same step for --settle-ms of wall time (clock settle,
+DESIGN.md s5 "Clock ramp": after an idle start the clocks take ~70 ms of load to come up).
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
   torchrun --nproc-per-node N bench.py --gpus N ...
@@ -27,7 +32,9 @@ from quantum_amd import batch, shard  # noqa: E402
 from quantum_amd.crypto import Context, derive_key  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, MI355X_MICROARCH.md "Chip-level parameters"
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r1_s3", "traffic.json")  # tools/pmc_traffic.py
+# PMC passes of this command (tools/pmc_traffic.py), newest first
+TRAFFIC_JSONS = [os.path.join(ROOT, "profiles", d, "traffic.json") for d in ("r2_final", "r1_s3")]
+CONFIG4_PACKETS = 64 << 20  # BASELINE config 4: 64 M packets over the node's GPUs
 SECRET = b"AES256Key-32Characters1234567890"
 SALT = bytes(range(32))
 AAD = bytes([10, 99, 0, 1])
@@ -38,32 +45,80 @@ def parse() -> argparse.Namespace:
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=100)  # ~0.35 s timed: the clocks ramp for ~70 ms after an idle gap
     p.add_argument("--warmup", type=int, default=10)
-    p.add_argument("--packets", type=int, default=1 << 20, help="packets per GPU")
+    p.add_argument("--workload", choices=["auto", "config2", "config4"], default="auto",
+                   help="auto: config2 at 1 GPU, config4 (64 M packets sharded) at more")
+    p.add_argument("--packets", type=int, default=0, help="packets per GPU (overrides the workload's)")
+    p.add_argument("--settle-ms", type=float, default=300.0, help="clock settle before warmup (0 = none)")
     p.add_argument("--len", type=int, default=1350, help="payload bytes per packet")
     p.add_argument("--stride", type=int, default=0, help="slot stride (0 = smallest 64-B multiple)")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
+    p.add_argument("--cpu-threads", type=int, default=0, help="0 = the CPU share this job was given")
     p.add_argument("--dist-backend", default="nccl", help="nccl (RCCL, default) or gloo (rehearsal)")
     p.add_argument("--one-device", action="store_true",
                    help="every rank on cuda:0 (multi-rank rehearsal on a 1-GPU box, gloo only)")
     return p.parse_args()
 
 
-def cpu_baseline(key: bytes, L: int, threads: int) -> dict:
-    """OpenSSL EVP AES-256-GCM with crypto/aes.go semantics (oracle/ossl_check.c), host cores."""
+def host_cpus() -> dict:
+    """What the host has and what this job may use: nproc, the affinity mask, the cgroup CPU quota,
+    the job's thread budget (OMP_NUM_THREADS, set to the box's share by the GPU pool), model, flags."""
+    info = {"nproc": os.cpu_count() or 1}
+    try:
+        info["affinity"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        info["affinity"] = info["nproc"]
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    info["cgroup_quota_cpus"] = quota
+    share = info["affinity"]
+    if quota:
+        share = min(share, max(1, int(quota)))
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        share = min(share, int(omp))
+    info["share"] = share
+    model, flags = "", set()
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name") and not model:
+                model = line.split(":", 1)[1].strip()
+            elif line.startswith("flags") and not flags:
+                flags = set(line.split(":", 1)[1].split())
+    except OSError:
+        pass
+    info["model"] = model
+    info["crypto_flags"] = sorted(f for f in ("aes", "vaes", "pclmulqdq", "vpclmulqdq", "avx2", "avx512f")
+                                  if f in flags)
+    return info
+
+
+def cpu_baseline(key: bytes, L: int, threads: int, host: dict) -> dict:
+    """OpenSSL EVP AES-256-GCM with crypto/aes.go semantics (oracle/ossl_check.c), host cores: one
+    thread alone, then `threads` at once (the CPU share the GPU pool grants this job)."""
     from oracle import oracle as O
 
-    # calibrate one thread, then size the all-thread sample to ~1.5 s wall (~threads*1.5 s CPU work)
-    n1 = 20000
+    # one thread for ~2 s, then the all-thread sample sized to ~1.5 s wall (~threads x 1.5 s of CPU work)
+    n0 = 20000
+    t0 = O.ossl_cpu_baseline(key, 1, n0, L)
+    n1 = max(n0, int(n0 / t0 * 2.0))
     t1 = O.ossl_cpu_baseline(key, 1, n1, L)
     rate1 = 2 * n1 * L / t1 / 2**30
     per_thread = max(20000, int(n1 / t1 * 1.5))
     tN = O.ossl_cpu_baseline(key, threads, per_thread, L)
     rateN = 2 * threads * per_thread * L / tN / 2**30
     return {"value": round(rateN, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
-            "sample": (f"{threads} threads x {per_thread} packets x {L} B seal+open, crypto/aes.go semantics "
-                       f"(getrandom nonce/packet, in place, 4-B AAD) on OpenSSL EVP aes-256-gcm; "
-                       f"1 thread: {rate1:.3f} GiB/s over {n1} packets")}
+            "one_core": round(rate1, 3), "nproc": host["nproc"],
+            "all_nproc_linear_estimate": round(rate1 * host["nproc"], 1),
+            "host": host,
+            "sample": (f"{threads} threads (this job's CPU share of a {host['nproc']}-CPU host) x {per_thread} "
+                       f"packets x {L} B seal+open, crypto/aes.go semantics (getrandom nonce/packet, in place, "
+                       f"4-B AAD) on OpenSSL EVP aes-256-gcm; 1 thread alone: {rate1:.3f} GiB/s over {n1} packets; "
+                       f"all_nproc_linear_estimate = one_core x nproc, not measured")}
 
 
 def stream_copy_gbs(ctx, nbytes: int, dev, stream, reps: int = 5) -> float:
@@ -86,16 +141,18 @@ def stream_copy_gbs(ctx, nbytes: int, dev, stream, reps: int = 5) -> float:
 
 def pmc_traffic(kind: str, N: int, L: int, stride: int):
     """HBM bytes per launch and LDS-array busy fraction of the dominant kernel from the committed
-    rocprofv3 PMC passes of this command (profiles/r1_s3/traffic.json), or None when they are absent or
-    for another workload."""
-    try:
-        t = json.load(open(TRAFFIC_JSON))
-    except (OSError, ValueError):
-        return None, None, None
-    if t.get("workload") != {"packets": N, "payload_len": L, "slot_stride": stride} or kind not in t["kernels"]:
-        return None, None, None
-    k = t["kernels"][kind]
-    return k["hbm_bytes"], k.get("lds_array_busy"), os.path.relpath(TRAFFIC_JSON, ROOT)
+    rocprofv3 PMC passes of this command (the newest profiles/*/traffic.json), or None when they are
+    absent or for another workload."""
+    for path in TRAFFIC_JSONS:
+        try:
+            t = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if t.get("workload") != {"packets": N, "payload_len": L, "slot_stride": stride} or kind not in t["kernels"]:
+            continue
+        k = t["kernels"][kind]
+        return k["hbm_bytes"], k.get("lds_array_busy"), os.path.relpath(path, ROOT)
+    return None, None, None
 
 
 def main() -> None:
@@ -117,7 +174,15 @@ def main() -> None:
         else:
             dist.init_process_group(args.dist_backend, init_method="env://")
 
-    N, L = args.packets, args.len
+    workload = args.workload if args.workload != "auto" else ("config2" if world == 1 else "config4")
+    if args.packets:
+        N = args.packets
+    elif workload == "config4":
+        lo, hi = shard.packet_range(CONFIG4_PACKETS, world, rank)
+        N = hi - lo
+    else:
+        N = 1 << 20
+    L = args.len
     stride = args.stride or batch.slot_stride(L, align=64)
     ctx = Context(device=local, max_keys=16)
     key = derive_key(SECRET, SALT)  # crypto/aes.go:66, host, once
@@ -143,12 +208,20 @@ def main() -> None:
         if ev is not None:
             ev[2].record(stream)
 
+    # clock settle: the same step back to back for settle_ms of wall time, so the timed steps run at
+    # the clocks the chip holds under this load (not timed, not counted as warmup)
+    settle = 0
+    t_settle = time.perf_counter()
+    while (time.perf_counter() - t_settle) * 1e3 < args.settle_ms:
+        step()
+        settle += 1
+        if settle % 8 == 0:
+            torch.cuda.synchronize()  # bound the launch queue; the loop keeps the GPU busy
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
-    ok = int(status.sum().item()) == N
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
 
+    torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -159,13 +232,15 @@ def main() -> None:
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    ok = int(status.sum().item()) == N  # the last timed open authenticated every packet
     # max over ranks, AND of the per-rank status (the only cross-rank traffic; no data collective)
     elapsed, ok = shard.reduce_step_time(elapsed, ok, dist, dev if args.dist_backend == "nccl" else None)
 
     seal_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
     open_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
     ms_step = elapsed * 1e3 / args.steps
-    total_bytes = world * 2 * N * L  # each payload byte counted once sealed and once unsealed
+    total_packets = CONFIG4_PACKETS if workload == "config4" and not args.packets else world * N
+    total_bytes = 2 * total_packets * L  # each payload byte counted once sealed and once unsealed
     value = total_bytes / (elapsed / args.steps) / 2**30
 
     # dominant kernel roofline: algorithmic bytes per launch: seal 2L+44, open 2L+32
@@ -189,19 +264,24 @@ def main() -> None:
             "warmup": args.warmup,
             "ms_per_step": round(ms_step, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if workload == "config4" and world > 1 and not args.packets else "weak",
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (seeded splitmix64 payloads and nonces, one PBKDF2-derived key)",
-            "config": {"workload": f"config2: {N} x {L} B packets per GPU, seal then unseal, 1 key, AAD 4 B",
-                       "packets_per_gpu": N, "payload_len": L, "slot_stride": stride, "payload_align": 64,
-                       "parallelism": f"replicas/shards x{world}, no collectives"},
+            "config": {"workload": (f"config4: {total_packets} x {L} B packets sharded over {world} GPUs "
+                                    f"({N} per GPU), seal then unseal, 1 key, AAD 4 B" if workload == "config4" else
+                                    f"config2: {N} x {L} B packets per GPU, seal then unseal, 1 key, AAD 4 B"),
+                       "packets_total": total_packets, "packets_per_gpu": N, "payload_len": L, "slot_stride": stride,
+                       "payload_align": 64, "parallelism": f"shards x{world}, no collectives",
+                       "clock_settle_steps": settle},
             "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "frac_read": round(achieved_read / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "traffic_source": traffic_src,
                          "traffic_over_algorithmic": round(traffic / (N * per_pkt), 3) if traffic else None,
                          "bytes_per_packet": per_pkt, "kernel_ms": round(kms, 4),
                          "achieved_read_only": round(achieved_read, 1),
+                         "read_bytes_per_packet": read_pkt,
                          "copy_achievable": round(copy_gbs, 1),
                          "frac_of_copy": round(achieved / copy_gbs, 4),
                          "binding_unit": "LDS (T-table AES + comb GHASH lookups, DESIGN.md 4.1)",
@@ -210,8 +290,8 @@ def main() -> None:
             "status_ok": ok,
         }
         if world == 1 and not args.no_cpu_baseline:
-            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-            line["cpu_baseline"] = cpu_baseline(key, L, threads)
+            host = host_cpus()
+            line["cpu_baseline"] = cpu_baseline(key, L, args.cpu_threads or host["share"], host)
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()

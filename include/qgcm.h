@@ -46,6 +46,9 @@ extern "C" {
 #define QGCM_MAX_PAYLOAD (1u << 28) /* largest plaintext per packet (GCM allows 2^36-32; packets are <= 9000) */
 #define QGCM_ERRLEN 120      /* crypto/dtls.go:23 errorLen */
 #define QGCM_MAX_BATCH (1u << 31) /* packets per batch call (tile indices stay 32-bit); more -> QGCM_E_ARG */
+/* largest max_keys of a context: the descriptor sort key is key_idx << 12 | length rank, 32 bits, and
+ * its all-ones value marks excluded packets, so key index 2^20 - 1 is reserved */
+#define QGCM_MAX_KEYS ((1u << 20) - 1)
 
 /* status codes */
 #define QGCM_OK 0
@@ -67,6 +70,9 @@ typedef struct qgcm_desc {
 } qgcm_desc;
 
 /* ---- context (replaces the per-process Go AEAD objects) ---- */
+/* max_keys in [1, QGCM_MAX_KEYS].  Key slots start unset: a packet naming an unset slot fails (status 0,
+ * slot untouched; QGCM_E_KEY / -1 from the uniform and per-packet calls), as Apply would on a peer
+ * whose Mapping.AES is nil (common/mapping.go:94-99 leaves it nil when the peer published no keys). */
 qgcm_ctx *qgcm_create(int device, uint32_t max_keys, char *err, int errlen);
 void qgcm_destroy(qgcm_ctx *ctx);
 const char *qgcm_strerror(int code);
@@ -90,7 +96,8 @@ int qgcm_x25519(uint8_t secret[32], const uint8_t priv[32], const uint8_t peer_p
 /* Seal n packets in place.  nonces: device array of n*12 bytes (nonce i for packet i, written
  * into the slot like crypto/aes.go:50), or NULL to use the nonce already present at
  * [4+L+16, 4+L+28) of each slot.  aad_len: 0 (nil additional) or 4 (the Payload IP header).
- * status (device, n bytes, may be NULL): 1 = sealed, 0 = rejected (bad key index). */
+ * status (device, n bytes, may be NULL): 1 = sealed, 0 = rejected (key index out of range or never set,
+ * payload of QGCM_MAX_PAYLOAD or more; the slot is untouched). */
 int qgcm_seal_batch(qgcm_ctx *ctx, uint8_t *d_arena, const qgcm_desc *d_descs, uint32_t n,
                     const uint8_t *d_nonces, uint32_t aad_len, uint8_t *d_status, void *stream);
 /* Open n packets in place.  status[i] = 1 if authentic (plaintext at [4, 4+len-28)),
@@ -144,6 +151,32 @@ long qgcm_coalescer_seal(qgcm_coalescer *c, uint32_t key_idx, uint8_t *data, lon
                          const uint8_t *aad, uint32_t aad_len);
 long qgcm_coalescer_open(qgcm_coalescer *c, uint32_t key_idx, uint8_t *data, long len,
                          const uint8_t *aad, uint32_t aad_len);
+
+/* ---- several GPUs behind one process (quantum is one process: main.go:29-114, 72-75) ---- */
+/* A group of `count` member contexts, member k on devices[k] (members may share a device).  Keyed
+ * traffic is hash-sharded: key index k belongs to member qgcm_group_shard(k) = ((k * 0x9E3779B97F4A7C15)
+ * mod 2^64 >> 32) mod count (quantum_amd/shard.py key_shard), so a peer's packets stay on
+ * one GPU and each member holds only its peers' keys.  No collective, no GPU-to-GPU traffic.
+ * NULL + err on failure. */
+typedef struct qgcm_group qgcm_group;
+qgcm_group *qgcm_group_create(const int *devices, int count, uint32_t max_keys, char *err, int errlen);
+void qgcm_group_destroy(qgcm_group *g);
+int qgcm_group_size(const qgcm_group *g);
+qgcm_ctx *qgcm_group_ctx(qgcm_group *g, int member);  /* member's context (device batches on it) */
+int qgcm_group_shard(const qgcm_group *g, uint32_t key_idx);
+/* Installs keys[i] as key first_idx + i on its owning member only (qgcm_set_keys there). */
+int qgcm_group_set_keys(qgcm_group *g, uint32_t first_idx, uint32_t count, const uint8_t *keys);
+/* Host batches over the group: packet i is the Raw slot at h_arena + h_descs[i].offset (seal: len = L,
+ * capacity 4 + L + 28; open: len = L + 28), any key mix.  Packets are split by owner; one host thread and
+ * one stream set per member gathers its packets into pinned staging, copies them to its device, runs the
+ * descriptor batch, copies back and writes the results into the same slots (input order kept).
+ * h_nonces: n * 12 B (seal; NULL = nonce already in the slot).  h_status[i] (may be NULL): 1 ok, 0 failed
+ * (as qgcm_seal_batch / qgcm_open_batch).  Returns the number of failed packets or a negative error.
+ * One call at a time per group (calls are serialized). */
+int qgcm_group_seal_host(qgcm_group *g, uint8_t *h_arena, const qgcm_desc *h_descs, uint32_t n,
+                         const uint8_t *h_nonces, uint32_t aad_len, uint8_t *h_status);
+int qgcm_group_open_host(qgcm_group *g, uint8_t *h_arena, const qgcm_desc *h_descs, uint32_t n, uint32_t aad_len,
+                         uint8_t *h_status);
 
 /* Pinned (page-locked) host memory for arenas handed to the *_host calls; NULL on failure. */
 void *qgcm_host_alloc(size_t bytes);

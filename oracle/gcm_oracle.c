@@ -48,6 +48,9 @@ static uint8_t gf8_mul(uint8_t a, uint8_t b) {
 
 static uint8_t rotl8(uint8_t x, int s) { return (uint8_t)((x << s) | (x >> (8 - s))); }
 
+/* xtime (FIPS-197 s4.2.1): multiplication by {02} */
+static uint8_t xtime(uint8_t a) { return (uint8_t)((a << 1) ^ ((a & 0x80) ? 0x1b : 0)); }
+
 /* S-box from its definition (FIPS-197 s5.1.1): multiplicative inverse then affine map. */
 static void build_sbox(void) {
     if (sbox_ready) return;
@@ -103,10 +106,12 @@ void oracle_aes256_encrypt_block(const uint8_t rk[240], const uint8_t in[16], ui
         if (round != 14) {
             for (int c = 0; c < 4; c++) {
                 uint8_t a0 = t[4 * c], a1 = t[4 * c + 1], a2 = t[4 * c + 2], a3 = t[4 * c + 3];
-                s[4 * c + 0] = gf8_mul(a0, 2) ^ gf8_mul(a1, 3) ^ a2 ^ a3;
-                s[4 * c + 1] = a0 ^ gf8_mul(a1, 2) ^ gf8_mul(a2, 3) ^ a3;
-                s[4 * c + 2] = a0 ^ a1 ^ gf8_mul(a2, 2) ^ gf8_mul(a3, 3);
-                s[4 * c + 3] = gf8_mul(a0, 3) ^ a1 ^ a2 ^ gf8_mul(a3, 2);
+                /* MixColumns (FIPS-197 s5.1.3): {02} = xtime, {03} = xtime ^ identity */
+                const uint8_t x0 = xtime(a0), x1 = xtime(a1), x2 = xtime(a2), x3 = xtime(a3);
+                s[4 * c + 0] = x0 ^ (x1 ^ a1) ^ a2 ^ a3;
+                s[4 * c + 1] = a0 ^ x1 ^ (x2 ^ a2) ^ a3;
+                s[4 * c + 2] = a0 ^ a1 ^ x2 ^ (x3 ^ a3);
+                s[4 * c + 3] = (x0 ^ a0) ^ a1 ^ a2 ^ x3;
             }
         } else {
             memcpy(s, t, 16);
@@ -118,19 +123,34 @@ void oracle_aes256_encrypt_block(const uint8_t rk[240], const uint8_t in[16], ui
 
 /* ---------------- SP 800-38D GHASH / GCTR ---------------- */
 
-/* Algorithm 1: Z = X * Y in GF(2^128), bit 0 = MSB of byte 0, R = 11100001 || 0^120. */
+static uint64_t be64(const uint8_t *p) {
+    uint64_t v = 0;
+    for (int j = 0; j < 8; j++) v = (v << 8) | p[j];
+    return v;
+}
+static void put_be64(uint8_t *p, uint64_t v) {
+    for (int j = 7; j >= 0; j--, v >>= 8) p[j] = (uint8_t)v;
+}
+
+/* Algorithm 1: Z = X * Y in GF(2^128), bit 0 = MSB of byte 0, R = 11100001 || 0^120.
+ * The 128-bit strings are held as two big-endian 64-bit halves (bit i of the string = bit 63 - i
+ * of the high half for i < 64), so "V >> 1" is a two-word shift; the steps are Algorithm 1's. */
 void oracle_gf128_mul(const uint8_t X[16], const uint8_t Y[16], uint8_t Z[16]) {
-    uint8_t z[16] = {0}, v[16];
-    memcpy(v, Y, 16);
+    const uint64_t xh = be64(X), xl = be64(X + 8);
+    uint64_t zh = 0, zl = 0, vh = be64(Y), vl = be64(Y + 8);
     for (int i = 0; i < 128; i++) {
-        if ((X[i >> 3] >> (7 - (i & 7))) & 1)
-            for (int j = 0; j < 16; j++) z[j] ^= v[j];
-        int lsb = v[15] & 1;
-        for (int j = 15; j > 0; j--) v[j] = (uint8_t)((v[j] >> 1) | (v[j - 1] << 7));
-        v[0] >>= 1;
-        if (lsb) v[0] ^= 0xe1;
+        const uint64_t xi = i < 64 ? (xh >> (63 - i)) & 1 : (xl >> (127 - i)) & 1;
+        if (xi) { /* Z_{i+1} = Z_i xor V_i */
+            zh ^= vh;
+            zl ^= vl;
+        }
+        const uint64_t lsb = vl & 1; /* V_{i+1} = V_i >> 1, xor R if LSB_1(V_i) = 1 */
+        vl = (vl >> 1) | (vh << 63);
+        vh >>= 1;
+        if (lsb) vh ^= 0xe1ULL << 56;
     }
-    memcpy(Z, z, 16);
+    put_be64(Z, zh);
+    put_be64(Z + 8, zl);
 }
 
 static void ghash_update(const uint8_t H[16], uint8_t Y[16], const uint8_t *data, size_t len) {
@@ -270,7 +290,13 @@ static inline uint8_t stream_byte(uint64_t seed, uint64_t b) {
 }
 
 void oracle_fill_stream(uint64_t seed, uint64_t byte_offset, uint8_t *dst, size_t n) {
-    for (size_t i = 0; i < n; i++) dst[i] = stream_byte(seed, byte_offset + i);
+    size_t i = 0;
+    for (; i < n && ((byte_offset + i) & 7); i++) dst[i] = stream_byte(seed, byte_offset + i);
+    for (; i + 8 <= n; i += 8) { /* whole little-endian words of the stream */
+        uint64_t w = oracle_splitmix64_at(seed, (byte_offset + i) >> 3);
+        for (int j = 0; j < 8; j++, w >>= 8) dst[i + j] = (uint8_t)w;
+    }
+    for (; i < n; i++) dst[i] = stream_byte(seed, byte_offset + i);
 }
 
 /* Seal a uniform batch laid out as common.Payload.Raw slots (common/payload.go:22-32):
@@ -281,5 +307,28 @@ void oracle_seal_uniform(const uint8_t key[32], uint8_t *arena, size_t stride, l
     for (long i = 0; i < n; i++) {
         uint8_t *raw = arena + (size_t)i * stride;
         oracle_aesgo_encrypt(key, raw + 4, L, aad_len ? raw : NULL, aad_len, nonces + 12 * i);
+    }
+}
+
+/* Descriptor batches (config 3: per-packet length and key; common/mapping.go:90-99 gives every peer
+ * its own AES): packet i is the Payload.Raw slot at arena + offs[i] holding [aad 4][payload] with
+ * keys + 32 * kidx[i] its key.  Seal: lens[i] = L, crypto/aes.go:41-52 with nonces[12 i..].  Open:
+ * lens[i] = L + 28, crypto/aes.go:57-62; status[i] = 1 / 0.  Packets [lo, hi) only, so callers can
+ * split a batch over threads. */
+void oracle_aesgo_seal_descs(const uint8_t *keys, uint8_t *arena, const uint64_t *offs, const uint32_t *lens,
+                             const uint32_t *kidx, const uint8_t *nonces, long aad_len, long lo, long hi) {
+    for (long i = lo; i < hi; i++) {
+        uint8_t *raw = arena + offs[i];
+        oracle_aesgo_encrypt(keys + 32 * (size_t)kidx[i], raw + 4, lens[i], aad_len ? raw : NULL, aad_len,
+                             nonces + 12 * (size_t)i);
+    }
+}
+
+void oracle_aesgo_open_descs(const uint8_t *keys, uint8_t *arena, const uint64_t *offs, const uint32_t *lens,
+                             const uint32_t *kidx, long aad_len, uint8_t *status, long lo, long hi) {
+    for (long i = lo; i < hi; i++) {
+        uint8_t *raw = arena + offs[i];
+        status[i] = oracle_aesgo_decrypt(keys + 32 * (size_t)kidx[i], raw + 4, lens[i], aad_len ? raw : NULL,
+                                         aad_len) >= 0;
     }
 }

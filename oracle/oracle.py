@@ -57,6 +57,10 @@ def lib() -> C.CDLL:
         L.oracle_fill_stream.argtypes = [C.c_uint64, C.c_uint64, C.c_void_p, C.c_size_t]
         L.oracle_seal_uniform.argtypes = [C.c_char_p, C.c_void_p, C.c_size_t, C.c_long, C.c_long,
                                           C.c_long, C.c_void_p]
+        L.oracle_aesgo_seal_descs.argtypes = [C.c_char_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                              C.c_void_p, C.c_long, C.c_long, C.c_long]
+        L.oracle_aesgo_open_descs.argtypes = [C.c_char_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                              C.c_long, C.c_void_p, C.c_long, C.c_long]
         _lib = L
     return _lib
 
@@ -75,6 +79,8 @@ def ossl() -> C.CDLL:
         L.ossl_x25519_base.argtypes = [C.c_char_p, C.c_char_p]
         L.ossl_seal_uniform.argtypes = [C.c_char_p, C.c_void_p, C.c_long, C.c_long, C.c_int, C.c_int,
                                         C.c_void_p]
+        L.ossl_seal_descs.argtypes = [C.c_char_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                      C.c_int, C.c_long, C.c_long]
         L.ossl_cpu_baseline.argtypes = [C.c_char_p, C.c_int, C.c_long, C.c_int]
         L.ossl_cpu_baseline.restype = C.c_double
         _ossl = L
@@ -187,3 +193,49 @@ def ossl_cpu_baseline(key: bytes, threads: int, packets_per_thread: int, L: int)
     if t < 0:
         raise RuntimeError("cpu baseline failed")
     return t
+
+
+# ---------------- descriptor batches (config 3), split over host threads ----------------
+# ctypes drops the GIL for the duration of each call, so chunks run on separate cores.
+
+def _chunks(n: int, threads: int) -> list[tuple[int, int]]:
+    threads = max(1, min(threads, n or 1))
+    step = (n + threads - 1) // threads
+    return [(lo, min(n, lo + step)) for lo in range(0, n, step)] if n else []
+
+
+def _run(fn, n: int, threads: int) -> None:
+    from concurrent.futures import ThreadPoolExecutor
+
+    with ThreadPoolExecutor(max(1, threads)) as ex:
+        list(ex.map(lambda r: fn(*r), _chunks(n, threads)))
+
+
+def aesgo_seal_descs(keys: bytes, arena, offs, lens, kidx, nonces, aad_len: int = 4, threads: int = 1) -> None:
+    """crypto/aes.go:41-52 on every packet of a descriptor batch, in place in `arena` (numpy uint8).
+    offs uint64, lens uint32 (= L), kidx uint32, nonces uint8 (12 per packet): contiguous numpy arrays."""
+    n = len(offs)
+    _run(lambda lo, hi: lib().oracle_aesgo_seal_descs(keys, arena.ctypes.data, offs.ctypes.data, lens.ctypes.data,
+                                                       kidx.ctypes.data, nonces.ctypes.data, aad_len, lo, hi), n,
+         threads)
+
+
+def aesgo_open_descs(keys: bytes, arena, offs, lens, kidx, status, aad_len: int = 4, threads: int = 1) -> None:
+    """crypto/aes.go:57-62 on every packet (lens = L + 28); status[i] = 1 authentic / 0 errOpen."""
+    n = len(offs)
+    _run(lambda lo, hi: lib().oracle_aesgo_open_descs(keys, arena.ctypes.data, offs.ctypes.data, lens.ctypes.data,
+                                                       kidx.ctypes.data, aad_len, status.ctypes.data, lo, hi), n,
+         threads)
+
+
+def ossl_seal_descs(keys: bytes, arena, offs, lens, kidx, nonces, aad_len: int = 4, threads: int = 1) -> None:
+    """OpenSSL cross-check of aesgo_seal_descs (golden digests of full-size batches)."""
+    n = len(offs)
+    rcs = []
+
+    def one(lo, hi):
+        rcs.append(ossl().ossl_seal_descs(keys, arena.ctypes.data, offs.ctypes.data, lens.ctypes.data,
+                                          kidx.ctypes.data, nonces.ctypes.data, aad_len, lo, hi))
+    _run(one, n, threads)
+    if any(rcs):
+        raise RuntimeError("openssl descriptor seal failed")

@@ -100,6 +100,32 @@ int ossl_seal_uniform(const uint8_t key[32], uint8_t *arena, long stride, long n
     return ok ? 0 : -1;
 }
 
+/* Descriptor batch (config 3), as oracle_aesgo_seal_descs: packet i at arena + offs[i] = [aad 4][L],
+ * key keys + 32 * kidx[i], nonce nonces + 12 i; packets [lo, hi).  For the golden digests. */
+int ossl_seal_descs(const uint8_t *keys, uint8_t *arena, const uint64_t *offs, const uint32_t *lens,
+                    const uint32_t *kidx, const uint8_t *nonces, int aad_len, long lo, long hi) {
+    EVP_CIPHER_CTX *c = EVP_CIPHER_CTX_new();
+    int ok = c != NULL, out = 0;
+    long cur = -1;
+    for (long i = lo; i < hi && ok; i++) {
+        if ((long)kidx[i] != cur) {
+            cur = kidx[i];
+            ok &= EVP_EncryptInit_ex(c, EVP_aes_256_gcm(), NULL, keys + 32 * (size_t)cur, NULL);
+        }
+        uint8_t *raw = arena + offs[i], *data = raw + 4;
+        const int L = (int)lens[i];
+        const uint8_t *iv = nonces + 12 * (size_t)i;
+        ok &= EVP_EncryptInit_ex(c, NULL, NULL, NULL, iv);
+        if (aad_len) ok &= EVP_EncryptUpdate(c, NULL, &out, raw, aad_len);
+        ok &= EVP_EncryptUpdate(c, data, &out, data, L);
+        ok &= EVP_EncryptFinal_ex(c, data + L, &out);
+        ok &= EVP_CIPHER_CTX_ctrl(c, EVP_CTRL_GCM_GET_TAG, 16, data + L);
+        memcpy(data + L + 16, iv, 12);
+    }
+    if (c) EVP_CIPHER_CTX_free(c);
+    return ok ? 0 : -1;
+}
+
 /* ---------------- CPU baseline: crypto/aes.go semantics, one worker per thread ---------------- */
 
 typedef struct {

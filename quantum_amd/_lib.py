@@ -28,6 +28,8 @@ EXPORTS = (
     "qgcm_udp_socket", "qgcm_udp_queue", "qgcm_udp_port", "qgcm_udp_close", "qgcm_udp_recv_slots",
     "qgcm_udp_send_slots",
     "qgcm_tun_open", "qgcm_tun_up", "qgcm_tun_read_slots", "qgcm_tun_write_slots", "qgcm_tun_close",
+    "qgcm_group_create", "qgcm_group_destroy", "qgcm_group_size", "qgcm_group_ctx", "qgcm_group_shard",
+    "qgcm_group_set_keys", "qgcm_group_seal_host", "qgcm_group_open_host",
 )
 
 QGCM_OK = 0
@@ -113,6 +115,18 @@ def _bind(L: C.CDLL) -> None:
     L.qgcm_udp_close.argtypes = [C.c_int]
     L.qgcm_udp_recv_slots.argtypes = [C.c_int, vp, u64, u32, vp, C.c_int]
     L.qgcm_udp_send_slots.argtypes = [C.c_int, vp, u64, u32, vp, C.c_char_p, C.c_int]
+    if hasattr(L, "qgcm_group_create"):  # (older builds loaded by the A/B tools lack the group calls)
+        L.qgcm_group_create.argtypes = [vp, i32, u32, C.c_char_p, i32]
+        L.qgcm_group_create.restype = vp
+        L.qgcm_group_destroy.argtypes = [vp]
+        L.qgcm_group_destroy.restype = None
+        L.qgcm_group_size.argtypes = [vp]
+        L.qgcm_group_ctx.argtypes = [vp, i32]
+        L.qgcm_group_ctx.restype = vp
+        L.qgcm_group_shard.argtypes = [vp, u32]
+        L.qgcm_group_set_keys.argtypes = [vp, u32, u32, u8p]
+        L.qgcm_group_seal_host.argtypes = [vp, vp, vp, u32, vp, u32, vp]
+        L.qgcm_group_open_host.argtypes = [vp, vp, vp, u32, u32, vp]
     if hasattr(L, "qgcm_tun_open"):  # (older builds loaded by the A/B tools lack the TUN calls)
         L.qgcm_tun_open.argtypes = [C.c_char_p, C.c_int, vp, C.c_char_p, sz]
         L.qgcm_tun_up.argtypes = [C.c_char_p, C.c_char_p, C.c_int, C.c_int]

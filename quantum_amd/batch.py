@@ -7,6 +7,7 @@ from __future__ import annotations
 
 import ctypes as C
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -45,9 +46,12 @@ def open_uniform(ctx: Context, arena: torch.Tensor, stride: int, n: int, sealed_
 
 def make_descs(offsets, lengths, keys, device) -> torch.Tensor:
     """Pack qgcm_desc records ({u64 offset, u32 len, u32 key_idx}) into a device uint8 tensor."""
-    off = torch.as_tensor(offsets, dtype=torch.int64).reshape(-1, 1)
-    ln = torch.as_tensor(lengths, dtype=torch.int64).reshape(-1, 1)
-    ky = torch.as_tensor(keys, dtype=torch.int64).reshape(-1, 1)
+    def col(x) -> torch.Tensor:
+        if isinstance(x, np.ndarray):  # unsigned numpy arrays (uint64 offsets) go through int64
+            x = x.astype(np.int64)
+        return torch.as_tensor(x, dtype=torch.int64).reshape(-1, 1)
+
+    off, ln, ky = col(offsets), col(lengths), col(keys)
     words = torch.cat([off & 0xFFFFFFFF, off >> 32, ln, ky], dim=1).to(torch.int64)
     words = torch.where(words >= 2**31, words - 2**32, words).to(torch.int32)
     return words.contiguous().view(torch.uint8).reshape(-1).to(device)

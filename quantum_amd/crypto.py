@@ -48,6 +48,15 @@ class Context:
         self.max_keys = max_keys
         self._next = 0
         self._mu = threading.Lock()
+        self._owned = True
+
+    @classmethod
+    def borrowed(cls, handle: int, device: int, max_keys: int) -> "Context":
+        """A view of a context owned elsewhere (a qgcm_group member): close() leaves it alone."""
+        c = cls.__new__(cls)
+        c.handle, c.device, c.max_keys = handle, device, max_keys
+        c._next, c._mu, c._owned = max_keys, threading.Lock(), False
+        return c
 
     def alloc_slot(self) -> int:
         with self._mu:
@@ -75,9 +84,9 @@ class Context:
         self._reserve(first + len(keys) // keyLength)
 
     def close(self) -> None:
-        if self.handle:
+        if self.handle and getattr(self, "_owned", True):
             _lib.lib().qgcm_destroy(self.handle)
-            self.handle = None
+        self.handle = None
 
     def __del__(self):  # pragma: no cover
         try:

@@ -31,6 +31,8 @@ struct Batch {
     const uint32_t *rk_table;   // [max_keys][kRkWords]
     const uint4 *gh_table;      // [max_keys][kGhEntries]
     const uint32_t *te;         // [512] Te0 then Te1
+    const uint8_t *key_valid;   // [max_keys]: 1 once qgcm_set_key(s) filled the slot (descriptor batches
+                                // skip packets whose key slot was never set: status 0, slot untouched)
     uint64_t stride;
     uint32_t uniform_len;
     uint32_t uniform_key;
@@ -54,7 +56,8 @@ int variant_wgs_per_cu(int variant);
 bool variant_desc(int variant);
 // sorted, 16-packet key-uniform worklist for the descriptor quad kernels (worklist.hip)
 size_t quad_worklist_bytes(uint32_t n, uint32_t max_keys, uint32_t *n_items_out);
-hipError_t launch_quad_worklist(const qgcm_desc *descs, uint32_t n, uint32_t max_keys, bool seal, void *ws,
+hipError_t launch_quad_worklist(const qgcm_desc *descs, uint32_t n, uint32_t max_keys, const uint8_t *key_valid,
+                                bool seal, void *ws,
                                 size_t ws_bytes, uint32_t **worklist_out, uint32_t **counter_out,
                                 uint32_t *n_items_out, hipStream_t s);
 hipError_t launch_packets(bool seal, int variant, const Batch &b, int grid, hipStream_t s);
@@ -76,7 +79,8 @@ bool ctx_key_ready(qgcm_ctx *ctx, uint32_t key_idx);
 hipError_t launch_key_setup(const uint8_t *d_keys, uint32_t first, uint32_t count, uint32_t *rk_table,
                             uint4 *gh_table, const uint8_t *d_sbox, hipStream_t s);
 // Groups descriptor batches into key-uniform 64-packet tiles (counting sort by key_idx).
-hipError_t launch_build_worklist(const qgcm_desc *descs, uint32_t n, uint32_t max_keys, uint32_t *counts,
+hipError_t launch_build_worklist(const qgcm_desc *descs, uint32_t n, uint32_t max_keys, const uint8_t *key_valid,
+                                 uint32_t *counts,
                                  uint32_t *cursors, uint32_t *worklist, uint32_t n_items_cap,
                                  hipStream_t s);
 hipError_t launch_fill_uniform(uint8_t *arena, uint64_t stride, uint32_t n, uint32_t len, uint32_t aad_word,

@@ -988,8 +988,8 @@ __global__ void __launch_bounds__(kOneThreads) gcm_one_kernel(Batch b, const uin
     const uint32_t n16 = (uint32_t)((4ull + Lin + (kSeal ? QGCM_OVERHEAD : 0) + 15) >> 4);
     // as the batch kernels: a key index out of range or an open shorter than 28 B fails the packet
     // (slot untouched); so does a slot past the LDS staging area or misaligned (the host never sends one)
-    if (key >= b.max_keys || (!kSeal && Lin < (uint32_t)QGCM_OVERHEAD) || Lin >= kOneCap || n16 * 16u > kOneCap - 16u ||
-        (off & 15u)) {
+    if (key >= b.max_keys || !b.key_valid[key] || (!kSeal && Lin < (uint32_t)QGCM_OVERHEAD) || Lin >= kOneCap ||
+        n16 * 16u > kOneCap - 16u || (off & 15u)) {
         if (tid == 0 && b.status) b.status[pkt] = 0;
         return;
     }
@@ -1437,12 +1437,14 @@ hipError_t launch_key_setup(const uint8_t *d_keys, uint32_t first, uint32_t coun
 
 // ---------------------------------------------------------------------------------------------
 // Worklist: counting sort of descriptor batches by key_idx into 64-aligned key groups, so every
-// wave64 tile is key-uniform.  Packets with key_idx >= max_keys are dropped (status stays 0).
-__global__ void wl_hist_kernel(const qgcm_desc *descs, uint32_t n, uint32_t max_keys, uint32_t *counts) {
+// wave64 tile is key-uniform.  Packets with key_idx >= max_keys or an unset key slot are dropped
+// (status stays 0).
+__global__ void wl_hist_kernel(const qgcm_desc *descs, uint32_t n, uint32_t max_keys, const uint8_t *key_valid,
+                               uint32_t *counts) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) {
         const uint32_t k = descs[i].key_idx;
-        if (k < max_keys) atomicAdd(&counts[k], 1u);
+        if (k < max_keys && key_valid[k]) atomicAdd(&counts[k], 1u);
     }
 }
 
@@ -1470,25 +1472,27 @@ __global__ void __launch_bounds__(1024) wl_scan_kernel(uint32_t *counts, uint32_
     }
 }
 
-__global__ void wl_scatter_kernel(const qgcm_desc *descs, uint32_t n, uint32_t max_keys, const uint32_t *offs,
-                                  uint32_t *cursors, uint32_t *worklist) {
+__global__ void wl_scatter_kernel(const qgcm_desc *descs, uint32_t n, uint32_t max_keys, const uint8_t *key_valid,
+                                  const uint32_t *offs, uint32_t *cursors, uint32_t *worklist) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) {
         const uint32_t k = descs[i].key_idx;
-        if (k < max_keys) worklist[offs[k] + atomicAdd(&cursors[k], 1u)] = i;
+        if (k < max_keys && key_valid[k]) worklist[offs[k] + atomicAdd(&cursors[k], 1u)] = i;
     }
 }
 
-hipError_t launch_build_worklist(const qgcm_desc *descs, uint32_t n, uint32_t max_keys, uint32_t *counts,
+hipError_t launch_build_worklist(const qgcm_desc *descs, uint32_t n, uint32_t max_keys, const uint8_t *key_valid,
+                                 uint32_t *counts,
                                  uint32_t *cursors, uint32_t *worklist, uint32_t n_items_cap, hipStream_t s) {
     hipError_t e;
     if ((e = hipMemsetAsync(counts, 0, sizeof(uint32_t) * max_keys, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(cursors, 0, sizeof(uint32_t) * max_keys, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(worklist, 0xff, sizeof(uint32_t) * n_items_cap, s)) != hipSuccess) return e;
     const int bs = 256, g = (int)((n + bs - 1) / bs);
-    if (n) hipLaunchKernelGGL(wl_hist_kernel, dim3(g), dim3(bs), 0, s, descs, n, max_keys, counts);
+    if (n) hipLaunchKernelGGL(wl_hist_kernel, dim3(g), dim3(bs), 0, s, descs, n, max_keys, key_valid, counts);
     hipLaunchKernelGGL(wl_scan_kernel, dim3(1), dim3(1024), 0, s, counts, max_keys);
-    if (n) hipLaunchKernelGGL(wl_scatter_kernel, dim3(g), dim3(bs), 0, s, descs, n, max_keys, counts, cursors, worklist);
+    if (n) hipLaunchKernelGGL(wl_scatter_kernel, dim3(g), dim3(bs), 0, s, descs, n, max_keys, key_valid, counts, cursors,
+                                     worklist);
     return hipGetLastError();
 }
 

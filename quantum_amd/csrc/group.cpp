@@ -1,0 +1,289 @@
+// group.cpp -- several GPUs behind one process: keyed host batches hash-sharded over device contexts.
+//
+// quantum is ONE process (main.go:29-114) whose NumWorkers outgoing/incoming workers
+// (main.go:72-75) all call the same Encryption plugin.  On an 8 x MI355X node the drop-in therefore
+// drives every GPU from that one process: a group holds one qgcm_ctx per
+// member (one per GPU; several members may share a device, which is how the 1-GPU tests run G = 2).
+//
+// Partitioning: packet i goes to member hash(key_idx) mod G, the hash of
+// quantum_amd/shard.py key_shard -- (key_idx * 0x9E3779B97F4A7C15 mod 2^64) >> 32.  A peer's packets
+// stay on one GPU (in order), and a member only holds the keys of its own peers:
+// qgcm_group_set_keys installs key k on member shard(k) only.  Packets are independent GCM
+// instances, so there is no collective and no GPU-to-GPU traffic.
+//
+// One host thread and one stream pair per member for the duration of a call.  Its packets are
+// gathered from the caller's arena into pinned staging chunks of up to kChunk bytes (records
+// 16-B aligned, with the descriptors and nonces of the chunk behind them), copied in, sealed/opened
+// by the member's descriptor batch (qgcm_seal_batch / qgcm_open_batch: sorted quad tiles), copied
+// back, and scattered into the caller's slots, which keep their input order.  Two staging slots per
+// member alternate, so the gather of chunk c + 1 overlaps chunk c on the device.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <memory>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "gcm_internal.h"
+
+namespace {
+
+constexpr uint64_t kChunk = 32ull << 20;  // staged slot bytes per chunk
+constexpr int kSlots = 2;                 // staging slots per member (double buffer)
+
+struct Stage {
+    uint8_t *h = nullptr, *d = nullptr;  // pinned host / device: [records][descs][nonces][status]
+    size_t cap = 0;
+    hipStream_t s = nullptr;
+    // the chunk currently in flight in this slot (scattered back once it has landed)
+    std::vector<uint32_t> pk;  // caller packet indices
+    std::vector<uint64_t> at;  // record offset of each packet in the staging area
+    uint64_t status_off = 0;
+    bool busy = false;
+};
+
+struct Member {
+    qgcm_ctx *ctx = nullptr;
+    int device = 0;
+    Stage st[kSlots];
+};
+
+inline uint64_t rec_bytes(bool seal, uint32_t len) {  // AAD word + packet (+ tag || nonce), 16-B aligned
+    return (4ull + len + (seal ? QGCM_OVERHEAD : 0) + 15) & ~15ull;
+}
+
+}  // namespace
+
+struct qgcm_group {
+    std::vector<Member> m;
+    uint32_t max_keys = 0;
+    std::mutex call_mu;  // one batch call at a time (members' staging is reused per call)
+};
+
+namespace {
+
+int grow(Stage &s, int device, size_t bytes) {
+    if (bytes <= s.cap) return QGCM_OK;
+    if (s.h) hipHostFree(s.h);
+    if (s.d) hipFree(s.d);
+    s.h = nullptr;
+    s.d = nullptr;
+    s.cap = 0;
+    if (hipSetDevice(device) != hipSuccess) return QGCM_E_HIP;
+    if (hipHostMalloc(&s.h, bytes, hipHostMallocDefault) != hipSuccess) return QGCM_E_NOMEM;
+    if (hipMalloc(&s.d, bytes) != hipSuccess) return QGCM_E_NOMEM;
+    s.cap = bytes;
+    return QGCM_OK;
+}
+
+// Copies the results of the chunk in flight in `s` back into the caller's slots (after its stream
+// has drained).  Seal: a sealed record comes back whole (ct, tag, nonce); a rejected one (no key on
+// this member) was left untouched.  Open: the payload region comes back -- plaintext, or zeros after
+// an authentication failure (Go 1.9 gcm Open), or the unchanged bytes of a rejected packet; Open
+// never writes the tag or the nonce.
+int land(Stage &s, bool seal, uint8_t *h_arena, const qgcm_desc *descs, uint8_t *h_status, int &bad) {
+    if (!s.busy) return QGCM_OK;
+    s.busy = false;
+    if (hipStreamSynchronize(s.s) != hipSuccess) return QGCM_E_HIP;
+    const uint8_t *st = s.h + s.status_off;
+    for (size_t j = 0; j < s.pk.size(); ++j) {
+        const uint32_t i = s.pk[j];
+        const qgcm_desc &d = descs[i];
+        if (seal) {
+            if (st[j] == 1) memcpy(h_arena + d.offset + 4, s.h + s.at[j] + 4, (size_t)d.len + QGCM_OVERHEAD);
+        } else {
+            memcpy(h_arena + d.offset + 4, s.h + s.at[j] + 4, (size_t)d.len - QGCM_OVERHEAD);
+        }
+        bad += st[j] != 1;
+        if (h_status) h_status[i] = st[j];
+    }
+    return QGCM_OK;
+}
+
+int run_member(Member &mb, bool seal, uint8_t *h_arena, const qgcm_desc *descs, const uint32_t *idx, size_t m,
+               const uint8_t *h_nonces, uint32_t aad_len, uint8_t *h_status, int *bad_out) {
+    int bad = 0, rc = QGCM_OK;
+    if (hipSetDevice(mb.device) != hipSuccess) return QGCM_E_HIP;
+    for (Stage &s : mb.st)
+        if (!s.s && hipStreamCreateWithFlags(&s.s, hipStreamNonBlocking) != hipSuccess) return QGCM_E_HIP;
+    size_t next = 0;
+    int k = 0;
+    while (next < m && rc == QGCM_OK) {
+        Stage &s = mb.st[k];
+        k = (k + 1) % kSlots;
+        if ((rc = land(s, seal, h_arena, descs, h_status, bad)) != QGCM_OK) break;
+        // chunk [next, end): records up to kChunk bytes (at least one packet)
+        size_t end = next;
+        uint64_t bytes = 0;
+        while (end < m) {
+            const uint64_t r = rec_bytes(seal, descs[idx[end]].len);
+            if (end > next && bytes + r > kChunk) break;
+            bytes += r;
+            ++end;
+        }
+        const size_t cn = end - next;
+        const uint64_t off_desc = bytes, off_non = off_desc + ((16ull * cn + 255) & ~255ull);
+        const uint64_t off_st = off_non + (seal && h_nonces ? (12ull * cn + 255) & ~255ull : 0);
+        const uint64_t total = off_st + ((cn + 255) & ~255ull);
+        if ((rc = grow(s, mb.device, std::max<uint64_t>(total, 1ull << 20))) != QGCM_OK) break;
+        s.pk.assign(idx + next, idx + end);
+        s.at.resize(cn);
+        s.status_off = off_st;
+        qgcm_desc *ld = reinterpret_cast<qgcm_desc *>(s.h + off_desc);
+        uint64_t pos = 0;
+        for (size_t j = 0; j < cn; ++j) {  // gather
+            const qgcm_desc &d = descs[s.pk[j]];
+            // seal: AAD, payload and the slot's tag/nonce area (the nonce may already be there); open: the
+            // sealed record is len bytes after the AAD
+            const uint64_t in = 4ull + d.len + (seal ? QGCM_OVERHEAD : 0);
+            s.at[j] = pos;
+            memcpy(s.h + pos, h_arena + d.offset, in);
+            ld[j] = qgcm_desc{pos, d.len, d.key_idx};
+            if (seal && h_nonces) memcpy(s.h + off_non + 12 * j, h_nonces + 12ull * s.pk[j], 12);
+            pos += rec_bytes(seal, d.len);
+        }
+        const uint64_t in_bytes = off_st;  // records, descriptors, nonces
+        if (hipMemcpyAsync(s.d, s.h, in_bytes, hipMemcpyHostToDevice, s.s) != hipSuccess) {
+            rc = QGCM_E_HIP;
+            break;
+        }
+        const qgcm_desc *dd = reinterpret_cast<const qgcm_desc *>(s.d + off_desc);
+        rc = seal ? qgcm_seal_batch(mb.ctx, s.d, dd, (uint32_t)cn, h_nonces ? s.d + off_non : nullptr, aad_len,
+                                    s.d + off_st, s.s)
+                  : qgcm_open_batch(mb.ctx, s.d, dd, (uint32_t)cn, aad_len, s.d + off_st, s.s);
+        if (rc != QGCM_OK) break;
+        if (hipMemcpyAsync(s.h, s.d, bytes, hipMemcpyDeviceToHost, s.s) != hipSuccess ||
+            hipMemcpyAsync(s.h + off_st, s.d + off_st, cn, hipMemcpyDeviceToHost, s.s) != hipSuccess) {
+            rc = QGCM_E_HIP;
+            break;
+        }
+        s.busy = true;
+        next = end;
+    }
+    for (Stage &s : mb.st) {
+        const int r = land(s, seal, h_arena, descs, h_status, bad);
+        if (rc == QGCM_OK) rc = r;
+    }
+    *bad_out = bad;
+    return rc;
+}
+
+int run_group(qgcm_group *g, bool seal, uint8_t *h_arena, const qgcm_desc *descs, uint32_t n,
+              const uint8_t *h_nonces, uint32_t aad_len, uint8_t *h_status) {
+    if (!g || (n && (!h_arena || !descs)) || aad_len > 4 || n > QGCM_MAX_BATCH) return QGCM_E_ARG;
+    if (n == 0) return 0;
+    std::lock_guard<std::mutex> lk(g->call_mu);
+    const int G = (int)g->m.size();
+    std::vector<std::vector<uint32_t>> part(G);
+    int pre_bad = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const qgcm_desc &d = descs[i];
+        const bool ok = d.key_idx < g->max_keys && (seal ? d.len < QGCM_MAX_PAYLOAD
+                                                          : d.len >= QGCM_OVERHEAD && d.len - QGCM_OVERHEAD < QGCM_MAX_PAYLOAD);
+        if (!ok || (d.offset & 3)) {  // rejected as the device batch would: status 0, slot untouched
+            if (h_status) h_status[i] = 0;
+            ++pre_bad;
+            continue;
+        }
+        part[qgcm_group_shard(g, d.key_idx)].push_back(i);
+    }
+    std::vector<int> rc(G, QGCM_OK), bad(G, 0);
+    std::vector<std::thread> thr;
+    for (int k = 0; k < G; ++k) {
+        if (part[k].empty()) continue;
+        thr.emplace_back([&, k] {
+            rc[k] = run_member(g->m[k], seal, h_arena, descs, part[k].data(), part[k].size(), h_nonces, aad_len,
+                               h_status, &bad[k]);
+        });
+    }
+    for (auto &t : thr) t.join();
+    int total_bad = pre_bad;
+    for (int k = 0; k < G; ++k) {
+        if (rc[k] != QGCM_OK) return rc[k];
+        total_bad += bad[k];
+    }
+    return total_bad;
+}
+
+}  // namespace
+
+extern "C" {
+
+qgcm_group *qgcm_group_create(const int *devices, int count, uint32_t max_keys, char *err, int errlen) {
+    if (!devices || count < 1 || count > 64) {
+        if (err && errlen > 0) snprintf(err, (size_t)errlen, "need 1..64 member devices");
+        return nullptr;
+    }
+    auto g = std::make_unique<qgcm_group>();
+    g->max_keys = max_keys;
+    for (int k = 0; k < count; ++k) {
+        Member mb;
+        mb.device = devices[k];
+        mb.ctx = qgcm_create(devices[k], max_keys, err, errlen);
+        if (!mb.ctx) {
+            for (Member &x : g->m) qgcm_destroy(x.ctx);
+            return nullptr;
+        }
+        g->m.push_back(mb);
+    }
+    return g.release();
+}
+
+void qgcm_group_destroy(qgcm_group *g) {
+    if (!g) return;
+    for (Member &mb : g->m) {
+        hipSetDevice(mb.device);
+        for (Stage &s : mb.st) {
+            if (s.s) {
+                hipStreamSynchronize(s.s);
+                hipStreamDestroy(s.s);
+            }
+            if (s.h) hipHostFree(s.h);
+            if (s.d) hipFree(s.d);
+        }
+        qgcm_destroy(mb.ctx);
+    }
+    delete g;
+}
+
+int qgcm_group_size(const qgcm_group *g) { return g ? (int)g->m.size() : 0; }
+
+qgcm_ctx *qgcm_group_ctx(qgcm_group *g, int member) {
+    return g && member >= 0 && member < (int)g->m.size() ? g->m[member].ctx : nullptr;
+}
+
+int qgcm_group_shard(const qgcm_group *g, uint32_t key_idx) {
+    if (!g || g->m.empty()) return QGCM_E_ARG;
+    const uint64_t h = ((uint64_t)key_idx * 0x9E3779B97F4A7C15ull) >> 32;
+    return (int)(h % g->m.size());
+}
+
+int qgcm_group_set_keys(qgcm_group *g, uint32_t first_idx, uint32_t count, const uint8_t *keys) {
+    if (!g || (count && !keys)) return QGCM_E_ARG;
+    if ((uint64_t)first_idx + count > g->max_keys) return QGCM_E_KEY;
+    // each member gets the keys it owns, in runs of consecutive indices
+    for (uint32_t i = 0; i < count;) {
+        const int k = qgcm_group_shard(g, first_idx + i);
+        uint32_t j = i + 1;
+        while (j < count && qgcm_group_shard(g, first_idx + j) == k) ++j;
+        const int rc = qgcm_set_keys(g->m[k].ctx, first_idx + i, j - i, keys + 32ull * i);
+        if (rc != QGCM_OK) return rc;
+        i = j;
+    }
+    return QGCM_OK;
+}
+
+int qgcm_group_seal_host(qgcm_group *g, uint8_t *h_arena, const qgcm_desc *h_descs, uint32_t n,
+                         const uint8_t *h_nonces, uint32_t aad_len, uint8_t *h_status) {
+    return run_group(g, true, h_arena, h_descs, n, h_nonces, aad_len, h_status);
+}
+
+int qgcm_group_open_host(qgcm_group *g, uint8_t *h_arena, const qgcm_desc *h_descs, uint32_t n, uint32_t aad_len,
+                         uint8_t *h_status) {
+    return run_group(g, false, h_arena, h_descs, n, nullptr, aad_len, h_status);
+}
+
+}  // extern "C"

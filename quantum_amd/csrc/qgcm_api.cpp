@@ -47,6 +47,7 @@ struct qgcm_ctx {
     uint4 *d_gh = nullptr;
     uint32_t *d_te = nullptr;
     uint8_t *d_sbox = nullptr;
+    uint8_t *d_key_valid = nullptr;  // device view of key_set (descriptor batches check it per packet)
     std::vector<uint8_t> key_set;  // host view of which slots are populated
     std::mutex key_mu;
 
@@ -152,6 +153,7 @@ Batch base_batch(const qgcm_ctx *ctx) {
     b.rk_table = ctx->d_rk;
     b.gh_table = ctx->d_gh;
     b.te = ctx->d_te;
+    b.key_valid = ctx->d_key_valid;
     b.max_keys = ctx->max_keys;
     return b;
 }
@@ -296,8 +298,8 @@ int run_descs_locked(qgcm_ctx *ctx, bool seal, const qgcm_desc *descs, uint32_t 
             ctx->qws_cap = need;
         }
         uint32_t *wl = nullptr, *counter = nullptr;
-        if (launch_quad_worklist(descs, n, ctx->max_keys, seal, ctx->d_qws, ctx->qws_cap, &wl, &counter, &items, s) !=
-            hipSuccess)
+        if (launch_quad_worklist(descs, n, ctx->max_keys, ctx->d_key_valid, seal, ctx->d_qws, ctx->qws_cap, &wl,
+                                 &counter, &items, s) != hipSuccess)
             return QGCM_E_HIP;
         b.worklist = wl;
         b.tile_counter = counter;
@@ -313,8 +315,8 @@ int run_descs_locked(qgcm_ctx *ctx, bool seal, const qgcm_desc *descs, uint32_t 
         if (hipMalloc(&ctx->d_worklist, (size_t)items * sizeof(uint32_t)) != hipSuccess) return QGCM_E_NOMEM;
         ctx->wl_cap = items;
     }
-    hipError_t e = launch_build_worklist(descs, n, ctx->max_keys, ctx->d_counts, ctx->d_cursors, ctx->d_worklist,
-                                         items, s);
+    hipError_t e = launch_build_worklist(descs, n, ctx->max_keys, ctx->d_key_valid, ctx->d_counts, ctx->d_cursors,
+                                         ctx->d_worklist, items, s);
     if (e != hipSuccess) return QGCM_E_HIP;
     b.worklist = ctx->d_worklist;
     b.n_items = items;
@@ -375,8 +377,8 @@ const char *qgcm_strerror(int code) {
 
 qgcm_ctx *qgcm_create(int device, uint32_t max_keys, char *err, int errlen) {
     (void)tl_dummy;
-    if (max_keys == 0 || max_keys > (1u << 20)) {
-        set_err(err, errlen, "max_keys must be in [1, 2^20]");
+    if (max_keys == 0 || max_keys > QGCM_MAX_KEYS) {
+        set_err(err, errlen, "max_keys must be in [1, 2^20 - 1]");
         return nullptr;
     }
     int ndev = 0;
@@ -435,6 +437,11 @@ qgcm_ctx *qgcm_create(int device, uint32_t max_keys, char *err, int errlen) {
     build_tables(sbox, te);
     bool ok = hipMalloc(&ctx->d_rk, (size_t)max_keys * kRkWords * 4) == hipSuccess &&
               hipMalloc(&ctx->d_gh, (size_t)max_keys * kGhEntries * 16) == hipSuccess &&
+              hipMalloc(&ctx->d_key_valid, max_keys) == hipSuccess &&
+              // unset slots hold zeros, never stale memory, and are marked invalid
+              hipMemset(ctx->d_rk, 0, (size_t)max_keys * kRkWords * 4) == hipSuccess &&
+              hipMemset(ctx->d_gh, 0, (size_t)max_keys * kGhEntries * 16) == hipSuccess &&
+              hipMemset(ctx->d_key_valid, 0, max_keys) == hipSuccess &&
               hipMalloc(&ctx->d_te, sizeof te) == hipSuccess && hipMalloc(&ctx->d_sbox, sizeof sbox) == hipSuccess &&
               hipMalloc(&ctx->d_counts, (size_t)max_keys * 4) == hipSuccess &&
               hipMalloc(&ctx->d_cursors, (size_t)max_keys * 4) == hipSuccess &&
@@ -459,6 +466,7 @@ void qgcm_destroy(qgcm_ctx *ctx) {
     hipFree(ctx->d_gh);
     hipFree(ctx->d_te);
     hipFree(ctx->d_sbox);
+    hipFree(ctx->d_key_valid);
     hipFree(ctx->d_counts);
     hipFree(ctx->d_cursors);
     hipFree(ctx->d_worklist);
@@ -491,6 +499,7 @@ int qgcm_set_keys(qgcm_ctx *ctx, uint32_t first_idx, uint32_t count, const uint8
     if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess ||
         hipMemcpyAsync(d_keys, keys, (size_t)count * 32, hipMemcpyHostToDevice, s) != hipSuccess ||
         launch_key_setup(d_keys, first_idx, count, ctx->d_rk, ctx->d_gh, ctx->d_sbox, s) != hipSuccess ||
+        hipMemsetAsync(ctx->d_key_valid + first_idx, 1, count, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
         rc = QGCM_E_HIP;
     if (s) hipStreamDestroy(s);

@@ -4,9 +4,10 @@
 // (key_idx, length descending) with a device radix sort, then each key's run is padded to a multiple
 // of 16 entries so that every 16-packet wave tile uses ONE key (round keys in SGPRs, one GHASH table
 // per wave) and holds packets of similar length (the 4-lane quads of a wave finish together).
-// Packets that cannot be processed (key index out of range, open with len < 28, payload of
-// QGCM_MAX_PAYLOAD or more) are left out: their
-// status stays 0 and their slot is untouched.
+// Packets that cannot be processed (key index out of range or naming a key slot that was never set,
+// open with len < 28, payload of QGCM_MAX_PAYLOAD or more) are left out: their status stays 0 and
+// their slot is untouched.  Excluded entries sort last under the all-ones key, which no valid packet
+// can produce: key indices stay below QGCM_MAX_KEYS = 2^20 - 1 (qgcm_create caps max_keys).
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 #include <stdint.h>
@@ -17,13 +18,16 @@ namespace qgcm {
 
 constexpr uint32_t kLenBits = 12;  // length rank bits of the sort key; key index in the top 20 bits
 
-__global__ void qwl_keys_kernel(const qgcm_desc *descs, uint32_t n, uint32_t max_keys, bool seal, uint32_t *sort_keys,
-                                uint32_t *vals) {
+// the largest valid key index, QGCM_MAX_KEYS - 1, must sort below the all-ones excluded marker
+static_assert(QGCM_MAX_KEYS - 1u < (1u << (32 - kLenBits)) - 1u, "key index would collide with the excluded marker");
+
+__global__ void qwl_keys_kernel(const qgcm_desc *descs, uint32_t n, uint32_t max_keys, const uint8_t *key_valid,
+                                bool seal, uint32_t *sort_keys, uint32_t *vals) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const qgcm_desc d = descs[i];
     uint32_t sk = 0xffffffffu;
-    const bool ok = d.key_idx < max_keys && (seal || d.len >= (uint32_t)QGCM_OVERHEAD) &&
+    const bool ok = d.key_idx < max_keys && key_valid[d.key_idx] && (seal || d.len >= (uint32_t)QGCM_OVERHEAD) &&
                     d.len - (seal ? 0u : (uint32_t)QGCM_OVERHEAD) < QGCM_MAX_PAYLOAD;
     if (ok) {
         const uint32_t L = seal ? d.len : d.len - QGCM_OVERHEAD;
@@ -104,7 +108,8 @@ size_t quad_worklist_bytes(uint32_t n, uint32_t max_keys, uint32_t *n_items_out)
     return 4 * al(4ull * n) + 3 * al(4ull * max_keys) + al(4ull * items) + al(16) + al(cub);
 }
 
-hipError_t launch_quad_worklist(const qgcm_desc *descs, uint32_t n, uint32_t max_keys, bool seal, void *ws,
+hipError_t launch_quad_worklist(const qgcm_desc *descs, uint32_t n, uint32_t max_keys, const uint8_t *key_valid,
+                                bool seal, void *ws,
                                 size_t ws_bytes, uint32_t **worklist_out, uint32_t **counter_out,
                                 uint32_t *n_items_out, hipStream_t s) {
     uint32_t items = 0;
@@ -128,7 +133,8 @@ hipError_t launch_quad_worklist(const qgcm_desc *descs, uint32_t n, uint32_t max
     if ((e = hipMemsetAsync(worklist, 0xff, 4ull * items, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(counter, 0, 16, s)) != hipSuccess) return e;
     const int bs = 256, g = (int)((n + bs - 1) / bs);
-    if (n) hipLaunchKernelGGL(qwl_keys_kernel, dim3(g), dim3(bs), 0, s, descs, n, max_keys, seal, k_in, v_in);
+    if (n) hipLaunchKernelGGL(qwl_keys_kernel, dim3(g), dim3(bs), 0, s, descs, n, max_keys, key_valid, seal, k_in,
+                                 v_in);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     // only the bits a valid key can use, plus one so that excluded entries (all ones) sort last
     int end_bit = kLenBits + 1;

@@ -49,3 +49,79 @@ def reduce_step_time(elapsed_s: float, ok: bool, dist=None, device=None) -> tupl
     t = torch.tensor([elapsed_s, 0.0 if ok else 1.0], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t[0].item()), t[1].item() == 0.0
+
+
+class Group:
+    """Several GPUs behind one process (qgcm_group_*, include/qgcm.h): quantum is one process
+    (main.go:29-114) whose workers all call one Encryption plugin, so its drop-in drives every GPU of a
+    node from that process.  Keyed host batches are split by key_shard over the member contexts (one
+    host thread and stream set per member, no collective); results land in the caller's slots."""
+
+    def __init__(self, devices, max_keys: int = 4096):
+        import ctypes as C
+
+        from . import _lib
+
+        devs = (C.c_int * len(devices))(*devices)
+        err = C.create_string_buffer(_lib.ERRLEN)
+        h = _lib.lib().qgcm_group_create(devs, len(devices), max_keys, err, _lib.ERRLEN)
+        if not h:
+            raise _lib.QgcmError(f"qgcm_group_create({list(devices)}): {err.value.decode()}")
+        self.handle, self.devices, self.max_keys = h, list(devices), max_keys
+
+    def member(self, m: int):
+        """Member m's device context (borrowed: the group owns it) for device batches on it."""
+        from . import _lib
+        from .crypto import Context
+
+        h = _lib.lib().qgcm_group_ctx(self.handle, m)
+        if not h:
+            raise _lib.QgcmError(f"no member {m}")
+        return Context.borrowed(h, self.devices[m], self.max_keys)
+
+    def shard(self, key_idx: int) -> int:
+        from . import _lib
+
+        return _lib.check(_lib.lib().qgcm_group_shard(self.handle, key_idx), "qgcm_group_shard")
+
+    def set_keys(self, first: int, keys: bytes) -> None:
+        from . import _lib
+
+        _lib.check(_lib.lib().qgcm_group_set_keys(self.handle, first, len(keys) // 32, keys), "qgcm_group_set_keys")
+
+    def _run(self, seal: bool, arena_ptr: int, descs, n: int, nonces_ptr, aad_len: int, status_ptr) -> int:
+        from . import _lib
+
+        L = _lib.lib()
+        d = descs.ctypes.data if hasattr(descs, "ctypes") else descs
+        rc = (L.qgcm_group_seal_host(self.handle, arena_ptr, d, n, nonces_ptr, aad_len, status_ptr) if seal else
+              L.qgcm_group_open_host(self.handle, arena_ptr, d, n, aad_len, status_ptr))
+        return _lib.check(rc, "qgcm_group_seal_host" if seal else "qgcm_group_open_host")
+
+    def seal_host(self, arena_ptr: int, descs, n: int, nonces_ptr=None, aad_len: int = 4, status_ptr=None) -> int:
+        """descs: numpy structured/uint8 array of qgcm_desc records (host).  Returns failed packets."""
+        return self._run(True, arena_ptr, descs, n, nonces_ptr, aad_len, status_ptr)
+
+    def open_host(self, arena_ptr: int, descs, n: int, aad_len: int = 4, status_ptr=None) -> int:
+        return self._run(False, arena_ptr, descs, n, None, aad_len, status_ptr)
+
+    def close(self) -> None:
+        from . import _lib
+
+        if self.handle:
+            _lib.lib().qgcm_group_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def host_descs(offsets, lengths, keys) -> np.ndarray:
+    """qgcm_desc records {u64 offset, u32 len, u32 key_idx} as a host numpy array."""
+    dt = np.dtype([("offset", "<u8"), ("len", "<u4"), ("key_idx", "<u4")])
+    d = np.zeros(len(offsets), dtype=dt)
+    d["offset"], d["len"], d["key_idx"] = offsets, lengths, keys
+    return d

@@ -41,6 +41,11 @@ def batch_digests():
 
 
 @pytest.fixture(scope="session")
+def config3_digest():
+    return golden("config3_digest.json")
+
+
+@pytest.fixture(scope="session")
 def ctx():
     """One device context per test session (GPU tests only)."""
     import torch

@@ -12,6 +12,9 @@ Sources (no reference code is copied; the reference ships no known-answer vector
   * kdf.json         PBKDF2-HMAC-SHA512 published vectors + the path's key; RFC 7748 X25519 vectors;
                      a 1024-peer derivation table digest (common/mapping.go:90-99).
   * batch_digest.json  SHA-256 of the sealed config-2 arena (2^20 x 1350 B) and of a smaller one.
+  * config3_digest.json  BASELINE config 3 (tests/config3_workload.py): 2^20 packets of U{64..9000} B
+                     under 1024 X25519+PBKDF2 peer keys; SHA-256 of the arena before sealing, sealed
+                     (OpenSSL, its first 4096 packets cross-checked against the restatement) and opened.
 """
 from __future__ import annotations
 
@@ -24,6 +27,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
 from oracle import oracle as O  # noqa: E402
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -184,6 +188,55 @@ def batch_digest(n: int, L: int, stride: int, key: bytes, check_oracle: int) -> 
                 sha256_plain=hashlib.sha256(plain.tobytes()).hexdigest(), oracle_checked_prefix=check_oracle)
 
 
+def peer_keys() -> bytes:
+    """The 1024 config-3 peer keys (common/mapping.go:90-99) from OpenSSL X25519 + hashlib PBKDF2."""
+    import config3_workload as W
+
+    me_priv, me_salt, privs, salts = W.peer_inputs(O)
+    out = bytearray()
+    for p_priv, p_salt in zip(privs, salts):
+        secret = O.ossl_x25519(me_priv, O.ossl_x25519_base(p_priv))
+        salt = O.ossl_x25519(me_salt, O.ossl_x25519_base(p_salt))
+        out += hashlib.pbkdf2_hmac("sha512", secret, salt, 10000, 32)
+    return bytes(out)
+
+
+def sha_chunks(a: np.ndarray) -> str:
+    hsh = hashlib.sha256()
+    for i in range(0, len(a), 1 << 28):
+        hsh.update(memoryview(a[i:i + (1 << 28)]))
+    return hsh.hexdigest()
+
+
+def config3(threads: int = 8) -> dict:
+    import config3_workload as W
+
+    keys = peer_keys()
+    lens, kidx = W.lengths(), W.key_indices()
+    offs, size = W.layout(lens)
+    nonces = W.nonces(O)
+    arena = W.host_arena(O, size, offs, kidx)
+    plain_sha = sha_chunks(arena)
+    check = 4096
+    ref = arena.copy() if check else None
+    O.ossl_seal_descs(keys, arena, offs, lens, kidx, nonces, 4, threads)
+    if check:
+        O.aesgo_seal_descs(keys, ref, offs[:check], lens[:check], kidx[:check], nonces, 4, threads)
+        end = int(offs[check])
+        assert np.array_equal(ref[:end], arena[:end]), "restatement != openssl on the config-3 prefix"
+        del ref
+    sealed_sha = sha_chunks(arena)
+    tails = arena[W.tail_index(offs, lens)]
+    opened = W.host_arena(O, size, offs, kidx)
+    opened[W.tail_index(offs, lens)] = tails  # Open leaves tag || nonce in the slot
+    opened_sha = sha_chunks(opened)
+    return dict(n=W.N, keys=W.NKEYS, sha256_of_1024_keys=hashlib.sha256(keys).hexdigest(),
+                payload_bytes=int(lens.sum()), arena_bytes=size, slot_bytes_used=int(offs[-1]) + ((4 + int(lens[-1]) + 31) & ~3),
+                sha256_plain=plain_sha, sha256_sealed=sealed_sha, sha256_opened=opened_sha,
+                oracle_checked_prefix=check, seeds=dict(len=W.SEED_LEN, key=W.SEED_KEY, arena=W.SEED_ARENA,
+                                                        nonce=W.SEED_NONCE, me=W.SEED_ME, peers=W.SEED_PEERS))
+
+
 def main() -> None:
     os.makedirs(HERE, exist_ok=True)
     json.dump(gcm_spec(), open(os.path.join(HERE, "gcm_spec.json"), "w"), indent=1)
@@ -194,6 +247,8 @@ def main() -> None:
     digests = [batch_digest(4096, 1350, 1392, key, 4096), batch_digest(1 << 20, 1350, 1392, key, 2048),
                batch_digest(1 << 14, 1350, 1472, key, 512)]
     json.dump(digests, open(os.path.join(HERE, "batch_digest.json"), "w"), indent=1)
+    if "--no-config3" not in sys.argv:
+        json.dump(config3(), open(os.path.join(HERE, "config3_digest.json"), "w"), indent=1)
     print("golden fixtures written")
 
 

@@ -146,3 +146,17 @@ def test_null_and_bad_args_rejected():
     assert L.qgcm_coalescer_open(None, 0, None, 0, None, 0) == -1
     L.qgcm_coalescer_destroy(None)
     assert not L.qgcm_host_alloc(0)
+
+
+def test_max_keys_bound():
+    """max_keys above QGCM_MAX_KEYS (2^20 - 1) is refused before any device work: key index 2^20 - 1
+    would sort onto the descriptor worklist's all-ones excluded marker (worklist.hip)."""
+    from quantum_amd import _lib
+
+    L = _lib.lib()
+    for bad in (0, 1 << 20, 1 << 31):
+        err = C.create_string_buffer(_lib.ERRLEN)
+        assert not L.qgcm_create(0, bad, err, _lib.ERRLEN)
+        assert b"max_keys" in err.value
+    hdr = open(os.path.join(ROOT, "include", "qgcm.h")).read()
+    assert "#define QGCM_MAX_KEYS ((1u << 20) - 1)" in hdr

@@ -35,3 +35,25 @@ def test_bench_two_ranks_one_device():
     assert line["scaling"] == "weak" and line["config"]["packets_per_gpu"] == 65536
     assert "cpu_baseline" not in line  # rank 0 at N=1 only
     assert line["value"] > 0
+
+
+def test_bench_config4_two_ranks_one_device():
+    """The driver's N > 1 default: config 4 (64 x 2^20 x 1350 B in total) sharded over the ranks, here 2
+    ranks x 2^25 packets (47 GB of slots each) on cuda:0 over gloo; strong scaling over the fixed total."""
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", "29534", os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--settle-ms", "0", "--dist-backend", "gloo",
+           "--one-device"]
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=400)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    line = json.loads(lines[0])
+    assert line["status_ok"] is True and line["scaling"] == "strong"
+    assert line["config"]["packets_total"] == 64 << 20 and line["config"]["packets_per_gpu"] == 32 << 20
+    assert line["config"]["workload"].startswith("config4")

@@ -1,0 +1,163 @@
+"""Several device contexts behind one process (qgcm_group_*, SURVEY.md s8e, main.go:72-75) and BASELINE
+config 4's per-GPU shard.
+
+* G = 2 and G = 3 member contexts on device 0 (the 1-GPU box stands in for a node's GPUs): a keyed
+  host batch is split by hash(key_idx) mod G (quantum_amd.shard.key_shard), each member runs its
+  packets on its own thread and streams, and every slot comes back in place bit-exact with the
+  oracle; keys live only on their owning member; tamper -> status 0 + zeroed plaintext; a key that no
+  member holds -> status 0, slot untouched.
+* One GPU's full config-4 shard: 8 x 2^20 packets x 1350 B (11.8 GB of slots resident), its first
+  2^20 slots equal to the committed config-2 digest, every packet authentic after the open and its
+  payload restored.
+"""
+import ctypes as C
+import hashlib
+import random
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+AAD = bytes([10, 99, 0, 1])
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as T
+
+    if not T.cuda.is_available():
+        pytest.skip("no GPU")
+    return T
+
+
+def host_buffer(nbytes: int, pinned: bool):
+    from quantum_amd import _lib
+
+    if pinned:
+        ptr = _lib.lib().qgcm_host_alloc(nbytes)
+        assert ptr
+        arr = np.frombuffer((C.c_uint8 * nbytes).from_address(ptr), dtype=np.uint8)
+        return arr, ptr, lambda: _lib.lib().qgcm_host_free(ptr)
+    arr = np.zeros(nbytes, dtype=np.uint8)
+    return arr, arr.ctypes.data, lambda: None
+
+
+@pytest.mark.parametrize("G,pinned", [(2, True), (3, False)])
+def test_group_keyed_host_batch_vs_oracle(torch, G, pinned):
+    from quantum_amd import shard
+
+    grp = shard.Group([0] * G, max_keys=256)
+    try:
+        rng = random.Random(0x6A0 + G)
+        nkeys = 40
+        keys = [rng.randbytes(32) for _ in range(nkeys)]
+        grp.set_keys(0, b"".join(keys))
+        assert [grp.shard(k) for k in range(256)] == shard.key_shard(np.arange(256), G).tolist()
+        owners = shard.key_shard(np.arange(nkeys), G)
+        assert len(set(owners.tolist())) == G  # every member owns some of the peers
+        n = 3000
+        kidx = [200 if i % 97 == 5 else rng.randrange(nkeys) for i in range(n)]  # key 200: no member has it
+        lens = [rng.choice([0, 1, 15, 16, 17, 1350, 1433, 4081]) if i % 4 else rng.randint(0, 3000) for i in range(n)]
+        offs, pos = [], 0
+        for i, L in enumerate(lens):  # 4-B and 16-B aligned slots mixed
+            offs.append(pos)
+            pos += (4 + L + 28 + 15) & ~15 if i % 2 else (4 + L + 28 + 3) & ~3
+        arena, aptr, free = host_buffer(pos + 64, pinned)
+        try:
+            arena[:] = np.frombuffer(rng.randbytes(pos + 64), dtype=np.uint8)
+            for i in range(n):
+                arena[offs[i]:offs[i] + 4] = np.frombuffer(AAD, dtype=np.uint8)
+            plain = arena.copy()
+            nonces = np.frombuffer(rng.randbytes(12 * n), dtype=np.uint8).copy()
+            ref = plain.copy()
+            for i, L in enumerate(lens):
+                if kidx[i] >= nkeys:
+                    continue
+                buf = bytearray(ref[offs[i] + 4:offs[i] + 4 + L + 28].tobytes())
+                O.aesgo_encrypt(keys[kidx[i]], buf, L, AAD, bytes(nonces[12 * i:12 * i + 12]))
+                ref[offs[i] + 4:offs[i] + 4 + L + 28] = np.frombuffer(bytes(buf), dtype=np.uint8)
+            descs = shard.host_descs(offs, lens, kidx)
+            status = np.full(n, 7, dtype=np.uint8)
+            unset = sum(k >= nkeys for k in kidx)
+            bad = grp.seal_host(aptr, descs, n, nonces.ctypes.data, 4, status.ctypes.data)
+            assert bad == unset
+            assert status.tolist() == [0 if k >= nkeys else 1 for k in kidx]
+            assert np.array_equal(arena, ref)  # every slot in place, input order kept
+
+            tampered = set(rng.sample([i for i in range(n) if kidx[i] < nkeys], 40))
+            for i in tampered:
+                arena[offs[i] + 4 + lens[i] + rng.randrange(28)] ^= 0x04
+            before = arena.copy()
+            d_open = shard.host_descs(offs, [L + 28 for L in lens], kidx)
+            status[:] = 7
+            bad = grp.open_host(aptr, d_open, n, 4, status.ctypes.data)
+            assert bad == unset + len(tampered)
+            for i, L in enumerate(lens):
+                o = offs[i]
+                if kidx[i] >= nkeys:
+                    assert status[i] == 0 and np.array_equal(arena[o:o + 4 + L + 28], before[o:o + 4 + L + 28])
+                elif i in tampered:
+                    assert status[i] == 0 and not arena[o + 4:o + 4 + L].any()
+                    assert np.array_equal(arena[o + 4 + L:o + 4 + L + 28], before[o + 4 + L:o + 4 + L + 28])
+                else:
+                    assert status[i] == 1 and np.array_equal(arena[o:o + 4 + L], plain[o:o + 4 + L])
+        finally:
+            free()
+    finally:
+        grp.close()
+
+
+def test_group_members_hold_only_their_keys(torch):
+    """A member's own context rejects a key another member owns (status 0, slot untouched)."""
+    from quantum_amd import batch, shard
+
+    grp = shard.Group([0, 0], max_keys=16)
+    try:
+        keys = [bytes([k]) * 32 for k in range(8)]
+        grp.set_keys(0, b"".join(keys))
+        owner = [grp.shard(k) for k in range(8)]
+        for m in (0, 1):
+            ctx = grp.member(m)
+            arena = torch.zeros(8 * 128, dtype=torch.uint8, device="cuda")
+            status = torch.full((8,), 7, dtype=torch.uint8, device="cuda")
+            batch.seal_batch(ctx, arena, batch.make_descs([128 * k for k in range(8)], [64] * 8, list(range(8)), "cuda"),
+                             8, None, status=status)
+            assert status.cpu().tolist() == [1 if owner[k] == m else 0 for k in range(8)]
+    finally:
+        grp.close()
+
+
+def test_config4_one_gpu_shard(torch, batch_digests):
+    """8 x 2^20 packets x 1350 B on one GPU = its shard of config 4 (64 x 2^20 over 8 GPUs)."""
+    from quantum_amd import batch
+    from quantum_amd.crypto import Context, derive_key
+
+    d = next(x for x in batch_digests if x["n"] == 1 << 20 and x["len"] == 1350)
+    N, L, stride = 8 << 20, d["len"], d["stride"]
+    ctx = Context(device=0, max_keys=4)
+    ctx.set_key(0, derive_key(b"AES256Key-32Characters1234567890", bytes(range(32))))
+    arena = torch.zeros(N * stride, dtype=torch.uint8, device="cuda")  # gaps zeroed, as the golden arena
+    nonces = torch.empty(12 * N, dtype=torch.uint8, device="cuda")
+    aad_word = int.from_bytes(AAD, "little")
+    batch.fill_uniform(arena, stride, N, L, aad_word, d["seed_payload"], nonces, d["seed_nonce"])
+    status = torch.zeros(N, dtype=torch.uint8, device="cuda")
+    batch.seal_uniform(ctx, arena, stride, N, L, 0, nonces, status=status)
+    assert int(status.sum()) == N
+    h = hashlib.sha256()
+    head = (1 << 20) * stride
+    for i in range(0, head, 1 << 28):
+        h.update(memoryview(arena[i:min(head, i + (1 << 28))].cpu().numpy()))
+    assert h.hexdigest() == d["sha256_sealed"]  # the first 2^20 slots are config 2's sealed arena
+    status.zero_()
+    batch.open_uniform(ctx, arena, stride, N, L + 28, 0, status=status)
+    assert int(status.sum()) == N
+    ref = torch.empty_like(arena)
+    batch.fill_uniform(ref, stride, N, L, aad_word, d["seed_payload"], None, 0)
+    a2, r2 = arena.view(N, stride), ref.view(N, stride)
+    assert torch.equal(a2[:, :4 + L], r2[:, :4 + L])  # every payload restored in place
+    del arena, ref, a2, r2, nonces
+    ctx.close()
+    torch.cuda.empty_cache()
