@@ -83,6 +83,8 @@ def ossl() -> C.CDLL:
                                       C.c_int, C.c_long, C.c_long]
         L.ossl_cpu_baseline.argtypes = [C.c_char_p, C.c_int, C.c_long, C.c_int]
         L.ossl_cpu_baseline.restype = C.c_double
+        L.ossl_cpu_baseline_mode.argtypes = [C.c_char_p, C.c_int, C.c_long, C.c_int, C.c_int]
+        L.ossl_cpu_baseline_mode.restype = C.c_double
         _ossl = L
     return _ossl
 
@@ -188,8 +190,10 @@ def ossl_seal_uniform(key: bytes, arena_addr: int, stride: int, n: int, L: int, 
         raise RuntimeError("openssl batch seal failed")
 
 
-def ossl_cpu_baseline(key: bytes, threads: int, packets_per_thread: int, L: int) -> float:
-    t = ossl().ossl_cpu_baseline(key, threads, packets_per_thread, L)
+def ossl_cpu_baseline(key: bytes, threads: int, packets_per_thread: int, L: int, mode: int = 0) -> float:
+    """Wall seconds for `threads` workers each sealing + opening packets_per_thread L-byte packets.
+    mode 0: a getrandom nonce per packet as crypto/aes.go:44 draws it; 1: counter nonces (no syscall)."""
+    t = ossl().ossl_cpu_baseline_mode(key, threads, packets_per_thread, L, mode)
     if t < 0:
         raise RuntimeError("cpu baseline failed")
     return t

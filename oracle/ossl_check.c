@@ -132,6 +132,7 @@ typedef struct {
     const uint8_t *key;
     long packets;
     int L;
+    int mode; /* 0: getrandom nonce per packet (crypto/aes.go:44); 1: counter nonce (no syscall) */
     int ok;
     double seconds;
 } worker_arg;
@@ -159,7 +160,12 @@ static void *baseline_worker(void *p) {
         int L = a->L;
         /* Encrypt: crypto/aes.go:41-52 -- fresh nonce from the kernel RNG per packet */
         uint8_t nonce[12];
-        if (getrandom(nonce, 12, 0) != 12) { ok = 0; break; }
+        if (a->mode == 0) {
+            if (getrandom(nonce, 12, 0) != 12) { ok = 0; break; }
+        } else {
+            memset(nonce, 0, 12);
+            memcpy(nonce, &i, sizeof i);
+        }
         ok &= EVP_EncryptInit_ex(e, NULL, NULL, NULL, nonce);
         ok &= EVP_EncryptUpdate(e, NULL, &out, raw, 4);
         ok &= EVP_EncryptUpdate(e, data, &out, data, L);
@@ -183,7 +189,7 @@ static void *baseline_worker(void *p) {
 
 /* Runs `threads` workers, each sealing+opening `packets_per_thread` packets of L bytes.
  * Returns wall seconds (max over workers), or -1 on failure. */
-double ossl_cpu_baseline(const uint8_t key[32], int threads, long packets_per_thread, int L) {
+double ossl_cpu_baseline_mode(const uint8_t key[32], int threads, long packets_per_thread, int L, int mode) {
     if (threads < 1 || threads > 1024 || L < 0 || L > 9000) return -1;
     pthread_t *tid = calloc((size_t)threads, sizeof(pthread_t));
     worker_arg *args = calloc((size_t)threads, sizeof(worker_arg));
@@ -192,6 +198,7 @@ double ossl_cpu_baseline(const uint8_t key[32], int threads, long packets_per_th
         args[t].key = key;
         args[t].packets = packets_per_thread;
         args[t].L = L;
+        args[t].mode = mode;
         pthread_create(&tid[t], NULL, baseline_worker, &args[t]);
     }
     int ok = 1;
@@ -203,4 +210,8 @@ double ossl_cpu_baseline(const uint8_t key[32], int threads, long packets_per_th
     free(tid);
     free(args);
     return ok ? wall : -1.0;
+}
+
+double ossl_cpu_baseline(const uint8_t key[32], int threads, long packets_per_thread, int L) {
+    return ossl_cpu_baseline_mode(key, threads, packets_per_thread, L, 0);
 }

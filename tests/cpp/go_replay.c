@@ -1,0 +1,217 @@
+/*
+ * go_replay.c -- replays, through include/qgcm.h, the exact C call sequence go/crypto/gpu_aes.go
+ * makes when go/crypto/gpu_aes_test.go runs (no Go toolchain exists in this image or on the GPU box,
+ * so the cgo shim is exercised by its calls, not by cgo).  TEST INFRASTRUCTURE: links the oracle
+ * (oracle/_build/liboracle.so) to check every sealed buffer: the nonce the library drew is in the
+ * output, so oracle_aesgo_encrypt(key, plaintext, L, aad, that nonce) must reproduce it exactly.
+ *
+ *   TestGPUAES        crypto/crypto_test.go:54-101 TestAES: 1472 x 0x01 in a 1500-B buffer, nil
+ *                     additional data (bytePtr(nil) = NULL, aad_len 0), Encrypt -> 1500, Decrypt -> 1472
+ *   TestGPUAESEdges   the shim's guards: no room for tag/nonce (never reaches C), empty payload,
+ *                     Decrypt of 0/5/11/12/27 bytes (-> errOpen before C below 28; libqgcm also
+ *                     returns -1 and leaves the bytes untouched when called), tamper -> zeroed plaintext
+ *   TestGPUAESCoalesced  16 threads x 200 packets through qgcm_coalescer_seal/open with 4-B AAD
+ *   TestGPUGroup      NewGPUGroup + NewGPUAES: key installed on the owning member only, calls on it
+ *   TestCreateError   qgcm_create on a device that does not exist: NULL + a message (cError)
+ * Usage: go_replay [TestName ...] (default: all).  Prints "--- PASS: Name" per test.
+ */
+#include <pthread.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "qgcm.h"
+
+/* oracle/gcm_oracle.c (test infrastructure) */
+long oracle_aesgo_encrypt(const uint8_t key[32], uint8_t *data, long length, const uint8_t *aad, long aad_len,
+                          const uint8_t nonce[12]);
+
+static int failures = 0;
+#define CHECK(c)                                                              \
+    do {                                                                      \
+        if (!(c)) {                                                           \
+            fprintf(stderr, "%s:%d: check failed: %s\n", __FILE__, __LINE__, #c); \
+            ++failures;                                                       \
+            return;                                                           \
+        }                                                                     \
+    } while (0)
+
+static const char kSecret[] = "AES256Key-32Characters1234567890";
+
+/* installKey: qgcm_derive_key + qgcm_set_key, returning the key for the oracle */
+static int install_key(qgcm_ctx *ctx, uint32_t idx, const uint8_t *salt, uint8_t key[32]) {
+    if (qgcm_derive_key((const uint8_t *)kSecret, 32, salt, 32, key) != QGCM_OK) return -1;
+    return qgcm_set_key(ctx, idx, key);
+}
+
+/* the sealed buffer data[0:L+28] equals the oracle's seal of `plain` under the nonce it carries */
+static int matches_oracle(const uint8_t key[32], const uint8_t *plain, long L, const uint8_t *aad, long aad_len,
+                          const uint8_t *sealed) {
+    uint8_t *buf = malloc((size_t)L + 28), nonce[12];
+    memcpy(nonce, sealed + L + 16, 12);
+    memcpy(buf, plain, (size_t)L);
+    int ok = oracle_aesgo_encrypt(key, buf, L, aad, aad_len, nonce) == L + 28 && !memcmp(buf, sealed, (size_t)L + 28);
+    free(buf);
+    return ok;
+}
+
+static void TestGPUAES(qgcm_ctx *ctx) {
+    uint8_t salt[32], key[32];
+    for (int i = 0; i < 32; ++i) salt[i] = (uint8_t)(i * 37 + 1); /* TestAES: a random salt */
+    CHECK(install_key(ctx, 0, salt, key) == QGCM_OK);
+    enum { bufLen = 1500, dataLen = bufLen - 28 };
+    uint8_t buf[bufLen], expected[dataLen];
+    memset(buf, 0, sizeof buf);
+    memset(buf, 1, dataLen); /* fillSlice(buf[:dataLen]) */
+    memset(expected, 1, dataLen);
+    /* aes.Encrypt(buf, dataLen, nil): bytePtr(nil) = NULL, len 0; seal_one with nonce NULL (getrandom) */
+    long n = qgcm_seal_one(ctx, 0, buf, dataLen, NULL, 0, NULL);
+    CHECK(n == bufLen);
+    CHECK(memcmp(buf, expected, dataLen) != 0);
+    CHECK(matches_oracle(key, expected, dataLen, NULL, 0, buf));
+    n = qgcm_open_one(ctx, 0, buf, bufLen, NULL, 0); /* aes.Decrypt(buf, nil) */
+    CHECK(n == dataLen);
+    CHECK(memcmp(buf, expected, dataLen) == 0);
+    printf("--- PASS: TestGPUAES\n");
+}
+
+static void TestGPUAESEdges(qgcm_ctx *ctx) {
+    uint8_t salt[32] = {0}, key[32];
+    CHECK(install_key(ctx, 1, salt, key) == QGCM_OK);
+    const uint8_t ip[4] = {10, 99, 0, 1};
+    /* empty payload: Encrypt(make([]byte, 28), 0, ip) -> 28, Decrypt -> 0 */
+    uint8_t empty[28];
+    memset(empty, 0xAA, sizeof empty);
+    CHECK(qgcm_seal_one(ctx, 1, empty, 0, ip, 4, NULL) == 28);
+    CHECK(matches_oracle(key, empty, 0, ip, 4, empty));
+    CHECK(qgcm_open_one(ctx, 1, empty, 28, ip, 4) == 0);
+    /* short Decrypt inputs: the shim answers errOpen itself below 28; the C call agrees and leaves them */
+    const long shorts[] = {0, 5, 11, 12, 27};
+    for (unsigned k = 0; k < sizeof shorts / sizeof shorts[0]; ++k) {
+        uint8_t s[28], before[28];
+        for (int i = 0; i < 28; ++i) s[i] = before[i] = (uint8_t)(i + k);
+        CHECK(qgcm_open_one(ctx, 1, shorts[k] ? s : NULL, shorts[k], ip, 4) == -1);
+        CHECK(memcmp(s, before, sizeof s) == 0);
+    }
+    /* tamper: Decrypt fails with the plaintext zeroed, tag and nonce untouched */
+    uint8_t data[1350 + 28], plain[1350];
+    for (int i = 0; i < 1350; ++i) plain[i] = data[i] = (uint8_t)(i * 7);
+    CHECK(qgcm_seal_one(ctx, 1, data, 1350, ip, 4, NULL) == 1350 + 28);
+    CHECK(matches_oracle(key, plain, 1350, ip, 4, data));
+    uint8_t tail[28];
+    memcpy(tail, data + 1350, 28);
+    data[7] ^= 1;
+    CHECK(qgcm_open_one(ctx, 1, data, sizeof data, ip, 4) == -1);
+    for (int i = 0; i < 1350; ++i) CHECK(data[i] == 0);
+    CHECK(memcmp(data + 1350, tail, 28) == 0);
+    /* an unset key slot (a Mapping whose AES was never created) fails, untouched */
+    uint8_t z[64 + 28] = {0};
+    CHECK(qgcm_seal_one(ctx, 63, z, 64, ip, 4, NULL) == -1);
+    for (unsigned i = 0; i < sizeof z; ++i) CHECK(z[i] == 0);
+    printf("--- PASS: TestGPUAESEdges\n");
+}
+
+struct worker {
+    qgcm_coalescer *co;
+    const uint8_t *key;
+    int w, ok;
+};
+
+static void *coalesced_worker(void *p) {
+    struct worker *a = p;
+    uint8_t buf[1472], plain[1472];
+    const uint8_t ip[4] = {10, 99, 0, (uint8_t)a->w};
+    a->ok = 1;
+    for (int i = 0; i < 200 && a->ok; ++i) {
+        const long l = (a->w * 131 + i * 17) % 1433;
+        for (long j = 0; j < l; ++j) plain[j] = buf[4 + j] = (uint8_t)(a->w + i + j);
+        const long n = qgcm_coalescer_seal(a->co, 2, buf + 4, l, ip, 4);
+        if (n != l + 28 || !matches_oracle(a->key, plain, l, ip, 4, buf + 4)) a->ok = 0;
+        const long m = qgcm_coalescer_open(a->co, 2, buf + 4, n, ip, 4);
+        if (m != l || memcmp(buf + 4, plain, (size_t)l)) a->ok = 0;
+    }
+    return NULL;
+}
+
+static void TestGPUAESCoalesced(qgcm_ctx *ctx) {
+    uint8_t salt[32], key[32];
+    for (int i = 0; i < 32; ++i) salt[i] = (uint8_t)(255 - i);
+    CHECK(install_key(ctx, 2, salt, key) == QGCM_OK);
+    char err[QGCM_ERRLEN];
+    qgcm_coalescer *co = qgcm_coalescer_create(ctx, 256, 100, 1472, 4, err, sizeof err); /* EnableCoalescer */
+    CHECK(co != NULL);
+    pthread_t th[16];
+    struct worker a[16];
+    for (int w = 0; w < 16; ++w) {
+        a[w] = (struct worker){co, key, w, 0};
+        pthread_create(&th[w], NULL, coalesced_worker, &a[w]);
+    }
+    int ok = 1;
+    for (int w = 0; w < 16; ++w) {
+        pthread_join(th[w], NULL);
+        ok &= a[w].ok;
+    }
+    qgcm_coalescer_destroy(co);
+    CHECK(ok);
+    printf("--- PASS: TestGPUAESCoalesced\n");
+}
+
+static void TestGPUGroup(void) {
+    const int devs[2] = {0, 0}; /* a node's GPUs, stood in for by two contexts on device 0 */
+    char err[QGCM_ERRLEN];
+    qgcm_group *g = qgcm_group_create(devs, 2, 16, err, sizeof err);
+    CHECK(g != NULL);
+    CHECK(qgcm_group_size(g) == 2);
+    int ok = 1;
+    for (uint32_t idx = 0; idx < 6 && ok; ++idx) { /* GPUGroup.NewGPUAES */
+        const int owner = qgcm_group_shard(g, idx);
+        qgcm_ctx *c = qgcm_group_ctx(g, owner), *other = qgcm_group_ctx(g, 1 - owner);
+        uint8_t salt[32], key[32];
+        memset(salt, (int)idx, sizeof salt);
+        ok &= install_key(c, idx, salt, key) == QGCM_OK;
+        uint8_t data[100 + 28], plain[100];
+        for (int i = 0; i < 100; ++i) plain[i] = data[i] = (uint8_t)(i ^ idx);
+        ok &= qgcm_seal_one(c, idx, data, 100, NULL, 0, NULL) == 128 && matches_oracle(key, plain, 100, NULL, 0, data);
+        ok &= qgcm_open_one(other, idx, data, 128, NULL, 0) == -1; /* the key lives on its owner only */
+        ok &= memcmp(data, plain, 100) != 0;                         /* ... and was left untouched */
+        ok &= qgcm_open_one(c, idx, data, 128, NULL, 0) == 100 && !memcmp(data, plain, 100);
+    }
+    qgcm_group_destroy(g);
+    CHECK(ok);
+    printf("--- PASS: TestGPUGroup\n");
+}
+
+static void TestCreateError(void) {
+    char err[QGCM_ERRLEN] = {0};
+    CHECK(qgcm_create(4096, 16, err, sizeof err) == NULL);
+    CHECK(err[0] != 0);
+    printf("--- PASS: TestCreateError\n");
+}
+
+static int want(int argc, char **argv, const char *name) {
+    if (argc < 2) return 1;
+    for (int i = 1; i < argc; ++i)
+        if (!strcmp(argv[i], name)) return 1;
+    return 0;
+}
+
+int main(int argc, char **argv) {
+    char err[QGCM_ERRLEN];
+    qgcm_ctx *ctx = NULL;
+    if (want(argc, argv, "TestGPUAES") || want(argc, argv, "TestGPUAESEdges") ||
+        want(argc, argv, "TestGPUAESCoalesced")) {
+        ctx = qgcm_create(0, 64, err, sizeof err); /* NewGPUContext(0, 64) */
+        if (!ctx) {
+            fprintf(stderr, "qgcm_create: %s\n", err);
+            return 1;
+        }
+    }
+    if (want(argc, argv, "TestGPUAES")) TestGPUAES(ctx);
+    if (want(argc, argv, "TestGPUAESEdges")) TestGPUAESEdges(ctx);
+    if (want(argc, argv, "TestGPUAESCoalesced")) TestGPUAESCoalesced(ctx);
+    if (want(argc, argv, "TestGPUGroup")) TestGPUGroup();
+    if (want(argc, argv, "TestCreateError")) TestCreateError();
+    if (ctx) qgcm_destroy(ctx);
+    return failures ? 1 : 0;
+}

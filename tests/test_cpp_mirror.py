@@ -32,3 +32,26 @@ def test_cpp_mirror_cpu(name):
 @pytest.mark.gpu
 def test_cpp_mirror_gpu():
     run(GPU_TESTS)
+
+
+GO_BIN = os.path.join(ROOT, "tests", "cpp", "go_replay")
+
+
+def run_go(names, timeout=120):
+    """tests/cpp/go_replay.c: the C calls go/crypto/gpu_aes.go makes under go/crypto/gpu_aes_test.go."""
+    if not os.path.exists(GO_BIN):
+        pytest.fail(f"{GO_BIN} is missing: build it with __graft_entry__.build()")
+    r = subprocess.run([GO_BIN, *names], capture_output=True, text=True, timeout=timeout)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out
+    for n in names:
+        assert f"--- PASS: {n}" in out, out
+
+
+def test_go_shim_replay_cpu():
+    run_go(["TestCreateError"])
+
+
+@pytest.mark.gpu
+def test_go_shim_replay_gpu():
+    run_go(["TestGPUAES", "TestGPUAESEdges", "TestGPUAESCoalesced", "TestGPUGroup"])
