@@ -187,6 +187,119 @@ __device__ __forceinline__ void ctr_blocks(const Ctr &c, uint32_t lo, const Keys
     for (int j = 0; j < N; ++j) round_last(s[j][0], s[j][1], s[j][2], s[j][3], k, lb);
 }
 
+// ---------------------------------------------------------------------------------------------
+// AES-256 counter-block engines for the quad kernel.  Measured on gfx950 (tools/microbench/
+// valu_ops*.hip, bitop3_forms.hip): v_perm_b32, v_alignbit_b32, shifts and ANY VALU op with an SGPR
+// operand issue at ~4.5 cycles per wave-instruction per SIMD; v_bitop3_b32 / v_and / v_or / v_xor with
+// VGPR operands only at ~2.7.  With the T-table round at 16 lookups (32 LDS cycles per wave per CU),
+// the Tab2 round's 16 v_perm + 4 v_alignbit + 4 SGPR-keyed v_bitop3 (~120 SIMD-cycles = 30 CU-cycles
+// per wave-round) nearly saturate the VALU as well as the LDS.
+//  Tab2: Te0/Te1 in LDS (64 KiB), Te2/Te3 = rot16 folded into the column XOR, round keys in SGPRs.
+//  Tab4: all four tables in LDS (128 KiB: [0, 64K) rows of Te0|Te1, [64K, 128K) rows of Te2|Te3), no
+//        rotation; round keys as per-lane VGPR copies, so every column XOR is an all-VGPR v_bitop3; the
+//        byte-1 lookups build their address with one all-VGPR AND-OR ((s & 0xff00) | lane base).
+struct Tab2 {
+    Keys kk;
+    uint32_t lb;
+    __device__ __forceinline__ void setup(Ctr &c, uint32_t n0, uint32_t n1, uint32_t n2, uint32_t hi) const {
+        ctr_setup(c, n0, n1, n2, hi, kk, lb);
+    }
+    __device__ __forceinline__ void block(const Ctr &c, uint32_t lo, uint32_t &k0, uint32_t &k1, uint32_t &k2,
+                                          uint32_t &k3) const {
+        ctr_block(c, lo, kk, lb, k0, k1, k2, k3);
+    }
+};
+
+constexpr uint32_t kTe4Bytes = 131072;
+// v_bitop3 truth tables in the LOP3 convention: f(0xf0, 0xcc, 0xaa) for operands (a, b, c)
+constexpr uint32_t kOpXor3 = 0x96;                                // a ^ b ^ c
+constexpr uint32_t kOpAndOr = (0xf0 & 0xcc) | 0xaa;               // (a & b) | c
+constexpr uint32_t kOpSel = ((0xf0 & ~0xaa) | (0xcc & 0xaa)) & 0xff;  // c ? b : a, bitwise
+template <uint32_t kOp>
+__device__ __forceinline__ uint32_t bop3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, kOp);
+}
+// a VGPR the compiler cannot fold into a constant (an SGPR or literal operand costs half rate)
+__device__ __forceinline__ uint32_t vreg(uint32_t x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
+
+struct Tab4 {
+    uint32_t lb, lb2;                  // lane bases: Te0/Te1 rows (< 64K), Te2/Te3 rows (| 64K)
+    uint32_t m8, m24, m16;             // 0x0000ff00, 0xff000000, 0xffff0000 as VGPRs
+    uint32_t rk[60];                   // FIPS-197 round-key words (12-55 as per-lane VGPR copies)
+
+    // address of Te_t[byte k of s]
+    __device__ __forceinline__ uint32_t addr(uint32_t s, int k, int t) const {
+        const uint32_t base = t >= 2 ? lb2 : lb;
+        const uint32_t a = k == 1 ? bop3<kOpAndOr>(s, m8, base) : perm(s, base, 0x0c020400u + (k << 8));
+        return a + ((t & 1) ? 128u : 0u);
+    }
+    __device__ __forceinline__ uint32_t T(uint32_t s, int k, int t) const { return lds32(addr(s, k, t)); }
+
+    // column c = Te0[s_c.b0] ^ Te1[s_c+1.b1] ^ Te2[s_c+2.b2] ^ Te3[s_c+3.b3] ^ rk_c
+    __device__ __forceinline__ void round_full(uint32_t (&st)[4], int r) const {
+        uint32_t a[4][4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int t = 0; t < 4; ++t) a[c][t] = T(st[(c + t) & 3], t, t);
+        asm volatile("" ::: "memory");  // all 16 lookups in flight before the first combine
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+            st[c] = bop3<kOpXor3>(bop3<kOpXor3>(a[c][0], a[c][1], a[c][2]), a[c][3], rk[4 * r + c]);
+    }
+    // final round: output byte j of column c = S(s_c+j.bj), taken from the table holding S at byte j
+    // (Te2 byte 0, Te3 byte 1, Te0 byte 2, Te1 byte 3), merged by all-VGPR byte selects
+    __device__ __forceinline__ void round_last(uint32_t (&st)[4]) const {
+        uint32_t a[4][4];
+        constexpr int tab[4] = {2, 3, 0, 1};
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) a[c][j] = T(st[(c + j) & 3], j, tab[j]);
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const uint32_t x = bop3<kOpSel>(a[c][0], a[c][1], m8);   // byte 1 from Te3, the rest from Te2
+            const uint32_t y = bop3<kOpSel>(a[c][2], a[c][3], m24);  // byte 3 from Te1, the rest from Te0
+            st[c] = bop3<kOpSel>(x, y, m16) ^ rk[56 + c];             // bytes 0-1 of x, 2-3 of y
+        }
+    }
+    // rounds 1-2 of the counter blocks nonce || (hi << 8 | lo), lo varying (as ctr_setup)
+    __device__ __forceinline__ void setup(Ctr &c, uint32_t n0, uint32_t n1, uint32_t n2, uint32_t hi) const {
+        const uint32_t s0 = n0 ^ rk[0], s1 = n1 ^ rk[1], s2 = n2 ^ rk[2];
+        const uint32_t s3 = bswap(hi << 8) ^ rk[3];  // byte 3 varies per block; unused below
+        c.x3 = rk[3] >> 24;
+        c.K0 = bop3<kOpXor3>(T(s0, 0, 0), T(s1, 1, 1), T(s2, 2, 2)) ^ rk[4];
+        const uint32_t t1 = bop3<kOpXor3>(bop3<kOpXor3>(T(s1, 0, 0), T(s2, 1, 1), T(s3, 2, 2)), T(s0, 3, 3), rk[5]);
+        const uint32_t t2 = bop3<kOpXor3>(bop3<kOpXor3>(T(s2, 0, 0), T(s3, 1, 1), T(s0, 2, 2)), T(s1, 3, 3), rk[6]);
+        const uint32_t t3 = bop3<kOpXor3>(bop3<kOpXor3>(T(s3, 0, 0), T(s0, 1, 1), T(s1, 2, 2)), T(s2, 3, 3), rk[7]);
+        c.U0 = bop3<kOpXor3>(T(t1, 1, 1), T(t2, 2, 2), T(t3, 3, 3)) ^ rk[8];
+        c.U1 = bop3<kOpXor3>(T(t1, 0, 0), T(t2, 1, 1), T(t3, 2, 2)) ^ rk[9];
+        c.U2 = bop3<kOpXor3>(T(t2, 0, 0), T(t3, 1, 1), T(t1, 3, 3)) ^ rk[10];
+        c.U3 = bop3<kOpXor3>(T(t3, 0, 0), T(t1, 2, 2), T(t2, 3, 3)) ^ rk[11];
+    }
+    __device__ __forceinline__ void block(const Ctr &c, uint32_t lo, uint32_t &k0, uint32_t &k1, uint32_t &k2,
+                                          uint32_t &k3) const {
+        const uint32_t x = lo ^ c.x3;
+        const uint32_t t0 = c.K0 ^ lds32(((x << 8) | lb2) + 128u);  // Te3[x]
+        uint32_t st[4];
+        st[0] = c.U0 ^ T(t0, 0, 0);
+        st[1] = c.U1 ^ T(t0, 3, 3);
+        st[2] = c.U2 ^ T(t0, 2, 2);
+        st[3] = c.U3 ^ T(t0, 1, 1);
+#pragma unroll
+        for (int r = 3; r < 14; ++r) round_full(st, r);
+        round_last(st);
+        k0 = st[0];
+        k1 = st[1];
+        k2 = st[2];
+        k3 = st[3];
+    }
+};
+
 // Y <- Y * H in GF(2^128) via the 4-bit comb in this wave's LDS table at gb (byte1/2 of gb hold
 // its base; byte0 is 0).  Entry (p, v) at gb + p*256 + v*16, p = nibble position (2*byte for the
 // high nibble, 2*byte+1 for the low one), v = nibble value.
@@ -609,11 +722,9 @@ __device__ __forceinline__ uint32_t quad_xor(uint32_t v) {
 }
 
 // One packet of a quad tile (4 lanes, lane m owns blocks b = m mod 4): CTR + GHASH + tag, in place.
-template <bool kSeal, bool kFold, bool kDesc, bool kGFin>
-__device__ __forceinline__ void quad_packet(const Batch &b, const uint32_t *__restrict__ rk_table, uint32_t pkt,
-                                            uint64_t off, uint32_t L, uint32_t wkey, uint32_t m, uint32_t lb,
-                                            uint32_t gH4, uint32_t gH) {
-    const Keys kk = {rk_table + (size_t)wkey * kRkWords, rk_table + (size_t)wkey * kRkWords + 64};
+template <bool kSeal, bool kFold, bool kDesc, bool kGFin, class Eng>
+__device__ __forceinline__ void quad_packet(const Batch &b, const Eng &eng, uint32_t pkt, uint64_t off, uint32_t L,
+                                            uint32_t wkey, uint32_t m, uint32_t gH4, uint32_t gH) {
     const uint4 *Hg = b.gh_table + (size_t)wkey * kGhEntries;  // comb tables of H^k (global)
     uint8_t *raw = b.arena + off;
     uint8_t *data = raw + 4;  // common.PacketStart
@@ -641,7 +752,7 @@ __device__ __forceinline__ void quad_packet(const Batch &b, const uint32_t *__re
     if constexpr (kFold) {
     Ctr cc;
     uint32_t hi = 0;
-    ctr_setup(cc, n0, n1, n2, 0, kk, lb);
+    eng.setup(cc, n0, n1, n2, 0);
     // Lane m walks blocks m, m+4, ... < d, then (lane d % 4 only) the virtual block d = E_K(J0):
     // one AES instance per step, and J0 fills the slot of the lane with the fewest data blocks.
     for (uint32_t bi = m; bi <= d; bi += 4) {
@@ -649,10 +760,10 @@ __device__ __forceinline__ void quad_packet(const Batch &b, const uint32_t *__re
         const uint32_t ctr = j0 ? 1u : bi + 2;  // J0, or inc32(J0) + bi
         if ((ctr >> 8) != hi) {
             hi = ctr >> 8;
-            ctr_setup(cc, n0, n1, n2, hi, kk, lb);
+            eng.setup(cc, n0, n1, n2, hi);
         }
         uint32_t k0, k1, k2, k3;
-        ctr_block(cc, ctr & 0xffu, kk, lb, k0, k1, k2, k3);
+        eng.block(cc, ctr & 0xffu, k0, k1, k2, k3);
         if (j0) {
             e0 = k0;
             e1 = k1;
@@ -692,18 +803,18 @@ __device__ __forceinline__ void quad_packet(const Batch &b, const uint32_t *__re
     } else {
     Ctr cc;
     uint32_t hi = 0;
-    ctr_setup(cc, n0, n1, n2, 0, kk, lb);
+    eng.setup(cc, n0, n1, n2, 0);
     for (uint32_t bi = m; bi < nfull; bi += 4) {
         const uint32_t ctr = bi + 2;  // inc32(J0) + bi
         if ((ctr >> 8) != hi) {
             hi = ctr >> 8;
-            ctr_setup(cc, n0, n1, n2, hi, kk, lb);
+            eng.setup(cc, n0, n1, n2, hi);
         }
         // the data load is issued before the AES rounds so its latency hides behind them
         W4 *p = reinterpret_cast<W4 *>(data + 16u * bi);
         const W4 in = load_block(p);
         uint32_t k0, k1, k2, k3;
-        ctr_block(cc, ctr & 0xffu, kk, lb, k0, k1, k2, k3);
+        eng.block(cc, ctr & 0xffu, k0, k1, k2, k3);
         const W4 out = {in.x ^ k0, in.y ^ k1, in.z ^ k2, in.w ^ k3};
         *p = out;
         const W4 &c = kSeal ? out : in;
@@ -721,10 +832,10 @@ __device__ __forceinline__ void quad_packet(const Batch &b, const uint32_t *__re
         const uint32_t ctr = part ? nfull + 2 : 1u;  // inc32(J0) + nfull, or J0
         if ((ctr >> 8) != hi) {
             hi = ctr >> 8;
-            ctr_setup(cc, n0, n1, n2, hi, kk, lb);
+            eng.setup(cc, n0, n1, n2, hi);
         }
         uint32_t k0, k1, k2, k3;
-        ctr_block(cc, ctr & 0xffu, kk, lb, k0, k1, k2, k3);
+        eng.block(cc, ctr & 0xffu, k0, k1, k2, k3);
         if (part) {
             uint8_t *blk = data + 16u * nfull;
             const W4 in = *reinterpret_cast<const W4 *>(blk);  // reads into tag area: inside the slot
@@ -820,35 +931,54 @@ __device__ __forceinline__ void quad_packet(const Batch &b, const uint32_t *__re
 // kGFin: the once-per-packet recombination multiplies by H^2..H^5 come from the global key table
 // (one multiply per lane); otherwise by repeated multiplies by H (comb table of H in LDS for single
 // key batches, global for descriptor batches).
-template <bool kSeal, int kW, bool kFold, int kWpe = kW / 4, bool kDesc = false, bool kGFin = true>
+// kTab: the AES engine (Tab2: 64 KiB of T-tables; Tab4: 128 KiB, single-key batches only).
+template <bool kSeal, int kW, bool kFold, int kWpe = kW / 4, bool kDesc = false, bool kGFin = true, int kTab = 2>
 __global__ void __launch_bounds__(kW * 64) __attribute__((amdgpu_waves_per_eu(kWpe, kWpe)))
 gcm_quad_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
+    static_assert(kTab == 2 || (kTab == 4 && !kDesc), "four-table engine: single-key batches");
     constexpr uint32_t kT = kW * 64;
+    constexpr uint32_t kTe = kTab == 4 ? kTe4Bytes : kTeBytes;  // LDS bytes of T-tables (comb tables after)
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = threadIdx.x >> 6;
     const uint32_t m = lane & 3u;          // block residue owned by this lane
     const uint32_t qd = lane >> 2;         // packet slot within the wave tile (16 per wave)
 
+    // dword i of each 64 KiB half: row x = i/64, slot i%64 (< 32: Te0 / Te2, else Te1 / Te3)
     for (uint32_t i = threadIdx.x; i < kTeBytes / 4; i += kT) {
         const uint32_t x = i >> 6, slot = i & 63u;
-        lds_st32(4 * i, b.te[(slot >> 5) * 256u + x]);
+        const uint32_t v = b.te[(slot >> 5) * 256u + x];
+        lds_st32(4 * i, v);
+        if constexpr (kTab == 4) lds_st32(kTeBytes + 4 * i, rot16(v));
     }
     if constexpr (!kDesc) {
         const uint4 *src = b.gh_table + (size_t)b.uniform_key * kGhEntries + kGhH4;
-        for (uint32_t e = threadIdx.x; e < 512u; e += kT) lds_st_comb<!kDesc>(kTeBytes, e, src[e]);
+        for (uint32_t e = threadIdx.x; e < 512u; e += kT) lds_st_comb<!kDesc>(kTe, e, src[e]);
         if constexpr (!kGFin) {
             const uint4 *srcH = b.gh_table + (size_t)b.uniform_key * kGhEntries + kGhH;
-            for (uint32_t e = threadIdx.x; e < 512u; e += kT) lds_st_comb<!kDesc>(kTeBytes + kGhBytes, e, srcH[e]);
+            for (uint32_t e = threadIdx.x; e < 512u; e += kT) lds_st_comb<!kDesc>(kTe + kGhBytes, e, srcH[e]);
         }
     }
     __syncthreads();
 
     const uint32_t lb = (lane & 31u) << 2;
+    Tab4 e4;
+    if constexpr (kTab == 4) {  // the single key's round keys as VGPR copies, masks and lane bases as VGPRs
+        const uint32_t *kp = rk_table + (size_t)b.uniform_key * kRkWords;
+        // rounds 3-13 (words 12-55) as VGPRs; the rarely used words of the counter setup and the final
+        // round stay SGPRs (128 VGPRs per lane at 16 waves/CU)
+#pragma unroll
+        for (int i = 0; i < 60; ++i) e4.rk[i] = i >= 12 && i < 56 ? vreg(kp[i]) : kp[i];
+        e4.lb = vreg(lb);
+        e4.lb2 = vreg(lb | kTeBytes);
+        e4.m8 = vreg(0x0000ff00u);
+        e4.m24 = vreg(0xff000000u);
+        e4.m16 = vreg(0xffff0000u);
+    }
     // single key: the H^4 table shared by the workgroup; descriptors: one H^4 table per wave
     // (reloaded when the wave's key changes).  The once-per-packet multiplies by H^2..H^5 read the
     // L2-resident key table from global memory, off the LDS pipe that bounds the kernel.
-    const uint32_t gH4 = kDesc ? kTeBytes + wave * kGhBytes : kTeBytes;
-    const uint32_t gH = kTeBytes + kGhBytes;  // comb table of H in LDS (single key, !kGFin)
+    const uint32_t gH4 = kDesc ? kTe + wave * kGhBytes : kTe;
+    const uint32_t gH = kTe + kGhBytes;  // comb table of H in LDS (single key, !kGFin)
     uint32_t cur_key = kDesc ? 0xffffffffu : b.uniform_key;
     const uint32_t ntiles = kDesc ? (b.n_items >> 4) : ((b.n + 15) >> 4);
 
@@ -914,7 +1044,12 @@ gcm_quad_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
                 continue;  // the whole quad leaves together
             }
         }
-        quad_packet<kSeal, kFold, kDesc, kGFin>(b, rk_table, pkt, off, L, wkey, m, lb, gH4, gH);
+        if constexpr (kTab == 4) {
+            quad_packet<kSeal, kFold, kDesc, kGFin>(b, e4, pkt, off, L, wkey, m, gH4, gH);
+        } else {
+            const Tab2 e2 = {{rk_table + (size_t)wkey * kRkWords, rk_table + (size_t)wkey * kRkWords + 64}, lb};
+            quad_packet<kSeal, kFold, kDesc, kGFin>(b, e2, pkt, off, L, wkey, m, gH4, gH);
+        }
     }
 }
 
@@ -1237,6 +1372,14 @@ Variant make_variant() {
                    lds_bytes<kW, kShared>(), false, 1, false};
 }
 
+// the four-table engine: 128 KiB of T-tables + the H^4 comb = one 16-wave workgroup per CU
+template <int kW>
+Variant make_quad4() {
+    return Variant{reinterpret_cast<const void *>(&gcm_quad_kernel<true, kW, false, kW / 4, false, true, 4>),
+                   reinterpret_cast<const void *>(&gcm_quad_kernel<false, kW, false, kW / 4, false, true, 4>), kW,
+                   kTe4Bytes + kGhBytes, true, 1, false};
+}
+
 template <int kW, bool kFold, int kWpe = kW / 4, bool kGFin = true>
 Variant make_quad() {
     return Variant{reinterpret_cast<const void *>(&gcm_quad_kernel<true, kW, kFold, kWpe, false, kGFin>),
@@ -1266,6 +1409,7 @@ hipError_t init_kernels() {
     g_variants[8] = make_quad_desc<8, 2>();        // descriptors: quad, 8 waves/CU
     g_variants[9] = make_quad<16, false, 8, false>();   // as 5, recombination by repeated H (LDS)
     g_variants[10] = make_quad_desc<12, 3, false>();    // as 7, recombination by repeated H (global)
+    g_variants[11] = make_quad4<16>();                  // quad, four T-tables (128 KiB), 16 waves/CU
     for (const Variant &v : g_variants) {
         for (const void *k : {v.seal, v.open}) {
             hipFuncAttributes a;

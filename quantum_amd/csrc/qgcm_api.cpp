@@ -70,7 +70,11 @@ struct qgcm_ctx {
         size_t cap = 0;
     };
     static constexpr int kOneSlots = 8;
+    // pool slots stay small (the latency kernel's LDS staging limit): payloads up to ~32 KiB, which
+    // covers every packet quantum sends (MTU 1433, jumbo 9000); larger calls share one big slot
+    static constexpr size_t kOneSlotCap = kOneCap + 4096;
     OneSlot one[kOneSlots];
+    OneSlot big;  // calls whose staging exceeds kOneSlotCap (released after the call past 64 MiB)
     std::atomic<uint32_t> one_rr{0};
 
     // host-batch pipeline (qgcm_seal_host / qgcm_open_host), guarded by io_mu
@@ -323,12 +327,25 @@ int run_descs_locked(qgcm_ctx *ctx, bool seal, const qgcm_desc *descs, uint32_t 
     return hip_fail(launch_packets(seal, v, b, grid_for(ctx, b.n_items, v), s));
 }
 
+// Per-packet streams are created at the highest priority the device offers, so a per-packet call
+// does not queue behind a long batch kernel on the (few, GPU_MAX_HW_QUEUES) hardware queues.
+hipError_t create_one_stream(hipStream_t *s) {
+    int lo = 0, hi = 0;
+    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) hi = 0;
+    return hipStreamCreateWithPriority(s, hipStreamNonBlocking, hi);
+}
+
 // Takes a free per-packet staging slot (the first one whose lock is free, starting round-robin; all
 // busy: waits on one) and makes its pinned buffer hold `bytes` (the kernel works on it in place,
-// zero-copy).  Returns nullptr on allocation failure.
+// zero-copy).  Pool slots are capped at kOneSlotCap bytes, so they never grow on the hot path past
+// the first call; larger payloads go through the one big slot.  Returns nullptr on allocation failure.
 qgcm_ctx::OneSlot *acquire_one(qgcm_ctx *ctx, size_t bytes, std::unique_lock<std::mutex> &lk) {
     const uint32_t start = ctx->one_rr.fetch_add(1, std::memory_order_relaxed);
     qgcm_ctx::OneSlot *sl = nullptr;
+    if (bytes > qgcm_ctx::kOneSlotCap) {
+        sl = &ctx->big;
+        lk = std::unique_lock<std::mutex>(sl->mu);
+    }
     for (int i = 0; i < qgcm_ctx::kOneSlots && !sl; ++i) {
         qgcm_ctx::OneSlot &c = ctx->one[(start + i) % qgcm_ctx::kOneSlots];
         std::unique_lock<std::mutex> l(c.mu, std::try_to_lock);
@@ -341,13 +358,14 @@ qgcm_ctx::OneSlot *acquire_one(qgcm_ctx *ctx, size_t bytes, std::unique_lock<std
         sl = &ctx->one[start % qgcm_ctx::kOneSlots];
         lk = std::unique_lock<std::mutex>(sl->mu);
     }
-    if (!sl->stream && hipStreamCreateWithFlags(&sl->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (!sl->stream && create_one_stream(&sl->stream) != hipSuccess) {
         sl->stream = nullptr;
         return nullptr;
     }
     if (bytes > sl->cap) {
-        size_t want = 4096;
-        while (want < bytes) want <<= 1;
+        size_t want = sl == &ctx->big ? bytes : qgcm_ctx::kOneSlotCap;
+        if (sl != &ctx->big)
+            while (want < bytes) want <<= 1;
         if (sl->h) hipHostFree(sl->h);
         sl->h = nullptr;
         sl->cap = 0;
@@ -355,6 +373,14 @@ qgcm_ctx::OneSlot *acquire_one(qgcm_ctx *ctx, size_t bytes, std::unique_lock<std
         sl->cap = want;
     }
     return sl;
+}
+
+// The big slot keeps up to 64 MiB pinned between calls; beyond that it is released after the call.
+void release_big(qgcm_ctx *ctx, qgcm_ctx::OneSlot *sl) {
+    if (sl != &ctx->big || sl->cap <= (64u << 20)) return;
+    hipHostFree(sl->h);
+    sl->h = nullptr;
+    sl->cap = 0;
 }
 
 }  // namespace
@@ -471,10 +497,12 @@ void qgcm_destroy(qgcm_ctx *ctx) {
     hipFree(ctx->d_cursors);
     hipFree(ctx->d_worklist);
     hipFree(ctx->d_qws);
-    for (auto &sl : ctx->one) {
+    auto free_slot = [](qgcm_ctx::OneSlot &sl) {
         if (sl.h) hipHostFree(sl.h);
         if (sl.stream) hipStreamDestroy(sl.stream);
-    }
+    };
+    for (auto &sl : ctx->one) free_slot(sl);
+    free_slot(ctx->big);
     hipFree(ctx->d_ring);
     hipFree(ctx->d_side);
     if (ctx->h_stat) hipHostFree(ctx->h_stat);
@@ -572,6 +600,7 @@ long qgcm_seal_one(qgcm_ctx *ctx, uint32_t key_idx, uint8_t *data, long length, 
     if (run_one(ctx, true, h, stride, (uint32_t)length, key_idx, aad_len, h + stride, s) != QGCM_OK) return -1;
     if (h[stride] != 1) return -1;
     memcpy(data, h + 4, (size_t)length + QGCM_OVERHEAD);
+    release_big(ctx, sl);
     return length + QGCM_OVERHEAD;
 }
 
@@ -592,7 +621,9 @@ long qgcm_open_one(qgcm_ctx *ctx, uint32_t key_idx, uint8_t *data, long len, con
     h[stride] = 0;
     if (run_one(ctx, false, h, stride, (uint32_t)len, key_idx, aad_len, h + stride, s) != QGCM_OK) return -1;
     memcpy(data, h + 4, (size_t)len - QGCM_OVERHEAD);  // plaintext, or zeros on auth failure
-    return h[stride] == 1 ? len - QGCM_OVERHEAD : -1;
+    const bool ok = h[stride] == 1;
+    release_big(ctx, sl);
+    return ok ? len - QGCM_OVERHEAD : -1;
 }
 
 // Host batches, pipelined: the batch is cut into ~64 MiB chunks, each with its own device slot while
