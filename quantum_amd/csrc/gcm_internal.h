@@ -45,10 +45,10 @@ struct Batch {
                                 // back and made system-visible (the host polls it instead of the stream)
 };
 
-constexpr int kNumVariants = 12;
+constexpr int kNumVariants = 14;
 constexpr int kVariantGeneral = 0;   // lane per packet, per-wave GHASH tables, any key mix
 constexpr int kVariantDescQuad = 7;  // default for descriptor batches: sorted quad tiles
-constexpr int kVariantUniform = 5;   // default for single-key (uniform) batches: quad kernel, 32 waves/CU
+constexpr int kVariantUniform = 12;  // default for single-key (uniform) batches: quad kernel (Tab2F), 32 waves/CU
 hipError_t init_kernels();
 int variant_waves(int variant);
 bool variant_quad(int variant);

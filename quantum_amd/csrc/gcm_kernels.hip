@@ -86,6 +86,22 @@ __device__ __forceinline__ void lds_st_comb(uint32_t base, uint32_t e, uint4 v) 
 #define TE0(s, k) lds32(TA(s, k))
 #define TE1(s, k) lds32(TA(s, k) + 128u)
 
+// T-table addressing, parameterised for the quad kernel's engines: kB = LDS byte address of the
+// tables (an immediate ds offset, so free), kAO = byte-1 lookups address by one all-VGPR AND-OR
+// ((s & 0xff00) | lane base, m8 = 0xff00 held in a VGPR: ~2.7 cycles per wave64 instruction) instead
+// of v_perm with an SGPR selector (~4.5 cycles; tools/microbench/valu_ops*.hip).
+template <uint32_t kB, bool kAO>
+struct TT {
+    uint32_t lb, m8;
+    __device__ __forceinline__ uint32_t a(uint32_t s, int k) const {
+        if (kAO && k == 1) return __builtin_amdgcn_bitop3_b32(s, m8, lb, (0xf0 & 0xcc) | 0xaa);
+        return perm(s, lb, 0x0c0c0400u + (k << 8));
+    }
+    __device__ __forceinline__ uint32_t t0(uint32_t s, int k) const { return lds32(a(s, k) + kB); }
+    __device__ __forceinline__ uint32_t t1(uint32_t s, int k) const { return lds32(a(s, k) + kB + 128u); }
+};
+typedef TT<0, false> TT0;
+
 struct Ctr {
     uint32_t K0, x3;          // round-1 column 0 without the varying term; rk0 word3 byte3
     uint32_t U0, U1, U2, U3;  // round-2 columns without the term that depends on column 0
@@ -100,69 +116,89 @@ struct Keys {
 
 // One full AES round (SubBytes, ShiftRows, MixColumns, AddRoundKey) on LE column words:
 // column c = Te0[s_c.b0] ^ Te1[s_c+1.b1] ^ rot16(Te0[s_c+2.b2] ^ Te1[s_c+3.b3]) ^ rk_c.
+template <class A>
 __device__ __forceinline__ void round_full(uint32_t &s0, uint32_t &s1, uint32_t &s2, uint32_t &s3, const Keys &k,
-                                           int r, uint32_t lb) {
+                                           int r, const A &t) {
     // All 16 lookups of the round are issued before the first combine (the asm is a scheduling
     // fence): up to 16 LDS reads in flight per wave instead of 1-2 under the 64-VGPR budget.
     // +2.9% on config 2 in an in-process A/B.
-    const uint32_t a0 = TE0(s2, 2), a1 = TE1(s3, 3), a2 = TE0(s3, 2), a3 = TE1(s0, 3);
-    const uint32_t a4 = TE0(s0, 2), a5 = TE1(s1, 3), a6 = TE0(s1, 2), a7 = TE1(s2, 3);
-    const uint32_t c0 = TE0(s0, 0), c1 = TE1(s1, 1), c2 = TE0(s1, 0), c3 = TE1(s2, 1);
-    const uint32_t c4 = TE0(s2, 0), c5 = TE1(s3, 1), c6 = TE0(s3, 0), c7 = TE1(s0, 1);
+    const uint32_t a0 = t.t0(s2, 2), a1 = t.t1(s3, 3), a2 = t.t0(s3, 2), a3 = t.t1(s0, 3);
+    const uint32_t a4 = t.t0(s0, 2), a5 = t.t1(s1, 3), a6 = t.t0(s1, 2), a7 = t.t1(s2, 3);
+    const uint32_t c0 = t.t0(s0, 0), c1 = t.t1(s1, 1), c2 = t.t0(s1, 0), c3 = t.t1(s2, 1);
+    const uint32_t c4 = t.t0(s2, 0), c5 = t.t1(s3, 1), c6 = t.t0(s3, 0), c7 = t.t1(s0, 1);
     asm volatile("" ::: "memory");
     s0 = xor3(c0, c1, rot16(xor3(a0, a1, k.rr[4 * r + 0])));
     s1 = xor3(c2, c3, rot16(xor3(a2, a3, k.rr[4 * r + 1])));
     s2 = xor3(c4, c5, rot16(xor3(a4, a5, k.rr[4 * r + 2])));
     s3 = xor3(c6, c7, rot16(xor3(a6, a7, k.rr[4 * r + 3])));
 }
+__device__ __forceinline__ void round_full(uint32_t &s0, uint32_t &s1, uint32_t &s2, uint32_t &s3, const Keys &k,
+                                           int r, uint32_t lb) {
+    round_full(s0, s1, s2, s3, k, r, TT0{lb, 0});
+}
 
 // Final round (no MixColumns): S-box bytes are byte1/byte2 of Te0 and byte3 of Te1.
+template <class A>
 __device__ __forceinline__ void round_last(uint32_t &s0, uint32_t &s1, uint32_t &s2, uint32_t &s3, const Keys &k,
-                                           uint32_t lb) {
+                                           const A &t) {
     const uint32_t *rk = k.rk + 56;
     // 16 lookups in flight, then combine (as round_full; +1.1% in an in-process A/B)
-    const uint32_t a0 = TE0(s1, 1), a1 = TE0(s0, 0), a2 = TE1(s3, 3), a3 = TE0(s2, 2);
-    const uint32_t b0 = TE0(s2, 1), b1 = TE0(s1, 0), b2 = TE1(s0, 3), b3 = TE0(s3, 2);
-    const uint32_t c0 = TE0(s3, 1), c1 = TE0(s2, 0), c2 = TE1(s1, 3), c3 = TE0(s0, 2);
-    const uint32_t d0 = TE0(s0, 1), d1 = TE0(s3, 0), d2 = TE1(s2, 3), d3 = TE0(s1, 2);
+    const uint32_t a0 = t.t0(s1, 1), a1 = t.t0(s0, 0), a2 = t.t1(s3, 3), a3 = t.t0(s2, 2);
+    const uint32_t b0 = t.t0(s2, 1), b1 = t.t0(s1, 0), b2 = t.t1(s0, 3), b3 = t.t0(s3, 2);
+    const uint32_t c0 = t.t0(s3, 1), c1 = t.t0(s2, 0), c2 = t.t1(s1, 3), c3 = t.t0(s0, 2);
+    const uint32_t d0 = t.t0(s0, 1), d1 = t.t0(s3, 0), d2 = t.t1(s2, 3), d3 = t.t0(s1, 2);
     asm volatile("" ::: "memory");
     s0 = xor3(perm(a0, a1, 0x0c0c0501u), perm(a2, a3, 0x07020c0cu), rk[0]);
     s1 = xor3(perm(b0, b1, 0x0c0c0501u), perm(b2, b3, 0x07020c0cu), rk[1]);
     s2 = xor3(perm(c0, c1, 0x0c0c0501u), perm(c2, c3, 0x07020c0cu), rk[2]);
     s3 = xor3(perm(d0, d1, 0x0c0c0501u), perm(d2, d3, 0x07020c0cu), rk[3]);
 }
+__device__ __forceinline__ void round_last(uint32_t &s0, uint32_t &s1, uint32_t &s2, uint32_t &s3, const Keys &k,
+                                           uint32_t lb) {
+    round_last(s0, s1, s2, s3, k, TT0{lb, 0});
+}
 
 // Precompute rounds 1-2 for counter blocks nonce || (ctr_hi << 8 | low byte).  Round 1: only
 // column 0 sees the varying byte (s3.b3, via Te3); round 2: each column sees exactly one byte
 // of that column 0.
+template <class A>
 __device__ __forceinline__ void ctr_setup(Ctr &c, uint32_t n0, uint32_t n1, uint32_t n2, uint32_t ctr_hi,
-                                          const Keys &k, uint32_t lb) {
+                                          const Keys &k, const A &t) {
     const uint32_t *rk = k.rk;
     const uint32_t s0 = n0 ^ rk[0], s1 = n1 ^ rk[1], s2 = n2 ^ rk[2];
     const uint32_t s3 = bswap(ctr_hi << 8) ^ rk[3];  // byte3 varies per block; unused below
     c.x3 = rk[3] >> 24;
-    c.K0 = xor3(TE0(s0, 0), TE1(s1, 1), rot16(TE0(s2, 2))) ^ rk[4];
-    const uint32_t t1 = xor3(TE0(s1, 0), TE1(s2, 1), rot16(xor3(TE0(s3, 2), TE1(s0, 3), k.rr[5])));
-    const uint32_t t2 = xor3(TE0(s2, 0), TE1(s3, 1), rot16(xor3(TE0(s0, 2), TE1(s1, 3), k.rr[6])));
-    const uint32_t t3 = xor3(TE0(s3, 0), TE1(s0, 1), rot16(xor3(TE0(s1, 2), TE1(s2, 3), k.rr[7])));
-    c.U0 = TE1(t1, 1) ^ rot16(xor3(TE0(t2, 2), TE1(t3, 3), k.rr[8]));
-    c.U1 = xor3(TE0(t1, 0), TE1(t2, 1), rot16(TE0(t3, 2))) ^ rk[9];
-    c.U2 = xor3(TE0(t2, 0), TE1(t3, 1), rot16(TE1(t1, 3))) ^ rk[10];
-    c.U3 = TE0(t3, 0) ^ rot16(xor3(TE0(t1, 2), TE1(t2, 3), k.rr[11]));
+    c.K0 = xor3(t.t0(s0, 0), t.t1(s1, 1), rot16(t.t0(s2, 2))) ^ rk[4];
+    const uint32_t t1 = xor3(t.t0(s1, 0), t.t1(s2, 1), rot16(xor3(t.t0(s3, 2), t.t1(s0, 3), k.rr[5])));
+    const uint32_t t2 = xor3(t.t0(s2, 0), t.t1(s3, 1), rot16(xor3(t.t0(s0, 2), t.t1(s1, 3), k.rr[6])));
+    const uint32_t t3 = xor3(t.t0(s3, 0), t.t1(s0, 1), rot16(xor3(t.t0(s1, 2), t.t1(s2, 3), k.rr[7])));
+    c.U0 = t.t1(t1, 1) ^ rot16(xor3(t.t0(t2, 2), t.t1(t3, 3), k.rr[8]));
+    c.U1 = xor3(t.t0(t1, 0), t.t1(t2, 1), rot16(t.t0(t3, 2))) ^ rk[9];
+    c.U2 = xor3(t.t0(t2, 0), t.t1(t3, 1), rot16(t.t1(t1, 3))) ^ rk[10];
+    c.U3 = t.t0(t3, 0) ^ rot16(xor3(t.t0(t1, 2), t.t1(t2, 3), k.rr[11]));
+}
+__device__ __forceinline__ void ctr_setup(Ctr &c, uint32_t n0, uint32_t n1, uint32_t n2, uint32_t ctr_hi,
+                                          const Keys &k, uint32_t lb) {
+    ctr_setup(c, n0, n1, n2, ctr_hi, k, TT0{lb, 0});
 }
 
 // E_K(nonce || ctr) for a counter whose high 24 bits match the cache; lo = ctr & 0xff.
+template <class A, uint32_t kB>
+__device__ __forceinline__ void ctr_block_t(const Ctr &c, uint32_t lo, const Keys &k, const A &t, uint32_t &s0,
+                                            uint32_t &s1, uint32_t &s2, uint32_t &s3) {
+    const uint32_t x = lo ^ c.x3;
+    const uint32_t t0 = c.K0 ^ rot16(lds32(((x << 8) | t.lb) + kB + 128u));  // Te3[x]
+    s0 = c.U0 ^ t.t0(t0, 0);
+    s1 = c.U1 ^ rot16(t.t1(t0, 3));  // Te3[t0.b3]
+    s2 = c.U2 ^ rot16(t.t0(t0, 2));  // Te2[t0.b2]
+    s3 = c.U3 ^ t.t1(t0, 1);
+#pragma unroll
+    for (int r = 3; r < 14; ++r) round_full(s0, s1, s2, s3, k, r, t);
+    round_last(s0, s1, s2, s3, k, t);
+}
 __device__ __forceinline__ void ctr_block(const Ctr &c, uint32_t lo, const Keys &k, uint32_t lb, uint32_t &s0,
                                           uint32_t &s1, uint32_t &s2, uint32_t &s3) {
-    const uint32_t x = lo ^ c.x3;
-    const uint32_t t0 = c.K0 ^ rot16(lds32(((x << 8) | lb) + 128u));  // Te3[x]
-    s0 = c.U0 ^ TE0(t0, 0);
-    s1 = c.U1 ^ rot16(TE1(t0, 3));  // Te3[t0.b3]
-    s2 = c.U2 ^ rot16(TE0(t0, 2));  // Te2[t0.b2]
-    s3 = c.U3 ^ TE1(t0, 1);
-#pragma unroll
-    for (int r = 3; r < 14; ++r) round_full(s0, s1, s2, s3, k, r, lb);
-    round_last(s0, s1, s2, s3, k, lb);
+    ctr_block_t<TT0, 0>(c, lo, k, TT0{lb, 0}, s0, s1, s2, s3);
 }
 
 // N consecutive counter blocks lo, lo+1, ... (same 256-block segment) in lockstep: N independent
@@ -198,15 +234,135 @@ __device__ __forceinline__ void ctr_blocks(const Ctr &c, uint32_t lo, const Keys
 //  Tab4: all four tables in LDS (128 KiB: [0, 64K) rows of Te0|Te1, [64K, 128K) rows of Te2|Te3), no
 //        rotation; round keys as per-lane VGPR copies, so every column XOR is an all-VGPR v_bitop3; the
 //        byte-1 lookups build their address with one all-VGPR AND-OR ((s & 0xff00) | lane base).
-struct Tab2 {
+template <bool kB64, bool kFence>
+__device__ __forceinline__ void ghash_mul(uint32_t &y0, uint32_t &y1, uint32_t &y2, uint32_t &y3, uint32_t gb);
+
+// kAO: byte-1 addresses by the all-VGPR AND-OR (TT); Tab2 = Tab2T<false>
+template <bool kAO>
+struct Tab2T {
     Keys kk;
-    uint32_t lb;
+    TT<0, kAO> t;
     __device__ __forceinline__ void setup(Ctr &c, uint32_t n0, uint32_t n1, uint32_t n2, uint32_t hi) const {
-        ctr_setup(c, n0, n1, n2, hi, kk, lb);
+        ctr_setup(c, n0, n1, n2, hi, kk, t);
     }
     __device__ __forceinline__ void block(const Ctr &c, uint32_t lo, uint32_t &k0, uint32_t &k1, uint32_t &k2,
                                           uint32_t &k3) const {
-        ctr_block(c, lo, kk, lb, k0, k1, k2, k3);
+        ctr_block_t<TT<0, kAO>, 0>(c, lo, kk, t, k0, k1, k2, k3);
+    }
+    template <bool kB64>
+    __device__ __forceinline__ void ghash(uint32_t &y0, uint32_t &y1, uint32_t &y2, uint32_t &y3, uint32_t gb) const {
+        ghash_mul<kB64, true>(y0, y1, y2, y3, gb);
+    }
+};
+typedef Tab2T<false> Tab2;
+
+// GHASH multiply by the uniform H^4 through a 5-bit comb (single-key batches, engine Tab2F).  The
+// 128 bits of Y (LE words y0..y3, bit t = bit t%32 of word t/32) are cut into 26 windows of 5 bits
+// (the last has 3); window i's table holds, for each of its 32 values v, the product with H^4 of the
+// element whose only bits are v at bits 5i..5i+4, as two 8-B halves: words 0-1 at 512 i + 8 v, words
+// 2-3 at 512 i + 256 + 8 v.  A half-table is one 256-B bank row, so the 32 lanes of a ds_read_b64
+// lane group read any 32 values without a conflict (64 banks for b64: MI355X_MICROARCH.md "LDS"),
+// and the address of window i is ((Y >> (5i mod 32 - 3)) & 0xf8): one shift and one all-VGPR AND,
+// its table offset an immediate.  26 x 2 ds_read_b64 = 52 LDS cycles per multiply against 64 for the
+// 4-bit comb (2 x 32 ds_read_b64), and 25 shifts + 26 ANDs instead of 48 v_perm/shift/AND-literal ops.
+constexpr uint32_t kG5Windows = 26;
+constexpr uint32_t kG5Bytes = kG5Windows * 512;  // 13 KiB, at LDS address 0 (T-tables after it)
+
+template <int kI>
+__device__ __forceinline__ uint32_t g5_addr(const uint32_t (&y)[4], uint32_t mf8) {
+    constexpr int p = 5 * kI, w = p >> 5, o = p & 31;
+    uint32_t x;
+    if constexpr (o > 27 && w < 3)
+        x = __builtin_amdgcn_alignbit(y[w + 1], y[w], o - 3);  // the window crosses into the next word
+    else if constexpr (o > 3)
+        x = y[w] >> (o - 3);
+    else if constexpr (o < 3)
+        x = y[w] << (3 - o);
+    else
+        x = y[w];
+    return x & mf8;
+}
+
+template <int kLo, int kHi>
+__device__ __forceinline__ void g5_chunk(const uint32_t (&y)[4], uint32_t mf8, uint32_t &a0, uint32_t &a1,
+                                         uint32_t &a2, uint32_t &a3) {
+    if constexpr (kLo < kHi) {
+        const uint32_t x = g5_addr<kLo>(y, mf8);
+        const u32x2 h0 = lds64(x + kLo * 512u), h1 = lds64(x + kLo * 512u + 256u);
+        if constexpr (kLo + 1 < kHi) {
+            const uint32_t x2 = g5_addr<kLo + 1>(y, mf8);
+            const u32x2 l0 = lds64(x2 + (kLo + 1) * 512u), l1 = lds64(x2 + (kLo + 1) * 512u + 256u);
+            a0 = xor3(a0, h0.x, l0.x);
+            a1 = xor3(a1, h0.y, l0.y);
+            a2 = xor3(a2, h1.x, l1.x);
+            a3 = xor3(a3, h1.y, l1.y);
+            g5_chunk<kLo + 2, kHi>(y, mf8, a0, a1, a2, a3);
+        } else {
+            a0 ^= h0.x;
+            a1 ^= h0.y;
+            a2 ^= h1.x;
+            a3 ^= h1.y;
+        }
+    }
+}
+
+__device__ __forceinline__ void ghash_mul5(uint32_t &y0, uint32_t &y1, uint32_t &y2, uint32_t &y3, uint32_t mf8) {
+    const uint32_t y[4] = {y0, y1, y2, y3};
+    uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+    // four chunks (7, 6, 7, 6 windows): at most 7 x 16 B of table rows live, as the 4-bit comb's 8
+    g5_chunk<0, 7>(y, mf8, a0, a1, a2, a3);
+    asm volatile("" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3)::"memory");
+    g5_chunk<7, 13>(y, mf8, a0, a1, a2, a3);
+    asm volatile("" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3)::"memory");
+    g5_chunk<13, 20>(y, mf8, a0, a1, a2, a3);
+    asm volatile("" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3)::"memory");
+    g5_chunk<20, 26>(y, mf8, a0, a1, a2, a3);
+    y0 = a0;
+    y1 = a1;
+    y2 = a2;
+    y3 = a3;
+}
+
+// Fills the 5-bit comb of H^4 at LDS address 0 from the key's 4-bit comb of H^4 (global, entry
+// 16 p + v: nibble position p = 2 * byte (high nibble) or 2 * byte + 1 (low), value v): the product
+// for bit t alone is entry p = 2 (t >> 3) + (t % 8 < 4), v = 1 << (t % 4); window entries are XORs
+// of those (GHASH multiplication is linear).
+__device__ __forceinline__ void g5_fill(const uint4 *__restrict__ comb4, uint32_t tid, uint32_t nthreads) {
+    for (uint32_t e = tid; e < kG5Windows * 32u; e += nthreads) {
+        const uint32_t i = e >> 5, v = e & 31u;
+        uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+        for (uint32_t j = 0; j < 5; ++j) {
+            const uint32_t t = 5 * i + j;
+            if (((v >> j) & 1u) && t < 128u) {
+                const uint4 c = comb4[16u * (2u * (t >> 3) + ((t & 7u) < 4u ? 1u : 0u)) + (1u << (t & 3u))];
+                a0 ^= c.x;
+                a1 ^= c.y;
+                a2 ^= c.z;
+                a3 ^= c.w;
+            }
+        }
+        *(lds_u64 *)(size_t)(512u * i + 8u * v) = u32x2{a0, a1};
+        *(lds_u64 *)(size_t)(512u * i + 256u + 8u * v) = u32x2{a2, a3};
+    }
+}
+
+// Tab2F: the Tab2 round with its tables at kG5Bytes (after the 5-bit comb), byte-1 addresses by an
+// all-VGPR AND-OR, and GHASH by the 5-bit comb.  LDS 77 KiB per workgroup: two 16-wave workgroups
+// per CU (32 waves/CU) as Tab2.
+struct Tab2F {
+    Keys kk;
+    TT<kG5Bytes, true> t;
+    uint32_t mf8;  // 0xf8 as a VGPR
+    __device__ __forceinline__ void setup(Ctr &c, uint32_t n0, uint32_t n1, uint32_t n2, uint32_t hi) const {
+        ctr_setup(c, n0, n1, n2, hi, kk, t);
+    }
+    __device__ __forceinline__ void block(const Ctr &c, uint32_t lo, uint32_t &k0, uint32_t &k1, uint32_t &k2,
+                                          uint32_t &k3) const {
+        ctr_block_t<TT<kG5Bytes, true>, kG5Bytes>(c, lo, kk, t, k0, k1, k2, k3);
+    }
+    template <bool kB64>
+    __device__ __forceinline__ void ghash(uint32_t &y0, uint32_t &y1, uint32_t &y2, uint32_t &y3, uint32_t) const {
+        ghash_mul5(y0, y1, y2, y3, mf8);
     }
 };
 
@@ -297,6 +453,10 @@ struct Tab4 {
         k1 = st[1];
         k2 = st[2];
         k3 = st[3];
+    }
+    template <bool kB64>
+    __device__ __forceinline__ void ghash(uint32_t &y0, uint32_t &y1, uint32_t &y2, uint32_t &y3, uint32_t gb) const {
+        ghash_mul<kB64, true>(y0, y1, y2, y3, gb);
     }
 };
 
@@ -793,7 +953,7 @@ __device__ __forceinline__ void quad_packet(const Batch &b, const Eng &eng, uint
             c.z &= q > 2 ? 0xffffffffu : (q == 2 ? lowmask(sb) : 0u);
             c.w &= q == 3 ? lowmask(sb) : 0u;
         }
-        ghash_mul<!kDesc>(z0, z1, z2, z3, gH4);
+        eng.template ghash<!kDesc>(z0, z1, z2, z3, gH4);
         z0 ^= c.x;
         z1 ^= c.y;
         z2 ^= c.z;
@@ -818,7 +978,7 @@ __device__ __forceinline__ void quad_packet(const Batch &b, const Eng &eng, uint
         const W4 out = {in.x ^ k0, in.y ^ k1, in.z ^ k2, in.w ^ k3};
         *p = out;
         const W4 &c = kSeal ? out : in;
-        ghash_mul<!kDesc>(z0, z1, z2, z3, gH4);
+        eng.template ghash<!kDesc>(z0, z1, z2, z3, gH4);
         z0 ^= c.x;
         z1 ^= c.y;
         z2 ^= c.z;
@@ -855,7 +1015,7 @@ __device__ __forceinline__ void quad_packet(const Batch &b, const Eng &eng, uint
             c.y &= q > 1 ? 0xffffffffu : (q == 1 ? lowmask(sb) : 0u);
             c.z &= q > 2 ? 0xffffffffu : (q == 2 ? lowmask(sb) : 0u);
             c.w &= q == 3 ? lowmask(sb) : 0u;
-            ghash_mul<!kDesc>(z0, z1, z2, z3, gH4);
+            eng.template ghash<!kDesc>(z0, z1, z2, z3, gH4);
             z0 ^= c.x;
             z1 ^= c.y;
             z2 ^= c.z;
@@ -935,9 +1095,13 @@ __device__ __forceinline__ void quad_packet(const Batch &b, const Eng &eng, uint
 template <bool kSeal, int kW, bool kFold, int kWpe = kW / 4, bool kDesc = false, bool kGFin = true, int kTab = 2>
 __global__ void __launch_bounds__(kW * 64) __attribute__((amdgpu_waves_per_eu(kWpe, kWpe)))
 gcm_quad_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
-    static_assert(kTab == 2 || (kTab == 4 && !kDesc), "four-table engine: single-key batches");
+    // kTab: 2 = Tab2, 5 = Tab2 with byte-1 AND-OR addresses, 3 = Tab2F, 4 = Tab4
+    static_assert(kTab == 2 || kTab == 5 || ((kTab == 4 || kTab == 3) && !kDesc),
+                  "Tab4/Tab2F engines: single-key batches");
+    static_assert(kTab != 3 || kGFin, "Tab2F: recombination from the global key table");
     constexpr uint32_t kT = kW * 64;
     constexpr uint32_t kTe = kTab == 4 ? kTe4Bytes : kTeBytes;  // LDS bytes of T-tables (comb tables after)
+    constexpr uint32_t kTeBase = kTab == 3 ? kG5Bytes : 0u;      // Tab2F: the 5-bit comb first, then Te
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = threadIdx.x >> 6;
     const uint32_t m = lane & 3u;          // block residue owned by this lane
@@ -947,10 +1111,12 @@ gcm_quad_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
     for (uint32_t i = threadIdx.x; i < kTeBytes / 4; i += kT) {
         const uint32_t x = i >> 6, slot = i & 63u;
         const uint32_t v = b.te[(slot >> 5) * 256u + x];
-        lds_st32(4 * i, v);
+        lds_st32(kTeBase + 4 * i, v);
         if constexpr (kTab == 4) lds_st32(kTeBytes + 4 * i, rot16(v));
     }
-    if constexpr (!kDesc) {
+    if constexpr (kTab == 3) {
+        g5_fill(b.gh_table + (size_t)b.uniform_key * kGhEntries + kGhH4, threadIdx.x, kT);
+    } else if constexpr (!kDesc) {
         const uint4 *src = b.gh_table + (size_t)b.uniform_key * kGhEntries + kGhH4;
         for (uint32_t e = threadIdx.x; e < 512u; e += kT) lds_st_comb<!kDesc>(kTe, e, src[e]);
         if constexpr (!kGFin) {
@@ -973,6 +1139,11 @@ gcm_quad_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
         e4.m8 = vreg(0x0000ff00u);
         e4.m24 = vreg(0xff000000u);
         e4.m16 = vreg(0xffff0000u);
+    }
+    uint32_t m8 = 0, mf8 = 0;
+    if constexpr (kTab == 3 || kTab == 5) {  // masks as VGPRs (an SGPR or literal operand issues at half rate)
+        m8 = vreg(0x0000ff00u);
+        mf8 = vreg(0x000000f8u);
     }
     // single key: the H^4 table shared by the workgroup; descriptors: one H^4 table per wave
     // (reloaded when the wave's key changes).  The once-per-packet multiplies by H^2..H^5 read the
@@ -1046,8 +1217,16 @@ gcm_quad_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
         }
         if constexpr (kTab == 4) {
             quad_packet<kSeal, kFold, kDesc, kGFin>(b, e4, pkt, off, L, wkey, m, gH4, gH);
+        } else if constexpr (kTab == 3) {
+            const Tab2F e3 = {{rk_table + (size_t)wkey * kRkWords, rk_table + (size_t)wkey * kRkWords + 64},
+                              {lb, m8}, mf8};
+            quad_packet<kSeal, kFold, kDesc, kGFin>(b, e3, pkt, off, L, wkey, m, gH4, gH);
+        } else if constexpr (kTab == 5) {
+            const Tab2T<true> e5 = {{rk_table + (size_t)wkey * kRkWords, rk_table + (size_t)wkey * kRkWords + 64},
+                                    {lb, m8}};
+            quad_packet<kSeal, kFold, kDesc, kGFin>(b, e5, pkt, off, L, wkey, m, gH4, gH);
         } else {
-            const Tab2 e2 = {{rk_table + (size_t)wkey * kRkWords, rk_table + (size_t)wkey * kRkWords + 64}, lb};
+            const Tab2 e2 = {{rk_table + (size_t)wkey * kRkWords, rk_table + (size_t)wkey * kRkWords + 64}, {lb, 0}};
             quad_packet<kSeal, kFold, kDesc, kGFin>(b, e2, pkt, off, L, wkey, m, gH4, gH);
         }
     }
@@ -1387,11 +1566,19 @@ Variant make_quad() {
                    kQuadLds + (kGFin ? 0u : kGhBytes), true, kWpe * 4 / kW, false};
 }
 
+// Tab2F engine (5-bit comb GHASH, byte-1 AND-OR addresses): 13 KiB comb + 64 KiB T-tables
+template <int kW, int kWpe>
+Variant make_quad2f() {
+    return Variant{reinterpret_cast<const void *>(&gcm_quad_kernel<true, kW, false, kWpe, false, true, 3>),
+                   reinterpret_cast<const void *>(&gcm_quad_kernel<false, kW, false, kWpe, false, true, 3>), kW,
+                   kG5Bytes + kTeBytes, true, kWpe * 4 / kW, false};
+}
+
 // descriptor batches: per-wave H^4 table, so LDS = Te + one 8 KiB table per wave
-template <int kW, int kWpe, bool kGFin = true>
+template <int kW, int kWpe, bool kGFin = true, int kTab = 2>
 Variant make_quad_desc() {
-    return Variant{reinterpret_cast<const void *>(&gcm_quad_kernel<true, kW, false, kWpe, true, kGFin>),
-                   reinterpret_cast<const void *>(&gcm_quad_kernel<false, kW, false, kWpe, true, kGFin>), kW,
+    return Variant{reinterpret_cast<const void *>(&gcm_quad_kernel<true, kW, false, kWpe, true, kGFin, kTab>),
+                   reinterpret_cast<const void *>(&gcm_quad_kernel<false, kW, false, kWpe, true, kGFin, kTab>), kW,
                    kTeBytes + (uint32_t)kW * kGhBytes, true, 1, true};
 }
 
@@ -1410,6 +1597,8 @@ hipError_t init_kernels() {
     g_variants[9] = make_quad<16, false, 8, false>();   // as 5, recombination by repeated H (LDS)
     g_variants[10] = make_quad_desc<12, 3, false>();    // as 7, recombination by repeated H (global)
     g_variants[11] = make_quad4<16>();                  // quad, four T-tables (128 KiB), 16 waves/CU
+    g_variants[13] = make_quad_desc<12, 3, true, 5>();  // as 7, byte-1 AND-OR addresses
+    g_variants[12] = make_quad2f<16, 8>();                // as 5, 5-bit comb GHASH + byte-1 AND-OR addresses
     for (const Variant &v : g_variants) {
         for (const void *k : {v.seal, v.open}) {
             hipFuncAttributes a;
