@@ -163,6 +163,9 @@ qgcm_group *qgcm_group_create(const int *devices, int count, uint32_t max_keys, 
 void qgcm_group_destroy(qgcm_group *g);
 int qgcm_group_size(const qgcm_group *g);
 qgcm_ctx *qgcm_group_ctx(qgcm_group *g, int member);  /* member's context (device batches on it) */
+/* Number of CPUs member's host thread is pinned to: its GPU's NUMA-local CPUs (sysfs local_cpulist of
+ * the PCI device) that the process may use; 0 = not pinned (no sysfs answer). */
+int qgcm_group_member_cpus(const qgcm_group *g, int member);
 int qgcm_group_shard(const qgcm_group *g, uint32_t key_idx);
 /* Installs keys[i] as key first_idx + i on its owning member only (qgcm_set_keys there). */
 int qgcm_group_set_keys(qgcm_group *g, uint32_t first_idx, uint32_t count, const uint8_t *keys);

@@ -17,7 +17,15 @@
 // by the member's descriptor batch (qgcm_seal_batch / qgcm_open_batch: sorted quad tiles), copied
 // back, and scattered into the caller's slots, which keep their input order.  Two staging slots per
 // member alternate, so the gather of chunk c + 1 overlaps chunk c on the device.
+//
+// NUMA: each member's thread runs on the CPUs local to its GPU (the PCI device's
+// local_cpulist in sysfs, intersected with the process's allowed CPUs), and it allocates that
+// member's pinned staging itself, so the gather/scatter copies and the DMA stay on the GPU's socket.
 #include <hip/hip_runtime.h>
+#include <pthread.h>
+#include <ctype.h>
+#include <sched.h>
+#include <stdlib.h>
 #include <stdio.h>
 #include <string.h>
 
@@ -49,7 +57,50 @@ struct Member {
     qgcm_ctx *ctx = nullptr;
     int device = 0;
     Stage st[kSlots];
+    cpu_set_t cpus;  // the GPU's local CPUs allowed to this process (empty: the thread is not pinned)
+    int ncpus = 0;
 };
+
+// "0-31,64-95" -> set bits (sysfs cpulist format)
+void parse_cpulist(const char *txt, cpu_set_t *set) {
+    CPU_ZERO(set);
+    const char *p = txt;
+    while (*p) {
+        char *e;
+        const long a = strtol(p, &e, 10);
+        if (e == p) break;
+        long b = a;
+        p = e;
+        if (*p == '-') {
+            b = strtol(p + 1, &e, 10);
+            p = e;
+        }
+        for (long c = a; c <= b && c < CPU_SETSIZE; ++c)
+            if (c >= 0) CPU_SET((int)c, set);
+        while (*p == ',' || *p == '\n' || *p == ' ') ++p;
+    }
+}
+
+// CPUs of the device's NUMA node that this process may run on; 0 when sysfs has no answer
+int gpu_local_cpus(int device, cpu_set_t *out) {
+    CPU_ZERO(out);
+    char bus[64] = {0};
+    if (hipDeviceGetPCIBusId(bus, (int)sizeof(bus), device) != hipSuccess) return 0;
+    for (char *c = bus; *c; ++c) *c = (char)tolower(*c);
+    char path[160];
+    snprintf(path, sizeof(path), "/sys/bus/pci/devices/%s/local_cpulist", bus);
+    FILE *f = fopen(path, "r");
+    if (!f) return 0;
+    char txt[4096] = {0};
+    const size_t got = fread(txt, 1, sizeof(txt) - 1, f);
+    fclose(f);
+    if (got == 0) return 0;
+    cpu_set_t local, allowed;
+    parse_cpulist(txt, &local);
+    if (sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return 0;
+    CPU_AND(out, &local, &allowed);
+    return CPU_COUNT(out);
+}
 
 inline uint64_t rec_bytes(bool seal, uint32_t len) {  // AAD word + packet (+ tag || nonce), 16-B aligned
     return (4ull + len + (seal ? QGCM_OVERHEAD : 0) + 15) & ~15ull;
@@ -106,6 +157,8 @@ int land(Stage &s, bool seal, uint8_t *h_arena, const qgcm_desc *descs, uint8_t 
 int run_member(Member &mb, bool seal, uint8_t *h_arena, const qgcm_desc *descs, const uint32_t *idx, size_t m,
                const uint8_t *h_nonces, uint32_t aad_len, uint8_t *h_status, int *bad_out) {
     int bad = 0, rc = QGCM_OK;
+    // a fresh thread per call: pin it before it allocates or touches staging (first touch = local pages)
+    if (mb.ncpus > 0) pthread_setaffinity_np(pthread_self(), sizeof(mb.cpus), &mb.cpus);
     if (hipSetDevice(mb.device) != hipSuccess) return QGCM_E_HIP;
     for (Stage &s : mb.st)
         if (!s.s && hipStreamCreateWithFlags(&s.s, hipStreamNonBlocking) != hipSuccess) return QGCM_E_HIP;
@@ -222,6 +275,7 @@ qgcm_group *qgcm_group_create(const int *devices, int count, uint32_t max_keys, 
     for (int k = 0; k < count; ++k) {
         Member mb;
         mb.device = devices[k];
+        mb.ncpus = gpu_local_cpus(devices[k], &mb.cpus);
         mb.ctx = qgcm_create(devices[k], max_keys, err, errlen);
         if (!mb.ctx) {
             for (Member &x : g->m) qgcm_destroy(x.ctx);
@@ -250,6 +304,10 @@ void qgcm_group_destroy(qgcm_group *g) {
 }
 
 int qgcm_group_size(const qgcm_group *g) { return g ? (int)g->m.size() : 0; }
+
+int qgcm_group_member_cpus(const qgcm_group *g, int member) {
+    return g && member >= 0 && member < (int)g->m.size() ? g->m[member].ncpus : QGCM_E_ARG;
+}
 
 qgcm_ctx *qgcm_group_ctx(qgcm_group *g, int member) {
     return g && member >= 0 && member < (int)g->m.size() ? g->m[member].ctx : nullptr;

@@ -84,6 +84,12 @@ class Group:
 
         return _lib.check(_lib.lib().qgcm_group_shard(self.handle, key_idx), "qgcm_group_shard")
 
+    def member_cpus(self, m: int) -> int:
+        """CPUs member m's host thread is pinned to (its GPU's NUMA-local CPUs; 0 = not pinned)."""
+        from . import _lib
+
+        return _lib.check(_lib.lib().qgcm_group_member_cpus(self.handle, m), "qgcm_group_member_cpus")
+
     def set_keys(self, first: int, keys: bytes) -> None:
         from . import _lib
 

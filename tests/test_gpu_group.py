@@ -130,6 +130,24 @@ def test_group_members_hold_only_their_keys(torch):
         grp.close()
 
 
+def test_group_member_threads_numa_local(torch):
+    """Each member's host thread is pinned to its GPU's NUMA-local CPUs (sysfs local_cpulist of the
+    PCI device, within the CPUs this process may use), SURVEY.md s8e."""
+    import os
+
+    from quantum_amd import shard
+
+    grp = shard.Group([0, 0], max_keys=4)
+    try:
+        allowed = len(os.sched_getaffinity(0))
+        n = [grp.member_cpus(m) for m in (0, 1)]
+        assert n[0] == n[1] and 0 <= n[0] <= allowed
+        if os.path.isdir("/sys/bus/pci/devices"):
+            assert n[0] > 0  # the box exposes the GPU's local_cpulist
+    finally:
+        grp.close()
+
+
 def test_config4_one_gpu_shard(torch, batch_digests):
     """8 x 2^20 packets x 1350 B on one GPU = its shard of config 4 (64 x 2^20 over 8 GPUs)."""
     from quantum_amd import batch
