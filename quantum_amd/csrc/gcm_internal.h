@@ -68,7 +68,8 @@ hipError_t launch_one(bool seal, const Batch &b, hipStream_t s);
 // Small descriptor batches through the latency kernel, one workgroup per packet, straight on the
 // caller's (pinned host or device) arena/descriptors/nonces/status -- the coalescer's flush path.
 constexpr uint32_t kOneBatchMax = 2048;
-constexpr uint32_t kOneUniformMax = 2048;  // measured cross-over with the quad kernel: 2048-4096 packets
+constexpr uint32_t kOneUniformMax = 2048;
+constexpr uint32_t kLaunchChunk = 1u << 19;  // packets per quad-kernel launch of a uniform batch  // measured cross-over with the quad kernel: 2048-4096 packets
 int run_one_descs(qgcm_ctx *ctx, bool seal, uint8_t *arena, const qgcm_desc *descs, uint32_t n,
                   const uint8_t *nonces, uint32_t aad_len, uint8_t *status, hipStream_t s);
 bool ctx_one_kernel(const qgcm_ctx *ctx);

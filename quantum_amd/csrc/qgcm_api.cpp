@@ -43,6 +43,8 @@ struct qgcm_ctx {
     bool variant_forced = false;            // QGCM_VARIANT given: uniform batches always run that variant
     uint32_t one_uniform_max = kOneUniformMax;  // uniform batches up to this many packets take the
                                                 // latency kernel (QGCM_ONE_UNIFORM_MAX, tuning)
+    uint32_t launch_chunk = kLaunchChunk;       // uniform batches launch at most this many packets per
+                                                // kernel (QGCM_LAUNCH_CHUNK, tuning; 0 = one launch)
     uint32_t *d_rk = nullptr;
     uint4 *d_gh = nullptr;
     uint32_t *d_te = nullptr;
@@ -256,7 +258,21 @@ int run_uniform(qgcm_ctx *ctx, bool seal, uint8_t *arena, uint64_t stride, uint3
         !((uintptr_t)arena & 15) && stage <= stride && stage <= kOneCap - 16)
         return hip_fail(launch_one(seal, b, s));
     const int v = ctx->uniform_variant;
-    return hip_fail(launch_packets(seal, v, b, grid_for(ctx, b.n_items, v), s));
+    // Large batches go out as back-to-back launches of launch_chunk packets on the same stream: one
+    // 2^23-packet launch ran at 768 GiB/s, the same batch as 2^19-packet launches at 827, at 2^20 packets
+    // either form 826-829 (tools/exp_chunked.py).
+    const uint32_t chunk = ctx->launch_chunk ? ctx->launch_chunk : n;
+    for (uint32_t p = 0; p < n; p += chunk) {
+        const uint32_t m = std::min(chunk, n - p);
+        Batch c = b;
+        c.arena = arena + (uint64_t)p * stride;
+        c.nonces = b.nonces ? b.nonces + 12ull * p : nullptr;
+        c.status = status ? status + p : nullptr;
+        c.n = m;
+        c.n_items = (uint32_t)(((uint64_t)m + 63) & ~63ull);
+        if (launch_packets(seal, v, c, grid_for(ctx, c.n_items, v), s) != hipSuccess) return QGCM_E_HIP;
+    }
+    return QGCM_OK;
 }
 
 int run_descs_locked(qgcm_ctx *ctx, bool seal, const qgcm_desc *descs, uint32_t n, hipStream_t s, Batch b,
@@ -452,6 +468,8 @@ qgcm_ctx *qgcm_create(int device, uint32_t max_keys, char *err, int errlen) {
     if (const char *v = getenv("QGCM_WGS_PER_CU")) ctx->wgs_per_cu_override = atoi(v);
     if (const char *v = getenv("QGCM_ONE_KERNEL")) ctx->one_kernel = atoi(v) != 0;
     if (const char *v = getenv("QGCM_ONE_UNIFORM_MAX")) ctx->one_uniform_max = (uint32_t)std::max(0, atoi(v));
+    if (const char *v = getenv("QGCM_LAUNCH_CHUNK"))  // rounded down to whole 64-packet tiles
+        ctx->launch_chunk = (uint32_t)std::max(0, atoi(v)) & ~63u;
     if (const char *v = getenv("QGCM_PIPE_CHUNK_MB")) ctx->host_chunk = (uint64_t)std::max(1, atoi(v)) << 20;
     if (const char *v = getenv("QGCM_PIPE_RING_MB")) ctx->host_ring = (uint64_t)std::max(1, atoi(v)) << 20;
     if (const char *v = getenv("QGCM_DESC_VARIANT")) {
