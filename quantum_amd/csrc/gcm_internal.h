@@ -69,7 +69,8 @@ hipError_t launch_one(bool seal, const Batch &b, hipStream_t s);
 // caller's (pinned host or device) arena/descriptors/nonces/status -- the coalescer's flush path.
 constexpr uint32_t kOneBatchMax = 2048;
 constexpr uint32_t kOneUniformMax = 2048;
-constexpr uint32_t kLaunchChunk = 1u << 19;  // packets per quad-kernel launch of a uniform batch  // measured cross-over with the quad kernel: 2048-4096 packets
+constexpr uint32_t kLaunchChunk = 1u << 19;  // packets per quad-kernel launch of a uniform batch
+constexpr uint32_t kDescChunk = 0;           // packets per sorted chunk of a descriptor batch (0 = all)  // measured cross-over with the quad kernel: 2048-4096 packets
 int run_one_descs(qgcm_ctx *ctx, bool seal, uint8_t *arena, const qgcm_desc *descs, uint32_t n,
                   const uint8_t *nonces, uint32_t aad_len, uint8_t *status, hipStream_t s);
 bool ctx_one_kernel(const qgcm_ctx *ctx);

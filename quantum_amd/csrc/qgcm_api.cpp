@@ -45,6 +45,8 @@ struct qgcm_ctx {
                                                 // latency kernel (QGCM_ONE_UNIFORM_MAX, tuning)
     uint32_t launch_chunk = kLaunchChunk;       // uniform batches launch at most this many packets per
                                                 // kernel (QGCM_LAUNCH_CHUNK, tuning; 0 = one launch)
+    uint32_t desc_chunk = kDescChunk;           // descriptor batches: packets per sorted chunk
+                                                // (QGCM_DESC_CHUNK, tuning; 0 = one launch)
     uint32_t *d_rk = nullptr;
     uint4 *d_gh = nullptr;
     uint32_t *d_te = nullptr;
@@ -307,6 +309,17 @@ int run_descs_locked(qgcm_ctx *ctx, bool seal, const qgcm_desc *descs, uint32_t 
     b.n = n;
     b.aad_len = aad_len;
     const int v = ctx->desc_variant;
+    if (variant_desc(v) && ctx->desc_chunk && n > ctx->desc_chunk) {
+        // back-to-back chunks on this stream, each with its own sorted worklist (the workspace is
+        // reused in stream order); descriptors, nonces and status are chunk-relative, offsets absolute
+        for (uint32_t p = 0; p < n; p += ctx->desc_chunk) {
+            const uint32_t m = std::min(ctx->desc_chunk, n - p);
+            const int rc = run_descs_locked(ctx, seal, descs + p, m, s, b, arena, nonces ? nonces + 12ull * p : nullptr,
+                                            aad_len, status ? status + p : nullptr);
+            if (rc != QGCM_OK) return rc;
+        }
+        return QGCM_OK;
+    }
     if (variant_desc(v)) {
         uint32_t items = 0;
         const size_t need = quad_worklist_bytes(n, ctx->max_keys, &items);
@@ -470,6 +483,7 @@ qgcm_ctx *qgcm_create(int device, uint32_t max_keys, char *err, int errlen) {
     if (const char *v = getenv("QGCM_ONE_UNIFORM_MAX")) ctx->one_uniform_max = (uint32_t)std::max(0, atoi(v));
     if (const char *v = getenv("QGCM_LAUNCH_CHUNK"))  // rounded down to whole 64-packet tiles
         ctx->launch_chunk = (uint32_t)std::max(0, atoi(v)) & ~63u;
+    if (const char *v = getenv("QGCM_DESC_CHUNK")) ctx->desc_chunk = (uint32_t)std::max(0, atoi(v));
     if (const char *v = getenv("QGCM_PIPE_CHUNK_MB")) ctx->host_chunk = (uint64_t)std::max(1, atoi(v)) << 20;
     if (const char *v = getenv("QGCM_PIPE_RING_MB")) ctx->host_ring = (uint64_t)std::max(1, atoi(v)) << 20;
     if (const char *v = getenv("QGCM_DESC_VARIANT")) {

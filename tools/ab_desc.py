@@ -2,7 +2,8 @@
 
 Each variant is its own qgcm context (QGCM_DESC_VARIANT is read at qgcm_create) with the same 1024
 keys.  Correctness: every variant's sealed arena must equal the first variant's byte for byte.
-Usage: python tools/ab_desc.py 7,10,8 [rounds]
+Usage: python tools/ab_desc.py 7,10,8 [rounds]; an entry v:cN runs variant v with QGCM_DESC_CHUNK=N
+(packets per sorted chunk), e.g. 7,7:c131072,7:c262144
 """
 import os
 import statistics
@@ -15,14 +16,15 @@ import torch  # noqa: E402
 from quantum_amd import batch  # noqa: E402
 from quantum_amd.crypto import Context  # noqa: E402
 
-variants = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "7,10").split(",")]
+variants = (sys.argv[1] if len(sys.argv) > 1 else "7,10").split(",")
 rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 N, NK = 1 << 20, 1024
 rng = np.random.default_rng(0x5EED0003)
 keys = rng.bytes(32 * NK)
 ctxs = {}
 for v in variants:
-    os.environ["QGCM_DESC_VARIANT"] = str(v)
+    os.environ["QGCM_DESC_VARIANT"] = v.split(":")[0]
+    os.environ["QGCM_DESC_CHUNK"] = v.split(":c")[1] if ":c" in v else "0"
     c = Context(device=0, max_keys=NK)
     c.set_keys(0, keys)
     ctxs[v] = c
