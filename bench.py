@@ -33,7 +33,8 @@ from quantum_amd.crypto import Context, derive_key  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, MI355X_MICROARCH.md "Chip-level parameters"
 # PMC passes of this command (tools/pmc_traffic.py), newest first
-TRAFFIC_JSONS = [os.path.join(ROOT, "profiles", d, "traffic.json") for d in ("r2_s2", "r2_final", "r1_s3")]
+LAUNCH_CHUNK = 1 << 19  # quantum_amd/csrc/gcm_internal.h kLaunchChunk
+TRAFFIC_JSONS = [os.path.join(ROOT, "profiles", d, "traffic.json") for d in ("r2_s3", "r2_s2", "r2_final", "r1_s3")]
 CONFIG4_PACKETS = 64 << 20  # BASELINE config 4: 64 M packets over the node's GPUs
 SECRET = b"AES256Key-32Characters1234567890"
 SALT = bytes(range(32))
@@ -252,6 +253,9 @@ def main() -> None:
     read_pkt = L + 16 if kname == "seal" else L + 32  # the HBM-read-only variant
     achieved_read = N * read_pkt / (kms * 1e-3) / 1e9
     traffic, lds_busy, traffic_src = pmc_traffic(kname, N, L, stride)
+    # libqgcm launches a uniform batch in chunks of LAUNCH_CHUNK packets: kms spans them all
+    chunk = int(os.environ.get("QGCM_LAUNCH_CHUNK", str(LAUNCH_CHUNK))) // 64 * 64 or N
+    launches = -(-N // chunk)
     copy_gbs = stream_copy_gbs(ctx, N * stride, dev, stream)  # after the timed region
 
     if rank == 0:
@@ -280,6 +284,8 @@ def main() -> None:
                          "traffic": traffic, "traffic_source": traffic_src,
                          "traffic_over_algorithmic": round(traffic / (N * per_pkt), 3) if traffic else None,
                          "bytes_per_packet": per_pkt, "kernel_ms": round(kms, 4),
+                         "launches_per_call": launches, "packets_per_launch": min(chunk, N),
+                         "launch_ms": round(kms / launches, 4),
                          "achieved_read_only": round(achieved_read, 1),
                          "read_bytes_per_packet": read_pkt,
                          "copy_achievable": round(copy_gbs, 1),
