@@ -5,17 +5,19 @@
 // plugin/encryption.go:22-37 makes for every tunnelled payload.
 //
 // Design (DESIGN.md has the numbers):
-//  * one lane = one packet = one GCM instance; a wave64 owns 64 packets that share a key
-//    (key-uniform tiles), so round keys sit in SGPRs and the GHASH multiplier H is uniform;
+//  * gcm_quad_kernel (the batch path): four lanes per packet (lane m owns blocks m mod 4), 16 packets
+//    per wave, key-uniform wave tiles so round keys sit in SGPRs and the GHASH multiplier is uniform;
+//    persistent grid of two 16-wave workgroups per CU; gcm_one_kernel: one workgroup per packet
+//    (the per-call Encrypt/Decrypt); gcm_kernel: the round-1 lane-per-packet design (A/B variants);
 //  * AES-256 by T-tables in LDS: Te0/Te1 replicated 32x so a ds_read_b32 is bank-conflict free;
-//    the lookup address (x<<8 | lane*4) is ONE v_perm_b32; Te2/Te3 = rot16(Te0/Te1) folded
-//    into the column XOR;
+//    the lookup address (x<<8 | lane*4) is ONE v_perm_b32 (one all-VGPR AND-OR for byte 1 in the
+//    Tab2F engine); Te2/Te3 = rot16(Te0/Te1) folded into the column XOR;
 //  * CTR caching: counters of a packet differ only in the low byte for 256 consecutive blocks,
 //    so rounds 1-2 collapse to 5 lookups per block (197 instead of 224 lookups per block);
-//  * GHASH by a 4-bit comb of the uniform H: 32 tables x 16 entries x 16 B = one 256-B bank row
-//    per table, so 64 lanes reading arbitrary nibbles via ds_read_b128 never conflict;
-//    the address is again one v_perm_b32;
-//  * the kernel is persistent: one 512-thread workgroup per CU fills the LDS tables once.
+//  * GHASH by comb tables of the uniform multiplier H^4 in LDS: the 5-bit comb of the default
+//    single-key engine (Tab2F: 26 windows x 2 ds_read_b64, one 256-B bank row per half-table), the
+//    4-bit comb elsewhere (one 256-B bank row per nibble table); each lane runs a Horner chain by H^4
+//    and the four chains are recombined once per packet.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -330,16 +332,21 @@ __device__ __forceinline__ void ghash_mul5(uint32_t &y0, uint32_t &y1, uint32_t 
 __device__ __forceinline__ void g5_fill(const uint4 *__restrict__ comb4, uint32_t tid, uint32_t nthreads) {
     for (uint32_t e = tid; e < kG5Windows * 32u; e += nthreads) {
         const uint32_t i = e >> 5, v = e & 31u;
-        uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+        // five unconditional loads in flight (an unset bit reads the all-zero entry v = 0 of its table)
+        uint4 c[5];
+#pragma unroll
         for (uint32_t j = 0; j < 5; ++j) {
-            const uint32_t t = 5 * i + j;
-            if (((v >> j) & 1u) && t < 128u) {
-                const uint4 c = comb4[16u * (2u * (t >> 3) + ((t & 7u) < 4u ? 1u : 0u)) + (1u << (t & 3u))];
-                a0 ^= c.x;
-                a1 ^= c.y;
-                a2 ^= c.z;
-                a3 ^= c.w;
-            }
+            const uint32_t t = 5 * i + j, tt = t < 128u ? t : 127u;
+            const uint32_t vv = (((v >> j) & 1u) && t < 128u) ? (1u << (tt & 3u)) : 0u;
+            c[j] = comb4[16u * (2u * (tt >> 3) + ((tt & 7u) < 4u ? 1u : 0u)) + vv];
+        }
+        uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < 5; ++j) {
+            a0 ^= c[j].x;
+            a1 ^= c[j].y;
+            a2 ^= c[j].z;
+            a3 ^= c[j].w;
         }
         *(lds_u64 *)(size_t)(512u * i + 8u * v) = u32x2{a0, a1};
         *(lds_u64 *)(size_t)(512u * i + 256u + 8u * v) = u32x2{a2, a3};
