@@ -45,10 +45,12 @@ def host_buffer(nbytes: int, pinned: bool):
     return arr, arr.ctypes.data, lambda: None
 
 
-@pytest.mark.parametrize("G,pinned", [(2, True), (3, False)])
-def test_group_keyed_host_batch_vs_oracle(torch, G, pinned):
+@pytest.mark.parametrize("G,pinned,threads", [(2, True, "4"), (3, False, "7"), (1, True, "1")])
+def test_group_keyed_host_batch_vs_oracle(torch, G, pinned, threads, monkeypatch):
+    """threads: QGCM_GROUP_THREADS, the gather/scatter copy threads per member (read at creation)."""
     from quantum_amd import shard
 
+    monkeypatch.setenv("QGCM_GROUP_THREADS", threads)
     grp = shard.Group([0] * G, max_keys=256)
     try:
         rng = random.Random(0x6A0 + G)

@@ -11,6 +11,9 @@
            with PCIe copies and the device (qgcm_compress_seal_host / qgcm_open_uncompress_host).
 
   config4_shard  one GPU's 8 x 2^20-packet shard of config 4 (64 x 2^20 x 1350 B over 8 GPUs).
+  group_e2e      keyed host batches through the one-process multi-GPU dispatcher (qgcm_group_*):
+                 2^20 x 1350 B, 64 keys, G member contexts (on the 1-GPU box all on device 0), pinned
+                 host arena; the PCIe-inclusive rate of quantum's single process.
 
 Prints one JSON line per config.  Usage: python tools/bench_configs.py [config3] [e2e] [config4_shard] ...
 """
@@ -241,9 +244,53 @@ def config4_shard(reps: int = 5, world: int = 8, rank: int = 0) -> dict:
             "unit": "GiB/s (this GPU)", "seal_ms": round(s, 3), "open_ms": round(o, 3), "status_ok": ok}
 
 
+def group_e2e(G: int = 1, reps: int = 3) -> dict:
+    from quantum_amd import shard
+
+    N, L, NK = 1 << 20, 1350, 64
+    stride = batch.slot_stride(L, align=64)
+    rng = np.random.default_rng(0x5EED0006)
+    grp = shard.Group([0] * G, max_keys=NK)
+    grp.set_keys(0, rng.bytes(32 * NK))
+    L_ = _lib.lib()
+    a_ptr, n_ptr = L_.qgcm_host_alloc(N * stride), L_.qgcm_host_alloc(12 * N)
+    host = np.frombuffer((C.c_uint8 * (N * stride)).from_address(a_ptr), np.uint8)
+    nonces = np.frombuffer((C.c_uint8 * (12 * N)).from_address(n_ptr), np.uint8)
+    host[:] = np.frombuffer(rng.bytes(N * stride), np.uint8)
+    nonces[:] = np.frombuffer(rng.bytes(12 * N), np.uint8)
+    offs = np.arange(N, dtype=np.int64) * stride
+    kidx = rng.integers(0, NK, size=N)
+    d_seal = shard.host_descs(offs, np.full(N, L), kidx)
+    d_open = shard.host_descs(offs, np.full(N, L + 28), kidx)
+    status = np.zeros(N, np.uint8)
+    plain = host[:4096 * stride].copy()
+    bad = grp.seal_host(a_ptr, d_seal, N, n_ptr, 4, status.ctypes.data)
+    bad += grp.open_host(a_ptr, d_open, N, 4, status.ctypes.data)
+    ok = bad == 0 and bool(np.array_equal(host[:4096 * stride].reshape(4096, stride)[:, :4 + L],
+                                          plain.reshape(4096, stride)[:, :4 + L]))
+    ts, to = [], []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        bad += grp.seal_host(a_ptr, d_seal, N, n_ptr, 4, None)
+        t1 = time.perf_counter()
+        bad += grp.open_host(a_ptr, d_open, N, 4, None)
+        t2 = time.perf_counter()
+        ts.append(t1 - t0)
+        to.append(t2 - t1)
+    s, o = float(np.median(ts)), float(np.median(to))
+    cpus = [grp.member_cpus(m) for m in range(G)]
+    grp.close()
+    del host, nonces
+    L_.qgcm_host_free(a_ptr)
+    L_.qgcm_host_free(n_ptr)
+    return {"config": "group_e2e_keyed_host", "members": G, "devices": [0] * G, "packets": N, "payload_len": L,
+            "keys": NK, "value": round(2 * N * L / (s + o) / 2**30, 2), "unit": "GiB/s", "seal_s": round(s, 4),
+            "open_s": round(o, 4), "member_cpus": cpus, "status_ok": ok and bad == 0}
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["config3", "e2e", "e2e_pageable", "config5", "config4_shard"]
     runs = {"config3": config3, "e2e": e2e, "e2e_pageable": lambda: e2e(pinned=False), "config5": config5,
-            "config4_shard": config4_shard}
+            "config4_shard": config4_shard, "group_e2e": group_e2e, "group_e2e2": lambda: group_e2e(2)}
     for w in which:
         print(json.dumps(runs[w]()), flush=True)
