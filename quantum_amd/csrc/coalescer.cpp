@@ -16,10 +16,20 @@
 //
 // kDepth batches per direction rotate FREE -> FILLING -> FLUSHING -> DONE -> FREE, so the next batch
 // fills while one is on the device and callers of the previous one copy out.
+//
+// Completion is published without the lane mutex: the flusher bumps the batch's 32-bit `done`
+// sequence and wakes its waiters with one futex call; callers check it, spin briefly, then sleep on
+// the futex, and hand the batch back with an atomic reader count (the last reader recycles it under
+// the mutex).  With a condition variable every notify_all made all of a batch's callers re-acquire
+// the lane mutex one after another before they could copy out.
 #include <hip/hip_runtime.h>
+#include <linux/futex.h>
 #include <string.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <mutex>
@@ -42,12 +52,26 @@ struct CBatch {
     uint32_t n = 0;         // reserved slots
     uint64_t used = 0;      // reserved arena bytes
     uint32_t writers = 0;   // callers still copying in
-    uint32_t readers = 0;   // callers still to copy out
-    uint64_t gen = 0;       // bumped each time the batch is recycled
-    int rc = QGCM_OK;       // batch-level result
+    std::atomic<uint32_t> readers{0};  // callers still to copy out
+    std::atomic<uint32_t> done{0};     // completion sequence: bumped once per flush (futex word)
+    int rc = QGCM_OK;       // batch-level result (written before `done` is bumped)
     St st = St::Free;
     Clock::time_point first, last;  // first and latest reservation
 };
+
+long futex(std::atomic<uint32_t> *w, int op, uint32_t v) {
+    return syscall(SYS_futex, reinterpret_cast<uint32_t *>(w), op, v, nullptr, nullptr, 0);
+}
+
+// Wait until *w != seen: a short spin (a batch on the latency kernel lands in tens of us), then sleep
+// on the futex.
+void wait_change(std::atomic<uint32_t> *w, uint32_t seen) {
+    for (int i = 0; i < 64; ++i) {
+        if (w->load(std::memory_order_acquire) != seen) return;
+        __builtin_ia32_pause();
+    }
+    while (w->load(std::memory_order_acquire) == seen) futex(w, FUTEX_WAIT_PRIVATE, seen);
+}
 
 struct Lane {
     bool seal = true;
@@ -139,9 +163,10 @@ void flusher(qgcm_coalescer *c, Lane *ln) {
 
         lk.lock();
         B.rc = rc;
-        B.readers = n;
+        B.readers.store(n, std::memory_order_relaxed);
         B.st = St::Done;
-        ln->cv_caller.notify_all();
+        B.done.fetch_add(1, std::memory_order_release);  // publishes rc, status and the slots
+        futex(&B.done, FUTEX_WAKE_PRIVATE, INT32_MAX);
     }
 }
 
@@ -173,7 +198,9 @@ long submit(qgcm_coalescer *c, Lane *ln, uint32_t key_idx, uint8_t *data, uint32
         ln->cv_caller.wait(lk);
     }
     CBatch &B = ln->b[idx];
-    const uint64_t gen = B.gen;
+    // the flush of this batch bumps `done` past this value (it cannot have happened yet: this caller
+    // is still a writer)
+    const uint32_t seen = B.done.load(std::memory_order_relaxed);
     lk.unlock();
 
     uint8_t *slot = B.h_arena + off;
@@ -183,9 +210,9 @@ long submit(qgcm_coalescer *c, Lane *ln, uint32_t key_idx, uint8_t *data, uint32
 
     lk.lock();
     if (--B.writers == 0) ln->cv_flush.notify_one();
-    ln->cv_caller.wait(lk, [&] { return B.gen == gen && B.st == St::Done; });
-    const int rc = B.rc;
     lk.unlock();
+    wait_change(&B.done, seen);
+    const int rc = B.rc;
 
     long out = -1;
     if (rc == QGCM_OK) {
@@ -201,13 +228,13 @@ long submit(qgcm_coalescer *c, Lane *ln, uint32_t key_idx, uint8_t *data, uint32
         }
     }
 
-    lk.lock();
-    if (--B.readers == 0) {
+    if (B.readers.fetch_sub(1, std::memory_order_acq_rel) == 1) {  // the last reader recycles the batch
+        lk.lock();
         B.n = 0;
         B.used = 0;
-        B.gen++;
         B.st = (&B == &ln->b[ln->fill]) ? St::Filling : St::Free;
         ln->cv_caller.notify_all();
+        ln->cv_flush.notify_one();
     }
     return out;
 }
