@@ -116,6 +116,22 @@ struct Keys {
     const uint32_t *rr;
 };
 
+// Wave priority while a round issues its 16 lookups (s_setprio n, back to 0 once they are issued):
+// the instruction arbiter then favours waves about to feed the LDS over waves combining results, so
+// the LDS queue runs dry less often.  Priority 1 on the full rounds: +1.9 / +3.4 / +4.6% on config 2
+// in three in-process A/Bs (tools/ab_libs.py), +1.7% on config 3 (tools/ab_libs_desc.py); priority 2
+// or 3, or also on the final round or the GHASH lookups, no better.  The values are
+// compile-time knobs (-DQGCM_ROUND_PRIO=n etc., 0 = off) for side builds in those A/Bs.
+#ifndef QGCM_ROUND_PRIO
+#define QGCM_ROUND_PRIO 1
+#endif
+#ifndef QGCM_LAST_PRIO
+#define QGCM_LAST_PRIO 0
+#endif
+#ifndef QGCM_GH_PRIO
+#define QGCM_GH_PRIO 0
+#endif
+
 // One full AES round (SubBytes, ShiftRows, MixColumns, AddRoundKey) on LE column words:
 // column c = Te0[s_c.b0] ^ Te1[s_c+1.b1] ^ rot16(Te0[s_c+2.b2] ^ Te1[s_c+3.b3]) ^ rk_c.
 template <class A>
@@ -124,11 +140,13 @@ __device__ __forceinline__ void round_full(uint32_t &s0, uint32_t &s1, uint32_t 
     // All 16 lookups of the round are issued before the first combine (the asm is a scheduling
     // fence): up to 16 LDS reads in flight per wave instead of 1-2 under the 64-VGPR budget.
     // +2.9% on config 2 in an in-process A/B.
+    if constexpr (QGCM_ROUND_PRIO > 0) __builtin_amdgcn_s_setprio(QGCM_ROUND_PRIO);
     const uint32_t a0 = t.t0(s2, 2), a1 = t.t1(s3, 3), a2 = t.t0(s3, 2), a3 = t.t1(s0, 3);
     const uint32_t a4 = t.t0(s0, 2), a5 = t.t1(s1, 3), a6 = t.t0(s1, 2), a7 = t.t1(s2, 3);
     const uint32_t c0 = t.t0(s0, 0), c1 = t.t1(s1, 1), c2 = t.t0(s1, 0), c3 = t.t1(s2, 1);
     const uint32_t c4 = t.t0(s2, 0), c5 = t.t1(s3, 1), c6 = t.t0(s3, 0), c7 = t.t1(s0, 1);
     asm volatile("" ::: "memory");
+    if constexpr (QGCM_ROUND_PRIO > 0) __builtin_amdgcn_s_setprio(0);
     s0 = xor3(c0, c1, rot16(xor3(a0, a1, k.rr[4 * r + 0])));
     s1 = xor3(c2, c3, rot16(xor3(a2, a3, k.rr[4 * r + 1])));
     s2 = xor3(c4, c5, rot16(xor3(a4, a5, k.rr[4 * r + 2])));
@@ -145,11 +163,13 @@ __device__ __forceinline__ void round_last(uint32_t &s0, uint32_t &s1, uint32_t 
                                            const A &t) {
     const uint32_t *rk = k.rk + 56;
     // 16 lookups in flight, then combine (as round_full; +1.1% in an in-process A/B)
+    if constexpr (QGCM_LAST_PRIO > 0) __builtin_amdgcn_s_setprio(QGCM_LAST_PRIO);
     const uint32_t a0 = t.t0(s1, 1), a1 = t.t0(s0, 0), a2 = t.t1(s3, 3), a3 = t.t0(s2, 2);
     const uint32_t b0 = t.t0(s2, 1), b1 = t.t0(s1, 0), b2 = t.t1(s0, 3), b3 = t.t0(s3, 2);
     const uint32_t c0 = t.t0(s3, 1), c1 = t.t0(s2, 0), c2 = t.t1(s1, 3), c3 = t.t0(s0, 2);
     const uint32_t d0 = t.t0(s0, 1), d1 = t.t0(s3, 0), d2 = t.t1(s2, 3), d3 = t.t0(s1, 2);
     asm volatile("" ::: "memory");
+    if constexpr (QGCM_LAST_PRIO > 0) __builtin_amdgcn_s_setprio(0);
     s0 = xor3(perm(a0, a1, 0x0c0c0501u), perm(a2, a3, 0x07020c0cu), rk[0]);
     s1 = xor3(perm(b0, b1, 0x0c0c0501u), perm(b2, b3, 0x07020c0cu), rk[1]);
     s2 = xor3(perm(c0, c1, 0x0c0c0501u), perm(c2, c3, 0x07020c0cu), rk[2]);
@@ -289,17 +309,20 @@ template <int kLo, int kHi>
 __device__ __forceinline__ void g5_chunk(const uint32_t (&y)[4], uint32_t mf8, uint32_t &a0, uint32_t &a1,
                                          uint32_t &a2, uint32_t &a3) {
     if constexpr (kLo < kHi) {
+        if constexpr (QGCM_GH_PRIO > 0) __builtin_amdgcn_s_setprio(QGCM_GH_PRIO);
         const uint32_t x = g5_addr<kLo>(y, mf8);
         const u32x2 h0 = lds64(x + kLo * 512u), h1 = lds64(x + kLo * 512u + 256u);
         if constexpr (kLo + 1 < kHi) {
             const uint32_t x2 = g5_addr<kLo + 1>(y, mf8);
             const u32x2 l0 = lds64(x2 + (kLo + 1) * 512u), l1 = lds64(x2 + (kLo + 1) * 512u + 256u);
+            if constexpr (QGCM_GH_PRIO > 0) __builtin_amdgcn_s_setprio(0);
             a0 = xor3(a0, h0.x, l0.x);
             a1 = xor3(a1, h0.y, l0.y);
             a2 = xor3(a2, h1.x, l1.x);
             a3 = xor3(a3, h1.y, l1.y);
             g5_chunk<kLo + 2, kHi>(y, mf8, a0, a1, a2, a3);
         } else {
+            if constexpr (QGCM_GH_PRIO > 0) __builtin_amdgcn_s_setprio(0);
             a0 ^= h0.x;
             a1 ^= h0.y;
             a2 ^= h1.x;
