@@ -175,11 +175,16 @@ int qgcm_group_set_keys(qgcm_group *g, uint32_t first_idx, uint32_t count, const
  * descriptor batch, copies back and writes the results into the same slots (input order kept).
  * h_nonces: n * 12 B (seal; NULL = nonce already in the slot).  h_status[i] (may be NULL): 1 ok, 0 failed
  * (as qgcm_seal_batch / qgcm_open_batch).  Returns the number of failed packets or a negative error.
- * One call at a time per group (calls are serialized). */
+ * One call at a time per group (calls are serialized).  When h_arena (and h_nonces) is pinned host memory
+ * (qgcm_host_alloc, hipHostMalloc, hipHostRegister) holding every record, the members' GPUs gather and
+ * scatter the records themselves over PCIe (zero-copy); otherwise host threads copy them through pinned
+ * staging (QGCM_GROUP_THREADS per member).  QGCM_GROUP_ZEROCOPY=0 forces the copy path. */
 int qgcm_group_seal_host(qgcm_group *g, uint8_t *h_arena, const qgcm_desc *h_descs, uint32_t n,
                          const uint8_t *h_nonces, uint32_t aad_len, uint8_t *h_status);
 int qgcm_group_open_host(qgcm_group *g, uint8_t *h_arena, const qgcm_desc *h_descs, uint32_t n, uint32_t aad_len,
                          uint8_t *h_status);
+/* 1 if the last qgcm_group_seal_host / open_host call took the zero-copy path, else 0. */
+int qgcm_group_last_zerocopy(const qgcm_group *g);
 
 /* Pinned (page-locked) host memory for arenas handed to the *_host calls; NULL on failure. */
 void *qgcm_host_alloc(size_t bytes);

@@ -30,6 +30,7 @@ EXPORTS = (
     "qgcm_tun_open", "qgcm_tun_up", "qgcm_tun_read_slots", "qgcm_tun_write_slots", "qgcm_tun_close",
     "qgcm_group_create", "qgcm_group_destroy", "qgcm_group_size", "qgcm_group_ctx", "qgcm_group_shard",
     "qgcm_group_set_keys", "qgcm_group_seal_host", "qgcm_group_open_host", "qgcm_group_member_cpus",
+    "qgcm_group_last_zerocopy",
 )
 
 QGCM_OK = 0
@@ -129,6 +130,8 @@ def _bind(L: C.CDLL) -> None:
         L.qgcm_group_open_host.argtypes = [vp, vp, vp, u32, u32, vp]
         if hasattr(L, "qgcm_group_member_cpus"):
             L.qgcm_group_member_cpus.argtypes = [vp, i32]
+        if hasattr(L, "qgcm_group_last_zerocopy"):
+            L.qgcm_group_last_zerocopy.argtypes = [vp]
     if hasattr(L, "qgcm_tun_open"):  # (older builds loaded by the A/B tools lack the TUN calls)
         L.qgcm_tun_open.argtypes = [C.c_char_p, C.c_int, vp, C.c_char_p, sz]
         L.qgcm_tun_up.argtypes = [C.c_char_p, C.c_char_p, C.c_int, C.c_int]

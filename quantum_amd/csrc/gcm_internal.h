@@ -75,6 +75,16 @@ int run_one_descs(qgcm_ctx *ctx, bool seal, uint8_t *arena, const qgcm_desc *des
                   const uint8_t *nonces, uint32_t aad_len, uint8_t *status, hipStream_t s);
 bool ctx_one_kernel(const qgcm_ctx *ctx);
 hipError_t launch_stream_copy(void *dst, const void *src, uint64_t bytes, int num_cus, hipStream_t s);
+// one record move of the group dispatcher's zero-copy path: src/dst device-accessible addresses
+// (pinned host or device), 4-B aligned; status_idx: the record's status byte (scatter only)
+struct RecMove {
+    uint64_t src, dst;
+    uint32_t bytes, status_idx;
+};
+// exact = false (gather): whole dwords, the last may extend past `bytes`; exact = true (scatter):
+// exactly `bytes`, and only moves whose status byte is 1 when d_status is given
+hipError_t launch_move_records(const RecMove *d_moves, uint32_t n, const uint8_t *d_status, bool exact, int num_cus,
+                               hipStream_t s);
 // context accessors for the coalescer (coalescer.cpp), defined in qgcm_api.cpp
 int ctx_device(const qgcm_ctx *ctx);
 bool ctx_key_ready(qgcm_ctx *ctx, uint32_t key_idx);

@@ -1914,6 +1914,45 @@ __global__ void __launch_bounds__(256) stream_copy_kernel(uint4 *__restrict__ ds
     for (; i < n16; i += step) dst[i] = src[i];
 }
 
+// Record moves for the group dispatcher's zero-copy path (group.cpp): one wave per record copies
+// `bytes` from src to dst (both 4-B aligned) with 16-B accesses, the rest by dwords.  Gather (pinned host -> device
+// staging): the last dword may read up to 3 bytes past the record, never past a 4-B boundary, so
+// never past the host allocation; the staging records are 16-B padded.  Scatter (staging -> pinned
+// host): whole dwords, then the 0-3 tail bytes one by one, so nothing beyond the record is written;
+// a move whose status byte is not 1 is skipped when `status` is given (a failed seal leaves the
+// caller's slot untouched).
+__global__ void __launch_bounds__(256) move_records_kernel(const RecMove *__restrict__ mv, uint32_t n,
+                                                           const uint8_t *__restrict__ status, bool exact) {
+    const uint32_t lane = threadIdx.x & 63u;
+    for (uint32_t r = blockIdx.x * 4u + (threadIdx.x >> 6); r < n; r += gridDim.x * 4u) {
+        const RecMove m = mv[r];
+        if (status && status[m.status_idx] != 1) continue;
+        // 16-B accesses (4-B alignment suffices) for the whole 16-B pieces inside the record, then dwords
+        const W4 *src16 = reinterpret_cast<const W4 *>(m.src);
+        W4 *dst16 = reinterpret_cast<W4 *>(m.dst);
+        const uint32_t n16 = m.bytes >> 4;
+        for (uint32_t i = lane; i < n16; i += 64) dst16[i] = src16[i];
+        const uint32_t *src = reinterpret_cast<const uint32_t *>(m.src);
+        uint32_t *dst = reinterpret_cast<uint32_t *>(m.dst);
+        const uint32_t nd = exact ? m.bytes >> 2 : (m.bytes + 3) >> 2;
+        if (lane < nd - 4 * n16) dst[4 * n16 + lane] = src[4 * n16 + lane];
+        if (exact && lane < (m.bytes & 3u)) {
+            const uint32_t b = (m.bytes & ~3u) + lane;
+            reinterpret_cast<uint8_t *>(m.dst)[b] = reinterpret_cast<const uint8_t *>(m.src)[b];
+        }
+    }
+}
+
+hipError_t launch_move_records(const RecMove *d_moves, uint32_t n, const uint8_t *d_status, bool exact, int num_cus,
+                               hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    // 8 waves per CU: PCIe-bound, and room for the other stream's kernels to run alongside
+    const uint32_t blocks = (n + 3) / 4, cap = (uint32_t)num_cus * 2u;
+    hipLaunchKernelGGL(move_records_kernel, dim3(blocks < cap ? blocks : cap), dim3(256), 0, s, d_moves, n, d_status,
+                       exact);
+    return hipGetLastError();
+}
+
 hipError_t launch_stream_copy(void *dst, const void *src, uint64_t bytes, int num_cus, hipStream_t s) {
     const uint64_t n16 = bytes / 16;
     if (n16 == 0) return hipSuccess;

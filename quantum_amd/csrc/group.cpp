@@ -27,6 +27,13 @@
 // 2^20 x 1350 B on one member, against 41 for qgcm_seal_host's contiguous pipeline).  Each member
 // therefore has a pool of copy threads (QGCM_GROUP_THREADS per member, default 4, the member thread
 // included, pinned like it) that split every chunk's gather and scatter by record.
+//
+// Zero-copy path: when the caller's arena (and nonce array) is pinned, device-accessible host memory
+// (qgcm_host_alloc / hipHostMalloc / hipHostRegister) and every record lies inside that allocation,
+// the member's GPU gathers the records itself (move_records_kernel: one wave per record, reads over
+// PCIe into device staging), runs the descriptor batch there and scatters the results back into the
+// slots -- the host only builds the per-record move lists (24 B per record).  QGCM_GROUP_ZEROCOPY=0
+// forces the CPU path.
 #include <hip/hip_runtime.h>
 #include <pthread.h>
 #include <ctype.h>
@@ -47,7 +54,9 @@
 
 namespace {
 
-constexpr uint64_t kChunk = 32ull << 20;  // staged slot bytes per chunk
+constexpr uint64_t kChunk = 32ull << 20;    // staged slot bytes per chunk, copy path (pinned staging)
+constexpr uint64_t kZcChunk = 256ull << 20; // zero-copy path (device staging): enough wave tiles per
+                                            // chunk to fill the GPU (a 32-MB chunk is ~1500 tiles)
 constexpr int kSlots = 2;                 // staging slots per member (double buffer)
 constexpr int kCopyThreads = 4;           // gather/scatter threads per member (QGCM_GROUP_THREADS)
 
@@ -127,10 +136,23 @@ class CopyPool {
     bool stop_ = false;
 };
 
+// zero-copy path state of a member (grow-only): host move lists / staging descriptors (pinned), their
+// device copies, device staging and the batch's status bytes
+struct ZC {
+    qgcm::RecMove *h_moves = nullptr, *d_moves = nullptr;  // [gather: m records + m nonces][scatter: m]
+    qgcm_desc *h_descs = nullptr, *d_descs = nullptr;
+    uint8_t *d_stage[kSlots] = {nullptr, nullptr};  // records then nonces, per slot
+    uint8_t *d_status = nullptr, *h_status = nullptr;
+    size_t cap = 0;         // records the lists are sized for
+    uint64_t stage_cap = 0;  // bytes per staging slot
+};
+
 struct Member {
     qgcm_ctx *ctx = nullptr;
     int device = 0;
+    int num_cus = 0;
     Stage st[kSlots];
+    ZC zc;
     cpu_set_t cpus;  // the GPU's local CPUs allowed to this process (empty: the thread is not pinned)
     int ncpus = 0;
     std::unique_ptr<CopyPool> pool;  // gather/scatter threads (created with the member)
@@ -192,6 +214,8 @@ inline uint64_t rec_bytes(bool seal, uint32_t len) {  // AAD word + packet (+ ta
 struct qgcm_group {
     std::vector<Member> m;
     uint32_t max_keys = 0;
+    bool zerocopy = true;  // QGCM_GROUP_ZEROCOPY=0: always gather/scatter on the CPU
+    int last_zc = 0;       // the last call took the zero-copy path (qgcm_group_last_zerocopy)
     std::mutex call_mu;  // one batch call at a time (members' staging is reused per call)
 };
 
@@ -318,6 +342,138 @@ int run_member(Member &mb, bool seal, uint8_t *h_arena, const qgcm_desc *descs, 
     return rc;
 }
 
+uint64_t g_zc_chunk = kZcChunk;  // QGCM_GROUP_ZC_CHUNK_MB (tuning)
+
+template <typename T>
+bool grow_pinned(T *&h, T *&d, size_t count) {
+    if (h) hipHostFree(h);
+    if (d) hipFree(d);
+    h = nullptr;
+    d = nullptr;
+    return hipHostMalloc(reinterpret_cast<void **>(&h), sizeof(T) * count, hipHostMallocDefault) == hipSuccess &&
+           hipMalloc(reinterpret_cast<void **>(&d), sizeof(T) * count) == hipSuccess;
+}
+
+// Device-accessible address of pinned host memory [p, p + bytes) inside one allocation, or 0.
+uint64_t pinned_view(const void *p, uint64_t bytes) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess || a.type != hipMemoryTypeHost || !a.devicePointer) {
+        (void)hipGetLastError();  // pageable memory reports an error: clear it
+        return 0;
+    }
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    if (hipMemGetAddressRange(&base, &size, a.devicePointer) != hipSuccess || !base) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    const uint64_t dv = reinterpret_cast<uint64_t>(a.devicePointer), b = reinterpret_cast<uint64_t>(base);
+    return dv >= b && dv + bytes <= b + size ? dv : 0;
+}
+
+int run_member_zc(Member &mb, bool seal, uint64_t v_arena, const qgcm_desc *descs, const uint32_t *idx, size_t m,
+                  uint64_t v_nonces, uint32_t aad_len, uint8_t *h_status, int *bad_out) {
+    if (mb.ncpus > 0) pthread_setaffinity_np(pthread_self(), sizeof(mb.cpus), &mb.cpus);
+    if (hipSetDevice(mb.device) != hipSuccess) return QGCM_E_HIP;
+    ZC &z = mb.zc;
+    for (Stage &s : mb.st)
+        if (!s.s && hipStreamCreateWithFlags(&s.s, hipStreamNonBlocking) != hipSuccess) return QGCM_E_HIP;
+    if (m > z.cap) {
+        const size_t cap = std::max<size_t>(m, 4096);
+        if (!grow_pinned(z.h_moves, z.d_moves, 3 * cap) || !grow_pinned(z.h_descs, z.d_descs, cap) ||
+            !grow_pinned(z.h_status, z.d_status, cap))
+            return QGCM_E_NOMEM;
+        z.cap = cap;
+    }
+    // staging slot: a chunk's records (up to `chunk` bytes, or one larger record) + 256-B pad + their nonces
+    const uint64_t chunk = g_zc_chunk;
+    uint64_t need = chunk;
+    for (size_t j = 0; j < m; ++j) need = std::max<uint64_t>(need, rec_bytes(seal, descs[idx[j]].len));
+    need += 256 + 12ull * (chunk / 32 + 1);  // records are >= 32 B: at most chunk / 32 + 1 per chunk
+    if (need > z.stage_cap) {
+        for (auto &st : z.d_stage) {
+            if (st) hipFree(st);
+            st = nullptr;
+        }
+        z.stage_cap = 0;
+        for (auto &st : z.d_stage)
+            if (hipMalloc(&st, need) != hipSuccess) return QGCM_E_NOMEM;
+        z.stage_cap = need;
+    }
+    qgcm::RecMove *gm = z.h_moves, *nm = z.h_moves + m, *sm = z.h_moves + 2 * m;
+    int rc = QGCM_OK;
+    size_t next = 0;
+    for (int c = 0; next < m && rc == QGCM_OK; ++c) {
+        const int k = c % kSlots;
+        hipStream_t s = mb.st[k].s;
+        uint8_t *stage = z.d_stage[k];
+        size_t end = next;
+        uint64_t bytes = 0;
+        while (end < m) {
+            const uint64_t r = rec_bytes(seal, descs[idx[end]].len);
+            if (end > next && bytes + r > chunk) break;
+            bytes += r;
+            ++end;
+        }
+        const size_t cn = end - next;
+        const uint64_t non_off = (bytes + 255) & ~255ull;
+        const bool with_nonces = seal && v_nonces;
+        uint64_t pos = 0;
+        for (size_t j = next; j < end; ++j) {
+            const qgcm_desc &d = descs[idx[j]];
+            const uint64_t in = 4ull + d.len + (seal ? QGCM_OVERHEAD : 0);
+            const uint64_t dst = reinterpret_cast<uint64_t>(stage) + pos;
+            gm[j] = qgcm::RecMove{v_arena + d.offset, dst, (uint32_t)in, 0};
+            if (with_nonces)
+                nm[j] = qgcm::RecMove{v_nonces + 12ull * idx[j],
+                                      reinterpret_cast<uint64_t>(stage) + non_off + 12ull * (j - next), 12u, 0};
+            const uint32_t out = seal ? d.len + QGCM_OVERHEAD : d.len - QGCM_OVERHEAD;
+            sm[j] = qgcm::RecMove{dst + 4, v_arena + d.offset + 4, out, (uint32_t)(j - next)};
+            z.h_descs[j] = qgcm_desc{pos, d.len, d.key_idx};
+            pos += rec_bytes(seal, d.len);
+        }
+        // this chunk's lists -> device (stream-ordered before the kernels that read them)
+        const size_t a = next;
+        if (hipMemcpyAsync(z.d_moves + a, gm + a, sizeof(qgcm::RecMove) * cn, hipMemcpyHostToDevice, s) != hipSuccess ||
+            (with_nonces &&
+             hipMemcpyAsync(z.d_moves + m + a, nm + a, sizeof(qgcm::RecMove) * cn, hipMemcpyHostToDevice, s) !=
+                 hipSuccess) ||
+            hipMemcpyAsync(z.d_moves + 2 * m + a, sm + a, sizeof(qgcm::RecMove) * cn, hipMemcpyHostToDevice, s) !=
+                hipSuccess ||
+            hipMemcpyAsync(z.d_descs + a, z.h_descs + a, sizeof(qgcm_desc) * cn, hipMemcpyHostToDevice, s) != hipSuccess) {
+            rc = QGCM_E_HIP;
+            break;
+        }
+        if (qgcm::launch_move_records(z.d_moves + a, (uint32_t)cn, nullptr, false, mb.num_cus, s) != hipSuccess ||
+            (with_nonces &&
+             qgcm::launch_move_records(z.d_moves + m + a, (uint32_t)cn, nullptr, false, mb.num_cus, s) != hipSuccess)) {
+            rc = QGCM_E_HIP;
+            break;
+        }
+        rc = seal ? qgcm_seal_batch(mb.ctx, stage, z.d_descs + a, (uint32_t)cn, with_nonces ? stage + non_off : nullptr,
+                                    aad_len, z.d_status + a, s)
+                  : qgcm_open_batch(mb.ctx, stage, z.d_descs + a, (uint32_t)cn, aad_len, z.d_status + a, s);
+        if (rc != QGCM_OK) break;
+        // scatter: a failed seal leaves the slot untouched; open writes plaintext or zeros
+        if (qgcm::launch_move_records(z.d_moves + 2 * m + a, (uint32_t)cn, seal ? z.d_status + a : nullptr, true,
+                                      mb.num_cus, s) != hipSuccess ||
+            hipMemcpyAsync(z.h_status + a, z.d_status + a, cn, hipMemcpyDeviceToHost, s) != hipSuccess) {
+            rc = QGCM_E_HIP;
+            break;
+        }
+        next = end;
+    }
+    for (Stage &st : mb.st)
+        if (hipStreamSynchronize(st.s) != hipSuccess && rc == QGCM_OK) rc = QGCM_E_HIP;
+    int bad = 0;
+    for (size_t j = 0; j < next; ++j) {
+        bad += z.h_status[j] != 1;
+        if (h_status) h_status[idx[j]] = z.h_status[j];
+    }
+    *bad_out = bad;
+    return rc;
+}
+
 int run_group(qgcm_group *g, bool seal, uint8_t *h_arena, const qgcm_desc *descs, uint32_t n,
               const uint8_t *h_nonces, uint32_t aad_len, uint8_t *h_status) {
     if (!g || (n && (!h_arena || !descs)) || aad_len > 4 || n > QGCM_MAX_BATCH) return QGCM_E_ARG;
@@ -337,13 +493,26 @@ int run_group(qgcm_group *g, bool seal, uint8_t *h_arena, const qgcm_desc *descs
         }
         part[qgcm_group_shard(g, d.key_idx)].push_back(i);
     }
+    // zero-copy when the arena (and nonces) are pinned and hold every record
+    uint64_t v_arena = 0, v_nonces = 0;
+    if (g->zerocopy) {
+        uint64_t extent = 0;
+        for (uint32_t i = 0; i < n; ++i)
+            extent = std::max<uint64_t>(extent, descs[i].offset + 4ull + descs[i].len + (seal ? QGCM_OVERHEAD : 0));
+        v_arena = pinned_view(h_arena, extent);
+        if (v_arena && seal && h_nonces && !(v_nonces = pinned_view(h_nonces, 12ull * n))) v_arena = 0;
+        if ((v_arena | v_nonces) & 3) v_arena = 0;  // the record moves are dword-wise
+    }
+    g->last_zc = v_arena ? 1 : 0;
     std::vector<int> rc(G, QGCM_OK), bad(G, 0);
     std::vector<std::thread> thr;
     for (int k = 0; k < G; ++k) {
         if (part[k].empty()) continue;
         thr.emplace_back([&, k] {
-            rc[k] = run_member(g->m[k], seal, h_arena, descs, part[k].data(), part[k].size(), h_nonces, aad_len,
-                               h_status, &bad[k]);
+            rc[k] = v_arena ? run_member_zc(g->m[k], seal, v_arena, descs, part[k].data(), part[k].size(), v_nonces,
+                                            aad_len, h_status, &bad[k])
+                            : run_member(g->m[k], seal, h_arena, descs, part[k].data(), part[k].size(), h_nonces,
+                                         aad_len, h_status, &bad[k]);
         });
     }
     for (auto &t : thr) t.join();
@@ -368,10 +537,13 @@ qgcm_group *qgcm_group_create(const int *devices, int count, uint32_t max_keys, 
     g->max_keys = max_keys;
     int threads = kCopyThreads;
     if (const char *v = getenv("QGCM_GROUP_THREADS")) threads = std::max(1, std::min(64, atoi(v)));
+    if (const char *v = getenv("QGCM_GROUP_ZEROCOPY")) g->zerocopy = atoi(v) != 0;
+    if (const char *v = getenv("QGCM_GROUP_ZC_CHUNK_MB")) g_zc_chunk = (uint64_t)std::max(1, atoi(v)) << 20;
     for (int k = 0; k < count; ++k) {
         Member mb;
         mb.device = devices[k];
         mb.ncpus = gpu_local_cpus(devices[k], &mb.cpus);
+        hipDeviceGetAttribute(&mb.num_cus, hipDeviceAttributeMultiprocessorCount, devices[k]);
         mb.ctx = qgcm_create(devices[k], max_keys, err, errlen);
         if (mb.ctx) mb.pool = std::make_unique<CopyPool>(threads, mb.cpus, mb.ncpus);
         if (!mb.ctx) {
@@ -395,12 +567,22 @@ void qgcm_group_destroy(qgcm_group *g) {
             if (s.h) hipHostFree(s.h);
             if (s.d) hipFree(s.d);
         }
+        ZC &z = mb.zc;
+        if (z.h_moves) hipHostFree(z.h_moves);
+        if (z.h_descs) hipHostFree(z.h_descs);
+        if (z.h_status) hipHostFree(z.h_status);
+        hipFree(z.d_moves);
+        hipFree(z.d_descs);
+        hipFree(z.d_status);
+        for (uint8_t *st : z.d_stage) hipFree(st);
         qgcm_destroy(mb.ctx);
     }
     delete g;
 }
 
 int qgcm_group_size(const qgcm_group *g) { return g ? (int)g->m.size() : 0; }
+
+int qgcm_group_last_zerocopy(const qgcm_group *g) { return g ? g->last_zc : QGCM_E_ARG; }
 
 int qgcm_group_member_cpus(const qgcm_group *g, int member) {
     return g && member >= 0 && member < (int)g->m.size() ? g->m[member].ncpus : QGCM_E_ARG;

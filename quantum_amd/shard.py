@@ -90,6 +90,12 @@ class Group:
 
         return _lib.check(_lib.lib().qgcm_group_member_cpus(self.handle, m), "qgcm_group_member_cpus")
 
+    def last_zerocopy(self) -> bool:
+        """True if the last seal_host / open_host call ran the zero-copy path (pinned arena)."""
+        from . import _lib
+
+        return _lib.check(_lib.lib().qgcm_group_last_zerocopy(self.handle), "qgcm_group_last_zerocopy") == 1
+
     def set_keys(self, first: int, keys: bytes) -> None:
         from . import _lib
 

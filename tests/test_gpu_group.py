@@ -45,12 +45,15 @@ def host_buffer(nbytes: int, pinned: bool):
     return arr, arr.ctypes.data, lambda: None
 
 
-@pytest.mark.parametrize("G,pinned,threads", [(2, True, "4"), (3, False, "7"), (1, True, "1")])
-def test_group_keyed_host_batch_vs_oracle(torch, G, pinned, threads, monkeypatch):
-    """threads: QGCM_GROUP_THREADS, the gather/scatter copy threads per member (read at creation)."""
+@pytest.mark.parametrize("G,pinned,threads,zc", [(2, True, "4", "1"), (3, False, "7", "1"), (1, True, "1", "1"),
+                                                  (2, True, "3", "0")])
+def test_group_keyed_host_batch_vs_oracle(torch, G, pinned, threads, zc, monkeypatch):
+    """threads: QGCM_GROUP_THREADS, the gather/scatter copy threads per member; zc: QGCM_GROUP_ZEROCOPY
+    (pinned arenas take the GPU gather/scatter path unless it is 0; pageable ones always the copy path)."""
     from quantum_amd import shard
 
     monkeypatch.setenv("QGCM_GROUP_THREADS", threads)
+    monkeypatch.setenv("QGCM_GROUP_ZEROCOPY", zc)
     grp = shard.Group([0] * G, max_keys=256)
     try:
         rng = random.Random(0x6A0 + G)
@@ -73,7 +76,8 @@ def test_group_keyed_host_batch_vs_oracle(torch, G, pinned, threads, monkeypatch
             for i in range(n):
                 arena[offs[i]:offs[i] + 4] = np.frombuffer(AAD, dtype=np.uint8)
             plain = arena.copy()
-            nonces = np.frombuffer(rng.randbytes(12 * n), dtype=np.uint8).copy()
+            nonces, _, free_n = host_buffer(12 * n, pinned)  # pinned nonces keep the seal zero-copy too
+            nonces[:] = np.frombuffer(rng.randbytes(12 * n), dtype=np.uint8)
             ref = plain.copy()
             for i, L in enumerate(lens):
                 if kidx[i] >= nkeys:
@@ -85,6 +89,7 @@ def test_group_keyed_host_batch_vs_oracle(torch, G, pinned, threads, monkeypatch
             status = np.full(n, 7, dtype=np.uint8)
             unset = sum(k >= nkeys for k in kidx)
             bad = grp.seal_host(aptr, descs, n, nonces.ctypes.data, 4, status.ctypes.data)
+            assert grp.last_zerocopy() == (pinned and zc == "1")
             assert bad == unset
             assert status.tolist() == [0 if k >= nkeys else 1 for k in kidx]
             assert np.array_equal(arena, ref)  # every slot in place, input order kept
@@ -96,6 +101,7 @@ def test_group_keyed_host_batch_vs_oracle(torch, G, pinned, threads, monkeypatch
             d_open = shard.host_descs(offs, [L + 28 for L in lens], kidx)
             status[:] = 7
             bad = grp.open_host(aptr, d_open, n, 4, status.ctypes.data)
+            assert grp.last_zerocopy() == (pinned and zc == "1")
             assert bad == unset + len(tampered)
             for i, L in enumerate(lens):
                 o = offs[i]
@@ -106,6 +112,8 @@ def test_group_keyed_host_batch_vs_oracle(torch, G, pinned, threads, monkeypatch
                     assert np.array_equal(arena[o + 4 + L:o + 4 + L + 28], before[o + 4 + L:o + 4 + L + 28])
                 else:
                     assert status[i] == 1 and np.array_equal(arena[o:o + 4 + L], plain[o:o + 4 + L])
+            del nonces
+            free_n()
         finally:
             free()
     finally:

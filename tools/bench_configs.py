@@ -279,13 +279,15 @@ def group_e2e(G: int = 1, reps: int = 3) -> dict:
         to.append(t2 - t1)
     s, o = float(np.median(ts)), float(np.median(to))
     cpus = [grp.member_cpus(m) for m in range(G)]
+    zc = grp.last_zerocopy()
     grp.close()
     del host, nonces
     L_.qgcm_host_free(a_ptr)
     L_.qgcm_host_free(n_ptr)
     return {"config": "group_e2e_keyed_host", "members": G, "devices": [0] * G, "packets": N, "payload_len": L,
             "keys": NK, "value": round(2 * N * L / (s + o) / 2**30, 2), "unit": "GiB/s", "seal_s": round(s, 4),
-            "open_s": round(o, 4), "member_cpus": cpus, "status_ok": ok and bad == 0}
+            "open_s": round(o, 4), "member_cpus": cpus, "zerocopy": zc,
+            "copy_threads": int(os.environ.get("QGCM_GROUP_THREADS", "4")), "status_ok": ok and bad == 0}
 
 
 if __name__ == "__main__":
