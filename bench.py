@@ -44,12 +44,12 @@ AAD = bytes([10, 99, 0, 1])
 def parse() -> argparse.Namespace:
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=100)  # ~0.35 s timed: the clocks ramp for ~70 ms after an idle gap
+    p.add_argument("--steps", type=int, default=500)  # ~1.7 s timed (the clocks ramp for ~70 ms after an idle gap)
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--workload", choices=["auto", "config2", "config4"], default="auto",
                    help="auto: config2 at 1 GPU, config4 (64 M packets sharded) at more")
     p.add_argument("--packets", type=int, default=0, help="packets per GPU (overrides the workload's)")
-    p.add_argument("--settle-ms", type=float, default=300.0, help="clock settle before warmup (0 = none)")
+    p.add_argument("--settle-ms", type=float, default=500.0, help="clock settle before warmup (0 = none)")
     p.add_argument("--len", type=int, default=1350, help="payload bytes per packet")
     p.add_argument("--stride", type=int, default=0, help="slot stride (0 = smallest 64-B multiple)")
     p.add_argument("--no-cpu-baseline", action="store_true")
