@@ -81,6 +81,7 @@ struct Lane {
     CBatch b[kDepth];
     int fill = 0;  // index of the batch callers reserve in
     hipStream_t stream = nullptr;
+    uint8_t *done = nullptr;  // pinned, one byte per packet: set by its workgroup (latency-kernel flushes)
     std::thread thr;
 };
 
@@ -144,8 +145,21 @@ void flusher(qgcm_coalescer *c, Lane *ln) {
         if (rc == QGCM_OK && one) {
             // small batch: one latency-kernel workgroup per packet, zero-copy on the pinned batch
             // (one launch instead of H2D copies + worklist build + batch kernel + D2H copies)
+            memset(ln->done, 0, n);
             rc = qgcm::run_one_descs(c->ctx, ln->seal, B.h_arena, B.h_descs, n, ln->seal ? B.h_nonces : nullptr,
-                                     c->aad_len, B.h_status, s);
+                                     c->aad_len, B.h_status, s, ln->done);
+            // completion by the workgroups' flags (each set after a system-scope fence behind its slot
+            // and status), not by a stream synchronization; the stream is the fallback after 1 s (it
+            // also reports faults)
+            const auto t0 = Clock::now();
+            for (uint32_t i = 0, spins = 0; rc == QGCM_OK && i < n; ++spins) {
+                if (__atomic_load_n(ln->done + i, __ATOMIC_ACQUIRE)) {
+                    ++i;
+                    continue;
+                }
+                __builtin_ia32_pause();
+                if ((spins & 1023) == 1023 && Clock::now() - t0 > std::chrono::seconds(1)) break;
+            }
         } else if (rc == QGCM_OK) {
             if (hipMemcpyAsync(B.d_arena, B.h_arena, used, hipMemcpyHostToDevice, s) != hipSuccess ||
                 hipMemcpyAsync(B.d_descs, B.h_descs, sizeof(qgcm_desc) * n, hipMemcpyHostToDevice, s) != hipSuccess ||
@@ -159,7 +173,9 @@ void flusher(qgcm_coalescer *c, Lane *ln) {
                  hipMemcpyAsync(B.h_status, B.d_status, n, hipMemcpyDeviceToHost, s) != hipSuccess))
                 rc = QGCM_E_HIP;
         }
-        if (hipStreamSynchronize(s) != hipSuccess) rc = QGCM_E_HIP;
+        bool landed = one && rc == QGCM_OK;
+        for (uint32_t i = 0; landed && i < n; ++i) landed = __atomic_load_n(ln->done + i, __ATOMIC_ACQUIRE) != 0;
+        if (!landed && hipStreamSynchronize(s) != hipSuccess) rc = QGCM_E_HIP;
 
         lk.lock();
         B.rc = rc;
@@ -251,6 +267,7 @@ void free_lane(Lane &ln) {
         hipFree(B.d_status);
     }
     if (ln.stream) hipStreamDestroy(ln.stream);
+    if (ln.done) hipHostFree(ln.done);
 }
 
 void set_err(char *err, size_t errlen, const char *msg) {
@@ -284,7 +301,8 @@ qgcm_coalescer *qgcm_coalescer_create(qgcm_ctx *ctx, uint32_t max_batch, uint32_
     for (int d = 0; d < 2 && ok; ++d) {
         Lane &ln = c->lanes[d];
         ln.seal = d == 0;
-        ok = hipStreamCreateWithFlags(&ln.stream, hipStreamNonBlocking) == hipSuccess;
+        ok = hipStreamCreateWithFlags(&ln.stream, hipStreamNonBlocking) == hipSuccess &&
+             hipHostMalloc(reinterpret_cast<void **>(&ln.done), qgcm::kOneBatchMax, hipHostMallocDefault) == hipSuccess;
         for (CBatch &B : ln.b) {
             ok = ok && hipHostMalloc(&B.h_arena, c->cap_bytes, hipHostMallocDefault) == hipSuccess &&
                  hipHostMalloc(&B.h_descs, sizeof(qgcm_desc) * max_batch, hipHostMallocDefault) == hipSuccess &&

@@ -41,7 +41,8 @@ struct Batch {
     uint32_t aad_len;           // 0 or 4
     uint32_t max_keys;
     uint32_t *tile_counter;     // descriptor quad kernels: dynamic tile index (zeroed per launch)
-    uint8_t *done;              // gcm_one_kernel, uniform form: set to 1 after the slot is written
+    uint8_t *done;              // gcm_one_kernel: done[0] (uniform form, one packet) or done[pkt] (descriptor
+                                // form) set to 1 after the slot is written
                                 // back and made system-visible (the host polls it instead of the stream)
 };
 
@@ -72,7 +73,8 @@ constexpr uint32_t kOneUniformMax = 2048;
 constexpr uint32_t kLaunchChunk = 1u << 19;  // packets per quad-kernel launch of a uniform batch
 constexpr uint32_t kDescChunk = 0;           // packets per sorted chunk of a descriptor batch (0 = all)  // measured cross-over with the quad kernel: 2048-4096 packets
 int run_one_descs(qgcm_ctx *ctx, bool seal, uint8_t *arena, const qgcm_desc *descs, uint32_t n,
-                  const uint8_t *nonces, uint32_t aad_len, uint8_t *status, hipStream_t s);
+                  const uint8_t *nonces, uint32_t aad_len, uint8_t *status, hipStream_t s,
+                  uint8_t *done = nullptr);
 bool ctx_one_kernel(const qgcm_ctx *ctx);
 hipError_t launch_stream_copy(void *dst, const void *src, uint64_t bytes, int num_cus, hipStream_t s);
 // one record move of the group dispatcher's zero-copy path: src/dst device-accessible addresses

@@ -1334,7 +1334,13 @@ __global__ void __launch_bounds__(kOneThreads) gcm_one_kernel(Batch b, const uin
     // (slot untouched); so does a slot past the LDS staging area or misaligned (the host never sends one)
     if (key >= b.max_keys || !b.key_valid[key] || (!kSeal && Lin < (uint32_t)QGCM_OVERHEAD) || Lin >= kOneCap ||
         n16 * 16u > kOneCap - 16u || (off & 15u)) {
-        if (tid == 0 && b.status) b.status[pkt] = 0;
+        if (tid == 0) {
+            if (b.status) b.status[pkt] = 0;
+            if (b.done) {  // the host waits on every packet's flag
+                __threadfence_system();
+                *reinterpret_cast<volatile uint8_t *>(b.done + (b.descs ? pkt : 0u)) = 1;
+            }
+        }
         return;
     }
     const uint32_t L = kSeal ? Lin : Lin - QGCM_OVERHEAD;
@@ -1545,7 +1551,7 @@ __global__ void __launch_bounds__(kOneThreads) gcm_one_kernel(Batch b, const uin
         __syncthreads();
         if (tid == 0) {
             __threadfence_system();
-            *reinterpret_cast<volatile uint8_t *>(b.done) = 1;
+            *reinterpret_cast<volatile uint8_t *>(b.done + (b.descs ? pkt : 0u)) = 1;
         }
     }
 }

@@ -215,7 +215,8 @@ int qgcm::ctx_device(const qgcm_ctx *ctx) { return ctx->device; }
 bool qgcm::ctx_one_kernel(const qgcm_ctx *ctx) { return ctx->one_kernel; }
 
 int qgcm::run_one_descs(qgcm_ctx *ctx, bool seal, uint8_t *arena, const qgcm_desc *descs, uint32_t n,
-                        const uint8_t *nonces, uint32_t aad_len, uint8_t *status, hipStream_t s) {
+                        const uint8_t *nonces, uint32_t aad_len, uint8_t *status, hipStream_t s,
+                        uint8_t *done) {
     if (!ctx || n == 0 || n > kOneBatchMax || !arena || !descs || aad_len > 4 || ((uintptr_t)arena & 15) ||
         (nonces && ((uintptr_t)nonces & 3)))
         return QGCM_E_ARG;
@@ -227,6 +228,7 @@ int qgcm::run_one_descs(qgcm_ctx *ctx, bool seal, uint8_t *arena, const qgcm_des
     b.status = status;
     b.n = n;
     b.aad_len = aad_len;
+    b.done = done;
     return hip_fail(launch_one(seal, b, s));
 }
 bool qgcm::ctx_key_ready(qgcm_ctx *ctx, uint32_t key_idx) { return key_ok(ctx, key_idx); }
