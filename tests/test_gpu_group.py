@@ -120,6 +120,49 @@ def test_group_keyed_host_batch_vs_oracle(torch, G, pinned, threads, zc, monkeyp
         grp.close()
 
 
+def test_group_zerocopy_records_at_the_allocation_end(torch):
+    """Zero-copy path: records whose last byte is the last bytes of a one-page pinned allocation, with
+    lengths that are not multiples of 4 or 16 (the gather reads whole dwords up to the next 4-B
+    boundary only, the scatter writes exact bytes); sealed and opened against the oracle."""
+    from quantum_amd import shard
+
+    grp = shard.Group([0], max_keys=4)
+    arena, aptr, free = host_buffer(4096, True)
+    nb, nptr, free_n = host_buffer(4096, True)
+    try:
+        key = bytes(range(32))
+        grp.set_keys(0, key)
+        rng = random.Random(0x0E7)
+        lens = [1, 1001, 2017]  # 4 + L + 28 = 33 / 1033 / 2049 B: the last record ends at byte 4093
+        offs = [0, 40]
+        offs.append(4093 - (4 + lens[2] + 28))
+        assert offs[2] % 4 == 0 and offs[1] + 4 + lens[1] + 28 <= offs[2]
+        arena[:] = np.frombuffer(rng.randbytes(4096), dtype=np.uint8)
+        for o in offs:
+            arena[o:o + 4] = np.frombuffer(AAD, dtype=np.uint8)
+        nb[:36] = np.frombuffer(rng.randbytes(36), dtype=np.uint8)
+        plain = arena.copy()
+        ref = plain.copy()
+        for i, L in enumerate(lens):
+            buf = bytearray(ref[offs[i] + 4:offs[i] + 4 + L + 28].tobytes())
+            O.aesgo_encrypt(key, buf, L, AAD, bytes(nb[12 * i:12 * i + 12]))
+            ref[offs[i] + 4:offs[i] + 4 + L + 28] = np.frombuffer(bytes(buf), dtype=np.uint8)
+        status = np.zeros(3, dtype=np.uint8)
+        assert grp.seal_host(aptr, shard.host_descs(offs, lens, [0, 0, 0]), 3, nptr, 4, status.ctypes.data) == 0
+        assert grp.last_zerocopy()
+        assert status.tolist() == [1, 1, 1] and np.array_equal(arena, ref)
+        assert grp.open_host(aptr, shard.host_descs(offs, [L + 28 for L in lens], [0, 0, 0]), 3, 4,
+                             status.ctypes.data) == 0
+        assert status.tolist() == [1, 1, 1]
+        for i, L in enumerate(lens):
+            assert np.array_equal(arena[offs[i]:offs[i] + 4 + L], plain[offs[i]:offs[i] + 4 + L])
+        assert np.array_equal(arena[4093:], plain[4093:])  # nothing written past the last record
+    finally:
+        free()
+        free_n()
+        grp.close()
+
+
 def test_group_members_hold_only_their_keys(torch):
     """A member's own context rejects a key another member owns (status 0, slot untouched)."""
     from quantum_amd import batch, shard
