@@ -41,12 +41,21 @@ struct Batch {
     uint32_t aad_len;           // 0 or 4
     uint32_t max_keys;
     uint32_t *tile_counter;     // descriptor quad kernels: dynamic tile index (zeroed per launch)
+    const uint32_t *tile_keys;  // descriptor quad kernels: key of each 16-entry tile (all ones: padding,
+                                // only after the last key run)
+    const uint64_t *tile_work;  // exclusive prefix sum of the tiles' work (n_items / 16 + 1 entries, the
+                                // last = total): where each workgroup of the segmented kernel starts
+    const uint2 *runs;          // segmented kernel: the key runs of the worklist (QuadWorklist)
+    uint32_t *run_next;
+    const uint32_t *nruns;
+    const uint32_t *tile_list;  // per-wave descriptor kernels: NULL = every tile of the worklist, else
+    const uint32_t *n_list;     // only these tiles (*n_list of them; the segmented kernel's short keys)
     uint8_t *done;              // gcm_one_kernel: done[0] (uniform form, one packet) or done[pkt] (descriptor
                                 // form) set to 1 after the slot is written
                                 // back and made system-visible (the host polls it instead of the stream)
 };
 
-constexpr int kNumVariants = 14;
+constexpr int kNumVariants = 15;
 constexpr int kVariantGeneral = 0;   // lane per packet, per-wave GHASH tables, any key mix
 constexpr int kVariantDescQuad = 7;  // default for descriptor batches: sorted quad tiles
 constexpr int kVariantUniform = 12;  // default for single-key (uniform) batches: quad kernel (Tab2F), 32 waves/CU
@@ -55,12 +64,26 @@ int variant_waves(int variant);
 bool variant_quad(int variant);
 int variant_wgs_per_cu(int variant);
 bool variant_desc(int variant);
+int variant_complement(int variant);  // kernel for the short keys of a segmented variant (-1: none)
 // sorted, 16-packet key-uniform worklist for the descriptor quad kernels (worklist.hip)
 size_t quad_worklist_bytes(uint32_t n, uint32_t max_keys, uint32_t *n_items_out);
+// Keys with fewer tiles than this are left to a per-wave kernel after the segmented kernel (one
+// 16-wave workgroup on a run of one or two tiles per wave would mostly wait at its barrier).
+constexpr uint32_t kSegMinTiles = 48;
+struct QuadWorklist {
+    uint32_t *worklist;      // n_items packet indices, 0xffffffff = padding
+    uint32_t *tile_keys;     // key of each 16-entry tile
+    uint64_t *tile_work;     // exclusive scan of the tiles' work, n_items / 16 + 1 entries
+    uint2 *runs;             // [nruns]: tiles [begin, end) of each present key, in key order
+    uint32_t *run_next;      // [nruns]: next tile to hand out of each run, relative (zeroed)
+    uint32_t *nruns;         // device word
+    uint32_t *short_tiles;   // [nshort]: the tiles of keys with fewer than kSegMinTiles tiles
+    uint32_t *nshort;        // device word
+    uint32_t *tile_counter;  // zeroed
+    uint32_t n_items;
+};
 hipError_t launch_quad_worklist(const qgcm_desc *descs, uint32_t n, uint32_t max_keys, const uint8_t *key_valid,
-                                bool seal, void *ws,
-                                size_t ws_bytes, uint32_t **worklist_out, uint32_t **counter_out,
-                                uint32_t *n_items_out, hipStream_t s);
+                                bool seal, void *ws, size_t ws_bytes, QuadWorklist *out, hipStream_t s);
 hipError_t launch_packets(bool seal, int variant, const Batch &b, int grid, hipStream_t s);
 // One packet, one 256-thread workgroup (qgcm_seal_one / qgcm_open_one): the slot (b.stride bytes,
 // a multiple of 16, at most kOneCap - 16) is staged in LDS; b.n must be 1.

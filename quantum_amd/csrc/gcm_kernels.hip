@@ -1181,7 +1181,7 @@ gcm_quad_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
     const uint32_t gH4 = kDesc ? kTe + wave * kGhBytes : kTe;
     const uint32_t gH = kTe + kGhBytes;  // comb table of H in LDS (single key, !kGFin)
     uint32_t cur_key = kDesc ? 0xffffffffu : b.uniform_key;
-    const uint32_t ntiles = kDesc ? (b.n_items >> 4) : ((b.n + 15) >> 4);
+    const uint32_t ntiles = kDesc ? (b.tile_list ? *b.n_list : b.n_items >> 4) : ((b.n + 15) >> 4);
 
     uint32_t tile = blockIdx.x * kW + wave;
     if constexpr (kDesc) {  // dynamic tiles: lengths vary by 100x between tiles
@@ -1195,7 +1195,8 @@ gcm_quad_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
         uint64_t off;
         uint32_t wkey = cur_key;
         if constexpr (kDesc) {
-            pkt = b.worklist[tile * 16u + qd];
+            const uint32_t wt = b.tile_list ? b.tile_list[tile] : tile;
+            pkt = b.worklist[wt * 16u + qd];
             valid = pkt != 0xffffffffu;
             qgcm_desc dsc = {0, 0, 0};
             if (valid) dsc = b.descs[pkt];
@@ -1261,6 +1262,197 @@ gcm_quad_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
         }
     }
 }
+
+// ---------------------------------------------------------------------------------------------
+// Descriptor batches through the Tab2F engine (BASELINE config 3: any key mix, any lengths):
+// gcm_seg_kernel.  The 5-bit comb of H^4 is 13 KiB, too large for one table per wave, so the
+// sixteen waves of a workgroup share ONE key's table and work on one key run of the sorted worklist
+// at a time.  A run's tiles are handed out by a global counter of that run (run_next), so any number
+// of workgroups can work on one run together: a single-key batch is one queue for the whole GPU,
+// longest tiles first, as the per-wave kernels' global tile queue.  A workgroup starts on the run
+// that holds its equal share of the batch's work (g / G of the scanned tile work) and, when that run
+// has no tiles left, moves forward (cyclically) to the next run that has: the workgroups spread over
+// the runs and gather on the last ones.  Moving to another run is a phase change: the waves meet at
+// a barrier, wave 0 finds the run, and the table is refilled when the key changes.  Runs are sorted
+// longest first, so the tiles drawn last from a run are short and the barrier wait is short; the
+// other workgroup of the CU keeps the LDS busy while one waits.  LDS: [0, 13K) the 5-bit comb,
+// [13K, 77K) Te, then the control words: 77 KiB per workgroup, two 16-wave workgroups per CU as the
+// single-key kernel.
+constexpr uint32_t kSegCtl = kG5Bytes + kTeBytes;  // run, phase key (LDS words)
+constexpr uint32_t kSegLds = kSegCtl + 16u;
+constexpr uint32_t kSegDone = 0xffffffffu;
+
+__device__ __forceinline__ volatile lds_u32 *seg_ctl(uint32_t i) { return (volatile lds_u32 *)(size_t)(kSegCtl + 4u * i); }
+
+// Wave-wide search: the first t in [lo, hi] with pred(t), for a pred that is monotone and true at hi
+// (63 probes per step, one load round each).
+template <class P>
+__device__ __forceinline__ uint32_t wave_lower_bound(uint32_t lo, uint32_t hi, uint32_t lane, P pred) {
+    while (hi - lo > 63u) {
+        const uint32_t step = (hi - lo + 62u) / 63u;
+        const uint32_t p = min(lo + lane * step, hi);
+        const uint64_t msk = __ballot(pred(p));  // lane 63 probes hi
+        const uint32_t f = (uint32_t)__ffsll((unsigned long long)msk) - 1u;
+        if (f == 0) return lo;
+        const uint32_t nlo = lo + (f - 1u) * step + 1u, nhi = min(lo + f * step, hi);
+        lo = nlo;
+        hi = nhi;
+    }
+    const uint64_t msk = __ballot(pred(min(lo + lane, hi)));
+    return lo + (uint32_t)__ffsll((unsigned long long)msk) - 1u;
+}
+
+// The first tile of workgroup g's range: the first tile whose work prefix reaches g / G of the total
+// (the same function gives WG g's end and WG g+1's start, so the ranges partition the tiles).
+__device__ __forceinline__ uint32_t seg_range_start(const Batch &b, uint32_t ntiles, uint32_t g, uint32_t lane) {
+    const uint64_t total = b.tile_work[ntiles];
+    const uint64_t target = g == 0 ? 0ull : g >= gridDim.x ? total : (uint64_t)((double)total * g / gridDim.x);
+    return wave_lower_bound(0u, ntiles, lane, [&](uint32_t t) { return b.tile_work[t] >= target; });
+}
+
+// QGCM_SEG_STATS (side builds only, tools/seg_stats.py): per-workgroup counters of the segmented
+// kernel in a device array: phases, tiles, start/end (100 MHz clock), waves' idle and busy time,
+// table fills, wave 0's time finding runs.
+#ifdef QGCM_SEG_STATS
+__device__ unsigned long long g_seg_stats[4096 * 8];
+#define SEG_STAT_ADD(i, v) \
+    do { if (lane == 0) atomicAdd(&g_seg_stats[blockIdx.x * 8u + (i)], (unsigned long long)(v)); } while (0)
+#define SEG_NOW() wall_clock64()
+#else
+#define SEG_STAT_ADD(i, v) do { } while (0)
+#define SEG_NOW() 0ull
+#endif
+
+// Wave 0: the next run to work on, published with its key (kSegDone: no tiles left anywhere).
+// First the runs are dealt out one by one from a global cursor (tile_counter[0]), so each has one
+// owner while unowned runs remain; after that the workgroup helps: it takes the first run at or after
+// r (cyclically; r starts at the workgroup's equal-work position) that still has tiles.  (Helping
+// any in-progress run before all are owned makes workgroups pile onto the same runs and move on
+// together: many short phases.)
+__device__ __forceinline__ void seg_next_phase(const Batch &b, uint32_t &r, uint32_t nruns, bool &helping,
+                                               uint32_t lane) {
+    uint32_t found = kSegDone;
+    if (!helping) {
+        uint32_t c = 0;
+        if (lane == 0) c = atomicAdd(b.tile_counter, 1u);
+        c = __builtin_amdgcn_readfirstlane(__shfl(c, 0));
+        if (c < nruns)
+            found = c;
+        else
+            helping = true;
+    }
+    if (helping) {
+        for (uint32_t base = 0; base < nruns; base += 64u) {
+            uint32_t i = r + base + lane;
+            i = i >= nruns ? i - nruns : i;  // r < nruns, and only lanes with base + lane < nruns look
+            bool left = false;
+            if (base + lane < nruns) {
+                const uint2 run = b.runs[i];
+                left = __hip_atomic_load(b.run_next + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < run.y - run.x;
+            }
+            const uint64_t msk = __ballot(left);
+            if (msk) {
+                found = __builtin_amdgcn_readfirstlane(__shfl(i, (int)__ffsll((unsigned long long)msk) - 1));
+                break;
+            }
+        }
+    }
+    uint32_t key = kSegDone;
+    if (found != kSegDone) {
+        r = found;
+        key = b.tile_keys[b.runs[found].x];
+    }
+    if (lane == 0) {
+        *seg_ctl(0) = found;
+        *seg_ctl(1) = key;
+    }
+}
+
+template <bool kSeal>
+__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8)))
+gcm_seg_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
+    constexpr uint32_t kT = 1024;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = threadIdx.x >> 6;
+    const uint32_t m = lane & 3u;
+    const uint32_t qd = lane >> 2;
+    for (uint32_t i = threadIdx.x; i < kTeBytes / 4; i += kT) {
+        const uint32_t x = i >> 6, slot = i & 63u;
+        lds_st32(kG5Bytes + 4 * i, b.te[(slot >> 5) * 256u + x]);
+    }
+    const uint32_t lb = (lane & 31u) << 2;
+    const uint32_t m8 = vreg(0x0000ff00u), mf8 = vreg(0x000000f8u);
+    const uint32_t ntiles = b.n_items >> 4;
+    uint32_t table_key = kSegDone;
+    uint32_t r = 0, nruns = 0;  // wave 0: the current run
+    bool helping = false;
+    if (wave == 0) {
+        nruns = *b.nruns;
+        if (nruns) {
+            const uint32_t t = min(seg_range_start(b, ntiles, blockIdx.x, lane), ntiles - 1u);
+            // the run holding tile t: the last run that begins at or before it
+            const uint32_t i = wave_lower_bound(0u, nruns, lane, [&](uint32_t j) { return j == nruns || b.runs[j].x > t; });
+            r = i ? i - 1u : 0u;
+        }
+        SEG_STAT_ADD(6, r);
+    }
+    __syncthreads();
+    [[maybe_unused]] unsigned long long t_idle = SEG_NOW();
+    if (wave == 0) SEG_STAT_ADD(2, t_idle);
+    [[maybe_unused]] uint32_t ntile_stat = 0;
+    for (;;) {
+        if (wave == 0) {
+            [[maybe_unused]] const unsigned long long t0 = SEG_NOW();
+            seg_next_phase(b, r, nruns, helping, lane);
+            SEG_STAT_ADD(7, SEG_NOW() - t0);
+            SEG_STAT_ADD(0, 1);
+        }
+        __syncthreads();
+        const uint32_t run = __builtin_amdgcn_readfirstlane(*seg_ctl(0));
+        const uint32_t key = __builtin_amdgcn_readfirstlane(*seg_ctl(1));
+        if (run == kSegDone) break;
+        if (key != table_key) {
+            g5_fill(b.gh_table + (size_t)key * kGhEntries + kGhH4, threadIdx.x, kT);
+            table_key = key;
+
+            __syncthreads();
+        }
+        [[maybe_unused]] const unsigned long long t_busy = SEG_NOW();
+        SEG_STAT_ADD(4, t_busy - t_idle);
+        const uint2 rt = b.runs[run];
+        const Tab2F e3 = {{rk_table + (size_t)key * kRkWords, rk_table + (size_t)key * kRkWords + 64}, {lb, m8}, mf8};
+        for (;;) {
+            uint32_t t = 0;
+            if (lane == 0) t = atomicAdd(b.run_next + run, 1u);
+            t = rt.x + __builtin_amdgcn_readfirstlane(__shfl(t, 0));
+            if (t >= rt.y) break;
+            const uint32_t pkt = b.worklist[t * 16u + qd];
+            if (pkt != 0xffffffffu) {  // the padding of a key run's last tile
+                const qgcm_desc dsc = b.descs[pkt];
+                const uint32_t L = kSeal ? dsc.len : dsc.len - QGCM_OVERHEAD;  // open: len >= 28 here
+                quad_packet<kSeal, false, true, true>(b, e3, pkt, dsc.offset, L, key, m, 0u, 0u);
+            }
+            ++ntile_stat;
+        }
+        t_idle = SEG_NOW();
+        SEG_STAT_ADD(5, t_idle - t_busy);
+        __syncthreads();  // the table and the control words are free again
+    }
+    SEG_STAT_ADD(1, ntile_stat);
+    if (wave == 0) SEG_STAT_ADD(3, SEG_NOW());
+}
+
+#ifdef QGCM_SEG_STATS
+extern "C" int qgcm_debug_seg_stats(unsigned long long *out, int n, int reset) {
+    if (n > 4096 * 8) n = 4096 * 8;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_seg_stats), (size_t)n * 8) != hipSuccess) return -1;
+    if (reset) {
+        static unsigned long long zero[4096 * 8];
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_seg_stats), zero, sizeof(zero)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
 
 // ---------------------------------------------------------------------------------------------
 // Latency kernel for ONE packet (qgcm_seal_one / qgcm_open_one, the per-call form of
@@ -1578,13 +1770,14 @@ struct Variant {
     bool quad;       // 16 packets per wave tile instead of 64
     int wgs_per_cu;  // resident workgroups per CU the persistent grid is sized for
     bool desc;       // consumes the sorted 16-packet worklist (launch_quad_worklist)
+    int complement;  // segmented: the per-wave variant that takes the short keys' tiles after it
 };
 
 template <int kW, bool kShared, int kIlp>
 Variant make_variant() {
     return Variant{reinterpret_cast<const void *>(&gcm_kernel<true, kW, kShared, kIlp>),
                    reinterpret_cast<const void *>(&gcm_kernel<false, kW, kShared, kIlp>), kW,
-                   lds_bytes<kW, kShared>(), false, 1, false};
+                   lds_bytes<kW, kShared>(), false, 1, false, -1};
 }
 
 // the four-table engine: 128 KiB of T-tables + the H^4 comb = one 16-wave workgroup per CU
@@ -1592,14 +1785,14 @@ template <int kW>
 Variant make_quad4() {
     return Variant{reinterpret_cast<const void *>(&gcm_quad_kernel<true, kW, false, kW / 4, false, true, 4>),
                    reinterpret_cast<const void *>(&gcm_quad_kernel<false, kW, false, kW / 4, false, true, 4>), kW,
-                   kTe4Bytes + kGhBytes, true, 1, false};
+                   kTe4Bytes + kGhBytes, true, 1, false, -1};
 }
 
 template <int kW, bool kFold, int kWpe = kW / 4, bool kGFin = true>
 Variant make_quad() {
     return Variant{reinterpret_cast<const void *>(&gcm_quad_kernel<true, kW, kFold, kWpe, false, kGFin>),
                    reinterpret_cast<const void *>(&gcm_quad_kernel<false, kW, kFold, kWpe, false, kGFin>), kW,
-                   kQuadLds + (kGFin ? 0u : kGhBytes), true, kWpe * 4 / kW, false};
+                   kQuadLds + (kGFin ? 0u : kGhBytes), true, kWpe * 4 / kW, false, -1};
 }
 
 // Tab2F engine (5-bit comb GHASH, byte-1 AND-OR addresses): 13 KiB comb + 64 KiB T-tables
@@ -1607,7 +1800,13 @@ template <int kW, int kWpe>
 Variant make_quad2f() {
     return Variant{reinterpret_cast<const void *>(&gcm_quad_kernel<true, kW, false, kWpe, false, true, 3>),
                    reinterpret_cast<const void *>(&gcm_quad_kernel<false, kW, false, kWpe, false, true, 3>), kW,
-                   kG5Bytes + kTeBytes, true, kWpe * 4 / kW, false};
+                   kG5Bytes + kTeBytes, true, kWpe * 4 / kW, false, -1};
+}
+
+// descriptor batches, Tab2F engine: one 5-bit comb per workgroup (gcm_seg_kernel)
+Variant make_seg() {
+    return Variant{reinterpret_cast<const void *>(&gcm_seg_kernel<true>),
+                   reinterpret_cast<const void *>(&gcm_seg_kernel<false>), 16, kSegLds, true, 2, true, 13};
 }
 
 // descriptor batches: per-wave H^4 table, so LDS = Te + one 8 KiB table per wave
@@ -1615,7 +1814,7 @@ template <int kW, int kWpe, bool kGFin = true, int kTab = 2>
 Variant make_quad_desc() {
     return Variant{reinterpret_cast<const void *>(&gcm_quad_kernel<true, kW, false, kWpe, true, kGFin, kTab>),
                    reinterpret_cast<const void *>(&gcm_quad_kernel<false, kW, false, kWpe, true, kGFin, kTab>), kW,
-                   kTeBytes + (uint32_t)kW * kGhBytes, true, 1, true};
+                   kTeBytes + (uint32_t)kW * kGhBytes, true, 1, true, -1};
 }
 
 static Variant g_variants[kNumVariants];
@@ -1635,6 +1834,7 @@ hipError_t init_kernels() {
     g_variants[11] = make_quad4<16>();                  // quad, four T-tables (128 KiB), 16 waves/CU
     g_variants[13] = make_quad_desc<12, 3, true, 5>();  // as 7, byte-1 AND-OR addresses
     g_variants[12] = make_quad2f<16, 8>();                // as 5, 5-bit comb GHASH + byte-1 AND-OR addresses
+    g_variants[14] = make_seg();                          // descriptors: Tab2F, one 5-bit comb per workgroup
     for (const Variant &v : g_variants) {
         for (const void *k : {v.seal, v.open}) {
             hipFuncAttributes a;
@@ -1662,6 +1862,7 @@ int variant_waves(int v) { return g_variants[v].waves; }
 bool variant_quad(int v) { return g_variants[v].quad; }
 int variant_wgs_per_cu(int v) { return g_variants[v].wgs_per_cu; }
 bool variant_desc(int v) { return g_variants[v].desc; }
+int variant_complement(int v) { return g_variants[v].complement; }
 
 hipError_t launch_packets(bool seal, int variant, const Batch &b, int grid, hipStream_t s) {
     if (variant < 0 || variant >= kNumVariants) return hipErrorInvalidValue;

@@ -332,14 +332,27 @@ int run_descs_locked(qgcm_ctx *ctx, bool seal, const qgcm_desc *descs, uint32_t 
             if (hipMalloc(&ctx->d_qws, need) != hipSuccess) return QGCM_E_NOMEM;
             ctx->qws_cap = need;
         }
-        uint32_t *wl = nullptr, *counter = nullptr;
-        if (launch_quad_worklist(descs, n, ctx->max_keys, ctx->d_key_valid, seal, ctx->d_qws, ctx->qws_cap, &wl,
-                                 &counter, &items, s) != hipSuccess)
+        QuadWorklist q{};
+        if (launch_quad_worklist(descs, n, ctx->max_keys, ctx->d_key_valid, seal, ctx->d_qws, ctx->qws_cap, &q, s) !=
+            hipSuccess)
             return QGCM_E_HIP;
-        b.worklist = wl;
-        b.tile_counter = counter;
-        b.n_items = items;
-        return hip_fail(launch_packets(seal, v, b, grid_for(ctx, b.n_items, v), s));
+        b.worklist = q.worklist;
+        b.tile_keys = q.tile_keys;
+        b.tile_work = q.tile_work;
+        b.runs = q.runs;
+        b.run_next = q.run_next;
+        b.nruns = q.nruns;
+        b.tile_counter = q.tile_counter;
+        b.n_items = q.n_items;
+        if (launch_packets(seal, v, b, grid_for(ctx, b.n_items, v), s) != hipSuccess) return QGCM_E_HIP;
+        const int vc = variant_complement(v);
+        if (vc < 0) return QGCM_OK;
+        // the short keys' tiles (fewer than kSegMinTiles per key) through the per-wave kernel; its
+        // dynamic tile counter is the next word of the zeroed counter block
+        b.tile_list = q.short_tiles;
+        b.n_list = q.nshort;
+        b.tile_counter = q.tile_counter + 3;
+        return hip_fail(launch_packets(seal, vc, b, grid_for(ctx, b.n_items, vc), s));
     }
     const uint64_t cap = (uint64_t)n + 64ull * (n < ctx->max_keys ? n : ctx->max_keys);
     const uint32_t items = (uint32_t)((cap + 63) & ~63ull);

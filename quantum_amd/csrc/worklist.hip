@@ -55,63 +55,112 @@ __global__ void qwl_count_kernel(const uint32_t *sk, uint32_t n, const uint32_t 
     if (j == n - 1 || sk[j + 1] == 0xffffffffu || (sk[j + 1] >> kLenBits) != k) counts[k] = j + 1 - first[k];
 }
 
-// Single workgroup: counts -> start (unpadded, sorted order) and pstart (padded to 16, worklist).
+// Single workgroup: counts -> start (unpadded, sorted order), pstart (padded to 16, worklist), and
+// for the segmented kernel the run table (runs[r] = the tiles [begin, end) of the r-th key with at
+// least kSegMinTiles tiles) and the list of the other keys' tiles (short_tiles, for the per-wave
+// kernel that runs after it).
 __global__ void __launch_bounds__(1024) qwl_scan_kernel(const uint32_t *counts, uint32_t max_keys, uint32_t *start,
-                                                        uint32_t *pstart) {
-    __shared__ uint32_t pu[1024], pp[1024];
+                                                        uint32_t *pstart, uint2 *runs, uint32_t *short_tiles,
+                                                        uint32_t *nruns_nshort) {
+    __shared__ uint32_t pu[1024], pp[1024], pr[1024], ps[1024];
     const uint32_t t = threadIdx.x;
     const uint32_t per = (max_keys + 1023) / 1024;
     const uint32_t lo = t * per, hi = min(lo + per, max_keys);
-    uint32_t su = 0, sp = 0;
+    uint32_t su = 0, sp = 0, sr = 0, ss = 0;
     for (uint32_t k = lo; k < hi; ++k) {
+        const uint32_t nt = (counts[k] + 15u) >> 4;
         su += counts[k];
-        sp += (counts[k] + 15u) & ~15u;
+        sp += nt << 4;
+        sr += nt >= kSegMinTiles ? 1u : 0u;
+        ss += nt < kSegMinTiles ? nt : 0u;
     }
     pu[t] = su;
     pp[t] = sp;
+    pr[t] = sr;
+    ps[t] = ss;
     __syncthreads();
     for (uint32_t d = 1; d < 1024; d <<= 1) {
-        const uint32_t a = t >= d ? pu[t - d] : 0, b = t >= d ? pp[t - d] : 0;
+        const uint32_t a = t >= d ? pu[t - d] : 0, b = t >= d ? pp[t - d] : 0, c = t >= d ? pr[t - d] : 0,
+                       e = t >= d ? ps[t - d] : 0;
         __syncthreads();
         pu[t] += a;
         pp[t] += b;
+        pr[t] += c;
+        ps[t] += e;
         __syncthreads();
     }
-    uint32_t ru = pu[t] - su, rp = pp[t] - sp;
+    uint32_t ru = pu[t] - su, rp = pp[t] - sp, rr = pr[t] - sr, rs = ps[t] - ss;
     for (uint32_t k = lo; k < hi; ++k) {
         start[k] = ru;
         pstart[k] = rp;
+        const uint32_t nt = (counts[k] + 15u) >> 4;
+        if (nt >= kSegMinTiles) {
+            runs[rr++] = uint2{rp >> 4, (rp >> 4) + nt};
+        } else {
+            for (uint32_t j = 0; j < nt; ++j) short_tiles[rs++] = (rp >> 4) + j;
+        }
         ru += counts[k];
-        rp += (counts[k] + 15u) & ~15u;
+        rp += nt << 4;
+    }
+    if (t == 1023) {
+        nruns_nshort[0] = pr[1023];
+        nruns_nshort[1] = ps[1023];
     }
 }
 
+// also the key of every tile (the first entry of each 16-entry tile of a key run)
 __global__ void qwl_scatter_kernel(const uint32_t *sorted_keys, const uint32_t *sorted_vals, uint32_t n,
-                                   const uint32_t *start, const uint32_t *pstart, uint32_t *worklist) {
+                                   const uint32_t *start, const uint32_t *pstart, uint32_t *worklist,
+                                   uint32_t *tile_keys) {
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n) return;
     const uint32_t sk = sorted_keys[j];
     if (sk == 0xffffffffu) return;
     const uint32_t k = sk >> kLenBits;
-    worklist[pstart[k] + (j - start[k])] = sorted_vals[j];
+    const uint32_t w = pstart[k] + (j - start[k]);
+    worklist[w] = sorted_vals[j];
+    if ((w & 15u) == 0) tile_keys[w >> 4] = k;
+}
+
+// Work of each tile (AES+GHASH block steps of its packets, plus a per-packet constant for the
+// counter setup, J0 and the tag), for the equal-work partition of the segmented kernel; the entry
+// after the last tile is 0 so that the exclusive scan ends with the total.
+__global__ void qwl_tile_work_kernel(const uint32_t *worklist, const qgcm_desc *descs, uint32_t ntiles, bool seal,
+                                     uint32_t *work) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t > ntiles) return;
+    uint32_t w = 0;
+    if (t < ntiles) {
+        for (uint32_t j = 0; j < 16; ++j) {
+            const uint32_t pkt = worklist[16 * t + j];
+            if (pkt == 0xffffffffu) continue;
+            const uint32_t L = seal ? descs[pkt].len : descs[pkt].len - QGCM_OVERHEAD;
+            w += ((L + 15u) >> 4) + 4u;
+        }
+    }
+    work[t] = w;
 }
 
 size_t quad_worklist_bytes(uint32_t n, uint32_t max_keys, uint32_t *n_items_out) {
     const uint64_t cap = (uint64_t)n + 16ull * (n < max_keys ? n : max_keys);
     const uint32_t items = (uint32_t)((cap + 15) & ~15ull);
-    size_t cub = 0;
+    size_t cub = 0, scan = 0;
     hipcub::DeviceRadixSort::SortPairs(nullptr, cub, (uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr,
                                        (uint32_t *)nullptr, (int)n);
+    hipcub::DeviceScan::ExclusiveSum(nullptr, scan, (uint32_t *)nullptr, (uint64_t *)nullptr, (int)(items / 16 + 1));
+    if (scan > cub) cub = scan;
     if (n_items_out) *n_items_out = items;
-    // keys in/out, vals in/out, counts, start, pstart, worklist, tile counter, cub temp (16-B aligned pieces)
+    // keys in/out, vals in/out, counts, start, pstart, run counters, runs, worklist, tile keys, short
+    // tiles, tile work, its exclusive scan, tile counter + run count + short count, cub temp (256-B
+    // aligned pieces)
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-    return 4 * al(4ull * n) + 3 * al(4ull * max_keys) + al(4ull * items) + al(16) + al(cub);
+    const size_t tiles1 = items / 16 + 1;
+    return 4 * al(4ull * n) + 4 * al(4ull * max_keys) + al(8ull * max_keys) + al(4ull * items) + 2 * al(items / 4) +
+           al(4 * tiles1) + al(8 * tiles1) + al(16) + al(cub);
 }
 
 hipError_t launch_quad_worklist(const qgcm_desc *descs, uint32_t n, uint32_t max_keys, const uint8_t *key_valid,
-                                bool seal, void *ws,
-                                size_t ws_bytes, uint32_t **worklist_out, uint32_t **counter_out,
-                                uint32_t *n_items_out, hipStream_t s) {
+                                bool seal, void *ws, size_t ws_bytes, QuadWorklist *out, hipStream_t s) {
     uint32_t items = 0;
     const size_t need = quad_worklist_bytes(n, max_keys, &items);
     if (ws_bytes < need) return hipErrorInvalidValue;
@@ -124,14 +173,23 @@ hipError_t launch_quad_worklist(const qgcm_desc *descs, uint32_t n, uint32_t max
     uint32_t *counts = (uint32_t *)p; p += al(4ull * max_keys);
     uint32_t *start = (uint32_t *)p;  p += al(4ull * max_keys);
     uint32_t *pstart = (uint32_t *)p; p += al(4ull * max_keys);
+    uint32_t *run_next = (uint32_t *)p; p += al(4ull * max_keys);
+    uint2 *runs = (uint2 *)p; p += al(8ull * max_keys);
     uint32_t *worklist = (uint32_t *)p; p += al(4ull * items);
-    uint32_t *counter = (uint32_t *)p;  p += al(16);
+    uint32_t *tile_keys = (uint32_t *)p; p += al(items / 4);
+    uint32_t *short_tiles = (uint32_t *)p; p += al(items / 4);
+    const uint32_t ntiles = items / 16;
+    uint32_t *work = (uint32_t *)p; p += al(4ull * (ntiles + 1));
+    uint64_t *work_x = (uint64_t *)p; p += al(8ull * (ntiles + 1));
+    uint32_t *counter = (uint32_t *)p;  p += al(16);  // [0] tile counter, [1] run count, [2] short tiles
     void *cub_tmp = p;
     size_t cub_bytes = need - (size_t)(p - static_cast<char *>(ws));
     hipError_t e;
     if ((e = hipMemsetAsync(counts, 0, 4ull * max_keys, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(worklist, 0xff, 4ull * items, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(tile_keys, 0xff, items / 4, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(counter, 0, 16, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(run_next, 0, 4ull * max_keys, s)) != hipSuccess) return e;
     const int bs = 256, g = (int)((n + bs - 1) / bs);
     if (n) hipLaunchKernelGGL(qwl_keys_kernel, dim3(g), dim3(bs), 0, s, descs, n, max_keys, key_valid, seal, k_in,
                                  v_in);
@@ -146,11 +204,27 @@ hipError_t launch_quad_worklist(const qgcm_desc *descs, uint32_t n, uint32_t max
         hipLaunchKernelGGL(qwl_first_kernel, dim3(g), dim3(bs), 0, s, k_out, n, start);
         hipLaunchKernelGGL(qwl_count_kernel, dim3(g), dim3(bs), 0, s, k_out, n, start, counts);
     }
-    hipLaunchKernelGGL(qwl_scan_kernel, dim3(1), dim3(1024), 0, s, counts, max_keys, start, pstart);
-    if (n) hipLaunchKernelGGL(qwl_scatter_kernel, dim3(g), dim3(bs), 0, s, k_out, v_out, n, start, pstart, worklist);
-    *worklist_out = worklist;
-    *counter_out = counter;
-    *n_items_out = items;
+    hipLaunchKernelGGL(qwl_scan_kernel, dim3(1), dim3(1024), 0, s, counts, max_keys, start, pstart, runs,
+                       short_tiles, counter + 1);
+    if (n) hipLaunchKernelGGL(qwl_scatter_kernel, dim3(g), dim3(bs), 0, s, k_out, v_out, n, start, pstart, worklist,
+                                 tile_keys);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(qwl_tile_work_kernel, dim3((ntiles + 1 + bs - 1) / bs), dim3(bs), 0, s, worklist, descs,
+                       ntiles, seal, work);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    cub_bytes = need - (size_t)(static_cast<char *>(cub_tmp) - static_cast<char *>(ws));
+    if ((e = hipcub::DeviceScan::ExclusiveSum(cub_tmp, cub_bytes, work, work_x, (int)(ntiles + 1), s)) != hipSuccess)
+        return e;
+    out->worklist = worklist;
+    out->tile_keys = tile_keys;
+    out->tile_work = work_x;
+    out->runs = runs;
+    out->run_next = run_next;
+    out->nruns = counter + 1;
+    out->short_tiles = short_tiles;
+    out->nshort = counter + 2;
+    out->tile_counter = counter;
+    out->n_items = items;
     return hipGetLastError();
 }
 

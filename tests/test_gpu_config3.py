@@ -57,7 +57,7 @@ def c3_ctxs(torch, c3_keys):
     out = {}
     old = os.environ.get("QGCM_DESC_VARIANT")
     try:
-        for v in (7, 10):
+        for v in (7, 10, 14):
             os.environ["QGCM_DESC_VARIANT"] = str(v)
             out[v] = Context(device=0, max_keys=W.NKEYS)
             out[v].set_keys(0, c3_keys)
@@ -89,7 +89,7 @@ def sha_device(torch, t) -> str:
     return h.hexdigest()
 
 
-@pytest.mark.parametrize("v", [7, 10])
+@pytest.mark.parametrize("v", [7, 10, 14])
 def test_config3_prefix_vs_oracle(torch, c3_ctxs, c3_keys, v):
     from quantum_amd import batch
 
@@ -138,13 +138,14 @@ def test_config3_prefix_vs_oracle(torch, c3_ctxs, c3_keys, v):
     assert np.array_equal(arena.cpu().numpy(), exp)  # restored / zeroed bytes identical to the oracle's
 
 
-def test_config3_full_arena_digest(torch, c3_ctxs, config3_digest):
+@pytest.mark.parametrize("v", [7, 14])
+def test_config3_full_arena_digest(torch, c3_ctxs, config3_digest, v):
     """All 2^20 packets (1024 keys, 4.75 GB of payload): digests before sealing, sealed and opened
     equal the golden ones (OpenSSL over the same workload, prefix cross-checked with the oracle)."""
     from quantum_amd import batch
 
     g = config3_digest
-    ctx = c3_ctxs[7]
+    ctx = c3_ctxs[v]
     lens, kidx = W.lengths(), W.key_indices()
     assert int(lens.sum()) == g["payload_bytes"]
     offs, size = W.layout(lens)

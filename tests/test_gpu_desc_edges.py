@@ -54,7 +54,7 @@ def packed(lens):
     return offs, pos + 64
 
 
-@pytest.mark.parametrize("v", [0, 7, 8, 10])
+@pytest.mark.parametrize("v", [0, 7, 8, 10, 14])
 def test_unset_key_slot_is_rejected(torch, v):
     from quantum_amd import batch
 

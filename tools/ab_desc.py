@@ -3,7 +3,8 @@
 Each variant is its own qgcm context (QGCM_DESC_VARIANT is read at qgcm_create) with the same 1024
 keys.  Correctness: every variant's sealed arena must equal the first variant's byte for byte.
 Usage: python tools/ab_desc.py 7,10,8 [rounds]; an entry v:cN runs variant v with QGCM_DESC_CHUNK=N
-(packets per sorted chunk), e.g. 7,7:c131072,7:c262144
+(packets per sorted chunk), e.g. 7,7:c131072,7:c262144.  AB_KEYS=k draws key indices from k keys
+(default 1024), AB_LEN=L gives every packet length L (default U{64..9000}).
 """
 import os
 import statistics
@@ -18,7 +19,10 @@ from quantum_amd.crypto import Context  # noqa: E402
 
 variants = (sys.argv[1] if len(sys.argv) > 1 else "7,10").split(",")
 rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 5
-N, NK = 1 << 20, 1024
+N = 1 << 20
+NUSE = int(os.environ.get("AB_KEYS", 1024))
+NK = max(1024, NUSE)
+FIXED_LEN = int(os.environ.get("AB_LEN", 0))
 rng = np.random.default_rng(0x5EED0003)
 keys = rng.bytes(32 * NK)
 ctxs = {}
@@ -29,7 +33,9 @@ for v in variants:
     c.set_keys(0, keys)
     ctxs[v] = c
 lens = rng.integers(64, 9001, size=N, dtype=np.int64)
-kidx = rng.integers(0, NK, size=N, dtype=np.int64)
+kidx = rng.integers(0, NUSE, size=N, dtype=np.int64)
+if FIXED_LEN:
+    lens[:] = FIXED_LEN
 slot = (4 + lens + 28 + 3) & ~3
 offs = np.zeros(N, dtype=np.int64)
 offs[1:] = np.cumsum(slot)[:-1]
