@@ -57,7 +57,7 @@ struct Batch {
 
 constexpr int kNumVariants = 15;
 constexpr int kVariantGeneral = 0;   // lane per packet, per-wave GHASH tables, any key mix
-constexpr int kVariantDescQuad = 7;  // default for descriptor batches: sorted quad tiles
+constexpr int kVariantDescQuad = 14;  // default for descriptor batches: segmented Tab2F kernel (+ 13 for short keys)
 constexpr int kVariantUniform = 12;  // default for single-key (uniform) batches: quad kernel (Tab2F), 32 waves/CU
 hipError_t init_kernels();
 int variant_waves(int variant);

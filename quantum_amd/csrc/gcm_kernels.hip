@@ -1136,6 +1136,8 @@ gcm_quad_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
     const uint32_t wave = threadIdx.x >> 6;
     const uint32_t m = lane & 3u;          // block residue owned by this lane
     const uint32_t qd = lane >> 2;         // packet slot within the wave tile (16 per wave)
+    // the short-key pass of a segmented launch with no short keys: leave before the table fill
+    if (kDesc && b.tile_list && __builtin_amdgcn_readfirstlane(*b.n_list) == 0) return;
 
     // dword i of each 64 KiB half: row x = i/64, slot i%64 (< 32: Te0 / Te2, else Te1 / Te3)
     for (uint32_t i = threadIdx.x; i < kTeBytes / 4; i += kT) {
@@ -1279,7 +1281,7 @@ gcm_quad_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
 // [13K, 77K) Te, then the control words: 77 KiB per workgroup, two 16-wave workgroups per CU as the
 // single-key kernel.
 constexpr uint32_t kSegCtl = kG5Bytes + kTeBytes;  // run, phase key (LDS words)
-constexpr uint32_t kSegLds = kSegCtl + 16u;
+constexpr uint32_t kSegLds = kSegCtl + 16u;  // two control slots of (run, key)
 constexpr uint32_t kSegDone = 0xffffffffu;
 
 __device__ __forceinline__ volatile lds_u32 *seg_ctl(uint32_t i) { return (volatile lds_u32 *)(size_t)(kSegCtl + 4u * i); }
@@ -1330,7 +1332,7 @@ __device__ unsigned long long g_seg_stats[4096 * 8];
 // any in-progress run before all are owned makes workgroups pile onto the same runs and move on
 // together: many short phases.)
 __device__ __forceinline__ void seg_next_phase(const Batch &b, uint32_t &r, uint32_t nruns, bool &helping,
-                                               uint32_t lane) {
+                                               uint32_t lane, uint32_t slot) {
     uint32_t found = kSegDone;
     if (!helping) {
         uint32_t c = 0;
@@ -1342,19 +1344,29 @@ __device__ __forceinline__ void seg_next_phase(const Batch &b, uint32_t &r, uint
             helping = true;
     }
     if (helping) {
-        for (uint32_t base = 0; base < nruns; base += 64u) {
-            uint32_t i = r + base + lane;
-            i = i >= nruns ? i - nruns : i;  // r < nruns, and only lanes with base + lane < nruns look
-            bool left = false;
-            if (base + lane < nruns) {
-                const uint2 run = b.runs[i];
-                left = __hip_atomic_load(b.run_next + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < run.y - run.x;
+        // four runs per lane per step (their loads in flight together): 256 runs per step
+        for (uint32_t base = 0; base < nruns; base += 256u) {
+            bool left[4];
+            uint32_t idx[4];
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j) {
+                const uint32_t o = base + 64u * j + lane;
+                uint32_t i = r + o;
+                i = i >= nruns ? i - nruns : i;  // r < nruns, and only offsets o < nruns look
+                idx[j] = i;
+                left[j] = false;
+                if (o < nruns) {
+                    const uint2 run = b.runs[i];
+                    left[j] = __hip_atomic_load(b.run_next + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+                              run.y - run.x;
+                }
             }
-            const uint64_t msk = __ballot(left);
-            if (msk) {
-                found = __builtin_amdgcn_readfirstlane(__shfl(i, (int)__ffsll((unsigned long long)msk) - 1));
-                break;
+#pragma unroll
+            for (uint32_t j = 0; j < 4 && found == kSegDone; ++j) {
+                const uint64_t msk = __ballot(left[j]);
+                if (msk) found = __builtin_amdgcn_readfirstlane(__shfl(idx[j], (int)__ffsll((unsigned long long)msk) - 1));
             }
+            if (found != kSegDone) break;
         }
     }
     uint32_t key = kSegDone;
@@ -1363,10 +1375,20 @@ __device__ __forceinline__ void seg_next_phase(const Batch &b, uint32_t &r, uint
         key = b.tile_keys[b.runs[found].x];
     }
     if (lane == 0) {
-        *seg_ctl(0) = found;
-        *seg_ctl(1) = key;
+        *seg_ctl(2 * slot) = found;
+        *seg_ctl(2 * slot + 1) = key;
     }
 }
+
+// Side-build knobs for A/Bs (tools/ab_libs_desc.py): QGCM_SEG_EARLY = wave 0 finds the next run as
+// soon as its own tiles are done instead of after the barrier; QGCM_SEG_PREFETCH = each wave claims
+// its next tile before working on the current one.
+#ifndef QGCM_SEG_EARLY
+#define QGCM_SEG_EARLY 0
+#endif
+#ifndef QGCM_SEG_PREFETCH
+#define QGCM_SEG_PREFETCH 0
+#endif
 
 template <bool kSeal>
 __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8, 8)))
@@ -1376,6 +1398,8 @@ gcm_seg_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
     const uint32_t wave = threadIdx.x >> 6;
     const uint32_t m = lane & 3u;
     const uint32_t qd = lane >> 2;
+    // no key run long enough (every tile goes to the per-wave kernel): leave before the table fill
+    if (__builtin_amdgcn_readfirstlane(*b.nruns) == 0) return;
     for (uint32_t i = threadIdx.x; i < kTeBytes / 4; i += kT) {
         const uint32_t x = i >> 6, slot = i & 63u;
         lds_st32(kG5Bytes + 4 * i, b.te[(slot >> 5) * 256u + x]);
@@ -1388,43 +1412,58 @@ gcm_seg_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
     bool helping = false;
     if (wave == 0) {
         nruns = *b.nruns;
-        if (nruns) {
-            const uint32_t t = min(seg_range_start(b, ntiles, blockIdx.x, lane), ntiles - 1u);
-            // the run holding tile t: the last run that begins at or before it
-            const uint32_t i = wave_lower_bound(0u, nruns, lane, [&](uint32_t j) { return j == nruns || b.runs[j].x > t; });
-            r = i ? i - 1u : 0u;
-        }
+        const uint32_t t = min(seg_range_start(b, ntiles, blockIdx.x, lane), ntiles - 1u);
+        // the run holding tile t: the last run that begins at or before it
+        const uint32_t i = wave_lower_bound(0u, nruns, lane, [&](uint32_t j) { return j == nruns || b.runs[j].x > t; });
+        r = i ? i - 1u : 0u;
         SEG_STAT_ADD(6, r);
+        if (QGCM_SEG_EARLY) {
+            [[maybe_unused]] const unsigned long long t0 = SEG_NOW();
+            seg_next_phase(b, r, nruns, helping, lane, 0u);
+            SEG_STAT_ADD(7, SEG_NOW() - t0);
+        }
     }
     __syncthreads();
     [[maybe_unused]] unsigned long long t_idle = SEG_NOW();
     if (wave == 0) SEG_STAT_ADD(2, t_idle);
     [[maybe_unused]] uint32_t ntile_stat = 0;
-    for (;;) {
-        if (wave == 0) {
-            [[maybe_unused]] const unsigned long long t0 = SEG_NOW();
-            seg_next_phase(b, r, nruns, helping, lane);
-            SEG_STAT_ADD(7, SEG_NOW() - t0);
-            SEG_STAT_ADD(0, 1);
+    // QGCM_SEG_EARLY: phase p's run and key are in control slot p % 2.  Wave 0 publishes phase p + 1's
+    // as soon as its own tiles of phase p are done (the run is then exhausted), while the other waves
+    // finish theirs.  Slot (p + 1) % 2 was last read in phase p - 1, before the barrier that began
+    // phase p, so the write cannot race a reader.  Otherwise wave 0 finds the run after the barrier
+    // (slot 0 only).
+    for (uint32_t slot = 0;; slot = QGCM_SEG_EARLY ? slot ^ 1u : 0u) {
+        if (!QGCM_SEG_EARLY) {
+            if (wave == 0) {
+                [[maybe_unused]] const unsigned long long t0 = SEG_NOW();
+                seg_next_phase(b, r, nruns, helping, lane, 0u);
+                SEG_STAT_ADD(7, SEG_NOW() - t0);
+            }
+            __syncthreads();
         }
-        __syncthreads();
-        const uint32_t run = __builtin_amdgcn_readfirstlane(*seg_ctl(0));
-        const uint32_t key = __builtin_amdgcn_readfirstlane(*seg_ctl(1));
+        if (wave == 0) SEG_STAT_ADD(0, 1);
+        const uint32_t run = __builtin_amdgcn_readfirstlane(*seg_ctl(2 * slot));
+        const uint32_t key = __builtin_amdgcn_readfirstlane(*seg_ctl(2 * slot + 1));
         if (run == kSegDone) break;
         if (key != table_key) {
             g5_fill(b.gh_table + (size_t)key * kGhEntries + kGhH4, threadIdx.x, kT);
             table_key = key;
-
             __syncthreads();
         }
         [[maybe_unused]] const unsigned long long t_busy = SEG_NOW();
         SEG_STAT_ADD(4, t_busy - t_idle);
         const uint2 rt = b.runs[run];
         const Tab2F e3 = {{rk_table + (size_t)key * kRkWords, rk_table + (size_t)key * kRkWords + 64}, {lb, m8}, mf8};
-        for (;;) {
-            uint32_t t = 0;
+        uint32_t t = 0;
+        if (QGCM_SEG_PREFETCH) {
             if (lane == 0) t = atomicAdd(b.run_next + run, 1u);
             t = rt.x + __builtin_amdgcn_readfirstlane(__shfl(t, 0));
+        }
+        for (;;) {
+            uint32_t nx = 0;
+            if (lane == 0) nx = atomicAdd(b.run_next + run, 1u);
+            nx = rt.x + __builtin_amdgcn_readfirstlane(__shfl(nx, 0));
+            if (!QGCM_SEG_PREFETCH) t = nx;
             if (t >= rt.y) break;
             const uint32_t pkt = b.worklist[t * 16u + qd];
             if (pkt != 0xffffffffu) {  // the padding of a key run's last tile
@@ -1433,9 +1472,15 @@ gcm_seg_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
                 quad_packet<kSeal, false, true, true>(b, e3, pkt, dsc.offset, L, key, m, 0u, 0u);
             }
             ++ntile_stat;
+            if (QGCM_SEG_PREFETCH) t = nx;
         }
         t_idle = SEG_NOW();
         SEG_STAT_ADD(5, t_idle - t_busy);
+        if (QGCM_SEG_EARLY && wave == 0) {
+            [[maybe_unused]] const unsigned long long t0 = SEG_NOW();
+            seg_next_phase(b, r, nruns, helping, lane, slot ^ 1u);
+            SEG_STAT_ADD(7, SEG_NOW() - t0);
+        }
         __syncthreads();  // the table and the control words are free again
     }
     SEG_STAT_ADD(1, ntile_stat);

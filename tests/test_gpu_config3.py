@@ -1,7 +1,8 @@
 """BASELINE config 3 on the GPU: 2^20 packets of U{64..9000} B under 1024 per-peer keys
 (common/mapping.go:90-99 key provenance, crypto/aes.go:41-62 per packet), through the descriptor
-batch entry points qgcm_seal_batch / qgcm_open_batch -- the default sorted quad-tile kernel
-(variant 7) and its repeated-H recombination form (variant 10).
+batch entry points qgcm_seal_batch / qgcm_open_batch -- the default segmented kernel (variant 14:
+one 5-bit comb per workgroup, short keys through variant 13), the per-wave sorted quad-tile kernel
+(variant 7, the round-1 default) and its repeated-H recombination form (variant 10).
 
 * a 32768-packet prefix of the workload (every one of the 1024 keys, the counter-segment edge
   lengths 4064..4097 and 8160..8193, 9000 B) byte-for-byte against the C restatement, then open with
