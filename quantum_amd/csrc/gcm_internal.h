@@ -43,8 +43,6 @@ struct Batch {
     uint32_t *tile_counter;     // descriptor quad kernels: dynamic tile index (zeroed per launch)
     const uint32_t *tile_keys;  // descriptor quad kernels: key of each 16-entry tile (all ones: padding,
                                 // only after the last key run)
-    const uint64_t *tile_work;  // exclusive prefix sum of the tiles' work (n_items / 16 + 1 entries, the
-                                // last = total): where each workgroup of the segmented kernel starts
     const uint2 *runs;          // segmented kernel: the key runs of the worklist (QuadWorklist)
     uint32_t *run_next;
     const uint32_t *nruns;
@@ -73,7 +71,6 @@ constexpr uint32_t kSegMinTiles = 48;
 struct QuadWorklist {
     uint32_t *worklist;      // n_items packet indices, 0xffffffff = padding
     uint32_t *tile_keys;     // key of each 16-entry tile
-    uint64_t *tile_work;     // exclusive scan of the tiles' work, n_items / 16 + 1 entries
     uint2 *runs;             // [nruns]: tiles [begin, end) of each present key, in key order
     uint32_t *run_next;      // [nruns]: next tile to hand out of each run, relative (zeroed)
     uint32_t *nruns;         // device word

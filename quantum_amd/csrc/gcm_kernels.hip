@@ -1271,11 +1271,12 @@ gcm_quad_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
 // sixteen waves of a workgroup share ONE key's table and work on one key run of the sorted worklist
 // at a time.  A run's tiles are handed out by a global counter of that run (run_next), so any number
 // of workgroups can work on one run together: a single-key batch is one queue for the whole GPU,
-// longest tiles first, as the per-wave kernels' global tile queue.  A workgroup starts on the run
-// that holds its equal share of the batch's work (g / G of the scanned tile work) and, when that run
-// has no tiles left, moves forward (cyclically) to the next run that has: the workgroups spread over
-// the runs and gather on the last ones.  Moving to another run is a phase change: the waves meet at
-// a barrier, wave 0 finds the run, and the table is refilled when the key changes.  Runs are sorted
+// longest tiles first, as the per-wave kernels' global tile queue.  Runs are first dealt out one per
+// workgroup from a global cursor (each run gets an owner that stays on it until it is exhausted);
+// once all are owned, a workgroup whose run is done helps: from its home position (its equal share
+// of the tiles) it moves forward cyclically to the next run with at least QGCM_SEG_HELP_MIN tiles
+// left, and leaves when there is none.  Moving to another run is a phase change: the waves meet at a
+// barrier, wave 0 finds the run, and the table is refilled when the key changes.  Runs are sorted
 // longest first, so the tiles drawn last from a run are short and the barrier wait is short; the
 // other workgroup of the CU keeps the LDS busy while one waits.  LDS: [0, 13K) the 5-bit comb,
 // [13K, 77K) Te, then the control words: 77 KiB per workgroup, two 16-wave workgroups per CU as the
@@ -1304,14 +1305,6 @@ __device__ __forceinline__ uint32_t wave_lower_bound(uint32_t lo, uint32_t hi, u
     return lo + (uint32_t)__ffsll((unsigned long long)msk) - 1u;
 }
 
-// The first tile of workgroup g's range: the first tile whose work prefix reaches g / G of the total
-// (the same function gives WG g's end and WG g+1's start, so the ranges partition the tiles).
-__device__ __forceinline__ uint32_t seg_range_start(const Batch &b, uint32_t ntiles, uint32_t g, uint32_t lane) {
-    const uint64_t total = b.tile_work[ntiles];
-    const uint64_t target = g == 0 ? 0ull : g >= gridDim.x ? total : (uint64_t)((double)total * g / gridDim.x);
-    return wave_lower_bound(0u, ntiles, lane, [&](uint32_t t) { return b.tile_work[t] >= target; });
-}
-
 // QGCM_SEG_STATS (side builds only, tools/seg_stats.py): per-workgroup counters of the segmented
 // kernel in a device array: phases, tiles, start/end (100 MHz clock), waves' idle and busy time,
 // table fills, wave 0's time finding runs.
@@ -1328,9 +1321,15 @@ __device__ unsigned long long g_seg_stats[4096 * 8];
 // Wave 0: the next run to work on, published with its key (kSegDone: no tiles left anywhere).
 // First the runs are dealt out one by one from a global cursor (tile_counter[0]), so each has one
 // owner while unowned runs remain; after that the workgroup helps: it takes the first run at or after
-// r (cyclically; r starts at the workgroup's equal-work position) that still has tiles.  (Helping
+// r (cyclically; r starts at the workgroup's equal share of the tiles) that has enough tiles left.  (Helping
 // any in-progress run before all are owned makes workgroups pile onto the same runs and move on
 // together: many short phases.)
+// A helper joins only a run with at least QGCM_SEG_HELP_MIN tiles left: fewer are finished by the
+// run's owner (a run's owner works on it until it is exhausted, so no tile is left behind) within
+// about one tile time, and joining would cost the helper a barrier and a table refill for little work.
+#ifndef QGCM_SEG_HELP_MIN
+#define QGCM_SEG_HELP_MIN 16
+#endif
 __device__ __forceinline__ void seg_next_phase(const Batch &b, uint32_t &r, uint32_t nruns, bool &helping,
                                                uint32_t lane, uint32_t slot) {
     uint32_t found = kSegDone;
@@ -1357,8 +1356,8 @@ __device__ __forceinline__ void seg_next_phase(const Batch &b, uint32_t &r, uint
                 left[j] = false;
                 if (o < nruns) {
                     const uint2 run = b.runs[i];
-                    left[j] = __hip_atomic_load(b.run_next + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
-                              run.y - run.x;
+                    left[j] = __hip_atomic_load(b.run_next + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) +
+                                  QGCM_SEG_HELP_MIN <= run.y - run.x;
                 }
             }
 #pragma unroll
@@ -1412,7 +1411,8 @@ gcm_seg_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
     bool helping = false;
     if (wave == 0) {
         nruns = *b.nruns;
-        const uint32_t t = min(seg_range_start(b, ntiles, blockIdx.x, lane), ntiles - 1u);
+        // home position: the workgroup's equal share of the tiles (where its help search starts)
+        const uint32_t t = (uint32_t)((uint64_t)ntiles * blockIdx.x / gridDim.x);
         // the run holding tile t: the last run that begins at or before it
         const uint32_t i = wave_lower_bound(0u, nruns, lane, [&](uint32_t j) { return j == nruns || b.runs[j].x > t; });
         r = i ? i - 1u : 0u;

@@ -338,7 +338,6 @@ int run_descs_locked(qgcm_ctx *ctx, bool seal, const qgcm_desc *descs, uint32_t 
             return QGCM_E_HIP;
         b.worklist = q.worklist;
         b.tile_keys = q.tile_keys;
-        b.tile_work = q.tile_work;
         b.runs = q.runs;
         b.run_next = q.run_next;
         b.nruns = q.nruns;

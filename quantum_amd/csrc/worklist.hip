@@ -9,7 +9,7 @@
 // their slot is untouched.  Excluded entries sort last under the all-ones key, which no valid packet
 // can produce: key indices stay below QGCM_MAX_KEYS = 2^20 - 1 (qgcm_create caps max_keys).
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
 #include <stdint.h>
 
 #include "gcm_internal.h"
@@ -122,41 +122,28 @@ __global__ void qwl_scatter_kernel(const uint32_t *sorted_keys, const uint32_t *
     if ((w & 15u) == 0) tile_keys[w >> 4] = k;
 }
 
-// Work of each tile (AES+GHASH block steps of its packets, plus a per-packet constant for the
-// counter setup, J0 and the tag), for the equal-work partition of the segmented kernel; the entry
-// after the last tile is 0 so that the exclusive scan ends with the total.
-__global__ void qwl_tile_work_kernel(const uint32_t *worklist, const qgcm_desc *descs, uint32_t ntiles, bool seal,
-                                     uint32_t *work) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t > ntiles) return;
-    uint32_t w = 0;
-    if (t < ntiles) {
-        for (uint32_t j = 0; j < 16; ++j) {
-            const uint32_t pkt = worklist[16 * t + j];
-            if (pkt == 0xffffffffu) continue;
-            const uint32_t L = seal ? descs[pkt].len : descs[pkt].len - QGCM_OVERHEAD;
-            w += ((L + 15u) >> 4) + 4u;
-        }
-    }
-    work[t] = w;
+// rocprim's radix sort takes its merge-sort path up to 2^20 items by default (a block sort and ~20
+// merge launches, ~150 us for a 2^20-packet batch); Onesweep (a histogram, a scan and one pass per
+// 8-bit digit) is used for every size here.
+using SortConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+                                              rocprim::default_config, 0>;
+
+static hipError_t sort_pairs(void *tmp, size_t &bytes, const uint32_t *k_in, uint32_t *k_out, const uint32_t *v_in,
+                             uint32_t *v_out, uint32_t n, int end_bit, hipStream_t s) {
+    return rocprim::radix_sort_pairs<SortConfig>(tmp, bytes, k_in, k_out, v_in, v_out, (size_t)n, 0, end_bit, s);
 }
 
 size_t quad_worklist_bytes(uint32_t n, uint32_t max_keys, uint32_t *n_items_out) {
     const uint64_t cap = (uint64_t)n + 16ull * (n < max_keys ? n : max_keys);
     const uint32_t items = (uint32_t)((cap + 15) & ~15ull);
-    size_t cub = 0, scan = 0;
-    hipcub::DeviceRadixSort::SortPairs(nullptr, cub, (uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr,
-                                       (uint32_t *)nullptr, (int)n);
-    hipcub::DeviceScan::ExclusiveSum(nullptr, scan, (uint32_t *)nullptr, (uint64_t *)nullptr, (int)(items / 16 + 1));
-    if (scan > cub) cub = scan;
+    size_t cub = 0;
+    sort_pairs(nullptr, cub, nullptr, nullptr, nullptr, nullptr, n, 32, 0);
     if (n_items_out) *n_items_out = items;
     // keys in/out, vals in/out, counts, start, pstart, run counters, runs, worklist, tile keys, short
-    // tiles, tile work, its exclusive scan, tile counter + run count + short count, cub temp (256-B
-    // aligned pieces)
+    // tiles, tile counter + run count + short count, sort temp (256-B aligned pieces)
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-    const size_t tiles1 = items / 16 + 1;
     return 4 * al(4ull * n) + 4 * al(4ull * max_keys) + al(8ull * max_keys) + al(4ull * items) + 2 * al(items / 4) +
-           al(4 * tiles1) + al(8 * tiles1) + al(16) + al(cub);
+           al(16) + al(cub);
 }
 
 hipError_t launch_quad_worklist(const qgcm_desc *descs, uint32_t n, uint32_t max_keys, const uint8_t *key_valid,
@@ -170,26 +157,26 @@ hipError_t launch_quad_worklist(const qgcm_desc *descs, uint32_t n, uint32_t max
     uint32_t *k_out = (uint32_t *)p; p += al(4ull * n);
     uint32_t *v_in = (uint32_t *)p;  p += al(4ull * n);
     uint32_t *v_out = (uint32_t *)p; p += al(4ull * n);
+    // zeroed together: counts, run counters, tile counter + run count + short count
+    char *zero0 = p;
     uint32_t *counts = (uint32_t *)p; p += al(4ull * max_keys);
-    uint32_t *start = (uint32_t *)p;  p += al(4ull * max_keys);
-    uint32_t *pstart = (uint32_t *)p; p += al(4ull * max_keys);
     uint32_t *run_next = (uint32_t *)p; p += al(4ull * max_keys);
-    uint2 *runs = (uint2 *)p; p += al(8ull * max_keys);
+    uint32_t *counter = (uint32_t *)p;  p += al(16);  // [0] tile counter, [1] run count, [2] short tiles
+    const size_t zero_bytes = (size_t)(p - zero0);
+    // all ones together: worklist (padding entries) and tile keys
+    char *ones0 = p;
     uint32_t *worklist = (uint32_t *)p; p += al(4ull * items);
     uint32_t *tile_keys = (uint32_t *)p; p += al(items / 4);
+    const size_t ones_bytes = (size_t)(p - ones0);
+    uint32_t *start = (uint32_t *)p;  p += al(4ull * max_keys);
+    uint32_t *pstart = (uint32_t *)p; p += al(4ull * max_keys);
+    uint2 *runs = (uint2 *)p; p += al(8ull * max_keys);
     uint32_t *short_tiles = (uint32_t *)p; p += al(items / 4);
-    const uint32_t ntiles = items / 16;
-    uint32_t *work = (uint32_t *)p; p += al(4ull * (ntiles + 1));
-    uint64_t *work_x = (uint64_t *)p; p += al(8ull * (ntiles + 1));
-    uint32_t *counter = (uint32_t *)p;  p += al(16);  // [0] tile counter, [1] run count, [2] short tiles
     void *cub_tmp = p;
     size_t cub_bytes = need - (size_t)(p - static_cast<char *>(ws));
     hipError_t e;
-    if ((e = hipMemsetAsync(counts, 0, 4ull * max_keys, s)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(worklist, 0xff, 4ull * items, s)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(tile_keys, 0xff, items / 4, s)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(counter, 0, 16, s)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(run_next, 0, 4ull * max_keys, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(zero0, 0, zero_bytes, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(ones0, 0xff, ones_bytes, s)) != hipSuccess) return e;
     const int bs = 256, g = (int)((n + bs - 1) / bs);
     if (n) hipLaunchKernelGGL(qwl_keys_kernel, dim3(g), dim3(bs), 0, s, descs, n, max_keys, key_valid, seal, k_in,
                                  v_in);
@@ -197,9 +184,7 @@ hipError_t launch_quad_worklist(const qgcm_desc *descs, uint32_t n, uint32_t max
     // only the bits a valid key can use, plus one so that excluded entries (all ones) sort last
     int end_bit = kLenBits + 1;
     while (end_bit < 32 && (1ull << (end_bit - kLenBits - 1)) < max_keys) ++end_bit;
-    if ((e = hipcub::DeviceRadixSort::SortPairs(cub_tmp, cub_bytes, k_in, k_out, v_in, v_out, (int)n, 0, end_bit,
-                                                s)) != hipSuccess)
-        return e;
+    if ((e = sort_pairs(cub_tmp, cub_bytes, k_in, k_out, v_in, v_out, n, end_bit, s)) != hipSuccess) return e;
     if (n) {
         hipLaunchKernelGGL(qwl_first_kernel, dim3(g), dim3(bs), 0, s, k_out, n, start);
         hipLaunchKernelGGL(qwl_count_kernel, dim3(g), dim3(bs), 0, s, k_out, n, start, counts);
@@ -209,15 +194,8 @@ hipError_t launch_quad_worklist(const qgcm_desc *descs, uint32_t n, uint32_t max
     if (n) hipLaunchKernelGGL(qwl_scatter_kernel, dim3(g), dim3(bs), 0, s, k_out, v_out, n, start, pstart, worklist,
                                  tile_keys);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(qwl_tile_work_kernel, dim3((ntiles + 1 + bs - 1) / bs), dim3(bs), 0, s, worklist, descs,
-                       ntiles, seal, work);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    cub_bytes = need - (size_t)(static_cast<char *>(cub_tmp) - static_cast<char *>(ws));
-    if ((e = hipcub::DeviceScan::ExclusiveSum(cub_tmp, cub_bytes, work, work_x, (int)(ntiles + 1), s)) != hipSuccess)
-        return e;
     out->worklist = worklist;
     out->tile_keys = tile_keys;
-    out->tile_work = work_x;
     out->runs = runs;
     out->run_next = run_next;
     out->nruns = counter + 1;
