@@ -1282,7 +1282,7 @@ gcm_quad_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
 // [13K, 77K) Te, then the control words: 77 KiB per workgroup, two 16-wave workgroups per CU as the
 // single-key kernel.
 constexpr uint32_t kSegCtl = kG5Bytes + kTeBytes;  // run, phase key (LDS words)
-constexpr uint32_t kSegLds = kSegCtl + 16u;  // two control slots of (run, key)
+constexpr uint32_t kSegLds = kSegCtl + 16u;
 constexpr uint32_t kSegDone = 0xffffffffu;
 
 __device__ __forceinline__ volatile lds_u32 *seg_ctl(uint32_t i) { return (volatile lds_u32 *)(size_t)(kSegCtl + 4u * i); }
@@ -1331,7 +1331,7 @@ __device__ unsigned long long g_seg_stats[4096 * 8];
 #define QGCM_SEG_HELP_MIN 16
 #endif
 __device__ __forceinline__ void seg_next_phase(const Batch &b, uint32_t &r, uint32_t nruns, bool &helping,
-                                               uint32_t lane, uint32_t slot) {
+                                               uint32_t lane) {
     uint32_t found = kSegDone;
     if (!helping) {
         uint32_t c = 0;
@@ -1374,19 +1374,14 @@ __device__ __forceinline__ void seg_next_phase(const Batch &b, uint32_t &r, uint
         key = b.tile_keys[b.runs[found].x];
     }
     if (lane == 0) {
-        *seg_ctl(2 * slot) = found;
-        *seg_ctl(2 * slot + 1) = key;
+        *seg_ctl(0) = found;
+        *seg_ctl(1) = key;
     }
 }
 
-// Side-build knobs for A/Bs (tools/ab_libs_desc.py): QGCM_SEG_EARLY = wave 0 finds the next run as
-// soon as its own tiles are done instead of after the barrier; QGCM_SEG_PREFETCH = each wave claims
-// its next tile before working on the current one.
-#ifndef QGCM_SEG_EARLY
-#define QGCM_SEG_EARLY 0
-#endif
-#ifndef QGCM_SEG_PREFETCH
-#define QGCM_SEG_PREFETCH 0
+// Side-build knob for A/Bs (tools/ab_libs_desc.py): QGCM_SEG_CLAIM tiles per atomic claim.
+#ifndef QGCM_SEG_CLAIM
+#define QGCM_SEG_CLAIM 1
 #endif
 
 template <bool kSeal>
@@ -1417,33 +1412,21 @@ gcm_seg_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
         const uint32_t i = wave_lower_bound(0u, nruns, lane, [&](uint32_t j) { return j == nruns || b.runs[j].x > t; });
         r = i ? i - 1u : 0u;
         SEG_STAT_ADD(6, r);
-        if (QGCM_SEG_EARLY) {
-            [[maybe_unused]] const unsigned long long t0 = SEG_NOW();
-            seg_next_phase(b, r, nruns, helping, lane, 0u);
-            SEG_STAT_ADD(7, SEG_NOW() - t0);
-        }
     }
     __syncthreads();
     [[maybe_unused]] unsigned long long t_idle = SEG_NOW();
     if (wave == 0) SEG_STAT_ADD(2, t_idle);
     [[maybe_unused]] uint32_t ntile_stat = 0;
-    // QGCM_SEG_EARLY: phase p's run and key are in control slot p % 2.  Wave 0 publishes phase p + 1's
-    // as soon as its own tiles of phase p are done (the run is then exhausted), while the other waves
-    // finish theirs.  Slot (p + 1) % 2 was last read in phase p - 1, before the barrier that began
-    // phase p, so the write cannot race a reader.  Otherwise wave 0 finds the run after the barrier
-    // (slot 0 only).
-    for (uint32_t slot = 0;; slot = QGCM_SEG_EARLY ? slot ^ 1u : 0u) {
-        if (!QGCM_SEG_EARLY) {
-            if (wave == 0) {
-                [[maybe_unused]] const unsigned long long t0 = SEG_NOW();
-                seg_next_phase(b, r, nruns, helping, lane, 0u);
-                SEG_STAT_ADD(7, SEG_NOW() - t0);
-            }
-            __syncthreads();
+    for (;;) {
+        if (wave == 0) {
+            [[maybe_unused]] const unsigned long long t0 = SEG_NOW();
+            seg_next_phase(b, r, nruns, helping, lane);
+            SEG_STAT_ADD(7, SEG_NOW() - t0);
         }
+        __syncthreads();
         if (wave == 0) SEG_STAT_ADD(0, 1);
-        const uint32_t run = __builtin_amdgcn_readfirstlane(*seg_ctl(2 * slot));
-        const uint32_t key = __builtin_amdgcn_readfirstlane(*seg_ctl(2 * slot + 1));
+        const uint32_t run = __builtin_amdgcn_readfirstlane(*seg_ctl(0));
+        const uint32_t key = __builtin_amdgcn_readfirstlane(*seg_ctl(1));
         if (run == kSegDone) break;
         if (key != table_key) {
             g5_fill(b.gh_table + (size_t)key * kGhEntries + kGhH4, threadIdx.x, kT);
@@ -1454,16 +1437,14 @@ gcm_seg_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
         SEG_STAT_ADD(4, t_busy - t_idle);
         const uint2 rt = b.runs[run];
         const Tab2F e3 = {{rk_table + (size_t)key * kRkWords, rk_table + (size_t)key * kRkWords + 64}, {lb, m8}, mf8};
-        uint32_t t = 0;
-        if (QGCM_SEG_PREFETCH) {
-            if (lane == 0) t = atomicAdd(b.run_next + run, 1u);
-            t = rt.x + __builtin_amdgcn_readfirstlane(__shfl(t, 0));
-        }
-        for (;;) {
-            uint32_t nx = 0;
-            if (lane == 0) nx = atomicAdd(b.run_next + run, 1u);
-            nx = rt.x + __builtin_amdgcn_readfirstlane(__shfl(nx, 0));
-            if (!QGCM_SEG_PREFETCH) t = nx;
+        // QGCM_SEG_CLAIM consecutive tiles per atomic (1 unless set in a side build)
+        for (uint32_t t = 0, left = 0;; ++t, --left) {
+            if (left == 0) {
+                uint32_t nx = 0;
+                if (lane == 0) nx = atomicAdd(b.run_next + run, (uint32_t)QGCM_SEG_CLAIM);
+                t = rt.x + __builtin_amdgcn_readfirstlane(__shfl(nx, 0));
+                left = QGCM_SEG_CLAIM;
+            }
             if (t >= rt.y) break;
             const uint32_t pkt = b.worklist[t * 16u + qd];
             if (pkt != 0xffffffffu) {  // the padding of a key run's last tile
@@ -1472,15 +1453,9 @@ gcm_seg_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
                 quad_packet<kSeal, false, true, true>(b, e3, pkt, dsc.offset, L, key, m, 0u, 0u);
             }
             ++ntile_stat;
-            if (QGCM_SEG_PREFETCH) t = nx;
         }
         t_idle = SEG_NOW();
         SEG_STAT_ADD(5, t_idle - t_busy);
-        if (QGCM_SEG_EARLY && wave == 0) {
-            [[maybe_unused]] const unsigned long long t0 = SEG_NOW();
-            seg_next_phase(b, r, nruns, helping, lane, slot ^ 1u);
-            SEG_STAT_ADD(7, SEG_NOW() - t0);
-        }
         __syncthreads();  // the table and the control words are free again
     }
     SEG_STAT_ADD(1, ntile_stat);

@@ -1,6 +1,7 @@
 """A/B whole builds of libqgcm on the config-3 workload (descriptor batches, 1024 keys, lengths
 U{64..9000}) in ONE process, interleaved rounds.  Every build seals the same batch; the sealed bytes
-must agree.  Usage: python tools/ab_libs_desc.py lib1.so lib2.so [...] [--rounds R]
+must agree.  Usage: python tools/ab_libs_desc.py lib1.so lib2.so [...] [--rounds R]; AB_KEYS=k draws the
+key indices from the first k keys (default 1024), AB_LEN=L gives every packet length L.
 """
 import ctypes as C
 import os
@@ -33,7 +34,9 @@ for path in args:
     libs[path] = (L, ctx)
 
 lens = rng.integers(64, 9001, size=N, dtype=np.int64)
-kidx = rng.integers(0, NK, size=N, dtype=np.int64)
+kidx = rng.integers(0, int(os.environ.get("AB_KEYS", NK)), size=N, dtype=np.int64)
+if int(os.environ.get("AB_LEN", 0)):
+    lens[:] = int(os.environ["AB_LEN"])
 slot = (4 + lens + 28 + 3) & ~3
 offs = np.zeros(N, dtype=np.int64)
 offs[1:] = np.cumsum(slot)[:-1]
