@@ -1,0 +1,148 @@
+"""Seeded random descriptor batches on the GPU against the oracle (crypto/aes.go:41-62 per packet,
+common/mapping.go:90-99 per-peer keys).
+
+Each case draws a batch shape the fixed tests do not: a skewed key mix (a few keys with runs long
+enough for the segmented kernel's shared-table path, many with a handful of packets for its
+per-wave pass), lengths from 0 to 9000 B with the counter-segment edges, slots packed at 4-B
+alignment with random gaps, AAD of 0 or 4 bytes, and invalid packets mixed in (unset key slots,
+key indices past max_keys, opens shorter than 28 B) that must come back status 0 with their slot
+untouched.  Seal is compared byte for byte with the C restatement; then a tampered sample is
+opened (status 0 and zeroed plaintext for the tampered, the rest authentic).  Every case runs
+through the default descriptor kernel (variant 14 + 13) and the per-wave kernel (variant 7).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+MAX_KEYS = 4096
+SET_KEYS = 3000  # slots [0, 3000) hold keys; [3000, 4096) were never set
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as T
+
+    if not T.cuda.is_available():
+        pytest.skip("no GPU")
+    return T
+
+
+@pytest.fixture(scope="module")
+def fuzz_keys():
+    return np.random.default_rng(0x5EED00F0).bytes(32 * MAX_KEYS)
+
+
+@pytest.fixture(scope="module")
+def fuzz_ctxs(torch, fuzz_keys):
+    from quantum_amd.crypto import Context
+
+    out = {}
+    old = os.environ.get("QGCM_DESC_VARIANT")
+    try:
+        for v in (None, 7):
+            if v is None:
+                os.environ.pop("QGCM_DESC_VARIANT", None)
+            else:
+                os.environ["QGCM_DESC_VARIANT"] = str(v)
+            c = Context(device=0, max_keys=MAX_KEYS)
+            c.set_keys(0, fuzz_keys[:32 * SET_KEYS])
+            out["default" if v is None else v] = c
+    finally:
+        if old is None:
+            os.environ.pop("QGCM_DESC_VARIANT", None)
+        else:
+            os.environ["QGCM_DESC_VARIANT"] = old
+    yield out
+    for c in out.values():
+        c.close()
+
+
+SIZES = (1, 17, 700, 3000, 9000, 24000, 16000, 5000)
+
+
+def draw_case(case: int):
+    rng = np.random.default_rng(0xF0220000 + case)
+    n = SIZES[case % len(SIZES)]
+    # skewed key mix: a few hot keys (long runs) and a long tail
+    hot = rng.integers(0, SET_KEYS, size=int(rng.integers(1, 4)))
+    tail = rng.integers(0, SET_KEYS, size=n)
+    kidx = np.where(rng.random(n) < rng.uniform(0.2, 0.9), hot[rng.integers(0, len(hot), size=n)], tail)
+    kidx = kidx.astype(np.uint32)
+    lens = rng.integers(0, 9001, size=n).astype(np.uint32)
+    edges = np.array([0, 1, 15, 16, 17, 1350, 4064, 4079, 4080, 4081, 4096, 8191, 8192, 9000], dtype=np.uint32)
+    pick = rng.random(n) < 0.2
+    lens[pick] = edges[rng.integers(0, len(edges), size=int(pick.sum()))]
+    # invalid packets: an unset key slot or a key index past max_keys
+    bad_key = rng.random(n) < 0.02
+    kidx[bad_key] = np.where(rng.random(int(bad_key.sum())) < 0.5,
+                             rng.integers(SET_KEYS, MAX_KEYS, size=int(bad_key.sum())),
+                             MAX_KEYS + rng.integers(0, 1000, size=int(bad_key.sum()))).astype(np.uint32)
+    gap = rng.integers(0, 5, size=n).astype(np.int64) * 4
+    slot = ((4 + lens.astype(np.int64) + 28 + 3) & ~3) + gap
+    offs = np.zeros(n, dtype=np.uint64)
+    offs[1:] = np.cumsum(slot)[:-1].astype(np.uint64)
+    size = int(offs[-1]) + int(slot[-1]) + 64
+    aad_len = int(rng.choice([0, 4]))
+    return rng, n, kidx, lens, offs, slot, size, aad_len, ~bad_key
+
+
+@pytest.mark.parametrize("variant", ["default", 7])
+@pytest.mark.parametrize("seed", range(len(SIZES)))
+def test_descriptor_fuzz_vs_oracle(torch, fuzz_ctxs, fuzz_keys, variant, seed):
+    from quantum_amd import batch
+
+    ctx = fuzz_ctxs[variant]
+    rng, n, kidx, lens, offs, slot, size, aad_len, valid = draw_case(seed)
+    plain = np.frombuffer(rng.bytes(size), dtype=np.uint8).copy()
+    nonces = np.frombuffer(rng.bytes(12 * n), dtype=np.uint8).copy()
+
+    # expected seal: the oracle on the valid packets; invalid slots stay as they were
+    ref = plain.copy()
+    vi = np.nonzero(valid)[0]
+    if len(vi):
+        O.aesgo_seal_descs(fuzz_keys, ref, np.ascontiguousarray(offs[vi]), np.ascontiguousarray(lens[vi]),
+                           np.ascontiguousarray(kidx[vi]), np.ascontiguousarray(nonces.reshape(n, 12)[vi]).reshape(-1),
+                           aad_len, 8)
+    arena = torch.from_numpy(plain.copy()).cuda()
+    status = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    batch.seal_batch(ctx, arena, batch.make_descs(offs, lens, kidx, "cuda"), n, torch.from_numpy(nonces).cuda(),
+                     aad_len=aad_len, status=status)
+    st = status.cpu().numpy()
+    assert np.array_equal(st, valid.astype(np.uint8)), f"seal status: {int((st != valid).sum())} packets differ"
+    got = arena.cpu().numpy()
+    if not np.array_equal(got, ref):
+        bad = [int(i) for i in range(n) if not np.array_equal(got[offs[i]:offs[i] + slot[i]], ref[offs[i]:offs[i] + slot[i]])]
+        pytest.fail(f"seed {seed}: {len(bad)} of {n} slots differ, first {bad[:5]} keys {kidx[bad[:5]].tolist()} "
+                    f"lengths {lens[bad[:5]].tolist()}")
+
+    # open: tamper a sample (a ciphertext, tag or nonce byte), and shorten a few descriptors below 28
+    tampered = ref.copy()
+    tam = np.zeros(n, dtype=bool)
+    for i in rng.choice(n, size=max(1, n // 50), replace=False):
+        L = int(lens[i])
+        pos = int(offs[i]) + 4 + int(rng.integers(0, L + 28))
+        tampered[pos] ^= 1 << int(rng.integers(0, 8))
+        tam[i] = True
+    olens = lens.astype(np.int64) + 28
+    short = rng.random(n) < 0.01
+    olens[short] = rng.integers(0, 28, size=int(short.sum()))
+    olens = olens.astype(np.uint32)
+    ok = valid & ~short
+    exp = tampered.copy()
+    ost = np.zeros(n, dtype=np.uint8)
+    oi = np.nonzero(ok)[0]
+    if len(oi):
+        sub = np.zeros(len(oi), dtype=np.uint8)
+        O.aesgo_open_descs(fuzz_keys, exp, np.ascontiguousarray(offs[oi]), np.ascontiguousarray(olens[oi]),
+                           np.ascontiguousarray(kidx[oi]), sub, aad_len, 8)
+        ost[oi] = sub
+    assert not np.any(ost[ok & ~tam] == 0), "oracle rejected an untampered packet"
+    arena.copy_(torch.from_numpy(tampered).cuda())
+    batch.open_batch(ctx, arena, batch.make_descs(offs, olens, kidx, "cuda"), n, aad_len=aad_len, status=status)
+    assert np.array_equal(status.cpu().numpy(), ost)
+    assert np.array_equal(arena.cpu().numpy(), exp)
