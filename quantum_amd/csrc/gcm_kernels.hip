@@ -37,7 +37,25 @@ struct __attribute__((aligned(4))) W4 {
 
 // Streamed payload block (read once per pass).  Serving the final-round S-box from L1 instead of
 // LDS, with these loads non-temporal, measured 5% slower: the LDS path stays.
-__device__ __forceinline__ W4 load_block(const W4 *p) { return *p; }
+// QGCM_NT_DATA (side builds, A/B only): 1 = payload loads non-temporal, 2 = stores, 3 = both.
+#ifndef QGCM_NT_DATA
+#define QGCM_NT_DATA 0
+#endif
+typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(4)));
+__device__ __forceinline__ W4 load_block(const W4 *p) {
+    if constexpr ((QGCM_NT_DATA & 1) != 0) {
+        const u32x4u v = __builtin_nontemporal_load(reinterpret_cast<const u32x4u *>(p));
+        return W4{v.x, v.y, v.z, v.w};
+    }
+    return *p;
+}
+__device__ __forceinline__ void store_block(W4 *p, const W4 &v) {
+    if constexpr ((QGCM_NT_DATA & 2) != 0) {
+        __builtin_nontemporal_store(u32x4u{v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4u *>(p));
+        return;
+    }
+    *p = v;
+}
 
 __device__ __forceinline__ uint32_t perm(uint32_t s0, uint32_t s1, uint32_t sel) {
     return __builtin_amdgcn_perm(s0, s1, sel);
@@ -1006,7 +1024,7 @@ __device__ __forceinline__ void quad_packet(const Batch &b, const Eng &eng, uint
         uint32_t k0, k1, k2, k3;
         eng.block(cc, ctr & 0xffu, k0, k1, k2, k3);
         const W4 out = {in.x ^ k0, in.y ^ k1, in.z ^ k2, in.w ^ k3};
-        *p = out;
+        store_block(p, out);
         const W4 &c = kSeal ? out : in;
         eng.template ghash<!kDesc>(z0, z1, z2, z3, gH4);
         z0 ^= c.x;
@@ -2098,12 +2116,9 @@ __device__ __forceinline__ uint8_t stream_byte(uint64_t seed, uint64_t b) {
     return (uint8_t)(splitmix_at(seed, b >> 3) >> (8 * (b & 7)));
 }
 
-// One thread per (slot, 4-byte group of the slot's first 4+L bytes).
-__global__ void fill_uniform_kernel(uint8_t *arena, uint64_t stride, uint32_t n, uint32_t len, uint32_t aad_word,
-                                    uint64_t seed_payload, uint8_t *nonces, uint64_t seed_nonce) {
-    const uint32_t groups = (4 + len + 3) / 4 + 3;  // +3 groups for the 12-byte nonce
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= (uint64_t)n * groups) return;
+__device__ __forceinline__ void fill_uniform_item(uint8_t *arena, uint64_t stride, uint32_t len, uint32_t groups,
+                                                  uint32_t aad_word, uint64_t seed_payload, uint8_t *nonces,
+                                                  uint64_t seed_nonce, uint64_t t) {
     const uint32_t slot = (uint32_t)(t / groups), g = (uint32_t)(t % groups);
     uint8_t *raw = arena + (uint64_t)slot * stride;
     const uint32_t dgroups = groups - 3;
@@ -2123,6 +2138,17 @@ __global__ void fill_uniform_kernel(uint8_t *arena, uint64_t stride, uint32_t n,
             nonces[pos] = stream_byte(seed_nonce, pos);
         }
     }
+}
+
+// One work item per (slot, 4-byte group of the slot's first 4+L bytes), grid-stride: a dispatch's
+// work-item count is a 32-bit field, and n x groups passes 2^32 at ~12.6 M slots of 1350 B (an
+// unbounded grid silently filled only the first 2^32 items).
+__global__ void fill_uniform_kernel(uint8_t *arena, uint64_t stride, uint32_t n, uint32_t len, uint32_t aad_word,
+                                    uint64_t seed_payload, uint8_t *nonces, uint64_t seed_nonce) {
+    const uint32_t groups = (4 + len + 3) / 4 + 3;  // +3 groups for the 12-byte nonce
+    const uint64_t total = (uint64_t)n * groups, step = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += step)
+        fill_uniform_item(arena, stride, len, groups, aad_word, seed_payload, nonces, seed_nonce, t);
 }
 
 // Streaming copy, 16 B per lane, grid-stride: the achievable-HBM reference the roofline is also
@@ -2196,9 +2222,9 @@ hipError_t launch_fill_uniform(uint8_t *arena, uint64_t stride, uint32_t n, uint
     const uint64_t total = (uint64_t)n * groups;
     if (total == 0) return hipSuccess;
     const int bs = 256;
-    const uint64_t g = (total + bs - 1) / bs;
-    hipLaunchKernelGGL(fill_uniform_kernel, dim3((uint32_t)g), dim3(bs), 0, s, arena, stride, n, len, aad_word,
-                       seed_payload, nonces, seed_nonce);
+    const uint64_t want = (total + bs - 1) / bs, cap = 1u << 20;  // 2^28 work items per pass at most
+    hipLaunchKernelGGL(fill_uniform_kernel, dim3((uint32_t)(want < cap ? want : cap)), dim3(bs), 0, s, arena, stride, n,
+                       len, aad_word, seed_payload, nonces, seed_nonce);
     return hipGetLastError();
 }
 
