@@ -4,7 +4,8 @@ Each variant is its own qgcm context (QGCM_DESC_VARIANT is read at qgcm_create) 
 keys.  Correctness: every variant's sealed arena must equal the first variant's byte for byte.
 Usage: python tools/ab_desc.py 7,10,8 [rounds]; an entry v:cN runs variant v with QGCM_DESC_CHUNK=N
 (packets per sorted chunk), e.g. 7,7:c131072,7:c262144.  AB_KEYS=k draws key indices from k keys
-(default 1024), AB_LEN=L gives every packet length L (default U{64..9000}).
+(default 1024), AB_LEN=L gives every packet length L (default U{64..9000}), AB_ALIGN=A aligns every slot
+to A bytes (default 4).
 """
 import os
 import statistics
@@ -36,7 +37,8 @@ lens = rng.integers(64, 9001, size=N, dtype=np.int64)
 kidx = rng.integers(0, NUSE, size=N, dtype=np.int64)
 if FIXED_LEN:
     lens[:] = FIXED_LEN
-slot = (4 + lens + 28 + 3) & ~3
+ALIGN = int(os.environ.get("AB_ALIGN", 4))  # slot alignment in bytes (4 = packed, as config 3)
+slot = (4 + lens + 28 + ALIGN - 1) & ~(ALIGN - 1)
 offs = np.zeros(N, dtype=np.int64)
 offs[1:] = np.cumsum(slot)[:-1]
 total = int(offs[-1] + slot[-1])
