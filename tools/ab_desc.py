@@ -5,7 +5,8 @@ keys.  Correctness: every variant's sealed arena must equal the first variant's 
 Usage: python tools/ab_desc.py 7,10,8 [rounds]; an entry v:cN runs variant v with QGCM_DESC_CHUNK=N
 (packets per sorted chunk), e.g. 7,7:c131072,7:c262144.  AB_KEYS=k draws key indices from k keys
 (default 1024), AB_LEN=L gives every packet length L (default U{64..9000}), AB_ALIGN=A aligns every slot
-to A bytes (default 4).
+to A bytes (default 4), AB_SHUFFLE=1 lists the descriptors in a random order,
+AB_KEYSORTED=1 lays the slots out in (key, length descending) order.
 """
 import os
 import statistics
@@ -37,6 +38,9 @@ lens = rng.integers(64, 9001, size=N, dtype=np.int64)
 kidx = rng.integers(0, NUSE, size=N, dtype=np.int64)
 if FIXED_LEN:
     lens[:] = FIXED_LEN
+if int(os.environ.get("AB_KEYSORTED", 0)):  # lay the slots out in (key, length descending) order
+    o = np.lexsort((-lens, kidx))
+    lens, kidx = lens[o], kidx[o]
 ALIGN = int(os.environ.get("AB_ALIGN", 4))  # slot alignment in bytes (4 = packed, as config 3)
 slot = (4 + lens + 28 + ALIGN - 1) & ~(ALIGN - 1)
 offs = np.zeros(N, dtype=np.int64)
@@ -46,8 +50,10 @@ plain = torch.randint(0, 256, (total + 64,), dtype=torch.uint8, device="cuda")
 arena = plain.clone()
 nonces = torch.randint(0, 256, (12 * N,), dtype=torch.uint8, device="cuda")
 status = torch.zeros(N, dtype=torch.uint8, device="cuda")
-d_seal = batch.make_descs(offs, lens, kidx, "cuda")
-d_open = batch.make_descs(offs, lens + 28, kidx, "cuda")
+# AB_SHUFFLE=1: the descriptors in a random order (same slots): a tile then gathers scattered slots
+order = np.random.default_rng(7).permutation(N) if int(os.environ.get("AB_SHUFFLE", 0)) else np.arange(N)
+d_seal = batch.make_descs(offs[order], lens[order], kidx[order], "cuda")
+d_open = batch.make_descs(offs[order], lens[order] + 28, kidx[order], "cuda")
 ref = None
 for v, c in ctxs.items():
     arena.copy_(plain)
