@@ -1345,6 +1345,12 @@ __device__ unsigned long long g_seg_stats[4096 * 8];
 // A helper joins only a run with at least QGCM_SEG_HELP_MIN tiles left: fewer are finished by the
 // run's owner (a run's owner works on it until it is exhausted, so no tile is left behind) within
 // about one tile time, and joining would cost the helper a barrier and a table refill for little work.
+// QGCM_SEG_START = 1: a helper's run search starts at a pseudo-random run (hash of the workgroup and
+// its last run) instead of at the run it just left, so helpers that search at the same moment do not
+// move as one convoy from run to run.
+#ifndef QGCM_SEG_START
+#define QGCM_SEG_START 1
+#endif
 #ifndef QGCM_SEG_HELP_MIN
 #define QGCM_SEG_HELP_MIN 16
 #endif
@@ -1361,6 +1367,10 @@ __device__ __forceinline__ void seg_next_phase(const Batch &b, uint32_t &r, uint
             helping = true;
     }
     if (helping) {
+        if (QGCM_SEG_START) {  // a pseudo-random start per search: helpers spread over the runs
+            const uint32_t h = (blockIdx.x * 0x9E3779B1u) ^ (r * 0x85EBCA6Bu + 0x632BE5ABu);
+            r = (uint32_t)(((uint64_t)(h ^ (h >> 15)) * nruns) >> 32);
+        }
         // four runs per lane per step (their loads in flight together): 256 runs per step
         for (uint32_t base = 0; base < nruns; base += 256u) {
             bool left[4];
