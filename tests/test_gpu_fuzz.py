@@ -146,3 +146,47 @@ def test_descriptor_fuzz_vs_oracle(torch, fuzz_ctxs, fuzz_keys, variant, seed):
     batch.open_batch(ctx, arena, batch.make_descs(offs, olens, kidx, "cuda"), n, aad_len=aad_len, status=status)
     assert np.array_equal(status.cpu().numpy(), ost)
     assert np.array_equal(arena.cpu().numpy(), exp)
+
+
+def test_descriptor_batch_4m_packets(torch, fuzz_ctxs, fuzz_keys):
+    """One descriptor batch of 2^22 packets (64 keys, U{64..2000} B, 4.4 GB of slots): the worklist
+    sort, the run table and the per-run tile queues at four times config 3's packet count.  A sample
+    of 4096 packets is compared with the oracle after sealing; after opening every packet must
+    authenticate and the sampled payloads must be back to their plaintext."""
+    from quantum_amd import batch
+
+    ctx = fuzz_ctxs["default"]
+    n = 1 << 22
+    rng = np.random.default_rng(0xF0224000)
+    kidx = rng.integers(0, 64, size=n).astype(np.uint32)
+    lens = rng.integers(64, 2001, size=n).astype(np.uint32)
+    slot = (4 + lens.astype(np.int64) + 28 + 3) & ~3
+    offs = np.zeros(n, dtype=np.uint64)
+    offs[1:] = np.cumsum(slot)[:-1].astype(np.uint64)
+    size = int(offs[-1]) + int(slot[-1]) + 64
+    arena = torch.randint(0, 256, (size,), dtype=torch.uint8, device="cuda")
+    nonces = torch.randint(0, 256, (12 * n,), dtype=torch.uint8, device="cuda")
+
+    sample = np.sort(rng.choice(n, size=4096, replace=False))
+    plain = {int(i): arena[int(offs[i]):int(offs[i]) + int(slot[i])].cpu().numpy().copy() for i in sample}
+    status = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    batch.seal_batch(ctx, arena, batch.make_descs(offs, lens, kidx, "cuda"), n, nonces, status=status)
+    assert bool(status.bool().all())
+    nz = nonces.cpu().numpy()
+    for i in sample:
+        i = int(i)
+        L = int(lens[i])
+        buf = plain[i].copy()
+        O.aesgo_seal_descs(fuzz_keys, buf, np.zeros(1, dtype=np.uint64), np.array([L], dtype=np.uint32),
+                           np.array([kidx[i]], dtype=np.uint32), np.ascontiguousarray(nz[12 * i:12 * i + 12]), 4, 1)
+        got = arena[int(offs[i]):int(offs[i]) + int(slot[i])].cpu().numpy()
+        assert np.array_equal(got[:4 + L + 28], buf[:4 + L + 28]), f"packet {i} (key {kidx[i]}, {L} B)"
+    batch.open_batch(ctx, arena, batch.make_descs(offs, lens + 28, kidx, "cuda"), n, status=status)
+    assert bool(status.bool().all())
+    for i in sample:
+        i = int(i)
+        L = int(lens[i])
+        got = arena[int(offs[i]):int(offs[i]) + 4 + L].cpu().numpy()
+        assert np.array_equal(got, plain[i][:4 + L])
+    del arena, nonces, status
+    torch.cuda.empty_cache()
