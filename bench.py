@@ -12,8 +12,15 @@ loop body (crypto/crypto_test.go:103-131) over a batch.
 Before the W warmup steps the GPU runs the same step for --settle-ms of wall time (clock settle,
 DESIGN.md s5 "Clock ramp": after an idle start the clocks take ~70 ms of load to come up).
 
+At N = 1, after the headline, the same process also times the other BASELINE configs into
+`extra_configs` (never `value`): config 3 on the parity-checked workload (quantum_amd/workloads.py,
+with its golden arena digests), config 2 from pinned host memory (PCIe included) and config 5.
+
   python bench.py [--gpus N] [--steps K] [--warmup W]
-  torchrun --nproc-per-node N bench.py --gpus N ...
+  python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+
+`--gpus N` with N > 1 and no launcher starts torch.distributed.run with N ranks itself; under a
+launcher WORLD_SIZE must equal N (anything else exits non-zero).
 """
 from __future__ import annotations
 
@@ -23,6 +30,7 @@ import os
 import sys
 import time
 
+import numpy as np
 import torch
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -53,6 +61,8 @@ def parse() -> argparse.Namespace:
     p.add_argument("--len", type=int, default=1350, help="payload bytes per packet")
     p.add_argument("--stride", type=int, default=0, help="slot stride (0 = smallest 64-B multiple)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-extra", action="store_true", help="skip configs 3 / 5 and the host-memory rate (N=1)")
+    p.add_argument("--no-verify", action="store_true", help="skip config 3's arena digests")
     p.add_argument("--cpu-threads", type=int, default=0, help="0 = the CPU share this job was given")
     p.add_argument("--dist-backend", default="nccl", help="nccl (RCCL, default) or gloo (rehearsal)")
     p.add_argument("--one-device", action="store_true",
@@ -156,8 +166,214 @@ def pmc_traffic(kind: str, N: int, L: int, stride: int):
     return None, None, None
 
 
+def _sha256_device(t) -> str:
+    import hashlib
+
+    h = hashlib.sha256()
+    step = 1 << 28
+    for i in range(0, t.numel(), step):
+        h.update(memoryview(t[i:i + step].cpu().numpy()))
+    return h.hexdigest()
+
+
+def extra_config3(reps: int = 5, verify: bool = True) -> dict:
+    """BASELINE config 3 on the parity-checked workload (quantum_amd/workloads.py, the one
+    tests/test_gpu_config3.py compares with the oracle and tests/golden/config3_digest.json pins):
+    2^20 packets of U{64..9000} B under 1024 X25519 + PBKDF2 peer keys, device-resident descriptor
+    batches (qgcm_seal_batch / qgcm_open_batch: device worklist sort + segmented kernel).  Each call is
+    timed with HIP events on its stream (sort included).  verify: the arena's SHA-256 after the timed
+    seal/open pairs (the opened state) and after one more seal, against the golden digests."""
+    from quantum_amd import workloads as W
+
+    t0 = time.perf_counter()
+    keys = W.peer_keys()
+    t_keys = time.perf_counter() - t0
+    ctx = Context(device=0, max_keys=W.NKEYS)
+    ctx.set_keys(0, keys)
+    lens, kidx = W.lengths(), W.key_indices()
+    offs, size = W.layout(lens)
+    arena = W.device_arena(torch, size, offs, kidx)
+    nonces = torch.from_numpy(W.nonces()).cuda()
+    status = torch.zeros(W.N, dtype=torch.uint8, device="cuda")
+    d_seal = batch.make_descs(offs, lens, kidx, "cuda")
+    d_open = batch.make_descs(offs, lens.astype(np.int64) + 28, kidx, "cuda")
+    stream = torch.cuda.current_stream()
+    ok = True
+    for _ in range(2):
+        batch.seal_batch(ctx, arena, d_seal, W.N, nonces, status=status, stream=stream)
+        ok &= int(status.sum()) == W.N
+        batch.open_batch(ctx, arena, d_open, W.N, status=status, stream=stream)
+        ok &= int(status.sum()) == W.N
+    ts, to = [], []
+    for _ in range(reps):
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        e[0].record(stream)
+        batch.seal_batch(ctx, arena, d_seal, W.N, nonces, status=status, stream=stream)
+        e[1].record(stream)
+        batch.open_batch(ctx, arena, d_open, W.N, status=status, stream=stream)
+        e[2].record(stream)
+        torch.cuda.synchronize()
+        ok &= int(status.sum()) == W.N
+        ts.append(e[0].elapsed_time(e[1]))
+        to.append(e[1].elapsed_time(e[2]))
+    seal_ms, open_ms = float(np.median(ts)), float(np.median(to))
+    payload = int(lens.sum())
+    out = {"workload": "config3: 2^20 x U{64..9000} B, 1024 peer keys (quantum_amd/workloads.py)",
+           "packets": W.N, "keys": W.NKEYS, "payload_bytes": payload,
+           "value": round(2 * payload / ((seal_ms + open_ms) * 1e-3) / 2**30, 2), "unit": "GiB/s",
+           "seal_ms": round(seal_ms, 3), "open_ms": round(open_ms, 3), "reps": reps,
+           "timing": "HIP events around each qgcm_seal_batch / qgcm_open_batch call (worklist sort included)",
+           "frac_seal": round((2 * payload + 44 * W.N) / (seal_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+           "frac_open": round((2 * payload + 32 * W.N) / (open_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+           "status_ok": ok, "key_setup_host_s": round(t_keys, 3)}
+    if verify:
+        gold = json.load(open(os.path.join(ROOT, "tests", "golden", "config3_digest.json")))
+        out["digest_opened_ok"] = _sha256_device(arena) == gold["sha256_opened"]
+        batch.seal_batch(ctx, arena, d_seal, W.N, nonces, status=status, stream=stream)
+        out["digest_sealed_ok"] = _sha256_device(arena) == gold["sha256_sealed"]
+    del arena
+    ctx.close()
+    torch.cuda.empty_cache()
+    return out
+
+
+def extra_e2e(key: bytes, reps: int = 3) -> dict:
+    """Config 2 from pinned HOST memory: qgcm_seal_host / qgcm_open_host (H2D + kernels + D2H,
+    pipelined in 64 MiB chunks over three streams): the PCIe-inclusive rate (never `value`)."""
+    from quantum_amd import _lib
+    import ctypes as C
+
+    N, L = 1 << 20, 1350
+    stride = batch.slot_stride(L, align=64)
+    ctx = Context(device=0, max_keys=4)
+    ctx.set_key(0, key)
+    Lb = _lib.lib()
+    dev = torch.zeros(N * stride, dtype=torch.uint8, device="cuda")
+    non_d = torch.zeros(12 * N, dtype=torch.uint8, device="cuda")
+    batch.fill_uniform(dev, stride, N, L, int.from_bytes(AAD, "little"), 0x5EED0001, non_d, 0x5EED0002)
+    a_ptr, n_ptr = Lb.qgcm_host_alloc(N * stride), Lb.qgcm_host_alloc(12 * N)
+    host = np.frombuffer((C.c_uint8 * (N * stride)).from_address(a_ptr), np.uint8)
+    nons = np.frombuffer((C.c_uint8 * (12 * N)).from_address(n_ptr), np.uint8)
+    host[:] = dev.cpu().numpy()
+    nons[:] = non_d.cpu().numpy()
+    batch.seal_uniform(ctx, dev, stride, N, L, 0, non_d)  # the device path's result, for the check
+    rc = Lb.qgcm_seal_host(ctx.handle, a_ptr, stride, N, L, 0, n_ptr, 4, None)
+    same = bool(np.array_equal(host, dev.cpu().numpy()))
+    del dev, non_d
+    rc |= Lb.qgcm_open_host(ctx.handle, a_ptr, stride, N, L + 28, 0, 4, None)
+    ts, to = [], []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        rc |= Lb.qgcm_seal_host(ctx.handle, a_ptr, stride, N, L, 0, n_ptr, 4, None)
+        t1 = time.perf_counter()
+        rc |= Lb.qgcm_open_host(ctx.handle, a_ptr, stride, N, L + 28, 0, 4, None)
+        t2 = time.perf_counter()
+        ts.append(t1 - t0)
+        to.append(t2 - t1)
+    s, o = float(np.median(ts)), float(np.median(to))
+    del host, nons
+    Lb.qgcm_host_free(a_ptr)
+    Lb.qgcm_host_free(n_ptr)
+    ctx.close()
+    torch.cuda.empty_cache()
+    return {"workload": f"config2 from pinned host memory: {N} x {L} B, H2D + seal/open + D2H",
+            "value": round(2 * N * L / (s + o) / 2**30, 2), "unit": "GiB/s", "seal_s": round(s, 4),
+            "open_s": round(o, 4), "pcie_GBps_each_way": round(N * stride / ((s + o) / 2) / 1e9, 2),
+            "matches_device_path": same, "status_ok": rc == 0, "reps": reps}
+
+
+def extra_config5(key: bytes, threads: int, reps: int = 3) -> dict:
+    """BASELINE config 5: snappy compress -> seal, then open -> uncompress, 2^20 x 1350 B packets in
+    pinned host memory (each packet's first half seeded random bytes, second half a repeated HTTP
+    request line), host codec workers overlapped with PCIe copies and the device
+    (qgcm_compress_seal_host / qgcm_open_uncompress_host; copies included)."""
+    from quantum_amd import _lib
+    import ctypes as C
+
+    N, L, stride = 1 << 20, 1350, 1472  # stride = common.MaxPacketLength (the Payload.Raw buffer)
+    ctx = Context(device=0, max_keys=4)
+    ctx.set_key(0, key)
+    Lb = _lib.lib()
+    a_ptr, n_ptr = Lb.qgcm_host_alloc(N * stride), Lb.qgcm_host_alloc(12 * N)
+    host = np.frombuffer((C.c_uint8 * (N * stride)).from_address(a_ptr), np.uint8).reshape(N, stride)
+    nons = np.frombuffer((C.c_uint8 * (12 * N)).from_address(n_ptr), np.uint8)
+    rng = np.random.default_rng(0x5EED0005)
+    host[:, :4] = np.frombuffer(AAD, np.uint8)
+    half = L // 2
+    host[:, 4:4 + half] = rng.integers(0, 256, (N, half), dtype=np.uint8)
+    line = np.frombuffer(b"GET /quantum/v1/peers HTTP/1.1\r\nHost: 10.99.0.1\r\n", np.uint8)
+    host[:, 4 + half:4 + L] = np.tile(line, (L - half) // len(line) + 1)[:L - half]
+    nons[:] = rng.integers(0, 256, 12 * N, dtype=np.uint8)
+    plain = host[:, :4 + L].copy()
+    lens = np.full(N, L, np.uint32)
+    ts, to, bad, sealed = [], [], 0, 0
+    for _ in range(reps):
+        lens[:] = L
+        t0 = time.perf_counter()
+        bad += batch.compress_seal_host(ctx, a_ptr, stride, N, lens, 0, n_ptr, threads=threads)
+        t1 = time.perf_counter()
+        sealed = int(lens.sum())
+        bad += batch.open_uncompress_host(ctx, a_ptr, stride, N, lens, 0, threads=threads)
+        t2 = time.perf_counter()
+        ts.append(t1 - t0)
+        to.append(t2 - t1)
+    restored = bool(np.array_equal(host[:, :4 + L], plain)) and bool((lens == L).all())
+    s, o = float(np.median(ts)), float(np.median(to))
+    del host, nons, plain
+    Lb.qgcm_host_free(a_ptr)
+    Lb.qgcm_host_free(n_ptr)
+    ctx.close()
+    return {"workload": f"config5: snappy -> AES-256-GCM chain, {N} x {L} B host packets, copies included",
+            "value": round(2 * N * L / (s + o) / 2**30, 2), "unit": "GiB/s of uncompressed payload",
+            "compress_seal_s": round(s, 4), "open_uncompress_s": round(o, 4),
+            "sealed_over_plain": round(sealed / (N * L), 4), "codec_threads": threads,
+            "codec": "this repo's C++ snappy block codec (host)", "status_ok": bad == 0, "restored": restored,
+            "reps": reps}
+
+
+def free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args: argparse.Namespace) -> None:
+    """`--gpus N` means N ranks.  Without a launcher around us (no WORLD_SIZE) and N > 1, start
+    torch.distributed.run with N local ranks on this script -- as a child process, before anything
+    here touches the GPU -- and exit with its status.  Under a launcher, WORLD_SIZE must equal N.
+    quantum runs one process per node (main.go:72-75); here the unit of independence is a GPU, so the
+    bench is one rank per GPU with no data-path collective."""
+    world = os.environ.get("WORLD_SIZE")
+    if world is not None:
+        if int(world) != args.gpus:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} ranks were launched")
+        return
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if args.gpus == 1:
+        return
+    if not args.one_device:
+        have = torch.cuda.device_count()  # does not initialise the GPU on this image
+        if have < args.gpus:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but only {have} GPU(s) are visible "
+                             "(--one-device --dist-backend gloo rehearses N ranks on one GPU)")
+    elif args.dist_backend == "nccl":
+        raise SystemExit("--one-device needs --dist-backend gloo (RCCL allows one rank per GPU)")
+    import subprocess
+
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__),
+           *sys.argv[1:]]
+    rc = subprocess.run(cmd, env=env).returncode
+    sys.exit(rc)
+
+
 def main() -> None:
     args = parse()
+    launch_ranks(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -295,10 +511,27 @@ def main() -> None:
             "kernels_ms": {"seal": round(seal_ms, 4), "open": round(open_ms, 4)},
             "status_ok": ok,
         }
+        host = host_cpus()
         if world == 1 and not args.no_cpu_baseline:
-            host = host_cpus()
             line["cpu_baseline"] = cpu_baseline(key, L, args.cpu_threads or host["share"], host)
+        if world == 1 and not args.no_extra:
+            # the other BASELINE configs, timed after the headline in this process (never `value`)
+            del arena_alloc, arena, nonces, status
+            torch.cuda.empty_cache()
+            extra = {}
+            for name, fn in (("config3", lambda: extra_config3(verify=not args.no_verify)),
+                             ("e2e_pinned_host", lambda: extra_e2e(key)),
+                             ("config5", lambda: extra_config5(key, args.cpu_threads or host["share"]))):
+                t0 = time.perf_counter()
+                try:
+                    extra[name] = fn()
+                except Exception as e:  # reported, and the run fails below: a broken config is not hidden
+                    extra[name] = {"error": f"{type(e).__name__}: {e}"}
+                extra[name]["wall_s"] = round(time.perf_counter() - t0, 2)
+            line["extra_configs"] = extra
         print(json.dumps(line), flush=True)
+        if any("error" in v for v in line.get("extra_configs", {}).values()):
+            sys.exit(1)
     if dist is not None:
         dist.destroy_process_group()
     ctx.close()

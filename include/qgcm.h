@@ -178,7 +178,8 @@ int qgcm_group_set_keys(qgcm_group *g, uint32_t first_idx, uint32_t count, const
  * One call at a time per group (calls are serialized).  When h_arena (and h_nonces) is pinned host memory
  * (qgcm_host_alloc, hipHostMalloc, hipHostRegister) holding every record, the members' GPUs gather and
  * scatter the records themselves over PCIe (zero-copy); otherwise host threads copy them through pinned
- * staging (QGCM_GROUP_THREADS per member).  QGCM_GROUP_ZEROCOPY=0 forces the copy path. */
+ * staging (QGCM_GROUP_THREADS per member); so does a batch with a record offset that is not a multiple of
+ * 4.  QGCM_GROUP_ZEROCOPY=0 forces the copy path. */
 int qgcm_group_seal_host(qgcm_group *g, uint8_t *h_arena, const qgcm_desc *h_descs, uint32_t n,
                          const uint8_t *h_nonces, uint32_t aad_len, uint8_t *h_status);
 int qgcm_group_open_host(qgcm_group *g, uint8_t *h_arena, const qgcm_desc *h_descs, uint32_t n, uint32_t aad_len,
@@ -257,6 +258,18 @@ int qgcm_tun_up(const char *ifname, const char *ip, int prefix, int mtu);
 int qgcm_tun_read_slots(int fd, uint8_t *arena, uint64_t stride, uint32_t max_n, uint32_t *lens, int timeout_ms);
 int qgcm_tun_write_slots(int fd, const uint8_t *arena, uint64_t stride, uint32_t n, const uint32_t *lens);
 int qgcm_tun_close(int fd);
+
+/* ---- introspection: which kernels served this context's calls ---- */
+/* Launch counts per kernel family since qgcm_create (uniform batches launch in chunks of 2^19
+ * packets; a descriptor batch launches the segmented kernel and then the per-wave kernel for its
+ * short keys; gcm_one_kernel serves per-packet calls, the coalescer's flushes and uniform batches of
+ * up to 2048 packets).  Writes min(n, QGCM_KERNEL_COUNTERS) counters, returns that number or -1. */
+#define QGCM_KERNEL_QUAD 0      /* gcm_quad_kernel, single-key (uniform) batches */
+#define QGCM_KERNEL_SEGMENTED 1 /* gcm_seg_kernel, descriptor batches (long key runs) */
+#define QGCM_KERNEL_PER_WAVE 2  /* gcm_quad_kernel, descriptor batches (short key runs) */
+#define QGCM_KERNEL_ONE 3       /* gcm_one_kernel, one workgroup per packet */
+#define QGCM_KERNEL_COUNTERS 4
+int qgcm_launch_counts(const qgcm_ctx *ctx, uint64_t *out, int n);
 
 /* ---- measurement: achievable HBM copy rate (reads + writes bytes) for the roofline ---- */
 /* 16-B aligned device buffers, bytes a multiple of 16.  Asynchronous on stream. */

@@ -51,12 +51,19 @@ class Context:
         self._owned = True
 
     @classmethod
-    def borrowed(cls, handle: int, device: int, max_keys: int) -> "Context":
-        """A view of a context owned elsewhere (a qgcm_group member): close() leaves it alone."""
+    def borrowed(cls, handle: int, device: int, max_keys: int, owner=None) -> "Context":
+        """A view of a context owned elsewhere (a qgcm_group member): close() leaves it alone.  The
+        view keeps `owner` alive; the owner invalidates the view (handle None) when it is closed."""
         c = cls.__new__(cls)
         c.handle, c.device, c.max_keys = handle, device, max_keys
-        c._next, c._mu, c._owned = max_keys, threading.Lock(), False
+        c._next, c._mu, c._owned, c._owner = max_keys, threading.Lock(), False, owner
         return c
+
+    def launch_counts(self) -> dict:
+        """Kernel launches that served this context's calls so far (qgcm_launch_counts)."""
+        out = (C.c_uint64 * 4)()
+        _lib.check(_lib.lib().qgcm_launch_counts(self.handle, out, 4), "qgcm_launch_counts")
+        return dict(zip(("quad", "segmented", "per_wave", "one"), (int(x) for x in out)))
 
     def alloc_slot(self) -> int:
         with self._mu:
@@ -87,6 +94,7 @@ class Context:
         if self.handle and getattr(self, "_owned", True):
             _lib.lib().qgcm_destroy(self.handle)
         self.handle = None
+        self._owner = None
 
     def __del__(self):  # pragma: no cover
         try:

@@ -7,9 +7,8 @@
 
 namespace qgcm {
 
-// LDS: Te0/Te1 replicated 32x, rows of 256 B (x<<8 | lane*4, Te1 at +128) = 64 KiB, then
-// 8 KiB GHASH comb tables (one per wave, or one per workgroup for single-key batches).
-// One workgroup per CU (DESIGN.md "Kernel").
+// LDS: Te0/Te1 replicated 32x, rows of 256 B (x<<8 | lane*4, Te1 at +128) = 64 KiB; 8 KiB per 4-bit
+// GHASH comb table.
 constexpr uint32_t kTeBytes = 65536;
 constexpr uint32_t kGhBytes = 8192;
 // Device key slot: 60 round-key words (+4 pad), their rot16 copies, and the 4-bit comb tables of
@@ -25,7 +24,7 @@ constexpr uint32_t kGhH8 = 2560, kGhH16 = 3072, kGhH32 = 3584, kGhH64 = 4096;
 struct Batch {
     uint8_t *arena;
     const qgcm_desc *descs;     // NULL -> uniform
-    const uint32_t *worklist;   // NULL -> identity; else n_items entries, 0xffffffff = padding
+    const uint32_t *worklist;   // descriptor kernels: n_items entries, 0xffffffff = padding
     const uint8_t *nonces;      // seal only; NULL -> nonce already in slot
     uint8_t *status;            // may be NULL
     const uint32_t *rk_table;   // [max_keys][kRkWords]
@@ -53,13 +52,13 @@ struct Batch {
                                 // back and made system-visible (the host polls it instead of the stream)
 };
 
-constexpr int kNumVariants = 15;
-constexpr int kVariantGeneral = 0;   // lane per packet, per-wave GHASH tables, any key mix
+constexpr int kNumVariants = 15;     // ids as in round 2; only the three below are built
+constexpr int kVariantUniform = 12;  // single-key (uniform) batches: quad kernel (Tab2F), 32 waves/CU
+constexpr int kVariantDescWave = 13;  // descriptor batches, per-wave 4-bit tables (Tab2), 12 waves/CU
 constexpr int kVariantDescQuad = 14;  // default for descriptor batches: segmented Tab2F kernel (+ 13 for short keys)
-constexpr int kVariantUniform = 12;  // default for single-key (uniform) batches: quad kernel (Tab2F), 32 waves/CU
 hipError_t init_kernels();
+bool variant_valid(int variant);
 int variant_waves(int variant);
-bool variant_quad(int variant);
 int variant_wgs_per_cu(int variant);
 bool variant_desc(int variant);
 int variant_complement(int variant);  // kernel for the short keys of a segmented variant (-1: none)
@@ -89,9 +88,9 @@ hipError_t launch_one(bool seal, const Batch &b, hipStream_t s);
 // Small descriptor batches through the latency kernel, one workgroup per packet, straight on the
 // caller's (pinned host or device) arena/descriptors/nonces/status -- the coalescer's flush path.
 constexpr uint32_t kOneBatchMax = 2048;
-constexpr uint32_t kOneUniformMax = 2048;
+constexpr uint32_t kOneUniformMax = 2048;    // measured cross-over with the quad kernel: 2048-4096 packets
 constexpr uint32_t kLaunchChunk = 1u << 19;  // packets per quad-kernel launch of a uniform batch
-constexpr uint32_t kDescChunk = 0;           // packets per sorted chunk of a descriptor batch (0 = all)  // measured cross-over with the quad kernel: 2048-4096 packets
+constexpr uint32_t kDescChunk = 0;           // packets per sorted chunk of a descriptor batch (0 = all)
 int run_one_descs(qgcm_ctx *ctx, bool seal, uint8_t *arena, const qgcm_desc *descs, uint32_t n,
                   const uint8_t *nonces, uint32_t aad_len, uint8_t *status, hipStream_t s,
                   uint8_t *done = nullptr);
@@ -112,11 +111,6 @@ int ctx_device(const qgcm_ctx *ctx);
 bool ctx_key_ready(qgcm_ctx *ctx, uint32_t key_idx);
 hipError_t launch_key_setup(const uint8_t *d_keys, uint32_t first, uint32_t count, uint32_t *rk_table,
                             uint4 *gh_table, const uint8_t *d_sbox, hipStream_t s);
-// Groups descriptor batches into key-uniform 64-packet tiles (counting sort by key_idx).
-hipError_t launch_build_worklist(const qgcm_desc *descs, uint32_t n, uint32_t max_keys, const uint8_t *key_valid,
-                                 uint32_t *counts,
-                                 uint32_t *cursors, uint32_t *worklist, uint32_t n_items_cap,
-                                 hipStream_t s);
 hipError_t launch_fill_uniform(uint8_t *arena, uint64_t stride, uint32_t n, uint32_t len, uint32_t aad_word,
                                uint64_t seed_payload, uint8_t *nonces, uint64_t seed_nonce, hipStream_t s);
 

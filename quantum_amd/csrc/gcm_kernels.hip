@@ -7,8 +7,9 @@
 // Design (DESIGN.md has the numbers):
 //  * gcm_quad_kernel (the batch path): four lanes per packet (lane m owns blocks m mod 4), 16 packets
 //    per wave, key-uniform wave tiles so round keys sit in SGPRs and the GHASH multiplier is uniform;
-//    persistent grid of two 16-wave workgroups per CU; gcm_one_kernel: one workgroup per packet
-//    (the per-call Encrypt/Decrypt); gcm_kernel: the round-1 lane-per-packet design (A/B variants);
+//    persistent grid of two 16-wave workgroups per CU; gcm_seg_kernel: the same engine over sorted
+//    key runs (descriptor batches); gcm_one_kernel: one workgroup per packet (the per-call
+//    Encrypt/Decrypt);
 //  * AES-256 by T-tables in LDS: Te0/Te1 replicated 32x so a ds_read_b32 is bank-conflict free;
 //    the lookup address (x<<8 | lane*4) is ONE v_perm_b32 (one all-VGPR AND-OR for byte 1 in the
 //    Tab2F engine); Te2/Te3 = rot16(Te0/Te1) folded into the column XOR;
@@ -81,24 +82,10 @@ typedef __attribute__((address_space(3))) u32x2 lds_u64;
 // them into ds_read2_b64, two 4 x 16-lane accesses: 8 LDS cycles instead of 2 x 2)
 __device__ __forceinline__ u32x2 lds64(uint32_t addr) { return *(const volatile lds_u64 *)(size_t)addr; }
 
-// GHASH comb tables in LDS, two layouts.  kB64: entry e = 16 p + v (nibble position p, value v) is
-// split into two 8-B halves, words 0-1 at base + 256 p + 8 v and words 2-3 at +128, read by two
-// ds_read_b64 (2 x 32-lane groups; the 16 entries of a half-row sit in 16 distinct bank pairs, so
-// any 32 nibbles are conflict-free).  Otherwise entry e is 16 B at base + 16 e, read by one
-// ds_read_b128 (4 x 16-lane groups).  Same LDS-array cycles per multiply (2 x 2 vs 4), but at 32
-// waves/CU the b64 form mixes better with the ds_read_b32 T-table stream
-// (tools/microbench/lds_mix.hip +6%; config 2 +2.1% in an in-process A/B) while at 12 waves/CU
-// (descriptor kernel) it is 1.2% slower: the single-key kernel uses kB64, the others do not.
-template <bool kB64>
-__device__ __forceinline__ void lds_st_comb(uint32_t base, uint32_t e, uint4 v) {
-    if constexpr (kB64) {
-        const uint32_t a = base + (e >> 4) * 256u + (e & 15u) * 8u;
-        *(lds_u64 *)(size_t)a = u32x2{v.x, v.y};
-        *(lds_u64 *)(size_t)(a + 128u) = u32x2{v.z, v.w};
-    } else {
-        lds_st128(base + e * 16u, v);
-    }
-}
+// GHASH 4-bit comb tables in LDS (descriptor per-wave kernel, latency kernel): entry e = 16 p + v
+// (nibble position p, value v) is 16 B at base + 16 e, read by one ds_read_b128 (4 x 16-lane groups;
+// at 12 waves/CU this measured 1.2% faster than two ds_read_b64 halves).
+__device__ __forceinline__ void lds_st_comb(uint32_t base, uint32_t e, uint4 v) { lds_st128(base + e * 16u, v); }
 
 // Te0[byte k of s] / Te1[byte k of s] from this lane's replica.
 // v_perm: result byte0 = lb.byte0 (lane*4), byte1 = s.byte k, bytes 2,3 = 0.
@@ -241,28 +228,6 @@ __device__ __forceinline__ void ctr_block(const Ctr &c, uint32_t lo, const Keys 
     ctr_block_t<TT0, 0>(c, lo, k, TT0{lb, 0}, s0, s1, s2, s3);
 }
 
-// N consecutive counter blocks lo, lo+1, ... (same 256-block segment) in lockstep: N independent
-// dependency chains per lane, so a wave keeps N x 16 LDS lookups in flight per round.
-template <int N>
-__device__ __forceinline__ void ctr_blocks(const Ctr &c, uint32_t lo, const Keys &k, uint32_t lb, uint32_t (&s)[N][4]) {
-#pragma unroll
-    for (int j = 0; j < N; ++j) {
-        const uint32_t x = (lo + j) ^ c.x3;
-        const uint32_t t0 = c.K0 ^ rot16(lds32(((x << 8) | lb) + 128u));
-        s[j][0] = c.U0 ^ TE0(t0, 0);
-        s[j][1] = c.U1 ^ rot16(TE1(t0, 3));
-        s[j][2] = c.U2 ^ rot16(TE0(t0, 2));
-        s[j][3] = c.U3 ^ TE1(t0, 1);
-    }
-#pragma unroll
-    for (int r = 3; r < 14; ++r) {
-#pragma unroll
-        for (int j = 0; j < N; ++j) round_full(s[j][0], s[j][1], s[j][2], s[j][3], k, r, lb);
-    }
-#pragma unroll
-    for (int j = 0; j < N; ++j) round_last(s[j][0], s[j][1], s[j][2], s[j][3], k, lb);
-}
-
 // ---------------------------------------------------------------------------------------------
 // AES-256 counter-block engines for the quad kernel.  Measured on gfx950 (tools/microbench/
 // valu_ops*.hip, bitop3_forms.hip): v_perm_b32, v_alignbit_b32, shifts and ANY VALU op with an SGPR
@@ -270,31 +235,28 @@ __device__ __forceinline__ void ctr_blocks(const Ctr &c, uint32_t lo, const Keys
 // VGPR operands only at ~2.7.  With the T-table round at 16 lookups (32 LDS cycles per wave per CU),
 // the Tab2 round's 16 v_perm + 4 v_alignbit + 4 SGPR-keyed v_bitop3 (~120 SIMD-cycles = 30 CU-cycles
 // per wave-round) nearly saturate the VALU as well as the LDS.
-//  Tab2: Te0/Te1 in LDS (64 KiB), Te2/Te3 = rot16 folded into the column XOR, round keys in SGPRs.
-//  Tab4: all four tables in LDS (128 KiB: [0, 64K) rows of Te0|Te1, [64K, 128K) rows of Te2|Te3), no
-//        rotation; round keys as per-lane VGPR copies, so every column XOR is an all-VGPR v_bitop3; the
-//        byte-1 lookups build their address with one all-VGPR AND-OR ((s & 0xff00) | lane base).
-template <bool kB64, bool kFence>
+//  Tab2: Te0/Te1 in LDS (64 KiB), Te2/Te3 = rot16 folded into the column XOR, round keys in SGPRs,
+//        byte-1 lookup addresses by one all-VGPR AND-OR; GHASH by the 4-bit comb of the wave's key
+//        (descriptor per-wave kernel).  Round 2 measured four T-tables in LDS (128 KiB, no rotations,
+//        all-VGPR XORs) 5% slower: one 16-wave workgroup per CU instead of two.
+//  Tab2F: Tab2 with the 5-bit comb GHASH (single-key batches and the segmented kernel).
+template <bool kFence>
 __device__ __forceinline__ void ghash_mul(uint32_t &y0, uint32_t &y1, uint32_t &y2, uint32_t &y3, uint32_t gb);
 
-// kAO: byte-1 addresses by the all-VGPR AND-OR (TT); Tab2 = Tab2T<false>
-template <bool kAO>
-struct Tab2T {
+struct Tab2 {
     Keys kk;
-    TT<0, kAO> t;
+    TT<0, true> t;
     __device__ __forceinline__ void setup(Ctr &c, uint32_t n0, uint32_t n1, uint32_t n2, uint32_t hi) const {
         ctr_setup(c, n0, n1, n2, hi, kk, t);
     }
     __device__ __forceinline__ void block(const Ctr &c, uint32_t lo, uint32_t &k0, uint32_t &k1, uint32_t &k2,
                                           uint32_t &k3) const {
-        ctr_block_t<TT<0, kAO>, 0>(c, lo, kk, t, k0, k1, k2, k3);
+        ctr_block_t<TT<0, true>, 0>(c, lo, kk, t, k0, k1, k2, k3);
     }
-    template <bool kB64>
     __device__ __forceinline__ void ghash(uint32_t &y0, uint32_t &y1, uint32_t &y2, uint32_t &y3, uint32_t gb) const {
-        ghash_mul<kB64, true>(y0, y1, y2, y3, gb);
+        ghash_mul<true>(y0, y1, y2, y3, gb);
     }
 };
-typedef Tab2T<false> Tab2;
 
 // GHASH multiply by the uniform H^4 through a 5-bit comb (single-key batches, engine Tab2F).  The
 // 128 bits of Y (LE words y0..y3, bit t = bit t%32 of word t/32) are cut into 26 windows of 5 bits
@@ -408,111 +370,22 @@ struct Tab2F {
                                           uint32_t &k3) const {
         ctr_block_t<TT<kG5Bytes, true>, kG5Bytes>(c, lo, kk, t, k0, k1, k2, k3);
     }
-    template <bool kB64>
     __device__ __forceinline__ void ghash(uint32_t &y0, uint32_t &y1, uint32_t &y2, uint32_t &y3, uint32_t) const {
         ghash_mul5(y0, y1, y2, y3, mf8);
     }
 };
 
-constexpr uint32_t kTe4Bytes = 131072;
-// v_bitop3 truth tables in the LOP3 convention: f(0xf0, 0xcc, 0xaa) for operands (a, b, c)
-constexpr uint32_t kOpXor3 = 0x96;                                // a ^ b ^ c
-constexpr uint32_t kOpAndOr = (0xf0 & 0xcc) | 0xaa;               // (a & b) | c
-constexpr uint32_t kOpSel = ((0xf0 & ~0xaa) | (0xcc & 0xaa)) & 0xff;  // c ? b : a, bitwise
-template <uint32_t kOp>
-__device__ __forceinline__ uint32_t bop3(uint32_t a, uint32_t b, uint32_t c) {
-    return __builtin_amdgcn_bitop3_b32(a, b, c, kOp);
-}
 // a VGPR the compiler cannot fold into a constant (an SGPR or literal operand costs half rate)
 __device__ __forceinline__ uint32_t vreg(uint32_t x) {
     asm volatile("" : "+v"(x));
     return x;
 }
 
-struct Tab4 {
-    uint32_t lb, lb2;                  // lane bases: Te0/Te1 rows (< 64K), Te2/Te3 rows (| 64K)
-    uint32_t m8, m24, m16;             // 0x0000ff00, 0xff000000, 0xffff0000 as VGPRs
-    uint32_t rk[60];                   // FIPS-197 round-key words (12-55 as per-lane VGPR copies)
-
-    // address of Te_t[byte k of s]
-    __device__ __forceinline__ uint32_t addr(uint32_t s, int k, int t) const {
-        const uint32_t base = t >= 2 ? lb2 : lb;
-        const uint32_t a = k == 1 ? bop3<kOpAndOr>(s, m8, base) : perm(s, base, 0x0c020400u + (k << 8));
-        return a + ((t & 1) ? 128u : 0u);
-    }
-    __device__ __forceinline__ uint32_t T(uint32_t s, int k, int t) const { return lds32(addr(s, k, t)); }
-
-    // column c = Te0[s_c.b0] ^ Te1[s_c+1.b1] ^ Te2[s_c+2.b2] ^ Te3[s_c+3.b3] ^ rk_c
-    __device__ __forceinline__ void round_full(uint32_t (&st)[4], int r) const {
-        uint32_t a[4][4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-#pragma unroll
-            for (int t = 0; t < 4; ++t) a[c][t] = T(st[(c + t) & 3], t, t);
-        asm volatile("" ::: "memory");  // all 16 lookups in flight before the first combine
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-            st[c] = bop3<kOpXor3>(bop3<kOpXor3>(a[c][0], a[c][1], a[c][2]), a[c][3], rk[4 * r + c]);
-    }
-    // final round: output byte j of column c = S(s_c+j.bj), taken from the table holding S at byte j
-    // (Te2 byte 0, Te3 byte 1, Te0 byte 2, Te1 byte 3), merged by all-VGPR byte selects
-    __device__ __forceinline__ void round_last(uint32_t (&st)[4]) const {
-        uint32_t a[4][4];
-        constexpr int tab[4] = {2, 3, 0, 1};
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) a[c][j] = T(st[(c + j) & 3], j, tab[j]);
-        asm volatile("" ::: "memory");
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const uint32_t x = bop3<kOpSel>(a[c][0], a[c][1], m8);   // byte 1 from Te3, the rest from Te2
-            const uint32_t y = bop3<kOpSel>(a[c][2], a[c][3], m24);  // byte 3 from Te1, the rest from Te0
-            st[c] = bop3<kOpSel>(x, y, m16) ^ rk[56 + c];             // bytes 0-1 of x, 2-3 of y
-        }
-    }
-    // rounds 1-2 of the counter blocks nonce || (hi << 8 | lo), lo varying (as ctr_setup)
-    __device__ __forceinline__ void setup(Ctr &c, uint32_t n0, uint32_t n1, uint32_t n2, uint32_t hi) const {
-        const uint32_t s0 = n0 ^ rk[0], s1 = n1 ^ rk[1], s2 = n2 ^ rk[2];
-        const uint32_t s3 = bswap(hi << 8) ^ rk[3];  // byte 3 varies per block; unused below
-        c.x3 = rk[3] >> 24;
-        c.K0 = bop3<kOpXor3>(T(s0, 0, 0), T(s1, 1, 1), T(s2, 2, 2)) ^ rk[4];
-        const uint32_t t1 = bop3<kOpXor3>(bop3<kOpXor3>(T(s1, 0, 0), T(s2, 1, 1), T(s3, 2, 2)), T(s0, 3, 3), rk[5]);
-        const uint32_t t2 = bop3<kOpXor3>(bop3<kOpXor3>(T(s2, 0, 0), T(s3, 1, 1), T(s0, 2, 2)), T(s1, 3, 3), rk[6]);
-        const uint32_t t3 = bop3<kOpXor3>(bop3<kOpXor3>(T(s3, 0, 0), T(s0, 1, 1), T(s1, 2, 2)), T(s2, 3, 3), rk[7]);
-        c.U0 = bop3<kOpXor3>(T(t1, 1, 1), T(t2, 2, 2), T(t3, 3, 3)) ^ rk[8];
-        c.U1 = bop3<kOpXor3>(T(t1, 0, 0), T(t2, 1, 1), T(t3, 2, 2)) ^ rk[9];
-        c.U2 = bop3<kOpXor3>(T(t2, 0, 0), T(t3, 1, 1), T(t1, 3, 3)) ^ rk[10];
-        c.U3 = bop3<kOpXor3>(T(t3, 0, 0), T(t1, 2, 2), T(t2, 3, 3)) ^ rk[11];
-    }
-    __device__ __forceinline__ void block(const Ctr &c, uint32_t lo, uint32_t &k0, uint32_t &k1, uint32_t &k2,
-                                          uint32_t &k3) const {
-        const uint32_t x = lo ^ c.x3;
-        const uint32_t t0 = c.K0 ^ lds32(((x << 8) | lb2) + 128u);  // Te3[x]
-        uint32_t st[4];
-        st[0] = c.U0 ^ T(t0, 0, 0);
-        st[1] = c.U1 ^ T(t0, 3, 3);
-        st[2] = c.U2 ^ T(t0, 2, 2);
-        st[3] = c.U3 ^ T(t0, 1, 1);
-#pragma unroll
-        for (int r = 3; r < 14; ++r) round_full(st, r);
-        round_last(st);
-        k0 = st[0];
-        k1 = st[1];
-        k2 = st[2];
-        k3 = st[3];
-    }
-    template <bool kB64>
-    __device__ __forceinline__ void ghash(uint32_t &y0, uint32_t &y1, uint32_t &y2, uint32_t &y3, uint32_t gb) const {
-        ghash_mul<kB64, true>(y0, y1, y2, y3, gb);
-    }
-};
-
 // Y <- Y * H in GF(2^128) via the 4-bit comb in this wave's LDS table at gb (byte1/2 of gb hold
 // its base; byte0 is 0).  Entry (p, v) at gb + p*256 + v*16, p = nibble position (2*byte for the
 // high nibble, 2*byte+1 for the low one), v = nibble value.
 // kFence = false (latency kernel, one wave): no chunk fences, so all 32 lookups can be in flight.
-template <bool kB64 = false, bool kFence = true>
+template <bool kFence = true>
 __device__ __forceinline__ void ghash_mul(uint32_t &y0, uint32_t &y1, uint32_t &y2, uint32_t &y3, uint32_t gb) {
     uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
     const uint32_t yw[4] = {y0, y1, y2, y3};
@@ -520,21 +393,6 @@ __device__ __forceinline__ void ghash_mul(uint32_t &y0, uint32_t &y1, uint32_t &
     // the LDS queue can overlap anyway (lgkmcnt tracks 15 in flight per wave).
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
-        if constexpr (kB64) {
-        const uint32_t hi = (yw[w] >> 1) & 0x78787878u;  // 8 x high nibble of each byte
-        const uint32_t lo = (yw[w] << 3) & 0x78787878u;  // 8 x low nibble
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int j = 4 * w + k;
-            const uint32_t ah = perm(gb, hi, 0x0c060500u | k) + (2 * j) * 256;
-            const uint32_t al = perm(gb, lo, 0x0c060500u | k) + (2 * j + 1) * 256;
-            const u32x2 h0 = lds64(ah), h1 = lds64(ah + 128u), l0 = lds64(al), l1 = lds64(al + 128u);
-            a0 = xor3(a0, h0.x, l0.x);
-            a1 = xor3(a1, h0.y, l0.y);
-            a2 = xor3(a2, h1.x, l1.x);
-            a3 = xor3(a3, h1.y, l1.y);
-        }
-        } else {
         const uint32_t hi = yw[w] & 0xf0f0f0f0u;
         const uint32_t lo = (yw[w] << 4) & 0xf0f0f0f0u;
 #pragma unroll
@@ -546,7 +404,6 @@ __device__ __forceinline__ void ghash_mul(uint32_t &y0, uint32_t &y1, uint32_t &
             a1 = xor3(a1, th.y, tl.y);
             a2 = xor3(a2, th.z, tl.z);
             a3 = xor3(a3, th.w, tl.w);
-        }
         }
         // chunk fence: the accumulators are consumed here and the next chunk's LDS loads cannot be
         // hoisted above it, so at most 8 x 16 B of table rows are live at once
@@ -695,234 +552,16 @@ __device__ __forceinline__ void write_tail(uint8_t *data, uint32_t L, uint32_t g
     if (s) store_bytes(data + (L & ~3u) + 28, n2 >> sh, s);
 }
 
-// Kernel variants.  kW waves per workgroup (one workgroup per CU); kShared: one GHASH table for
-// the whole workgroup (uniform single-key batches) instead of one per wave; kIlp counter blocks
-// per lane per iteration.
-template <int kW, bool kShared>
-constexpr uint32_t lds_bytes() {
-    return kTeBytes + (kShared ? 1u : (uint32_t)kW) * kGhBytes;
-}
-
-template <bool kSeal, int kW, bool kShared, int kIlp>
-__global__ void __launch_bounds__(kW * 64) __attribute__((amdgpu_waves_per_eu(kW / 4, kW / 4)))
-gcm_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
-    constexpr uint32_t kT = kW * 64;
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = threadIdx.x >> 6;
-
-    // Fill the replicated T-tables: dword i = row x = i/64, slot i%64 (<32: Te0, else Te1).
-    for (uint32_t i = threadIdx.x; i < kTeBytes / 4; i += kT) {
-        const uint32_t x = i >> 6, slot = i & 63u;
-        lds_st32(4 * i, b.te[(slot >> 5) * 256u + x]);
-    }
-    const uint32_t gb = kTeBytes + (kShared ? 0u : wave) * kGhBytes;
-    uint32_t cur_key = 0xffffffffu;
-    if (kShared) {
-        const uint4 *src = b.gh_table + (size_t)b.uniform_key * kGhEntries;
-        for (uint32_t e = threadIdx.x; e < 512u; e += kT) lds_st_comb<false>(kTeBytes, e, src[e]);  // H only
-        cur_key = b.uniform_key;
-    }
-    __syncthreads();
-
-    const uint32_t lb = (lane & 31u) << 2;
-    const uint32_t ntiles = b.n_items >> 6;
-
-    for (uint32_t tile = blockIdx.x * kW + wave; tile < ntiles; tile += gridDim.x * kW) {
-        const uint32_t item = tile * 64u + lane;
-        const uint32_t pkt = b.worklist ? b.worklist[item] : item;
-        bool valid = pkt < b.n;
-        uint64_t off = 0;
-        uint32_t len = 0, key = 0;
-        if (valid) {
-            if (b.descs) {
-                const qgcm_desc d = b.descs[pkt];
-                off = d.offset;
-                len = d.len;
-                key = d.key_idx;
-            } else {
-                off = (uint64_t)pkt * b.stride;
-                len = b.uniform_len;
-                key = b.uniform_key;
-            }
-        }
-        const uint64_t vmask = __ballot(valid);
-        if (vmask == 0) continue;
-        const int first = __ffsll((unsigned long long)vmask) - 1;
-        const uint32_t wkey = kShared ? b.uniform_key : __builtin_amdgcn_readfirstlane(__shfl(key, first));
-        if (!kShared && wkey != cur_key) {
-            const uint4 *src = b.gh_table + (size_t)wkey * kGhEntries;
-#pragma unroll
-            for (int r = 0; r < 8; ++r) {
-                const uint32_t e = r * 64 + lane;
-                lds_st_comb<false>(gb, e, src[e]);
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            cur_key = wkey;
-        }
-        const Keys kk = {rk_table + (size_t)wkey * kRkWords, rk_table + (size_t)wkey * kRkWords + 64};
-
-        // Per-lane framing (crypto/aes.go:41-62).
-        uint32_t L;
-        if (kSeal) {
-            L = len;
-        } else {
-            valid = valid && len >= (uint32_t)QGCM_OVERHEAD;  // Open: ciphertext shorter than tag
-            L = len - QGCM_OVERHEAD;
-        }
-        valid = valid && L < QGCM_MAX_PAYLOAD;
-        if (!valid) {
-            if (!kSeal && b.status && pkt < b.n) b.status[pkt] = 0;
-            continue;
-        }
-        uint8_t *raw = b.arena + off;
-        uint8_t *data = raw + 4;  // common.PacketStart
-
-        uint32_t g0 = 0, g1 = 0, g2 = 0, g3 = 0, n0, n1, n2;
-        if (kSeal && b.nonces) {
-            const uint32_t *np = reinterpret_cast<const uint32_t *>(b.nonces + 12ull * pkt);
-            n0 = np[0];
-            n1 = np[1];
-            n2 = np[2];
-        } else {
-            read_tail(data, L, g0, g1, g2, g3, n0, n1, n2);
-        }
-
-        // GHASH(A): the additional data is the 4-B private-IP header Raw[0:4].
-        uint32_t y0 = 0, y1 = 0, y2 = 0, y3 = 0;
-        if (b.aad_len) {
-            y0 = *reinterpret_cast<const uint32_t *>(raw) & (b.aad_len >= 4 ? 0xffffffffu : lowmask(b.aad_len));
-            ghash_mul(y0, y1, y2, y3, gb);
-        }
-
-        Ctr cc;
-        ctr_setup(cc, n0, n1, n2, 0, kk, lb);
-        uint32_t e0, e1, e2, e3;  // E_K(J0), J0 = nonce || 0^31 || 1
-        ctr_block(cc, 1, kk, lb, e0, e1, e2, e3);
-
-        const uint32_t nfull = L >> 4;
-        uint32_t i = 0;
-        // One block through the counter cache (re-derived at each 256-block segment).
-        auto single = [&](uint32_t bi) {
-            const uint32_t ctr = bi + 2;  // inc32(J0) + bi
-            if ((ctr & 0xffu) == 0) ctr_setup(cc, n0, n1, n2, ctr >> 8, kk, lb);
-            // the data load is issued before the AES rounds so its latency hides behind them
-            W4 *p = reinterpret_cast<W4 *>(data + 16u * bi);
-            const W4 in = load_block(p);
-            uint32_t k0, k1, k2, k3;
-            ctr_block(cc, ctr & 0xffu, kk, lb, k0, k1, k2, k3);
-            const W4 out = {in.x ^ k0, in.y ^ k1, in.z ^ k2, in.w ^ k3};
-            *p = out;
-            const W4 &c = kSeal ? out : in;
-            y0 ^= c.x;
-            y1 ^= c.y;
-            y2 ^= c.z;
-            y3 ^= c.w;
-            ghash_mul(y0, y1, y2, y3, gb);
-        };
-        if constexpr (kIlp > 1) {
-            for (; i + kIlp <= nfull; i += kIlp) {
-                const uint32_t ctr = i + 2, lo = ctr & 0xffu;
-                uint32_t ks[kIlp][4];
-                if (lo == 0) ctr_setup(cc, n0, n1, n2, ctr >> 8, kk, lb);
-                if (lo + (kIlp - 1) <= 255u) {
-                    ctr_blocks<kIlp>(cc, lo, kk, lb, ks);
-                } else {
-#pragma unroll
-                    for (int j = 0; j < kIlp; ++j) {
-                        const uint32_t cj = ctr + j;
-                        if ((cj & 0xffu) == 0) ctr_setup(cc, n0, n1, n2, cj >> 8, kk, lb);
-                        ctr_block(cc, cj & 0xffu, kk, lb, ks[j][0], ks[j][1], ks[j][2], ks[j][3]);
-                    }
-                }
-                W4 *p = reinterpret_cast<W4 *>(data + 16u * i);
-                W4 in[kIlp];
-#pragma unroll
-                for (int j = 0; j < kIlp; ++j) in[j] = p[j];
-#pragma unroll
-                for (int j = 0; j < kIlp; ++j) {
-                    const W4 out = {in[j].x ^ ks[j][0], in[j].y ^ ks[j][1], in[j].z ^ ks[j][2], in[j].w ^ ks[j][3]};
-                    p[j] = out;
-                    const W4 &c = kSeal ? out : in[j];
-                    y0 ^= c.x;
-                    y1 ^= c.y;
-                    y2 ^= c.z;
-                    y3 ^= c.w;
-                    ghash_mul(y0, y1, y2, y3, gb);
-                }
-            }
-        }
-        for (; i < nfull; ++i) single(i);
-        const uint32_t r = L & 15u;
-        uint32_t prefix = 0;
-        if (r) {
-            const uint32_t ctr = nfull + 2;
-            if ((ctr & 0xffu) == 0) ctr_setup(cc, n0, n1, n2, ctr >> 8, kk, lb);
-            uint32_t k0, k1, k2, k3;
-            ctr_block(cc, ctr & 0xffu, kk, lb, k0, k1, k2, k3);
-            uint8_t *blk = data + 16u * nfull;
-            const W4 in = *reinterpret_cast<const W4 *>(blk);  // reads into tag area: inside the slot
-            const uint32_t q = r >> 2, s = r & 3u;
-            const uint32_t m0 = q > 0 ? 0xffffffffu : (q == 0 ? lowmask(s) : 0u);
-            const uint32_t m1 = q > 1 ? 0xffffffffu : (q == 1 ? lowmask(s) : 0u);
-            const uint32_t m2 = q > 2 ? 0xffffffffu : (q == 2 ? lowmask(s) : 0u);
-            const uint32_t m3 = q == 3 ? lowmask(s) : 0u;
-            const uint32_t o0 = in.x ^ k0, o1 = in.y ^ k1, o2 = in.z ^ k2, o3 = in.w ^ k3;
-            uint32_t *bw = reinterpret_cast<uint32_t *>(blk);
-            if (q > 0) bw[0] = o0;
-            if (q > 1) bw[1] = o1;
-            if (q > 2) bw[2] = o2;
-            const uint32_t oq = sel4(q, o0, o1, o2, o3) & lowmask(s);
-            if (kSeal) {
-                prefix = oq;  // written by write_tail together with tag||nonce
-                y0 ^= o0 & m0;
-                y1 ^= o1 & m1;
-                y2 ^= o2 & m2;
-                y3 ^= o3 & m3;
-            } else {
-                store_bytes(blk + 4 * q, oq, s);
-                y0 ^= in.x & m0;
-                y1 ^= in.y & m1;
-                y2 ^= in.z & m2;
-                y3 ^= in.w & m3;
-            }
-            ghash_mul(y0, y1, y2, y3, gb);
-        }
-        // [len(A)]_64 || [len(C)]_64 in bits, big endian.
-        y1 ^= bswap(b.aad_len * 8u);
-        y3 ^= bswap(L * 8u);
-        ghash_mul(y0, y1, y2, y3, gb);
-        const uint32_t t0 = y0 ^ e0, t1 = y1 ^ e1, t2 = y2 ^ e2, t3 = y3 ^ e3;
-
-        if (kSeal) {
-            write_tail(data, L, t0, t1, t2, t3, n0, n1, n2, prefix);
-            if (b.status) b.status[pkt] = 1;
-        } else {
-            const bool ok = ((t0 ^ g0) | (t1 ^ g1) | (t2 ^ g2) | (t3 ^ g3)) == 0;
-            if (!ok) {
-                // Go 1.9 crypto/cipher gcm Open: zero the would-be plaintext on tag mismatch.
-                uint32_t *dw = reinterpret_cast<uint32_t *>(data);
-                for (uint32_t i = 0; i < (L >> 2); ++i) dw[i] = 0;
-                store_bytes(data + (L & ~3u), 0, L & 3u);
-            }
-            if (b.status) b.status[pkt] = ok ? 1 : 0;
-        }
-    }
-}
-
 // ---------------------------------------------------------------------------------------------
 // Quad kernel (single-key batches): FOUR lanes per packet.  Lane m of a quad owns the packet's
 // 16-B blocks b = m, m+4, m+8, ... so every wave instruction moves 16 contiguous 64-B granules
 // (one per packet) -- full-granule HBM traffic, and only 16 packets in flight per wave, which keeps
 // 16 waves per CU within the caches.  GHASH runs as four interleaved Horner chains
 // Z_m <- Z_m * H^4 ^ C_b (comb table of H^4), recombined once per packet:
-//   Y = ( sum_m Z_m * H^(e_m - 1)  ^  [len(A)]||[len(C)] ) * H,   e_m = d + 1 - b_last(m),
+//   Y = sum_m Z_m * H^(e_m)  ^  [len(A)]||[len(C)] * H,   e_m = d + 1 - b_last(m) in [2, 5],
 // with the additional data A folded in as block -1 of lane 3 (SP 800-38D GHASH, restated for a
 // 4-way interleave; checked against the oracle in tests).  E_K(J0) is computed by lane d % 4 in the
 // slot where it has no data block.
-constexpr uint32_t kQuadLds = kTeBytes + kGhBytes;  // T-tables + the comb table of H^4
-
 __device__ __forceinline__ uint32_t quad_xor(uint32_t v) {
     v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xf, 0xf, false);  // quad_perm [1,0,3,2]
     v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xf, 0xf, false);  // quad_perm [2,3,0,1]
@@ -930,9 +569,9 @@ __device__ __forceinline__ uint32_t quad_xor(uint32_t v) {
 }
 
 // One packet of a quad tile (4 lanes, lane m owns blocks b = m mod 4): CTR + GHASH + tag, in place.
-template <bool kSeal, bool kFold, bool kDesc, bool kGFin, class Eng>
+template <bool kSeal, class Eng>
 __device__ __forceinline__ void quad_packet(const Batch &b, const Eng &eng, uint32_t pkt, uint64_t off, uint32_t L,
-                                            uint32_t wkey, uint32_t m, uint32_t gH4, uint32_t gH) {
+                                            uint32_t wkey, uint32_t m, uint32_t gH4) {
     const uint4 *Hg = b.gh_table + (size_t)wkey * kGhEntries;  // comb tables of H^k (global)
     uint8_t *raw = b.arena + off;
     uint8_t *data = raw + 4;  // common.PacketStart
@@ -957,58 +596,7 @@ __device__ __forceinline__ void quad_packet(const Batch &b, const Eng &eng, uint
 
     uint32_t e0 = 0, e1 = 0, e2 = 0, e3 = 0;  // E_K(J0)
     uint32_t prefix = 0;
-    if constexpr (kFold) {
-    Ctr cc;
-    uint32_t hi = 0;
-    eng.setup(cc, n0, n1, n2, 0);
-    // Lane m walks blocks m, m+4, ... < d, then (lane d % 4 only) the virtual block d = E_K(J0):
-    // one AES instance per step, and J0 fills the slot of the lane with the fewest data blocks.
-    for (uint32_t bi = m; bi <= d; bi += 4) {
-        const bool j0 = bi == d;
-        const uint32_t ctr = j0 ? 1u : bi + 2;  // J0, or inc32(J0) + bi
-        if ((ctr >> 8) != hi) {
-            hi = ctr >> 8;
-            eng.setup(cc, n0, n1, n2, hi);
-        }
-        uint32_t k0, k1, k2, k3;
-        eng.block(cc, ctr & 0xffu, k0, k1, k2, k3);
-        if (j0) {
-            e0 = k0;
-            e1 = k1;
-            e2 = k2;
-            e3 = k3;
-            break;
-        }
-        W4 *p = reinterpret_cast<W4 *>(data + 16u * bi);
-        const W4 in = *p;  // a partial block reads into the tag area: inside the slot
-        const W4 out = {in.x ^ k0, in.y ^ k1, in.z ^ k2, in.w ^ k3};
-        W4 c = kSeal ? out : in;
-        if (bi < nfull) {
-            *p = out;
-        } else {  // the partial last block (r bytes)
-            const uint32_t q = r >> 2, sb = r & 3u;
-            uint32_t *bw = reinterpret_cast<uint32_t *>(p);
-            if (q > 0) bw[0] = out.x;
-            if (q > 1) bw[1] = out.y;
-            if (q > 2) bw[2] = out.z;
-            const uint32_t oq = sel4(q, out.x, out.y, out.z, out.w) & lowmask(sb);
-            if (kSeal)
-                prefix = oq;  // written with tag||nonce by write_tail
-            else
-                store_bytes(reinterpret_cast<uint8_t *>(p) + 4 * q, oq, sb);
-            c.x &= q > 0 ? 0xffffffffu : lowmask(sb);
-            c.y &= q > 1 ? 0xffffffffu : (q == 1 ? lowmask(sb) : 0u);
-            c.z &= q > 2 ? 0xffffffffu : (q == 2 ? lowmask(sb) : 0u);
-            c.w &= q == 3 ? lowmask(sb) : 0u;
-        }
-        eng.template ghash<!kDesc>(z0, z1, z2, z3, gH4);
-        z0 ^= c.x;
-        z1 ^= c.y;
-        z2 ^= c.z;
-        z3 ^= c.w;
-        blast = (int)bi;
-    }
-    } else {
+    {
     Ctr cc;
     uint32_t hi = 0;
     eng.setup(cc, n0, n1, n2, 0);
@@ -1026,7 +614,7 @@ __device__ __forceinline__ void quad_packet(const Batch &b, const Eng &eng, uint
         const W4 out = {in.x ^ k0, in.y ^ k1, in.z ^ k2, in.w ^ k3};
         store_block(p, out);
         const W4 &c = kSeal ? out : in;
-        eng.template ghash<!kDesc>(z0, z1, z2, z3, gH4);
+        eng.ghash(z0, z1, z2, z3, gH4);
         z0 ^= c.x;
         z1 ^= c.y;
         z2 ^= c.z;
@@ -1063,7 +651,7 @@ __device__ __forceinline__ void quad_packet(const Batch &b, const Eng &eng, uint
             c.y &= q > 1 ? 0xffffffffu : (q == 1 ? lowmask(sb) : 0u);
             c.z &= q > 2 ? 0xffffffffu : (q == 2 ? lowmask(sb) : 0u);
             c.w &= q == 3 ? lowmask(sb) : 0u;
-            eng.template ghash<!kDesc>(z0, z1, z2, z3, gH4);
+            eng.ghash(z0, z1, z2, z3, gH4);
             z0 ^= c.x;
             z1 ^= c.y;
             z2 ^= c.z;
@@ -1079,7 +667,7 @@ __device__ __forceinline__ void quad_packet(const Batch &b, const Eng &eng, uint
     }
     // Y = sum_m Z_m * H^(e_m)  ^  ([len(A)]||[len(C)]) * H,  e_m = d + 1 - b_last(m) in [2, 5]
     // (a lane without blocks has Z_m = 0 or only the AAD block, b_last = -1, d <= 3).
-    if constexpr (kGFin) {
+    {
         const uint32_t em = d + 1u - (uint32_t)blast;
         const uint32_t tsel = em == 2 ? kGhH2 : em == 3 ? kGhH3 : em == 4 ? kGhH4 : kGhH5;
         ghash_mul_global(z0, z1, z2, z3, Hg + tsel);
@@ -1089,21 +677,6 @@ __device__ __forceinline__ void quad_packet(const Batch &b, const Eng &eng, uint
         z1 = quad_xor(z1) ^ l1;
         z2 = quad_xor(z2) ^ l2;
         z3 = quad_xor(z3) ^ l3;
-    } else {
-        for (int t = (int)d - blast; t > 0; --t) {
-            if constexpr (kDesc)
-                ghash_mul_global(z0, z1, z2, z3, Hg);
-            else
-                ghash_mul<!kDesc>(z0, z1, z2, z3, gH);
-        }
-        z0 = quad_xor(z0);
-        z1 = quad_xor(z1) ^ bswap(b.aad_len * 8u);  // [len(A)]_64 || [len(C)]_64, big endian
-        z2 = quad_xor(z2);
-        z3 = quad_xor(z3) ^ bswap(L * 8u);
-        if constexpr (kDesc)
-            ghash_mul_global(z0, z1, z2, z3, Hg);
-        else
-            ghash_mul<!kDesc>(z0, z1, z2, z3, gH);
     }
     e0 = quad_xor(e0);
     e1 = quad_xor(e1);
@@ -1136,20 +709,24 @@ __device__ __forceinline__ void quad_packet(const Batch &b, const Eng &eng, uint
     }
 }
 
-// kGFin: the once-per-packet recombination multiplies by H^2..H^5 come from the global key table
-// (one multiply per lane); otherwise by repeated multiplies by H (comb table of H in LDS for single
-// key batches, global for descriptor batches).
-// kTab: the AES engine (Tab2: 64 KiB of T-tables; Tab4: 128 KiB, single-key batches only).
-template <bool kSeal, int kW, bool kFold, int kWpe = kW / 4, bool kDesc = false, bool kGFin = true, int kTab = 2>
-__global__ void __launch_bounds__(kW * 64) __attribute__((amdgpu_waves_per_eu(kWpe, kWpe)))
+// kDesc = false: single-key (uniform) batches, engine Tab2F (5-bit comb of H^4 shared by the
+// workgroup), two 16-wave workgroups per CU (32 waves/CU, 64 VGPRs).  kDesc = true: the per-wave
+// descriptor kernel, engine Tab2 (each wave keeps the 4-bit comb of its current key's H^4 in its own
+// 8 KiB of LDS), one 12-wave workgroup per CU; it takes the tiles of the keys too short for the
+// segmented kernel (and every tile when QGCM_DESC_VARIANT=13).  Both recombine the four Horner chains
+// once per packet by H^2..H^5 from the global key table (L2-resident), off the LDS pipe.
+template <bool kDesc>
+constexpr int quad_waves() { return kDesc ? 12 : 16; }
+template <bool kDesc>
+constexpr int quad_wpe() { return kDesc ? 3 : 8; }
+
+template <bool kSeal, bool kDesc>
+__global__ void __launch_bounds__(quad_waves<kDesc>() * 64) __attribute__((amdgpu_waves_per_eu(quad_wpe<kDesc>(),
+                                                                                                  quad_wpe<kDesc>())))
 gcm_quad_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
-    // kTab: 2 = Tab2, 5 = Tab2 with byte-1 AND-OR addresses, 3 = Tab2F, 4 = Tab4
-    static_assert(kTab == 2 || kTab == 5 || ((kTab == 4 || kTab == 3) && !kDesc),
-                  "Tab4/Tab2F engines: single-key batches");
-    static_assert(kTab != 3 || kGFin, "Tab2F: recombination from the global key table");
+    constexpr uint32_t kW = quad_waves<kDesc>();
     constexpr uint32_t kT = kW * 64;
-    constexpr uint32_t kTe = kTab == 4 ? kTe4Bytes : kTeBytes;  // LDS bytes of T-tables (comb tables after)
-    constexpr uint32_t kTeBase = kTab == 3 ? kG5Bytes : 0u;      // Tab2F: the 5-bit comb first, then Te
+    constexpr uint32_t kTeBase = kDesc ? 0u : kG5Bytes;  // Tab2F: the 5-bit comb first, then Te
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = threadIdx.x >> 6;
     const uint32_t m = lane & 3u;          // block residue owned by this lane
@@ -1157,49 +734,19 @@ gcm_quad_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
     // the short-key pass of a segmented launch with no short keys: leave before the table fill
     if (kDesc && b.tile_list && __builtin_amdgcn_readfirstlane(*b.n_list) == 0) return;
 
-    // dword i of each 64 KiB half: row x = i/64, slot i%64 (< 32: Te0 / Te2, else Te1 / Te3)
+    // dword i of the 64 KiB of T-tables: row x = i/64, slot i%64 (< 32: Te0, else Te1)
     for (uint32_t i = threadIdx.x; i < kTeBytes / 4; i += kT) {
         const uint32_t x = i >> 6, slot = i & 63u;
-        const uint32_t v = b.te[(slot >> 5) * 256u + x];
-        lds_st32(kTeBase + 4 * i, v);
-        if constexpr (kTab == 4) lds_st32(kTeBytes + 4 * i, rot16(v));
+        lds_st32(kTeBase + 4 * i, b.te[(slot >> 5) * 256u + x]);
     }
-    if constexpr (kTab == 3) {
-        g5_fill(b.gh_table + (size_t)b.uniform_key * kGhEntries + kGhH4, threadIdx.x, kT);
-    } else if constexpr (!kDesc) {
-        const uint4 *src = b.gh_table + (size_t)b.uniform_key * kGhEntries + kGhH4;
-        for (uint32_t e = threadIdx.x; e < 512u; e += kT) lds_st_comb<!kDesc>(kTe, e, src[e]);
-        if constexpr (!kGFin) {
-            const uint4 *srcH = b.gh_table + (size_t)b.uniform_key * kGhEntries + kGhH;
-            for (uint32_t e = threadIdx.x; e < 512u; e += kT) lds_st_comb<!kDesc>(kTe + kGhBytes, e, srcH[e]);
-        }
-    }
+    if constexpr (!kDesc) g5_fill(b.gh_table + (size_t)b.uniform_key * kGhEntries + kGhH4, threadIdx.x, kT);
     __syncthreads();
 
     const uint32_t lb = (lane & 31u) << 2;
-    Tab4 e4;
-    if constexpr (kTab == 4) {  // the single key's round keys as VGPR copies, masks and lane bases as VGPRs
-        const uint32_t *kp = rk_table + (size_t)b.uniform_key * kRkWords;
-        // rounds 3-13 (words 12-55) as VGPRs; the rarely used words of the counter setup and the final
-        // round stay SGPRs (128 VGPRs per lane at 16 waves/CU)
-#pragma unroll
-        for (int i = 0; i < 60; ++i) e4.rk[i] = i >= 12 && i < 56 ? vreg(kp[i]) : kp[i];
-        e4.lb = vreg(lb);
-        e4.lb2 = vreg(lb | kTeBytes);
-        e4.m8 = vreg(0x0000ff00u);
-        e4.m24 = vreg(0xff000000u);
-        e4.m16 = vreg(0xffff0000u);
-    }
-    uint32_t m8 = 0, mf8 = 0;
-    if constexpr (kTab == 3 || kTab == 5) {  // masks as VGPRs (an SGPR or literal operand issues at half rate)
-        m8 = vreg(0x0000ff00u);
-        mf8 = vreg(0x000000f8u);
-    }
-    // single key: the H^4 table shared by the workgroup; descriptors: one H^4 table per wave
-    // (reloaded when the wave's key changes).  The once-per-packet multiplies by H^2..H^5 read the
-    // L2-resident key table from global memory, off the LDS pipe that bounds the kernel.
-    const uint32_t gH4 = kDesc ? kTe + wave * kGhBytes : kTe;
-    const uint32_t gH = kTe + kGhBytes;  // comb table of H in LDS (single key, !kGFin)
+    // masks as VGPRs (an SGPR or literal operand issues at half rate)
+    const uint32_t m8 = vreg(0x0000ff00u), mf8 = vreg(0x000000f8u);
+    // descriptors: one H^4 table per wave after the T-tables (reloaded when the wave's key changes)
+    const uint32_t gH4 = kDesc ? kTeBytes + wave * kGhBytes : 0u;
     uint32_t cur_key = kDesc ? 0xffffffffu : b.uniform_key;
     const uint32_t ntiles = kDesc ? (b.tile_list ? *b.n_list : b.n_items >> 4) : ((b.n + 15) >> 4);
 
@@ -1230,7 +777,7 @@ gcm_quad_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
 #pragma unroll
                     for (int r = 0; r < 8; ++r) {
                         const uint32_t e = r * 64 + lane;
-                        lds_st_comb<!kDesc>(gH4, e, src[e]);
+                        lds_st_comb(gH4, e, src[e]);
                     }
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                     __builtin_amdgcn_wave_barrier();
@@ -1266,19 +813,11 @@ gcm_quad_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
                 continue;  // the whole quad leaves together
             }
         }
-        if constexpr (kTab == 4) {
-            quad_packet<kSeal, kFold, kDesc, kGFin>(b, e4, pkt, off, L, wkey, m, gH4, gH);
-        } else if constexpr (kTab == 3) {
-            const Tab2F e3 = {{rk_table + (size_t)wkey * kRkWords, rk_table + (size_t)wkey * kRkWords + 64},
-                              {lb, m8}, mf8};
-            quad_packet<kSeal, kFold, kDesc, kGFin>(b, e3, pkt, off, L, wkey, m, gH4, gH);
-        } else if constexpr (kTab == 5) {
-            const Tab2T<true> e5 = {{rk_table + (size_t)wkey * kRkWords, rk_table + (size_t)wkey * kRkWords + 64},
-                                    {lb, m8}};
-            quad_packet<kSeal, kFold, kDesc, kGFin>(b, e5, pkt, off, L, wkey, m, gH4, gH);
+        const Keys kk = {rk_table + (size_t)wkey * kRkWords, rk_table + (size_t)wkey * kRkWords + 64};
+        if constexpr (kDesc) {
+            quad_packet<kSeal>(b, Tab2{kk, {lb, m8}}, pkt, off, L, wkey, m, gH4);
         } else {
-            const Tab2 e2 = {{rk_table + (size_t)wkey * kRkWords, rk_table + (size_t)wkey * kRkWords + 64}, {lb, 0}};
-            quad_packet<kSeal, kFold, kDesc, kGFin>(b, e2, pkt, off, L, wkey, m, gH4, gH);
+            quad_packet<kSeal>(b, Tab2F{kk, {lb, m8}, mf8}, pkt, off, L, wkey, m, gH4);
         }
     }
 }
@@ -1478,7 +1017,7 @@ gcm_seg_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
             if (pkt != 0xffffffffu) {  // the padding of a key run's last tile
                 const qgcm_desc dsc = b.descs[pkt];
                 const uint32_t L = kSeal ? dsc.len : dsc.len - QGCM_OVERHEAD;  // open: len >= 28 here
-                quad_packet<kSeal, false, true, true>(b, e3, pkt, dsc.offset, L, key, m, 0u, 0u);
+                quad_packet<kSeal>(b, e3, pkt, dsc.offset, L, key, m, 0u);
             }
             ++ntile_stat;
         }
@@ -1625,7 +1164,7 @@ __global__ void __launch_bounds__(kOneThreads) gcm_one_kernel(Batch b, const uin
 #pragma unroll
     for (int k = 0; k < kGhIt; ++k) {
         const uint32_t i = tid + k * kOneThreads, l = i >> 9;
-        if (l < ntabs) lds_st_comb<false>(kTeBytes + l * kGhBytes, i & 511u, gv[k]);
+        if (l < ntabs) lds_st_comb(kTeBytes + l * kGhBytes, i & 511u, gv[k]);
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -1709,7 +1248,7 @@ __global__ void __launch_bounds__(kOneThreads) gcm_one_kernel(Batch b, const uin
                     c.z &= m2;
                     c.w &= m3;
                 }
-                if (bi >= 64u || aad_lane) ghash_mul<false, false>(z0, z1, z2, z3, kTeBytes + 6 * kGhBytes);  // H^64
+                if (bi >= 64u || aad_lane) ghash_mul<false>(z0, z1, z2, z3, kTeBytes + 6 * kGhBytes);  // H^64
                 z0 ^= c.x;
                 z1 ^= c.y;
                 z2 ^= c.z;
@@ -1721,7 +1260,7 @@ __global__ void __launch_bounds__(kOneThreads) gcm_one_kernel(Batch b, const uin
             const int levels = top ? 32 - __builtin_clz(top) : 0;
             for (int l = 0; l < levels; ++l) {
                 uint32_t p0 = z0, p1 = z1, p2 = z2, p3 = z3;
-                ghash_mul<false, false>(p0, p1, p2, p3, kTeBytes + l * kGhBytes);
+                ghash_mul<false>(p0, p1, p2, p3, kTeBytes + l * kGhBytes);
                 z0 ^= __shfl_down(p0, 1u << l, 64);
                 z1 ^= __shfl_down(p1, 1u << l, 64);
                 z2 ^= __shfl_down(p2, 1u << l, 64);
@@ -1734,7 +1273,7 @@ __global__ void __launch_bounds__(kOneThreads) gcm_one_kernel(Batch b, const uin
                 z2 = 0;
                 z3 = bswap(L * 8u);
             }
-            ghash_mul<false, false>(z0, z1, z2, z3, kTeBytes + (m == 0 ? kGhBytes : 0u));
+            ghash_mul<false>(z0, z1, z2, z3, kTeBytes + (m == 0 ? kGhBytes : 0u));
             z0 ^= __shfl_down(z0, 1u, 64);
             z1 ^= __shfl_down(z1, 1u, 64);
             z2 ^= __shfl_down(z2, 1u, 64);
@@ -1810,80 +1349,36 @@ hipError_t launch_one(bool seal, const Batch &b, hipStream_t s) {
     return hipLaunchKernel(k, dim3(b.n), dim3(kOneThreads), args, kOneLds, s);
 }
 
-// Variant table: index = QGCM variant id (Batch-independent), see qgcm_api.cpp.
+// Variant table: index = QGCM variant id (Batch-independent), see qgcm_api.cpp.  The ids are the
+// round-2 ones (the A/B variants measured then -- lane-per-packet, 4-bit-comb and four-table
+// single-key kernels, folded J0, repeated-H recombination -- were removed in round 3; DESIGN.md keeps
+// their numbers): 12 = single-key quad kernel (Tab2F), 13 = per-wave descriptor kernel (Tab2),
+// 14 = segmented descriptor kernel (Tab2F) + 13 for the short keys.
 struct Variant {
     const void *seal, *open;
     int waves;
     uint32_t lds;
-    bool quad;       // 16 packets per wave tile instead of 64
     int wgs_per_cu;  // resident workgroups per CU the persistent grid is sized for
     bool desc;       // consumes the sorted 16-packet worklist (launch_quad_worklist)
     int complement;  // segmented: the per-wave variant that takes the short keys' tiles after it
 };
 
-template <int kW, bool kShared, int kIlp>
-Variant make_variant() {
-    return Variant{reinterpret_cast<const void *>(&gcm_kernel<true, kW, kShared, kIlp>),
-                   reinterpret_cast<const void *>(&gcm_kernel<false, kW, kShared, kIlp>), kW,
-                   lds_bytes<kW, kShared>(), false, 1, false, -1};
-}
-
-// the four-table engine: 128 KiB of T-tables + the H^4 comb = one 16-wave workgroup per CU
-template <int kW>
-Variant make_quad4() {
-    return Variant{reinterpret_cast<const void *>(&gcm_quad_kernel<true, kW, false, kW / 4, false, true, 4>),
-                   reinterpret_cast<const void *>(&gcm_quad_kernel<false, kW, false, kW / 4, false, true, 4>), kW,
-                   kTe4Bytes + kGhBytes, true, 1, false, -1};
-}
-
-template <int kW, bool kFold, int kWpe = kW / 4, bool kGFin = true>
-Variant make_quad() {
-    return Variant{reinterpret_cast<const void *>(&gcm_quad_kernel<true, kW, kFold, kWpe, false, kGFin>),
-                   reinterpret_cast<const void *>(&gcm_quad_kernel<false, kW, kFold, kWpe, false, kGFin>), kW,
-                   kQuadLds + (kGFin ? 0u : kGhBytes), true, kWpe * 4 / kW, false, -1};
-}
-
-// Tab2F engine (5-bit comb GHASH, byte-1 AND-OR addresses): 13 KiB comb + 64 KiB T-tables
-template <int kW, int kWpe>
-Variant make_quad2f() {
-    return Variant{reinterpret_cast<const void *>(&gcm_quad_kernel<true, kW, false, kWpe, false, true, 3>),
-                   reinterpret_cast<const void *>(&gcm_quad_kernel<false, kW, false, kWpe, false, true, 3>), kW,
-                   kG5Bytes + kTeBytes, true, kWpe * 4 / kW, false, -1};
-}
-
-// descriptor batches, Tab2F engine: one 5-bit comb per workgroup (gcm_seg_kernel)
-Variant make_seg() {
-    return Variant{reinterpret_cast<const void *>(&gcm_seg_kernel<true>),
-                   reinterpret_cast<const void *>(&gcm_seg_kernel<false>), 16, kSegLds, true, 2, true, 13};
-}
-
-// descriptor batches: per-wave H^4 table, so LDS = Te + one 8 KiB table per wave
-template <int kW, int kWpe, bool kGFin = true, int kTab = 2>
-Variant make_quad_desc() {
-    return Variant{reinterpret_cast<const void *>(&gcm_quad_kernel<true, kW, false, kWpe, true, kGFin, kTab>),
-                   reinterpret_cast<const void *>(&gcm_quad_kernel<false, kW, false, kWpe, true, kGFin, kTab>), kW,
-                   kTeBytes + (uint32_t)kW * kGhBytes, true, 1, true, -1};
-}
-
 static Variant g_variants[kNumVariants];
 
 hipError_t init_kernels() {
-    g_variants[0] = make_variant<8, false, 4>();  // general: lane per packet, per-wave GHASH tables
-    g_variants[1] = make_quad<16, false>();        // single key: 4 lanes per packet, 16 waves/CU
-    g_variants[2] = make_quad<16, true>();         // same, partial block and J0 folded into the loop
-    g_variants[3] = make_variant<8, true, 4>();    // single key, lane per packet, shared GHASH table
-    g_variants[4] = make_quad<12, false, 6>();     // quad, 12-wave workgroups, two per CU (24 waves/CU)
-    g_variants[5] = make_quad<16, false, 8>();     // quad, 16-wave workgroups, two per CU (32 waves/CU)
-    g_variants[6] = make_quad<8, false, 4>();      // quad, 8-wave workgroups, two per CU (16 waves/CU)
-    g_variants[7] = make_quad_desc<12, 3>();       // descriptors: quad, 12 waves/CU, per-wave H^4 tables
-    g_variants[8] = make_quad_desc<8, 2>();        // descriptors: quad, 8 waves/CU
-    g_variants[9] = make_quad<16, false, 8, false>();   // as 5, recombination by repeated H (LDS)
-    g_variants[10] = make_quad_desc<12, 3, false>();    // as 7, recombination by repeated H (global)
-    g_variants[11] = make_quad4<16>();                  // quad, four T-tables (128 KiB), 16 waves/CU
-    g_variants[13] = make_quad_desc<12, 3, true, 5>();  // as 7, byte-1 AND-OR addresses
-    g_variants[12] = make_quad2f<16, 8>();                // as 5, 5-bit comb GHASH + byte-1 AND-OR addresses
-    g_variants[14] = make_seg();                          // descriptors: Tab2F, one 5-bit comb per workgroup
+    g_variants[kVariantUniform] = Variant{reinterpret_cast<const void *>(&gcm_quad_kernel<true, false>),
+                                          reinterpret_cast<const void *>(&gcm_quad_kernel<false, false>),
+                                          quad_waves<false>(), kG5Bytes + kTeBytes,
+                                          quad_wpe<false>() * 4 / quad_waves<false>(), false, -1};
+    g_variants[kVariantDescWave] = Variant{reinterpret_cast<const void *>(&gcm_quad_kernel<true, true>),
+                                           reinterpret_cast<const void *>(&gcm_quad_kernel<false, true>),
+                                           quad_waves<true>(), kTeBytes + (uint32_t)quad_waves<true>() * kGhBytes,
+                                           1, true, -1};
+    g_variants[kVariantDescQuad] = Variant{reinterpret_cast<const void *>(&gcm_seg_kernel<true>),
+                                           reinterpret_cast<const void *>(&gcm_seg_kernel<false>), 16, kSegLds, 2, true,
+                                           kVariantDescWave};
     for (const Variant &v : g_variants) {
+        if (!v.seal) continue;
         for (const void *k : {v.seal, v.open}) {
             hipFuncAttributes a;
             hipError_t e = hipFuncGetAttributes(&a, k);
@@ -1906,14 +1401,14 @@ hipError_t init_kernels() {
     return hipSuccess;
 }
 
+bool variant_valid(int v) { return v >= 0 && v < kNumVariants && g_variants[v].seal != nullptr; }
 int variant_waves(int v) { return g_variants[v].waves; }
-bool variant_quad(int v) { return g_variants[v].quad; }
 int variant_wgs_per_cu(int v) { return g_variants[v].wgs_per_cu; }
 bool variant_desc(int v) { return g_variants[v].desc; }
 int variant_complement(int v) { return g_variants[v].complement; }
 
 hipError_t launch_packets(bool seal, int variant, const Batch &b, int grid, hipStream_t s) {
-    if (variant < 0 || variant >= kNumVariants) return hipErrorInvalidValue;
+    if (!variant_valid(variant)) return hipErrorInvalidValue;
     const Variant &v = g_variants[variant];
     void *args[] = {const_cast<Batch *>(&b), const_cast<uint32_t **>(&b.rk_table)};
     return hipLaunchKernel(seal ? v.seal : v.open, dim3(grid), dim3(v.waves * 64), args, v.lds, s);
@@ -2050,67 +1545,6 @@ hipError_t launch_key_setup(const uint8_t *d_keys, uint32_t first, uint32_t coun
                             uint4 *gh_table, const uint8_t *d_sbox, hipStream_t s) {
     if (count == 0) return hipSuccess;
     hipLaunchKernelGGL(key_setup_kernel, dim3(count), dim3(256), 0, s, d_keys, first, rk_table, gh_table, d_sbox);
-    return hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------------------------
-// Worklist: counting sort of descriptor batches by key_idx into 64-aligned key groups, so every
-// wave64 tile is key-uniform.  Packets with key_idx >= max_keys or an unset key slot are dropped
-// (status stays 0).
-__global__ void wl_hist_kernel(const qgcm_desc *descs, uint32_t n, uint32_t max_keys, const uint8_t *key_valid,
-                               uint32_t *counts) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) {
-        const uint32_t k = descs[i].key_idx;
-        if (k < max_keys && key_valid[k]) atomicAdd(&counts[k], 1u);
-    }
-}
-
-// Single workgroup: counts[k] -> padded exclusive offsets (in place), cursors zeroed by memset.
-__global__ void __launch_bounds__(1024) wl_scan_kernel(uint32_t *counts, uint32_t max_keys) {
-    __shared__ uint32_t partial[1024];
-    const uint32_t t = threadIdx.x;
-    const uint32_t per = (max_keys + 1023) / 1024;
-    const uint32_t lo = t * per, hi = min(lo + per, max_keys);
-    uint32_t sum = 0;
-    for (uint32_t k = lo; k < hi; ++k) sum += (counts[k] + 63u) & ~63u;
-    partial[t] = sum;
-    __syncthreads();
-    for (uint32_t d = 1; d < 1024; d <<= 1) {
-        const uint32_t v = t >= d ? partial[t - d] : 0;
-        __syncthreads();
-        partial[t] += v;
-        __syncthreads();
-    }
-    uint32_t run = partial[t] - sum;
-    for (uint32_t k = lo; k < hi; ++k) {
-        const uint32_t c = (counts[k] + 63u) & ~63u;
-        counts[k] = run;
-        run += c;
-    }
-}
-
-__global__ void wl_scatter_kernel(const qgcm_desc *descs, uint32_t n, uint32_t max_keys, const uint8_t *key_valid,
-                                  const uint32_t *offs, uint32_t *cursors, uint32_t *worklist) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) {
-        const uint32_t k = descs[i].key_idx;
-        if (k < max_keys && key_valid[k]) worklist[offs[k] + atomicAdd(&cursors[k], 1u)] = i;
-    }
-}
-
-hipError_t launch_build_worklist(const qgcm_desc *descs, uint32_t n, uint32_t max_keys, const uint8_t *key_valid,
-                                 uint32_t *counts,
-                                 uint32_t *cursors, uint32_t *worklist, uint32_t n_items_cap, hipStream_t s) {
-    hipError_t e;
-    if ((e = hipMemsetAsync(counts, 0, sizeof(uint32_t) * max_keys, s)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(cursors, 0, sizeof(uint32_t) * max_keys, s)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(worklist, 0xff, sizeof(uint32_t) * n_items_cap, s)) != hipSuccess) return e;
-    const int bs = 256, g = (int)((n + bs - 1) / bs);
-    if (n) hipLaunchKernelGGL(wl_hist_kernel, dim3(g), dim3(bs), 0, s, descs, n, max_keys, key_valid, counts);
-    hipLaunchKernelGGL(wl_scan_kernel, dim3(1), dim3(1024), 0, s, counts, max_keys);
-    if (n) hipLaunchKernelGGL(wl_scatter_kernel, dim3(g), dim3(bs), 0, s, descs, n, max_keys, key_valid, counts, cursors,
-                                     worklist);
     return hipGetLastError();
 }
 

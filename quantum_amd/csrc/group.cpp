@@ -216,6 +216,7 @@ struct qgcm_group {
     uint32_t max_keys = 0;
     bool zerocopy = true;  // QGCM_GROUP_ZEROCOPY=0: always gather/scatter on the CPU
     int last_zc = 0;       // the last call took the zero-copy path (qgcm_group_last_zerocopy)
+    uint64_t zc_chunk = kZcChunk;  // zero-copy staging chunk bytes (QGCM_GROUP_ZC_CHUNK_MB, tuning)
     std::mutex call_mu;  // one batch call at a time (members' staging is reused per call)
 };
 
@@ -342,8 +343,6 @@ int run_member(Member &mb, bool seal, uint8_t *h_arena, const qgcm_desc *descs, 
     return rc;
 }
 
-uint64_t g_zc_chunk = kZcChunk;  // QGCM_GROUP_ZC_CHUNK_MB (tuning)
-
 template <typename T>
 bool grow_pinned(T *&h, T *&d, size_t count) {
     if (h) hipHostFree(h);
@@ -371,10 +370,10 @@ uint64_t pinned_view(const void *p, uint64_t bytes) {
     return dv >= b && dv + bytes <= b + size ? dv : 0;
 }
 
+// Zero-copy form of run_member: the member's GPU gathers its records from the pinned arena itself.
+// v_arena / v_nonces: the arena's and nonces' device views resolved on this member's device.
 int run_member_zc(Member &mb, bool seal, uint64_t v_arena, const qgcm_desc *descs, const uint32_t *idx, size_t m,
-                  uint64_t v_nonces, uint32_t aad_len, uint8_t *h_status, int *bad_out) {
-    if (mb.ncpus > 0) pthread_setaffinity_np(pthread_self(), sizeof(mb.cpus), &mb.cpus);
-    if (hipSetDevice(mb.device) != hipSuccess) return QGCM_E_HIP;
+                  uint64_t v_nonces, uint32_t aad_len, uint8_t *h_status, int *bad_out, uint64_t chunk) {
     ZC &z = mb.zc;
     for (Stage &s : mb.st)
         if (!s.s && hipStreamCreateWithFlags(&s.s, hipStreamNonBlocking) != hipSuccess) return QGCM_E_HIP;
@@ -386,7 +385,6 @@ int run_member_zc(Member &mb, bool seal, uint64_t v_arena, const qgcm_desc *desc
         z.cap = cap;
     }
     // staging slot: a chunk's records (up to `chunk` bytes, or one larger record) + 256-B pad + their nonces
-    const uint64_t chunk = g_zc_chunk;
     uint64_t need = chunk;
     for (size_t j = 0; j < m; ++j) need = std::max<uint64_t>(need, rec_bytes(seal, descs[idx[j]].len));
     need += 256 + 12ull * (chunk / 32 + 1);  // records are >= 32 B: at most chunk / 32 + 1 per chunk
@@ -486,36 +484,49 @@ int run_group(qgcm_group *g, bool seal, uint8_t *h_arena, const qgcm_desc *descs
         const qgcm_desc &d = descs[i];
         const bool ok = d.key_idx < g->max_keys && (seal ? d.len < QGCM_MAX_PAYLOAD
                                                           : d.len >= QGCM_OVERHEAD && d.len - QGCM_OVERHEAD < QGCM_MAX_PAYLOAD);
-        if (!ok || (d.offset & 3)) {  // rejected as the device batch would: status 0, slot untouched
+        if (!ok) {  // rejected as the device batch would: status 0, slot untouched
             if (h_status) h_status[i] = 0;
             ++pre_bad;
             continue;
         }
         part[qgcm_group_shard(g, d.key_idx)].push_back(i);
     }
-    // zero-copy when the arena (and nonces) are pinned and hold every record
-    uint64_t v_arena = 0, v_nonces = 0;
-    if (g->zerocopy) {
-        uint64_t extent = 0;
-        for (uint32_t i = 0; i < n; ++i)
-            extent = std::max<uint64_t>(extent, descs[i].offset + 4ull + descs[i].len + (seal ? QGCM_OVERHEAD : 0));
-        v_arena = pinned_view(h_arena, extent);
-        if (v_arena && seal && h_nonces && !(v_nonces = pinned_view(h_nonces, 12ull * n))) v_arena = 0;
-        if ((v_arena | v_nonces) & 3) v_arena = 0;  // the record moves are dword-wise
+    // zero-copy when the arena (and nonces) are pinned and hold every record, and every record starts
+    // on a 4-B boundary (the record moves are dword-wise; other batches take the copy path, which
+    // re-aligns records in staging).  Each member resolves the device view on its own device.
+    bool zc = g->zerocopy;
+    uint64_t extent = 0;
+    for (uint32_t i = 0; zc && i < n; ++i) {
+        extent = std::max<uint64_t>(extent, descs[i].offset + 4ull + descs[i].len + (seal ? QGCM_OVERHEAD : 0));
+        zc = !(descs[i].offset & 3);
     }
-    g->last_zc = v_arena ? 1 : 0;
-    std::vector<int> rc(G, QGCM_OK), bad(G, 0);
+    zc = zc && !((uintptr_t)h_arena & 3) && !(seal && h_nonces && ((uintptr_t)h_nonces & 3));
+    std::vector<int> rc(G, QGCM_OK), bad(G, 0), used_zc(G, 1);
     std::vector<std::thread> thr;
     for (int k = 0; k < G; ++k) {
         if (part[k].empty()) continue;
         thr.emplace_back([&, k] {
-            rc[k] = v_arena ? run_member_zc(g->m[k], seal, v_arena, descs, part[k].data(), part[k].size(), v_nonces,
-                                            aad_len, h_status, &bad[k])
-                            : run_member(g->m[k], seal, h_arena, descs, part[k].data(), part[k].size(), h_nonces,
-                                         aad_len, h_status, &bad[k]);
+            Member &mb = g->m[k];
+            if (mb.ncpus > 0) pthread_setaffinity_np(pthread_self(), sizeof(mb.cpus), &mb.cpus);
+            if (hipSetDevice(mb.device) != hipSuccess) {
+                rc[k] = QGCM_E_HIP;
+                return;
+            }
+            uint64_t va = 0, vn = 0;
+            if (zc) {
+                va = pinned_view(h_arena, extent);
+                if (va && seal && h_nonces && !(vn = pinned_view(h_nonces, 12ull * n))) va = 0;
+                if ((va | vn) & 3) va = 0;
+            }
+            used_zc[k] = va ? 1 : 0;
+            rc[k] = va ? run_member_zc(mb, seal, va, descs, part[k].data(), part[k].size(), vn, aad_len, h_status,
+                                       &bad[k], g->zc_chunk)
+                       : run_member(mb, seal, h_arena, descs, part[k].data(), part[k].size(), h_nonces, aad_len,
+                                    h_status, &bad[k]);
         });
     }
     for (auto &t : thr) t.join();
+    g->last_zc = zc && std::all_of(used_zc.begin(), used_zc.end(), [](int u) { return u == 1; }) ? 1 : 0;
     int total_bad = pre_bad;
     for (int k = 0; k < G; ++k) {
         if (rc[k] != QGCM_OK) return rc[k];
@@ -538,7 +549,7 @@ qgcm_group *qgcm_group_create(const int *devices, int count, uint32_t max_keys, 
     int threads = kCopyThreads;
     if (const char *v = getenv("QGCM_GROUP_THREADS")) threads = std::max(1, std::min(64, atoi(v)));
     if (const char *v = getenv("QGCM_GROUP_ZEROCOPY")) g->zerocopy = atoi(v) != 0;
-    if (const char *v = getenv("QGCM_GROUP_ZC_CHUNK_MB")) g_zc_chunk = (uint64_t)std::max(1, atoi(v)) << 20;
+    if (const char *v = getenv("QGCM_GROUP_ZC_CHUNK_MB")) g->zc_chunk = (uint64_t)std::max(1, atoi(v)) << 20;
     for (int k = 0; k < count; ++k) {
         Member mb;
         mb.device = devices[k];

@@ -11,15 +11,12 @@
 #include <string.h>
 #include <sys/random.h>
 
-#include <atomic>
-#include <chrono>
-#include <memory>
-#include <thread>
 #include <algorithm>
 #include <atomic>
 #include <chrono>
-#include <chrono>
+#include <memory>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "../../include/qgcm.h"
@@ -57,8 +54,6 @@ struct qgcm_ctx {
 
     // descriptor-batch workspace (worklist), guarded by ws_mu for the whole enqueue
     std::mutex ws_mu;
-    uint32_t *d_counts = nullptr, *d_cursors = nullptr, *d_worklist = nullptr;
-    size_t wl_cap = 0;
     void *d_qws = nullptr;  // sorted quad worklist workspace
     size_t qws_cap = 0;
 
@@ -97,6 +92,9 @@ struct qgcm_ctx {
     // orders reuse of the descriptor workspace across streams (guarded by ws_mu)
     hipEvent_t ws_done = nullptr;
     bool ws_pending = false;
+
+    std::atomic<uint64_t> launches[QGCM_KERNEL_COUNTERS] = {};  // qgcm_launch_counts
+    void count(int k, uint64_t v = 1) { launches[k].fetch_add(v, std::memory_order_relaxed); }
 };
 
 namespace {
@@ -147,7 +145,7 @@ int hip_fail(hipError_t e) { return e == hipSuccess ? QGCM_OK : QGCM_E_HIP; }
 
 int grid_for(const qgcm_ctx *ctx, uint32_t n_items, int variant) {
     const uint32_t waves = (uint32_t)variant_waves(variant);
-    const uint32_t tiles = variant_quad(variant) ? (n_items + 15) / 16 : n_items / 64;
+    const uint32_t tiles = (n_items + 15) / 16;  // 16-packet wave tiles
     const uint32_t wgs = (tiles + waves - 1) / waves;
     // persistent grid: the resident workgroups (each fills its own LDS tables once)
     const uint32_t per_cu = ctx->wgs_per_cu_override > 0 ? (uint32_t)ctx->wgs_per_cu_override
@@ -190,6 +188,7 @@ int run_one(qgcm_ctx *ctx, bool seal, uint8_t *slot, uint64_t stride, uint32_t l
         b.n_items = 64;
         b.aad_len = aad_len;
         if (launch_one(seal, b, s) != hipSuccess) return QGCM_E_HIP;
+        ctx->count(QGCM_KERNEL_ONE);
         const auto t0 = std::chrono::steady_clock::now();
         for (uint32_t spins = 0; *done == 0; ++spins) {
             __builtin_ia32_pause();
@@ -229,7 +228,9 @@ int qgcm::run_one_descs(qgcm_ctx *ctx, bool seal, uint8_t *arena, const qgcm_des
     b.n = n;
     b.aad_len = aad_len;
     b.done = done;
-    return hip_fail(launch_one(seal, b, s));
+    if (launch_one(seal, b, s) != hipSuccess) return QGCM_E_HIP;
+    ctx->count(QGCM_KERNEL_ONE);
+    return QGCM_OK;
 }
 bool qgcm::ctx_key_ready(qgcm_ctx *ctx, uint32_t key_idx) { return key_ok(ctx, key_idx); }
 
@@ -259,8 +260,11 @@ int run_uniform(qgcm_ctx *ctx, bool seal, uint8_t *arena, uint64_t stride, uint3
     // workgroup per packet, when the slots allow it and no kernel variant is forced (QGCM_VARIANT).
     const uint64_t stage = (4ull + len + (seal ? QGCM_OVERHEAD : 0) + 15) & ~15ull;
     if (ctx->one_kernel && !ctx->variant_forced && n <= ctx->one_uniform_max && !(stride & 15) &&
-        !((uintptr_t)arena & 15) && stage <= stride && stage <= kOneCap - 16)
-        return hip_fail(launch_one(seal, b, s));
+        !((uintptr_t)arena & 15) && stage <= stride && stage <= kOneCap - 16) {
+        if (launch_one(seal, b, s) != hipSuccess) return QGCM_E_HIP;
+        ctx->count(QGCM_KERNEL_ONE);
+        return QGCM_OK;
+    }
     const int v = ctx->uniform_variant;
     // Large batches go out as back-to-back launches of launch_chunk packets on the same stream: one
     // 2^23-packet launch ran at 768 GiB/s, the same batch as 2^19-packet launches at 827, at 2^20 packets
@@ -275,6 +279,7 @@ int run_uniform(qgcm_ctx *ctx, bool seal, uint8_t *arena, uint64_t stride, uint3
         c.n = m;
         c.n_items = (uint32_t)(((uint64_t)m + 63) & ~63ull);
         if (launch_packets(seal, v, c, grid_for(ctx, c.n_items, v), s) != hipSuccess) return QGCM_E_HIP;
+        ctx->count(QGCM_KERNEL_QUAD);
     }
     return QGCM_OK;
 }
@@ -311,7 +316,7 @@ int run_descs_locked(qgcm_ctx *ctx, bool seal, const qgcm_desc *descs, uint32_t 
     b.n = n;
     b.aad_len = aad_len;
     const int v = ctx->desc_variant;
-    if (variant_desc(v) && ctx->desc_chunk && n > ctx->desc_chunk) {
+    if (ctx->desc_chunk && n > ctx->desc_chunk) {
         // back-to-back chunks on this stream, each with its own sorted worklist (the workspace is
         // reused in stream order); descriptors, nonces and status are chunk-relative, offsets absolute
         for (uint32_t p = 0; p < n; p += ctx->desc_chunk) {
@@ -322,7 +327,7 @@ int run_descs_locked(qgcm_ctx *ctx, bool seal, const qgcm_desc *descs, uint32_t 
         }
         return QGCM_OK;
     }
-    if (variant_desc(v)) {
+    {
         uint32_t items = 0;
         const size_t need = quad_worklist_bytes(n, ctx->max_keys, &items);
         if (need > ctx->qws_cap) {
@@ -344,6 +349,7 @@ int run_descs_locked(qgcm_ctx *ctx, bool seal, const qgcm_desc *descs, uint32_t 
         b.tile_counter = q.tile_counter;
         b.n_items = q.n_items;
         if (launch_packets(seal, v, b, grid_for(ctx, b.n_items, v), s) != hipSuccess) return QGCM_E_HIP;
+        ctx->count(v == kVariantDescQuad ? QGCM_KERNEL_SEGMENTED : QGCM_KERNEL_PER_WAVE);
         const int vc = variant_complement(v);
         if (vc < 0) return QGCM_OK;
         // the short keys' tiles (fewer than kSegMinTiles per key) through the per-wave kernel; its
@@ -351,23 +357,10 @@ int run_descs_locked(qgcm_ctx *ctx, bool seal, const qgcm_desc *descs, uint32_t 
         b.tile_list = q.short_tiles;
         b.n_list = q.nshort;
         b.tile_counter = q.tile_counter + 3;
-        return hip_fail(launch_packets(seal, vc, b, grid_for(ctx, b.n_items, vc), s));
+        if (launch_packets(seal, vc, b, grid_for(ctx, b.n_items, vc), s) != hipSuccess) return QGCM_E_HIP;
+        ctx->count(QGCM_KERNEL_PER_WAVE);
+        return QGCM_OK;
     }
-    const uint64_t cap = (uint64_t)n + 64ull * (n < ctx->max_keys ? n : ctx->max_keys);
-    const uint32_t items = (uint32_t)((cap + 63) & ~63ull);
-    if (items > ctx->wl_cap) {
-        if (ctx->d_worklist) hipFree(ctx->d_worklist);
-        ctx->d_worklist = nullptr;
-        ctx->wl_cap = 0;
-        if (hipMalloc(&ctx->d_worklist, (size_t)items * sizeof(uint32_t)) != hipSuccess) return QGCM_E_NOMEM;
-        ctx->wl_cap = items;
-    }
-    hipError_t e = launch_build_worklist(descs, n, ctx->max_keys, ctx->d_key_valid, ctx->d_counts, ctx->d_cursors,
-                                         ctx->d_worklist, items, s);
-    if (e != hipSuccess) return QGCM_E_HIP;
-    b.worklist = ctx->d_worklist;
-    b.n_items = items;
-    return hip_fail(launch_packets(seal, v, b, grid_for(ctx, b.n_items, v), s));
 }
 
 // Per-packet streams are created at the highest priority the device offers, so a per-packet call
@@ -418,13 +411,18 @@ qgcm_ctx::OneSlot *acquire_one(qgcm_ctx *ctx, size_t bytes, std::unique_lock<std
     return sl;
 }
 
-// The big slot keeps up to 64 MiB pinned between calls; beyond that it is released after the call.
-void release_big(qgcm_ctx *ctx, qgcm_ctx::OneSlot *sl) {
-    if (sl != &ctx->big || sl->cap <= (64u << 20)) return;
-    hipHostFree(sl->h);
-    sl->h = nullptr;
-    sl->cap = 0;
-}
+// The big slot keeps up to 64 MiB pinned between calls; beyond that it is released after the call
+// (on every return path: the guard runs while the slot's lock is still held).
+struct BigRelease {
+    qgcm_ctx *ctx;
+    qgcm_ctx::OneSlot *sl;
+    ~BigRelease() {
+        if (!sl || sl != &ctx->big || sl->cap <= (64u << 20)) return;
+        hipHostFree(sl->h);
+        sl->h = nullptr;
+        sl->cap = 0;
+    }
+};
 
 }  // namespace
 
@@ -487,7 +485,7 @@ qgcm_ctx *qgcm_create(int device, uint32_t max_keys, char *err, int errlen) {
     ctx->key_set.assign(max_keys, 0);
     if (const char *v = getenv("QGCM_VARIANT")) {  // kernel variant overrides (tuning and tests)
         const int iv = atoi(v);
-        if (iv >= 0 && iv < kNumVariants && !variant_desc(iv)) {
+        if (variant_valid(iv) && !variant_desc(iv)) {
             ctx->uniform_variant = iv;
             ctx->variant_forced = true;
         }
@@ -502,7 +500,7 @@ qgcm_ctx *qgcm_create(int device, uint32_t max_keys, char *err, int errlen) {
     if (const char *v = getenv("QGCM_PIPE_RING_MB")) ctx->host_ring = (uint64_t)std::max(1, atoi(v)) << 20;
     if (const char *v = getenv("QGCM_DESC_VARIANT")) {
         const int iv = atoi(v);
-        if (iv == kVariantGeneral || (iv >= 0 && iv < kNumVariants && variant_desc(iv))) ctx->desc_variant = iv;
+        if (variant_valid(iv) && variant_desc(iv)) ctx->desc_variant = iv;
     }
     uint8_t sbox[256];
     uint32_t te[512];
@@ -515,8 +513,6 @@ qgcm_ctx *qgcm_create(int device, uint32_t max_keys, char *err, int errlen) {
               hipMemset(ctx->d_gh, 0, (size_t)max_keys * kGhEntries * 16) == hipSuccess &&
               hipMemset(ctx->d_key_valid, 0, max_keys) == hipSuccess &&
               hipMalloc(&ctx->d_te, sizeof te) == hipSuccess && hipMalloc(&ctx->d_sbox, sizeof sbox) == hipSuccess &&
-              hipMalloc(&ctx->d_counts, (size_t)max_keys * 4) == hipSuccess &&
-              hipMalloc(&ctx->d_cursors, (size_t)max_keys * 4) == hipSuccess &&
               hipMemcpy(ctx->d_te, te, sizeof te, hipMemcpyHostToDevice) == hipSuccess &&
               hipMemcpy(ctx->d_sbox, sbox, sizeof sbox, hipMemcpyHostToDevice) == hipSuccess &&
               hipEventCreateWithFlags(&ctx->ws_done, hipEventDisableTiming) == hipSuccess;
@@ -539,9 +535,6 @@ void qgcm_destroy(qgcm_ctx *ctx) {
     hipFree(ctx->d_te);
     hipFree(ctx->d_sbox);
     hipFree(ctx->d_key_valid);
-    hipFree(ctx->d_counts);
-    hipFree(ctx->d_cursors);
-    hipFree(ctx->d_worklist);
     hipFree(ctx->d_qws);
     auto free_slot = [](qgcm_ctx::OneSlot &sl) {
         if (sl.h) hipHostFree(sl.h);
@@ -634,6 +627,7 @@ long qgcm_seal_one(qgcm_ctx *ctx, uint32_t key_idx, uint8_t *data, long length, 
     std::unique_lock<std::mutex> lk;
     qgcm_ctx::OneSlot *sl = acquire_one(ctx, stride + 16, lk);
     if (!sl) return -1;
+    const BigRelease rel{ctx, sl};
     uint8_t *h = sl->h;
     memset(h, 0, stride);
     if (aad_len) memcpy(h, aad, aad_len);
@@ -646,7 +640,6 @@ long qgcm_seal_one(qgcm_ctx *ctx, uint32_t key_idx, uint8_t *data, long length, 
     if (run_one(ctx, true, h, stride, (uint32_t)length, key_idx, aad_len, h + stride, s) != QGCM_OK) return -1;
     if (h[stride] != 1) return -1;
     memcpy(data, h + 4, (size_t)length + QGCM_OVERHEAD);
-    release_big(ctx, sl);
     return length + QGCM_OVERHEAD;
 }
 
@@ -659,6 +652,7 @@ long qgcm_open_one(qgcm_ctx *ctx, uint32_t key_idx, uint8_t *data, long len, con
     std::unique_lock<std::mutex> lk;
     qgcm_ctx::OneSlot *sl = acquire_one(ctx, stride + 16, lk);
     if (!sl) return -1;
+    const BigRelease rel{ctx, sl};
     uint8_t *h = sl->h;
     memset(h, 0, stride);
     if (aad_len) memcpy(h, aad, aad_len);
@@ -667,9 +661,7 @@ long qgcm_open_one(qgcm_ctx *ctx, uint32_t key_idx, uint8_t *data, long len, con
     h[stride] = 0;
     if (run_one(ctx, false, h, stride, (uint32_t)len, key_idx, aad_len, h + stride, s) != QGCM_OK) return -1;
     memcpy(data, h + 4, (size_t)len - QGCM_OVERHEAD);  // plaintext, or zeros on auth failure
-    const bool ok = h[stride] == 1;
-    release_big(ctx, sl);
-    return ok ? len - QGCM_OVERHEAD : -1;
+    return h[stride] == 1 ? len - QGCM_OVERHEAD : -1;
 }
 
 // Host batches, pipelined: the batch is cut into ~64 MiB chunks, each with its own device slot while
@@ -1019,6 +1011,13 @@ int qgcm_fill_uniform(uint8_t *d_arena, uint64_t stride, uint32_t n, uint32_t le
     if ((n && !d_arena) || (n && stride < (uint64_t)len + 4)) return QGCM_E_ARG;
     return hip_fail(launch_fill_uniform(d_arena, stride, n, len, aad_word, seed_payload, d_nonces, seed_nonce,
                                         (hipStream_t)stream));
+}
+
+int qgcm_launch_counts(const qgcm_ctx *ctx, uint64_t *out, int n) {
+    if (!ctx || n < 0 || (n && !out)) return -1;
+    const int m = n < QGCM_KERNEL_COUNTERS ? n : QGCM_KERNEL_COUNTERS;
+    for (int i = 0; i < m; ++i) out[i] = ctx->launches[i].load(std::memory_order_relaxed);
+    return m;
 }
 
 int qgcm_stream_copy(qgcm_ctx *ctx, void *d_dst, const void *d_src, uint64_t bytes, void *stream) {

@@ -68,16 +68,24 @@ class Group:
         if not h:
             raise _lib.QgcmError(f"qgcm_group_create({list(devices)}): {err.value.decode()}")
         self.handle, self.devices, self.max_keys = h, list(devices), max_keys
+        self._views = []  # weak references to the member contexts handed out
 
     def member(self, m: int):
-        """Member m's device context (borrowed: the group owns it) for device batches on it."""
+        """Member m's device context (borrowed: the group owns it) for device batches on it.  The view
+        keeps the group alive; closing the group invalidates it (its handle becomes None)."""
+        import weakref
+
         from . import _lib
         from .crypto import Context
 
+        if not self.handle:
+            raise _lib.QgcmError("group is closed")
         h = _lib.lib().qgcm_group_ctx(self.handle, m)
         if not h:
             raise _lib.QgcmError(f"no member {m}")
-        return Context.borrowed(h, self.devices[m], self.max_keys)
+        c = Context.borrowed(h, self.devices[m], self.max_keys, owner=self)
+        self._views.append(weakref.ref(c))
+        return c
 
     def shard(self, key_idx: int) -> int:
         from . import _lib
@@ -121,6 +129,12 @@ class Group:
         from . import _lib
 
         if self.handle:
+            for ref in self._views:  # borrowed member contexts must not outlive the members
+                c = ref()
+                if c is not None:
+                    c.handle = None
+                    c._owner = None
+            self._views = []
             _lib.lib().qgcm_group_destroy(self.handle)
             self.handle = None
 

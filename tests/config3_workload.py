@@ -1,86 +1,36 @@
-"""BASELINE config 3, defined once for the golden generator (tests/golden/make_golden.py) and the GPU
-parity tests (tests/test_gpu_config3.py) -- TEST INFRASTRUCTURE.
+"""BASELINE config 3 for the golden generator (tests/golden/make_golden.py) and the GPU parity tests
+(tests/test_gpu_config3.py) -- TEST INFRASTRUCTURE.
 
-2^20 packets, payload lengths ~ U{64..9000} (the first few forced onto the counter-segment edges of
-the kernels: block 254/255 -> 256 is where the counter cache of a packet is re-derived, L = 4064..4097,
-and again at 8160..8193), 1024 per-peer keys derived as common/mapping.go:90-99 does it (X25519 of
-this node's private key with the peer's public key = secret, the same for the salts, then
-crypto/aes.go:66 PBKDF2-HMAC-SHA512 x10000), key index ~ U[0, 1024), AAD = the peer's private IPv4
-10.99.(k >> 8).(k & 255) in Raw[0:4] (worker/outgoing.go:28-35 writes the sender IP there).
-
-Slots are packed Payload.Raw records, 4-B aligned: slot i at offs[i], (4 + L + 28 + 3) & ~3 bytes.
-Arena bytes before sealing: qgcm_fill_uniform over 1 MiB chunks (chunk c = [AAD_WORD][splitmix64
-stream of SEED_ARENA at byte offset c * (2^20 - 4)]), then each packet's 4-B AAD.  Nonces: the
-splitmix64 stream of SEED_NONCE, 12 B per packet.  Lengths and key indices: splitmix64 outputs.
+The workload itself is defined once in quantum_amd/workloads.py (bench.py measures the same one);
+this module adds the oracle-side views: the peer inputs and nonces drawn through the oracle's own
+splitmix64 stream (so the package's numpy stream is checked against the C restatement) and the whole
+arena built on the host.
 """
 from __future__ import annotations
 
 import numpy as np
 
-N = 1 << 20
-NKEYS = 1024
-CHUNK = 1 << 20
-AAD_WORD = int.from_bytes(bytes([10, 99, 0, 1]), "little")
-SEED_ME, SEED_PEERS = 0x5EED0003, 0x5EED0004  # tests/golden/kdf.json "peers"
-SEED_LEN, SEED_KEY = 0x5EED0031, 0x5EED0032
-SEED_ARENA, SEED_NONCE = 0x5EED0033, 0x5EED0034
-FORCED = [4064, 4065, 4079, 4080, 4081, 4095, 4096, 4097, 8160, 8161, 8176, 8191, 8192, 8193, 8999, 9000,
-          64, 65, 1350, 1433]
-
-_M = np.uint64(0xFFFFFFFFFFFFFFFF)
-
-
-def splitmix64(seed: int, k: np.ndarray) -> np.ndarray:
-    """Output k of the splitmix64 generator started at seed (oracle_splitmix64_at), vectorised."""
-    with np.errstate(over="ignore"):
-        z = np.uint64(seed) + (k.astype(np.uint64) + np.uint64(1)) * np.uint64(0x9E3779B97F4A7C15)
-        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
-        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
-        return z ^ (z >> np.uint64(31))
-
-
-def lengths(n: int = N) -> np.ndarray:
-    i = np.arange(n, dtype=np.uint64)
-    L = (np.uint64(64) + splitmix64(SEED_LEN, i) % np.uint64(8937)).astype(np.uint32)
-    m = min(n, len(FORCED))
-    L[:m] = FORCED[:m]
-    return L
-
-
-def key_indices(n: int = N) -> np.ndarray:
-    return (splitmix64(SEED_KEY, np.arange(n, dtype=np.uint64)) % np.uint64(NKEYS)).astype(np.uint32)
-
-
-def layout(lens: np.ndarray) -> tuple[np.ndarray, int]:
-    """Packed 4-B aligned slot offsets and the arena size (whole fill chunks, >= 64 B of slack)."""
-    slot = (4 + lens.astype(np.uint64) + 28 + 3) & ~np.uint64(3)
-    offs = np.zeros(len(lens), dtype=np.uint64)
-    offs[1:] = np.cumsum(slot)[:-1]
-    used = int(offs[-1] + slot[-1]) if len(lens) else 0
-    chunks = (used + 64 + CHUNK - 1) // CHUNK
-    return offs, chunks * CHUNK
-
-
-def aad_of_key(k: np.ndarray) -> np.ndarray:
-    """(n, 4) uint8: 10.99.(k >> 8).(k & 255)."""
-    a = np.empty((len(k), 4), dtype=np.uint8)
-    a[:, 0], a[:, 1] = 10, 99
-    a[:, 2] = (k >> 8) & 0xFF
-    a[:, 3] = k & 0xFF
-    return a
+from quantum_amd.workloads import (AAD_WORD, CHUNK, FORCED, N, NKEYS, SEED_ARENA, SEED_KEY, SEED_LEN,  # noqa: F401
+                                   SEED_ME, SEED_NONCE, SEED_PEERS, aad_of_key, key_indices, layout, lengths,
+                                   put_aads, splitmix64, tail_index)
+from quantum_amd import workloads as _W
 
 
 def peer_inputs(O) -> tuple[bytes, bytes, list[bytes], list[bytes]]:
-    """This node's private key and salt, and each peer's private key and salt (kdf.json recipe)."""
+    """This node's private key and salt, and each peer's private key and salt (kdf.json recipe),
+    from the oracle's stream; equal to quantum_amd.workloads.peer_inputs() (asserted here)."""
     me_priv = O.stream_bytes(SEED_ME, 0, 32)
     me_salt = O.stream_bytes(SEED_ME, 32, 32)
     privs = [O.stream_bytes(SEED_PEERS, 64 * i, 32) for i in range(NKEYS)]
     salts = [O.stream_bytes(SEED_PEERS, 64 * i + 32, 32) for i in range(NKEYS)]
+    assert (me_priv, me_salt, privs, salts) == _W.peer_inputs()
     return me_priv, me_salt, privs, salts
 
 
 def nonces(O, n: int = N) -> np.ndarray:
-    return np.frombuffer(O.stream_bytes(SEED_NONCE, 0, 12 * n), dtype=np.uint8).copy()
+    out = np.frombuffer(O.stream_bytes(SEED_NONCE, 0, 12 * n), dtype=np.uint8).copy()
+    assert np.array_equal(out, _W.nonces(n))
+    return out
 
 
 def host_arena(O, size: int, offs: np.ndarray, kidx: np.ndarray) -> np.ndarray:
@@ -94,19 +44,3 @@ def host_arena(O, size: int, offs: np.ndarray, kidx: np.ndarray) -> np.ndarray:
     del stream
     put_aads(a, offs, kidx)
     return a
-
-
-def put_aads(a, offs: np.ndarray, kidx: np.ndarray) -> None:
-    """Raw[0:4] of every slot = its peer's IP (numpy array, or a torch tensor on any device)."""
-    idx = offs.astype(np.int64)[:, None] + np.arange(4, dtype=np.int64)
-    if isinstance(a, np.ndarray):
-        a[idx] = aad_of_key(kidx)
-    else:
-        import torch
-
-        a[torch.from_numpy(idx).to(a.device)] = torch.from_numpy(aad_of_key(kidx)).to(a.device)
-
-
-def tail_index(offs: np.ndarray, lens: np.ndarray) -> np.ndarray:
-    """(n, 28) byte indices of every slot's tag || nonce."""
-    return (offs.astype(np.int64) + 4 + lens.astype(np.int64))[:, None] + np.arange(28, dtype=np.int64)

@@ -57,3 +57,22 @@ def test_bench_config4_two_ranks_one_device():
     assert line["status_ok"] is True and line["scaling"] == "strong"
     assert line["config"]["packets_total"] == 64 << 20 and line["config"]["packets_per_gpu"] == 32 << 20
     assert line["config"]["workload"].startswith("config4")
+
+
+def test_bench_gpus_flag_spawns_ranks():
+    """`python bench.py --gpus 2` with no launcher around it starts the two ranks itself (here both on
+    cuda:0 over gloo) and reports n_gpus 2 -- the flag can no longer silently measure one GPU."""
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["OMP_NUM_THREADS"] = "1"
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+           "--packets", "65536", "--settle-ms", "0", "--dist-backend", "gloo", "--one-device"]
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["status_ok"] is True and line["config"]["packets_per_gpu"] == 65536

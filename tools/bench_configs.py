@@ -32,94 +32,36 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 from quantum_amd import _lib, batch  # noqa: E402
-from quantum_amd.crypto import Context, derive_key, derive_keys, x25519, x25519_base  # noqa: E402
+from quantum_amd.crypto import Context, derive_key  # noqa: E402
 
 
 def config3(reps: int = 5) -> dict:
-    N, NK = 1 << 20, 1024
-    rng = np.random.default_rng(0x5EED0003)
-    # per-peer keys: secret = X25519(peer.pub, my.priv), salt = X25519(peer.pubsalt, my.privsalt)
-    t0 = time.perf_counter()
-    me_priv, me_salt = rng.bytes(32), rng.bytes(32)
-    secrets, salts = bytearray(), bytearray()
-    for _ in range(NK):
-        secrets += x25519(me_priv, x25519_base(rng.bytes(32)))
-        salts += x25519(me_salt, x25519_base(rng.bytes(32)))
-    keys = derive_keys(bytes(secrets), bytes(salts))
-    t_keys = time.perf_counter() - t0
-    ctx = Context(device=0, max_keys=NK)
-    t0 = time.perf_counter()
-    ctx.set_keys(0, keys)
-    t_set = time.perf_counter() - t0
+    """Config 3 on the parity-checked workload (quantum_amd/workloads.py), as bench.py's extra_configs."""
+    import bench
 
-    lens = rng.integers(64, 9001, size=N, dtype=np.int64)
-    kidx = rng.integers(0, NK, size=N, dtype=np.int64)
-    slot = (4 + lens + 28 + 3) & ~3
-    offs = np.zeros(N, dtype=np.int64)
-    offs[1:] = np.cumsum(slot)[:-1]
-    total = int(offs[-1] + slot[-1])
-    arena = torch.randint(0, 256, (total + 64,), dtype=torch.uint8, device="cuda")
-    nonces = torch.randint(0, 256, (12 * N,), dtype=torch.uint8, device="cuda")
-    status = torch.zeros(N, dtype=torch.uint8, device="cuda")
-    d_seal = batch.make_descs(offs, lens, kidx, "cuda")
-    d_open = batch.make_descs(offs, lens + 28, kidx, "cuda")
-    for _ in range(2):
-        batch.seal_batch(ctx, arena, d_seal, N, nonces, status=status)
-        batch.open_batch(ctx, arena, d_open, N, status=status)
-    torch.cuda.synchronize()
-    ok = int(status.sum()) == N
-    ts, to = [], []
-    for _ in range(reps):
-        e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
-        e[0].record()
-        batch.seal_batch(ctx, arena, d_seal, N, nonces, status=status)
-        e[1].record()
-        batch.open_batch(ctx, arena, d_open, N, status=status)
-        e[2].record()
-        torch.cuda.synchronize()
-        ts.append(e[0].elapsed_time(e[1]))
-        to.append(e[1].elapsed_time(e[2]))
-    ok = ok and int(status.sum()) == N
-    seal_ms, open_ms = float(np.median(ts)), float(np.median(to))
-    payload = int(lens.sum())
-    ctx.close()
-    return {"config": "config3", "packets": N, "keys": NK, "payload_bytes": payload,
-            "value": round(2 * payload / ((seal_ms + open_ms) * 1e-3) / 2**30, 2), "unit": "GiB/s",
-            "seal_ms": round(seal_ms, 3), "open_ms": round(open_ms, 3), "status_ok": ok,
-            "key_setup_s": {"x25519_pbkdf2_host": round(t_keys, 3), "device_expand": round(t_set, 4)}}
+    return dict(bench.extra_config3(reps=reps, verify=False), config="config3")
 
 
 def e2e(reps: int = 3, pinned: bool = True) -> dict:
     """Config 2 from host memory through qgcm_seal_host/qgcm_open_host (pipelined chunks)."""
+    if pinned:
+        import bench
+
+        return dict(bench.extra_e2e(derive_key(b"AES256Key-32Characters1234567890", bytes(range(32))), reps),
+                    config="e2e_config2_host_memory", host_memory="pinned")
     N, L = 1 << 20, 1350
     stride = batch.slot_stride(L, align=64)
     ctx = Context(device=0, max_keys=4)
-    key = derive_key(b"AES256Key-32Characters1234567890", bytes(range(32)))
-    ctx.set_key(0, key)
+    ctx.set_key(0, derive_key(b"AES256Key-32Characters1234567890", bytes(range(32))))
     L_ = _lib.lib()
     dev = torch.zeros(N * stride, dtype=torch.uint8, device="cuda")
     non_d = torch.zeros(12 * N, dtype=torch.uint8, device="cuda")
     batch.fill_uniform(dev, stride, N, L, 0x0100630a, 0x5EED0001, non_d, 0x5EED0002)
-    keep = []
-    if pinned:
-        a_ptr, n_ptr = L_.qgcm_host_alloc(N * stride), L_.qgcm_host_alloc(12 * N)
-        host = np.frombuffer((C.c_uint8 * (N * stride)).from_address(a_ptr), np.uint8)
-        nonces = np.frombuffer((C.c_uint8 * (12 * N)).from_address(n_ptr), np.uint8)
-        host[:] = dev.cpu().numpy()
-        nonces[:] = non_d.cpu().numpy()
-    else:
-        host = bytearray(dev.cpu().numpy().tobytes())
-        nonces = bytearray(non_d.cpu().numpy().tobytes())
-        a_ptr, ka = batch.host_ptr(host)
-        n_ptr, kn = batch.host_ptr(nonces)
-        keep = [ka, kn]
-    # correctness: the host pipeline seals exactly what the device path seals
-    ref = dev.clone()
-    batch.seal_uniform(ctx, ref, stride, N, L, 0, non_d)
-    rc = L_.qgcm_seal_host(ctx.handle, a_ptr, stride, N, L, 0, n_ptr, 4, None)
-    same = bytes(memoryview(host)) == ref.cpu().numpy().tobytes()
-    del ref
-    rc |= L_.qgcm_open_host(ctx.handle, a_ptr, stride, N, L + 28, 0, 4, None)
+    host = bytearray(dev.cpu().numpy().tobytes())
+    nonces = bytearray(non_d.cpu().numpy().tobytes())
+    a_ptr, ka = batch.host_ptr(host)
+    n_ptr, kn = batch.host_ptr(nonces)
+    rc = 0
     ts, to = [], []
     for _ in range(reps):
         t0 = time.perf_counter()
@@ -130,71 +72,18 @@ def e2e(reps: int = 3, pinned: bool = True) -> dict:
         ts.append(t1 - t0)
         to.append(t2 - t1)
     s, o = float(np.median(ts)), float(np.median(to))
-    del host, nonces, keep
-    if pinned:
-        L_.qgcm_host_free(a_ptr)
-        L_.qgcm_host_free(n_ptr)
+    del ka, kn
     ctx.close()
-    return {"config": "e2e_config2_host_memory", "host_memory": "pinned" if pinned else "pageable",
-            "packets": N, "payload_len": L, "stride": stride,
+    return {"config": "e2e_config2_host_memory", "host_memory": "pageable", "packets": N, "payload_len": L,
             "value": round(2 * N * L / (s + o) / 2**30, 2), "unit": "GiB/s", "seal_s": round(s, 4),
-            "open_s": round(o, 4), "bytes_each_way_per_call": N * stride,
-            "pcie_GBps_each_way": round(N * stride / ((s + o) / 2) / 1e9, 2),
-            "matches_device_path": same, "status_ok": rc == 0}
+            "open_s": round(o, 4), "status_ok": rc == 0}
 
 
 def config5(reps: int = 3, threads: int = 16) -> dict:
-    N, L, stride = 1 << 20, 1350, 1472  # stride = common.MaxPacketLength (the Payload.Raw buffer)
-    ctx = Context(device=0, max_keys=4)
-    key = derive_key(b"AES256Key-32Characters1234567890", bytes(range(32)))
-    ctx.set_key(0, key)
-    L_ = _lib.lib()
-    a_ptr, n_ptr = L_.qgcm_host_alloc(N * stride), L_.qgcm_host_alloc(12 * N)
-    host = np.frombuffer((C.c_uint8 * (N * stride)).from_address(a_ptr), np.uint8).reshape(N, stride)
-    nonces = np.frombuffer((C.c_uint8 * (12 * N)).from_address(n_ptr), np.uint8)
-    rng = np.random.default_rng(0x5EED0005)
-    host[:, :4] = np.frombuffer(bytes([10, 99, 0, 1]), np.uint8)
-    half = L // 2
-    host[:, 4:4 + half] = rng.integers(0, 256, (N, half), dtype=np.uint8)
-    line = np.frombuffer(b"GET /quantum/v1/peers HTTP/1.1\r\nHost: 10.99.0.1\r\n", np.uint8)
-    host[:, 4 + half:4 + L] = np.tile(line, (L - half) // len(line) + 1)[:L - half]
-    nonces[:] = rng.integers(0, 256, 12 * N, dtype=np.uint8)
-    plain = host[:, :4 + L].copy()
-    lens = np.full(N, L, np.uint32)
-    # codec alone on the host (the same workers), for the bottleneck breakdown
-    tmp = host.copy()
-    tl = np.full(N, L, np.uint32)
-    c0 = time.perf_counter()
-    L_.qgcm_snappy_compress_slots(tmp.ctypes.data, stride, N, tl.ctypes.data, threads)
-    c1 = time.perf_counter()
-    ratio = float(tl.sum()) / (N * L)
-    L_.qgcm_snappy_uncompress_slots(tmp.ctypes.data, stride, N, tl.ctypes.data, None, threads)
-    c2 = time.perf_counter()
-    codec_ok = bool(np.array_equal(tmp[:, :4 + L], plain))
-    del tmp
-    ts, to, bad = [], [], 0
-    for _ in range(reps):
-        lens[:] = L
-        t0 = time.perf_counter()
-        bad += batch.compress_seal_host(ctx, a_ptr, stride, N, lens, 0, n_ptr, threads=threads)
-        t1 = time.perf_counter()
-        sealed = int(lens.sum())
-        bad += batch.open_uncompress_host(ctx, a_ptr, stride, N, lens, 0, threads=threads)
-        t3 = time.perf_counter()
-        ts.append(t1 - t0)
-        to.append(t3 - t1)
-    restored = bool(np.array_equal(host[:, :4 + L], plain)) and bool((lens == L).all())
-    s, o = float(np.median(ts)), float(np.median(to))
-    del host, nonces, plain
-    L_.qgcm_host_free(a_ptr)
-    L_.qgcm_host_free(n_ptr)
-    ctx.close()
-    return {"config": "config5_snappy_then_gcm_host", "packets": N, "payload_len": L, "stride": stride,
-            "threads": threads, "compressed_over_plain": round(ratio, 4), "sealed_bytes": sealed,
-            "value": round(2 * N * L / (s + o) / 2**30, 2), "unit": "GiB/s (of uncompressed payload)",
-            "compress_seal_s": round(s, 4), "open_uncompress_s": round(o, 4),
-            "host_codec_only_s": {"compress": round(c1 - c0, 4), "uncompress": round(c2 - c1, 4)},
-            "status_ok": bad == 0, "restored": restored, "codec_roundtrip_ok": codec_ok}
+    import bench
+
+    return dict(bench.extra_config5(derive_key(b"AES256Key-32Characters1234567890", bytes(range(32))), threads,
+                                    reps), config="config5_snappy_then_gcm_host")
 
 
 def config4_shard(reps: int = 5, world: int = 8, rank: int = 0) -> dict:

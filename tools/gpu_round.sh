@@ -1,0 +1,42 @@
+#!/bin/bash
+# One GPU-box session: GPU tests, smoke, bench (with extra configs), an in-process A/B against a
+# reference build, and the config-2 profile (trace + PMC).  Every GPU step has its own time limit;
+# the script stops at the first step that faults, aborts or times out (a plain test failure goes on).
+# Usage: bash tools/gpu_round.sh <tag> [steps...]   steps: tests smoke bench ab prof prof3 (default: all)
+set -u
+TAG=$1; shift
+STEPS=${*:-"tests smoke bench ab prof"}
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+export TMPDIR=/tmp
+check() {  # name rc
+  echo "$1 rc=$2" | tee -a $OUT/steps.txt
+  if [ "$2" -ge 124 ]; then echo "stopping after $1 (rc $2)" | tee -a $OUT/steps.txt; exit "$2"; fi
+}
+for s in $STEPS; do
+  case $s in
+    tests)
+      timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/gpu_tests.txt 2>&1
+      check tests $? ;;
+    smoke)
+      timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
+      check smoke $? ;;
+    bench)
+      timeout -k 10 600 python3 bench.py > $OUT/bench_line.json 2> $OUT/bench.err
+      check bench $? ;;
+    ab)
+      timeout -k 10 300 python3 tools/ab_libs.py ablib/libqgcm_r2.so quantum_amd/libqgcm.so --rounds 15 > $OUT/ab.txt 2>&1
+      check ab $? ;;
+    prof)
+      bash tools/profile.sh $TAG > $OUT/profile.log 2>&1
+      check prof $?
+      mkdir -p profiles/$TAG
+      python3 tools/trace_summary.py gpurun_out/prof_$TAG > $OUT/kernel_stats_summary.txt 2>&1
+      python3 tools/pmc_traffic.py gpurun_out/prof_$TAG 1048576 1350 1408 524288 > $OUT/traffic_print.txt 2>&1
+      cp gpurun_out/prof_$TAG/traffic.json $OUT/ 2>/dev/null ;;
+    prof3)
+      bash tools/profile_config3.sh $TAG > $OUT/profile3.log 2>&1
+      check prof3 $? ;;
+  esac
+done
+echo all done | tee -a $OUT/steps.txt

@@ -3,7 +3,7 @@
 # run, never combined with other trace domains).  Usage: bash tools/profile.sh <tag> [bench args]
 set -u
 TAG=${1:-r1}; shift || true
-ARGS=${*:-"--no-cpu-baseline --steps 100"}  # 100 timed steps after 10 warmup (tools/trace_summary.py default)
+ARGS=${*:-"--no-cpu-baseline --no-extra --steps 100"}  # 100 timed steps after 10 warmup (tools/trace_summary.py default)
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
