@@ -1090,81 +1090,96 @@ __device__ __forceinline__ void block_mask(uint32_t r, uint32_t &m0, uint32_t &m
     m3 = q == 3 ? lowmask(sb) : 0u;
 }
 
-// One workgroup per packet.  Uniform form (b.descs == NULL): slot i at b.arena + i * b.stride,
-// b.uniform_len = L (seal) or L + 28 (open), b.uniform_key.  Descriptor form (the coalescer's small
-// batches): packet blockIdx.x is b.descs[blockIdx.x] in b.arena.  Slots are 16-B aligned and
-// (4 + len (+ 28 for seal) + 15) & ~15 bytes long, at most kOneCap - 16; seal nonces come from
-// b.nonces (12 B per packet) when it is set, else from the slot.  b.status[packet] = verdict.
-template <bool kSeal>
-__global__ void __launch_bounds__(kOneThreads) gcm_one_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
-    const uint32_t tid = threadIdx.x;
-    const uint32_t lane = tid & 63u;
-    const uint32_t pkt = blockIdx.x;
-    uint64_t off = (uint64_t)pkt * b.stride;  // uniform form: slot pkt of the batch
-    uint32_t Lin = b.uniform_len, key = b.uniform_key;
-    if (b.descs) {
-        const qgcm_desc dsc = b.descs[pkt];
-        off = dsc.offset;
-        Lin = dsc.len;
-        key = dsc.key_idx;
+// Slot access of the latency engine.  kSys = false: plain 16-B loads and stores (the slot is device
+// memory, or pinned host memory handed over at a kernel launch).  kSys = true (the resident kernel,
+// whose slots in pinned host memory are rewritten by the host while the kernel runs): every access
+// is a relaxed system-scope 8-B atomic (global_load/store sc0 sc1: around the GPU caches, so no
+// cache invalidation or write-back of the XCD's L2 -- which a bulk kernel may be filling -- is needed).
+template <bool kSys>
+__device__ __forceinline__ uint4 slot_ld16(const uint8_t *slot, uint32_t i) {
+    if constexpr (kSys) {
+        const uint64_t *p = reinterpret_cast<const uint64_t *>(slot) + 2 * i;
+        const uint64_t a = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const uint64_t c = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return uint4{(uint32_t)a, (uint32_t)(a >> 32), (uint32_t)c, (uint32_t)(c >> 32)};
     }
-    const uint32_t n16 = (uint32_t)((4ull + Lin + (kSeal ? QGCM_OVERHEAD : 0) + 15) >> 4);
-    // as the batch kernels: a key index out of range or an open shorter than 28 B fails the packet
-    // (slot untouched); so does a slot past the LDS staging area or misaligned (the host never sends one)
-    if (key >= b.max_keys || !b.key_valid[key] || (!kSeal && Lin < (uint32_t)QGCM_OVERHEAD) || Lin >= kOneCap ||
-        n16 * 16u > kOneCap - 16u || (off & 15u)) {
-        if (tid == 0) {
-            if (b.status) b.status[pkt] = 0;
-            if (b.done) {  // the host waits on every packet's flag
-                __threadfence_system();
-                *reinterpret_cast<volatile uint8_t *>(b.done + (b.descs ? pkt : 0u)) = 1;
-            }
-        }
+    return reinterpret_cast<const uint4 *>(slot)[i];
+}
+template <bool kSys>
+__device__ __forceinline__ void slot_st16(uint8_t *slot, uint32_t i, uint4 v) {
+    if constexpr (kSys) {
+        uint64_t *p = reinterpret_cast<uint64_t *>(slot) + 2 * i;
+        __hip_atomic_store(p, (uint64_t)v.x | (uint64_t)v.y << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(p + 1, (uint64_t)v.z | (uint64_t)v.w << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         return;
     }
-    const uint32_t L = kSeal ? Lin : Lin - QGCM_OVERHEAD;
-    const uint32_t A = kOneBuf + 12u, P = kOneBuf + 16u;  // slot base (AAD), payload base
-    uint8_t *slot = b.arena + off;
-    const uint4 *gslot = reinterpret_cast<const uint4 *>(slot);
-    // 1. stage the slot: every load issued before the table fill, so the PCIe round trip overlaps it
-    uint4 v[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const uint32_t i = tid + k * kOneThreads;
-        if (i < n16) v[k] = gslot[i];
-    }
-    // The table fills load everything first and store after (one memory latency, not one per
-    // iteration): Te0/Te1 words for 32 replicas per row, then the comb tables of H^(2^l) -- only the
-    // ones this packet's GHASH reads (H and H^2 always, the Estrin levels up to
-    // bit-length(min(d, 63)), H^64 once a lane owns two blocks).
-    constexpr int kTeIt = kTeBytes / 16 / kOneThreads;       // 16
-    constexpr int kGhIt = kOneTabs * 512 / kOneThreads;      // 14
-    const uint4 *gh = b.gh_table + (size_t)key * kGhEntries;
-    const uint32_t dd = (L + 15u) >> 4;
-    const uint32_t dtop = dd < 63u ? dd : 63u;
-    const uint32_t ntabs = dd >= 64u ? kOneTabs : (dtop > 3u ? 32u - __builtin_clz(dtop) : 2u);
+    reinterpret_cast<uint4 *>(slot)[i] = v;
+}
+
+// Fills the replicated T-tables (64 KiB at LDS 0): loads first, stores after (one memory latency).
+__device__ __forceinline__ void one_fill_te(const uint32_t *te, uint32_t tid) {
+    constexpr int kTeIt = kTeBytes / 16 / kOneThreads;  // 16
     uint32_t tv[kTeIt];
-    uint4 gv[kGhIt];
 #pragma unroll
     for (int k = 0; k < kTeIt; ++k) {
         const uint32_t i = tid + k * kOneThreads;
-        tv[k] = b.te[((i >> 3) & 1u) * 256u + (i >> 4)];
-    }
-#pragma unroll
-    for (int k = 0; k < kGhIt; ++k) {
-        const uint32_t i = tid + k * kOneThreads, l = i >> 9;
-        const uint32_t src = l == 0 ? kGhH : l == 1 ? kGhH2 : l == 2 ? kGhH4 : kGhH8 + (l - 3) * 512u;
-        if (l < ntabs) gv[k] = gh[src + (i & 511u)];
+        tv[k] = te[((i >> 3) & 1u) * 256u + (i >> 4)];
     }
 #pragma unroll
     for (int k = 0; k < kTeIt; ++k) {
         const uint32_t i = tid + k * kOneThreads;
         lds_st128(16 * i, uint4{tv[k], tv[k], tv[k], tv[k]});
     }
+}
+
+// One packet on one 256-thread workgroup, tables already in LDS except (fill_te) the T-tables and the
+// comb tables of H^(2^l) that this packet needs beyond what `tab_key` / `tab_n` say is loaded (both
+// workgroup-uniform, updated here).  The slot (16-B aligned, (4 + Lin (+ 28 for seal) + 15) & ~15
+// bytes, checked by the caller) is staged in LDS, sealed or opened there and written back whole.
+// nonce: seal only, 12 B, or NULL for the nonce already in the slot.  Returns the verdict (1 ok, 0
+// authentication failure), the same on every thread.  Ends with a workgroup barrier.
+template <bool kSeal, bool kSys>
+__device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_table, uint8_t *slot, uint32_t Lin,
+                               uint32_t key, uint32_t aad_len, const uint8_t *nonce, bool fill_te, uint32_t &tab_key,
+                               uint32_t &tab_n) {
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63u;
+    const uint32_t n16 = (uint32_t)((4ull + Lin + (kSeal ? QGCM_OVERHEAD : 0) + 15) >> 4);
+    const uint32_t L = kSeal ? Lin : Lin - QGCM_OVERHEAD;
+    const uint32_t A = kOneBuf + 12u, P = kOneBuf + 16u;  // slot base (AAD), payload base
+    // 1. stage the slot: every load issued before the table fill, so the PCIe round trip overlaps it
+    uint4 v[4];
 #pragma unroll
-    for (int k = 0; k < kGhIt; ++k) {
-        const uint32_t i = tid + k * kOneThreads, l = i >> 9;
-        if (l < ntabs) lds_st_comb(kTeBytes + l * kGhBytes, i & 511u, gv[k]);
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t i = tid + k * kOneThreads;
+        if (i < n16) v[k] = slot_ld16<kSys>(slot, i);
+    }
+    // The table fills load everything first and store after (one memory latency, not one per
+    // iteration): Te0/Te1 words for 32 replicas per row, then the comb tables of H^(2^l) -- only the
+    // ones this packet's GHASH reads (H and H^2 always, the Estrin levels up to
+    // bit-length(min(d, 63)), H^64 once a lane owns two blocks) and not loaded yet for this key.
+    constexpr int kGhIt = kOneTabs * 512 / kOneThreads;  // 14
+    const uint4 *gh = b.gh_table + (size_t)key * kGhEntries;
+    const uint32_t dd = (L + 15u) >> 4;
+    const uint32_t dtop = dd < 63u ? dd : 63u;
+    const uint32_t ntabs = dd >= 64u ? kOneTabs : (dtop > 3u ? 32u - __builtin_clz(dtop) : 2u);
+    const uint32_t t0 = key == tab_key ? tab_n : 0u;  // tables [0, t0) already hold this key's
+    if (fill_te) one_fill_te(b.te, tid);
+    if (ntabs > t0) {
+        uint4 gv[kGhIt];
+#pragma unroll
+        for (int k = 0; k < kGhIt; ++k) {
+            const uint32_t i = tid + k * kOneThreads, l = i >> 9;
+            const uint32_t src = l == 0 ? kGhH : l == 1 ? kGhH2 : l == 2 ? kGhH4 : kGhH8 + (l - 3) * 512u;
+            if (l >= t0 && l < ntabs) gv[k] = gh[src + (i & 511u)];
+        }
+#pragma unroll
+        for (int k = 0; k < kGhIt; ++k) {
+            const uint32_t i = tid + k * kOneThreads, l = i >> 9;
+            if (l >= t0 && l < ntabs) lds_st_comb(kTeBytes + l * kGhBytes, i & 511u, gv[k]);
+        }
+        tab_key = key;
+        tab_n = ntabs;
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -1178,7 +1193,7 @@ __global__ void __launch_bounds__(kOneThreads) gcm_one_kernel(Batch b, const uin
         }
     }
     for (uint32_t i = tid + 4 * kOneThreads; i < n16; i += kOneThreads) {  // slots over 16 KiB
-        const uint4 w = gslot[i];
+        const uint4 w = slot_ld16<kSys>(slot, i);
         const uint32_t a = A + 16 * i;
         lds_st32(a, w.x);
         lds_st32(a + 4, w.y);
@@ -1192,8 +1207,8 @@ __global__ void __launch_bounds__(kOneThreads) gcm_one_kernel(Batch b, const uin
     const uint32_t nfull = L >> 4, r = L & 15u;
     const uint32_t d = nfull + (r ? 1u : 0u);
     uint32_t n0, n1, n2;
-    if (kSeal && b.nonces) {  // the nonce goes into the slot with the tag
-        const uint32_t *np = reinterpret_cast<const uint32_t *>(b.nonces + 12ull * pkt);
+    if (kSeal && nonce) {  // the nonce goes into the slot with the tag
+        const uint32_t *np = reinterpret_cast<const uint32_t *>(nonce);
         n0 = np[0];
         n1 = np[1];
         n2 = np[2];
@@ -1235,8 +1250,8 @@ __global__ void __launch_bounds__(kOneThreads) gcm_one_kernel(Batch b, const uin
         if (tid < 64) {
             const uint32_t m = lane;
             uint32_t z0 = 0, z1 = 0, z2 = 0, z3 = 0;
-            const bool aad_lane = m == (d & 63u) && b.aad_len;
-            if (aad_lane) z0 = lds32(A) & (b.aad_len >= 4 ? 0xffffffffu : lowmask(b.aad_len));
+            const bool aad_lane = m == (d & 63u) && aad_len;
+            if (aad_lane) z0 = lds32(A) & (aad_len >= 4 ? 0xffffffffu : lowmask(aad_len));
             // blocks bi = d-1-m-64k >= 0, in increasing order: exponent d+1-bi = m+2 (mod 64) at the end
             const uint32_t first = (d - 1u - m) & 63u;
             for (uint32_t bi = first; bi < d && m < d; bi += 64) {
@@ -1269,7 +1284,7 @@ __global__ void __launch_bounds__(kOneThreads) gcm_one_kernel(Batch b, const uin
             // Y = S H^2 (lane 0) + [len(A)]_64 || [len(C)]_64 H (lane 1), in one multiply step
             if (m == 1) {
                 z0 = 0;
-                z1 = bswap(b.aad_len * 8u);
+                z1 = bswap(aad_len * 8u);
                 z2 = 0;
                 z3 = bswap(L * 8u);
             }
@@ -1282,6 +1297,7 @@ __global__ void __launch_bounds__(kOneThreads) gcm_one_kernel(Batch b, const uin
         }
     };
 
+    uint32_t ok = 1;
     if (kSeal) {
         ctr_pass(0);
         __syncthreads();
@@ -1293,20 +1309,19 @@ __global__ void __launch_bounds__(kOneThreads) gcm_one_kernel(Batch b, const uin
             lds_st32u(P + L + 4, e.y ^ y.y);
             lds_st32u(P + L + 8, e.z ^ y.z);
             lds_st32u(P + L + 12, e.w ^ y.w);
-            if (b.nonces) {
+            if (nonce) {
                 lds_st32u(P + L + 16, n0);
                 lds_st32u(P + L + 20, n1);
                 lds_st32u(P + L + 24, n2);
             }
-            if (b.status) b.status[pkt] = 1;
         }
     } else {
         ghash();
         ctr_pass(2);  // E_K(J0) on wave 1 while wave 0 hashes
         __syncthreads();
         const uint4 e = lds128(kOneScratch), y = lds128(kOneScratch + 16);
-        const bool ok = ((e.x ^ y.x ^ lds32u(P + L)) | (e.y ^ y.y ^ lds32u(P + L + 4)) |
-                         (e.z ^ y.z ^ lds32u(P + L + 8)) | (e.w ^ y.w ^ lds32u(P + L + 12))) == 0;
+        ok = ((e.x ^ y.x ^ lds32u(P + L)) | (e.y ^ y.y ^ lds32u(P + L + 4)) | (e.z ^ y.z ^ lds32u(P + L + 8)) |
+              (e.w ^ y.w ^ lds32u(P + L + 12))) == 0;
         if (ok) {
             ctr_pass(1);
         } else {  // Go 1.9 crypto/cipher gcm Open: zero the would-be plaintext on tag mismatch
@@ -1316,15 +1331,52 @@ __global__ void __launch_bounds__(kOneThreads) gcm_one_kernel(Batch b, const uin
                 lds_st128(P + 16 * j, z);
             }
         }
-        if (tid == 0 && b.status) b.status[pkt] = ok ? 1 : 0;
     }
     __syncthreads();
     // 4. write the slot back (the bytes outside the payload/tag are rewritten unchanged)
-    uint4 *oslot = reinterpret_cast<uint4 *>(slot);
     for (uint32_t i = tid; i < n16; i += kOneThreads) {
         const uint32_t a = A + 16 * i;
-        oslot[i] = uint4{lds32(a), lds32(a + 4), lds32(a + 8), lds32(a + 12)};
+        slot_st16<kSys>(slot, i, uint4{lds32(a), lds32(a + 4), lds32(a + 8), lds32(a + 12)});
     }
+    return ok;
+}
+
+// One workgroup per packet.  Uniform form (b.descs == NULL): slot i at b.arena + i * b.stride,
+// b.uniform_len = L (seal) or L + 28 (open), b.uniform_key.  Descriptor form (the coalescer's small
+// batches): packet blockIdx.x is b.descs[blockIdx.x] in b.arena.  Slots are 16-B aligned and
+// (4 + len (+ 28 for seal) + 15) & ~15 bytes long, at most kOneCap - 16; seal nonces come from
+// b.nonces (12 B per packet) when it is set, else from the slot.  b.status[packet] = verdict.
+template <bool kSeal>
+__global__ void __launch_bounds__(kOneThreads) gcm_one_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
+    const uint32_t tid = threadIdx.x;
+    const uint32_t pkt = blockIdx.x;
+    uint64_t off = (uint64_t)pkt * b.stride;  // uniform form: slot pkt of the batch
+    uint32_t Lin = b.uniform_len, key = b.uniform_key;
+    if (b.descs) {
+        const qgcm_desc dsc = b.descs[pkt];
+        off = dsc.offset;
+        Lin = dsc.len;
+        key = dsc.key_idx;
+    }
+    const uint32_t n16 = (uint32_t)((4ull + Lin + (kSeal ? QGCM_OVERHEAD : 0) + 15) >> 4);
+    // as the batch kernels: a key index out of range or an open shorter than 28 B fails the packet
+    // (slot untouched); so does a slot past the LDS staging area or misaligned (the host never sends one)
+    if (key >= b.max_keys || !b.key_valid[key] || (!kSeal && Lin < (uint32_t)QGCM_OVERHEAD) || Lin >= kOneCap ||
+        n16 * 16u > kOneCap - 16u || (off & 15u)) {
+        if (tid == 0) {
+            if (b.status) b.status[pkt] = 0;
+            if (b.done) {  // the host waits on every packet's flag
+                __threadfence_system();
+                *reinterpret_cast<volatile uint8_t *>(b.done + (b.descs ? pkt : 0u)) = 1;
+            }
+        }
+        return;
+    }
+    uint32_t tab_key = 0xffffffffu, tab_n = 0;
+    const uint32_t ok = one_packet<kSeal, false>(b, rk_table, b.arena + off, Lin, key, b.aad_len,
+                                                 kSeal && b.nonces ? b.nonces + 12ull * pkt : nullptr, true, tab_key,
+                                                 tab_n);
+    if (tid == 0 && b.status) b.status[pkt] = ok;
     if (b.done) {  // completion flag: every thread's stores reach the system before thread 0 sets it
         __threadfence_system();
         __syncthreads();
