@@ -124,6 +124,18 @@ long qgcm_seal_one(qgcm_ctx *ctx, uint32_t key_idx, uint8_t *data, long length, 
 long qgcm_open_one(qgcm_ctx *ctx, uint32_t key_idx, uint8_t *data, long len, const uint8_t *aad,
                    uint32_t aad_len);
 
+/* Per-packet calls are served by a RESIDENT kernel (16 workgroups by default, QGCM_RESIDENT_WORKERS;
+ * 16 request slots each, QGCM_RESIDENT_SLOTS) that polls pinned host memory, so a call costs no
+ * launch; payloads past ~16 KiB and QGCM_RESIDENT=0 take a gcm_one_kernel launch per call instead.
+ * The kernel is started by the first call and ends by itself after QGCM_RESIDENT_IDLE_US (2000) without
+ * a request or QGCM_RESIDENT_LIFE_US (8000) of life, after serving what is pending (the next call starts
+ * it again): work queued behind it on a shared hardware queue, or a device-wide synchronize, waits that
+ * long at most.  qgcm_set_key(s) and qgcm_destroy end it too (it caches key tables).
+ * qgcm_resident_stop ends it now; qgcm_resident_stats writes {requests served, instances launched,
+ * request slots, workers running now} (min(n, 4) values, returns that number or -1). */
+int qgcm_resident_stop(qgcm_ctx *ctx);
+int qgcm_resident_stats(const qgcm_ctx *ctx, uint64_t *out, int n);
+
 /* ---- host batches (end-to-end incl. PCIe) ---- */
 /* Slots in host memory at i*stride; copies in, runs the device batch, copies back, synchronously.
  * Pipelined in ~32 MiB chunks over 3 streams (H2D of chunk c+1 || kernel c || D2H of chunk c-1);
@@ -268,7 +280,8 @@ int qgcm_tun_close(int fd);
 #define QGCM_KERNEL_SEGMENTED 1 /* gcm_seg_kernel, descriptor batches (long key runs) */
 #define QGCM_KERNEL_PER_WAVE 2  /* gcm_quad_kernel, descriptor batches (short key runs) */
 #define QGCM_KERNEL_ONE 3       /* gcm_one_kernel, one workgroup per packet */
-#define QGCM_KERNEL_COUNTERS 4
+#define QGCM_KERNEL_RESIDENT 4  /* per-packet calls served by the resident kernel (requests, not launches) */
+#define QGCM_KERNEL_COUNTERS 5
 int qgcm_launch_counts(const qgcm_ctx *ctx, uint64_t *out, int n);
 
 /* ---- measurement: achievable HBM copy rate (reads + writes bytes) for the roofline ---- */

@@ -30,7 +30,7 @@ EXPORTS = (
     "qgcm_tun_open", "qgcm_tun_up", "qgcm_tun_read_slots", "qgcm_tun_write_slots", "qgcm_tun_close",
     "qgcm_group_create", "qgcm_group_destroy", "qgcm_group_size", "qgcm_group_ctx", "qgcm_group_shard",
     "qgcm_group_set_keys", "qgcm_group_seal_host", "qgcm_group_open_host", "qgcm_group_member_cpus",
-    "qgcm_group_last_zerocopy", "qgcm_launch_counts",
+    "qgcm_group_last_zerocopy", "qgcm_launch_counts", "qgcm_resident_stop", "qgcm_resident_stats",
 )
 
 QGCM_OK = 0
@@ -97,6 +97,9 @@ def _bind(L: C.CDLL) -> None:
     L.qgcm_stream_copy.argtypes = [vp, vp, vp, u64, vp]
     if hasattr(L, "qgcm_launch_counts"):
         L.qgcm_launch_counts.argtypes = [vp, vp, i32]
+    if hasattr(L, "qgcm_resident_stop"):
+        L.qgcm_resident_stop.argtypes = [vp]
+        L.qgcm_resident_stats.argtypes = [vp, vp, i32]
     sz = C.c_size_t
     L.qgcm_snappy_max_compressed_length.argtypes = [sz]
     L.qgcm_snappy_max_compressed_length.restype = sz

@@ -61,9 +61,18 @@ class Context:
 
     def launch_counts(self) -> dict:
         """Kernel launches that served this context's calls so far (qgcm_launch_counts)."""
+        out = (C.c_uint64 * 5)()
+        _lib.check(_lib.lib().qgcm_launch_counts(self.handle, out, 5), "qgcm_launch_counts")
+        return dict(zip(("quad", "segmented", "per_wave", "one", "resident"), (int(x) for x in out)))
+
+    def resident_stats(self) -> dict:
+        """The resident per-packet kernel: requests served, instances launched, slots, workers running."""
         out = (C.c_uint64 * 4)()
-        _lib.check(_lib.lib().qgcm_launch_counts(self.handle, out, 4), "qgcm_launch_counts")
-        return dict(zip(("quad", "segmented", "per_wave", "one"), (int(x) for x in out)))
+        _lib.check(_lib.lib().qgcm_resident_stats(self.handle, out, 4), "qgcm_resident_stats")
+        return dict(zip(("served", "launches", "slots", "running"), (int(x) for x in out)))
+
+    def resident_stop(self) -> None:
+        _lib.check(_lib.lib().qgcm_resident_stop(self.handle), "qgcm_resident_stop")
 
     def alloc_slot(self) -> int:
         with self._mu:

@@ -85,6 +85,39 @@ hipError_t launch_packets(bool seal, int variant, const Batch &b, int grid, hipS
 // a multiple of 16, at most kOneCap - 16) is staged in LDS; b.n must be 1.
 constexpr uint32_t kOneCap = 32768;
 hipError_t launch_one(bool seal, const Batch &b, hipStream_t s);
+
+// Resident per-packet service (resident.cpp): `workers` 256-thread workgroups of gcm_one_kernel's
+// engine stay on the GPU and serve requests the host posts into pinned (coherent) host memory, so a
+// per-packet call costs no launch.  Worker w owns request slots [w * per_worker, (w+1) * per_worker).
+// Host -> device: the slot bytes, meta[s] = {op (1 seal, 0 open), len, key_idx, aad_len}, then
+// seq[s] (31-bit, increments per request), then bell[16 w] += 1 (bell[16 w + 1] = stop).  Device ->
+// host: the slot bytes, then done[s] = seq << 1 | verdict.  Every host-memory access of the kernel is
+// a relaxed system-scope atomic (no cache maintenance).  An instance ends on the host's stop word, or
+// when worker 0 sees no request for idle_ticks or the instance is life_ticks old (100 MHz clock): it
+// raises ctl[1], every worker serves what is pending and leaves, and the last one writes *over = gen.
+constexpr uint32_t kResSlotBytes = 16384;  // request slot: [aad 4][payload][tag 16][nonce 12], 16-B rounded
+constexpr uint32_t kResMaxPerWorker = 64;
+struct ResArgs {
+    uint32_t *bell;         // host: [16 * workers] words, worker w's bell at 16 w, stop at 16 w + 1
+    const uint32_t *seq;    // host: [S]
+    const uint4 *meta;      // host: [S]
+    uint32_t *done;         // host: [S]
+    uint32_t *over;         // host: generation of the last instance that ended
+    uint8_t *data;          // host: [S][kResSlotBytes]
+    uint64_t *ctl;          // device, zeroed per launch: [0] last activity (clock), [1] shutdown, [2] exited
+    uint32_t workers, per_worker, gen, pad;
+    uint64_t idle_ticks, life_ticks;
+};
+hipError_t launch_resident(const Batch &b, const ResArgs &a, hipStream_t s);
+struct Resident;
+Resident *resident_create(int device, const Batch &base, int num_cus);  // nullptr: not available
+void resident_destroy(Resident *r);
+int resident_quiesce(Resident *r);
+int resident_workers_running(const Resident *r);
+void resident_stats(const Resident *r, uint64_t out[4]);  // served, launches, slots, workers running
+constexpr long kResNotServed = -1000;  // resident_call: the request does not fit; take the launch path
+long resident_call(Resident *r, bool seal, uint32_t key, uint8_t *data, long len, const uint8_t *aad,
+                   uint32_t aad_len, const uint8_t *nonce);
 // Small descriptor batches through the latency kernel, one workgroup per packet, straight on the
 // caller's (pinned host or device) arena/descriptors/nonces/status -- the coalescer's flush path.
 constexpr uint32_t kOneBatchMax = 2048;

@@ -1134,10 +1134,11 @@ __device__ __forceinline__ void one_fill_te(const uint32_t *te, uint32_t tid) {
 
 // One packet on one 256-thread workgroup, tables already in LDS except (fill_te) the T-tables and the
 // comb tables of H^(2^l) that this packet needs beyond what `tab_key` / `tab_n` say is loaded (both
-// workgroup-uniform, updated here).  The slot (16-B aligned, (4 + Lin (+ 28 for seal) + 15) & ~15
+// workgroup-uniform, updated here; a caller serving several packets puts a workgroup barrier
+// between two calls).  The slot (16-B aligned, (4 + Lin (+ 28 for seal) + 15) & ~15
 // bytes, checked by the caller) is staged in LDS, sealed or opened there and written back whole.
 // nonce: seal only, 12 B, or NULL for the nonce already in the slot.  Returns the verdict (1 ok, 0
-// authentication failure), the same on every thread.  Ends with a workgroup barrier.
+// authentication failure), the same on every thread.
 template <bool kSeal, bool kSys>
 __device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_table, uint8_t *slot, uint32_t Lin,
                                uint32_t key, uint32_t aad_len, const uint8_t *nonce, bool fill_te, uint32_t &tab_key,
@@ -1387,6 +1388,130 @@ __global__ void __launch_bounds__(kOneThreads) gcm_one_kernel(Batch b, const uin
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Resident per-packet service (resident.cpp; gcm_internal.h ResArgs has the protocol): each
+// workgroup keeps gcm_one_kernel's T-tables in LDS for its whole life (and the comb tables of the key
+// it served last), thread 0 polls its worker's bell word in pinned host memory (one 8-B read per
+// poll, s_sleep between polls), and on a change wave 0 scans the worker's request slots, then the
+// whole workgroup serves every pending slot in place in host memory with the latency engine.
+constexpr uint32_t kResCtl = (kOneLds + 15u) & ~15u;  // LDS: [0] command, [8,16) pending mask, [16,36) request
+constexpr uint32_t kResDone = kResCtl + 64;           // the done sequence of each of this worker's slots
+constexpr uint32_t kResLds = kResDone + 4 * kResMaxPerWorker;
+static_assert(kResLds <= 160u * 1024u, "gfx950 LDS is 160 KiB per workgroup");
+
+__device__ __forceinline__ uint32_t ld_sys32(const uint32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint64_t ld_sys64(const uint64_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ void __launch_bounds__(kOneThreads) gcm_resident_kernel(Batch b, const uint32_t *__restrict__ rk_table,
+                                                                   ResArgs a) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, w = blockIdx.x;
+    const uint32_t P = a.per_worker, first = w * P;
+    one_fill_te(b.te, tid);
+    if (tid < P) lds_st32(kResDone + 4 * tid, ld_sys32(a.done + first + tid) >> 1);
+    uint32_t tab_key = 0xffffffffu, tab_n = 0;
+    const uint64_t t_start = wall_clock64();
+    uint32_t last_bell = 0;
+    bool scanned = false;
+    __syncthreads();
+    for (;;) {
+        // 0: idle, 1: scan and serve, 2: serve what is pending, then leave
+        if (tid == 0) {
+            uint32_t cmd = 0;
+            const uint64_t hb = ld_sys64(reinterpret_cast<const uint64_t *>(a.bell + 16u * w));
+            const uint32_t bell = (uint32_t)hb, stop = (uint32_t)(hb >> 32);
+            if (stop || __hip_atomic_load(a.ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                cmd = 2;
+            } else if (!scanned || bell != last_bell) {
+                cmd = 1;
+                last_bell = bell;  // read before the scan: a request posted after it rings again
+                scanned = true;
+            } else if (w == 0) {  // the instance's end: no request for idle_ticks, or life_ticks old
+                const uint64_t now = wall_clock64();
+                uint64_t act = __hip_atomic_load(a.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                act = act > t_start ? act : t_start;
+                if (now - act > a.idle_ticks || now - t_start > a.life_ticks)
+                    __hip_atomic_store(a.ctl + 1, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            lds_st32(kResCtl, cmd);
+            if (cmd == 0) __builtin_amdgcn_s_sleep(8);
+        }
+        __syncthreads();
+        const uint32_t cmd = lds32(kResCtl);
+        if (cmd == 0) {
+            __syncthreads();  // every thread has read the command before thread 0 writes the next
+            continue;
+        }
+        if (tid < 64) {  // wave 0: which of this worker's slots hold a request not served yet
+            bool pend = false;
+            if (lane < P) pend = (ld_sys32(a.seq + first + lane) & 0x7fffffffu) != lds32(kResDone + 4 * lane);
+            const uint64_t m = __ballot(pend);
+            if (lane == 0) {
+                lds_st32(kResCtl + 8, (uint32_t)m);
+                lds_st32(kResCtl + 12, (uint32_t)(m >> 32));
+            }
+        }
+        __syncthreads();
+        uint64_t mask = lds32(kResCtl + 8) | (uint64_t)lds32(kResCtl + 12) << 32;
+        while (mask) {
+            const uint32_t j = (uint32_t)__builtin_ctzll(mask);
+            mask &= mask - 1;
+            const uint32_t sl = first + j;
+            if (tid == 0) {  // the sequence first, then the meta the host wrote before it
+                const uint32_t q = ld_sys32(a.seq + sl) & 0x7fffffffu;
+                const uint64_t *mp = reinterpret_cast<const uint64_t *>(a.meta + sl);
+                const uint64_t m0 = ld_sys64(mp), m1 = ld_sys64(mp + 1);
+                lds_st32(kResCtl + 16, q);
+                lds_st32(kResCtl + 20, (uint32_t)m0);
+                lds_st32(kResCtl + 24, (uint32_t)(m0 >> 32));
+                lds_st32(kResCtl + 28, (uint32_t)m1);
+                lds_st32(kResCtl + 32, (uint32_t)(m1 >> 32));
+            }
+            __syncthreads();
+            const uint32_t q = lds32(kResCtl + 16), op = lds32(kResCtl + 20), Lin = lds32(kResCtl + 24);
+            const uint32_t key = lds32(kResCtl + 28), aad = lds32(kResCtl + 32);
+            // as gcm_one_kernel: an unset or out-of-range key, an open shorter than the tag or a slot
+            // past its staging area fails the request with the slot untouched
+            const uint64_t stage = (4ull + Lin + (op ? QGCM_OVERHEAD : 0) + 15) & ~15ull;
+            const bool valid = op <= 1u && aad <= 4u && key < b.max_keys && b.key_valid[key] &&
+                               (op ? Lin < QGCM_MAX_PAYLOAD : Lin >= (uint32_t)QGCM_OVERHEAD) &&
+                               stage <= kResSlotBytes && stage <= kOneCap - 16;
+            uint32_t ok = 0;
+            uint8_t *slot = a.data + (size_t)sl * kResSlotBytes;
+            if (valid)
+                ok = op ? one_packet<true, true>(b, rk_table, slot, Lin, key, aad, nullptr, false, tab_key, tab_n)
+                        : one_packet<false, true>(b, rk_table, slot, Lin, key, aad, nullptr, false, tab_key, tab_n);
+            // every storing wave drains its (write-through) stores, then one lane publishes the verdict
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (tid == 0) {
+                __hip_atomic_store(a.done + sl, q << 1 | ok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                lds_st32(kResDone + 4 * j, q);
+                __hip_atomic_fetch_max(a.ctl, wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        __syncthreads();
+        if (cmd == 2) break;
+    }
+    if (tid == 0) {
+        const uint64_t n = __hip_atomic_fetch_add(a.ctl + 2, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (n + 1 == a.workers) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(a.over, a.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
+hipError_t launch_resident(const Batch &b, const ResArgs &a, hipStream_t s) {
+    if (a.workers == 0 || a.per_worker == 0 || a.per_worker > kResMaxPerWorker) return hipErrorInvalidValue;
+    void *args[] = {const_cast<Batch *>(&b), const_cast<uint32_t **>(&b.rk_table), const_cast<ResArgs *>(&a)};
+    return hipLaunchKernel(reinterpret_cast<const void *>(&gcm_resident_kernel), dim3(a.workers), dim3(kOneThreads),
+                           args, kResLds, s);
+}
+
 hipError_t launch_one(bool seal, const Batch &b, hipStream_t s) {
     if (b.n == 0 || ((uintptr_t)b.arena & 15)) return hipErrorInvalidValue;
     if (!b.descs) {  // uniform: slots that hold the 16-B-rounded staging area and fit it in LDS
@@ -1442,12 +1567,14 @@ hipError_t init_kernels() {
         }
     }
     for (const void *k : {reinterpret_cast<const void *>(&gcm_one_kernel<true>),
-                          reinterpret_cast<const void *>(&gcm_one_kernel<false>)}) {
+                          reinterpret_cast<const void *>(&gcm_one_kernel<false>),
+                          reinterpret_cast<const void *>(&gcm_resident_kernel)}) {
         hipFuncAttributes a;
         hipError_t e = hipFuncGetAttributes(&a, k);
         if (e != hipSuccess) return e;
         if (a.sharedSizeBytes != 0) return hipErrorInvalidKernelFile;
-        e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kOneLds);
+        e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                k == reinterpret_cast<const void *>(&gcm_resident_kernel) ? kResLds : kOneLds);
         if (e != hipSuccess) return e;
     }
     return hipSuccess;

@@ -95,6 +95,12 @@ struct qgcm_ctx {
 
     std::atomic<uint64_t> launches[QGCM_KERNEL_COUNTERS] = {};  // qgcm_launch_counts
     void count(int k, uint64_t v = 1) { launches[k].fetch_add(v, std::memory_order_relaxed); }
+
+    // resident per-packet service (resident.cpp), created on the first per-packet call
+    bool res_on = true;  // QGCM_RESIDENT=0: every per-packet call launches gcm_one_kernel
+    std::atomic<qgcm::Resident *> res{nullptr};
+    std::atomic<bool> res_failed{false};
+    std::mutex res_mu;
 };
 
 namespace {
@@ -144,13 +150,15 @@ void set_err(char *err, int errlen, const char *msg) {
 int hip_fail(hipError_t e) { return e == hipSuccess ? QGCM_OK : QGCM_E_HIP; }
 
 int grid_for(const qgcm_ctx *ctx, uint32_t n_items, int variant) {
+    // CUs held by a running resident per-packet kernel (one workgroup each) are left to it
+    const int cus = std::max(1, ctx->num_cus - resident_workers_running(ctx->res.load(std::memory_order_acquire)));
     const uint32_t waves = (uint32_t)variant_waves(variant);
     const uint32_t tiles = (n_items + 15) / 16;  // 16-packet wave tiles
     const uint32_t wgs = (tiles + waves - 1) / waves;
     // persistent grid: the resident workgroups (each fills its own LDS tables once)
     const uint32_t per_cu = ctx->wgs_per_cu_override > 0 ? (uint32_t)ctx->wgs_per_cu_override
                                                          : (uint32_t)variant_wgs_per_cu(variant);
-    const uint32_t cap = (uint32_t)ctx->num_cus * per_cu;
+    const uint32_t cap = (uint32_t)cus * per_cu;
     return (int)(wgs < cap ? (wgs ? wgs : 1) : cap);
 }
 
@@ -200,6 +208,20 @@ int run_one(qgcm_ctx *ctx, bool seal, uint8_t *slot, uint64_t stride, uint32_t l
     }
     const int rc = run_uniform(ctx, seal, slot, stride, 1, len, key_idx, nullptr, aad_len, status, s);
     return rc == QGCM_OK ? hip_fail(hipStreamSynchronize(s)) : rc;
+}
+
+// The context's resident per-packet service, created on first use (nullptr: off or unavailable).
+Resident *get_resident(qgcm_ctx *ctx) {
+    Resident *r = ctx->res.load(std::memory_order_acquire);
+    if (r || !ctx->res_on || ctx->res_failed.load(std::memory_order_relaxed)) return r;
+    std::lock_guard<std::mutex> g(ctx->res_mu);
+    r = ctx->res.load(std::memory_order_acquire);
+    if (!r) {
+        r = resident_create(ctx->device, base_batch(ctx), ctx->num_cus);
+        if (!r) ctx->res_failed = true;
+        ctx->res.store(r, std::memory_order_release);
+    }
+    return r;
 }
 
 bool key_ok(qgcm_ctx *ctx, uint32_t k) {
@@ -492,6 +514,7 @@ qgcm_ctx *qgcm_create(int device, uint32_t max_keys, char *err, int errlen) {
     }
     if (const char *v = getenv("QGCM_WGS_PER_CU")) ctx->wgs_per_cu_override = atoi(v);
     if (const char *v = getenv("QGCM_ONE_KERNEL")) ctx->one_kernel = atoi(v) != 0;
+    if (const char *v = getenv("QGCM_RESIDENT")) ctx->res_on = atoi(v) != 0;
     if (const char *v = getenv("QGCM_ONE_UNIFORM_MAX")) ctx->one_uniform_max = (uint32_t)std::max(0, atoi(v));
     if (const char *v = getenv("QGCM_LAUNCH_CHUNK"))  // rounded down to whole 64-packet tiles
         ctx->launch_chunk = (uint32_t)std::max(0, atoi(v)) & ~63u;
@@ -528,6 +551,7 @@ qgcm_ctx *qgcm_create(int device, uint32_t max_keys, char *err, int errlen) {
 
 void qgcm_destroy(qgcm_ctx *ctx) {
     if (!ctx) return;
+    resident_destroy(ctx->res.exchange(nullptr));  // before the device-wide synchronize below
     hipSetDevice(ctx->device);
     hipDeviceSynchronize();
     hipFree(ctx->d_rk);
@@ -575,6 +599,9 @@ int qgcm_set_keys(qgcm_ctx *ctx, uint32_t first_idx, uint32_t count, const uint8
         std::lock_guard<std::mutex> g(ctx->key_mu);
         for (uint32_t i = 0; i < count; ++i) ctx->key_set[first_idx + i] = 1;
     }
+    // a running resident instance may hold the old key tables (and key-valid bytes) in its caches:
+    // end it; the next per-packet call starts a fresh one
+    if (rc == QGCM_OK && resident_quiesce(ctx->res.load(std::memory_order_acquire)) != QGCM_OK) rc = QGCM_E_HIP;
     return rc;
 }
 
@@ -623,6 +650,13 @@ long qgcm_seal_one(qgcm_ctx *ctx, uint32_t key_idx, uint8_t *data, long length, 
         return -1;
     }
     if (hipSetDevice(ctx->device) != hipSuccess) return -1;
+    if (Resident *r = get_resident(ctx)) {  // no launch per call
+        const long rc = resident_call(r, true, key_idx, data, length, aad, aad_len, nb);
+        if (rc != kResNotServed) {
+            ctx->count(QGCM_KERNEL_RESIDENT);
+            return rc;
+        }
+    }
     const uint64_t stride = ((uint64_t)length + 4 + QGCM_OVERHEAD + 15) & ~15ull;
     std::unique_lock<std::mutex> lk;
     qgcm_ctx::OneSlot *sl = acquire_one(ctx, stride + 16, lk);
@@ -648,6 +682,13 @@ long qgcm_open_one(qgcm_ctx *ctx, uint32_t key_idx, uint8_t *data, long len, con
     if (len < QGCM_OVERHEAD) return -1;  // crypto/aes.go:58-60: errOpen (the reference panics below 12)
     if (!key_ok(ctx, key_idx)) return -1;
     if (hipSetDevice(ctx->device) != hipSuccess) return -1;
+    if (Resident *r = get_resident(ctx)) {  // no launch per call
+        const long rc = resident_call(r, false, key_idx, data, len, aad, aad_len, nullptr);
+        if (rc != kResNotServed) {
+            ctx->count(QGCM_KERNEL_RESIDENT);
+            return rc;
+        }
+    }
     const uint64_t stride = ((uint64_t)len + 4 + 15) & ~15ull;
     std::unique_lock<std::mutex> lk;
     qgcm_ctx::OneSlot *sl = acquire_one(ctx, stride + 16, lk);
@@ -1011,6 +1052,20 @@ int qgcm_fill_uniform(uint8_t *d_arena, uint64_t stride, uint32_t n, uint32_t le
     if ((n && !d_arena) || (n && stride < (uint64_t)len + 4)) return QGCM_E_ARG;
     return hip_fail(launch_fill_uniform(d_arena, stride, n, len, aad_word, seed_payload, d_nonces, seed_nonce,
                                         (hipStream_t)stream));
+}
+
+int qgcm_resident_stop(qgcm_ctx *ctx) {
+    if (!ctx) return QGCM_E_ARG;
+    return resident_quiesce(ctx->res.load(std::memory_order_acquire));
+}
+
+int qgcm_resident_stats(const qgcm_ctx *ctx, uint64_t *out, int n) {
+    if (!ctx || n < 0 || (n && !out)) return -1;
+    uint64_t v[4];
+    resident_stats(ctx->res.load(std::memory_order_acquire), v);
+    const int m = n < 4 ? n : 4;
+    for (int i = 0; i < m; ++i) out[i] = v[i];
+    return m;
 }
 
 int qgcm_launch_counts(const qgcm_ctx *ctx, uint64_t *out, int n) {

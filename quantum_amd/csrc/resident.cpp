@@ -1,0 +1,272 @@
+// resident.cpp -- the per-packet Encrypt/Decrypt contract (crypto/aes.go:41-62, one packet per
+// plugin/encryption.go Apply from each of quantum's 2 x NumWorkers goroutines, worker/outgoing.go:83-93,
+// worker/incoming.go:82-92) without a kernel launch per call.
+//
+// A resident kernel (gcm_kernels.hip gcm_resident_kernel) keeps `workers` workgroups on the GPU; each
+// owns `per_worker` request slots in one pinned, coherent host region.  A call copies its packet into
+// a free slot of the least-loaded worker, writes the request's meta and sequence number, rings the
+// worker's bell and spins on the slot's done word; the worker seals or opens the slot in place over
+// PCIe and publishes the verdict.  No hipLaunch, no stream and no hardware queue per call.
+//
+// Lifetime: an instance ends by itself when it has seen no request for QGCM_RESIDENT_IDLE_US or is
+// QGCM_RESIDENT_LIFE_US old (so work queued behind it on a shared hardware queue, or a
+// device-wide synchronize, waits a bounded time), and on qgcm_resident_stop / qgcm_set_keys (the
+// workers cache key tables) / qgcm_destroy.  Before leaving, every worker serves what is pending; a
+// request posted after that is seen by its caller (the instance's `over` word names its generation)
+// and the caller launches the next instance, which serves it.  At most one instance runs at a time.
+#include <hip/hip_runtime.h>
+#include <sched.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/random.h>
+
+#include <atomic>
+#include <chrono>
+#include <memory>
+#include <mutex>
+
+#include "gcm_internal.h"
+
+namespace qgcm {
+
+struct Resident {
+    int device = 0;
+    Batch base{};
+    uint32_t W = 16, P = 16, S = 256;
+    uint64_t idle_ticks = 200000, life_ticks = 800000;  // 100 MHz: 2 ms, 8 ms
+    uint8_t *host = nullptr;  // pinned coherent region (below)
+    uint32_t *bell = nullptr, *seq = nullptr, *done = nullptr, *over = nullptr;
+    uint4 *meta = nullptr;
+    uint8_t *data = nullptr;
+    uint64_t *d_ctl = nullptr;
+    hipStream_t stream = nullptr;
+    std::unique_ptr<uint32_t[]> seqh;                  // last sequence per slot (owned by the slot holder)
+    std::unique_ptr<std::atomic<uint32_t>[]> busy;     // slot taken
+    std::unique_ptr<std::atomic<int32_t>[]> inflight;  // requests per worker
+    std::atomic<uint32_t> rr{0};
+    std::mutex launch_mu;
+    std::atomic<uint32_t> gen{0};  // generation of the current (or last) instance; 0 = never launched
+    std::atomic<bool> broken{false};
+    std::atomic<uint64_t> served{0}, launches{0};
+};
+
+namespace {
+
+uint64_t env_u64(const char *name, uint64_t dflt) {
+    const char *v = getenv(name);
+    return v && *v ? strtoull(v, nullptr, 10) : dflt;
+}
+
+// Launches instance g + 1 if instance g (0: none yet) has ended and nobody has launched since.
+int relaunch(Resident *r, uint32_t g) {
+    std::lock_guard<std::mutex> lk(r->launch_mu);
+    if (r->gen.load(std::memory_order_acquire) != g) return QGCM_OK;  // another caller did it
+    if (hipSetDevice(r->device) != hipSuccess) return QGCM_E_HIP;
+    // instance g has written `over` (its last worker is leaving): wait for the launch to retire
+    if (g != 0 && hipStreamSynchronize(r->stream) != hipSuccess) {
+        r->broken = true;
+        return QGCM_E_HIP;
+    }
+    ResArgs a{};
+    a.bell = r->bell;
+    a.seq = r->seq;
+    a.meta = r->meta;
+    a.done = r->done;
+    a.over = r->over;
+    a.data = r->data;
+    a.ctl = r->d_ctl;
+    a.workers = r->W;
+    a.per_worker = r->P;
+    a.gen = g + 1;
+    a.idle_ticks = r->idle_ticks;
+    a.life_ticks = r->life_ticks;
+    if (hipMemsetAsync(r->d_ctl, 0, 4 * sizeof(uint64_t), r->stream) != hipSuccess ||
+        launch_resident(r->base, a, r->stream) != hipSuccess) {
+        r->broken = true;
+        return QGCM_E_HIP;
+    }
+    r->launches.fetch_add(1, std::memory_order_relaxed);
+    r->gen.store(g + 1, std::memory_order_release);
+    return QGCM_OK;
+}
+
+bool instance_over(const Resident *r, uint32_t g) {
+    return g == 0 || __atomic_load_n(r->over, __ATOMIC_ACQUIRE) == g;
+}
+
+}  // namespace
+
+Resident *resident_create(int device, const Batch &base, int num_cus) {
+    auto r = std::make_unique<Resident>();
+    r->device = device;
+    r->base = base;
+    r->W = (uint32_t)env_u64("QGCM_RESIDENT_WORKERS", 16);
+    r->P = (uint32_t)env_u64("QGCM_RESIDENT_SLOTS", 16);
+    if (r->W < 1 || (int)r->W > num_cus / 2 || r->P < 1 || r->P > kResMaxPerWorker) return nullptr;
+    r->S = r->W * r->P;
+    r->idle_ticks = env_u64("QGCM_RESIDENT_IDLE_US", 2000) * 100;  // s_memrealtime: 100 MHz
+    r->life_ticks = env_u64("QGCM_RESIDENT_LIFE_US", 8000) * 100;
+    // host region: bells (64 B per worker), seq, done, over, meta, then the slots (4 KiB aligned)
+    const size_t o_seq = 64ull * r->W, o_done = o_seq + 4ull * r->S, o_over = o_done + 4ull * r->S;
+    const size_t o_meta = (o_over + 64 + 15) & ~15ull, o_data = (o_meta + 16ull * r->S + 4095) & ~4095ull;
+    const size_t bytes = o_data + (size_t)kResSlotBytes * r->S;
+    if (hipSetDevice(device) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void **>(&r->host), bytes, hipHostMallocCoherent) != hipSuccess)
+        return nullptr;
+    memset(r->host, 0, o_data);
+    r->bell = reinterpret_cast<uint32_t *>(r->host);
+    r->seq = reinterpret_cast<uint32_t *>(r->host + o_seq);
+    r->done = reinterpret_cast<uint32_t *>(r->host + o_done);
+    r->over = reinterpret_cast<uint32_t *>(r->host + o_over);
+    r->meta = reinterpret_cast<uint4 *>(r->host + o_meta);
+    r->data = r->host + o_data;
+    r->seqh.reset(new uint32_t[r->S]());
+    r->busy.reset(new std::atomic<uint32_t>[r->S]);
+    for (uint32_t i = 0; i < r->S; ++i) r->busy[i] = 0;
+    r->inflight.reset(new std::atomic<int32_t>[r->W]);
+    for (uint32_t i = 0; i < r->W; ++i) r->inflight[i] = 0;
+    int lo = 0, hi = 0;
+    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) hi = 0;
+    if (hipMalloc(reinterpret_cast<void **>(&r->d_ctl), 4 * sizeof(uint64_t)) != hipSuccess ||
+        hipStreamCreateWithPriority(&r->stream, hipStreamNonBlocking, hi) != hipSuccess) {
+        resident_destroy(r.release());
+        return nullptr;
+    }
+    return r.release();
+}
+
+// Ends the running instance (if any) after it has served what is pending; the next call relaunches.
+int resident_quiesce(Resident *r) {
+    if (!r) return QGCM_OK;
+    std::lock_guard<std::mutex> lk(r->launch_mu);
+    const uint32_t g = r->gen.load(std::memory_order_acquire);
+    if (g == 0) return QGCM_OK;
+    for (uint32_t w = 0; w < r->W; ++w) __atomic_store_n(&r->bell[16 * w + 1], 1u, __ATOMIC_RELEASE);
+    const hipError_t e = hipSetDevice(r->device) == hipSuccess ? hipStreamSynchronize(r->stream) : hipErrorUnknown;
+    for (uint32_t w = 0; w < r->W; ++w) __atomic_store_n(&r->bell[16 * w + 1], 0u, __ATOMIC_RELEASE);
+    if (e != hipSuccess) {
+        r->broken = true;
+        return QGCM_E_HIP;
+    }
+    return QGCM_OK;
+}
+
+void resident_destroy(Resident *r) {
+    if (!r) return;
+    resident_quiesce(r);
+    hipSetDevice(r->device);
+    if (r->stream) hipStreamDestroy(r->stream);
+    if (r->d_ctl) hipFree(r->d_ctl);
+    if (r->host) hipHostFree(r->host);
+    delete r;
+}
+
+int resident_workers_running(const Resident *r) {
+    if (!r) return 0;
+    const uint32_t g = r->gen.load(std::memory_order_acquire);
+    return instance_over(r, g) ? 0 : (int)r->W;
+}
+
+void resident_stats(const Resident *r, uint64_t out[4]) {
+    out[0] = r ? r->served.load() : 0;
+    out[1] = r ? r->launches.load() : 0;
+    out[2] = r ? r->W * (uint64_t)r->P : 0;
+    out[3] = (uint64_t)resident_workers_running(r);
+}
+
+long resident_call(Resident *r, bool seal, uint32_t key, uint8_t *data, long len, const uint8_t *aad,
+                   uint32_t aad_len, const uint8_t *nonce) {
+    const uint64_t stage = (4ull + (uint64_t)len + (seal ? QGCM_OVERHEAD : 0) + 15) & ~15ull;
+    if (!r || r->broken || stage > kResSlotBytes || stage > kOneCap - 16) return kResNotServed;
+    uint8_t nb[12];
+    if (seal) {
+        if (nonce)
+            memcpy(nb, nonce, 12);
+        else if (getrandom(nb, 12, 0) != 12)  // crypto/aes.go:44 rand.Read(nonce)
+            return -1;
+    }
+    // a free slot of the least-loaded worker (starting round-robin, so ties spread)
+    uint32_t s = 0, w = 0;
+    for (uint32_t tries = 0;; ++tries) {
+        const uint32_t start = r->rr.fetch_add(1, std::memory_order_relaxed) % r->W;
+        w = start;
+        int32_t best = r->inflight[start].load(std::memory_order_relaxed);
+        for (uint32_t i = 1; i < r->W && best > 0; ++i) {
+            const uint32_t c = (start + i) % r->W;
+            const int32_t f = r->inflight[c].load(std::memory_order_relaxed);
+            if (f < best) {
+                best = f;
+                w = c;
+            }
+        }
+        bool got = false;
+        for (uint32_t k = 0; k < r->W && !got; ++k) {
+            const uint32_t ww = (w + k) % r->W;
+            for (uint32_t i = 0; i < r->P; ++i) {
+                const uint32_t c = ww * r->P + (i + tries) % r->P;
+                uint32_t z = 0;
+                if (r->busy[c].load(std::memory_order_relaxed) == 0 &&
+                    r->busy[c].compare_exchange_strong(z, 1, std::memory_order_acquire)) {
+                    s = c;
+                    w = ww;
+                    got = true;
+                    break;
+                }
+            }
+        }
+        if (got) break;
+        sched_yield();  // every slot in flight
+    }
+    r->inflight[w].fetch_add(1, std::memory_order_relaxed);
+    uint8_t *slot = r->data + (size_t)s * kResSlotBytes;
+    uint32_t hdr = 0;
+    if (aad_len) memcpy(&hdr, aad, aad_len);
+    memcpy(slot, &hdr, 4);
+    memcpy(slot + 4, data, (size_t)len);
+    if (seal) memcpy(slot + 4 + len + 16, nb, 12);
+    r->meta[s] = uint4{seal ? 1u : 0u, (uint32_t)len, key, aad_len};
+    uint32_t q = (r->seqh[s] + 1) & 0x7fffffffu;
+    if (q == 0) q = 1;
+    r->seqh[s] = q;
+    __atomic_store_n(&r->seq[s], q, __ATOMIC_RELEASE);
+    __atomic_fetch_add(&r->bell[16 * w], 1u, __ATOMIC_SEQ_CST);
+    long rc = 0;
+    uint32_t g = r->gen.load(std::memory_order_acquire);
+    if (instance_over(r, g) && relaunch(r, g) != QGCM_OK) return -1;  // broken: the slot stays taken
+    uint32_t v = 0;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t spins = 0;; ++spins) {
+        v = __atomic_load_n(&r->done[s], __ATOMIC_ACQUIRE);
+        if ((v >> 1) == q) break;
+        if ((spins & 63) == 63) {
+            g = r->gen.load(std::memory_order_acquire);
+            // the instance ended with this request still pending: launch the next one
+            if (instance_over(r, g) && relaunch(r, g) != QGCM_OK) return -1;  // broken: the slot stays taken
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
+                r->broken = true;  // never observed; the slot stays taken (the device may still serve it)
+                return -1;
+            }
+        }
+        if (spins < 4096)
+            __builtin_ia32_pause();
+        else
+            sched_yield();
+    }
+    r->served.fetch_add(1, std::memory_order_relaxed);
+    if (seal) {
+        rc = -1;
+        if (v & 1) {  // a rejected seal leaves the caller's buffer untouched
+            memcpy(data, slot + 4, (size_t)len + QGCM_OVERHEAD);
+            rc = len + QGCM_OVERHEAD;
+        }
+    } else {
+        memcpy(data, slot + 4, (size_t)len - QGCM_OVERHEAD);  // plaintext, or zeros on auth failure
+        rc = (v & 1) ? len - QGCM_OVERHEAD : -1;
+    }
+    r->inflight[w].fetch_sub(1, std::memory_order_relaxed);
+    r->busy[s].store(0, std::memory_order_release);
+    return rc;
+}
+
+}  // namespace qgcm

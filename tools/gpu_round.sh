@@ -2,7 +2,8 @@
 # One GPU-box session: GPU tests, smoke, bench (with extra configs), an in-process A/B against a
 # reference build, and the config-2 profile (trace + PMC).  Every GPU step has its own time limit;
 # the script stops at the first step that faults, aborts or times out (a plain test failure goes on).
-# Usage: bash tools/gpu_round.sh <tag> [steps...]   steps: tests smoke bench ab prof prof3 (default: all)
+# Usage: bash tools/gpu_round.sh <tag> [steps...]
+#   steps: rtests tests smoke bench ab prof pp prof3 (default: tests smoke bench ab prof)
 set -u
 TAG=$1; shift
 STEPS=${*:-"tests smoke bench ab prof"}
@@ -34,6 +35,18 @@ for s in $STEPS; do
       python3 tools/trace_summary.py gpurun_out/prof_$TAG > $OUT/kernel_stats_summary.txt 2>&1
       python3 tools/pmc_traffic.py gpurun_out/prof_$TAG 1048576 1350 1408 524288 > $OUT/traffic_print.txt 2>&1
       cp gpurun_out/prof_$TAG/traffic.json $OUT/ 2>/dev/null ;;
+    pp)
+      for t in 1 16 64 256; do
+        timeout -k 10 120 tools/bin/per_packet_bench $t 1350 2 0 >> $OUT/per_packet.jsonl 2>> $OUT/per_packet.err
+        check pp_$t $?
+      done
+      for t in 16 64; do
+        timeout -k 10 120 tools/bin/per_packet_bench $t 1350 2 1 >> $OUT/per_packet.jsonl 2>> $OUT/per_packet.err
+        check pp_bulk_$t $?
+      done ;;
+    rtests)
+      timeout -k 10 300 python3 -u -m pytest tests/test_gpu_resident.py -x -v --timeout 120 --timeout-method thread > $OUT/resident_tests.txt 2>&1
+      check rtests $? ;;
     prof3)
       bash tools/profile_config3.sh $TAG > $OUT/profile3.log 2>&1
       check prof3 $? ;;
