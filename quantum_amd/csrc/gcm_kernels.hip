@@ -1421,6 +1421,13 @@ __global__ void __launch_bounds__(kOneThreads) gcm_resident_kernel(Batch b, cons
         // 0: idle, 1: scan and serve, 2: serve what is pending, then leave
         if (tid == 0) {
             uint32_t cmd = 0;
+            if (w == 0) {  // the instance's end: no request for idle_ticks, or life_ticks old (busy or not)
+                const uint64_t now = wall_clock64();
+                uint64_t act = __hip_atomic_load(a.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                act = act > t_start ? act : t_start;
+                if (now - act > a.idle_ticks || now - t_start > a.life_ticks)
+                    __hip_atomic_store(a.ctl + 1, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
             const uint64_t hb = ld_sys64(reinterpret_cast<const uint64_t *>(a.bell + 16u * w));
             const uint32_t bell = (uint32_t)hb, stop = (uint32_t)(hb >> 32);
             if (stop || __hip_atomic_load(a.ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
@@ -1429,12 +1436,6 @@ __global__ void __launch_bounds__(kOneThreads) gcm_resident_kernel(Batch b, cons
                 cmd = 1;
                 last_bell = bell;  // read before the scan: a request posted after it rings again
                 scanned = true;
-            } else if (w == 0) {  // the instance's end: no request for idle_ticks, or life_ticks old
-                const uint64_t now = wall_clock64();
-                uint64_t act = __hip_atomic_load(a.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                act = act > t_start ? act : t_start;
-                if (now - act > a.idle_ticks || now - t_start > a.life_ticks)
-                    __hip_atomic_store(a.ctl + 1, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             lds_st32(kResCtl, cmd);
             if (cmd == 0) __builtin_amdgcn_s_sleep(8);
