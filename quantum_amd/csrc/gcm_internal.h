@@ -87,24 +87,33 @@ constexpr uint32_t kOneCap = 32768;
 hipError_t launch_one(bool seal, const Batch &b, hipStream_t s);
 
 // Resident per-packet service (resident.cpp): `workers` 256-thread workgroups of gcm_one_kernel's
-// engine stay on the GPU and serve requests the host posts into pinned (coherent) host memory, so a
-// per-packet call costs no launch.  Worker w owns request slots [w * per_worker, (w+1) * per_worker).
-// Host -> device: the slot bytes, meta[s] = {op (1 seal, 0 open), len, key_idx, aad_len}, then
-// seq[s] (31-bit, increments per request), then bell[16 w] += 1 (bell[16 w + 1] = stop).  Device ->
-// host: the slot bytes, then done[s] = seq << 1 | verdict.  Every host-memory access of the kernel is
-// a relaxed system-scope atomic (no cache maintenance).  An instance ends on the host's stop word, or
-// when worker 0 sees no request for idle_ticks or the instance is life_ticks old (100 MHz clock): it
-// raises ctl[1], every worker serves what is pending and leaves, and the last one writes *over = gen.
+// engine plus one dispatcher workgroup stay on the GPU and serve requests the host posts into pinned
+// (coherent) host memory, so a per-packet call costs no launch.  Slot s belongs to worker s / per_worker.
+// Host -> device: the slot bytes, meta[s] = {op (1 seal, 0 open), len, key_idx, aad_len}, then seq[s]
+// (31-bit, +1 per request), then bell[0] += 1 (bell[1] = stop).  The dispatcher (one wave) is the only
+// reader of host memory while idle: it polls bell[0] (one 8-B read per poll, s_sleep between polls) and
+// on a change reads every slot's seq, forwards each new request's meta and seq to device memory and
+// rings its worker's device bell; the worker (polling that bell in L2) serves the slot in place over
+// PCIe and writes done[s] = seq << 1 | verdict into host memory.  Every host-memory access of the kernel
+// is a relaxed system-scope atomic (no cache maintenance).  An instance ends on the host's stop word, or
+// when the dispatcher sees no request for idle_ticks or the instance is life_ticks old (100 MHz clock):
+// it forwards what is pending and raises the device shutdown word, every worker serves what it was given
+// and leaves, and the last workgroup to leave writes *over = gen.
 constexpr uint32_t kResSlotBytes = 16384;  // request slot: [aad 4][payload][tag 16][nonce 12], 16-B rounded
 constexpr uint32_t kResMaxPerWorker = 64;
+constexpr uint32_t kResMaxSlots = 256;     // the dispatcher wave scans 4 slots per lane
+// device control region (zeroed per launch): [0, 64) words (u64 [1] shutdown, [2] workgroups left),
+// then one 64-B line per worker bell, then assigned seq [S] (u32), then the forwarded meta [S] (uint4)
+constexpr uint32_t kResDevBell = 64;
+inline size_t res_dev_bytes(uint32_t workers, uint32_t slots) { return kResDevBell + 64ull * workers + 4ull * slots + 16ull * slots + 16; }
 struct ResArgs {
-    uint32_t *bell;         // host: [16 * workers] words, worker w's bell at 16 w, stop at 16 w + 1
+    uint32_t *bell;         // host: [0] bell, [1] stop
     const uint32_t *seq;    // host: [S]
     const uint4 *meta;      // host: [S]
     uint32_t *done;         // host: [S]
     uint32_t *over;         // host: generation of the last instance that ended
     uint8_t *data;          // host: [S][kResSlotBytes]
-    uint64_t *ctl;          // device, zeroed per launch: [0] last activity (clock), [1] shutdown, [2] exited
+    uint8_t *dev;           // device control region (res_dev_bytes), zeroed per launch
     uint32_t workers, per_worker, gen, pad;
     uint64_t idle_ticks, life_ticks;
 };

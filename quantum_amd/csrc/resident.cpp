@@ -2,11 +2,12 @@
 // plugin/encryption.go Apply from each of quantum's 2 x NumWorkers goroutines, worker/outgoing.go:83-93,
 // worker/incoming.go:82-92) without a kernel launch per call.
 //
-// A resident kernel (gcm_kernels.hip gcm_resident_kernel) keeps `workers` workgroups on the GPU; each
-// owns `per_worker` request slots in one pinned, coherent host region.  A call copies its packet into
-// a free slot of the least-loaded worker, writes the request's meta and sequence number, rings the
-// worker's bell and spins on the slot's done word; the worker seals or opens the slot in place over
-// PCIe and publishes the verdict.  No hipLaunch, no stream and no hardware queue per call.
+// A resident kernel (gcm_kernels.hip gcm_resident_kernel) keeps `workers` workgroups and a dispatcher
+// on the GPU; each worker owns `per_worker` request slots in one pinned, coherent host region.  A call
+// copies its packet into a free slot of the least-loaded worker, writes the request's meta and
+// sequence number, rings the bell and spins on the slot's done word; the dispatcher forwards the
+// request to the worker, which seals or opens the slot in place over PCIe and publishes the verdict.
+// No hipLaunch, no stream and no hardware queue per call.
 //
 // Lifetime: an instance ends by itself when it has seen no request for QGCM_RESIDENT_IDLE_US or is
 // QGCM_RESIDENT_LIFE_US old (so work queued behind it on a shared hardware queue, or a
@@ -39,7 +40,8 @@ struct Resident {
     uint32_t *bell = nullptr, *seq = nullptr, *done = nullptr, *over = nullptr;
     uint4 *meta = nullptr;
     uint8_t *data = nullptr;
-    uint64_t *d_ctl = nullptr;
+    uint8_t *d_ctl = nullptr;  // device control region (res_dev_bytes)
+    size_t ctl_bytes = 0;
     hipStream_t stream = nullptr;
     std::unique_ptr<uint32_t[]> seqh;                  // last sequence per slot (owned by the slot holder)
     std::unique_ptr<std::atomic<uint32_t>[]> busy;     // slot taken
@@ -75,13 +77,13 @@ int relaunch(Resident *r, uint32_t g) {
     a.done = r->done;
     a.over = r->over;
     a.data = r->data;
-    a.ctl = r->d_ctl;
+    a.dev = r->d_ctl;
     a.workers = r->W;
     a.per_worker = r->P;
     a.gen = g + 1;
     a.idle_ticks = r->idle_ticks;
     a.life_ticks = r->life_ticks;
-    if (hipMemsetAsync(r->d_ctl, 0, 4 * sizeof(uint64_t), r->stream) != hipSuccess ||
+    if (hipMemsetAsync(r->d_ctl, 0, r->ctl_bytes, r->stream) != hipSuccess ||
         launch_resident(r->base, a, r->stream) != hipSuccess) {
         r->broken = true;
         return QGCM_E_HIP;
@@ -103,12 +105,14 @@ Resident *resident_create(int device, const Batch &base, int num_cus) {
     r->base = base;
     r->W = (uint32_t)env_u64("QGCM_RESIDENT_WORKERS", 16);
     r->P = (uint32_t)env_u64("QGCM_RESIDENT_SLOTS", 16);
-    if (r->W < 1 || (int)r->W > num_cus / 2 || r->P < 1 || r->P > kResMaxPerWorker) return nullptr;
+    if (r->W < 1 || (int)r->W > num_cus / 2 || r->P < 1 || r->P > kResMaxPerWorker || r->W * r->P > kResMaxSlots)
+        return nullptr;
     r->S = r->W * r->P;
+    r->ctl_bytes = res_dev_bytes(r->W, r->S);
     r->idle_ticks = env_u64("QGCM_RESIDENT_IDLE_US", 2000) * 100;  // s_memrealtime: 100 MHz
     r->life_ticks = env_u64("QGCM_RESIDENT_LIFE_US", 8000) * 100;
-    // host region: bells (64 B per worker), seq, done, over, meta, then the slots (4 KiB aligned)
-    const size_t o_seq = 64ull * r->W, o_done = o_seq + 4ull * r->S, o_over = o_done + 4ull * r->S;
+    // host region: bell and stop (a 64-B line), seq, done, over, meta, then the slots (4 KiB aligned)
+    const size_t o_seq = 64, o_done = o_seq + 4ull * r->S, o_over = o_done + 4ull * r->S;
     const size_t o_meta = (o_over + 64 + 15) & ~15ull, o_data = (o_meta + 16ull * r->S + 4095) & ~4095ull;
     const size_t bytes = o_data + (size_t)kResSlotBytes * r->S;
     if (hipSetDevice(device) != hipSuccess ||
@@ -128,7 +132,7 @@ Resident *resident_create(int device, const Batch &base, int num_cus) {
     for (uint32_t i = 0; i < r->W; ++i) r->inflight[i] = 0;
     int lo = 0, hi = 0;
     if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) hi = 0;
-    if (hipMalloc(reinterpret_cast<void **>(&r->d_ctl), 4 * sizeof(uint64_t)) != hipSuccess ||
+    if (hipMalloc(reinterpret_cast<void **>(&r->d_ctl), r->ctl_bytes) != hipSuccess ||
         hipStreamCreateWithPriority(&r->stream, hipStreamNonBlocking, hi) != hipSuccess) {
         resident_destroy(r.release());
         return nullptr;
@@ -142,9 +146,9 @@ int resident_quiesce(Resident *r) {
     std::lock_guard<std::mutex> lk(r->launch_mu);
     const uint32_t g = r->gen.load(std::memory_order_acquire);
     if (g == 0) return QGCM_OK;
-    for (uint32_t w = 0; w < r->W; ++w) __atomic_store_n(&r->bell[16 * w + 1], 1u, __ATOMIC_RELEASE);
+    __atomic_store_n(&r->bell[1], 1u, __ATOMIC_RELEASE);
     const hipError_t e = hipSetDevice(r->device) == hipSuccess ? hipStreamSynchronize(r->stream) : hipErrorUnknown;
-    for (uint32_t w = 0; w < r->W; ++w) __atomic_store_n(&r->bell[16 * w + 1], 0u, __ATOMIC_RELEASE);
+    __atomic_store_n(&r->bell[1], 0u, __ATOMIC_RELEASE);
     if (e != hipSuccess) {
         r->broken = true;
         return QGCM_E_HIP;
@@ -230,7 +234,7 @@ long resident_call(Resident *r, bool seal, uint32_t key, uint8_t *data, long len
     if (q == 0) q = 1;
     r->seqh[s] = q;
     __atomic_store_n(&r->seq[s], q, __ATOMIC_RELEASE);
-    __atomic_fetch_add(&r->bell[16 * w], 1u, __ATOMIC_SEQ_CST);
+    __atomic_fetch_add(&r->bell[0], 1u, __ATOMIC_SEQ_CST);
     long rc = 0;
     uint32_t g = r->gen.load(std::memory_order_acquire);
     if (instance_over(r, g) && relaunch(r, g) != QGCM_OK) return -1;  // broken: the slot stays taken

@@ -245,7 +245,8 @@ def test_next_to_bulk_batch(torch):
         assert int(status.sum()) == n
         ref = head.cpu().numpy()
         h = ref.copy()
-        O.lib().oracle_seal_uniform(bkey, h.ctypes.data, stride, 4096, L, 4, nonces[:12 * 4096].cpu().numpy().ctypes.data)
+        nh = nonces[:12 * 4096].cpu().numpy()  # kept alive across the call (ctypes takes a raw address)
+        O.lib().oracle_seal_uniform(bkey, h.ctypes.data, stride, 4096, L, 4, nh.ctypes.data)
         batch.seal_uniform(ctx, head, stride, 4096, L, 63, nonces[:12 * 4096])
         assert np.array_equal(head.cpu().numpy(), h)
     finally:
