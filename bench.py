@@ -109,27 +109,44 @@ def host_cpus() -> dict:
 
 
 def cpu_baseline(key: bytes, L: int, threads: int, host: dict) -> dict:
-    """OpenSSL EVP AES-256-GCM with crypto/aes.go semantics (oracle/ossl_check.c), host cores: one
-    thread alone, then `threads` at once (the CPU share the GPU pool grants this job)."""
+    """BASELINE config 1 on the host cores: the reference's plugin chain over common.Payload
+    (Encryption + Mock, sorted; NewTunPayload -> Apply(Outgoing) -> NewSockPayload -> Apply(Incoming))
+    on 10 000 x L-byte payloads per thread -- this repo's C++ mirror of the Go plugin code over OpenSSL
+    EVP AES-256-GCM with crypto/aes.go semantics (oracle/cpu_chain.cpp) -- one thread alone, then
+    `threads` at once (the CPU share the GPU pool grants this job).  Also the bare AES-GCM loop
+    (oracle/ossl_check.c: one reused buffer, no plugin chain) for reference."""
+    import subprocess
+
     from oracle import oracle as O
 
-    # one thread for ~2 s, then the all-thread sample sized to ~1.5 s wall (~threads x 1.5 s of CPU work)
+    exe = os.path.join(ROOT, "oracle", "_build", "cpu_chain")
+
+    def chain(t: int, seconds: float) -> dict:
+        out = subprocess.run([exe, str(t), "10000", str(L), str(seconds)], capture_output=True, text=True, timeout=120)
+        if out.returncode != 0:
+            raise RuntimeError(f"cpu_chain failed: {out.stderr[-500:]}")
+        return json.loads(out.stdout.strip().splitlines()[-1])
+
+    one = chain(1, 3.0)
+    alln = chain(threads, 3.0)
+    # the bare AES-GCM loop (no plugin chain, one reused buffer), one thread, ~2 s
     n0 = 20000
     t0 = O.ossl_cpu_baseline(key, 1, n0, L)
     n1 = max(n0, int(n0 / t0 * 2.0))
-    t1 = O.ossl_cpu_baseline(key, 1, n1, L)
-    rate1 = 2 * n1 * L / t1 / 2**30
-    per_thread = max(20000, int(n1 / t1 * 1.5))
-    tN = O.ossl_cpu_baseline(key, threads, per_thread, L)
-    rateN = 2 * threads * per_thread * L / tN / 2**30
-    return {"value": round(rateN, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
-            "one_core": round(rate1, 3), "nproc": host["nproc"],
-            "all_nproc_linear_estimate": round(rate1 * host["nproc"], 1),
+    aes_only = 2 * n1 * L / O.ossl_cpu_baseline(key, 1, n1, L) / 2**30
+    return {"value": round(alln["GiB_s"], 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "one_core": round(one["GiB_s"], 3), "nproc": host["nproc"],
+            "aes_gcm_only_one_core": round(aes_only, 3),
+            "all_nproc_linear_extrapolation_not_measured": round(one["GiB_s"] * host["nproc"], 1),
+            "intact": bool(one["intact"] and alln["intact"]),
             "host": host,
-            "sample": (f"{threads} threads (this job's CPU share of a {host['nproc']}-CPU host) x {per_thread} "
-                       f"packets x {L} B seal+open, crypto/aes.go semantics (getrandom nonce/packet, in place, "
-                       f"4-B AAD) on OpenSSL EVP aes-256-gcm; 1 thread alone: {rate1:.3f} GiB/s over {n1} packets; "
-                       f"all_nproc_linear_estimate = one_core x nproc, not measured")}
+            "sample": (f"config 1: the plugin chain (Encryption + Mock over common.Payload, both directions) on "
+                       f"{threads} threads (this job's CPU share of a {host['nproc']}-CPU host) x 10000 payloads x "
+                       f"{L} B each, looped for 3 s ({alln['packets_per_s']:.0f} packets/s sealed and opened); "
+                       f"C++ mirror of the Go plugins (oracle/cpu_chain.cpp) over OpenSSL EVP aes-256-gcm with "
+                       f"crypto/aes.go semantics (getrandom nonce per packet, in place); one thread alone "
+                       f"{one['GiB_s']:.3f} GiB/s; the bare AES-GCM loop without the chain "
+                       f"{aes_only:.3f} GiB/s on one thread")}
 
 
 def stream_copy_gbs(ctx, nbytes: int, dev, stream, reps: int = 5) -> float:

@@ -100,23 +100,29 @@ class GPUContext {
     std::mutex mu_;
 };
 
-// crypto/aes.go:22-26, bound to a device key slot.
+// crypto/aes.go:22-26, bound to a device key slot.  Encrypt / Decrypt are virtual so that a test or
+// baseline harness can run the same plugin chain over another AES-GCM (oracle/cpu_chain.cpp: the
+// reference's CPU configuration with OpenSSL standing in for Go's crypto/cipher).
 class AES {
   public:
     AES(std::shared_ptr<GPUContext> g, uint32_t slot) : g_(std::move(g)), slot_(slot) {}
+    virtual ~AES() = default;
     int EncryptedSize(common::Slice data) const { return (int)data.len + Overhead + NonceSize; }  // :29-31
     int DecryptedSize(common::Slice data) const { return (int)data.len - Overhead - NonceSize; }  // :34-36
     // crypto/aes.go:41-52: seals data[0:length] in place with a fresh random nonce, appends tag and
     // nonce; data needs capacity length + 28.  additional may be empty (nil).
-    std::pair<int, Error> Encrypt(common::Slice data, int length, common::Slice additional) const;
+    virtual std::pair<int, Error> Encrypt(common::Slice data, int length, common::Slice additional) const;
     // crypto/aes.go:57-62: opens data in place (nonce = last 12 B, tag the 16 before), returns
     // len - 28; on authentication failure the plaintext region is zeroed (Go 1.9 gcm.Open).
-    std::pair<int, Error> Decrypt(common::Slice data, common::Slice additional) const;
+    virtual std::pair<int, Error> Decrypt(common::Slice data, common::Slice additional) const;
     uint32_t Slot() const { return slot_; }
+
+  protected:
+    AES() = default;
 
   private:
     std::shared_ptr<GPUContext> g_;
-    uint32_t slot_;
+    uint32_t slot_ = 0;
 };
 
 // crypto/aes.go:65-83: PBKDF2-HMAC-SHA512(secret, salt, 10000, 32) on the host, key schedule and

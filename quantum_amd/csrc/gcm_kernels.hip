@@ -1484,6 +1484,18 @@ __device__ __forceinline__ bool res_forward(const ResArgs &a, const ResDev &d, u
     return __ballot(fresh[0] || fresh[1] || fresh[2] || fresh[3]) != 0;
 }
 
+// QGCM_RES_TRACE (side builds only, tools/res_trace.py): per request, the 100-MHz clock when the
+// dispatcher read the bell change, when it had forwarded, when the worker saw its bell, when it
+// started and finished the packet, and when it published the verdict.
+#ifdef QGCM_RES_TRACE
+__device__ unsigned long long g_res_trace[1 << 16][8];
+__device__ unsigned int g_res_trace_n;
+__device__ unsigned long long g_res_disp[2];  // dispatcher: last bell-change read, last forward end
+#define RES_TR(x) x
+#else
+#define RES_TR(x)
+#endif
+
 __global__ void __launch_bounds__(kOneThreads) gcm_resident_kernel(Batch b, const uint32_t *__restrict__ rk_table,
                                                                    ResArgs a) {
     const uint32_t tid = threadIdx.x, lane = tid & 63u, w = blockIdx.x;
@@ -1506,7 +1518,13 @@ __global__ void __launch_bounds__(kOneThreads) gcm_resident_kernel(Batch b, cons
                 if (first || ending || bell != last) {
                     last = bell;  // read before the scan: a request posted after it rings again
                     first = false;
-                    if (res_forward(a, d, lane)) act = now;
+                    if (res_forward(a, d, lane)) {
+                        act = now;
+                        RES_TR(if (lane == 0) {
+                            g_res_disp[0] = now;
+                            g_res_disp[1] = wall_clock64();
+                        })
+                    }
                 }
                 if (ending) break;  // everything posted before the last read of the bell is forwarded
                 __builtin_amdgcn_s_sleep(4);
@@ -1541,6 +1559,7 @@ __global__ void __launch_bounds__(kOneThreads) gcm_resident_kernel(Batch b, cons
                 __syncthreads();  // every thread has read the command before thread 0 writes the next
                 continue;
             }
+            RES_TR(const unsigned long long t_seen = wall_clock64();)
             if (tid < 64) {  // wave 0: which of this worker's slots were forwarded and are not served yet
                 bool pend = false;
                 if (lane < P) {
@@ -1580,6 +1599,7 @@ __global__ void __launch_bounds__(kOneThreads) gcm_resident_kernel(Batch b, cons
                                    stage <= kResSlotBytes && stage <= kOneCap - 16;
                 uint32_t ok = 0;
                 uint8_t *slot = a.data + (size_t)sl * kResSlotBytes;
+                RES_TR(const unsigned long long t_pk0 = wall_clock64();)
                 if (valid)
                     ok = op ? one_packet<true, true>(b, rk_table, slot, Lin, key, aad, nullptr, false, tab_key, tab_n)
                             : one_packet<false, true>(b, rk_table, slot, Lin, key, aad, nullptr, false, tab_key, tab_n);
@@ -1587,8 +1607,20 @@ __global__ void __launch_bounds__(kOneThreads) gcm_resident_kernel(Batch b, cons
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __syncthreads();
                 if (tid == 0) {
+                    RES_TR(const unsigned long long t_pk1 = wall_clock64();)
                     __hip_atomic_store(a.done + sl, q << 1 | ok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     lds_st32(kResDone + 4 * j, q);
+                    RES_TR({
+                        const unsigned int k = atomicAdd(&g_res_trace_n, 1u) & 0xffffu;
+                        g_res_trace[k][0] = g_res_disp[0];
+                        g_res_trace[k][1] = g_res_disp[1];
+                        g_res_trace[k][2] = t_seen;
+                        g_res_trace[k][3] = t_pk0;
+                        g_res_trace[k][4] = t_pk1;
+                        g_res_trace[k][5] = wall_clock64();
+                        g_res_trace[k][6] = sl;
+                        g_res_trace[k][7] = Lin;
+                    })
                 }
             }
             __syncthreads();
@@ -1603,6 +1635,17 @@ __global__ void __launch_bounds__(kOneThreads) gcm_resident_kernel(Batch b, cons
         }
     }
 }
+
+#ifdef QGCM_RES_TRACE
+extern "C" int qgcm_debug_res_trace(unsigned long long *out, int n) {
+    unsigned int cnt = 0;
+    if (hipMemcpyFromSymbol(&cnt, HIP_SYMBOL(g_res_trace_n), 4) != hipSuccess) return -1;
+    if (cnt > (1u << 16)) cnt = 1u << 16;
+    if ((unsigned)n > cnt) n = (int)cnt;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_res_trace), (size_t)n * 64) != hipSuccess) return -1;
+    return n;
+}
+#endif
 
 hipError_t launch_resident(const Batch &b, const ResArgs &a, hipStream_t s) {
     if (a.workers == 0 || a.per_worker == 0 || a.per_worker > kResMaxPerWorker ||
