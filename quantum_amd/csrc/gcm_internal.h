@@ -89,11 +89,12 @@ hipError_t launch_one(bool seal, const Batch &b, hipStream_t s);
 // Resident per-packet service (resident.cpp): `workers` 256-thread workgroups of gcm_one_kernel's
 // engine plus one dispatcher workgroup stay on the GPU and serve requests the host posts into pinned
 // (coherent) host memory, so a per-packet call costs no launch.  Slot s belongs to worker s / per_worker.
-// Host -> device: the slot bytes, meta[s] = {op (1 seal, 0 open), len, key_idx, aad_len}, then seq[s]
-// (31-bit, +1 per request), then bell[0] += 1 (bell[1] = stop).  The dispatcher (one wave) is the only
+// Host -> device: the slot bytes, then the slot's 16-B request record req[s] = {seq (31-bit, +1 per
+// request), op (1 seal, 0 open) | aad_len << 1, len, key_idx} in one aligned 16-B store (one snapshot
+// for the GPU's 16-B read), then bell[0] += 1 (bell[1] = stop).  The dispatcher (one wave) is the only
 // reader of host memory while idle: it polls bell[0] (one 8-B read per poll, s_sleep between polls) and
-// on a change reads every slot's seq, forwards each new request's meta and seq to device memory and
-// rings its worker's device bell; the worker (polling that bell in L2) serves the slot in place over
+// on a change reads every request record (one 16-B load per slot, all in flight together), forwards
+// each new request to device memory and rings its worker's device bell; the worker (polling that bell in L2) serves the slot in place over
 // PCIe and writes done[s] = seq << 1 | verdict into host memory.  Every host-memory access of the kernel
 // is a relaxed system-scope atomic (no cache maintenance).  An instance ends on the host's stop word, or
 // when the dispatcher sees no request for idle_ticks or the instance is life_ticks old (100 MHz clock):
@@ -108,8 +109,7 @@ constexpr uint32_t kResDevBell = 64;
 inline size_t res_dev_bytes(uint32_t workers, uint32_t slots) { return kResDevBell + 64ull * workers + 4ull * slots + 16ull * slots + 16; }
 struct ResArgs {
     uint32_t *bell;         // host: [0] bell, [1] stop
-    const uint32_t *seq;    // host: [S]
-    const uint4 *meta;      // host: [S]
+    const uint4 *req;       // host: [S] request records
     uint32_t *done;         // host: [S]
     uint32_t *over;         // host: generation of the last instance that ended
     uint8_t *data;          // host: [S][kResSlotBytes]

@@ -1090,27 +1090,35 @@ __device__ __forceinline__ void block_mask(uint32_t r, uint32_t &m0, uint32_t &m
     m3 = q == 3 ? lowmask(sb) : 0u;
 }
 
+// 16-B accesses of pinned host memory that go around the GPU caches (buffer instructions with sc0 sc1:
+// a kernel that keeps running while the host rewrites the memory must not hit stale lines, and its
+// results must reach the host without an L2 write-back).  A wave's 16-B lanes leave as whole 64-B
+// requests; 8-B system-scope atomics cost about a round trip each (tools/microbench/hostmem.hip: a
+// 1408-B request read and written back in 5.3 us vs 31.3 us).
+constexpr int kSc0Sc1 = 1 | 16;  // cache-policy bits of the buffer intrinsics on gfx950: sc0 = 1, sc1 = 16
+__device__ __forceinline__ uint4 host_ld16(const void *base, uint32_t bytes, uint32_t off) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, (int)bytes, 0x00020000);
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, kSc0Sc1);
+    return uint4{v.x, v.y, v.z, v.w};
+}
+__device__ __forceinline__ void host_st16(void *base, uint32_t bytes, uint32_t off, uint4 v) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, 0, (int)bytes, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(u32x4{v.x, v.y, v.z, v.w}, r, (int)off, 0, kSc0Sc1);
+}
+
 // Slot access of the latency engine.  kSys = false: plain 16-B loads and stores (the slot is device
 // memory, or pinned host memory handed over at a kernel launch).  kSys = true (the resident kernel,
-// whose slots in pinned host memory are rewritten by the host while the kernel runs): every access
-// is a relaxed system-scope 8-B atomic (global_load/store sc0 sc1: around the GPU caches, so no
-// cache invalidation or write-back of the XCD's L2 -- which a bulk kernel may be filling -- is needed).
+// whose slots in pinned host memory are rewritten by the host while the kernel runs): host_ld16 /
+// host_st16 within the kResSlotBytes slot.
 template <bool kSys>
 __device__ __forceinline__ uint4 slot_ld16(const uint8_t *slot, uint32_t i) {
-    if constexpr (kSys) {
-        const uint64_t *p = reinterpret_cast<const uint64_t *>(slot) + 2 * i;
-        const uint64_t a = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        const uint64_t c = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        return uint4{(uint32_t)a, (uint32_t)(a >> 32), (uint32_t)c, (uint32_t)(c >> 32)};
-    }
+    if constexpr (kSys) return host_ld16(slot, kResSlotBytes, 16 * i);
     return reinterpret_cast<const uint4 *>(slot)[i];
 }
 template <bool kSys>
 __device__ __forceinline__ void slot_st16(uint8_t *slot, uint32_t i, uint4 v) {
     if constexpr (kSys) {
-        uint64_t *p = reinterpret_cast<uint64_t *>(slot) + 2 * i;
-        __hip_atomic_store(p, (uint64_t)v.x | (uint64_t)v.y << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(p + 1, (uint64_t)v.z | (uint64_t)v.w << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        host_st16(slot, kResSlotBytes, 16 * i, v);
         return;
     }
     reinterpret_cast<uint4 *>(slot)[i] = v;
@@ -1435,24 +1443,25 @@ __device__ __forceinline__ ResDev res_dev(const ResArgs &a) {
 // whether anything was forwarded.  Wave-uniform.
 __device__ __forceinline__ bool res_forward(const ResArgs &a, const ResDev &d, uint32_t lane) {
     const uint32_t S = a.workers * a.per_worker;
-    uint32_t q[4];
+    // slot 64 k + l is lane l's k-th: every request record in flight together (one PCIe round trip)
+    uint4 m[4];
 #pragma unroll
-    for (uint32_t k = 0; k < 4; ++k) {  // every load in flight together: one PCIe round trip
+    for (uint32_t k = 0; k < 4; ++k) {
         const uint32_t sl = lane + 64u * k;
-        q[k] = sl < S ? ld_sys32(a.seq + sl) & 0x7fffffffu : 0u;
+        m[k] = sl < S ? host_ld16(a.req, 16 * S, 16 * sl) : uint4{0, 0, 0, 0};
     }
+    uint32_t q[4];
     bool fresh[4];
     uint32_t any = 0;
 #pragma unroll
     for (uint32_t k = 0; k < 4; ++k) {
         const uint32_t sl = lane + 64u * k;
+        q[k] = m[k].x & 0x7fffffffu;
         fresh[k] = sl < S && q[k] != lds32(kResDone + 4 * sl);
-        if (fresh[k]) {
-            const uint64_t *mp = reinterpret_cast<const uint64_t *>(a.meta + sl);
-            const uint64_t m0 = ld_sys64(mp), m1 = ld_sys64(mp + 1);
-            st_agent(reinterpret_cast<uint64_t *>(d.fmeta + 4 * sl), m0);
-            st_agent(reinterpret_cast<uint64_t *>(d.fmeta + 4 * sl) + 1, m1);
+        if (fresh[k]) {  // forward {op, len, key, aad_len} as the workers read it
             any |= 1u << (sl / a.per_worker % 32u);
+            st_agent(reinterpret_cast<uint64_t *>(d.fmeta + 4 * sl), (uint64_t)(m[k].y & 1u) | (uint64_t)m[k].z << 32);
+            st_agent(reinterpret_cast<uint64_t *>(d.fmeta + 4 * sl) + 1, (uint64_t)m[k].w | (uint64_t)(m[k].y >> 1) << 32);
         }
     }
     // meta before sequence: the worker reads the meta only after it has seen the sequence
@@ -1467,12 +1476,10 @@ __device__ __forceinline__ bool res_forward(const ResArgs &a, const ResDev &d, u
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     // one bell add per worker that got work (workers <= 32 here; more: each slot rings its own)
-    uint64_t ring = 0;
     if (a.workers <= 32u) {
         uint32_t r = any;
         for (uint32_t off = 32; off > 0; off >>= 1) r |= __shfl_xor(r, off, 64);
-        ring = r;
-        if (lane < a.workers && ((ring >> lane) & 1u))
+        if (lane < a.workers && ((r >> lane) & 1u))
             __hip_atomic_fetch_add(d.wbell + 16u * lane, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
 #pragma unroll
@@ -1521,8 +1528,8 @@ __global__ void __launch_bounds__(kOneThreads) gcm_resident_kernel(Batch b, cons
                     if (res_forward(a, d, lane)) {
                         act = now;
                         RES_TR(if (lane == 0) {
-                            g_res_disp[0] = now;
-                            g_res_disp[1] = wall_clock64();
+                            st_agent(&g_res_disp[0], (unsigned long long)now);
+                            st_agent(&g_res_disp[1], (unsigned long long)wall_clock64());
                         })
                     }
                 }
@@ -1612,8 +1619,8 @@ __global__ void __launch_bounds__(kOneThreads) gcm_resident_kernel(Batch b, cons
                     lds_st32(kResDone + 4 * j, q);
                     RES_TR({
                         const unsigned int k = atomicAdd(&g_res_trace_n, 1u) & 0xffffu;
-                        g_res_trace[k][0] = g_res_disp[0];
-                        g_res_trace[k][1] = g_res_disp[1];
+                        g_res_trace[k][0] = ld_agent(&g_res_disp[0]);
+                        g_res_trace[k][1] = ld_agent(&g_res_disp[1]);
                         g_res_trace[k][2] = t_seen;
                         g_res_trace[k][3] = t_pk0;
                         g_res_trace[k][4] = t_pk1;

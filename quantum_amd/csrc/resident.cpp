@@ -15,8 +15,13 @@
 // workers cache key tables) / qgcm_destroy.  Before leaving, every worker serves what is pending; a
 // request posted after that is seen by its caller (the instance's `over` word names its generation)
 // and the caller launches the next instance, which serves it.  At most one instance runs at a time.
+#include <emmintrin.h>
 #include <hip/hip_runtime.h>
+#include <linux/futex.h>
 #include <sched.h>
+#include <sys/syscall.h>
+#include <time.h>
+#include <unistd.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -26,6 +31,7 @@
 #include <chrono>
 #include <memory>
 #include <mutex>
+#include <thread>
 
 #include "gcm_internal.h"
 
@@ -37,8 +43,8 @@ struct Resident {
     uint32_t W = 16, P = 16, S = 256;
     uint64_t idle_ticks = 200000, life_ticks = 800000;  // 100 MHz: 2 ms, 8 ms
     uint8_t *host = nullptr;  // pinned coherent region (below)
-    uint32_t *bell = nullptr, *seq = nullptr, *done = nullptr, *over = nullptr;
-    uint4 *meta = nullptr;
+    uint32_t *bell = nullptr, *done = nullptr, *over = nullptr;
+    uint4 *req = nullptr;
     uint8_t *data = nullptr;
     uint8_t *d_ctl = nullptr;  // device control region (res_dev_bytes)
     size_t ctl_bytes = 0;
@@ -51,9 +57,21 @@ struct Resident {
     std::atomic<uint32_t> gen{0};  // generation of the current (or last) instance; 0 = never launched
     std::atomic<bool> broken{false};
     std::atomic<uint64_t> served{0}, launches{0};
+    // callers that stop spinning sleep on a futex; one completion thread watches their done words
+    uint64_t spin_ns = 20000;                           // QGCM_RESIDENT_SPIN_US
+    std::unique_ptr<std::atomic<uint32_t>[]> want;      // per slot: the sequence a sleeping caller waits for
+    std::unique_ptr<std::atomic<uint32_t>[]> wake;      // per slot futex word
+    std::atomic<uint32_t> sleepers{0};                  // futex word of the completion thread
+    std::atomic<bool> quit{false};
+    std::thread waker;
+    std::mutex waker_mu;
 };
 
 namespace {
+
+long futex(std::atomic<uint32_t> *w, int op, uint32_t val, const struct timespec *ts) {
+    return syscall(SYS_futex, reinterpret_cast<uint32_t *>(w), op, val, ts, nullptr, 0);
+}
 
 uint64_t env_u64(const char *name, uint64_t dflt) {
     const char *v = getenv(name);
@@ -72,8 +90,7 @@ int relaunch(Resident *r, uint32_t g) {
     }
     ResArgs a{};
     a.bell = r->bell;
-    a.seq = r->seq;
-    a.meta = r->meta;
+    a.req = r->req;
     a.done = r->done;
     a.over = r->over;
     a.data = r->data;
@@ -97,6 +114,26 @@ bool instance_over(const Resident *r, uint32_t g) {
     return g == 0 || __atomic_load_n(r->over, __ATOMIC_ACQUIRE) == g;
 }
 
+// The completion thread: while callers sleep, it watches their slots' done words and wakes each caller
+// whose verdict has arrived (and launches the next instance when one ends with callers waiting).
+void waker_loop(Resident *r) {
+    while (!r->quit.load(std::memory_order_acquire)) {
+        if (r->sleepers.load(std::memory_order_acquire) == 0) {
+            const struct timespec ts = {0, 10 * 1000 * 1000};
+            futex(&r->sleepers, FUTEX_WAIT_PRIVATE, 0, &ts);
+            continue;
+        }
+        for (uint32_t s = 0; s < r->S; ++s) {
+            const uint32_t w = r->want[s].load(std::memory_order_acquire);
+            if (w && (__atomic_load_n(&r->done[s], __ATOMIC_ACQUIRE) >> 1) == w && r->wake[s].exchange(1) == 0)
+                futex(&r->wake[s], FUTEX_WAKE_PRIVATE, 1, nullptr);
+        }
+        const uint32_t g = r->gen.load(std::memory_order_acquire);
+        if (instance_over(r, g)) relaunch(r, g);
+        for (int i = 0; i < 32; ++i) _mm_pause();
+    }
+}
+
 }  // namespace
 
 Resident *resident_create(int device, const Batch &base, int num_cus) {
@@ -109,27 +146,30 @@ Resident *resident_create(int device, const Batch &base, int num_cus) {
         return nullptr;
     r->S = r->W * r->P;
     r->ctl_bytes = res_dev_bytes(r->W, r->S);
+    r->spin_ns = env_u64("QGCM_RESIDENT_SPIN_US", 20) * 1000;
     r->idle_ticks = env_u64("QGCM_RESIDENT_IDLE_US", 2000) * 100;  // s_memrealtime: 100 MHz
     r->life_ticks = env_u64("QGCM_RESIDENT_LIFE_US", 8000) * 100;
-    // host region: bell and stop (a 64-B line), seq, done, over, meta, then the slots (4 KiB aligned)
-    const size_t o_seq = 64, o_done = o_seq + 4ull * r->S, o_over = o_done + 4ull * r->S;
-    const size_t o_meta = (o_over + 64 + 15) & ~15ull, o_data = (o_meta + 16ull * r->S + 4095) & ~4095ull;
+    // host region: bell and stop (a 64-B line), done, over, the request records, then the slots
+    const size_t o_done = 64, o_over = o_done + 4ull * r->S;
+    const size_t o_req = (o_over + 64 + 15) & ~15ull, o_data = (o_req + 16ull * r->S + 4095) & ~4095ull;
     const size_t bytes = o_data + (size_t)kResSlotBytes * r->S;
     if (hipSetDevice(device) != hipSuccess ||
         hipHostMalloc(reinterpret_cast<void **>(&r->host), bytes, hipHostMallocCoherent) != hipSuccess)
         return nullptr;
     memset(r->host, 0, o_data);
     r->bell = reinterpret_cast<uint32_t *>(r->host);
-    r->seq = reinterpret_cast<uint32_t *>(r->host + o_seq);
     r->done = reinterpret_cast<uint32_t *>(r->host + o_done);
     r->over = reinterpret_cast<uint32_t *>(r->host + o_over);
-    r->meta = reinterpret_cast<uint4 *>(r->host + o_meta);
+    r->req = reinterpret_cast<uint4 *>(r->host + o_req);
     r->data = r->host + o_data;
     r->seqh.reset(new uint32_t[r->S]());
     r->busy.reset(new std::atomic<uint32_t>[r->S]);
     for (uint32_t i = 0; i < r->S; ++i) r->busy[i] = 0;
     r->inflight.reset(new std::atomic<int32_t>[r->W]);
     for (uint32_t i = 0; i < r->W; ++i) r->inflight[i] = 0;
+    r->want.reset(new std::atomic<uint32_t>[r->S]);
+    r->wake.reset(new std::atomic<uint32_t>[r->S]);
+    for (uint32_t i = 0; i < r->S; ++i) r->want[i] = r->wake[i] = 0;
     int lo = 0, hi = 0;
     if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) hi = 0;
     if (hipMalloc(reinterpret_cast<void **>(&r->d_ctl), r->ctl_bytes) != hipSuccess ||
@@ -158,6 +198,9 @@ int resident_quiesce(Resident *r) {
 
 void resident_destroy(Resident *r) {
     if (!r) return;
+    r->quit = true;
+    futex(&r->sleepers, FUTEX_WAKE_PRIVATE, 1, nullptr);
+    if (r->waker.joinable()) r->waker.join();
     resident_quiesce(r);
     hipSetDevice(r->device);
     if (r->stream) hipStreamDestroy(r->stream);
@@ -229,33 +272,57 @@ long resident_call(Resident *r, bool seal, uint32_t key, uint8_t *data, long len
     memcpy(slot, &hdr, 4);
     memcpy(slot + 4, data, (size_t)len);
     if (seal) memcpy(slot + 4 + len + 16, nb, 12);
-    r->meta[s] = uint4{seal ? 1u : 0u, (uint32_t)len, key, aad_len};
     uint32_t q = (r->seqh[s] + 1) & 0x7fffffffu;
     if (q == 0) q = 1;
     r->seqh[s] = q;
-    __atomic_store_n(&r->seq[s], q, __ATOMIC_RELEASE);
+    // the request record in one aligned 16-B store, after the slot bytes (x86 keeps store order; the
+    // GPU reads the record with one 16-B load)
+    std::atomic_thread_fence(std::memory_order_release);
+    _mm_store_si128(reinterpret_cast<__m128i *>(&r->req[s]),
+                    _mm_set_epi32((int)key, (int)len, (int)((seal ? 1u : 0u) | aad_len << 1), (int)q));
     __atomic_fetch_add(&r->bell[0], 1u, __ATOMIC_SEQ_CST);
     long rc = 0;
     uint32_t g = r->gen.load(std::memory_order_acquire);
     if (instance_over(r, g) && relaunch(r, g) != QGCM_OK) return -1;  // broken: the slot stays taken
     uint32_t v = 0;
     const auto t0 = std::chrono::steady_clock::now();
+    bool asleep = false;
     for (uint32_t spins = 0;; ++spins) {
         v = __atomic_load_n(&r->done[s], __ATOMIC_ACQUIRE);
         if ((v >> 1) == q) break;
-        if ((spins & 63) == 63) {
+        if ((spins & 63) == 63 || asleep) {
             g = r->gen.load(std::memory_order_acquire);
             // the instance ended with this request still pending: launch the next one
             if (instance_over(r, g) && relaunch(r, g) != QGCM_OK) return -1;  // broken: the slot stays taken
-            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
+            const auto waited = std::chrono::steady_clock::now() - t0;
+            if (waited > std::chrono::seconds(5)) {
                 r->broken = true;  // never observed; the slot stays taken (the device may still serve it)
                 return -1;
             }
+            // past the spin budget: sleep until the completion thread sees the verdict (with many more
+            // callers than CPUs, spinning ones would take the CPUs the posting ones need)
+            if (!asleep && (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(waited).count() > r->spin_ns) {
+                if (!r->waker.joinable()) {
+                    std::lock_guard<std::mutex> lk(r->waker_mu);
+                    if (!r->waker.joinable()) r->waker = std::thread(waker_loop, r);
+                }
+                r->wake[s].store(0, std::memory_order_relaxed);
+                r->want[s].store(q, std::memory_order_release);
+                if (r->sleepers.fetch_add(1) == 0) futex(&r->sleepers, FUTEX_WAKE_PRIVATE, 1, nullptr);
+                asleep = true;
+                continue;  // re-check done before the first wait
+            }
         }
-        if (spins < 4096)
+        if (asleep) {
+            const struct timespec ts = {0, 200 * 1000};
+            futex(&r->wake[s], FUTEX_WAIT_PRIVATE, 0, &ts);
+        } else {
             __builtin_ia32_pause();
-        else
-            sched_yield();
+        }
+    }
+    if (asleep) {
+        r->want[s].store(0, std::memory_order_relaxed);
+        r->sleepers.fetch_sub(1);
     }
     r->served.fetch_add(1, std::memory_order_relaxed);
     if (seal) {
