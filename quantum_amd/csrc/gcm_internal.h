@@ -108,13 +108,14 @@ constexpr uint32_t kResMaxSlots = 256;     // the dispatcher wave scans 4 slots 
 constexpr uint32_t kResDevBell = 64;
 inline size_t res_dev_bytes(uint32_t workers, uint32_t slots) { return kResDevBell + 64ull * workers + 4ull * slots + 16ull * slots + 16; }
 struct ResArgs {
-    uint32_t *bell;         // host: [0] bell, [1] stop
+    uint32_t *bell;         // host: dispatch: [0] bell, [1] stop; direct: worker w's bell at 16 w, stop at 16 w + 1
     const uint4 *req;       // host: [S] request records
     uint32_t *done;         // host: [S]
     uint32_t *over;         // host: generation of the last instance that ended
     uint8_t *data;          // host: [S][kResSlotBytes]
     uint8_t *dev;           // device control region (res_dev_bytes), zeroed per launch
-    uint32_t workers, per_worker, gen, pad;
+    uint32_t workers, per_worker, gen;
+    uint32_t dispatch;      // 1: a dispatcher workgroup forwards requests; 0: each worker polls its own bell
     uint64_t idle_ticks, life_ticks;
 };
 hipError_t launch_resident(const Batch &b, const ResArgs &a, hipStream_t s);

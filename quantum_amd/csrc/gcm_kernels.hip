@@ -1406,7 +1406,8 @@ __global__ void __launch_bounds__(kOneThreads) gcm_one_kernel(Batch b, const uin
 // worker: 16 pollers cut a concurrent host batch's PCIe rate from 34 to 3.3 GiB/s).
 constexpr uint32_t kResCtl = (kOneLds + 15u) & ~15u;  // LDS: [0] command, [8,16) pending mask, [16,36) request
 constexpr uint32_t kResDone = kResCtl + 64;           // worker: the done sequence of each of its slots
-constexpr uint32_t kResLds = kResDone + 4 * kResMaxSlots;  // dispatcher: the forwarded sequence of every slot
+constexpr uint32_t kResRec = kResDone + 4 * kResMaxSlots;  // (dispatcher: the forwarded sequence of every slot)
+constexpr uint32_t kResLds = kResRec + 16 * kResMaxPerWorker;  // direct mode: the worker's request records
 static_assert(kResLds <= 160u * 1024u, "gfx950 LDS is 160 KiB per workgroup");
 
 __device__ __forceinline__ uint32_t ld_sys32(const uint32_t *p) {
@@ -1508,7 +1509,90 @@ __global__ void __launch_bounds__(kOneThreads) gcm_resident_kernel(Batch b, cons
     const uint32_t tid = threadIdx.x, lane = tid & 63u, w = blockIdx.x;
     const uint32_t S = a.workers * a.per_worker;
     const ResDev d = res_dev(a);
-    if (w == a.workers) {  // ---- the dispatcher (wave 0 only) ----
+    if (!a.dispatch) {  // ---- direct mode: every worker polls its own bell in host memory ----
+        const uint32_t P = a.per_worker, first = w * P;
+        one_fill_te(b.te, tid);
+        if (tid < P) lds_st32(kResDone + 4 * tid, ld_sys32(a.done + first + tid) >> 1);
+        uint32_t tab_key = 0xffffffffu, tab_n = 0, last_bell = 0, idle = 0;
+        bool scanned = false;
+        const uint64_t t_start = wall_clock64();
+        __syncthreads();
+        for (;;) {
+            // 0: idle, 1: scan and serve, 2: scan and serve, then leave
+            if (tid == 0) {
+                uint32_t cmd = 0;
+                if (w == 0) {  // the instance's end: no request for idle_ticks, or life_ticks old
+                    const uint64_t now = wall_clock64();
+                    const uint64_t act = ld_agent(d.words);  // last activity of any worker (0: none yet)
+                    const int64_t quiet = (int64_t)(now - (act > t_start ? act : t_start));
+                    if (quiet > (int64_t)a.idle_ticks || now - t_start > a.life_ticks) st_agent(d.words + 1, (uint64_t)1);
+                }
+                const uint64_t hb = ld_sys64(reinterpret_cast<const uint64_t *>(a.bell + 16u * w));
+                const uint32_t bell = (uint32_t)hb, stop = (uint32_t)(hb >> 32);
+                if (stop || ld_agent(d.words + 1)) {
+                    cmd = 2;
+                } else if (!scanned || bell != last_bell) {
+                    cmd = 1;
+                    last_bell = bell;  // read before the scan: a request posted after it rings again
+                    scanned = true;
+                }
+                lds_st32(kResCtl, cmd);
+                idle = cmd ? 0 : idle + 1;
+                if (cmd == 0) {  // back off when quiet: fewer PCIe reads next to bulk traffic
+                    if (idle < 256)
+                        __builtin_amdgcn_s_sleep(2);
+                    else
+                        __builtin_amdgcn_s_sleep(32);
+                }
+            }
+            __syncthreads();
+            const uint32_t cmd = lds32(kResCtl);
+            if (cmd == 0) {
+                __syncthreads();  // every thread has read the command before thread 0 writes the next
+                continue;
+            }
+            if (tid < 64) {  // wave 0: this worker's request records (one 16-B load per slot, one round trip)
+                bool pend = false;
+                if (lane < P) {
+                    const uint4 m = host_ld16(a.req, 16 * S, 16 * (first + lane));
+                    pend = (m.x & 0x7fffffffu) != lds32(kResDone + 4 * lane);
+                    if (pend) lds_st128(kResRec + 16 * lane, m);
+                }
+                const uint64_t m = __ballot(pend);
+                if (lane == 0) {
+                    lds_st32(kResCtl + 8, (uint32_t)m);
+                    lds_st32(kResCtl + 12, (uint32_t)(m >> 32));
+                }
+            }
+            __syncthreads();
+            uint64_t mask = lds32(kResCtl + 8) | (uint64_t)lds32(kResCtl + 12) << 32;
+            while (mask) {
+                const uint32_t j = (uint32_t)__builtin_ctzll(mask);
+                mask &= mask - 1;
+                const uint32_t sl = first + j;
+                const uint4 m = lds128(kResRec + 16 * j);
+                const uint32_t q = m.x & 0x7fffffffu, op = m.y & 1u, aad = m.y >> 1, Lin = m.z, key = m.w;
+                const uint64_t stage = (4ull + Lin + (op ? QGCM_OVERHEAD : 0) + 15) & ~15ull;
+                const bool valid = aad <= 4u && key < b.max_keys && b.key_valid[key] &&
+                                   (op ? Lin < QGCM_MAX_PAYLOAD : Lin >= (uint32_t)QGCM_OVERHEAD) &&
+                                   stage <= kResSlotBytes && stage <= kOneCap - 16;
+                uint32_t ok = 0;
+                uint8_t *slot = a.data + (size_t)sl * kResSlotBytes;
+                if (valid)
+                    ok = op ? one_packet<true, true>(b, rk_table, slot, Lin, key, aad, nullptr, false, tab_key, tab_n)
+                            : one_packet<false, true>(b, rk_table, slot, Lin, key, aad, nullptr, false, tab_key, tab_n);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+                if (tid == 0) {
+                    __hip_atomic_store(a.done + sl, q << 1 | ok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    lds_st32(kResDone + 4 * j, q);
+                    __hip_atomic_fetch_max(d.words, wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+            __syncthreads();
+            if (cmd == 2) break;
+        }
+    } else if (w == a.workers) {  // ---- the dispatcher (wave 0 only) ----
         if (tid < 64) {
             for (uint32_t sl = lane; sl < S; sl += 64) lds_st32(kResDone + 4 * sl, ld_sys32(a.done + sl) >> 1);
             const uint64_t t_start = wall_clock64();
@@ -1636,7 +1720,7 @@ __global__ void __launch_bounds__(kOneThreads) gcm_resident_kernel(Batch b, cons
     }
     if (tid == 0) {  // the last workgroup to leave tells the host this instance is over
         const uint64_t n = __hip_atomic_fetch_add(d.words + 2, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (n == a.workers) {
+        if (n + 1 == a.workers + (a.dispatch ? 1u : 0u)) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __hip_atomic_store(a.over, a.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
@@ -1659,7 +1743,7 @@ hipError_t launch_resident(const Batch &b, const ResArgs &a, hipStream_t s) {
         a.workers * a.per_worker > kResMaxSlots)
         return hipErrorInvalidValue;
     void *args[] = {const_cast<Batch *>(&b), const_cast<uint32_t **>(&b.rk_table), const_cast<ResArgs *>(&a)};
-    return hipLaunchKernel(reinterpret_cast<const void *>(&gcm_resident_kernel), dim3(a.workers + 1),
+    return hipLaunchKernel(reinterpret_cast<const void *>(&gcm_resident_kernel), dim3(a.workers + (a.dispatch ? 1 : 0)),
                            dim3(kOneThreads), args, kResLds, s);
 }
 

@@ -57,6 +57,7 @@ struct Resident {
     std::atomic<uint32_t> gen{0};  // generation of the current (or last) instance; 0 = never launched
     std::atomic<bool> broken{false};
     std::atomic<uint64_t> served{0}, launches{0};
+    bool dispatch = true;  // QGCM_RESIDENT_DISPATCH: one dispatcher polls host memory (1) or every worker (0)
     // callers that stop spinning sleep on a futex; one completion thread watches their done words
     uint64_t spin_ns = 20000;                           // QGCM_RESIDENT_SPIN_US
     std::unique_ptr<std::atomic<uint32_t>[]> want;      // per slot: the sequence a sleeping caller waits for
@@ -99,6 +100,7 @@ int relaunch(Resident *r, uint32_t g) {
     a.per_worker = r->P;
     a.gen = g + 1;
     a.idle_ticks = r->idle_ticks;
+    a.dispatch = r->dispatch ? 1u : 0u;
     a.life_ticks = r->life_ticks;
     if (hipMemsetAsync(r->d_ctl, 0, r->ctl_bytes, r->stream) != hipSuccess ||
         launch_resident(r->base, a, r->stream) != hipSuccess) {
@@ -147,10 +149,11 @@ Resident *resident_create(int device, const Batch &base, int num_cus) {
     r->S = r->W * r->P;
     r->ctl_bytes = res_dev_bytes(r->W, r->S);
     r->spin_ns = env_u64("QGCM_RESIDENT_SPIN_US", 20) * 1000;
+    r->dispatch = env_u64("QGCM_RESIDENT_DISPATCH", 1) != 0;
     r->idle_ticks = env_u64("QGCM_RESIDENT_IDLE_US", 2000) * 100;  // s_memrealtime: 100 MHz
     r->life_ticks = env_u64("QGCM_RESIDENT_LIFE_US", 8000) * 100;
-    // host region: bell and stop (a 64-B line), done, over, the request records, then the slots
-    const size_t o_done = 64, o_over = o_done + 4ull * r->S;
+    // host region: bells (a 64-B line per worker: bell, stop), done, over, the request records, then the slots
+    const size_t o_done = 64ull * r->W, o_over = o_done + 4ull * r->S;
     const size_t o_req = (o_over + 64 + 15) & ~15ull, o_data = (o_req + 16ull * r->S + 4095) & ~4095ull;
     const size_t bytes = o_data + (size_t)kResSlotBytes * r->S;
     if (hipSetDevice(device) != hipSuccess ||
@@ -186,9 +189,9 @@ int resident_quiesce(Resident *r) {
     std::lock_guard<std::mutex> lk(r->launch_mu);
     const uint32_t g = r->gen.load(std::memory_order_acquire);
     if (g == 0) return QGCM_OK;
-    __atomic_store_n(&r->bell[1], 1u, __ATOMIC_RELEASE);
+    for (uint32_t w = 0; w < r->W; ++w) __atomic_store_n(&r->bell[16 * w + 1], 1u, __ATOMIC_RELEASE);
     const hipError_t e = hipSetDevice(r->device) == hipSuccess ? hipStreamSynchronize(r->stream) : hipErrorUnknown;
-    __atomic_store_n(&r->bell[1], 0u, __ATOMIC_RELEASE);
+    for (uint32_t w = 0; w < r->W; ++w) __atomic_store_n(&r->bell[16 * w + 1], 0u, __ATOMIC_RELEASE);
     if (e != hipSuccess) {
         r->broken = true;
         return QGCM_E_HIP;
@@ -280,7 +283,7 @@ long resident_call(Resident *r, bool seal, uint32_t key, uint8_t *data, long len
     std::atomic_thread_fence(std::memory_order_release);
     _mm_store_si128(reinterpret_cast<__m128i *>(&r->req[s]),
                     _mm_set_epi32((int)key, (int)len, (int)((seal ? 1u : 0u) | aad_len << 1), (int)q));
-    __atomic_fetch_add(&r->bell[0], 1u, __ATOMIC_SEQ_CST);
+    __atomic_fetch_add(&r->bell[r->dispatch ? 0 : 16 * w], 1u, __ATOMIC_SEQ_CST);
     long rc = 0;
     uint32_t g = r->gen.load(std::memory_order_acquire);
     if (instance_over(r, g) && relaunch(r, g) != QGCM_OK) return -1;  // broken: the slot stays taken
