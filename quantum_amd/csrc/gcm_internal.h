@@ -87,35 +87,27 @@ constexpr uint32_t kOneCap = 32768;
 hipError_t launch_one(bool seal, const Batch &b, hipStream_t s);
 
 // Resident per-packet service (resident.cpp): `workers` 256-thread workgroups of gcm_one_kernel's
-// engine plus one dispatcher workgroup stay on the GPU and serve requests the host posts into pinned
-// (coherent) host memory, so a per-packet call costs no launch.  Slot s belongs to worker s / per_worker.
+// engine stay on the GPU and serve requests the host posts into pinned (coherent) host memory, so a
+// per-packet call costs no launch.  Slot s belongs to worker s / per_worker.
 // Host -> device: the slot bytes, then the slot's 16-B request record req[s] = {seq (31-bit, +1 per
 // request), op (1 seal, 0 open) | aad_len << 1, len, key_idx} in one aligned 16-B store (one snapshot
-// for the GPU's 16-B read), then bell[0] += 1 (bell[1] = stop).  The dispatcher (one wave) is the only
-// reader of host memory while idle: it polls bell[0] (one 8-B read per poll, s_sleep between polls) and
-// on a change reads every request record (one 16-B load per slot, all in flight together), forwards
-// each new request to device memory and rings its worker's device bell; the worker (polling that bell in L2) serves the slot in place over
-// PCIe and writes done[s] = seq << 1 | verdict into host memory.  Every host-memory access of the kernel
-// is a relaxed system-scope atomic (no cache maintenance).  An instance ends on the host's stop word, or
-// when the dispatcher sees no request for idle_ticks or the instance is life_ticks old (100 MHz clock):
-// it forwards what is pending and raises the device shutdown word, every worker serves what it was given
-// and leaves, and the last workgroup to leave writes *over = gen.
+// for the GPU's 16-B read), then bell[16 w] += 1 for the slot's worker w (bell[16 w + 1] = stop).
+// Device -> host: the slot bytes, then done[s] = seq << 1 | verdict.  Every host-memory access of the
+// kernel goes around the GPU caches (16-B sc0 sc1 buffer accesses, system-scope atomics for the words).
+// An instance ends on the host's stop words, or when worker 0 sees no request served for idle_ticks or
+// the instance is life_ticks old (100 MHz clock): it raises the device shutdown word, every worker
+// serves what its records hold and leaves, and the last one writes *over = gen.
 constexpr uint32_t kResSlotBytes = 16384;  // request slot: [aad 4][payload][tag 16][nonce 12], 16-B rounded
 constexpr uint32_t kResMaxPerWorker = 64;
-constexpr uint32_t kResMaxSlots = 256;     // the dispatcher wave scans 4 slots per lane
-// device control region (zeroed per launch): [0, 64) words (u64 [1] shutdown, [2] workgroups left),
-// then one 64-B line per worker bell, then assigned seq [S] (u32), then the forwarded meta [S] (uint4)
-constexpr uint32_t kResDevBell = 64;
-inline size_t res_dev_bytes(uint32_t workers, uint32_t slots) { return kResDevBell + 64ull * workers + 4ull * slots + 16ull * slots + 16; }
+constexpr size_t kResDevBytes = 64;        // device control words: [0] last activity, [1] shutdown, [2] left
 struct ResArgs {
-    uint32_t *bell;         // host: dispatch: [0] bell, [1] stop; direct: worker w's bell at 16 w, stop at 16 w + 1
+    uint32_t *bell;         // host: worker w's bell at 16 w, stop at 16 w + 1 (a 64-B line each)
     const uint4 *req;       // host: [S] request records
     uint32_t *done;         // host: [S]
     uint32_t *over;         // host: generation of the last instance that ended
     uint8_t *data;          // host: [S][kResSlotBytes]
-    uint8_t *dev;           // device control region (res_dev_bytes), zeroed per launch
-    uint32_t workers, per_worker, gen;
-    uint32_t dispatch;      // 1: a dispatcher workgroup forwards requests; 0: each worker polls its own bell
+    uint8_t *dev;           // device control words (kResDevBytes), zeroed per launch
+    uint32_t workers, per_worker, gen, pad;
     uint64_t idle_ticks, life_ticks;
 };
 hipError_t launch_resident(const Batch &b, const ResArgs &a, hipStream_t s);

@@ -1397,17 +1397,19 @@ __global__ void __launch_bounds__(kOneThreads) gcm_one_kernel(Batch b, const uin
 }
 
 // ---------------------------------------------------------------------------------------------
-// Resident per-packet service (resident.cpp; gcm_internal.h ResArgs has the protocol).  Workgroups
-// 0..workers-1 are workers: each keeps gcm_one_kernel's T-tables in LDS for its whole life (and the
-// comb tables of the key it served last), thread 0 polls the worker's bell in device memory, and on
-// a change wave 0 looks up which of the worker's slots were forwarded to it, then the whole workgroup
-// serves each of them in place in host memory with the latency engine.  Workgroup `workers` is the
-// dispatcher: one wave, the only poller of host memory (a first build polled host memory from every
-// worker: 16 pollers cut a concurrent host batch's PCIe rate from 34 to 3.3 GiB/s).
-constexpr uint32_t kResCtl = (kOneLds + 15u) & ~15u;  // LDS: [0] command, [8,16) pending mask, [16,36) request
-constexpr uint32_t kResDone = kResCtl + 64;           // worker: the done sequence of each of its slots
-constexpr uint32_t kResRec = kResDone + 4 * kResMaxSlots;  // (dispatcher: the forwarded sequence of every slot)
-constexpr uint32_t kResLds = kResRec + 16 * kResMaxPerWorker;  // direct mode: the worker's request records
+// Resident per-packet service (resident.cpp; gcm_internal.h ResArgs has the protocol).  Each
+// workgroup is a worker: it keeps gcm_one_kernel's T-tables in LDS for its whole life (and the comb
+// tables of the key it served last); thread 0 polls the worker's bell word in pinned host memory (one
+// 8-B read per poll, s_sleep between polls, longer sleeps when quiet), and on a change wave 0 reads the
+// worker's request records (one 16-B load per slot, one round trip), then the whole workgroup serves
+// each new request in place in host memory with the latency engine.  Measured against a build where
+// one dispatcher wave polled for all workers and forwarded requests through device memory: 414 K vs
+// 300 K round trips/s from 16 threads, 13.8 vs 19.4 us per call alone, and a host batch alongside kept
+// its PCIe rate either way (profiles/r3_s8/resident_sweep.txt).
+constexpr uint32_t kResCtl = (kOneLds + 15u) & ~15u;  // LDS: [0] command, [8,16) pending mask
+constexpr uint32_t kResDone = kResCtl + 64;           // the done sequence of each of the worker's slots
+constexpr uint32_t kResRec = kResDone + 4 * kResMaxPerWorker;  // the request records being served
+constexpr uint32_t kResLds = kResRec + 16 * kResMaxPerWorker;
 static_assert(kResLds <= 160u * 1024u, "gfx950 LDS is 160 KiB per workgroup");
 
 __device__ __forceinline__ uint32_t ld_sys32(const uint32_t *p) {
@@ -1425,91 +1427,12 @@ __device__ __forceinline__ void st_agent(T *p, T v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-struct ResDev {  // views of the device control region
-    uint64_t *words;    // [1] shutdown, [2] workgroups left
-    uint32_t *wbell;    // worker w's bell at 16 w (one 64-B line each)
-    uint32_t *assigned; // [S] the last sequence forwarded per slot
-    uint32_t *fmeta;    // [S][4] its meta
-};
-__device__ __forceinline__ ResDev res_dev(const ResArgs &a) {
-    const uint32_t S = a.workers * a.per_worker;
-    uint8_t *p = a.dev;
-    return ResDev{reinterpret_cast<uint64_t *>(p), reinterpret_cast<uint32_t *>(p + kResDevBell),
-                  reinterpret_cast<uint32_t *>(p + kResDevBell + 64ull * a.workers),
-                  reinterpret_cast<uint32_t *>(p + ((kResDevBell + 64ull * a.workers + 4ull * S + 15) & ~15ull))};
-}
-
-// The dispatcher's wave: forwards every slot whose host sequence differs from what it last forwarded
-// (meta first, then the sequence, drained, then one bell add per worker that got work).  Returns
-// whether anything was forwarded.  Wave-uniform.
-__device__ __forceinline__ bool res_forward(const ResArgs &a, const ResDev &d, uint32_t lane) {
-    const uint32_t S = a.workers * a.per_worker;
-    // slot 64 k + l is lane l's k-th: every request record in flight together (one PCIe round trip)
-    uint4 m[4];
-#pragma unroll
-    for (uint32_t k = 0; k < 4; ++k) {
-        const uint32_t sl = lane + 64u * k;
-        m[k] = sl < S ? host_ld16(a.req, 16 * S, 16 * sl) : uint4{0, 0, 0, 0};
-    }
-    uint32_t q[4];
-    bool fresh[4];
-    uint32_t any = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < 4; ++k) {
-        const uint32_t sl = lane + 64u * k;
-        q[k] = m[k].x & 0x7fffffffu;
-        fresh[k] = sl < S && q[k] != lds32(kResDone + 4 * sl);
-        if (fresh[k]) {  // forward {op, len, key, aad_len} as the workers read it
-            any |= 1u << (sl / a.per_worker % 32u);
-            st_agent(reinterpret_cast<uint64_t *>(d.fmeta + 4 * sl), (uint64_t)(m[k].y & 1u) | (uint64_t)m[k].z << 32);
-            st_agent(reinterpret_cast<uint64_t *>(d.fmeta + 4 * sl) + 1, (uint64_t)m[k].w | (uint64_t)(m[k].y >> 1) << 32);
-        }
-    }
-    // meta before sequence: the worker reads the meta only after it has seen the sequence
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-    for (uint32_t k = 0; k < 4; ++k) {
-        const uint32_t sl = lane + 64u * k;
-        if (fresh[k]) {
-            st_agent(d.assigned + sl, q[k]);
-            lds_st32(kResDone + 4 * sl, q[k]);
-        }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    // one bell add per worker that got work (workers <= 32 here; more: each slot rings its own)
-    if (a.workers <= 32u) {
-        uint32_t r = any;
-        for (uint32_t off = 32; off > 0; off >>= 1) r |= __shfl_xor(r, off, 64);
-        if (lane < a.workers && ((r >> lane) & 1u))
-            __hip_atomic_fetch_add(d.wbell + 16u * lane, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-#pragma unroll
-        for (uint32_t k = 0; k < 4; ++k)
-            if (fresh[k])
-                __hip_atomic_fetch_add(d.wbell + 16u * ((lane + 64u * k) / a.per_worker), 1u, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-    }
-    return __ballot(fresh[0] || fresh[1] || fresh[2] || fresh[3]) != 0;
-}
-
-// QGCM_RES_TRACE (side builds only, tools/res_trace.py): per request, the 100-MHz clock when the
-// dispatcher read the bell change, when it had forwarded, when the worker saw its bell, when it
-// started and finished the packet, and when it published the verdict.
-#ifdef QGCM_RES_TRACE
-__device__ unsigned long long g_res_trace[1 << 16][8];
-__device__ unsigned int g_res_trace_n;
-__device__ unsigned long long g_res_disp[2];  // dispatcher: last bell-change read, last forward end
-#define RES_TR(x) x
-#else
-#define RES_TR(x)
-#endif
-
 __global__ void __launch_bounds__(kOneThreads) gcm_resident_kernel(Batch b, const uint32_t *__restrict__ rk_table,
                                                                    ResArgs a) {
     const uint32_t tid = threadIdx.x, lane = tid & 63u, w = blockIdx.x;
     const uint32_t S = a.workers * a.per_worker;
-    const ResDev d = res_dev(a);
-    if (!a.dispatch) {  // ---- direct mode: every worker polls its own bell in host memory ----
+    uint64_t *const ctl = reinterpret_cast<uint64_t *>(a.dev);  // [0] last activity, [1] shutdown, [2] left
+    {
         const uint32_t P = a.per_worker, first = w * P;
         one_fill_te(b.te, tid);
         if (tid < P) lds_st32(kResDone + 4 * tid, ld_sys32(a.done + first + tid) >> 1);
@@ -1523,13 +1446,13 @@ __global__ void __launch_bounds__(kOneThreads) gcm_resident_kernel(Batch b, cons
                 uint32_t cmd = 0;
                 if (w == 0) {  // the instance's end: no request for idle_ticks, or life_ticks old
                     const uint64_t now = wall_clock64();
-                    const uint64_t act = ld_agent(d.words);  // last activity of any worker (0: none yet)
+                    const uint64_t act = ld_agent(ctl);  // last activity of any worker (0: none yet)
                     const int64_t quiet = (int64_t)(now - (act > t_start ? act : t_start));
-                    if (quiet > (int64_t)a.idle_ticks || now - t_start > a.life_ticks) st_agent(d.words + 1, (uint64_t)1);
+                    if (quiet > (int64_t)a.idle_ticks || now - t_start > a.life_ticks) st_agent(ctl + 1, (uint64_t)1);
                 }
                 const uint64_t hb = ld_sys64(reinterpret_cast<const uint64_t *>(a.bell + 16u * w));
                 const uint32_t bell = (uint32_t)hb, stop = (uint32_t)(hb >> 32);
-                if (stop || ld_agent(d.words + 1)) {
+                if (stop || ld_agent(ctl + 1)) {
                     cmd = 2;
                 } else if (!scanned || bell != last_bell) {
                     cmd = 1;
@@ -1586,132 +1509,7 @@ __global__ void __launch_bounds__(kOneThreads) gcm_resident_kernel(Batch b, cons
                 if (tid == 0) {
                     __hip_atomic_store(a.done + sl, q << 1 | ok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     lds_st32(kResDone + 4 * j, q);
-                    __hip_atomic_fetch_max(d.words, wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-            }
-            __syncthreads();
-            if (cmd == 2) break;
-        }
-    } else if (w == a.workers) {  // ---- the dispatcher (wave 0 only) ----
-        if (tid < 64) {
-            for (uint32_t sl = lane; sl < S; sl += 64) lds_st32(kResDone + 4 * sl, ld_sys32(a.done + sl) >> 1);
-            const uint64_t t_start = wall_clock64();
-            uint64_t act = t_start;
-            uint32_t last = 0;
-            bool first = true, ending = false;
-            for (;;) {
-                const uint64_t hb = ld_sys64(reinterpret_cast<const uint64_t *>(a.bell));
-                const uint32_t bell = __builtin_amdgcn_readfirstlane((uint32_t)hb);
-                const uint32_t stop = __builtin_amdgcn_readfirstlane((uint32_t)(hb >> 32));
-                const uint64_t now = wall_clock64();
-                if (stop || (int64_t)(now - act) > (int64_t)a.idle_ticks || now - t_start > a.life_ticks)
-                    ending = true;
-                if (first || ending || bell != last) {
-                    last = bell;  // read before the scan: a request posted after it rings again
-                    first = false;
-                    if (res_forward(a, d, lane)) {
-                        act = now;
-                        RES_TR(if (lane == 0) {
-                            st_agent(&g_res_disp[0], (unsigned long long)now);
-                            st_agent(&g_res_disp[1], (unsigned long long)wall_clock64());
-                        })
-                    }
-                }
-                if (ending) break;  // everything posted before the last read of the bell is forwarded
-                __builtin_amdgcn_s_sleep(4);
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (lane == 0) st_agent(d.words + 1, (uint64_t)1);  // shutdown: workers serve what they got, then leave
-        }
-    } else {  // ---- a worker ----
-        const uint32_t P = a.per_worker, first = w * P;
-        one_fill_te(b.te, tid);
-        if (tid < P) lds_st32(kResDone + 4 * tid, ld_sys32(a.done + first + tid) >> 1);
-        uint32_t tab_key = 0xffffffffu, tab_n = 0;
-        uint32_t last_bell = 0;
-        __syncthreads();
-        for (;;) {
-            // 0: idle, 1: serve what was forwarded, 2: serve what was forwarded, then leave
-            if (tid == 0) {
-                uint32_t cmd = 0;
-                const uint32_t bell = ld_agent(d.wbell + 16u * w);
-                if (bell != last_bell) {
-                    cmd = 1;
-                    last_bell = bell;
-                } else if (ld_agent(d.words + 1)) {
-                    cmd = 2;  // the dispatcher forwarded everything before raising shutdown
-                }
-                lds_st32(kResCtl, cmd);
-                if (cmd == 0) __builtin_amdgcn_s_sleep(2);
-            }
-            __syncthreads();
-            const uint32_t cmd = lds32(kResCtl);
-            if (cmd == 0) {
-                __syncthreads();  // every thread has read the command before thread 0 writes the next
-                continue;
-            }
-            RES_TR(const unsigned long long t_seen = wall_clock64();)
-            if (tid < 64) {  // wave 0: which of this worker's slots were forwarded and are not served yet
-                bool pend = false;
-                if (lane < P) {
-                    const uint32_t q = ld_agent(d.assigned + first + lane);
-                    pend = q != 0 && q != lds32(kResDone + 4 * lane);
-                }
-                const uint64_t m = __ballot(pend);
-                if (lane == 0) {
-                    lds_st32(kResCtl + 8, (uint32_t)m);
-                    lds_st32(kResCtl + 12, (uint32_t)(m >> 32));
-                }
-            }
-            __syncthreads();
-            uint64_t mask = lds32(kResCtl + 8) | (uint64_t)lds32(kResCtl + 12) << 32;
-            while (mask) {
-                const uint32_t j = (uint32_t)__builtin_ctzll(mask);
-                mask &= mask - 1;
-                const uint32_t sl = first + j;
-                if (tid == 0) {  // the forwarded sequence, then its meta (stored before it)
-                    const uint32_t q = ld_agent(d.assigned + sl);
-                    const uint64_t *mp = reinterpret_cast<const uint64_t *>(d.fmeta + 4 * sl);
-                    const uint64_t m0 = ld_agent(mp), m1 = ld_agent(mp + 1);
-                    lds_st32(kResCtl + 16, q);
-                    lds_st32(kResCtl + 20, (uint32_t)m0);
-                    lds_st32(kResCtl + 24, (uint32_t)(m0 >> 32));
-                    lds_st32(kResCtl + 28, (uint32_t)m1);
-                    lds_st32(kResCtl + 32, (uint32_t)(m1 >> 32));
-                }
-                __syncthreads();
-                const uint32_t q = lds32(kResCtl + 16), op = lds32(kResCtl + 20), Lin = lds32(kResCtl + 24);
-                const uint32_t key = lds32(kResCtl + 28), aad = lds32(kResCtl + 32);
-                // as gcm_one_kernel: an unset or out-of-range key, an open shorter than the tag or a slot
-                // past its staging area fails the request with the slot untouched
-                const uint64_t stage = (4ull + Lin + (op ? QGCM_OVERHEAD : 0) + 15) & ~15ull;
-                const bool valid = op <= 1u && aad <= 4u && key < b.max_keys && b.key_valid[key] &&
-                                   (op ? Lin < QGCM_MAX_PAYLOAD : Lin >= (uint32_t)QGCM_OVERHEAD) &&
-                                   stage <= kResSlotBytes && stage <= kOneCap - 16;
-                uint32_t ok = 0;
-                uint8_t *slot = a.data + (size_t)sl * kResSlotBytes;
-                RES_TR(const unsigned long long t_pk0 = wall_clock64();)
-                if (valid)
-                    ok = op ? one_packet<true, true>(b, rk_table, slot, Lin, key, aad, nullptr, false, tab_key, tab_n)
-                            : one_packet<false, true>(b, rk_table, slot, Lin, key, aad, nullptr, false, tab_key, tab_n);
-                // every storing wave drains its (write-through) stores, then one lane publishes the verdict
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __syncthreads();
-                if (tid == 0) {
-                    RES_TR(const unsigned long long t_pk1 = wall_clock64();)
-                    __hip_atomic_store(a.done + sl, q << 1 | ok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    lds_st32(kResDone + 4 * j, q);
-                    RES_TR({
-                        const unsigned int k = atomicAdd(&g_res_trace_n, 1u) & 0xffffu;
-                        g_res_trace[k][0] = ld_agent(&g_res_disp[0]);
-                        g_res_trace[k][1] = ld_agent(&g_res_disp[1]);
-                        g_res_trace[k][2] = t_seen;
-                        g_res_trace[k][3] = t_pk0;
-                        g_res_trace[k][4] = t_pk1;
-                        g_res_trace[k][5] = wall_clock64();
-                        g_res_trace[k][6] = sl;
-                        g_res_trace[k][7] = Lin;
-                    })
+                    __hip_atomic_fetch_max(ctl, wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
             }
             __syncthreads();
@@ -1719,31 +1517,18 @@ __global__ void __launch_bounds__(kOneThreads) gcm_resident_kernel(Batch b, cons
         }
     }
     if (tid == 0) {  // the last workgroup to leave tells the host this instance is over
-        const uint64_t n = __hip_atomic_fetch_add(d.words + 2, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (n + 1 == a.workers + (a.dispatch ? 1u : 0u)) {
+        const uint64_t n = __hip_atomic_fetch_add(ctl + 2, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (n + 1 == a.workers) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __hip_atomic_store(a.over, a.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
 }
 
-#ifdef QGCM_RES_TRACE
-extern "C" int qgcm_debug_res_trace(unsigned long long *out, int n) {
-    unsigned int cnt = 0;
-    if (hipMemcpyFromSymbol(&cnt, HIP_SYMBOL(g_res_trace_n), 4) != hipSuccess) return -1;
-    if (cnt > (1u << 16)) cnt = 1u << 16;
-    if ((unsigned)n > cnt) n = (int)cnt;
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_res_trace), (size_t)n * 64) != hipSuccess) return -1;
-    return n;
-}
-#endif
-
 hipError_t launch_resident(const Batch &b, const ResArgs &a, hipStream_t s) {
-    if (a.workers == 0 || a.per_worker == 0 || a.per_worker > kResMaxPerWorker ||
-        a.workers * a.per_worker > kResMaxSlots)
-        return hipErrorInvalidValue;
+    if (a.workers == 0 || a.per_worker == 0 || a.per_worker > kResMaxPerWorker) return hipErrorInvalidValue;
     void *args[] = {const_cast<Batch *>(&b), const_cast<uint32_t **>(&b.rk_table), const_cast<ResArgs *>(&a)};
-    return hipLaunchKernel(reinterpret_cast<const void *>(&gcm_resident_kernel), dim3(a.workers + (a.dispatch ? 1 : 0)),
+    return hipLaunchKernel(reinterpret_cast<const void *>(&gcm_resident_kernel), dim3(a.workers),
                            dim3(kOneThreads), args, kResLds, s);
 }
 

@@ -2,12 +2,12 @@
 // plugin/encryption.go Apply from each of quantum's 2 x NumWorkers goroutines, worker/outgoing.go:83-93,
 // worker/incoming.go:82-92) without a kernel launch per call.
 //
-// A resident kernel (gcm_kernels.hip gcm_resident_kernel) keeps `workers` workgroups and a dispatcher
-// on the GPU; each worker owns `per_worker` request slots in one pinned, coherent host region.  A call
-// copies its packet into a free slot of the least-loaded worker, writes the request's meta and
-// sequence number, rings the bell and spins on the slot's done word; the dispatcher forwards the
-// request to the worker, which seals or opens the slot in place over PCIe and publishes the verdict.
-// No hipLaunch, no stream and no hardware queue per call.
+// A resident kernel (gcm_kernels.hip gcm_resident_kernel) keeps `workers` workgroups on the GPU; each
+// owns `per_worker` request slots in one pinned, coherent host region.  A call copies its packet into
+// a free slot of the least-loaded worker, writes the slot's 16-B request record, rings the worker's
+// bell and waits on the slot's done word (spinning, then asleep on a futex that a completion thread
+// wakes); the worker seals or opens the slot in place over PCIe and publishes the verdict.  No
+// hipLaunch, no stream and no hardware queue per call.
 //
 // Lifetime: an instance ends by itself when it has seen no request for QGCM_RESIDENT_IDLE_US or is
 // QGCM_RESIDENT_LIFE_US old (so work queued behind it on a shared hardware queue, or a
@@ -46,8 +46,7 @@ struct Resident {
     uint32_t *bell = nullptr, *done = nullptr, *over = nullptr;
     uint4 *req = nullptr;
     uint8_t *data = nullptr;
-    uint8_t *d_ctl = nullptr;  // device control region (res_dev_bytes)
-    size_t ctl_bytes = 0;
+    uint8_t *d_ctl = nullptr;  // device control words (kResDevBytes)
     hipStream_t stream = nullptr;
     std::unique_ptr<uint32_t[]> seqh;                  // last sequence per slot (owned by the slot holder)
     std::unique_ptr<std::atomic<uint32_t>[]> busy;     // slot taken
@@ -57,7 +56,6 @@ struct Resident {
     std::atomic<uint32_t> gen{0};  // generation of the current (or last) instance; 0 = never launched
     std::atomic<bool> broken{false};
     std::atomic<uint64_t> served{0}, launches{0};
-    bool dispatch = true;  // QGCM_RESIDENT_DISPATCH: one dispatcher polls host memory (1) or every worker (0)
     // callers that stop spinning sleep on a futex; one completion thread watches their done words
     uint64_t spin_ns = 20000;                           // QGCM_RESIDENT_SPIN_US
     std::unique_ptr<std::atomic<uint32_t>[]> want;      // per slot: the sequence a sleeping caller waits for
@@ -100,9 +98,8 @@ int relaunch(Resident *r, uint32_t g) {
     a.per_worker = r->P;
     a.gen = g + 1;
     a.idle_ticks = r->idle_ticks;
-    a.dispatch = r->dispatch ? 1u : 0u;
     a.life_ticks = r->life_ticks;
-    if (hipMemsetAsync(r->d_ctl, 0, r->ctl_bytes, r->stream) != hipSuccess ||
+    if (hipMemsetAsync(r->d_ctl, 0, kResDevBytes, r->stream) != hipSuccess ||
         launch_resident(r->base, a, r->stream) != hipSuccess) {
         r->broken = true;
         return QGCM_E_HIP;
@@ -144,12 +141,9 @@ Resident *resident_create(int device, const Batch &base, int num_cus) {
     r->base = base;
     r->W = (uint32_t)env_u64("QGCM_RESIDENT_WORKERS", 16);
     r->P = (uint32_t)env_u64("QGCM_RESIDENT_SLOTS", 16);
-    if (r->W < 1 || (int)r->W > num_cus / 2 || r->P < 1 || r->P > kResMaxPerWorker || r->W * r->P > kResMaxSlots)
-        return nullptr;
+    if (r->W < 1 || (int)r->W > num_cus / 2 || r->P < 1 || r->P > kResMaxPerWorker) return nullptr;
     r->S = r->W * r->P;
-    r->ctl_bytes = res_dev_bytes(r->W, r->S);
     r->spin_ns = env_u64("QGCM_RESIDENT_SPIN_US", 20) * 1000;
-    r->dispatch = env_u64("QGCM_RESIDENT_DISPATCH", 1) != 0;
     r->idle_ticks = env_u64("QGCM_RESIDENT_IDLE_US", 2000) * 100;  // s_memrealtime: 100 MHz
     r->life_ticks = env_u64("QGCM_RESIDENT_LIFE_US", 8000) * 100;
     // host region: bells (a 64-B line per worker: bell, stop), done, over, the request records, then the slots
@@ -175,7 +169,7 @@ Resident *resident_create(int device, const Batch &base, int num_cus) {
     for (uint32_t i = 0; i < r->S; ++i) r->want[i] = r->wake[i] = 0;
     int lo = 0, hi = 0;
     if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) hi = 0;
-    if (hipMalloc(reinterpret_cast<void **>(&r->d_ctl), r->ctl_bytes) != hipSuccess ||
+    if (hipMalloc(reinterpret_cast<void **>(&r->d_ctl), kResDevBytes) != hipSuccess ||
         hipStreamCreateWithPriority(&r->stream, hipStreamNonBlocking, hi) != hipSuccess) {
         resident_destroy(r.release());
         return nullptr;
@@ -283,7 +277,7 @@ long resident_call(Resident *r, bool seal, uint32_t key, uint8_t *data, long len
     std::atomic_thread_fence(std::memory_order_release);
     _mm_store_si128(reinterpret_cast<__m128i *>(&r->req[s]),
                     _mm_set_epi32((int)key, (int)len, (int)((seal ? 1u : 0u) | aad_len << 1), (int)q));
-    __atomic_fetch_add(&r->bell[r->dispatch ? 0 : 16 * w], 1u, __ATOMIC_SEQ_CST);
+    __atomic_fetch_add(&r->bell[16 * w], 1u, __ATOMIC_SEQ_CST);
     long rc = 0;
     uint32_t g = r->gen.load(std::memory_order_acquire);
     if (instance_over(r, g) && relaunch(r, g) != QGCM_OK) return -1;  // broken: the slot stays taken

@@ -13,13 +13,10 @@ run() {  # label, env..., then -- threads payload bulk mode
   local rc=$?
   if [ $rc -ge 124 ]; then echo "stop rc=$rc" >> $OUT/sweep.txt; exit $rc; fi
 }
-for mode in 1 0; do
-  run t1_d$mode QGCM_RESIDENT_DISPATCH=$mode -- 1 1350 0 resident
-  run t16_d$mode QGCM_RESIDENT_DISPATCH=$mode -- 16 1350 0 resident
-  run t64_d$mode QGCM_RESIDENT_DISPATCH=$mode -- 64 1350 0 resident
-  run t256_d$mode QGCM_RESIDENT_DISPATCH=$mode -- 256 1350 0 resident
-  run bulk16_d$mode QGCM_RESIDENT_DISPATCH=$mode -- 16 1350 1 resident
+for t in 1 4 16 64 256; do
+  run t$t X=1 -- $t 1350 0 resident
 done
+run bulk16 X=1 -- 16 1350 1 resident
 run p64 X=1 -- 1 64 0 resident
 run p9000 X=1 -- 1 9000 0 resident
 run launch16 X=1 -- 16 1350 1 launch
