@@ -1056,9 +1056,11 @@ extern "C" int qgcm_debug_seg_stats(unsigned long long *out, int n, int reset) {
 //     value), then Y = S H^2 + [len(A)]||[len(C)] H -- 2 + 7 serial multiplies at 1350 B where the
 //     quad chains took 23, 16 at 9000 B where they took 142.  The seven comb tables (H^(2^l),
 //     l = 0..6) sit in LDS;
-//  4. writes the slot back with one wave of 16-B stores.
-// Open computes GHASH over the staged ciphertext first and decrypts only when the tag matches
-// (zeroed plaintext otherwise, as Go 1.9 Open).
+//  4. writes the slot back with 16-B stores.
+// The write-back overlaps GHASH: a seal's waves 1-3 store the ciphertext rows before the tag while
+// wave 0 hashes; an open's waves 1-3 run the counter blocks and store the plaintext straight from
+// registers while wave 0 hashes the staged ciphertext, and on a tag mismatch (rare) the payload is
+// overwritten with zeros once those stores have landed (as Go 1.9 Open: zeroed plaintext).
 // LDS: [0, 64K) Te, [64K, 120K) comb tables of H^(2^l), [120K, 120K + kOneCap) the slot at +12
 // (payload 16-B aligned), then 64 B of scratch (E_K(J0), the GHASH value).
 constexpr uint32_t kOneThreads = 256;
@@ -1122,6 +1124,13 @@ __device__ __forceinline__ void slot_st16(uint8_t *slot, uint32_t i, uint4 v) {
         return;
     }
     reinterpret_cast<uint4 *>(slot)[i] = v;
+}
+// 16 B at a 4-B aligned byte offset of the slot (an open's plaintext block j at 4 + 16 j)
+template <bool kSys>
+__device__ __forceinline__ void slot_st16_at(uint8_t *slot, uint32_t off, uint4 v) {
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc(slot, 0, (int)(kSys ? kResSlotBytes : kOneCap), 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(u32x4{v.x, v.y, v.z, v.w}, r, (int)off, 0, kSys ? kSc0Sc1 : 0);
 }
 
 // Fills the replicated T-tables (64 KiB at LDS 0): loads first, stores after (one memory latency).
@@ -1229,12 +1238,9 @@ __device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_t
     uint32_t m0, m1, m2, m3;
     block_mask(r, m0, m1, m2, m3);
 
-    // 2. counter blocks: block j < d XORs its keystream into the staged payload; block d is E_K(J0)
-    // mode 0: payload blocks and J0; 1: payload blocks only; 2: J0 only (thread 64, wave 1)
-    auto ctr_pass = [&](int mode) {
-        const uint32_t j_first = mode == 2 ? (tid == 64 ? d : d + 1) : tid;
-        const uint32_t j_end = mode == 1 ? d : d + 1;
-        for (uint32_t j = j_first; j < j_end; j += kOneThreads) {
+    // 2. (seal) counter blocks: block j < d XORs its keystream into the staged payload; block d is E_K(J0)
+    auto ctr_pass = [&]() {
+        for (uint32_t j = tid; j <= d; j += kOneThreads) {
             const uint32_t ctr = j == d ? 1u : j + 2u;  // J0, or inc32(J0) + j
             Ctr cc;
             ctr_setup(cc, n0, n1, n2, ctr >> 8, kk, lb);
@@ -1306,11 +1312,19 @@ __device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_t
         }
     };
 
+    auto row = [&](uint32_t i) {
+        const uint32_t a = A + 16 * i;
+        return uint4{lds32(a), lds32(a + 4), lds32(a + 8), lds32(a + 12)};
+    };
     uint32_t ok = 1;
     if (kSeal) {
-        ctr_pass(0);
+        ctr_pass();
         __syncthreads();
-        ghash();
+        const uint32_t early = (4u + L) >> 4;  // slot rows that end before the tag
+        if (tid < 64)
+            ghash();
+        else
+            for (uint32_t i = tid - 64; i < early; i += kOneThreads - 64) slot_st16<kSys>(slot, i, row(i));
         __syncthreads();
         if (tid == 0) {
             const uint4 e = lds128(kOneScratch), y = lds128(kOneScratch + 16);
@@ -1324,28 +1338,46 @@ __device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_t
                 lds_st32u(P + L + 24, n2);
             }
         }
+        __syncthreads();
+        for (uint32_t i = early + tid; i < n16; i += kOneThreads) slot_st16<kSys>(slot, i, row(i));
     } else {
-        ghash();
-        ctr_pass(2);  // E_K(J0) on wave 1 while wave 0 hashes
+        if (tid < 64) {
+            ghash();
+        } else {  // counter blocks (block d = E_K(J0)); the plaintext goes out while wave 0 hashes
+            for (uint32_t j = tid - 64; j <= d; j += kOneThreads - 64) {
+                const uint32_t ctr = j == d ? 1u : j + 2u;
+                Ctr cc;
+                ctr_setup(cc, n0, n1, n2, ctr >> 8, kk, lb);
+                uint32_t k0, k1, k2, k3;
+                ctr_block(cc, ctr & 0xffu, kk, lb, k0, k1, k2, k3);
+                if (j == d) {
+                    lds_st128(kOneScratch, uint4{k0, k1, k2, k3});
+                } else {
+                    if (j == nfull) {  // partial block: the tag bytes after it are rewritten unchanged
+                        k0 &= m0;
+                        k1 &= m1;
+                        k2 &= m2;
+                        k3 &= m3;
+                    }
+                    const uint4 in = lds128(P + 16 * j);
+                    slot_st16_at<kSys>(slot, 4 + 16 * j, uint4{in.x ^ k0, in.y ^ k1, in.z ^ k2, in.w ^ k3});
+                }
+            }
+        }
         __syncthreads();
         const uint4 e = lds128(kOneScratch), y = lds128(kOneScratch + 16);
         ok = ((e.x ^ y.x ^ lds32u(P + L)) | (e.y ^ y.y ^ lds32u(P + L + 4)) | (e.z ^ y.z ^ lds32u(P + L + 8)) |
               (e.w ^ y.w ^ lds32u(P + L + 12))) == 0;
-        if (ok) {
-            ctr_pass(1);
-        } else {  // Go 1.9 crypto/cipher gcm Open: zero the would-be plaintext on tag mismatch
+        if (!ok) {  // Go 1.9 crypto/cipher gcm Open: zero the would-be plaintext on tag mismatch
             for (uint32_t j = tid; j < d; j += kOneThreads) {
                 const uint4 in = lds128(P + 16 * j);
                 const uint4 z = j == nfull ? uint4{in.x & ~m0, in.y & ~m1, in.z & ~m2, in.w & ~m3} : uint4{0, 0, 0, 0};
                 lds_st128(P + 16 * j, z);
             }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the plaintext stores have landed
+            __syncthreads();
+            for (uint32_t j = tid; j < d; j += kOneThreads) slot_st16_at<kSys>(slot, 4 + 16 * j, lds128(P + 16 * j));
         }
-    }
-    __syncthreads();
-    // 4. write the slot back (the bytes outside the payload/tag are rewritten unchanged)
-    for (uint32_t i = tid; i < n16; i += kOneThreads) {
-        const uint32_t a = A + 16 * i;
-        slot_st16<kSys>(slot, i, uint4{lds32(a), lds32(a + 4), lds32(a + 8), lds32(a + 12)});
     }
     return ok;
 }
@@ -1399,10 +1431,10 @@ __global__ void __launch_bounds__(kOneThreads) gcm_one_kernel(Batch b, const uin
 // ---------------------------------------------------------------------------------------------
 // Resident per-packet service (resident.cpp; gcm_internal.h ResArgs has the protocol).  Each
 // workgroup is a worker: it keeps gcm_one_kernel's T-tables in LDS for its whole life (and the comb
-// tables of the key it served last); thread 0 polls the worker's bell word in pinned host memory (one
-// 8-B read per poll, s_sleep between polls, longer sleeps when quiet), and on a change wave 0 reads the
-// worker's request records (one 16-B load per slot, one round trip), then the whole workgroup serves
-// each new request in place in host memory with the latency engine.  Measured against a build where
+// tables of the key it served last); wave 0 polls the worker's request records in pinned host memory
+// (one 16-B load per slot, one round trip per poll; only the bell word once it has been quiet for a
+// while), and the whole workgroup serves each new request in place in host memory with the latency
+// engine.  Measured against a build where
 // one dispatcher wave polled for all workers and forwarded requests through device memory: 414 K vs
 // 300 K round trips/s from 16 threads, 13.8 vs 19.4 us per call alone, and a host batch alongside kept
 // its PCIe rate either way (profiles/r3_s8/resident_sweep.txt).
@@ -1430,91 +1462,104 @@ __device__ __forceinline__ void st_agent(T *p, T v) {
 __global__ void __launch_bounds__(kOneThreads) gcm_resident_kernel(Batch b, const uint32_t *__restrict__ rk_table,
                                                                    ResArgs a) {
     const uint32_t tid = threadIdx.x, lane = tid & 63u, w = blockIdx.x;
-    const uint32_t S = a.workers * a.per_worker;
+    const uint32_t S = a.workers * a.per_worker, P = a.per_worker, first = w * P;
     uint64_t *const ctl = reinterpret_cast<uint64_t *>(a.dev);  // [0] last activity, [1] shutdown, [2] left
-    {
-        const uint32_t P = a.per_worker, first = w * P;
-        one_fill_te(b.te, tid);
-        if (tid < P) lds_st32(kResDone + 4 * tid, ld_sys32(a.done + first + tid) >> 1);
-        uint32_t tab_key = 0xffffffffu, tab_n = 0, last_bell = 0, idle = 0;
-        bool scanned = false;
-        const uint64_t t_start = wall_clock64();
-        __syncthreads();
-        for (;;) {
-            // 0: idle, 1: scan and serve, 2: scan and serve, then leave
-            if (tid == 0) {
-                uint32_t cmd = 0;
-                if (w == 0) {  // the instance's end: no request for idle_ticks, or life_ticks old
-                    const uint64_t now = wall_clock64();
-                    const uint64_t act = ld_agent(ctl);  // last activity of any worker (0: none yet)
-                    const int64_t quiet = (int64_t)(now - (act > t_start ? act : t_start));
-                    if (quiet > (int64_t)a.idle_ticks || now - t_start > a.life_ticks) st_agent(ctl + 1, (uint64_t)1);
-                }
-                const uint64_t hb = ld_sys64(reinterpret_cast<const uint64_t *>(a.bell + 16u * w));
-                const uint32_t bell = (uint32_t)hb, stop = (uint32_t)(hb >> 32);
-                if (stop || ld_agent(ctl + 1)) {
-                    cmd = 2;
-                } else if (!scanned || bell != last_bell) {
-                    cmd = 1;
-                    last_bell = bell;  // read before the scan: a request posted after it rings again
-                    scanned = true;
-                }
-                lds_st32(kResCtl, cmd);
-                idle = cmd ? 0 : idle + 1;
-                if (cmd == 0) {  // back off when quiet: fewer PCIe reads next to bulk traffic
-                    if (idle < 256)
-                        __builtin_amdgcn_s_sleep(2);
-                    else
-                        __builtin_amdgcn_s_sleep(32);
-                }
-            }
-            __syncthreads();
-            const uint32_t cmd = lds32(kResCtl);
-            if (cmd == 0) {
-                __syncthreads();  // every thread has read the command before thread 0 writes the next
-                continue;
-            }
-            if (tid < 64) {  // wave 0: this worker's request records (one 16-B load per slot, one round trip)
+    one_fill_te(b.te, tid);
+    if (tid < P) lds_st32(kResDone + 4 * tid, ld_sys32(a.done + first + tid) >> 1);
+    uint32_t tab_key = 0xffffffffu, tab_n = 0;
+    // wave 0's poll state (wave-uniform)
+    uint32_t idle = 0, last_bell = 0;
+    bool quiet = false, force = false;
+    const uint64_t t_start = wall_clock64();
+    __syncthreads();
+    for (;;) {
+        if (tid < 64) {
+            // One poll.  Active: every slot's request record and the bell line (bell, stop) in one round
+            // trip.  Quiet (after 256 empty polls): the bell line alone, and the records only once the
+            // bell has moved -- read after the bell value has arrived, so a request whose bell increment
+            // the poll missed rings it again later, and one it saw has its record in place (the host
+            // writes the record before the bell).
+            uint4 bl = {0, 0, 0, 0};
+            if (lane == 0) bl = host_ld16(a.bell, 64u * a.workers, 64u * w);
+            auto read_records = [&]() {
                 bool pend = false;
                 if (lane < P) {
                     const uint4 m = host_ld16(a.req, 16 * S, 16 * (first + lane));
                     pend = (m.x & 0x7fffffffu) != lds32(kResDone + 4 * lane);
                     if (pend) lds_st128(kResRec + 16 * lane, m);
                 }
-                const uint64_t m = __ballot(pend);
-                if (lane == 0) {
-                    lds_st32(kResCtl + 8, (uint32_t)m);
-                    lds_st32(kResCtl + 12, (uint32_t)(m >> 32));
+                return __ballot(pend);
+            };
+            uint64_t pm = quiet ? 0ull : read_records();
+            uint32_t stop = 0;
+            if (lane == 0) {
+                stop = bl.y;
+                if (w == 0) {  // the instance's end: no request for idle_ticks, or life_ticks old
+                    const uint64_t now = wall_clock64();
+                    const uint64_t act = ld_agent(ctl);  // last activity of any worker (0: none yet)
+                    const int64_t q = (int64_t)(now - (act > t_start ? act : t_start));
+                    if (q > (int64_t)a.idle_ticks || now - t_start > a.life_ticks) st_agent(ctl + 1, (uint64_t)1);
                 }
+                stop |= ld_agent(ctl + 1) != 0 ? 1u : 0u;
             }
-            __syncthreads();
-            uint64_t mask = lds32(kResCtl + 8) | (uint64_t)lds32(kResCtl + 12) << 32;
-            while (mask) {
-                const uint32_t j = (uint32_t)__builtin_ctzll(mask);
-                mask &= mask - 1;
-                const uint32_t sl = first + j;
-                const uint4 m = lds128(kResRec + 16 * j);
-                const uint32_t q = m.x & 0x7fffffffu, op = m.y & 1u, aad = m.y >> 1, Lin = m.z, key = m.w;
-                const uint64_t stage = (4ull + Lin + (op ? QGCM_OVERHEAD : 0) + 15) & ~15ull;
-                const bool valid = aad <= 4u && key < b.max_keys && b.key_valid[key] &&
-                                   (op ? Lin < QGCM_MAX_PAYLOAD : Lin >= (uint32_t)QGCM_OVERHEAD) &&
-                                   stage <= kResSlotBytes && stage <= kOneCap - 16;
-                uint32_t ok = 0;
-                uint8_t *slot = a.data + (size_t)sl * kResSlotBytes;
-                if (valid)
-                    ok = op ? one_packet<true, true>(b, rk_table, slot, Lin, key, aad, nullptr, false, tab_key, tab_n)
-                            : one_packet<false, true>(b, rk_table, slot, Lin, key, aad, nullptr, false, tab_key, tab_n);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __syncthreads();
-                if (tid == 0) {
-                    __hip_atomic_store(a.done + sl, q << 1 | ok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    lds_st32(kResDone + 4 * j, q);
-                    __hip_atomic_fetch_max(ctl, wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t bell = __builtin_amdgcn_readfirstlane(bl.x);
+            stop = __builtin_amdgcn_readfirstlane(stop);
+            if (quiet && (force || bell != last_bell)) {
+                pm = read_records();
+                force = false;
+            }
+            last_bell = bell;
+            if (pm) {
+                idle = 0;
+                quiet = false;
+            } else if (!stop) {
+                if (++idle == 256) {
+                    quiet = true;
+                    force = true;  // one more record read after the next bell read
                 }
+                if (quiet)
+                    __builtin_amdgcn_s_sleep(32);
+                else
+                    __builtin_amdgcn_s_sleep(2);
             }
-            __syncthreads();
-            if (cmd == 2) break;
+            if (lane == 0) {
+                lds_st32(kResCtl, stop ? 2u : pm ? 1u : 0u);
+                lds_st32(kResCtl + 8, (uint32_t)pm);
+                lds_st32(kResCtl + 12, (uint32_t)(pm >> 32));
+            }
         }
+        __syncthreads();
+        const uint32_t cmd = lds32(kResCtl);  // 0: nothing to do, 1: serve, 2: serve, then leave
+        uint64_t mask = lds32(kResCtl + 8) | (uint64_t)lds32(kResCtl + 12) << 32;
+        if (cmd == 0) {
+            __syncthreads();  // every thread has read the command before wave 0 writes the next
+            continue;
+        }
+        while (mask) {
+            const uint32_t j = (uint32_t)__builtin_ctzll(mask);
+            mask &= mask - 1;
+            const uint32_t sl = first + j;
+            const uint4 m = lds128(kResRec + 16 * j);
+            const uint32_t q = m.x & 0x7fffffffu, op = m.y & 1u, aad = m.y >> 1, Lin = m.z, key = m.w;
+            const uint64_t stage = (4ull + Lin + (op ? QGCM_OVERHEAD : 0) + 15) & ~15ull;
+            const bool valid = aad <= 4u && key < b.max_keys && b.key_valid[key] &&
+                               (op ? Lin < QGCM_MAX_PAYLOAD : Lin >= (uint32_t)QGCM_OVERHEAD) &&
+                               stage <= kResSlotBytes && stage <= kOneCap - 16;
+            uint32_t ok = 0;
+            uint8_t *slot = a.data + (size_t)sl * kResSlotBytes;
+            if (valid)
+                ok = op ? one_packet<true, true>(b, rk_table, slot, Lin, key, aad, nullptr, false, tab_key, tab_n)
+                        : one_packet<false, true>(b, rk_table, slot, Lin, key, aad, nullptr, false, tab_key, tab_n);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the slot's bytes have reached the host
+            __syncthreads();
+            if (tid == 0) {
+                __hip_atomic_store(a.done + sl, q << 1 | ok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                lds_st32(kResDone + 4 * j, q);
+                __hip_atomic_fetch_max(ctl, wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        __syncthreads();
+        if (cmd == 2) break;
     }
     if (tid == 0) {  // the last workgroup to leave tells the host this instance is over
         const uint64_t n = __hip_atomic_fetch_add(ctl + 2, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
