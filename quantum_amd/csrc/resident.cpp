@@ -23,10 +23,12 @@
 #include <time.h>
 #include <unistd.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <sys/random.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <memory>
@@ -58,6 +60,8 @@ struct Resident {
     std::atomic<uint64_t> served{0}, launches{0};
     // callers that stop spinning sleep on a futex; one completion thread watches their done words
     uint64_t spin_ns = 20000;                           // QGCM_RESIDENT_SPIN_US
+    int32_t max_spinners = 8;                           // QGCM_RESIDENT_SPINNERS (default: half the CPU share)
+    std::atomic<int32_t> spinners{0};                   // callers spinning now
     std::unique_ptr<std::atomic<uint32_t>[]> want;      // per slot: the sequence a sleeping caller waits for
     std::unique_ptr<std::atomic<uint32_t>[]> wake;      // per slot futex word
     std::atomic<uint32_t> sleepers{0};                  // futex word of the completion thread
@@ -75,6 +79,24 @@ long futex(std::atomic<uint32_t> *w, int op, uint32_t val, const struct timespec
 uint64_t env_u64(const char *name, uint64_t dflt) {
     const char *v = getenv(name);
     return v && *v ? strtoull(v, nullptr, 10) : dflt;
+}
+
+// CPUs this process may use: the affinity mask, capped by a cgroup-v2 CPU quota (the GPU boxes give
+// a job 16 CPUs of a 256-CPU host by quota, with all 256 in the mask).
+int cpu_share() {
+    cpu_set_t set;
+    int n = sched_getaffinity(0, sizeof(set), &set) == 0 ? CPU_COUNT(&set) : 1;
+    if (FILE *f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+        char q[32] = {0};
+        unsigned long period = 0;
+        if (fscanf(f, "%31s %lu", q, &period) == 2 && strcmp(q, "max") != 0 && period) {
+            const unsigned long quota = strtoul(q, nullptr, 10);
+            const int c = (int)((quota + period - 1) / period);
+            if (c >= 1 && c < n) n = c;
+        }
+        fclose(f);
+    }
+    return n < 1 ? 1 : n;
 }
 
 // Launches instance g + 1 if instance g (0: none yet) has ended and nobody has launched since.
@@ -144,6 +166,9 @@ Resident *resident_create(int device, const Batch &base, int num_cus) {
     if (r->W < 1 || (int)r->W > num_cus / 2 || r->P < 1 || r->P > kResMaxPerWorker) return nullptr;
     r->S = r->W * r->P;
     r->spin_ns = env_u64("QGCM_RESIDENT_SPIN_US", 20) * 1000;
+    // callers beyond this many sleep at once instead of spinning: with many more callers than CPUs,
+    // spinning ones take the CPUs that posting callers, the completion thread and other host work need
+    r->max_spinners = (int32_t)env_u64("QGCM_RESIDENT_SPINNERS", (uint64_t)std::max(1, cpu_share() / 2));
     r->idle_ticks = env_u64("QGCM_RESIDENT_IDLE_US", 2000) * 100;  // s_memrealtime: 100 MHz
     r->life_ticks = env_u64("QGCM_RESIDENT_LIFE_US", 8000) * 100;
     // host region: bells (a 64-B line per worker: bell, stop), done, over, the request records, then the slots
@@ -284,10 +309,13 @@ long resident_call(Resident *r, bool seal, uint32_t key, uint8_t *data, long len
     uint32_t v = 0;
     const auto t0 = std::chrono::steady_clock::now();
     bool asleep = false;
+    bool spinning = r->spinners.fetch_add(1, std::memory_order_relaxed) < r->max_spinners;
+    if (!spinning) r->spinners.fetch_sub(1, std::memory_order_relaxed);
+    const uint64_t spin_ns = spinning ? r->spin_ns : 0;
     for (uint32_t spins = 0;; ++spins) {
         v = __atomic_load_n(&r->done[s], __ATOMIC_ACQUIRE);
         if ((v >> 1) == q) break;
-        if ((spins & 63) == 63 || asleep) {
+        if ((spins & 63) == 63 || asleep || spin_ns == 0) {
             g = r->gen.load(std::memory_order_acquire);
             // the instance ended with this request still pending: launch the next one
             if (instance_over(r, g) && relaunch(r, g) != QGCM_OK) return -1;  // broken: the slot stays taken
@@ -298,7 +326,11 @@ long resident_call(Resident *r, bool seal, uint32_t key, uint8_t *data, long len
             }
             // past the spin budget: sleep until the completion thread sees the verdict (with many more
             // callers than CPUs, spinning ones would take the CPUs the posting ones need)
-            if (!asleep && (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(waited).count() > r->spin_ns) {
+            if (!asleep && (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(waited).count() >= spin_ns) {
+                if (spinning) {
+                    r->spinners.fetch_sub(1, std::memory_order_relaxed);
+                    spinning = false;
+                }
                 if (!r->waker.joinable()) {
                     std::lock_guard<std::mutex> lk(r->waker_mu);
                     if (!r->waker.joinable()) r->waker = std::thread(waker_loop, r);
@@ -321,6 +353,7 @@ long resident_call(Resident *r, bool seal, uint32_t key, uint8_t *data, long len
         r->want[s].store(0, std::memory_order_relaxed);
         r->sleepers.fetch_sub(1);
     }
+    if (spinning) r->spinners.fetch_sub(1, std::memory_order_relaxed);
     r->served.fetch_add(1, std::memory_order_relaxed);
     if (seal) {
         rc = -1;

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Resident per-packet kernel experiments (tools/bin/per_packet_bench): thread counts, next to a bulk
-# host batch, hardware-queue count and lifetime knobs.
+# host batch, worker count and spinner cap, payload sizes.
 set -u
 OUT=gpurun_out/${1:-exp_res}
 mkdir -p $OUT
@@ -17,6 +17,11 @@ for t in 1 4 16 64 256; do
   run t$t X=1 -- $t 1350 0 resident
 done
 run bulk16 X=1 -- 16 1350 1 resident
+run bulk64 X=1 -- 64 1350 1 resident
+run t64_w32 QGCM_RESIDENT_WORKERS=32 -- 64 1350 0 resident
+run t256_w64 QGCM_RESIDENT_WORKERS=64 QGCM_RESIDENT_SLOTS=8 -- 256 1350 0 resident
+run t64_spin64 QGCM_RESIDENT_SPINNERS=64 -- 64 1350 0 resident
+run t16_spin2 QGCM_RESIDENT_SPINNERS=2 -- 16 1350 0 resident
 run p64 X=1 -- 1 64 0 resident
 run p9000 X=1 -- 1 9000 0 resident
 run launch16 X=1 -- 16 1350 1 launch

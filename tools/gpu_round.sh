@@ -3,7 +3,7 @@
 # reference build, and the config-2 profile (trace + PMC).  Every GPU step has its own time limit;
 # the script stops at the first step that faults, aborts or times out (a plain test failure goes on).
 # Usage: bash tools/gpu_round.sh <tag> [steps...]
-#   steps: rtests tests smoke bench ab prof pp prof3 (default: tests smoke bench ab prof)
+#   steps: rtests tests smoke bench ab prof pp prof3 exp_res align (default: tests smoke bench ab prof)
 set -u
 TAG=$1; shift
 STEPS=${*:-"tests smoke bench ab prof"}
@@ -50,6 +50,20 @@ for s in $STEPS; do
     prof3)
       bash tools/profile_config3.sh $TAG > $OUT/profile3.log 2>&1
       check prof3 $? ;;
+    exp_res)
+      timeout -k 10 600 bash tools/exp_resident.sh $TAG
+      check exp_res $? ;;
+    align)  # config 3 packed vs 64-B aligned payloads: time, then WRITE_SIZE / FETCH_SIZE per layout
+      timeout -k 10 300 python3 tools/exp_config3_align.py 9 > $OUT/align.json 2> $OUT/align.err
+      check align $?
+      for form in packed aligned; do
+        for c in WRITE_SIZE FETCH_SIZE; do
+          timeout -k 10 300 rocprofv3 --pmc $c -d $OUT/pmc_${form}_$c -o $c --output-format csv -- python3 tools/exp_config3_align.py 2 $form > $OUT/pmc_${form}_$c.log 2>&1
+          check pmc_${form}_$c $?
+        done
+        mkdir -p $OUT/pmc_$form && cp -r $OUT/pmc_${form}_*/* $OUT/pmc_$form/ 2>/dev/null
+        python3 tools/pmc_config3.py $OUT/pmc_$form > $OUT/traffic_$form.txt 2>&1
+      done ;;
   esac
 done
 echo all done | tee -a $OUT/steps.txt
