@@ -151,7 +151,7 @@ void waker_loop(Resident *r) {
         }
         const uint32_t g = r->gen.load(std::memory_order_acquire);
         if (instance_over(r, g)) relaunch(r, g);
-        for (int i = 0; i < 32; ++i) _mm_pause();
+        sched_yield();  // hand the CPU to a runnable caller when the job's CPUs are all busy
     }
 }
 

@@ -8,6 +8,7 @@
 //        -Wl,-rpath,$PWD/quantum_amd -o gpurun_out/per_packet_bench
 // Usage: per_packet_bench [threads=64] [payload=1350] [seconds=2] [bulk=0] [mode=both|resident|launch]
 #include <qgcm.h>
+#include <sys/resource.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -35,6 +36,29 @@ static qgcm_ctx *make_ctx(bool resident) {
     if (qgcm_derive_key((const uint8_t *)secret, 32, salt, 32, key) != QGCM_OK || qgcm_set_key(ctx, 0, key) != QGCM_OK)
         exit(1);
     return ctx;
+}
+
+// cgroup-v2 CPU throttling of this job (a CPU quota throttles the whole process once the period's
+// budget is spent; spinning callers spend it) and the process's CPU time
+struct CpuStat {
+    unsigned long long nr_throttled = 0, throttled_usec = 0;
+    double cpu_s = 0;
+};
+static CpuStat cpu_stat() {
+    CpuStat c;
+    if (FILE *f = fopen("/sys/fs/cgroup/cpu.stat", "r")) {
+        char k[64];
+        unsigned long long v;
+        while (fscanf(f, "%63s %llu", k, &v) == 2) {
+            if (!strcmp(k, "nr_throttled")) c.nr_throttled = v;
+            if (!strcmp(k, "throttled_usec")) c.throttled_usec = v;
+        }
+        fclose(f);
+    }
+    struct rusage ru;
+    if (getrusage(RUSAGE_SELF, &ru) == 0)
+        c.cpu_s = ru.ru_utime.tv_sec + ru.ru_stime.tv_sec + 1e-6 * (ru.ru_utime.tv_usec + ru.ru_stime.tv_usec);
+    return c;
 }
 
 struct Result {
@@ -117,7 +141,10 @@ int main(int argc, char **argv) {
         run(ctx, threads, payload, 0.2);  // warm up (first launch, staging slots)
         const long b0 = bulk_calls.load();
         const auto tb = Clock::now();
+        const CpuStat c0 = cpu_stat();
         const Result r = run(ctx, threads, payload, seconds);
+        const CpuStat c1 = cpu_stat();
+        const double wall = std::chrono::duration<double>(Clock::now() - tb).count();
         const double bulk_gibs = (bulk_calls.load() - b0) / 2.0 * 2.0 * bn * bl /
                                  std::chrono::duration<double>(Clock::now() - tb).count() / (1 << 30);
         uint64_t st[4] = {0, 0, 0, 0}, lc[QGCM_KERNEL_COUNTERS] = {};
@@ -130,6 +157,8 @@ int main(int argc, char **argv) {
                2.0 * r.rt_per_s * payload / (1 << 30), r.p50_us, r.p99_us, r.fail, (unsigned long long)st[0],
                (unsigned long long)st[1], (unsigned long long)lc[QGCM_KERNEL_ONE]);
         if (bulk) printf(", \"bulk_GiB_s\": %.2f", bulk_gibs);
+        printf(", \"cpus_busy\": %.2f, \"cgroup_throttled\": %llu, \"cgroup_throttled_ms\": %.1f", (c1.cpu_s - c0.cpu_s) / wall,
+               c1.nr_throttled - c0.nr_throttled, (c1.throttled_usec - c0.throttled_usec) / 1000.0);
         printf("}\n");
         fflush(stdout);
         if (r.fail) rc = 2;
