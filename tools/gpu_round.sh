@@ -3,7 +3,7 @@
 # reference build, and the config-2 profile (trace + PMC).  Every GPU step has its own time limit;
 # the script stops at the first step that faults, aborts or times out (a plain test failure goes on).
 # Usage: bash tools/gpu_round.sh <tag> [steps...]
-#   steps: rtests tests smoke bench ab prof pp prof3 exp_res align (default: tests smoke bench ab prof)
+#   steps: rtests tests smoke bench ab prof pp prof3 exp_res barreq align (default: tests smoke bench ab prof)
 set -u
 TAG=$1; shift
 STEPS=${*:-"tests smoke bench ab prof"}
@@ -53,6 +53,9 @@ for s in $STEPS; do
     exp_res)
       timeout -k 10 600 bash tools/exp_resident.sh $TAG
       check exp_res $? ;;
+    barreq)
+      timeout -k 10 400 bash tools/exp_barreq.sh $TAG
+      check barreq $? ;;
     align)  # config 3 packed vs 64-B aligned payloads: time, then WRITE_SIZE / FETCH_SIZE per layout
       timeout -k 10 300 python3 tools/exp_config3_align.py 9 > $OUT/align.json 2> $OUT/align.err
       check align $?
