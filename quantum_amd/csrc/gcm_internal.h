@@ -87,25 +87,29 @@ constexpr uint32_t kOneCap = 32768;
 hipError_t launch_one(bool seal, const Batch &b, hipStream_t s);
 
 // Resident per-packet service (resident.cpp): `workers` 256-thread workgroups of gcm_one_kernel's
-// engine stay on the GPU and serve requests the host posts into pinned (coherent) host memory, so a
-// per-packet call costs no launch.  Slot s belongs to worker s / per_worker.
-// Host -> device: the slot bytes, then the slot's 16-B request record req[s] = {seq (31-bit, +1 per
-// request), op (1 seal, 0 open) | aad_len << 1, len, key_idx} in one aligned 16-B store (one snapshot
-// for the GPU's 16-B read), then bell[16 w] += 1 for the slot's worker w (bell[16 w + 1] = stop).
-// Device -> host: the slot bytes, then done[s] = seq << 1 | verdict.  Every host-memory access of the
-// kernel goes around the GPU caches (16-B sc0 sc1 buffer accesses, system-scope atomics for the words).
-// An instance ends on the host's stop words, or when worker 0 sees no request served for idle_ticks or
-// the instance is life_ticks old (100 MHz clock): it raises the device shutdown word, every worker
-// serves what its records hold and leaves, and the last one writes *over = gen.
+// engine stay on the GPU and serve requests the host posts, so a per-packet call costs no launch.
+// Slot s belongs to worker s / per_worker.  Requests travel in DEVICE memory (fine-grained, which the
+// host CPU writes through the BAR: posted writes, and the GPU polls and reads its own HBM); results
+// travel in pinned host memory (the GPU's posted writes, which the host reads from its cache).
+// Host -> device: the slot's input bytes into in[s], then req[s].y..w = {op (1 seal, 0 open) |
+// aad_len << 1, len, key_idx}, then req[s].x = seq (31-bit, +1 per request), each step fenced
+// (sfence: the write-combined stores land in that order).  stop[16 w] != 0 ends worker w.
+// Device -> host: the result bytes into out[s], then done[s] = seq << 1 | verdict.  Every access of
+// memory the other side writes goes around the GPU caches (16-B sc0 sc1 buffer accesses, system-scope
+// atomics for the words).  An instance ends on the host's stop words, or when worker 0 sees no request
+// served for idle_ticks or the instance is life_ticks old (100 MHz clock): it raises the device
+// shutdown word, every worker serves what its records hold and leaves, and the last one writes
+// *over = gen.
 constexpr uint32_t kResSlotBytes = 16384;  // request slot: [aad 4][payload][tag 16][nonce 12], 16-B rounded
 constexpr uint32_t kResMaxPerWorker = 64;
 constexpr size_t kResDevBytes = 64;        // device control words: [0] last activity, [1] shutdown, [2] left
 struct ResArgs {
-    uint32_t *bell;         // host: worker w's bell at 16 w, stop at 16 w + 1 (a 64-B line each)
-    const uint4 *req;       // host: [S] request records
+    const uint4 *req;       // device (host-written): [S] request records
+    const uint32_t *stop;   // device (host-written): worker w's stop word at 16 w
+    const uint8_t *in;      // device (host-written): [S][kResSlotBytes] request bytes
+    uint8_t *out;           // host: [S][kResSlotBytes] result bytes
     uint32_t *done;         // host: [S]
     uint32_t *over;         // host: generation of the last instance that ended
-    uint8_t *data;          // host: [S][kResSlotBytes]
     uint8_t *dev;           // device control words (kResDevBytes), zeroed per launch
     uint32_t workers, per_worker, gen, pad;
     uint64_t idle_ticks, life_ticks;

@@ -1157,7 +1157,8 @@ __device__ __forceinline__ void one_fill_te(const uint32_t *te, uint32_t tid) {
 // nonce: seal only, 12 B, or NULL for the nonce already in the slot.  Returns the verdict (1 ok, 0
 // authentication failure), the same on every thread.
 template <bool kSeal, bool kSys>
-__device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_table, uint8_t *slot, uint32_t Lin,
+__device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_table, const uint8_t *in, uint8_t *out,
+                               uint32_t Lin,
                                uint32_t key, uint32_t aad_len, const uint8_t *nonce, bool fill_te, uint32_t &tab_key,
                                uint32_t &tab_n) {
     const uint32_t tid = threadIdx.x;
@@ -1170,7 +1171,7 @@ __device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_t
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const uint32_t i = tid + k * kOneThreads;
-        if (i < n16) v[k] = slot_ld16<kSys>(slot, i);
+        if (i < n16) v[k] = slot_ld16<kSys>(in, i);
     }
     // The table fills load everything first and store after (one memory latency, not one per
     // iteration): Te0/Te1 words for 32 replicas per row, then the comb tables of H^(2^l) -- only the
@@ -1211,7 +1212,7 @@ __device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_t
         }
     }
     for (uint32_t i = tid + 4 * kOneThreads; i < n16; i += kOneThreads) {  // slots over 16 KiB
-        const uint4 w = slot_ld16<kSys>(slot, i);
+        const uint4 w = slot_ld16<kSys>(in, i);
         const uint32_t a = A + 16 * i;
         lds_st32(a, w.x);
         lds_st32(a + 4, w.y);
@@ -1255,8 +1256,8 @@ __device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_t
                     k2 &= m2;
                     k3 &= m3;
                 }
-                const uint4 in = lds128(P + 16 * j);
-                lds_st128(P + 16 * j, uint4{in.x ^ k0, in.y ^ k1, in.z ^ k2, in.w ^ k3});
+                const uint4 cv = lds128(P + 16 * j);
+                lds_st128(P + 16 * j, uint4{cv.x ^ k0, cv.y ^ k1, cv.z ^ k2, cv.w ^ k3});
             }
         }
     };
@@ -1324,7 +1325,7 @@ __device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_t
         if (tid < 64)
             ghash();
         else
-            for (uint32_t i = tid - 64; i < early; i += kOneThreads - 64) slot_st16<kSys>(slot, i, row(i));
+            for (uint32_t i = tid - 64; i < early; i += kOneThreads - 64) slot_st16<kSys>(out, i, row(i));
         __syncthreads();
         if (tid == 0) {
             const uint4 e = lds128(kOneScratch), y = lds128(kOneScratch + 16);
@@ -1339,7 +1340,7 @@ __device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_t
             }
         }
         __syncthreads();
-        for (uint32_t i = early + tid; i < n16; i += kOneThreads) slot_st16<kSys>(slot, i, row(i));
+        for (uint32_t i = early + tid; i < n16; i += kOneThreads) slot_st16<kSys>(out, i, row(i));
     } else {
         if (tid < 64) {
             ghash();
@@ -1359,8 +1360,8 @@ __device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_t
                         k2 &= m2;
                         k3 &= m3;
                     }
-                    const uint4 in = lds128(P + 16 * j);
-                    slot_st16_at<kSys>(slot, 4 + 16 * j, uint4{in.x ^ k0, in.y ^ k1, in.z ^ k2, in.w ^ k3});
+                    const uint4 cv = lds128(P + 16 * j);
+                    slot_st16_at<kSys>(out, 4 + 16 * j, uint4{cv.x ^ k0, cv.y ^ k1, cv.z ^ k2, cv.w ^ k3});
                 }
             }
         }
@@ -1370,13 +1371,13 @@ __device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_t
               (e.w ^ y.w ^ lds32u(P + L + 12))) == 0;
         if (!ok) {  // Go 1.9 crypto/cipher gcm Open: zero the would-be plaintext on tag mismatch
             for (uint32_t j = tid; j < d; j += kOneThreads) {
-                const uint4 in = lds128(P + 16 * j);
-                const uint4 z = j == nfull ? uint4{in.x & ~m0, in.y & ~m1, in.z & ~m2, in.w & ~m3} : uint4{0, 0, 0, 0};
+                const uint4 cv = lds128(P + 16 * j);
+                const uint4 z = j == nfull ? uint4{cv.x & ~m0, cv.y & ~m1, cv.z & ~m2, cv.w & ~m3} : uint4{0, 0, 0, 0};
                 lds_st128(P + 16 * j, z);
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the plaintext stores have landed
             __syncthreads();
-            for (uint32_t j = tid; j < d; j += kOneThreads) slot_st16_at<kSys>(slot, 4 + 16 * j, lds128(P + 16 * j));
+            for (uint32_t j = tid; j < d; j += kOneThreads) slot_st16_at<kSys>(out, 4 + 16 * j, lds128(P + 16 * j));
         }
     }
     return ok;
@@ -1414,7 +1415,7 @@ __global__ void __launch_bounds__(kOneThreads) gcm_one_kernel(Batch b, const uin
         return;
     }
     uint32_t tab_key = 0xffffffffu, tab_n = 0;
-    const uint32_t ok = one_packet<kSeal, false>(b, rk_table, b.arena + off, Lin, key, b.aad_len,
+    const uint32_t ok = one_packet<kSeal, false>(b, rk_table, b.arena + off, b.arena + off, Lin, key, b.aad_len,
                                                  kSeal && b.nonces ? b.nonces + 12ull * pkt : nullptr, true, tab_key,
                                                  tab_n);
     if (tid == 0 && b.status) b.status[pkt] = ok;
@@ -1431,13 +1432,13 @@ __global__ void __launch_bounds__(kOneThreads) gcm_one_kernel(Batch b, const uin
 // ---------------------------------------------------------------------------------------------
 // Resident per-packet service (resident.cpp; gcm_internal.h ResArgs has the protocol).  Each
 // workgroup is a worker: it keeps gcm_one_kernel's T-tables in LDS for its whole life (and the comb
-// tables of the key it served last); wave 0 polls the worker's request records in pinned host memory
-// (one 16-B load per slot, one round trip per poll; only the bell word once it has been quiet for a
-// while), and the whole workgroup serves each new request in place in host memory with the latency
-// engine.  Measured against a build where
-// one dispatcher wave polled for all workers and forwarded requests through device memory: 414 K vs
-// 300 K round trips/s from 16 threads, 13.8 vs 19.4 us per call alone, and a host batch alongside kept
-// its PCIe rate either way (profiles/r3_s8/resident_sweep.txt).
+// tables of the key it served last); wave 0 polls the worker's request records, which the host writes
+// into device memory over the BAR (one 16-B load per slot from the GPU's own HBM, no PCIe round trip),
+// and the whole workgroup serves each new request: the input from device memory, the result into
+// pinned host memory.  Measured (tools/microbench/barreq.hip, profiles/r3_s12): a 1408-B request
+// served in 3.97 us per round trip from device memory against 6.22 us from pinned host memory; and
+// against a build where one dispatcher wave polled for all workers and forwarded requests, direct
+// polling served 414 K vs 300 K round trips/s from 16 threads (profiles/r3_s8/resident_sweep.txt).
 constexpr uint32_t kResCtl = (kOneLds + 15u) & ~15u;  // LDS: [0] command, [8,16) pending mask
 constexpr uint32_t kResDone = kResCtl + 64;           // the done sequence of each of the worker's slots
 constexpr uint32_t kResRec = kResDone + 4 * kResMaxPerWorker;  // the request records being served
@@ -1445,9 +1446,6 @@ constexpr uint32_t kResLds = kResRec + 16 * kResMaxPerWorker;
 static_assert(kResLds <= 160u * 1024u, "gfx950 LDS is 160 KiB per workgroup");
 
 __device__ __forceinline__ uint32_t ld_sys32(const uint32_t *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ uint64_t ld_sys64(const uint64_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 template <class T>
@@ -1466,34 +1464,21 @@ __global__ void __launch_bounds__(kOneThreads) gcm_resident_kernel(Batch b, cons
     uint64_t *const ctl = reinterpret_cast<uint64_t *>(a.dev);  // [0] last activity, [1] shutdown, [2] left
     one_fill_te(b.te, tid);
     if (tid < P) lds_st32(kResDone + 4 * tid, ld_sys32(a.done + first + tid) >> 1);
-    uint32_t tab_key = 0xffffffffu, tab_n = 0;
-    // wave 0's poll state (wave-uniform)
-    uint32_t idle = 0, last_bell = 0;
-    bool quiet = false, force = false;
+    uint32_t tab_key = 0xffffffffu, tab_n = 0, idle = 0;  // idle: wave 0's count of empty polls
     const uint64_t t_start = wall_clock64();
     __syncthreads();
     for (;;) {
-        if (tid < 64) {
-            // One poll.  Active: every slot's request record and the bell line (bell, stop) in one round
-            // trip.  Quiet (after 256 empty polls): the bell line alone, and the records only once the
-            // bell has moved -- read after the bell value has arrived, so a request whose bell increment
-            // the poll missed rings it again later, and one it saw has its record in place (the host
-            // writes the record before the bell).
-            uint4 bl = {0, 0, 0, 0};
-            if (lane == 0) bl = host_ld16(a.bell, 64u * a.workers, 64u * w);
-            auto read_records = [&]() {
-                bool pend = false;
-                if (lane < P) {
-                    const uint4 m = host_ld16(a.req, 16 * S, 16 * (first + lane));
-                    pend = (m.x & 0x7fffffffu) != lds32(kResDone + 4 * lane);
-                    if (pend) lds_st128(kResRec + 16 * lane, m);
-                }
-                return __ballot(pend);
-            };
-            uint64_t pm = quiet ? 0ull : read_records();
+        if (tid < 64) {  // one poll: every slot's record and the worker's stop word
+            bool pend = false;
+            if (lane < P) {
+                const uint4 m = host_ld16(a.req, 16 * S, 16 * (first + lane));
+                pend = (m.x & 0x7fffffffu) != lds32(kResDone + 4 * lane);
+                if (pend) lds_st128(kResRec + 16 * lane, m);
+            }
+            const uint64_t pm = __ballot(pend);
             uint32_t stop = 0;
             if (lane == 0) {
-                stop = bl.y;
+                stop = host_ld16(a.stop, 64u * a.workers, 64u * w).x;
                 if (w == 0) {  // the instance's end: no request for idle_ticks, or life_ticks old
                     const uint64_t now = wall_clock64();
                     const uint64_t act = ld_agent(ctl);  // last activity of any worker (0: none yet)
@@ -1501,31 +1486,18 @@ __global__ void __launch_bounds__(kOneThreads) gcm_resident_kernel(Batch b, cons
                     if (q > (int64_t)a.idle_ticks || now - t_start > a.life_ticks) st_agent(ctl + 1, (uint64_t)1);
                 }
                 stop |= ld_agent(ctl + 1) != 0 ? 1u : 0u;
-            }
-            const uint32_t bell = __builtin_amdgcn_readfirstlane(bl.x);
-            stop = __builtin_amdgcn_readfirstlane(stop);
-            if (quiet && (force || bell != last_bell)) {
-                pm = read_records();
-                force = false;
-            }
-            last_bell = bell;
-            if (pm) {
-                idle = 0;
-                quiet = false;
-            } else if (!stop) {
-                if (++idle == 256) {
-                    quiet = true;
-                    force = true;  // one more record read after the next bell read
-                }
-                if (quiet)
-                    __builtin_amdgcn_s_sleep(32);
-                else
-                    __builtin_amdgcn_s_sleep(2);
-            }
-            if (lane == 0) {
                 lds_st32(kResCtl, stop ? 2u : pm ? 1u : 0u);
                 lds_st32(kResCtl + 8, (uint32_t)pm);
                 lds_st32(kResCtl + 12, (uint32_t)(pm >> 32));
+            }
+            stop = __builtin_amdgcn_readfirstlane(stop);
+            if (pm) {
+                idle = 0;
+            } else if (!stop) {  // back off once quiet (the polls read HBM, not PCIe)
+                if (++idle < 4096)
+                    __builtin_amdgcn_s_sleep(1);
+                else
+                    __builtin_amdgcn_s_sleep(16);
             }
         }
         __syncthreads();
@@ -1546,11 +1518,12 @@ __global__ void __launch_bounds__(kOneThreads) gcm_resident_kernel(Batch b, cons
                                (op ? Lin < QGCM_MAX_PAYLOAD : Lin >= (uint32_t)QGCM_OVERHEAD) &&
                                stage <= kResSlotBytes && stage <= kOneCap - 16;
             uint32_t ok = 0;
-            uint8_t *slot = a.data + (size_t)sl * kResSlotBytes;
+            const uint8_t *in = a.in + (size_t)sl * kResSlotBytes;
+            uint8_t *out = a.out + (size_t)sl * kResSlotBytes;
             if (valid)
-                ok = op ? one_packet<true, true>(b, rk_table, slot, Lin, key, aad, nullptr, false, tab_key, tab_n)
-                        : one_packet<false, true>(b, rk_table, slot, Lin, key, aad, nullptr, false, tab_key, tab_n);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the slot's bytes have reached the host
+                ok = op ? one_packet<true, true>(b, rk_table, in, out, Lin, key, aad, nullptr, false, tab_key, tab_n)
+                        : one_packet<false, true>(b, rk_table, in, out, Lin, key, aad, nullptr, false, tab_key, tab_n);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the result bytes have reached the host
             __syncthreads();
             if (tid == 0) {
                 __hip_atomic_store(a.done + sl, q << 1 | ok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -3,11 +3,13 @@
 // worker/incoming.go:82-92) without a kernel launch per call.
 //
 // A resident kernel (gcm_kernels.hip gcm_resident_kernel) keeps `workers` workgroups on the GPU; each
-// owns `per_worker` request slots in one pinned, coherent host region.  A call copies its packet into
-// a free slot of the least-loaded worker, writes the slot's 16-B request record, rings the worker's
-// bell and waits on the slot's done word (spinning, then asleep on a futex that a completion thread
-// wakes); the worker seals or opens the slot in place over PCIe and publishes the verdict.  No
-// hipLaunch, no stream and no hardware queue per call.
+// owns `per_worker` request slots.  A call takes a free slot of the least-loaded worker, writes its
+// packet and then the slot's request record into DEVICE memory through the BAR (fine-grained VRAM the
+// CPU may write: posted, write-combined stores, ordered by sfence), and waits on the slot's done word
+// in pinned host memory (spinning, then asleep on a futex that a completion thread wakes); the worker,
+// polling its records in its own HBM, seals or opens the packet and writes the result and the verdict
+// into host memory.  No hipLaunch, no stream and no hardware queue per call, and no PCIe read on the
+// request path.
 //
 // Lifetime: an instance ends by itself when it has seen no request for QGCM_RESIDENT_IDLE_US or is
 // QGCM_RESIDENT_LIFE_US old (so work queued behind it on a shared hardware queue, or a
@@ -17,6 +19,8 @@
 // and the caller launches the next instance, which serves it.  At most one instance runs at a time.
 #include <emmintrin.h>
 #include <hip/hip_runtime.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
 #include <linux/futex.h>
 #include <sched.h>
 #include <sys/syscall.h>
@@ -44,10 +48,11 @@ struct Resident {
     Batch base{};
     uint32_t W = 16, P = 16, S = 256;
     uint64_t idle_ticks = 200000, life_ticks = 800000;  // 100 MHz: 2 ms, 8 ms
-    uint8_t *host = nullptr;  // pinned coherent region (below)
-    uint32_t *bell = nullptr, *done = nullptr, *over = nullptr;
+    uint8_t *host = nullptr;  // pinned coherent region: done words, over, the result slots
+    uint8_t *devm = nullptr;  // fine-grained device region the CPU writes: records, stop words, request slots
+    uint32_t *done = nullptr, *over = nullptr, *stop = nullptr;
     uint4 *req = nullptr;
-    uint8_t *data = nullptr;
+    uint8_t *in = nullptr, *out = nullptr;
     uint8_t *d_ctl = nullptr;  // device control words (kResDevBytes)
     hipStream_t stream = nullptr;
     std::unique_ptr<uint32_t[]> seqh;                  // last sequence per slot (owned by the slot holder)
@@ -110,11 +115,12 @@ int relaunch(Resident *r, uint32_t g) {
         return QGCM_E_HIP;
     }
     ResArgs a{};
-    a.bell = r->bell;
     a.req = r->req;
+    a.stop = r->stop;
+    a.in = r->in;
+    a.out = r->out;
     a.done = r->done;
     a.over = r->over;
-    a.data = r->data;
     a.dev = r->d_ctl;
     a.workers = r->W;
     a.per_worker = r->P;
@@ -155,6 +161,28 @@ void waker_loop(Resident *r) {
     }
 }
 
+// The device region: fine-grained VRAM (the GPU reads it around its caches) that the host CPU is
+// allowed to write (HSA access for the CPU agent: a BAR mapping at the same address).
+hsa_status_t find_cpu_agent(hsa_agent_t a, void *out) {
+    hsa_device_type_t t;
+    if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) == HSA_STATUS_SUCCESS && t == HSA_DEVICE_TYPE_CPU) {
+        *static_cast<hsa_agent_t *>(out) = a;
+        return HSA_STATUS_INFO_BREAK;
+    }
+    return HSA_STATUS_SUCCESS;
+}
+
+bool device_region(Resident *r, size_t bytes) {
+    if (hipExtMallocWithFlags(reinterpret_cast<void **>(&r->devm), bytes, hipDeviceMallocFinegrained) != hipSuccess) {
+        r->devm = nullptr;
+        return false;
+    }
+    static const bool hsa_up = hsa_init() == HSA_STATUS_SUCCESS;  // the runtime HIP runs on (a reference)
+    hsa_agent_t cpu{0};
+    return hsa_up && hsa_iterate_agents(find_cpu_agent, &cpu) == HSA_STATUS_INFO_BREAK && cpu.handle &&
+           hsa_amd_agents_allow_access(1, &cpu, nullptr, r->devm) == HSA_STATUS_SUCCESS;
+}
+
 }  // namespace
 
 Resident *resident_create(int device, const Batch &base, int num_cus) {
@@ -171,19 +199,28 @@ Resident *resident_create(int device, const Batch &base, int num_cus) {
     r->max_spinners = (int32_t)env_u64("QGCM_RESIDENT_SPINNERS", (uint64_t)std::max(1, cpu_share() / 2));
     r->idle_ticks = env_u64("QGCM_RESIDENT_IDLE_US", 2000) * 100;  // s_memrealtime: 100 MHz
     r->life_ticks = env_u64("QGCM_RESIDENT_LIFE_US", 8000) * 100;
-    // host region: bells (a 64-B line per worker: bell, stop), done, over, the request records, then the slots
-    const size_t o_done = 64ull * r->W, o_over = o_done + 4ull * r->S;
-    const size_t o_req = (o_over + 64 + 15) & ~15ull, o_data = (o_req + 16ull * r->S + 4095) & ~4095ull;
-    const size_t bytes = o_data + (size_t)kResSlotBytes * r->S;
+    // host region: done, over, then the result slots; device region: the stop words (a 64-B line per
+    // worker), the request records, then the request slots
+    const size_t o_over = (4ull * r->S + 63) & ~63ull, o_out = (o_over + 64 + 4095) & ~4095ull;
+    const size_t host_bytes = o_out + (size_t)kResSlotBytes * r->S;
+    const size_t o_req = 64ull * r->W, o_in = (o_req + 16ull * r->S + 4095) & ~4095ull;
+    const size_t dev_bytes = o_in + (size_t)kResSlotBytes * r->S;
     if (hipSetDevice(device) != hipSuccess ||
-        hipHostMalloc(reinterpret_cast<void **>(&r->host), bytes, hipHostMallocCoherent) != hipSuccess)
+        hipHostMalloc(reinterpret_cast<void **>(&r->host), host_bytes, hipHostMallocCoherent) != hipSuccess)
         return nullptr;
-    memset(r->host, 0, o_data);
-    r->bell = reinterpret_cast<uint32_t *>(r->host);
-    r->done = reinterpret_cast<uint32_t *>(r->host + o_done);
+    memset(r->host, 0, o_out);
+    if (!device_region(r.get(), dev_bytes)) {
+        resident_destroy(r.release());
+        return nullptr;
+    }
+    r->done = reinterpret_cast<uint32_t *>(r->host);
     r->over = reinterpret_cast<uint32_t *>(r->host + o_over);
-    r->req = reinterpret_cast<uint4 *>(r->host + o_req);
-    r->data = r->host + o_data;
+    r->out = r->host + o_out;
+    r->stop = reinterpret_cast<uint32_t *>(r->devm);
+    r->req = reinterpret_cast<uint4 *>(r->devm + o_req);
+    r->in = r->devm + o_in;
+    memset(r->devm, 0, o_in);  // stop words and records, through the BAR
+    _mm_sfence();
     r->seqh.reset(new uint32_t[r->S]());
     r->busy.reset(new std::atomic<uint32_t>[r->S]);
     for (uint32_t i = 0; i < r->S; ++i) r->busy[i] = 0;
@@ -208,9 +245,11 @@ int resident_quiesce(Resident *r) {
     std::lock_guard<std::mutex> lk(r->launch_mu);
     const uint32_t g = r->gen.load(std::memory_order_acquire);
     if (g == 0) return QGCM_OK;
-    for (uint32_t w = 0; w < r->W; ++w) __atomic_store_n(&r->bell[16 * w + 1], 1u, __ATOMIC_RELEASE);
+    for (uint32_t w = 0; w < r->W; ++w) __atomic_store_n(&r->stop[16 * w], 1u, __ATOMIC_RELEASE);
+    _mm_sfence();
     const hipError_t e = hipSetDevice(r->device) == hipSuccess ? hipStreamSynchronize(r->stream) : hipErrorUnknown;
-    for (uint32_t w = 0; w < r->W; ++w) __atomic_store_n(&r->bell[16 * w + 1], 0u, __ATOMIC_RELEASE);
+    for (uint32_t w = 0; w < r->W; ++w) __atomic_store_n(&r->stop[16 * w], 0u, __ATOMIC_RELEASE);
+    _mm_sfence();
     if (e != hipSuccess) {
         r->broken = true;
         return QGCM_E_HIP;
@@ -228,6 +267,7 @@ void resident_destroy(Resident *r) {
     if (r->stream) hipStreamDestroy(r->stream);
     if (r->d_ctl) hipFree(r->d_ctl);
     if (r->host) hipHostFree(r->host);
+    if (r->devm) hipFree(r->devm);
     delete r;
 }
 
@@ -288,21 +328,25 @@ long resident_call(Resident *r, bool seal, uint32_t key, uint8_t *data, long len
         sched_yield();  // every slot in flight
     }
     r->inflight[w].fetch_add(1, std::memory_order_relaxed);
-    uint8_t *slot = r->data + (size_t)s * kResSlotBytes;
+    // the request into device memory (write-combined stores through the BAR), then its record: the
+    // fields with the old sequence (which the worker has served, so it ignores the record), then the new
+    // sequence; sfence orders each step's stores before the next ones
+    uint8_t *slot = r->in + (size_t)s * kResSlotBytes;
     uint32_t hdr = 0;
     if (aad_len) memcpy(&hdr, aad, aad_len);
     memcpy(slot, &hdr, 4);
     memcpy(slot + 4, data, (size_t)len);
     if (seal) memcpy(slot + 4 + len + 16, nb, 12);
-    uint32_t q = (r->seqh[s] + 1) & 0x7fffffffu;
+    const uint32_t q0 = r->seqh[s];
+    uint32_t q = (q0 + 1) & 0x7fffffffu;
     if (q == 0) q = 1;
     r->seqh[s] = q;
-    // the request record in one aligned 16-B store, after the slot bytes (x86 keeps store order; the
-    // GPU reads the record with one 16-B load)
-    std::atomic_thread_fence(std::memory_order_release);
+    _mm_sfence();
     _mm_store_si128(reinterpret_cast<__m128i *>(&r->req[s]),
-                    _mm_set_epi32((int)key, (int)len, (int)((seal ? 1u : 0u) | aad_len << 1), (int)q));
-    __atomic_fetch_add(&r->bell[16 * w], 1u, __ATOMIC_SEQ_CST);
+                    _mm_set_epi32((int)key, (int)len, (int)((seal ? 1u : 0u) | aad_len << 1), (int)q0));
+    _mm_sfence();
+    __atomic_store_n(reinterpret_cast<uint32_t *>(&r->req[s]), q, __ATOMIC_RELAXED);
+    _mm_sfence();
     long rc = 0;
     uint32_t g = r->gen.load(std::memory_order_acquire);
     if (instance_over(r, g) && relaunch(r, g) != QGCM_OK) return -1;  // broken: the slot stays taken
@@ -355,14 +399,15 @@ long resident_call(Resident *r, bool seal, uint32_t key, uint8_t *data, long len
     }
     if (spinning) r->spinners.fetch_sub(1, std::memory_order_relaxed);
     r->served.fetch_add(1, std::memory_order_relaxed);
+    const uint8_t *res = r->out + (size_t)s * kResSlotBytes;
     if (seal) {
         rc = -1;
         if (v & 1) {  // a rejected seal leaves the caller's buffer untouched
-            memcpy(data, slot + 4, (size_t)len + QGCM_OVERHEAD);
+            memcpy(data, res + 4, (size_t)len + QGCM_OVERHEAD);
             rc = len + QGCM_OVERHEAD;
         }
     } else {
-        memcpy(data, slot + 4, (size_t)len - QGCM_OVERHEAD);  // plaintext, or zeros on auth failure
+        memcpy(data, res + 4, (size_t)len - QGCM_OVERHEAD);  // plaintext, or zeros on auth failure
         rc = (v & 1) ? len - QGCM_OVERHEAD : -1;
     }
     r->inflight[w].fetch_sub(1, std::memory_order_relaxed);
