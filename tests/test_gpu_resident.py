@@ -265,3 +265,63 @@ def test_launch_path_when_disabled(torch):
         assert c["resident"] == 0 and c["one"] == 2
     finally:
         ctx.close()
+
+
+def test_aad_lengths_and_tamper_kinds(torch):
+    """AAD of 0-4 bytes (nil additional data, as crypto_test.go:54-101 passes) and every tamper kind
+    (a ciphertext byte, the last one, the tag, the nonce, the AAD), from 8 threads through the resident
+    kernel: sealed bytes equal the oracle's, a tampered open fails exactly where the oracle's does,
+    zeroes the plaintext and leaves tag and nonce as they were."""
+    from quantum_amd.crypto import AES
+
+    ctx = make_ctx()
+    try:
+        key = bytes(range(7, 39))
+        aes = AES(key, ctx=ctx)
+        before = ctx.launch_counts()
+        errs = []
+
+        def work(t):
+            rng = random.Random(100 + t)
+            for i in range(30):
+                aad = [b"", b"\x0a", b"\x0a\x63", b"\x0a\x63\x00", AAD][i % 5]
+                L = rng.choice([0, 5, 16, 31, 100, 1350, rng.randrange(0, 4000)])
+                pt, nonce = rng.randbytes(L), rng.randbytes(12)
+                data, want = bytearray(pt + bytes(28)), bytearray(pt + bytes(28))
+                n, err = aes.Encrypt(data, L, aad or None, nonce=nonce)
+                O.aesgo_encrypt(key, want, L, aad, nonce)
+                if err is not None or n != L + 28 or data != want:
+                    errs.append(f"seal t={t} L={L} aad={len(aad)}")
+                    continue
+                kind = i % 6
+                bad, bad_aad = bytearray(data), bytearray(aad)
+                if kind == 1 and L:
+                    bad[rng.randrange(L)] ^= 0x80
+                elif kind == 2 and L:
+                    bad[L - 1] ^= 1
+                elif kind == 3:
+                    bad[L + rng.randrange(16)] ^= 4
+                elif kind == 4:
+                    bad[L + 16 + rng.randrange(12)] ^= 2
+                elif kind == 5 and aad:
+                    bad_aad[0] ^= 1
+                ref = bytearray(bad)
+                want_n = O.aesgo_decrypt(key, ref, bytes(bad_aad))
+                tail = bytes(bad[L:])
+                n, err = aes.Decrypt(bad, bytes(bad_aad) or None)
+                if want_n < 0:
+                    if err is None or bytes(bad[:L]) != bytes(L) or bytes(bad[L:]) != tail:
+                        errs.append(f"tamper t={t} L={L} kind={kind}")
+                elif err is not None or n != L or bytes(bad[:L]) != pt:
+                    errs.append(f"open t={t} L={L} kind={kind}")
+
+        ths = [threading.Thread(target=work, args=(t,)) for t in range(8)]
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        assert not errs, errs[:5]
+        after = ctx.launch_counts()
+        assert after["resident"] - before["resident"] == 8 * 30 * 2 and after["one"] == before["one"]
+    finally:
+        ctx.close()
