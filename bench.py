@@ -388,6 +388,30 @@ def launch_ranks(args: argparse.Namespace) -> None:
     sys.exit(rc)
 
 
+def extra_per_packet(seconds: float = 1.5) -> dict:
+    """The per-call drop-in (qgcm_seal_one / qgcm_open_one, crypto/aes.go:41-62 from quantum's worker
+    threads, worker/outgoing.go:83-93): tools/bin/per_packet_bench (built by __graft_entry__.build()),
+    one 1350-B seal+open in flight per thread, through the resident kernel and through a kernel launch
+    per call, 1 and 16 threads.  Run as a child process after the headline."""
+    import subprocess
+
+    exe = os.path.join(ROOT, "tools", "bin", "per_packet_bench")
+    if not os.path.exists(exe):
+        return {"skipped": "tools/bin/per_packet_bench not built (python -c 'import __graft_entry__ as g; g.build()')"}
+    out = {"workload": "per-packet Encrypt/Decrypt calls, 1350 B, one packet in flight per thread",
+           "unit": "seal+open round trips/s"}
+    for threads, mode in ((1, "both"), (16, "both")):
+        r = subprocess.run([exe, str(threads), "1350", str(seconds), "0", mode], capture_output=True, text=True,
+                           timeout=120)
+        if r.returncode != 0:
+            raise RuntimeError(f"per_packet_bench {threads}: rc {r.returncode}: {r.stderr[-300:]}")
+        for ln in r.stdout.splitlines():
+            d = json.loads(ln)
+            out[f"{d['path']}_t{threads}"] = {k: d[k] for k in ("round_trips_per_s", "call_pair_p50_us",
+                                                                 "call_pair_p99_us", "failures", "cpus_busy")}
+    return out
+
+
 def main() -> None:
     args = parse()
     launch_ranks(args)
@@ -538,7 +562,8 @@ def main() -> None:
             extra = {}
             for name, fn in (("config3", lambda: extra_config3(verify=not args.no_verify)),
                              ("e2e_pinned_host", lambda: extra_e2e(key)),
-                             ("config5", lambda: extra_config5(key, args.cpu_threads or host["share"]))):
+                             ("config5", lambda: extra_config5(key, args.cpu_threads or host["share"])),
+                             ("per_packet", extra_per_packet)):
                 t0 = time.perf_counter()
                 try:
                     extra[name] = fn()
