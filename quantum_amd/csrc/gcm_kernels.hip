@@ -1069,6 +1069,19 @@ constexpr uint32_t kOneBuf = kTeBytes + kOneTabs * kGhBytes;
 constexpr uint32_t kOneScratch = kOneBuf + kOneCap;
 constexpr uint32_t kOneLds = kOneScratch + 64;
 static_assert(kOneLds <= 160u * 1024u, "gfx950 LDS is 160 KiB per workgroup");
+// QGCM_RES_TRACE (side builds, tools/res_trace.sh): per served request the resident kernel adds the
+// device-clock intervals poll -> input staged -> result computed -> result writes acknowledged to
+// g_res_trace; one_packet stamps the middle two into LDS words past the resident control block.
+#ifdef QGCM_RES_TRACE
+constexpr uint32_t kResTrace = ((kOneLds + 15u) & ~15u) + 16;  // inside kResCtl's 64 B: [16, 32)
+__device__ __forceinline__ void res_stamp(uint32_t slot) {
+    if (threadIdx.x == 0) {
+        const uint64_t t = wall_clock64();
+        lds_st32(kResTrace + 8 * slot, (uint32_t)t);
+        lds_st32(kResTrace + 8 * slot + 4, (uint32_t)(t >> 32));
+    }
+}
+#endif
 
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
 __device__ __forceinline__ uint32_t lds8(uint32_t addr) { return *(const lds_u8 *)(size_t)addr; }
@@ -1220,6 +1233,9 @@ __device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_t
         lds_st32(a + 12, w.w);
     }
     __syncthreads();
+#ifdef QGCM_RES_TRACE
+    if (kSys) res_stamp(0);
+#endif
 
     const Keys kk = {rk_table + (size_t)key * kRkWords, rk_table + (size_t)key * kRkWords + 64};
     const uint32_t lb = (lane & 31u) << 2;
@@ -1340,6 +1356,9 @@ __device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_t
             }
         }
         __syncthreads();
+#ifdef QGCM_RES_TRACE
+        if (kSys) res_stamp(1);
+#endif
         for (uint32_t i = early + tid; i < n16; i += kOneThreads) slot_st16<kSys>(out, i, row(i));
     } else {
         if (tid < 64) {
@@ -1369,6 +1388,9 @@ __device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_t
         const uint4 e = lds128(kOneScratch), y = lds128(kOneScratch + 16);
         ok = ((e.x ^ y.x ^ lds32u(P + L)) | (e.y ^ y.y ^ lds32u(P + L + 4)) | (e.z ^ y.z ^ lds32u(P + L + 8)) |
               (e.w ^ y.w ^ lds32u(P + L + 12))) == 0;
+#ifdef QGCM_RES_TRACE
+        if (kSys) res_stamp(1);
+#endif
         if (!ok) {  // Go 1.9 crypto/cipher gcm Open: zero the would-be plaintext on tag mismatch
             for (uint32_t j = tid; j < d; j += kOneThreads) {
                 const uint4 cv = lds128(P + 16 * j);
@@ -1444,6 +1466,9 @@ constexpr uint32_t kResDone = kResCtl + 64;           // the done sequence of ea
 constexpr uint32_t kResRec = kResDone + 4 * kResMaxPerWorker;  // the request records being served
 constexpr uint32_t kResLds = kResRec + 16 * kResMaxPerWorker;
 static_assert(kResLds <= 160u * 1024u, "gfx950 LDS is 160 KiB per workgroup");
+#ifdef QGCM_RES_TRACE
+__device__ unsigned long long g_res_trace[8];  // sums: poll->staged, staged->computed, computed->acked, count
+#endif
 
 __device__ __forceinline__ uint32_t ld_sys32(const uint32_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1503,6 +1528,9 @@ __global__ void __launch_bounds__(kOneThreads) gcm_resident_kernel(Batch b, cons
         __syncthreads();
         const uint32_t cmd = lds32(kResCtl);  // 0: nothing to do, 1: serve, 2: serve, then leave
         uint64_t mask = lds32(kResCtl + 8) | (uint64_t)lds32(kResCtl + 12) << 32;
+#ifdef QGCM_RES_TRACE
+        uint64_t t_poll = wall_clock64();  // after the poll that found the requests
+#endif
         if (cmd == 0) {
             __syncthreads();  // every thread has read the command before wave 0 writes the next
             continue;
@@ -1525,6 +1553,18 @@ __global__ void __launch_bounds__(kOneThreads) gcm_resident_kernel(Batch b, cons
                         : one_packet<false, true>(b, rk_table, in, out, Lin, key, aad, nullptr, false, tab_key, tab_n);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the result bytes have reached the host
             __syncthreads();
+#ifdef QGCM_RES_TRACE
+            if (tid == 0 && valid) {
+                const uint64_t t_end = wall_clock64();
+                const uint64_t t0 = lds32(kResTrace) | (uint64_t)lds32(kResTrace + 4) << 32;
+                const uint64_t t1 = lds32(kResTrace + 8) | (uint64_t)lds32(kResTrace + 12) << 32;
+                atomicAdd(&g_res_trace[0], (unsigned long long)(t0 - t_poll));
+                atomicAdd(&g_res_trace[1], (unsigned long long)(t1 - t0));
+                atomicAdd(&g_res_trace[2], (unsigned long long)(t_end - t1));
+                atomicAdd(&g_res_trace[3], 1ull);
+                t_poll = t_end;  // the next pending request of this poll starts here
+            }
+#endif
             if (tid == 0) {
                 __hip_atomic_store(a.done + sl, q << 1 | ok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 lds_st32(kResDone + 4 * j, q);
@@ -1542,6 +1582,17 @@ __global__ void __launch_bounds__(kOneThreads) gcm_resident_kernel(Batch b, cons
         }
     }
 }
+
+#ifdef QGCM_RES_TRACE
+extern "C" int qgcm_debug_res_trace(unsigned long long out[4], int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_res_trace), 4 * sizeof(unsigned long long)) != hipSuccess) return -1;
+    if (reset) {
+        const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_res_trace), z, sizeof z) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
 
 hipError_t launch_resident(const Batch &b, const ResArgs &a, hipStream_t s) {
     if (a.workers == 0 || a.per_worker == 0 || a.per_worker > kResMaxPerWorker) return hipErrorInvalidValue;

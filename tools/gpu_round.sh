@@ -53,6 +53,9 @@ for s in $STEPS; do
     exp_res)
       timeout -k 10 600 bash tools/exp_resident.sh $TAG
       check exp_res $? ;;
+    res_trace)
+      timeout -k 10 300 bash tools/res_trace.sh $TAG
+      check res_trace $? ;;
     barreq)
       timeout -k 10 400 bash tools/exp_barreq.sh $TAG
       check barreq $? ;;

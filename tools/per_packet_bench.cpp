@@ -7,6 +7,7 @@
 // Build: g++ -O2 -std=c++17 -Iinclude tools/per_packet_bench.cpp -Lquantum_amd -lqgcm -lpthread
 //        -Wl,-rpath,$PWD/quantum_amd -o gpurun_out/per_packet_bench
 // Usage: per_packet_bench [threads=64] [payload=1350] [seconds=2] [bulk=0] [mode=both|resident|launch]
+#include <dlfcn.h>
 #include <qgcm.h>
 #include <sys/resource.h>
 #include <stdio.h>
@@ -141,6 +142,11 @@ int main(int argc, char **argv) {
         run(ctx, threads, payload, 0.2);  // warm up (first launch, staging slots)
         const long b0 = bulk_calls.load();
         const auto tb = Clock::now();
+        // a QGCM_RES_TRACE side build of the library exports the resident kernel's device-side intervals
+        using TraceFn = int (*)(unsigned long long *, int);
+        const TraceFn trace = (TraceFn)dlsym(RTLD_DEFAULT, "qgcm_debug_res_trace");
+        unsigned long long tr[4] = {0, 0, 0, 0};
+        if (trace) trace(tr, 1);
         const CpuStat c0 = cpu_stat();
         const Result r = run(ctx, threads, payload, seconds);
         const CpuStat c1 = cpu_stat();
@@ -157,6 +163,9 @@ int main(int argc, char **argv) {
                2.0 * r.rt_per_s * payload / (1 << 30), r.p50_us, r.p99_us, r.fail, (unsigned long long)st[0],
                (unsigned long long)st[1], (unsigned long long)lc[QGCM_KERNEL_ONE]);
         if (bulk) printf(", \"bulk_GiB_s\": %.2f", bulk_gibs);
+        if (trace && resident && trace(tr, 0) == 0 && tr[3])
+            printf(", \"device_us\": {\"poll_to_staged\": %.2f, \"staged_to_computed\": %.2f, \"computed_to_acked\": %.2f, \"requests\": %llu}",
+                   tr[0] / 100.0 / tr[3], tr[1] / 100.0 / tr[3], tr[2] / 100.0 / tr[3], tr[3]);
         printf(", \"cpus_busy\": %.2f, \"cgroup_throttled\": %llu, \"cgroup_throttled_ms\": %.1f", (c1.cpu_s - c0.cpu_s) / wall,
                c1.nr_throttled - c0.nr_throttled, (c1.throttled_usec - c0.throttled_usec) / 1000.0);
         printf("}\n");
