@@ -1467,7 +1467,8 @@ constexpr uint32_t kResRec = kResDone + 4 * kResMaxPerWorker;  // the request re
 constexpr uint32_t kResLds = kResRec + 16 * kResMaxPerWorker;
 static_assert(kResLds <= 160u * 1024u, "gfx950 LDS is 160 KiB per workgroup");
 #ifdef QGCM_RES_TRACE
-__device__ unsigned long long g_res_trace[8];  // sums: poll->staged, staged->computed, computed->acked, count
+__device__ unsigned long long g_res_trace[8];  // sums: poll->staged, staged->computed, computed->acked, count,
+                                               // shader clocks and 100-MHz ticks poll->acked
 #endif
 
 __device__ __forceinline__ uint32_t ld_sys32(const uint32_t *p) {
@@ -1530,6 +1531,7 @@ __global__ void __launch_bounds__(kOneThreads) gcm_resident_kernel(Batch b, cons
         uint64_t mask = lds32(kResCtl + 8) | (uint64_t)lds32(kResCtl + 12) << 32;
 #ifdef QGCM_RES_TRACE
         uint64_t t_poll = wall_clock64();  // after the poll that found the requests
+        uint64_t c_poll = clock64();       // shader clock, for the clock rate while serving
 #endif
         if (cmd == 0) {
             __syncthreads();  // every thread has read the command before wave 0 writes the next
@@ -1562,7 +1564,11 @@ __global__ void __launch_bounds__(kOneThreads) gcm_resident_kernel(Batch b, cons
                 atomicAdd(&g_res_trace[1], (unsigned long long)(t1 - t0));
                 atomicAdd(&g_res_trace[2], (unsigned long long)(t_end - t1));
                 atomicAdd(&g_res_trace[3], 1ull);
+                const uint64_t c_end = clock64();
+                atomicAdd(&g_res_trace[4], (unsigned long long)(c_end - c_poll));
+                atomicAdd(&g_res_trace[5], (unsigned long long)(t_end - t_poll));
                 t_poll = t_end;  // the next pending request of this poll starts here
+                c_poll = c_end;
             }
 #endif
             if (tid == 0) {
@@ -1584,8 +1590,8 @@ __global__ void __launch_bounds__(kOneThreads) gcm_resident_kernel(Batch b, cons
 }
 
 #ifdef QGCM_RES_TRACE
-extern "C" int qgcm_debug_res_trace(unsigned long long out[4], int reset) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_res_trace), 4 * sizeof(unsigned long long)) != hipSuccess) return -1;
+extern "C" int qgcm_debug_res_trace(unsigned long long out[6], int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_res_trace), 6 * sizeof(unsigned long long)) != hipSuccess) return -1;
     if (reset) {
         const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_res_trace), z, sizeof z) != hipSuccess) return -1;
