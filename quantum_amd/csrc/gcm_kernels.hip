@@ -1073,9 +1073,9 @@ static_assert(kOneLds <= 160u * 1024u, "gfx950 LDS is 160 KiB per workgroup");
 // device-clock intervals poll -> input staged -> result computed -> result writes acknowledged to
 // g_res_trace; one_packet stamps the middle two into LDS words past the resident control block.
 #ifdef QGCM_RES_TRACE
-constexpr uint32_t kResTrace = ((kOneLds + 15u) & ~15u) + 16;  // inside kResCtl's 64 B: [16, 32)
-__device__ __forceinline__ void res_stamp(uint32_t slot) {
-    if (threadIdx.x == 0) {
+constexpr uint32_t kResTrace = ((kOneLds + 15u) & ~15u) + 16;  // inside kResCtl's 64 B: [16, 48)
+__device__ __forceinline__ void res_stamp(uint32_t slot, uint32_t by = 0) {
+    if (threadIdx.x == by) {
         const uint64_t t = wall_clock64();
         lds_st32(kResTrace + 8 * slot, (uint32_t)t);
         lds_st32(kResTrace + 8 * slot + 4, (uint32_t)(t >> 32));
@@ -1337,11 +1337,17 @@ __device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_t
     if (kSeal) {
         ctr_pass();
         __syncthreads();
+#ifdef QGCM_RES_TRACE
+        if (kSys) res_stamp(2);
+#endif
         const uint32_t early = (4u + L) >> 4;  // slot rows that end before the tag
         if (tid < 64)
             ghash();
         else
             for (uint32_t i = tid - 64; i < early; i += kOneThreads - 64) slot_st16<kSys>(out, i, row(i));
+#ifdef QGCM_RES_TRACE
+        if (kSys) res_stamp(3);
+#endif
         __syncthreads();
         if (tid == 0) {
             const uint4 e = lds128(kOneScratch), y = lds128(kOneScratch + 16);
@@ -1363,6 +1369,9 @@ __device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_t
     } else {
         if (tid < 64) {
             ghash();
+#ifdef QGCM_RES_TRACE
+            if (kSys) res_stamp(2);
+#endif
         } else {  // counter blocks (block d = E_K(J0)); the plaintext goes out while wave 0 hashes
             for (uint32_t j = tid - 64; j <= d; j += kOneThreads - 64) {
                 const uint32_t ctr = j == d ? 1u : j + 2u;
@@ -1383,6 +1392,9 @@ __device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_t
                     slot_st16_at<kSys>(out, 4 + 16 * j, uint4{cv.x ^ k0, cv.y ^ k1, cv.z ^ k2, cv.w ^ k3});
                 }
             }
+#ifdef QGCM_RES_TRACE
+            if (kSys) res_stamp(3, 64);
+#endif
         }
         __syncthreads();
         const uint4 e = lds128(kOneScratch), y = lds128(kOneScratch + 16);
@@ -1467,8 +1479,10 @@ constexpr uint32_t kResRec = kResDone + 4 * kResMaxPerWorker;  // the request re
 constexpr uint32_t kResLds = kResRec + 16 * kResMaxPerWorker;
 static_assert(kResLds <= 160u * 1024u, "gfx950 LDS is 160 KiB per workgroup");
 #ifdef QGCM_RES_TRACE
-__device__ unsigned long long g_res_trace[8];  // sums: poll->staged, staged->computed, computed->acked, count,
-                                               // shader clocks and 100-MHz ticks poll->acked
+// per op (open 0, seal 1), sums of: poll -> staged, staged -> stamp 2, staged -> stamp 3, staged ->
+// computed, computed -> acked, count, shader clocks and 100-MHz ticks poll -> acked.  Seal: stamp 2 =
+// counter blocks done, 3 = GHASH done; open: 2 = GHASH done (wave 0), 3 = counter blocks done (waves 1-3).
+__device__ unsigned long long g_res_trace[16];
 #endif
 
 __device__ __forceinline__ uint32_t ld_sys32(const uint32_t *p) {
@@ -1558,15 +1572,19 @@ __global__ void __launch_bounds__(kOneThreads) gcm_resident_kernel(Batch b, cons
 #ifdef QGCM_RES_TRACE
             if (tid == 0 && valid) {
                 const uint64_t t_end = wall_clock64();
-                const uint64_t t0 = lds32(kResTrace) | (uint64_t)lds32(kResTrace + 4) << 32;
-                const uint64_t t1 = lds32(kResTrace + 8) | (uint64_t)lds32(kResTrace + 12) << 32;
-                atomicAdd(&g_res_trace[0], (unsigned long long)(t0 - t_poll));
-                atomicAdd(&g_res_trace[1], (unsigned long long)(t1 - t0));
-                atomicAdd(&g_res_trace[2], (unsigned long long)(t_end - t1));
-                atomicAdd(&g_res_trace[3], 1ull);
+                uint64_t ts[4];
+                for (int k = 0; k < 4; ++k)
+                    ts[k] = lds32(kResTrace + 8 * k) | (uint64_t)lds32(kResTrace + 8 * k + 4) << 32;
+                unsigned long long *g = g_res_trace + 8 * op;
+                atomicAdd(&g[0], (unsigned long long)(ts[0] - t_poll));
+                atomicAdd(&g[1], (unsigned long long)(ts[2] - ts[0]));
+                atomicAdd(&g[2], (unsigned long long)(ts[3] - ts[0]));
+                atomicAdd(&g[3], (unsigned long long)(ts[1] - ts[0]));
+                atomicAdd(&g[4], (unsigned long long)(t_end - ts[1]));
+                atomicAdd(&g[5], 1ull);
                 const uint64_t c_end = clock64();
-                atomicAdd(&g_res_trace[4], (unsigned long long)(c_end - c_poll));
-                atomicAdd(&g_res_trace[5], (unsigned long long)(t_end - t_poll));
+                atomicAdd(&g[6], (unsigned long long)(c_end - c_poll));
+                atomicAdd(&g[7], (unsigned long long)(t_end - t_poll));
                 t_poll = t_end;  // the next pending request of this poll starts here
                 c_poll = c_end;
             }
@@ -1590,10 +1608,10 @@ __global__ void __launch_bounds__(kOneThreads) gcm_resident_kernel(Batch b, cons
 }
 
 #ifdef QGCM_RES_TRACE
-extern "C" int qgcm_debug_res_trace(unsigned long long out[6], int reset) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_res_trace), 6 * sizeof(unsigned long long)) != hipSuccess) return -1;
+extern "C" int qgcm_debug_res_trace(unsigned long long out[16], int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_res_trace), 16 * sizeof(unsigned long long)) != hipSuccess) return -1;
     if (reset) {
-        const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        const unsigned long long z[16] = {};
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_res_trace), z, sizeof z) != hipSuccess) return -1;
     }
     return 0;

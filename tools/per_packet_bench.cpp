@@ -145,7 +145,7 @@ int main(int argc, char **argv) {
         // a QGCM_RES_TRACE side build of the library exports the resident kernel's device-side intervals
         using TraceFn = int (*)(unsigned long long *, int);
         const TraceFn trace = (TraceFn)dlsym(RTLD_DEFAULT, "qgcm_debug_res_trace");
-        unsigned long long tr[6] = {0, 0, 0, 0, 0, 0};
+        unsigned long long tr[16] = {};
         if (trace) trace(tr, 1);
         const CpuStat c0 = cpu_stat();
         const Result r = run(ctx, threads, payload, seconds);
@@ -163,10 +163,17 @@ int main(int argc, char **argv) {
                2.0 * r.rt_per_s * payload / (1 << 30), r.p50_us, r.p99_us, r.fail, (unsigned long long)st[0],
                (unsigned long long)st[1], (unsigned long long)lc[QGCM_KERNEL_ONE]);
         if (bulk) printf(", \"bulk_GiB_s\": %.2f", bulk_gibs);
-        if (trace && resident && trace(tr, 0) == 0 && tr[3])
-            printf(", \"device_us\": {\"poll_to_staged\": %.2f, \"staged_to_computed\": %.2f, \"computed_to_acked\": %.2f, \"requests\": %llu, \"shader_MHz\": %.0f}",
-                   tr[0] / 100.0 / tr[3], tr[1] / 100.0 / tr[3], tr[2] / 100.0 / tr[3], tr[3],
-                   tr[5] ? tr[4] * 100.0 / tr[5] : 0.0);
+        if (trace && resident && trace(tr, 0) == 0) {
+            for (int op = 1; op >= 0; --op) {
+                const unsigned long long *g = tr + 8 * op, n = g[5];
+                if (!n) continue;
+                printf(", \"device_us_%s\": {\"poll_to_staged\": %.2f, \"%s\": %.2f, \"%s\": %.2f, \"staged_to_computed\": %.2f, "
+                       "\"computed_to_acked\": %.2f, \"requests\": %llu, \"shader_MHz\": %.0f}",
+                       op ? "seal" : "open", g[0] / 100.0 / n, op ? "staged_to_ctr_done" : "staged_to_ghash_done",
+                       g[1] / 100.0 / n, op ? "staged_to_ghash_done" : "staged_to_ctr_done", g[2] / 100.0 / n,
+                       g[3] / 100.0 / n, g[4] / 100.0 / n, n, g[7] ? g[6] * 100.0 / g[7] : 0.0);
+            }
+        }
         printf(", \"cpus_busy\": %.2f, \"cgroup_throttled\": %llu, \"cgroup_throttled_ms\": %.1f", (c1.cpu_s - c0.cpu_s) / wall,
                c1.nr_throttled - c0.nr_throttled, (c1.throttled_usec - c0.throttled_usec) / 1000.0);
         printf("}\n");
