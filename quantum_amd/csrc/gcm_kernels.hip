@@ -1063,11 +1063,13 @@ extern "C" int qgcm_debug_seg_stats(unsigned long long *out, int n, int reset) {
 // overwritten with zeros once those stores have landed (as Go 1.9 Open: zeroed plaintext).
 // LDS: [0, 64K) Te, [64K, 120K) comb tables of H^(2^l), [120K, 120K + kOneCap) the slot at +12
 // (payload 16-B aligned), then 64 B of scratch (E_K(J0), the GHASH value).
-constexpr uint32_t kOneThreads = 256;
+constexpr uint32_t kOneThreads = 512;
 constexpr uint32_t kOneTabs = 7;
 constexpr uint32_t kOneBuf = kTeBytes + kOneTabs * kGhBytes;
-constexpr uint32_t kOneScratch = kOneBuf + kOneCap;
-constexpr uint32_t kOneLds = kOneScratch + 64;
+constexpr uint32_t kOneScratch = kOneBuf + kOneCap;  // [0, 16) E_K(J0), [16, 32) the GHASH value
+constexpr uint32_t kOneX = kOneScratch + 64;         // GHASH Estrin exchange: 2 x 64 chains x 16 B
+constexpr uint32_t kOneLds = kOneX + 2048;
+constexpr uint32_t kOneSliceMax = kOneThreads / 4;  // counter blocks (J0 included) a column-sliced pass takes
 static_assert(kOneLds <= 160u * 1024u, "gfx950 LDS is 160 KiB per workgroup");
 // QGCM_RES_TRACE (side builds, tools/res_trace.sh): per served request the resident kernel adds the
 // device-clock intervals poll -> input staged -> result computed -> result writes acknowledged to
@@ -1146,9 +1148,41 @@ __device__ __forceinline__ void slot_st16_at(uint8_t *slot, uint32_t off, uint4 
     __builtin_amdgcn_raw_buffer_store_b128(u32x4{v.x, v.y, v.z, v.w}, r, (int)off, 0, kSys ? kSc0Sc1 : 0);
 }
 
+// Z <- Z * T on the 8 lanes e = 0..7 of one GHASH chain (the latency engine): lane e looks up the
+// four 4-bit comb windows of bytes 2e and 2e+1 of Z (entry (p, v) at gb + 256 p + 16 v, as ghash_mul),
+// then the chain's 8 partial products are XOR-reduced by DPP (quad_perm within each quad, then
+// row_half_mirror across the two quads of the half-row), so every lane ends with the product.
+__device__ __forceinline__ void ghash_mul8(uint32_t &z0, uint32_t &z1, uint32_t &z2, uint32_t &z3, uint32_t gb,
+                                           uint32_t e) {
+    const uint32_t w = e >> 1, k0 = 2u * (e & 1u);
+    const uint32_t y = w == 0 ? z0 : w == 1 ? z1 : w == 2 ? z2 : z3;
+    const uint32_t hi = y & 0xf0f0f0f0u, lo = (y << 4) & 0xf0f0f0f0u;  // nibble values x 16
+    const uint32_t r0 = gb + 1024u * e;                                // rows 4e .. 4e+3
+    const uint4 t0 = lds128(r0 + ((hi >> (8 * k0)) & 0xffu));
+    const uint4 t1 = lds128(r0 + 256u + ((lo >> (8 * k0)) & 0xffu));
+    const uint4 t2 = lds128(r0 + 512u + ((hi >> (8 * k0 + 8)) & 0xffu));
+    const uint4 t3 = lds128(r0 + 768u + ((lo >> (8 * k0 + 8)) & 0xffu));
+    uint32_t a0 = xor3(t0.x, t1.x, t2.x) ^ t3.x, a1 = xor3(t0.y, t1.y, t2.y) ^ t3.y;
+    uint32_t a2 = xor3(t0.z, t1.z, t2.z) ^ t3.z, a3 = xor3(t0.w, t1.w, t2.w) ^ t3.w;
+    a0 = quad_xor(a0);
+    a1 = quad_xor(a1);
+    a2 = quad_xor(a2);
+    a3 = quad_xor(a3);
+    z0 = a0 ^ (uint32_t)__builtin_amdgcn_mov_dpp((int)a0, 0x141, 0xf, 0xf, false);  // row_half_mirror
+    z1 = a1 ^ (uint32_t)__builtin_amdgcn_mov_dpp((int)a1, 0x141, 0xf, 0xf, false);
+    z2 = a2 ^ (uint32_t)__builtin_amdgcn_mov_dpp((int)a2, 0x141, 0xf, 0xf, false);
+    z3 = a3 ^ (uint32_t)__builtin_amdgcn_mov_dpp((int)a3, 0x141, 0xf, 0xf, false);
+}
+
+// Workgroup barrier for LDS data only: __syncthreads() also waits for every outstanding global
+// store (its release fence is s_waitcnt vmcnt(0)), and the latency engine's result stores go to host
+// memory over PCIe while it keeps computing -- waiting for their acknowledgement at each barrier cost
+// ~1.5 us per packet.  Only LDS is shared through these barriers; the caller orders the stores.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // Fills the replicated T-tables (64 KiB at LDS 0): loads first, stores after (one memory latency).
 __device__ __forceinline__ void one_fill_te(const uint32_t *te, uint32_t tid) {
-    constexpr int kTeIt = kTeBytes / 16 / kOneThreads;  // 16
+    constexpr int kTeIt = kTeBytes / 16 / kOneThreads;  // 8
     uint32_t tv[kTeIt];
 #pragma unroll
     for (int k = 0; k < kTeIt; ++k) {
@@ -1190,7 +1224,7 @@ __device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_t
     // iteration): Te0/Te1 words for 32 replicas per row, then the comb tables of H^(2^l) -- only the
     // ones this packet's GHASH reads (H and H^2 always, the Estrin levels up to
     // bit-length(min(d, 63)), H^64 once a lane owns two blocks) and not loaded yet for this key.
-    constexpr int kGhIt = kOneTabs * 512 / kOneThreads;  // 14
+    constexpr int kGhIt = kOneTabs * 512 / kOneThreads;  // 7
     const uint4 *gh = b.gh_table + (size_t)key * kGhEntries;
     const uint32_t dd = (L + 15u) >> 4;
     const uint32_t dtop = dd < 63u ? dd : 63u;
@@ -1232,7 +1266,7 @@ __device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_t
         lds_st32(a + 8, w.z);
         lds_st32(a + 12, w.w);
     }
-    __syncthreads();
+    lds_barrier();
 #ifdef QGCM_RES_TRACE
     if (kSys) res_stamp(0);
 #endif
@@ -1254,79 +1288,130 @@ __device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_t
     }
     uint32_t m0, m1, m2, m3;
     block_mask(r, m0, m1, m2, m3);
+    const bool sliced = d + 1 <= kOneSliceMax;  // workgroup-uniform
 
-    // 2. (seal) counter blocks: block j < d XORs its keystream into the staged payload; block d is E_K(J0)
-    auto ctr_pass = [&]() {
-        for (uint32_t j = tid; j <= d; j += kOneThreads) {
-            const uint32_t ctr = j == d ? 1u : j + 2u;  // J0, or inc32(J0) + j
-            Ctr cc;
-            ctr_setup(cc, n0, n1, n2, ctr >> 8, kk, lb);
-            uint32_t k0, k1, k2, k3;
-            ctr_block(cc, ctr & 0xffu, kk, lb, k0, k1, k2, k3);
+    // 2. Counter blocks; block d is E_K(J0) (into scratch), and emit(j, q, w) takes word q of block j's
+    // keystream (masked to the payload in the partial block).  Packets of up to kOneSliceMax blocks
+    // (2032 B) run column-sliced: the four lanes of a quad own the four columns of one block's state,
+    // each looks up 4 table entries per round instead of 16 and takes the other columns from its quad
+    // by DPP -- a lone packet is bound by the rounds' latency, which this cuts, not by the tables.
+    // Longer packets: one lane per block (ctr_setup + ctr_block).
+    auto ctr_run = [&](auto &&emit) {
+        auto put = [&](uint32_t j, uint32_t q, uint32_t w) {
             if (j == d) {
-                lds_st128(kOneScratch, uint4{k0, k1, k2, k3});
+                lds_st32(kOneScratch + 4 * q, w);
             } else {
-                if (j == nfull) {  // partial block: the bytes past L (tag area) stay as they are
-                    k0 &= m0;
-                    k1 &= m1;
-                    k2 &= m2;
-                    k3 &= m3;
+                if (j == nfull) w &= q == 0 ? m0 : q == 1 ? m1 : q == 2 ? m2 : m3;
+                emit(j, q, w);
+            }
+        };
+        if (sliced) {
+            const uint32_t j = tid >> 2, q = tid & 3u;
+            if (j <= d) {  // quad-uniform: the DPP exchanges stay within active quads
+                uint32_t rq[11];
+#pragma unroll
+                for (int i = 0; i < 11; ++i) rq[i] = kk.rr[4 * (3 + i) + q];  // this column's round keys
+                const uint32_t rl = kk.rk[56 + q];
+                Ctr cc;
+                ctr_setup(cc, n0, n1, n2, 0u, kk, lb);  // every counter here is below 256: one segment
+                const uint32_t ctr = j == d ? 1u : j + 2u;
+                const uint32_t x = (ctr & 0xffu) ^ cc.x3;
+                const uint32_t tv = cc.K0 ^ rot16(lds32(((x << 8) | lb) + 128u));  // as ctr_block_t
+                const uint32_t kq = (4u - q) & 3u;  // byte of tv that column q looks up: 0, 3, 2, 1
+                uint32_t sv = lds32(perm(tv, lb, 0x0c0c0400u + (kq << 8)) + ((q & 1u) ? 128u : 0u));
+                if (q == 1 || q == 2) sv = rot16(sv);
+                sv ^= q == 0 ? cc.U0 : q == 1 ? cc.U1 : q == 2 ? cc.U2 : cc.U3;
+                const TT0 t{lb, 0};
+                // column q of round rr: Te0[s_q.b0] ^ Te1[s_q+1.b1] ^ rot16(Te0[s_q+2.b2] ^ Te1[s_q+3.b3] ^ rr)
+#pragma unroll
+                for (int i = 0; i < 11; ++i) {
+                    const uint32_t s1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)sv, 0x39, 0xf, 0xf, false);
+                    const uint32_t s2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)sv, 0x4E, 0xf, 0xf, false);
+                    const uint32_t s3 = (uint32_t)__builtin_amdgcn_mov_dpp((int)sv, 0x93, 0xf, 0xf, false);
+                    const uint32_t c0 = t.t0(sv, 0), c1 = t.t1(s1, 1), a0 = t.t0(s2, 2), a1 = t.t1(s3, 3);
+                    asm volatile("" ::: "memory");
+                    sv = xor3(c0, c1, rot16(xor3(a0, a1, rq[i])));
                 }
-                const uint4 cv = lds128(P + 16 * j);
-                lds_st128(P + 16 * j, uint4{cv.x ^ k0, cv.y ^ k1, cv.z ^ k2, cv.w ^ k3});
+                const uint32_t s1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)sv, 0x39, 0xf, 0xf, false);
+                const uint32_t s2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)sv, 0x4E, 0xf, 0xf, false);
+                const uint32_t s3 = (uint32_t)__builtin_amdgcn_mov_dpp((int)sv, 0x93, 0xf, 0xf, false);
+                const uint32_t a0 = t.t0(s1, 1), a1 = t.t0(sv, 0), a2 = t.t1(s3, 3), a3 = t.t0(s2, 2);
+                asm volatile("" ::: "memory");
+                put(j, q, xor3(perm(a0, a1, 0x0c0c0501u), perm(a2, a3, 0x07020c0cu), rl));  // as round_last
+            }
+        } else {
+            for (uint32_t j = tid; j <= d; j += kOneThreads) {
+                const uint32_t ctr = j == d ? 1u : j + 2u;  // J0, or inc32(J0) + j
+                Ctr cc;
+                ctr_setup(cc, n0, n1, n2, ctr >> 8, kk, lb);
+                uint32_t k0, k1, k2, k3;
+                ctr_block(cc, ctr & 0xffu, kk, lb, k0, k1, k2, k3);
+                put(j, 0, k0);
+                put(j, 1, k1);
+                put(j, 2, k2);
+                put(j, 3, k3);
             }
         }
     };
-    // 3. GHASH over the staged ciphertext (wave 0), the hash into scratch + 16
+
+    // 3. GHASH over the staged ciphertext on all 512 threads, the hash into scratch + 16.  Chain c
+    // (64 chains, 8 lanes each: lane e looks up the 4 comb windows of bytes 2e, 2e+1, and the chain's
+    // lanes XOR their partial products by DPP, ghash_mul8) owns the blocks whose exponent in
+    // Y = sum_i B_i H^(N+1-i) is c + 2 mod 64 (the AAD block included): a Horner chain by H^64, then
+    // sum_c Z_c H^c by radix-2 Estrin levels (multiply by H^(2^l), add chain c + 2^l's product through
+    // LDS), then Y = S H^2 + [len(A)]||[len(C)] H.  Every thread calls it (it has workgroup barriers).
     auto ghash = [&]() {
-        if (tid < 64) {
-            const uint32_t m = lane;
-            uint32_t z0 = 0, z1 = 0, z2 = 0, z3 = 0;
-            const bool aad_lane = m == (d & 63u) && aad_len;
-            if (aad_lane) z0 = lds32(A) & (aad_len >= 4 ? 0xffffffffu : lowmask(aad_len));
-            // blocks bi = d-1-m-64k >= 0, in increasing order: exponent d+1-bi = m+2 (mod 64) at the end
-            const uint32_t first = (d - 1u - m) & 63u;
-            for (uint32_t bi = first; bi < d && m < d; bi += 64) {
-                uint4 c = lds128(P + 16 * bi);
-                // (a chain's first step multiplies Z = 0, or the AAD block when it owns both)
-                if (bi == nfull) {
-                    c.x &= m0;
-                    c.y &= m1;
-                    c.z &= m2;
-                    c.w &= m3;
-                }
-                if (bi >= 64u || aad_lane) ghash_mul<false>(z0, z1, z2, z3, kTeBytes + 6 * kGhBytes);  // H^64
-                z0 ^= c.x;
-                z1 ^= c.y;
-                z2 ^= c.z;
-                z3 ^= c.w;
+        const uint32_t c = tid >> 3, e = tid & 7u;
+        uint32_t z0 = 0, z1 = 0, z2 = 0, z3 = 0;
+        const bool aad_chain = c == (d & 63u) && aad_len;
+        if (aad_chain) z0 = lds32(A) & (aad_len >= 4 ? 0xffffffffu : lowmask(aad_len));
+        // blocks bi = d-1-c-64k >= 0, in increasing order (chain-uniform loop)
+        for (uint32_t bi = (d - 1u - c) & 63u; c < d && bi < d; bi += 64) {
+            uint4 cb = lds128(P + 16 * bi);
+            if (bi == nfull) {
+                cb.x &= m0;
+                cb.y &= m1;
+                cb.z &= m2;
+                cb.w &= m3;
             }
-            // S = sum_m Z_m H^m: level l adds lane m + 2^l's value times H^(2^l) into lane m
-            // (only lanes m <= min(d, 63) hold nonzero Z: levels with 2^l > that are skipped)
-            const uint32_t top = d < 63u ? d : 63u;
-            const int levels = top ? 32 - __builtin_clz(top) : 0;
-            for (int l = 0; l < levels; ++l) {
-                uint32_t p0 = z0, p1 = z1, p2 = z2, p3 = z3;
-                ghash_mul<false>(p0, p1, p2, p3, kTeBytes + l * kGhBytes);
-                z0 ^= __shfl_down(p0, 1u << l, 64);
-                z1 ^= __shfl_down(p1, 1u << l, 64);
-                z2 ^= __shfl_down(p2, 1u << l, 64);
-                z3 ^= __shfl_down(p3, 1u << l, 64);
-            }
-            // Y = S H^2 (lane 0) + [len(A)]_64 || [len(C)]_64 H (lane 1), in one multiply step
-            if (m == 1) {
-                z0 = 0;
-                z1 = bswap(aad_len * 8u);
-                z2 = 0;
-                z3 = bswap(L * 8u);
-            }
-            ghash_mul<false>(z0, z1, z2, z3, kTeBytes + (m == 0 ? kGhBytes : 0u));
-            z0 ^= __shfl_down(z0, 1u, 64);
-            z1 ^= __shfl_down(z1, 1u, 64);
-            z2 ^= __shfl_down(z2, 1u, 64);
-            z3 ^= __shfl_down(z3, 1u, 64);
-            if (m == 0) lds_st128(kOneScratch + 16, uint4{z0, z1, z2, z3});
+            if (bi >= 64u || aad_chain) ghash_mul8(z0, z1, z2, z3, kTeBytes + 6 * kGhBytes, e);  // H^64
+            z0 ^= cb.x;
+            z1 ^= cb.y;
+            z2 ^= cb.z;
+            z3 ^= cb.w;
         }
+        // only chains 0..top hold a value (the others skip the multiplies: their lanes would all read
+        // entry 0 of eight different rows, an 8-way bank conflict on every read)
+        const uint32_t top = d < 63u ? d : 63u;
+        const int levels = top ? 32 - __builtin_clz(top) : 0;
+        for (int l = 0; l < levels; ++l) {
+            uint32_t p0 = z0, p1 = z1, p2 = z2, p3 = z3;
+            if (c <= top) ghash_mul8(p0, p1, p2, p3, kTeBytes + l * kGhBytes, e);
+            const uint32_t xb = kOneX + 1024u * (l & 1);  // double-buffered: one barrier per level
+            if (e == 0) lds_st128(xb + 16 * c, uint4{p0, p1, p2, p3});
+            lds_barrier();
+            const uint32_t pc = c + (1u << l);
+            if (pc < 64u) {
+                const uint4 q = lds128(xb + 16 * pc);
+                z0 ^= q.x;
+                z1 ^= q.y;
+                z2 ^= q.z;
+                z3 ^= q.w;
+            }
+        }
+        // Y = S H^2 (chain 0) + [len(A)]_64 || [len(C)]_64 H (chain 1), in one multiply step
+        if (c == 1) {
+            z0 = 0;
+            z1 = bswap(aad_len * 8u);
+            z2 = 0;
+            z3 = bswap(L * 8u);
+        }
+        if (c < 2) ghash_mul8(z0, z1, z2, z3, kTeBytes + (c == 0 ? kGhBytes : 0u), e);
+        z0 ^= __shfl_down(z0, 8u, 64);
+        z1 ^= __shfl_down(z1, 8u, 64);
+        z2 ^= __shfl_down(z2, 8u, 64);
+        z3 ^= __shfl_down(z3, 8u, 64);
+        if (tid == 0) lds_st128(kOneScratch + 16, uint4{z0, z1, z2, z3});
     };
 
     auto row = [&](uint32_t i) {
@@ -1335,20 +1420,22 @@ __device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_t
     };
     uint32_t ok = 1;
     if (kSeal) {
-        ctr_pass();
-        __syncthreads();
+        ctr_run([&](uint32_t j, uint32_t q, uint32_t w) {  // ciphertext into the staged payload
+            const uint32_t a = P + 16 * j + 4 * q;
+            lds_st32(a, lds32(a) ^ w);
+        });
+        lds_barrier();
 #ifdef QGCM_RES_TRACE
         if (kSys) res_stamp(2);
 #endif
-        const uint32_t early = (4u + L) >> 4;  // slot rows that end before the tag
-        if (tid < 64)
-            ghash();
-        else
-            for (uint32_t i = tid - 64; i < early; i += kOneThreads - 64) slot_st16<kSys>(out, i, row(i));
+        // the rows that end before the tag go out now; their stores complete while GHASH runs
+        const uint32_t early = (4u + L) >> 4;
+        for (uint32_t i = tid; i < early; i += kOneThreads) slot_st16<kSys>(out, i, row(i));
+        ghash();
 #ifdef QGCM_RES_TRACE
         if (kSys) res_stamp(3);
 #endif
-        __syncthreads();
+        lds_barrier();
         if (tid == 0) {
             const uint4 e = lds128(kOneScratch), y = lds128(kOneScratch + 16);
             lds_st32u(P + L, e.x ^ y.x);
@@ -1361,42 +1448,28 @@ __device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_t
                 lds_st32u(P + L + 24, n2);
             }
         }
-        __syncthreads();
+        lds_barrier();
 #ifdef QGCM_RES_TRACE
         if (kSys) res_stamp(1);
 #endif
         for (uint32_t i = early + tid; i < n16; i += kOneThreads) slot_st16<kSys>(out, i, row(i));
     } else {
-        if (tid < 64) {
-            ghash();
+        // the plaintext goes straight from registers to the output (the staged ciphertext stays for
+        // GHASH); on a tag mismatch it is overwritten with zeros below, once these stores have landed
+        const __amdgpu_buffer_rsrc_t ro =
+            __builtin_amdgcn_make_buffer_rsrc(out, 0, (int)(kSys ? kResSlotBytes : kOneCap), 0x00020000);
+        ctr_run([&](uint32_t j, uint32_t q, uint32_t w) {
+            const uint32_t off = 4 + 16 * j + 4 * q;
+            __builtin_amdgcn_raw_buffer_store_b32(lds32(P + 16 * j + 4 * q) ^ w, ro, (int)off, 0, kSys ? kSc0Sc1 : 0);
+        });
 #ifdef QGCM_RES_TRACE
-            if (kSys) res_stamp(2);
+        if (kSys) res_stamp(3);
 #endif
-        } else {  // counter blocks (block d = E_K(J0)); the plaintext goes out while wave 0 hashes
-            for (uint32_t j = tid - 64; j <= d; j += kOneThreads - 64) {
-                const uint32_t ctr = j == d ? 1u : j + 2u;
-                Ctr cc;
-                ctr_setup(cc, n0, n1, n2, ctr >> 8, kk, lb);
-                uint32_t k0, k1, k2, k3;
-                ctr_block(cc, ctr & 0xffu, kk, lb, k0, k1, k2, k3);
-                if (j == d) {
-                    lds_st128(kOneScratch, uint4{k0, k1, k2, k3});
-                } else {
-                    if (j == nfull) {  // partial block: the tag bytes after it are rewritten unchanged
-                        k0 &= m0;
-                        k1 &= m1;
-                        k2 &= m2;
-                        k3 &= m3;
-                    }
-                    const uint4 cv = lds128(P + 16 * j);
-                    slot_st16_at<kSys>(out, 4 + 16 * j, uint4{cv.x ^ k0, cv.y ^ k1, cv.z ^ k2, cv.w ^ k3});
-                }
-            }
+        ghash();
 #ifdef QGCM_RES_TRACE
-            if (kSys) res_stamp(3, 64);
+        if (kSys) res_stamp(2);
 #endif
-        }
-        __syncthreads();
+        lds_barrier();
         const uint4 e = lds128(kOneScratch), y = lds128(kOneScratch + 16);
         ok = ((e.x ^ y.x ^ lds32u(P + L)) | (e.y ^ y.y ^ lds32u(P + L + 4)) | (e.z ^ y.z ^ lds32u(P + L + 8)) |
               (e.w ^ y.w ^ lds32u(P + L + 12))) == 0;
@@ -1404,14 +1477,14 @@ __device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_t
         if (kSys) res_stamp(1);
 #endif
         if (!ok) {  // Go 1.9 crypto/cipher gcm Open: zero the would-be plaintext on tag mismatch
-            for (uint32_t j = tid; j < d; j += kOneThreads) {
-                const uint4 cv = lds128(P + 16 * j);
-                const uint4 z = j == nfull ? uint4{cv.x & ~m0, cv.y & ~m1, cv.z & ~m2, cv.w & ~m3} : uint4{0, 0, 0, 0};
-                lds_st128(P + 16 * j, z);
+            for (uint32_t jj = tid; jj < d; jj += kOneThreads) {
+                const uint4 cv = lds128(P + 16 * jj);
+                const uint4 z = jj == nfull ? uint4{cv.x & ~m0, cv.y & ~m1, cv.z & ~m2, cv.w & ~m3} : uint4{0, 0, 0, 0};
+                lds_st128(P + 16 * jj, z);
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the plaintext stores have landed
             __syncthreads();
-            for (uint32_t j = tid; j < d; j += kOneThreads) slot_st16_at<kSys>(out, 4 + 16 * j, lds128(P + 16 * j));
+            for (uint32_t jj = tid; jj < d; jj += kOneThreads) slot_st16_at<kSys>(out, 4 + 16 * jj, lds128(P + 16 * jj));
         }
     }
     return ok;
