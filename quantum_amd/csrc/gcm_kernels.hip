@@ -1296,7 +1296,7 @@ __device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_t
     // each looks up 4 table entries per round instead of 16 and takes the other columns from its quad
     // by DPP -- a lone packet is bound by the rounds' latency, which this cuts, not by the tables.
     // Longer packets: one lane per block (ctr_setup + ctr_block).
-    auto ctr_run = [&](auto &&emit) {
+    auto ctr_run = [&](auto &&emit, auto &&emit4) {
         auto put = [&](uint32_t j, uint32_t q, uint32_t w) {
             if (j == d) {
                 lds_st32(kOneScratch + 4 * q, w);
@@ -1346,10 +1346,17 @@ __device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_t
                 ctr_setup(cc, n0, n1, n2, ctr >> 8, kk, lb);
                 uint32_t k0, k1, k2, k3;
                 ctr_block(cc, ctr & 0xffu, kk, lb, k0, k1, k2, k3);
-                put(j, 0, k0);
-                put(j, 1, k1);
-                put(j, 2, k2);
-                put(j, 3, k3);
+                if (j == d) {
+                    lds_st128(kOneScratch, uint4{k0, k1, k2, k3});
+                } else {
+                    if (j == nfull) {
+                        k0 &= m0;
+                        k1 &= m1;
+                        k2 &= m2;
+                        k3 &= m3;
+                    }
+                    emit4(j, uint4{k0, k1, k2, k3});  // a whole block per lane: contiguous 16-B accesses
+                }
             }
         }
     };
@@ -1420,10 +1427,15 @@ __device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_t
     };
     uint32_t ok = 1;
     if (kSeal) {
-        ctr_run([&](uint32_t j, uint32_t q, uint32_t w) {  // ciphertext into the staged payload
-            const uint32_t a = P + 16 * j + 4 * q;
-            lds_st32(a, lds32(a) ^ w);
-        });
+        ctr_run(
+            [&](uint32_t j, uint32_t q, uint32_t w) {  // ciphertext into the staged payload
+                const uint32_t a = P + 16 * j + 4 * q;
+                lds_st32(a, lds32(a) ^ w);
+            },
+            [&](uint32_t j, uint4 k) {
+                const uint4 cv = lds128(P + 16 * j);
+                lds_st128(P + 16 * j, uint4{cv.x ^ k.x, cv.y ^ k.y, cv.z ^ k.z, cv.w ^ k.w});
+            });
         lds_barrier();
 #ifdef QGCM_RES_TRACE
         if (kSys) res_stamp(2);
@@ -1458,10 +1470,16 @@ __device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_t
         // GHASH); on a tag mismatch it is overwritten with zeros below, once these stores have landed
         const __amdgpu_buffer_rsrc_t ro =
             __builtin_amdgcn_make_buffer_rsrc(out, 0, (int)(kSys ? kResSlotBytes : kOneCap), 0x00020000);
-        ctr_run([&](uint32_t j, uint32_t q, uint32_t w) {
-            const uint32_t off = 4 + 16 * j + 4 * q;
-            __builtin_amdgcn_raw_buffer_store_b32(lds32(P + 16 * j + 4 * q) ^ w, ro, (int)off, 0, kSys ? kSc0Sc1 : 0);
-        });
+        ctr_run(
+            [&](uint32_t j, uint32_t q, uint32_t w) {  // quads: four lanes store one block's 16 B together
+                const uint32_t off = 4 + 16 * j + 4 * q;
+                __builtin_amdgcn_raw_buffer_store_b32(lds32(P + 16 * j + 4 * q) ^ w, ro, (int)off, 0,
+                                                      kSys ? kSc0Sc1 : 0);
+            },
+            [&](uint32_t j, uint4 k) {
+                const uint4 cv = lds128(P + 16 * j);
+                slot_st16_at<kSys>(out, 4 + 16 * j, uint4{cv.x ^ k.x, cv.y ^ k.y, cv.z ^ k.z, cv.w ^ k.w});
+            });
 #ifdef QGCM_RES_TRACE
         if (kSys) res_stamp(3);
 #endif

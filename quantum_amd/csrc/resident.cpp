@@ -64,7 +64,7 @@ struct Resident {
     std::atomic<bool> broken{false};
     std::atomic<uint64_t> served{0}, launches{0};
     // callers that stop spinning sleep on a futex; one completion thread watches their done words
-    uint64_t spin_ns = 100000;                          // QGCM_RESIDENT_SPIN_US
+    uint64_t spin_ns = 20000;                           // QGCM_RESIDENT_SPIN_US
     int32_t max_spinners = 8;                           // QGCM_RESIDENT_SPINNERS (default: half the CPU share)
     std::atomic<int32_t> spinners{0};                   // callers spinning now
     std::unique_ptr<std::atomic<uint32_t>[]> want;      // per slot: the sequence a sleeping caller waits for
@@ -193,7 +193,7 @@ Resident *resident_create(int device, const Batch &base, int num_cus) {
     r->P = (uint32_t)env_u64("QGCM_RESIDENT_SLOTS", 16);
     if (r->W < 1 || (int)r->W > num_cus / 2 || r->P < 1 || r->P > kResMaxPerWorker) return nullptr;
     r->S = r->W * r->P;
-    r->spin_ns = env_u64("QGCM_RESIDENT_SPIN_US", 100) * 1000;
+    r->spin_ns = env_u64("QGCM_RESIDENT_SPIN_US", 20) * 1000;
     // callers beyond this many sleep at once instead of spinning: with many more callers than CPUs,
     // spinning ones take the CPUs that posting callers, the completion thread and other host work need
     r->max_spinners = (int32_t)env_u64("QGCM_RESIDENT_SPINNERS", (uint64_t)std::max(1, cpu_share() / 2));
