@@ -1387,23 +1387,40 @@ __device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_t
             z2 ^= cb.z;
             z3 ^= cb.w;
         }
-        // only chains 0..top hold a value (the others skip the multiplies: their lanes would all read
-        // entry 0 of eight different rows, an 8-way bank conflict on every read)
+        // Level l: chains c = 2^l mod 2^(l+1) multiply by H^(2^l) and chains c = 0 mod 2^(l+1) add
+        // that product from chain c + 2^l (only those chains are read later: the sum ends in chain 0).
+        // Levels 0-2 stay within a wave (8 chains per wave: __shfl_down); levels 3-5 go through LDS.
+        // Only chains 0..top hold a value: idle chains skip their multiplies (their lanes would read
+        // entry 0 of eight different rows, an 8-way bank conflict on every read).
         const uint32_t top = d < 63u ? d : 63u;
         const int levels = top ? 32 - __builtin_clz(top) : 0;
         for (int l = 0; l < levels; ++l) {
+            const uint32_t span = 1u << l;
             uint32_t p0 = z0, p1 = z1, p2 = z2, p3 = z3;
-            if (c <= top) ghash_mul8(p0, p1, p2, p3, kTeBytes + l * kGhBytes, e);
-            const uint32_t xb = kOneX + 1024u * (l & 1);  // double-buffered: one barrier per level
-            if (e == 0) lds_st128(xb + 16 * c, uint4{p0, p1, p2, p3});
-            lds_barrier();
-            const uint32_t pc = c + (1u << l);
-            if (pc < 64u) {
-                const uint4 q = lds128(xb + 16 * pc);
-                z0 ^= q.x;
-                z1 ^= q.y;
-                z2 ^= q.z;
-                z3 ^= q.w;
+            if ((c & (2 * span - 1)) == span && c <= top) ghash_mul8(p0, p1, p2, p3, kTeBytes + l * kGhBytes, e);
+            const bool take = (c & (2 * span - 1)) == 0;
+            if (l < 3) {
+                p0 = __shfl_down(p0, 8u << l, 64);
+                p1 = __shfl_down(p1, 8u << l, 64);
+                p2 = __shfl_down(p2, 8u << l, 64);
+                p3 = __shfl_down(p3, 8u << l, 64);
+            } else {
+                const uint32_t xb = kOneX + 1024u * (l & 1);  // double-buffered: one barrier per level
+                if (e == 0 && !take) lds_st128(xb + 16 * c, uint4{p0, p1, p2, p3});
+                lds_barrier();
+                if (take && c + span < 64u) {
+                    const uint4 q = lds128(xb + 16 * (c + span));
+                    p0 = q.x;
+                    p1 = q.y;
+                    p2 = q.z;
+                    p3 = q.w;
+                }
+            }
+            if (take && c + span <= top) {
+                z0 ^= p0;
+                z1 ^= p1;
+                z2 ^= p2;
+                z3 ^= p3;
             }
         }
         // Y = S H^2 (chain 0) + [len(A)]_64 || [len(C)]_64 H (chain 1), in one multiply step
