@@ -1213,13 +1213,6 @@ __device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_t
     const uint32_t n16 = (uint32_t)((4ull + Lin + (kSeal ? QGCM_OVERHEAD : 0) + 15) >> 4);
     const uint32_t L = kSeal ? Lin : Lin - QGCM_OVERHEAD;
     const uint32_t A = kOneBuf + 12u, P = kOneBuf + 16u;  // slot base (AAD), payload base
-    // the column-sliced rounds' keys (step 2): lane q = tid % 4 keeps column q's round keys in VGPRs,
-    // loaded first so their latency hides behind the slot's
-    const Keys kk = {rk_table + (size_t)key * kRkWords, rk_table + (size_t)key * kRkWords + 64};
-    uint32_t rq[11];
-#pragma unroll
-    for (int i = 0; i < 11; ++i) rq[i] = kk.rr[4 * (3 + i) + (tid & 3u)];
-    const uint32_t rl = kk.rk[56 + (tid & 3u)];
     // 1. stage the slot: every load issued before the table fill, so the PCIe round trip overlaps it
     uint4 v[4];
 #pragma unroll
@@ -1278,6 +1271,7 @@ __device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_t
     if (kSys) res_stamp(0);
 #endif
 
+    const Keys kk = {rk_table + (size_t)key * kRkWords, rk_table + (size_t)key * kRkWords + 64};
     const uint32_t lb = (lane & 31u) << 2;
     const uint32_t nfull = L >> 4, r = L & 15u;
     const uint32_t d = nfull + (r ? 1u : 0u);
@@ -1314,6 +1308,10 @@ __device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_t
         if (sliced) {
             const uint32_t j = tid >> 2, q = tid & 3u;
             if (j <= d) {  // quad-uniform: the DPP exchanges stay within active quads
+                uint32_t rq[11];
+#pragma unroll
+                for (int i = 0; i < 11; ++i) rq[i] = kk.rr[4 * (3 + i) + q];  // this column's round keys
+                const uint32_t rl = kk.rk[56 + q];
                 Ctr cc;
                 ctr_setup(cc, n0, n1, n2, 0u, kk, lb);  // every counter here is below 256: one segment
                 const uint32_t ctr = j == d ? 1u : j + 2u;
