@@ -1,6 +1,6 @@
 """Latency of small device-resident uniform batches (qgcm_seal_uniform / qgcm_open_uniform, 1350 B)
 through the latency kernel (the default up to 256 packets; QGCM_ONE_UNIFORM_MAX raises the cut-off
-here) and through the quad batch kernel (QGCM_VARIANT=5 forces it), in one process: one JSON line per batch size with the median microseconds per call."""
+here) and through the quad batch kernel (QGCM_VARIANT=12 forces it), in one process: one JSON line per batch size with the median microseconds per call."""
 import json
 import os
 import statistics
@@ -18,7 +18,7 @@ L = 1350
 key = bytes(range(32))
 ctxs = {}
 os.environ["QGCM_ONE_UNIFORM_MAX"] = "1000000"  # measure the latency kernel past its default cut-off
-for name, env in (("one_kernel", None), ("quad", "5")):
+for name, env in (("one_kernel", None), ("quad", "12")):
     if env:
         os.environ["QGCM_VARIANT"] = env
     c = Context(device=0, max_keys=2)
