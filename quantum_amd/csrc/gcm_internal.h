@@ -81,12 +81,12 @@ struct QuadWorklist {
 hipError_t launch_quad_worklist(const qgcm_desc *descs, uint32_t n, uint32_t max_keys, const uint8_t *key_valid,
                                 bool seal, void *ws, size_t ws_bytes, QuadWorklist *out, hipStream_t s);
 hipError_t launch_packets(bool seal, int variant, const Batch &b, int grid, hipStream_t s);
-// One packet, one 256-thread workgroup (qgcm_seal_one / qgcm_open_one): the slot (b.stride bytes,
+// One packet, one 512-thread workgroup (qgcm_seal_one / qgcm_open_one): the slot (b.stride bytes,
 // a multiple of 16, at most kOneCap - 16) is staged in LDS; b.n must be 1.
 constexpr uint32_t kOneCap = 32768;
 hipError_t launch_one(bool seal, const Batch &b, hipStream_t s);
 
-// Resident per-packet service (resident.cpp): `workers` 256-thread workgroups of gcm_one_kernel's
+// Resident per-packet service (resident.cpp): `workers` 512-thread workgroups of gcm_one_kernel's
 // engine stay on the GPU and serve requests the host posts, so a per-packet call costs no launch.
 // Slot s belongs to worker s / per_worker.  Requests travel in DEVICE memory (fine-grained, which the
 // host CPU writes through the BAR: posted writes, and the GPU polls and reads its own HBM); results

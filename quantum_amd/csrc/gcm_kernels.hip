@@ -1046,23 +1046,25 @@ extern "C" int qgcm_debug_seg_stats(unsigned long long *out, int n, int reset) {
 // crypto/aes.go:41-62 behind plugin/encryption.go:22-37).  The batch kernels give a packet 1-4
 // lanes and stream it from memory block by block; for a lone packet on pinned host memory that
 // means ~85 serial PCIe round trips and 22-85 serial AES+GHASH steps per MTU packet (55 us of
-// kernel at 1350 B).  Here one 256-thread workgroup
-//  1. stages the whole slot [aad|data|tag|nonce] into LDS with one coalesced wave of 16-B loads
-//     (one PCIe round trip) while it fills the T-tables and the comb table of H^4;
-//  2. runs every counter block on its own thread (block j on thread j mod 256; block d = E_K(J0));
-//  3. runs GHASH on the 64 lanes of wave 0: lane m owns the blocks whose exponent in
-//     Y = sum_i B_i H^(N+1-i) is m + 2 mod 64 (the AAD block included), a Horner chain by H^64,
-//     then sum_m Z_m H^m by six radix-2 Estrin levels (multiply by H^(2^l), add the partner lane's
-//     value), then Y = S H^2 + [len(A)]||[len(C)] H -- 2 + 7 serial multiplies at 1350 B where the
-//     quad chains took 23, 16 at 9000 B where they took 142.  The seven comb tables (H^(2^l),
-//     l = 0..6) sit in LDS;
-//  4. writes the slot back with 16-B stores.
-// The write-back overlaps GHASH: a seal's waves 1-3 store the ciphertext rows before the tag while
-// wave 0 hashes; an open's waves 1-3 run the counter blocks and store the plaintext straight from
-// registers while wave 0 hashes the staged ciphertext, and on a tag mismatch (rare) the payload is
-// overwritten with zeros once those stores have landed (as Go 1.9 Open: zeroed plaintext).
+// kernel at 1350 B).  Here one 512-thread workgroup (8 waves, one CU)
+//  1. stages the whole slot [aad|data|tag|nonce] into LDS with one pass of 16-B loads (one memory
+//     round trip) while it fills the T-tables and the comb tables this packet needs;
+//  2. runs the counter blocks column-sliced up to kOneSliceMax blocks (a quad per block, lane q owns
+//     state column q, 4 lookups per round and lane, DPP for the other columns), one lane per block
+//     beyond (block d = E_K(J0));
+//  3. runs GHASH on 64 chains of 8 lanes: chain c owns the blocks whose exponent in
+//     Y = sum_i B_i H^(N+1-i) is c + 2 mod 64 (the AAD block included), a Horner chain by H^64,
+//     then sum_c Z_c H^c by radix-2 Estrin levels (multiply by H^(2^l), add the partner chain's
+//     product), then Y = S H^2 + [len(A)]||[len(C)] H -- 1 + 6 + 1 dependent multiplies at 1350 B
+//     where the quad chains took 23; each multiply is split over the chain's 8 lanes (ghash_mul8).
+//     The seven comb tables (H^(2^l), l = 0..6) sit in LDS;
+//  4. writes the result with 16-B stores, overlapped with GHASH: a seal stores the ciphertext rows
+//     before the tag as soon as the counter blocks are done, an open stores the plaintext straight
+//     from the counter lanes (the staged ciphertext stays for GHASH) and, on a tag mismatch (rare),
+//     overwrites it with zeros once those stores have landed (as Go 1.9 Open: zeroed plaintext).
+// DESIGN.md 4.3 has the device-side timeline of each step.
 // LDS: [0, 64K) Te, [64K, 120K) comb tables of H^(2^l), [120K, 120K + kOneCap) the slot at +12
-// (payload 16-B aligned), then 64 B of scratch (E_K(J0), the GHASH value).
+// (payload 16-B aligned), 64 B of scratch (E_K(J0), the GHASH value), 2 KiB of GHASH exchange.
 constexpr uint32_t kOneThreads = 512;
 constexpr uint32_t kOneTabs = 7;
 constexpr uint32_t kOneBuf = kTeBytes + kOneTabs * kGhBytes;
@@ -1196,7 +1198,7 @@ __device__ __forceinline__ void one_fill_te(const uint32_t *te, uint32_t tid) {
     }
 }
 
-// One packet on one 256-thread workgroup, tables already in LDS except (fill_te) the T-tables and the
+// One packet on one kOneThreads workgroup, tables already in LDS except (fill_te) the T-tables and the
 // comb tables of H^(2^l) that this packet needs beyond what `tab_key` / `tab_n` say is loaded (both
 // workgroup-uniform, updated here; a caller serving several packets puts a workgroup barrier
 // between two calls).  The slot (16-B aligned, (4 + Lin (+ 28 for seal) + 15) & ~15
@@ -1589,7 +1591,7 @@ static_assert(kResLds <= 160u * 1024u, "gfx950 LDS is 160 KiB per workgroup");
 #ifdef QGCM_RES_TRACE
 // per op (open 0, seal 1), sums of: poll -> staged, staged -> stamp 2, staged -> stamp 3, staged ->
 // computed, computed -> acked, count, shader clocks and 100-MHz ticks poll -> acked.  Seal: stamp 2 =
-// counter blocks done, 3 = GHASH done; open: 2 = GHASH done (wave 0), 3 = counter blocks done (waves 1-3).
+// counter blocks done, 3 = GHASH done; open: 3 = counter blocks done (thread 0's), 2 = GHASH done.
 __device__ unsigned long long g_res_trace[16];
 #endif
 
