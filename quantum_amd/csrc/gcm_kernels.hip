@@ -1224,13 +1224,12 @@ __device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_t
     }
     // The table fills load everything first and store after (one memory latency, not one per
     // iteration): Te0/Te1 words for 32 replicas per row, then the comb tables of H^(2^l) -- only the
-    // ones this packet's GHASH reads (H and H^2 always, the Estrin levels up to
-    // bit-length(min(d, 63)), H^64 once a lane owns two blocks) and not loaded yet for this key.
+    // ones this packet's GHASH reads (H^(2^l) for the Estrin levels up to bit-length(min(d + 2, 63)),
+    // H^64 once a chain owns two exponents) and not loaded yet for this key.
     constexpr int kGhIt = kOneTabs * 512 / kOneThreads;  // 7
     const uint4 *gh = b.gh_table + (size_t)key * kGhEntries;
-    const uint32_t dd = (L + 15u) >> 4;
-    const uint32_t dtop = dd < 63u ? dd : 63u;
-    const uint32_t ntabs = dd >= 64u ? kOneTabs : (dtop > 3u ? 32u - __builtin_clz(dtop) : 2u);
+    const uint32_t emax = ((L + 15u) >> 4) + 2u;  // GHASH exponents 1 .. d + 2 (step 3)
+    const uint32_t ntabs = emax >= 64u ? kOneTabs : 32u - __builtin_clz(emax);
     const uint32_t t0 = key == tab_key ? tab_n : 0u;  // tables [0, t0) already hold this key's
     if (fill_te) one_fill_te(b.te, tid);
     if (ntabs > t0) {
@@ -1372,30 +1371,39 @@ __device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_t
     auto ghash = [&]() {
         const uint32_t c = tid >> 3, e = tid & 7u;
         uint32_t z0 = 0, z1 = 0, z2 = 0, z3 = 0;
-        const bool aad_chain = c == (d & 63u) && aad_len;
-        if (aad_chain) z0 = lds32(A) & (aad_len >= 4 ? 0xffffffffu : lowmask(aad_len));
-        // blocks bi = d-1-c-64k >= 0, in increasing order (chain-uniform loop)
-        for (uint32_t bi = (d - 1u - c) & 63u; c < d && bi < d; bi += 64) {
-            uint4 cb = lds128(P + 16 * bi);
-            if (bi == nfull) {
-                cb.x &= m0;
-                cb.y &= m1;
-                cb.z &= m2;
-                cb.w &= m3;
+        // Exponents 1 (the length block) .. d + 2 (the AAD block; zero without additional data), so
+        // Y = sum_c Z_c H^c with no multiply after the tree.  Chain c's exponents e = c (mod 64), highest
+        // first (chain-uniform loop); chain 0's lowest is 64, hence its one more multiply by H^64.
+        const uint32_t emax = d + 2u;
+        const uint32_t ehi = c == 0 ? (emax & ~63u) : (c <= emax ? c + ((emax - c) & ~63u) : 0u);
+        const uint32_t elo = c ? c : 64u;
+        const uint32_t steps = ehi >= elo ? (ehi - elo) / 64u + 1u : 0u;  // ehi = 0: none
+        for (uint32_t k = 0; k < steps; ++k) {
+            const uint32_t ex = ehi - 64u * k;
+            uint4 cb;
+            if (ex == emax) {  // the additional data
+                cb = uint4{aad_len ? lds32(A) & (aad_len >= 4 ? 0xffffffffu : lowmask(aad_len)) : 0u, 0u, 0u, 0u};
+            } else if (ex == 1) {  // [len(A)]_64 || [len(C)]_64 in bits
+                cb = uint4{0u, bswap(aad_len * 8u), 0u, bswap(L * 8u)};
+            } else {  // ciphertext block d + 1 - ex
+                const uint32_t bi = d + 1u - ex;
+                cb = lds128(P + 16 * bi);
+                if (bi == nfull) {
+                    cb.x &= m0;
+                    cb.y &= m1;
+                    cb.z &= m2;
+                    cb.w &= m3;
+                }
             }
-            if (bi >= 64u || aad_chain) ghash_mul8(z0, z1, z2, z3, kTeBytes + 6 * kGhBytes, e);  // H^64
+            if (k) ghash_mul8(z0, z1, z2, z3, kTeBytes + 6 * kGhBytes, e);  // H^64
             z0 ^= cb.x;
             z1 ^= cb.y;
             z2 ^= cb.z;
             z3 ^= cb.w;
         }
-        // Level l: chains c = 2^l mod 2^(l+1) multiply by H^(2^l) and chains c = 0 mod 2^(l+1) add
-        // that product from chain c + 2^l (only those chains are read later: the sum ends in chain 0).
-        // Levels 0-2 stay within a wave (8 chains per wave: __shfl_down); levels 3-5 go through LDS.
-        // Only chains 0..top hold a value: idle chains skip their multiplies (their lanes would read
-        // entry 0 of eight different rows, an 8-way bank conflict on every read).
-        const uint32_t top = d < 63u ? d : 63u;
-        const int levels = top ? 32 - __builtin_clz(top) : 0;
+        if (c == 0 && steps) ghash_mul8(z0, z1, z2, z3, kTeBytes + 6 * kGhBytes, e);
+        const uint32_t top = emax < 63u ? emax : 63u;
+        const int levels = 32 - __builtin_clz(top);  // emax >= 2
         for (int l = 0; l < levels; ++l) {
             const uint32_t span = 1u << l;
             uint32_t p0 = z0, p1 = z1, p2 = z2, p3 = z3;
@@ -1425,18 +1433,6 @@ __device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_t
                 z3 ^= p3;
             }
         }
-        // Y = S H^2 (chain 0) + [len(A)]_64 || [len(C)]_64 H (chain 1), in one multiply step
-        if (c == 1) {
-            z0 = 0;
-            z1 = bswap(aad_len * 8u);
-            z2 = 0;
-            z3 = bswap(L * 8u);
-        }
-        if (c < 2) ghash_mul8(z0, z1, z2, z3, kTeBytes + (c == 0 ? kGhBytes : 0u), e);
-        z0 ^= __shfl_down(z0, 8u, 64);
-        z1 ^= __shfl_down(z1, 8u, 64);
-        z2 ^= __shfl_down(z2, 8u, 64);
-        z3 ^= __shfl_down(z3, 8u, 64);
         if (tid == 0) lds_st128(kOneScratch + 16, uint4{z0, z1, z2, z3});
     };
 
