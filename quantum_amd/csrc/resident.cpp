@@ -57,16 +57,22 @@ struct Resident {
     hipStream_t stream = nullptr;
     std::unique_ptr<uint32_t[]> seqh;                  // last sequence per slot (owned by the slot holder)
     std::unique_ptr<std::atomic<uint32_t>[]> busy;     // slot taken
-    std::unique_ptr<std::atomic<int32_t>[]> inflight;  // requests per worker
-    std::atomic<uint32_t> rr{0};
+    // per worker, each on its own cache line (every call updates them): requests served, callers
+    // spinning now.  A caller's home worker is fixed per thread (quantum's workers are long-lived
+    // locked OS threads), so concurrent callers touch different lines.
+    struct alignas(64) WorkerCounts {
+        std::atomic<uint64_t> served{0};
+        std::atomic<int32_t> spinners{0};
+    };
+    std::unique_ptr<WorkerCounts[]> wc;
     std::mutex launch_mu;
     std::atomic<uint32_t> gen{0};  // generation of the current (or last) instance; 0 = never launched
     std::atomic<bool> broken{false};
-    std::atomic<uint64_t> served{0}, launches{0};
+    std::atomic<uint64_t> launches{0};
     // callers that stop spinning sleep on a futex; one completion thread watches their done words
     uint64_t spin_ns = 20000;                           // QGCM_RESIDENT_SPIN_US
-    int32_t max_spinners = 8;                           // QGCM_RESIDENT_SPINNERS (default: half the CPU share)
-    std::atomic<int32_t> spinners{0};                   // callers spinning now
+    int32_t max_spinners = 8;  // QGCM_RESIDENT_SPINNERS (default: half the CPU share), spread over workers
+    int32_t max_spin_w = 1;    // spinners per worker: ceil(max_spinners / W)
     std::unique_ptr<std::atomic<uint32_t>[]> want;      // per slot: the sequence a sleeping caller waits for
     std::unique_ptr<std::atomic<uint32_t>[]> wake;      // per slot futex word
     std::atomic<uint32_t> sleepers{0};                  // futex word of the completion thread
@@ -224,8 +230,8 @@ Resident *resident_create(int device, const Batch &base, int num_cus) {
     r->seqh.reset(new uint32_t[r->S]());
     r->busy.reset(new std::atomic<uint32_t>[r->S]);
     for (uint32_t i = 0; i < r->S; ++i) r->busy[i] = 0;
-    r->inflight.reset(new std::atomic<int32_t>[r->W]);
-    for (uint32_t i = 0; i < r->W; ++i) r->inflight[i] = 0;
+    r->wc.reset(new Resident::WorkerCounts[r->W]);
+    r->max_spin_w = std::max<int32_t>(1, (r->max_spinners + (int32_t)r->W - 1) / (int32_t)r->W);
     r->want.reset(new std::atomic<uint32_t>[r->S]);
     r->wake.reset(new std::atomic<uint32_t>[r->S]);
     for (uint32_t i = 0; i < r->S; ++i) r->want[i] = r->wake[i] = 0;
@@ -278,7 +284,9 @@ int resident_workers_running(const Resident *r) {
 }
 
 void resident_stats(const Resident *r, uint64_t out[4]) {
-    out[0] = r ? r->served.load() : 0;
+    uint64_t served = 0;
+    for (uint32_t w = 0; r && w < r->W; ++w) served += r->wc[w].served.load(std::memory_order_relaxed);
+    out[0] = served;
     out[1] = r ? r->launches.load() : 0;
     out[2] = r ? r->W * (uint64_t)r->P : 0;
     out[3] = (uint64_t)resident_workers_running(r);
@@ -295,23 +303,15 @@ long resident_call(Resident *r, bool seal, uint32_t key, uint8_t *data, long len
         else if (getrandom(nb, 12, 0) != 12)  // crypto/aes.go:44 rand.Read(nonce)
             return -1;
     }
-    // a free slot of the least-loaded worker (starting round-robin, so ties spread)
-    uint32_t s = 0, w = 0;
+    // a free slot of this thread's home worker, else of the next workers in turn
+    static std::atomic<uint32_t> next_thread{0};
+    thread_local const uint32_t t_index = next_thread.fetch_add(1, std::memory_order_relaxed);
+    const uint32_t home = t_index % r->W;
+    uint32_t s = 0, w = home;
     for (uint32_t tries = 0;; ++tries) {
-        const uint32_t start = r->rr.fetch_add(1, std::memory_order_relaxed) % r->W;
-        w = start;
-        int32_t best = r->inflight[start].load(std::memory_order_relaxed);
-        for (uint32_t i = 1; i < r->W && best > 0; ++i) {
-            const uint32_t c = (start + i) % r->W;
-            const int32_t f = r->inflight[c].load(std::memory_order_relaxed);
-            if (f < best) {
-                best = f;
-                w = c;
-            }
-        }
         bool got = false;
         for (uint32_t k = 0; k < r->W && !got; ++k) {
-            const uint32_t ww = (w + k) % r->W;
+            const uint32_t ww = (home + k) % r->W;
             for (uint32_t i = 0; i < r->P; ++i) {
                 const uint32_t c = ww * r->P + (i + tries) % r->P;
                 uint32_t z = 0;
@@ -327,7 +327,6 @@ long resident_call(Resident *r, bool seal, uint32_t key, uint8_t *data, long len
         if (got) break;
         sched_yield();  // every slot in flight
     }
-    r->inflight[w].fetch_add(1, std::memory_order_relaxed);
     // the request into device memory (write-combined stores through the BAR), then its record: the
     // fields with the old sequence (which the worker has served, so it ignores the record), then the new
     // sequence; sfence orders each step's stores before the next ones
@@ -353,8 +352,8 @@ long resident_call(Resident *r, bool seal, uint32_t key, uint8_t *data, long len
     uint32_t v = 0;
     const auto t0 = std::chrono::steady_clock::now();
     bool asleep = false;
-    bool spinning = r->spinners.fetch_add(1, std::memory_order_relaxed) < r->max_spinners;
-    if (!spinning) r->spinners.fetch_sub(1, std::memory_order_relaxed);
+    bool spinning = r->wc[w].spinners.fetch_add(1, std::memory_order_relaxed) < r->max_spin_w;
+    if (!spinning) r->wc[w].spinners.fetch_sub(1, std::memory_order_relaxed);
     const uint64_t spin_ns = spinning ? r->spin_ns : 0;
     for (uint32_t spins = 0;; ++spins) {
         v = __atomic_load_n(&r->done[s], __ATOMIC_ACQUIRE);
@@ -372,7 +371,7 @@ long resident_call(Resident *r, bool seal, uint32_t key, uint8_t *data, long len
             // callers than CPUs, spinning ones would take the CPUs the posting ones need)
             if (!asleep && (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(waited).count() >= spin_ns) {
                 if (spinning) {
-                    r->spinners.fetch_sub(1, std::memory_order_relaxed);
+                    r->wc[w].spinners.fetch_sub(1, std::memory_order_relaxed);
                     spinning = false;
                 }
                 if (!r->waker.joinable()) {
@@ -397,8 +396,8 @@ long resident_call(Resident *r, bool seal, uint32_t key, uint8_t *data, long len
         r->want[s].store(0, std::memory_order_relaxed);
         r->sleepers.fetch_sub(1);
     }
-    if (spinning) r->spinners.fetch_sub(1, std::memory_order_relaxed);
-    r->served.fetch_add(1, std::memory_order_relaxed);
+    if (spinning) r->wc[w].spinners.fetch_sub(1, std::memory_order_relaxed);
+    r->wc[w].served.fetch_add(1, std::memory_order_relaxed);
     const uint8_t *res = r->out + (size_t)s * kResSlotBytes;
     if (seal) {
         rc = -1;
@@ -410,7 +409,6 @@ long resident_call(Resident *r, bool seal, uint32_t key, uint8_t *data, long len
         memcpy(data, res + 4, (size_t)len - QGCM_OVERHEAD);  // plaintext, or zeros on auth failure
         rc = (v & 1) ? len - QGCM_OVERHEAD : -1;
     }
-    r->inflight[w].fetch_sub(1, std::memory_order_relaxed);
     r->busy[s].store(0, std::memory_order_release);
     return rc;
 }
