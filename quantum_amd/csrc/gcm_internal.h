@@ -122,6 +122,7 @@ int resident_quiesce(Resident *r);
 int resident_workers_running(const Resident *r);
 void resident_stats(const Resident *r, uint64_t out[4]);  // served, launches, slots, workers running
 constexpr long kResNotServed = -1000;  // resident_call: the request does not fit; take the launch path
+bool random_nonce(uint8_t out[12]);   // getrandom, buffered per thread, fork-safe (resident.cpp)
 long resident_call(Resident *r, bool seal, uint32_t key, uint8_t *data, long len, const uint8_t *aad,
                    uint32_t aad_len, const uint8_t *nonce);
 // Small descriptor batches through the latency kernel, one workgroup per packet, straight on the

@@ -224,10 +224,11 @@ Resident *get_resident(qgcm_ctx *ctx) {
     return r;
 }
 
+// Lock-free: every per-packet call asks, from all worker threads at once (key_set is sized once at
+// qgcm_create and its bytes are written under key_mu, set after the device tables are ready).
 bool key_ok(qgcm_ctx *ctx, uint32_t k) {
     if (k >= ctx->max_keys) return false;
-    std::lock_guard<std::mutex> g(ctx->key_mu);
-    return ctx->key_set[k] != 0;
+    return __atomic_load_n(&ctx->key_set[k], __ATOMIC_ACQUIRE) != 0;
 }
 
 }  // namespace
@@ -597,7 +598,7 @@ int qgcm_set_keys(qgcm_ctx *ctx, uint32_t first_idx, uint32_t count, const uint8
     hipFree(d_keys);
     if (rc == QGCM_OK) {
         std::lock_guard<std::mutex> g(ctx->key_mu);
-        for (uint32_t i = 0; i < count; ++i) ctx->key_set[first_idx + i] = 1;
+        for (uint32_t i = 0; i < count; ++i) __atomic_store_n(&ctx->key_set[first_idx + i], (uint8_t)1, __ATOMIC_RELEASE);
     }
     // a running resident instance may hold the old key tables (and key-valid bytes) in its caches:
     // end it; the next per-packet call starts a fresh one
@@ -646,17 +647,17 @@ long qgcm_seal_one(qgcm_ctx *ctx, uint32_t key_idx, uint8_t *data, long length, 
     uint8_t nb[12];
     if (nonce) {
         memcpy(nb, nonce, 12);
-    } else if (getrandom(nb, 12, 0) != 12) {  // crypto/aes.go:44 rand.Read(nonce)
+    } else if (!random_nonce(nb)) {  // crypto/aes.go:44 rand.Read(nonce)
         return -1;
     }
-    if (hipSetDevice(ctx->device) != hipSuccess) return -1;
-    if (Resident *r = get_resident(ctx)) {  // no launch per call
+    if (Resident *r = get_resident(ctx)) {  // no launch per call (and no HIP call)
         const long rc = resident_call(r, true, key_idx, data, length, aad, aad_len, nb);
         if (rc != kResNotServed) {
             ctx->count(QGCM_KERNEL_RESIDENT);
             return rc;
         }
     }
+    if (hipSetDevice(ctx->device) != hipSuccess) return -1;
     const uint64_t stride = ((uint64_t)length + 4 + QGCM_OVERHEAD + 15) & ~15ull;
     std::unique_lock<std::mutex> lk;
     qgcm_ctx::OneSlot *sl = acquire_one(ctx, stride + 16, lk);
@@ -681,14 +682,14 @@ long qgcm_open_one(qgcm_ctx *ctx, uint32_t key_idx, uint8_t *data, long len, con
     if (!ctx || (!data && len) || len < 0 || len - QGCM_OVERHEAD >= (long)QGCM_MAX_PAYLOAD || aad_len > 4 || (aad_len && !aad)) return -1;
     if (len < QGCM_OVERHEAD) return -1;  // crypto/aes.go:58-60: errOpen (the reference panics below 12)
     if (!key_ok(ctx, key_idx)) return -1;
-    if (hipSetDevice(ctx->device) != hipSuccess) return -1;
-    if (Resident *r = get_resident(ctx)) {  // no launch per call
+    if (Resident *r = get_resident(ctx)) {  // no launch per call (and no HIP call)
         const long rc = resident_call(r, false, key_idx, data, len, aad, aad_len, nullptr);
         if (rc != kResNotServed) {
             ctx->count(QGCM_KERNEL_RESIDENT);
             return rc;
         }
     }
+    if (hipSetDevice(ctx->device) != hipSuccess) return -1;
     const uint64_t stride = ((uint64_t)len + 4 + 15) & ~15ull;
     std::unique_lock<std::mutex> lk;
     qgcm_ctx::OneSlot *sl = acquire_one(ctx, stride + 16, lk);

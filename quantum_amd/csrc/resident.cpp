@@ -30,6 +30,8 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <errno.h>
+#include <pthread.h>
 #include <sys/random.h>
 
 #include <algorithm>
@@ -191,6 +193,43 @@ bool device_region(Resident *r, size_t bytes) {
 
 }  // namespace
 
+// 12 bytes from getrandom (crypto/rand in crypto/aes.go:44), drawn 4 KiB at a time per thread: one
+// syscall per 341 nonces instead of one per packet.  A forked child must never reuse its parent's
+// unread bytes (a repeated GCM nonce under one key is fatal), so the buffer is dropped when the
+// process's fork generation (bumped in the child by a pthread_atfork handler) has changed.
+namespace {
+std::atomic<uint32_t> g_fork_gen{0};
+void on_fork_child() { g_fork_gen.fetch_add(1, std::memory_order_relaxed); }
+}  // namespace
+bool random_nonce(uint8_t out[12]) {
+    static std::once_flag once;
+    std::call_once(once, [] { pthread_atfork(nullptr, nullptr, on_fork_child); });
+    struct Buf {
+        uint8_t b[4092];  // a multiple of 12
+        uint32_t pos = sizeof(b);
+        uint32_t gen = 0;
+    };
+    thread_local Buf t;
+    const uint32_t gen = g_fork_gen.load(std::memory_order_relaxed);
+    if (t.pos + 12 > sizeof(t.b) || t.gen != gen) {
+        size_t got = 0;
+        while (got < sizeof(t.b)) {
+            const ssize_t n = getrandom(t.b + got, sizeof(t.b) - got, 0);
+            if (n < 0) {
+                if (errno == EINTR) continue;
+                return false;
+            }
+            got += (size_t)n;
+        }
+        t.pos = 0;
+        t.gen = gen;
+    }
+    memcpy(out, t.b + t.pos, 12);
+    memset(t.b + t.pos, 0, 12);  // consumed bytes do not linger
+    t.pos += 12;
+    return true;
+}
+
 Resident *resident_create(int device, const Batch &base, int num_cus) {
     auto r = std::make_unique<Resident>();
     r->device = device;
@@ -300,7 +339,7 @@ long resident_call(Resident *r, bool seal, uint32_t key, uint8_t *data, long len
     if (seal) {
         if (nonce)
             memcpy(nb, nonce, 12);
-        else if (getrandom(nb, 12, 0) != 12)  // crypto/aes.go:44 rand.Read(nonce)
+        else if (!random_nonce(nb))  // crypto/aes.go:44 rand.Read(nonce)
             return -1;
     }
     // a free slot of this thread's home worker, else of the next workers in turn
@@ -327,9 +366,9 @@ long resident_call(Resident *r, bool seal, uint32_t key, uint8_t *data, long len
         if (got) break;
         sched_yield();  // every slot in flight
     }
-    // the request into device memory (write-combined stores through the BAR), then its record: the
-    // fields with the old sequence (which the worker has served, so it ignores the record), then the new
-    // sequence; sfence orders each step's stores before the next ones
+    // the request into device memory (write-combined stores through the BAR) with its record's fields
+    // under the old sequence (which the worker has served, so it ignores the record), then the new
+    // sequence; sfence orders the first stores before it and pushes it out
     uint8_t *slot = r->in + (size_t)s * kResSlotBytes;
     uint32_t hdr = 0;
     if (aad_len) memcpy(&hdr, aad, aad_len);
@@ -340,10 +379,9 @@ long resident_call(Resident *r, bool seal, uint32_t key, uint8_t *data, long len
     uint32_t q = (q0 + 1) & 0x7fffffffu;
     if (q == 0) q = 1;
     r->seqh[s] = q;
-    _mm_sfence();
     _mm_store_si128(reinterpret_cast<__m128i *>(&r->req[s]),
                     _mm_set_epi32((int)key, (int)len, (int)((seal ? 1u : 0u) | aad_len << 1), (int)q0));
-    _mm_sfence();
+    _mm_sfence();  // the slot bytes and the record's fields before the sequence
     __atomic_store_n(reinterpret_cast<uint32_t *>(&r->req[s]), q, __ATOMIC_RELAXED);
     _mm_sfence();
     long rc = 0;

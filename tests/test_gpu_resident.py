@@ -325,3 +325,43 @@ def test_aad_lengths_and_tamper_kinds(torch):
         assert after["resident"] - before["resident"] == 8 * 30 * 2 and after["one"] == before["one"]
     finally:
         ctx.close()
+
+
+def test_drawn_nonces_unique_and_open(torch):
+    """Seals without an explicit nonce draw it from getrandom, buffered per thread (resident.cpp
+    random_nonce): 8 threads x 2000 seals give 16000 distinct nonces, and every packet opens."""
+    from quantum_amd.crypto import AES
+
+    ctx = make_ctx()
+    try:
+        key = bytes(range(40, 72))
+        aes = AES(key, ctx=ctx)
+        nonces, errs = [], []
+        lock = threading.Lock()
+
+        def work(t):
+            mine = []
+            for i in range(2000):
+                L = 64 + (i % 7)
+                data = bytearray(bytes([t, i & 255]) * (L // 2) + bytes(L % 2) + bytes(28))
+                n, err = aes.Encrypt(data, L, AAD)
+                if err is not None or n != L + 28:
+                    errs.append(f"seal t={t} i={i}")
+                    continue
+                mine.append(bytes(data[L + 16:L + 28]))
+                if i % 50 == 0:
+                    want = bytearray(data)
+                    if O.aesgo_decrypt(key, want, AAD) != L:
+                        errs.append(f"oracle open t={t} i={i}")
+            with lock:
+                nonces.extend(mine)
+
+        ths = [threading.Thread(target=work, args=(t,)) for t in range(8)]
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        assert not errs, errs[:5]
+        assert len(nonces) == 16000 and len(set(nonces)) == 16000
+    finally:
+        ctx.close()
