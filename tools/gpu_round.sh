@@ -56,6 +56,9 @@ for s in $STEPS; do
     res_trace)
       timeout -k 10 300 bash tools/res_trace.sh $TAG
       check res_trace $? ;;
+    c5trace)
+      bash tools/trace_config5.sh $TAG
+      check c5trace $? ;;
     barreq)
       timeout -k 10 400 bash tools/exp_barreq.sh $TAG
       check barreq $? ;;
