@@ -853,7 +853,11 @@ static int run_host_chain(qgcm_ctx *ctx, bool seal, uint8_t *h_arena, uint64_t s
     std::lock_guard<std::mutex> g(ctx->io_mu);
     if (hipSetDevice(ctx->device) != hipSuccess) return QGCM_E_HIP;
     auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
-    uint64_t cpk = (kPipeChunk / stride) & ~255ull;  // whole codec items per chunk
+    static const uint64_t chunk_bytes = [] {  // QGCM_CHAIN_CHUNK_MB: A/B knob for the chunk size
+        const char *v = getenv("QGCM_CHAIN_CHUNK_MB");
+        return v && *v ? (uint64_t)strtoull(v, nullptr, 10) << 20 : kPipeChunk;
+    }();
+    uint64_t cpk = (chunk_bytes / stride) & ~255ull;  // whole codec items per chunk
     if (cpk < 256) cpk = 256;
     if (cpk > n) cpk = n;
     const uint64_t nchunks = (n + cpk - 1) / cpk;

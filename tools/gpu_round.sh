@@ -59,6 +59,9 @@ for s in $STEPS; do
     c5trace)
       bash tools/trace_config5.sh $TAG
       check c5trace $? ;;
+    exp_chain)
+      timeout -k 10 900 bash tools/exp_chain.sh $TAG
+      check exp_chain $? ;;
     barreq)
       timeout -k 10 400 bash tools/exp_barreq.sh $TAG
       check barreq $? ;;
