@@ -208,9 +208,10 @@ void qgcm_host_free(void *p);
 int qgcm_random_nonces(uint8_t *h_out, uint32_t n);
 
 /* ---- snappy block format: the compression plugin (plugin/compression.go) ---- */
-/* Host codec (C++, from the published format; golang/snappy is not in the reference).  Encode output
- * is a valid snappy stream (not golang/snappy's exact bytes); Decode accepts every valid stream and
- * returns -1 on malformed input (compression.go:22-25 decode error). */
+/* Host codec (C++; golang/snappy is not in the reference).  Encode restates golang/snappy's block
+ * encoder (compression.go:17 snappy.Encode), the same bytes as libsnappy 1.1.8 (tests/golden/
+ * snappy.json); Decode accepts every valid stream and returns -1 on malformed input
+ * (compression.go:22-25 decode error). */
 size_t qgcm_snappy_max_compressed_length(size_t n);
 long qgcm_snappy_compress(const uint8_t *src, size_t n, uint8_t *dst, size_t cap);
 long qgcm_snappy_uncompressed_length(const uint8_t *src, size_t n);
@@ -225,13 +226,27 @@ int qgcm_snappy_compress_slots_limit(uint8_t *arena, uint64_t stride, uint32_t n
                                      uint8_t *status, int threads);
 int qgcm_snappy_uncompress_slots(uint8_t *arena, uint64_t stride, uint32_t n, uint32_t *lens,
                                  uint8_t *status, int threads);
+/* Device codec (gfx950, one wave per packet), the same bytes as the host codec: Payload.Raw slots at
+ * i*stride in device memory (stride a multiple of 4), packet i = d_lens[i] bytes at slot+4, replaced
+ * in place (compression.go:39-51), d_lens[i] updated.  compress: packets longer than max_len, or
+ * whose compressed form exceeds limit, fail; uncompress: packets longer than max_len, that do not
+ * decode, or that decode to more than cap bytes fail.  A failed packet's slot and length are
+ * untouched (d_status[i] = 0; 1 = ok; may be NULL).  All limits are at most stride - 4; compress's
+ * max_len and uncompress's cap at most QGCM_SNAPPY_DEVICE_MAX, uncompress's max_len at most
+ * qgcm_snappy_max_compressed_length(QGCM_SNAPPY_DEVICE_MAX).  Asynchronous on stream. */
+#define QGCM_SNAPPY_DEVICE_MAX 16384
+int qgcm_snappy_compress_batch(qgcm_ctx *ctx, uint8_t *d_arena, uint64_t stride, uint32_t n, uint32_t *d_lens,
+                               uint32_t max_len, uint32_t limit, uint8_t *d_status, void *stream);
+int qgcm_snappy_uncompress_batch(qgcm_ctx *ctx, uint8_t *d_arena, uint64_t stride, uint32_t n, uint32_t *d_lens,
+                                 uint32_t max_len, uint32_t cap, uint8_t *d_status, void *stream);
 
 /* ---- Compression + Encryption chain (BASELINE config 5) ---- */
 /* Host batches in the order main.go:50-51 sorts the plugins: outgoing compression.go then
  * encryption.go Apply, incoming the reverse.  Slot i at i*stride holds [aad 4][packet lens[i] B].
  * compress_seal: snappy-compress each packet in place, then seal it (lens[i] <- compressed + 28).
  * open_uncompress: open each sealed packet, then uncompress (lens[i] <- plaintext length).
- * Chunks pipeline the host codec (`threads` workers) with PCIe copies and the device kernels.
+ * Chunks pipeline the codec (`threads` host workers and/or the device codec, qgcm_chain_codec) with
+ * PCIe copies and the device kernels.
  * Returns the number of failed packets (status 0: codec error, no room for the tag and nonce, or
  * failed authentication -- plaintext zeroed as in qgcm_open_batch), or a negative error. */
 int qgcm_compress_seal_host(qgcm_ctx *ctx, uint8_t *h_arena, uint64_t stride, uint32_t n, uint32_t *lens,
@@ -239,6 +254,12 @@ int qgcm_compress_seal_host(qgcm_ctx *ctx, uint8_t *h_arena, uint64_t stride, ui
                             uint8_t *h_status);
 int qgcm_open_uncompress_host(qgcm_ctx *ctx, uint8_t *h_arena, uint64_t stride, uint32_t n, uint32_t *lens,
                               uint32_t key_idx, uint32_t aad_len, int threads, uint8_t *h_status);
+/* Where the chained calls run the snappy codec: 0 = host workers only; 1 = split (default): the device
+ * codec takes the chunks the host workers cannot keep up with (seal: the last untouched chunks when a
+ * stream slot is free and the next host chunk is not compressed yet; open: when the host decode backlog
+ * exceeds a chunk); 2 = device only.  The bytes are the same either way.  Returns the previous mode
+ * (mode -1: just read it) or QGCM_E_ARG.  QGCM_CHAIN_DEVICE sets the initial mode. */
+int qgcm_chain_codec(qgcm_ctx *ctx, int mode);
 
 /* ---- batched UDP I/O (socket/udp.go:35-70, one syscall per batch) ---- */
 /* Datagram i is slot i's Raw[:lens[i]] (wire format [4-B IP][packet]), moved with recvmmsg/sendmmsg
@@ -281,7 +302,9 @@ int qgcm_tun_close(int fd);
 #define QGCM_KERNEL_PER_WAVE 2  /* gcm_quad_kernel, descriptor batches (short key runs) */
 #define QGCM_KERNEL_ONE 3       /* gcm_one_kernel, one workgroup per packet */
 #define QGCM_KERNEL_RESIDENT 4  /* per-packet calls served by the resident kernel (requests, not launches) */
-#define QGCM_KERNEL_COUNTERS 5
+#define QGCM_KERNEL_SNAPPY_ENC 5 /* snappy_compress_kernel (device codec; chained calls: one per device chunk) */
+#define QGCM_KERNEL_SNAPPY_DEC 6 /* snappy_uncompress_kernel */
+#define QGCM_KERNEL_COUNTERS 7
 int qgcm_launch_counts(const qgcm_ctx *ctx, uint64_t *out, int n);
 
 /* ---- measurement: achievable HBM copy rate (reads + writes bytes) for the roofline ---- */

@@ -25,6 +25,7 @@ EXPORTS = (
     "qgcm_snappy_max_compressed_length", "qgcm_snappy_compress", "qgcm_snappy_uncompressed_length",
     "qgcm_snappy_uncompress", "qgcm_snappy_compress_slots", "qgcm_snappy_uncompress_slots",
     "qgcm_snappy_compress_slots_limit", "qgcm_compress_seal_host", "qgcm_open_uncompress_host",
+    "qgcm_snappy_compress_batch", "qgcm_snappy_uncompress_batch", "qgcm_chain_codec",
     "qgcm_udp_socket", "qgcm_udp_queue", "qgcm_udp_port", "qgcm_udp_close", "qgcm_udp_recv_slots",
     "qgcm_udp_send_slots",
     "qgcm_tun_open", "qgcm_tun_up", "qgcm_tun_read_slots", "qgcm_tun_write_slots", "qgcm_tun_close",
@@ -113,6 +114,9 @@ def _bind(L: C.CDLL) -> None:
     L.qgcm_snappy_uncompress_slots.argtypes = [vp, u64, u32, vp, vp, C.c_int]
     L.qgcm_fill_uniform.argtypes = [vp, u64, u32, u32, u32, u64, vp, u64, vp]
     L.qgcm_snappy_compress_slots_limit.argtypes = [vp, u64, u32, vp, u64, vp, C.c_int]
+    L.qgcm_snappy_compress_batch.argtypes = [vp, vp, u64, u32, vp, u32, u32, vp, vp]
+    L.qgcm_snappy_uncompress_batch.argtypes = [vp, vp, u64, u32, vp, u32, u32, vp, vp]
+    L.qgcm_chain_codec.argtypes = [vp, i32]
     L.qgcm_compress_seal_host.argtypes = [vp, vp, u64, u32, vp, u32, vp, u32, C.c_int, vp]
     L.qgcm_open_uncompress_host.argtypes = [vp, vp, u64, u32, vp, u32, u32, C.c_int, vp]
     L.qgcm_udp_socket.argtypes = [C.c_char_p, C.c_int, C.c_int]

@@ -77,6 +77,22 @@ def fill_uniform(arena: torch.Tensor, stride: int, n: int, length: int, aad_word
                                             seed_nonce, _stream_handle(stream)), "qgcm_fill_uniform")
 
 
+def snappy_compress(ctx: Context, arena: torch.Tensor, stride: int, n: int, lens: torch.Tensor, max_len: int,
+                    limit: int, status: torch.Tensor | None = None, stream: torch.cuda.Stream | None = None) -> None:
+    """Device snappy Encode of each slot's packet in place (compression.go Outgoing); `lens` a device
+    int32/uint32 tensor, updated to the compressed lengths."""
+    _lib.check(_lib.lib().qgcm_snappy_compress_batch(ctx.handle, _ptr(arena), stride, n, _ptr(lens), max_len, limit,
+                                                     _ptr(status), _stream_handle(stream)), "qgcm_snappy_compress_batch")
+
+
+def snappy_uncompress(ctx: Context, arena: torch.Tensor, stride: int, n: int, lens: torch.Tensor, max_len: int,
+                      cap: int, status: torch.Tensor | None = None, stream: torch.cuda.Stream | None = None) -> None:
+    """Device snappy Decode of each slot's packet in place (compression.go Incoming)."""
+    _lib.check(_lib.lib().qgcm_snappy_uncompress_batch(ctx.handle, _ptr(arena), stride, n, _ptr(lens), max_len, cap,
+                                                       _ptr(status), _stream_handle(stream)),
+               "qgcm_snappy_uncompress_batch")
+
+
 def host_ptr(buf: bytearray) -> tuple[int, object]:
     arr = (C.c_uint8 * len(buf)).from_buffer(buf)
     return C.addressof(arr), arr
@@ -90,6 +106,11 @@ def compress_seal_host(ctx: Context, arena_ptr: int, stride: int, n: int, lens, 
     return _lib.check(_lib.lib().qgcm_compress_seal_host(ctx.handle, arena_ptr, stride, n, lens.ctypes.data, key_idx,
                                                          nonces_ptr, aad_len, threads, status_ptr),
                       "qgcm_compress_seal_host")
+
+
+def chain_codec(ctx: Context, mode: int = -1) -> int:
+    """Where the chained calls run the snappy codec (0 host, 1 split, 2 device); returns the previous mode."""
+    return _lib.check(_lib.lib().qgcm_chain_codec(ctx.handle, mode), "qgcm_chain_codec")
 
 
 def open_uncompress_host(ctx: Context, arena_ptr: int, stride: int, n: int, lens, key_idx: int,

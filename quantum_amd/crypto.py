@@ -61,9 +61,10 @@ class Context:
 
     def launch_counts(self) -> dict:
         """Kernel launches that served this context's calls so far (qgcm_launch_counts)."""
-        out = (C.c_uint64 * 5)()
-        _lib.check(_lib.lib().qgcm_launch_counts(self.handle, out, 5), "qgcm_launch_counts")
-        return dict(zip(("quad", "segmented", "per_wave", "one", "resident"), (int(x) for x in out)))
+        names = ("quad", "segmented", "per_wave", "one", "resident", "snappy_enc", "snappy_dec")
+        out = (C.c_uint64 * len(names))()
+        _lib.check(_lib.lib().qgcm_launch_counts(self.handle, out, len(names)), "qgcm_launch_counts")
+        return dict(zip(names, (int(x) for x in out)))
 
     def resident_stats(self) -> dict:
         """The resident per-packet kernel: requests served, instances launched, slots, workers running."""

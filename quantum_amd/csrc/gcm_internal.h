@@ -149,6 +149,25 @@ hipError_t launch_move_records(const RecMove *d_moves, uint32_t n, const uint8_t
 // context accessors for the coalescer (coalescer.cpp), defined in qgcm_api.cpp
 int ctx_device(const qgcm_ctx *ctx);
 bool ctx_key_ready(qgcm_ctx *ctx, uint32_t key_idx);
+// Device snappy codec (snappy_kernels.hip): one wave per Payload.Raw slot at i * stride.
+// LDS per wave: [hash table | staged input at off_in | output at off_out], wave_bytes in all.
+constexpr uint32_t kSnapDevMax = 16384;  // longest packet (in and out) the device codec takes
+struct SnapArgs {
+    uint8_t *arena;
+    uint64_t stride;
+    uint32_t n;
+    uint32_t *lens;             // packet lengths, updated on success
+    uint8_t *status;            // 1 ok / 0 failed, may be NULL
+    const uint8_t *status_in;   // uncompress: only packets whose status_in is 1 (NULL: all)
+    qgcm_desc *descs;           // compress: seal descriptors out {i * stride, len or QGCM_MAX_PAYLOAD, key}
+    uint32_t key_idx;
+    uint32_t max_in;            // packets longer than this fail
+    uint32_t limit;             // compress: longest output kept; uncompress: output capacity
+    uint32_t sub;               // uncompress: lens[i] - sub is the compressed length (28 after an open)
+    uint32_t off_in, off_out, wave_bytes;
+};
+hipError_t launch_snappy(bool compress, const SnapArgs &a, int waves_per_wg, int grid, hipStream_t s);
+
 hipError_t launch_key_setup(const uint8_t *d_keys, uint32_t first, uint32_t count, uint32_t *rk_table,
                             uint4 *gh_table, const uint8_t *d_sbox, hipStream_t s);
 hipError_t launch_fill_uniform(uint8_t *arena, uint64_t stride, uint32_t n, uint32_t len, uint32_t aad_word,

@@ -87,6 +87,7 @@ struct qgcm_ctx {
     uint8_t *d_side = nullptr;  // run_host: nonces (12 n) and status (n) of the whole batch
     size_t side_cap = 0;
     qgcm_desc *h_desc = nullptr;  // pinned descriptor staging of the chained (snappy + GCM) path
+    uint32_t *h_lens = nullptr;   // pinned length staging of its device-codec chunks (hdesc_cap entries)
     size_t hdesc_cap = 0;
 
     // orders reuse of the descriptor workspace across streams (guarded by ws_mu)
@@ -95,6 +96,10 @@ struct qgcm_ctx {
 
     std::atomic<uint64_t> launches[QGCM_KERNEL_COUNTERS] = {};  // qgcm_launch_counts
     void count(int k, uint64_t v = 1) { launches[k].fetch_add(v, std::memory_order_relaxed); }
+
+    // where the chained snappy + GCM calls run the codec: 0 host, 1 host/device split, 2 device
+    // (QGCM_CHAIN_DEVICE, qgcm_chain_codec)
+    std::atomic<int> chain_codec{1};
 
     // resident per-packet service (resident.cpp), created on the first per-packet call
     bool res_on = true;  // QGCM_RESIDENT=0: every per-packet call launches gcm_one_kernel
@@ -515,6 +520,7 @@ qgcm_ctx *qgcm_create(int device, uint32_t max_keys, char *err, int errlen) {
     }
     if (const char *v = getenv("QGCM_WGS_PER_CU")) ctx->wgs_per_cu_override = atoi(v);
     if (const char *v = getenv("QGCM_ONE_KERNEL")) ctx->one_kernel = atoi(v) != 0;
+    if (const char *v = getenv("QGCM_CHAIN_DEVICE")) ctx->chain_codec = std::max(0, std::min(2, atoi(v)));
     if (const char *v = getenv("QGCM_RESIDENT")) ctx->res_on = atoi(v) != 0;
     if (const char *v = getenv("QGCM_ONE_UNIFORM_MAX")) ctx->one_uniform_max = (uint32_t)std::max(0, atoi(v));
     if (const char *v = getenv("QGCM_LAUNCH_CHUNK"))  // rounded down to whole 64-packet tiles
@@ -571,6 +577,7 @@ void qgcm_destroy(qgcm_ctx *ctx) {
     hipFree(ctx->d_side);
     if (ctx->h_stat) hipHostFree(ctx->h_stat);
     if (ctx->h_desc) hipHostFree(ctx->h_desc);
+    if (ctx->h_lens) hipHostFree(ctx->h_lens);
     for (hipStream_t p : ctx->pipe)
         if (p) hipStreamDestroy(p);
     if (ctx->ws_done) hipEventDestroy(ctx->ws_done);
@@ -811,21 +818,37 @@ static int run_host(qgcm_ctx *ctx, bool seal, uint8_t *h_arena, uint64_t stride,
     return bad;
 }
 
+// Device snappy batch (snappy_kernels.hip), defined below.
+static int run_snappy(qgcm_ctx *ctx, bool compress, uint8_t *d_arena, uint64_t stride, uint32_t n, uint32_t *d_lens,
+                      uint32_t max_in, uint32_t limit, uint8_t *d_status, const uint8_t *d_status_in,
+                      qgcm_desc *d_descs, uint32_t key_idx, uint32_t sub, hipStream_t s);
+
 // Compression + Encryption chain over host batches (BASELINE config 5; plugin order main.go:50-51:
 // outgoing compression.go then encryption.go, incoming the reverse).  Chunks of ~32 MiB of slots go
-// through three streams as in run_host.  A pool of `threads` codec workers runs for the whole call,
-// taking 256-packet items in chunk order: on seal it compresses ahead and the main thread enqueues a
-// chunk (H2D, seal, D2H) as soon as its items are done; on open the main thread releases a chunk to
-// the workers once its D2H has landed.  Codec, PCIe and the device overlap.  Packet lengths differ
-// after compression, so each chunk is a descriptor batch (one key).
+// through three streams (a stream per chunk: H2D, kernels, D2H in order, three rotating slots).
+// Each chunk's codec runs either on the host -- a pool of `threads` workers for the whole call,
+// 256-packet items -- or on the device (snappy_kernels.hip, the same bytes):
+//  * seal: host workers compress items ahead from the front of the batch; when a stream slot frees
+//    up and the next host chunk is not compressed yet, the device takes the LAST untouched chunk
+//    (whole chunks from the back, claimed against the workers' front by one atomic word), ships it
+//    uncompressed and compresses it in place before the seal.  The host codec and PCIe thus set the
+//    split themselves: the device takes what the host cores cannot keep up with.
+//  * open: chunk by chunk in order; a chunk is decoded on the device when the host workers' backlog
+//    (released, not yet decoded items) exceeds QGCM_CHAIN_DEV_BACKLOG items (default one chunk),
+//    else after its D2H on the host.
+// A device chunk crosses PCIe at full width on the uncompressed side (the host cannot size the rows
+// before the kernel ran); a host chunk's rows are as wide as its longest record.  QGCM_CHAIN_DEVICE:
+// 0 = host codec only, 1 = the split above (default), 2 = device codec only (A/B knobs).
 namespace {
 
 struct CodecPool {
     static constexpr uint32_t kItem = 256;  // packets per work item
-    std::atomic<uint64_t> next{0};          // next item to claim
-    std::atomic<uint64_t> limit{0};         // items released to the workers (open)
+    std::atomic<uint64_t> claim{0};         // seal: front item << 32 | first device chunk
+    std::atomic<uint64_t> next{0};          // open: next item to claim
+    std::atomic<uint64_t> limit{0};         // open: items released to the workers
     std::atomic<bool> stop{false};
     std::unique_ptr<std::atomic<uint32_t>[]> done;  // finished items per chunk
+    std::unique_ptr<std::atomic<uint8_t>[]> on_dev;  // open: chunk decoded on the device (items skipped)
     std::vector<std::thread> workers;
 
     void wait_chunk(uint64_t c, uint32_t items) const {
@@ -840,6 +863,11 @@ struct CodecPool {
         if (!workers.empty()) join();
     }
 };
+
+int env_int(const char *name, int dflt) {
+    const char *v = getenv(name);
+    return v && *v ? atoi(v) : dflt;
+}
 
 }  // namespace
 
@@ -857,14 +885,18 @@ static int run_host_chain(qgcm_ctx *ctx, bool seal, uint8_t *h_arena, uint64_t s
         const char *v = getenv("QGCM_CHAIN_CHUNK_MB");
         return v && *v ? (uint64_t)strtoull(v, nullptr, 10) << 20 : kPipeChunk;
     }();
+    const int dev_mode = ctx->chain_codec.load();
     uint64_t cpk = (chunk_bytes / stride) & ~255ull;  // whole codec items per chunk
     if (cpk < 256) cpk = 256;
     if (cpk > n) cpk = n;
     const uint64_t nchunks = (n + cpk - 1) / cpk;
     const bool non = seal && h_nonces;
     const uint64_t off_non = al(cpk * stride), off_st = off_non + (non ? al(12 * cpk) : 0);
-    const uint64_t off_desc = off_st + al(cpk), slot = off_desc + al(16 * cpk);
+    const uint64_t off_desc = off_st + al(cpk), off_lens = off_desc + al(16 * cpk), slot = off_lens + al(4 * cpk);
     const int nslots = nchunks < (uint64_t)kPipeStreams ? (int)nchunks : kPipeStreams;
+    // every packet a slot can hold fits the device codec, so a chunk's result does not depend on where
+    // its codec ran
+    const bool dev_ok = dev_mode > 0 && stride - 4 <= kSnapDevMax;
     if (slot * nslots > ctx->ring_cap) {
         if (ctx->d_ring) hipFree(ctx->d_ring);
         ctx->d_ring = nullptr;
@@ -880,10 +912,14 @@ static int run_host_chain(qgcm_ctx *ctx, bool seal, uint8_t *h_arena, uint64_t s
         ctx->hstat_cap = n;
     }
     if (cpk * nslots > ctx->hdesc_cap) {
-        if (ctx->h_desc) hipHostFree(ctx->h_desc);
+        for (void *p : {(void *)ctx->h_desc, (void *)ctx->h_lens})
+            if (p) hipHostFree(p);
         ctx->h_desc = nullptr;
+        ctx->h_lens = nullptr;
         ctx->hdesc_cap = 0;
         if (hipHostMalloc(reinterpret_cast<void **>(&ctx->h_desc), cpk * nslots * sizeof(qgcm_desc),
+                          hipHostMallocDefault) != hipSuccess ||
+            hipHostMalloc(reinterpret_cast<void **>(&ctx->h_lens), cpk * nslots * sizeof(uint32_t),
                           hipHostMallocDefault) != hipSuccess)
             return QGCM_E_NOMEM;
         ctx->hdesc_cap = cpk * nslots;
@@ -898,94 +934,184 @@ static int run_host_chain(qgcm_ctx *ctx, bool seal, uint8_t *h_arena, uint64_t s
     };
     CodecPool pool;
     pool.done.reset(new std::atomic<uint32_t>[nchunks]);
-    for (uint64_t c = 0; c < nchunks; ++c) pool.done[c] = 0;
-    if (seal) pool.limit = total_items;
+    pool.on_dev.reset(new std::atomic<uint8_t>[nchunks]);
+    for (uint64_t c = 0; c < nchunks; ++c) {
+        pool.done[c] = 0;
+        pool.on_dev[c] = 0;
+    }
+    pool.claim = nchunks;  // front item 0, no device chunk yet
+    auto process = [&](uint64_t it, std::vector<uint8_t> &tmp) {
+        const uint64_t i0 = it * CodecPool::kItem, i1 = std::min<uint64_t>(n, i0 + CodecPool::kItem);
+        for (uint64_t i = i0; i < i1; ++i) {
+            uint8_t *pkt = h_arena + i * stride + 4;
+            if (seal) {
+                // compression.go:44-51; a packet whose compressed form leaves no room for the
+                // tag and nonce fails, untouched
+                const long c = lens[i] <= max_plain ? qgcm_snappy_compress(pkt, lens[i], tmp.data(), tmp.size()) : -1;
+                if (c < 0 || (uint64_t)c > max_plain) {
+                    codec[i] = 0;
+                } else {
+                    memcpy(pkt, tmp.data(), (size_t)c);
+                    lens[i] = (uint32_t)c;
+                }
+            } else if (ctx->h_stat[i] == 1) {  // compression.go:35-43, on authentic packets only
+                const uint32_t sl = lens[i] - QGCM_OVERHEAD;
+                const long u = qgcm_snappy_uncompress(pkt, sl, tmp.data(), stride - 4);
+                if (u < 0) {
+                    codec[i] = 0;
+                    lens[i] = sl;
+                } else {
+                    memcpy(pkt, tmp.data(), (size_t)u);
+                    lens[i] = (uint32_t)u;
+                }
+            }
+        }
+    };
     auto work = [&] {
         std::vector<uint8_t> tmp(std::max<uint64_t>(stride, qgcm_snappy_max_compressed_length(stride)));
         for (;;) {
-            uint64_t it = pool.next.load();
-            for (;;) {
-                if (it >= total_items || pool.stop) return;
-                if (it < pool.limit.load(std::memory_order_acquire)) {
-                    if (pool.next.compare_exchange_weak(it, it + 1)) break;
-                } else {
-                    std::this_thread::yield();
-                    it = pool.next.load();
+            uint64_t it;
+            if (seal) {  // claim the front item unless the device owns its chunk
+                uint64_t st = pool.claim.load();
+                for (;;) {
+                    const uint64_t f = st >> 32, dlo = st & 0xffffffffull;
+                    if (pool.stop || f >= total_items || f / per_chunk >= dlo) return;
+                    if (pool.claim.compare_exchange_weak(st, st + (1ull << 32))) break;
                 }
-            }
-            const uint64_t i0 = it * CodecPool::kItem, i1 = std::min<uint64_t>(n, i0 + CodecPool::kItem);
-            for (uint64_t i = i0; i < i1; ++i) {
-                uint8_t *pkt = h_arena + i * stride + 4;
-                if (seal) {
-                    // compression.go:44-51; a packet whose compressed form leaves no room for the
-                    // tag and nonce fails, untouched
-                    const long c = lens[i] <= max_plain ? qgcm_snappy_compress(pkt, lens[i], tmp.data(), tmp.size())
-                                                        : -1;
-                    if (c < 0 || (uint64_t)c > max_plain) {
-                        codec[i] = 0;
+                it = st >> 32;
+            } else {
+                it = pool.next.load();
+                for (;;) {
+                    if (it >= total_items || pool.stop) return;
+                    if (it < pool.limit.load(std::memory_order_acquire)) {
+                        if (pool.next.compare_exchange_weak(it, it + 1)) break;
                     } else {
-                        memcpy(pkt, tmp.data(), (size_t)c);
-                        lens[i] = (uint32_t)c;
-                    }
-                } else if (ctx->h_stat[i] == 1) {  // compression.go:35-43, on authentic packets only
-                    const uint32_t sl = lens[i] - QGCM_OVERHEAD;
-                    const long u = qgcm_snappy_uncompress(pkt, sl, tmp.data(), stride - 4);
-                    if (u < 0) {
-                        codec[i] = 0;
-                        lens[i] = sl;
-                    } else {
-                        memcpy(pkt, tmp.data(), (size_t)u);
-                        lens[i] = (uint32_t)u;
+                        std::this_thread::yield();
+                        it = pool.next.load();
                     }
                 }
             }
+            if (seal || !pool.on_dev[it / per_chunk].load(std::memory_order_acquire)) process(it, tmp);
             pool.done[it / per_chunk].fetch_add(1, std::memory_order_release);
         }
     };
-    const int nt = std::max(1, std::min(threads, 256));
+    // seal: the device takes the last chunk no worker has started
+    auto claim_dev = [&]() -> int64_t {
+        uint64_t st = pool.claim.load();
+        for (;;) {
+            const uint64_t f = st >> 32, dlo = st & 0xffffffffull;
+            if (dlo == 0 || (dlo - 1) * per_chunk < f) return -1;
+            if (pool.claim.compare_exchange_weak(st, (f << 32) | (dlo - 1))) return (int64_t)(dlo - 1);
+        }
+    };
+    const int nt = (seal && dev_ok && dev_mode == 2) ? 0 : std::max(1, std::min(threads, 256));
     for (int t = 0; t < nt; ++t) pool.workers.emplace_back(work);
-    int rc = QGCM_OK;
-    for (uint64_t c = 0; c < nchunks && rc == QGCM_OK; ++c) {
-        const int k = (int)(c % nslots);
-        hipStream_t s = ctx->pipe[k];
-        uint8_t *d = ctx->d_ring + k * slot, *d_non = d + off_non, *d_st = d + off_st;
-        qgcm_desc *d_desc = reinterpret_cast<qgcm_desc *>(d + off_desc);
-        qgcm_desc *hd = ctx->h_desc + k * cpk;
+    const uint64_t backlog_max = (uint64_t)env_int("QGCM_CHAIN_DEV_BACKLOG", (int)per_chunk);
+    std::vector<int64_t> slot_chunk(nslots, -1);
+    // a slot's previous chunk has landed: device chunks' lengths back to the caller; open: release
+    // its items to the host workers (device chunks' items are skipped)
+    auto finalize = [&](int k) {
+        const int64_t c = slot_chunk[k];
+        if (c < 0) return;
         const uint64_t c0 = c * cpk, cn = (n - c0) < cpk ? (n - c0) : cpk;
-        uint8_t *h = h_arena + c0 * stride;
-        // chunk c - nslots used this stream's staging: wait for it to land (open: then its packets
-        // can be decompressed)
-        if (c >= (uint64_t)nslots) {
+        if (pool.on_dev[c]) memcpy(lens + c0, ctx->h_lens + (uint64_t)k * cpk, 4 * cn);
+        slot_chunk[k] = -1;
+    };
+    int rc = QGCM_OK;
+    uint64_t host_next = 0, released = 0;
+    for (uint64_t e = 0; rc == QGCM_OK; ++e) {
+        const int k = (int)(e % nslots);
+        hipStream_t s = ctx->pipe[k];
+        if (slot_chunk[k] >= 0) {
             if (hipStreamSynchronize(s) != hipSuccess) {
                 rc = QGCM_E_HIP;
                 break;
             }
-            if (!seal) pool.limit.store((c - nslots + 1) * per_chunk, std::memory_order_release);
+            const int64_t prev = slot_chunk[k];
+            finalize(k);
+            if (!seal) {  // chunks are enqueued in order on open: release up to the one that landed
+                released = std::max<uint64_t>(released, (uint64_t)(prev + 1) * per_chunk);
+                pool.limit.store(std::min<uint64_t>(released, total_items), std::memory_order_release);
+            }
         }
-        if (seal) pool.wait_chunk(c, items_in(c));
-        // Only the bytes a slot uses cross PCIe: the chunk's rows are copied 2-D, each as wide as the
-        // chunk's longest record (AAD, packet, tag||nonce) instead of the whole slot stride --
-        // compressed packets fill ~60% of a 1472-B Payload.Raw.
+        int64_t c = -1;
+        bool dev = false;
+        if (seal) {
+            for (;;) {
+                const uint64_t dlo = pool.claim.load() & 0xffffffffull;
+                if (host_next >= dlo) break;
+                if (pool.done[host_next].load(std::memory_order_acquire) == items_in(host_next)) {
+                    c = (int64_t)host_next++;
+                    break;
+                }
+                if (dev_ok && (c = claim_dev()) >= 0) {
+                    dev = true;
+                    break;
+                }
+                std::this_thread::yield();
+            }
+        } else if (e < nchunks) {
+            c = (int64_t)e;
+            uint64_t backlog = 0;  // released host items not decoded yet
+            for (uint64_t q = 0; q < nchunks && q * per_chunk < released; ++q)
+                if (!pool.on_dev[q]) backlog += items_in(q) - pool.done[q].load(std::memory_order_acquire);
+            dev = dev_ok && (dev_mode == 2 || backlog > backlog_max);
+        }
+        if (c < 0) break;
+        pool.on_dev[c].store(dev ? 1 : 0, std::memory_order_release);
+        slot_chunk[k] = c;
+        uint8_t *d = ctx->d_ring + k * slot, *d_non = d + off_non, *d_st = d + off_st;
+        qgcm_desc *d_desc = reinterpret_cast<qgcm_desc *>(d + off_desc);
+        uint32_t *d_lens = reinterpret_cast<uint32_t *>(d + off_lens);
+        qgcm_desc *hd = ctx->h_desc + k * cpk;
+        uint32_t *hl = ctx->h_lens + (uint64_t)k * cpk;
+        const uint64_t c0 = c * cpk, cn = (n - c0) < cpk ? (n - c0) : cpk;
+        uint8_t *h = h_arena + c0 * stride;
+        // Only the bytes a slot uses cross PCIe: a host chunk's rows are copied 2-D, each as wide as
+        // the chunk's longest record (AAD, packet, tag||nonce) instead of the whole slot stride --
+        // compressed packets fill ~60% of a 1472-B Payload.Raw.  A device chunk's output lengths are
+        // not known when its copies are queued, so its slots travel whole both ways (the bytes past a
+        // packet come back as they went: untouched, as compression.go's copy leaves them).
         uint64_t width = 4;
+        uint32_t max_in = 0;
         for (uint64_t i = 0; i < cn; ++i) {
+            const uint32_t L = lens[c0 + i];
+            if (seal && dev) {
+                max_in = std::max(max_in, L);
+                continue;
+            }
             const bool ok = !seal || codec[c0 + i];
-            hd[i] = qgcm_desc{i * stride, ok ? lens[c0 + i] : QGCM_MAX_PAYLOAD, key_idx};
-            if (ok) width = std::max<uint64_t>(width, 4ull + lens[c0 + i] + (seal ? QGCM_OVERHEAD : 0));
+            hd[i] = qgcm_desc{i * stride, ok ? L : QGCM_MAX_PAYLOAD, key_idx};
+            if (ok) width = std::max<uint64_t>(width, 4ull + L + (seal ? QGCM_OVERHEAD : 0));
+            if (!seal) max_in = std::max(max_in, L >= QGCM_OVERHEAD ? L - (uint32_t)QGCM_OVERHEAD : 0u);
         }
-        width = std::min<uint64_t>(stride, (width + 3) & ~3ull);
-        auto copy = [&](void *dst, const void *src, hipMemcpyKind kind) {
-            return width * 10 >= stride * 9 ? hipMemcpyAsync(dst, src, cn * stride, kind, s)
-                                            : hipMemcpy2DAsync(dst, stride, src, stride, width, cn, kind, s);
+        if (dev) width = stride;
+        max_in = std::min<uint32_t>(max_in, max_plain);  // seal: longer packets fail, as on the host
+        auto copy = [&](void *dst, const void *src, uint64_t w, hipMemcpyKind kind) {
+            w = std::min<uint64_t>(stride, (w + 3) & ~3ull);
+            return w * 10 >= stride * 9 ? hipMemcpyAsync(dst, src, cn * stride, kind, s)
+                                        : hipMemcpy2DAsync(dst, stride, src, stride, w, cn, kind, s);
         };
-        if (copy(d, h, hipMemcpyHostToDevice) != hipSuccess ||
-            hipMemcpyAsync(d_desc, hd, cn * sizeof(qgcm_desc), hipMemcpyHostToDevice, s) != hipSuccess ||
-            (non && hipMemcpyAsync(d_non, h_nonces + 12 * c0, 12 * cn, hipMemcpyHostToDevice, s) != hipSuccess)) {
-            rc = QGCM_E_HIP;
-            break;
+        if (dev) {
+            memcpy(hl, lens + c0, 4 * cn);
+            if (hipMemcpyAsync(d_lens, hl, 4 * cn, hipMemcpyHostToDevice, s) != hipSuccess) rc = QGCM_E_HIP;
         }
-        rc = run_descs(ctx, seal, d, d_desc, (uint32_t)cn, non ? d_non : nullptr, aad_len, d_st, s);
-        if (rc == QGCM_OK && (copy(h, d, hipMemcpyDeviceToHost) != hipSuccess ||
-                              hipMemcpyAsync(ctx->h_stat + c0, d_st, cn, hipMemcpyDeviceToHost, s) != hipSuccess))
+        if (rc == QGCM_OK &&
+            (copy(d, h, width, hipMemcpyHostToDevice) != hipSuccess ||
+             (!(seal && dev) &&
+              hipMemcpyAsync(d_desc, hd, cn * sizeof(qgcm_desc), hipMemcpyHostToDevice, s) != hipSuccess) ||
+             (non && hipMemcpyAsync(d_non, h_nonces + 12 * c0, 12 * cn, hipMemcpyHostToDevice, s) != hipSuccess)))
+            rc = QGCM_E_HIP;
+        if (rc == QGCM_OK && seal && dev)  // compress in place; failures get the sentinel length (seal skips them)
+            rc = run_snappy(ctx, true, d, stride, (uint32_t)cn, d_lens, max_in, max_plain, nullptr, nullptr, d_desc,
+                            key_idx, 0, s);
+        if (rc == QGCM_OK) rc = run_descs(ctx, seal, d, d_desc, (uint32_t)cn, non ? d_non : nullptr, aad_len, d_st, s);
+        if (rc == QGCM_OK && !seal && dev)  // authentic packets only; a failed decode clears the status
+            rc = run_snappy(ctx, false, d, stride, (uint32_t)cn, d_lens, max_in, (uint32_t)(stride - 4), d_st, d_st,
+                            nullptr, 0, QGCM_OVERHEAD, s);
+        if (rc == QGCM_OK && (copy(h, d, width, hipMemcpyDeviceToHost) != hipSuccess ||
+                              hipMemcpyAsync(ctx->h_stat + c0, d_st, cn, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                              (dev && hipMemcpyAsync(hl, d_lens, 4 * cn, hipMemcpyDeviceToHost, s) != hipSuccess)))
             rc = QGCM_E_HIP;
     }
     for (int k = 0; k < nslots; ++k)
@@ -994,8 +1120,10 @@ static int run_host_chain(qgcm_ctx *ctx, bool seal, uint8_t *h_arena, uint64_t s
         pool.join();
         return rc;
     }
+    for (int k = 0; k < nslots; ++k) finalize(k);
     if (!seal) pool.limit.store(total_items, std::memory_order_release);
-    for (uint64_t c = 0; c < nchunks; ++c) pool.wait_chunk(c, items_in(c));
+    for (uint64_t c = 0; c < nchunks; ++c)
+        if (!(seal && pool.on_dev[c])) pool.wait_chunk(c, items_in(c));
     pool.join();
     int bad = 0;
     for (uint32_t i = 0; i < n; ++i) {
@@ -1005,6 +1133,68 @@ static int run_host_chain(qgcm_ctx *ctx, bool seal, uint8_t *h_arena, uint64_t s
         if (h_status) h_status[i] = ok ? 1 : 0;
     }
     return bad;
+}
+
+// Device snappy batch (snappy_kernels.hip): LDS layout per wave, workgroup size and grid from the
+// longest packet the call admits.
+static int run_snappy(qgcm_ctx *ctx, bool compress, uint8_t *d_arena, uint64_t stride, uint32_t n, uint32_t *d_lens,
+                      uint32_t max_in, uint32_t limit, uint8_t *d_status, const uint8_t *d_status_in,
+                      qgcm_desc *d_descs, uint32_t key_idx, uint32_t sub, hipStream_t s) {
+    // compress: inputs up to kSnapDevMax; uncompress: outputs up to kSnapDevMax, inputs up to the longest
+    // stream such an output can have
+    const uint64_t in_max = compress ? kSnapDevMax : qgcm_snappy_max_compressed_length(kSnapDevMax);
+    if (!ctx || (n && (!d_arena || !d_lens)) || (stride & 3) || stride < 4 || max_in > in_max ||
+        max_in > stride - 4 || limit > stride - 4 || (!compress && limit > kSnapDevMax))
+        return QGCM_E_ARG;
+    if (n == 0) return QGCM_OK;
+    auto a16 = [](uint32_t x) { return (x + 15u) & ~15u; };
+    SnapArgs a{};
+    a.arena = d_arena;
+    a.stride = stride;
+    a.n = n;
+    a.lens = d_lens;
+    a.status = d_status;
+    a.status_in = d_status_in;
+    a.descs = d_descs;
+    a.key_idx = key_idx;
+    a.max_in = max_in;
+    a.limit = limit;
+    a.sub = sub;
+    uint32_t tab = 0;
+    if (compress) {
+        uint32_t bits = 8;
+        while (bits < 14 && (1u << bits) < max_in) ++bits;
+        tab = 2u << bits;
+    }
+    a.off_in = tab;
+    a.off_out = a.off_in + a16(max_in + 12);  // + the two slack dwords of stage_in
+    a.wave_bytes = a.off_out + a16((compress ? (uint32_t)qgcm_snappy_max_compressed_length(max_in) : limit) + 8);
+    int waves = 4;
+    while (waves > 1 && (size_t)waves * a.wave_bytes > 64u * 1024u) --waves;
+    int per_cu = (int)((160u * 1024u) / ((uint32_t)waves * a.wave_bytes));
+    per_cu = std::max(1, std::min(per_cu, 8));
+    const uint64_t need = (n + (uint64_t)waves - 1) / waves;
+    const int grid = (int)std::min<uint64_t>(need, (uint64_t)ctx->num_cus * per_cu);
+    if (hipSetDevice(ctx->device) != hipSuccess) return QGCM_E_HIP;
+    ctx->count(compress ? QGCM_KERNEL_SNAPPY_ENC : QGCM_KERNEL_SNAPPY_DEC);
+    return hip_fail(launch_snappy(compress, a, waves, grid, s));
+}
+
+int qgcm_snappy_compress_batch(qgcm_ctx *ctx, uint8_t *d_arena, uint64_t stride, uint32_t n, uint32_t *d_lens,
+                               uint32_t max_len, uint32_t limit, uint8_t *d_status, void *stream) {
+    return run_snappy(ctx, true, d_arena, stride, n, d_lens, max_len, limit, d_status, nullptr, nullptr, 0, 0,
+                      (hipStream_t)stream);
+}
+
+int qgcm_snappy_uncompress_batch(qgcm_ctx *ctx, uint8_t *d_arena, uint64_t stride, uint32_t n, uint32_t *d_lens,
+                                 uint32_t max_len, uint32_t cap, uint8_t *d_status, void *stream) {
+    return run_snappy(ctx, false, d_arena, stride, n, d_lens, max_len, cap, d_status, nullptr, nullptr, 0, 0,
+                      (hipStream_t)stream);
+}
+
+int qgcm_chain_codec(qgcm_ctx *ctx, int mode) {
+    if (!ctx || mode < -1 || mode > 2) return QGCM_E_ARG;
+    return mode < 0 ? ctx->chain_codec.load() : ctx->chain_codec.exchange(mode);
 }
 
 int qgcm_compress_seal_host(qgcm_ctx *ctx, uint8_t *h_arena, uint64_t stride, uint32_t n, uint32_t *lens,

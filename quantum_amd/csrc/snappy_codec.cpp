@@ -13,10 +13,17 @@
 //     11 copy      len 1..64 = 1 + tag bits 2..7, offset = next 4 bytes LE
 //   a copy repeats `len` bytes starting `offset` back in the output (may overlap: RLE).
 //
-// The encoder is a greedy hash matcher (4-byte hash, match extension, copies split at 64 bytes);
-// its output is any valid stream, not golang/snappy's exact bytes (those are parity-unpinned: the
-// tests check round trips and cross-decode with an independent snappy).  The decoder accepts every
-// valid stream and rejects malformed ones without reading or writing out of bounds.
+// The encoder restates golang/snappy's block encoder (encode.go Encode + encode_other.go
+// encodeBlock / emitLiteral / emitCopy, the algorithm the package has used since 2016 -- unpinned in
+// the reference's GOPATH build, Makefile:52-54 -- and the one Google's C++ snappy CompressFragment
+// uses): a 2^8..2^14-entry table of uint16 positions hashed by (u32 * 0x1e35a7bd) >> shift, probes
+// every (skip >> 5) bytes with skip += (skip >> 5) after each miss, no probe within 15 bytes of the
+// block end (inputMargin), after each copy the positions s-1 and s re-hashed and s tried at once,
+// copies split into 64-byte pieces keeping >= 4 for the last, blocks of 64 KiB, inputs shorter than
+// 17 bytes one literal.  Output bytes are checked equal to libsnappy 1.1.8's on a corpus
+// (tests/test_snappy.py); the device encoder (snappy_kernels.hip) is checked equal to this one.  The
+// decoder accepts every valid stream and rejects malformed ones without reading or writing out of
+// bounds.
 #include <stdint.h>
 #include <string.h>
 
@@ -75,6 +82,71 @@ uint8_t *emit_copy(uint8_t *op, size_t offset, size_t len) {
     return emit_copy_upto64(op, offset, len);
 }
 
+constexpr size_t kInputMargin = 15;               // encode.go inputMargin (16 - 1)
+constexpr size_t kMinBlock = 1 + 1 + kInputMargin;  // encode.go minNonLiteralBlockSize
+
+// Length of the common prefix of a[0..) and b[0..), b ending at end (8 bytes at a time, the first
+// differing byte from the XOR's trailing zeros; encode_other.go compares bytewise, same result).
+inline size_t match_len(const uint8_t *a, const uint8_t *b, const uint8_t *end) {
+    size_t m = 0;
+    while (b + m + 8 <= end) {
+        uint64_t x, y;
+        memcpy(&x, a + m, 8);
+        memcpy(&y, b + m, 8);
+        if (x != y) return m + ((size_t)__builtin_ctzll(x ^ y) >> 3);
+        m += 8;
+    }
+    while (b + m < end && a[m] == b[m]) ++m;
+    return m;
+}
+
+// encode_other.go encodeBlock: one block of kMinBlock..65536 bytes.
+uint8_t *encode_block(uint8_t *op, const uint8_t *src, size_t len) {
+    int shift = 24;  // table of 2^8 .. 2^14 entries, the smallest >= len
+    for (size_t ts = 256; ts < (1u << 14) && ts < len; ts <<= 1) --shift;
+    uint16_t table[1 << 14];
+    memset(table, 0, sizeof(uint16_t) << (32 - shift));
+    const size_t s_limit = len - kInputMargin;
+    size_t next_emit = 0, s = 1;
+    uint32_t next_hash = hash4(load32(src + s), shift);
+    for (;;) {
+        size_t skip = 32, next_s = s, cand = 0;
+        for (;;) {  // probe every (skip >> 5) bytes until a 4-byte match
+            s = next_s;
+            const size_t step = skip >> 5;
+            next_s = s + step;
+            skip += step;
+            if (next_s > s_limit) goto remainder;
+            cand = table[next_hash];
+            table[next_hash] = (uint16_t)s;
+            next_hash = hash4(load32(src + next_s), shift);
+            if (load32(src + s) == load32(src + cand)) break;
+        }
+        op = emit_literal(op, src + next_emit, s - next_emit);
+        for (;;) {  // copies back to back while the position after one starts another
+            const size_t base = s;
+            s += 4 + match_len(src + cand + 4, src + s + 4, src + len);
+            op = emit_copy(op, base - cand, s - base);
+            next_emit = s;
+            if (s >= s_limit) goto remainder;
+            uint64_t x;
+            memcpy(&x, src + s - 1, 8);
+            table[hash4((uint32_t)x, shift)] = (uint16_t)(s - 1);
+            const uint32_t h = hash4((uint32_t)(x >> 8), shift);
+            cand = table[h];
+            table[h] = (uint16_t)s;
+            if ((uint32_t)(x >> 8) != load32(src + cand)) {
+                next_hash = hash4((uint32_t)(x >> 16), shift);
+                ++s;
+                break;
+            }
+        }
+    }
+remainder:
+    if (next_emit < len) op = emit_literal(op, src + next_emit, len - next_emit);
+    return op;
+}
+
 }  // namespace
 
 extern "C" {
@@ -91,55 +163,10 @@ long qgcm_snappy_compress(const uint8_t *src, size_t n, uint8_t *dst, size_t cap
         }
         *op++ = (uint8_t)(v | 0x80);
     }
-    // blocks of at most 64 KiB, as the format's 2-byte offsets expect
+    // blocks of at most 64 KiB, as the format's 2-byte offsets expect (encode.go Encode)
     for (size_t base = 0; base < n; base += 65536) {
-        const uint8_t *in = src + base;
         const size_t len = std::min<size_t>(65536, n - base);
-        size_t emit = 0;
-        if (len >= 16) {
-            int bits = 8;
-            while (bits < 14 && (1u << bits) < len) ++bits;
-            const int shift = 32 - bits;
-            uint16_t table[1 << 14];
-            memset(table, 0, sizeof(uint16_t) << bits);
-            const size_t limit = len - 4;  // last position a 4-byte load may start
-            size_t i = 1, skip = 32;
-            while (i <= limit) {
-                const uint32_t cur = load32(in + i);
-                const uint32_t h = hash4(cur, shift);
-                const size_t cand = table[h];
-                table[h] = (uint16_t)i;
-                if (cand < i && load32(in + cand) == cur) {
-                    if (i > emit) op = emit_literal(op, in + emit, i - emit);
-                    // extend the match 8 bytes at a time (the first differing byte from the XOR's
-                    // trailing zeros), then bytewise for the last < 8
-                    size_t m = 4;
-                    for (;;) {
-                        if (i + m + 8 > len) {
-                            while (i + m < len && in[cand + m] == in[i + m]) ++m;
-                            break;
-                        }
-                        uint64_t a, b;
-                        memcpy(&a, in + cand + m, 8);
-                        memcpy(&b, in + i + m, 8);
-                        if (a != b) {
-                            m += (size_t)__builtin_ctzll(a ^ b) >> 3;
-                            break;
-                        }
-                        m += 8;
-                    }
-                    op = emit_copy(op, i - cand, m);
-                    i += m;
-                    emit = i;
-                    skip = 32;
-                    if (i - 1 <= limit) table[hash4(load32(in + i - 1), shift)] = (uint16_t)(i - 1);
-                } else {
-                    i += skip >> 5;  // snappy's heuristic: step further after misses
-                    ++skip;
-                }
-            }
-        }
-        if (emit < len) op = emit_literal(op, in + emit, len - emit);
+        op = len < kMinBlock ? emit_literal(op, src + base, len) : encode_block(op, src + base, len);
     }
     return (long)(op - dst);
 }

@@ -1,0 +1,184 @@
+"""GPU: the device snappy codec (qgcm_snappy_compress_batch / qgcm_snappy_uncompress_batch,
+snappy_kernels.hip) behind plugin/compression.go:16-51.
+
+Bar: byte-exact.  The device encoder's output equals libsnappy 1.1.8's bytes on the golden corpus
+(tests/golden/snappy.json, every case up to the device's 16 KiB limit) and the host encoder's on a
+config-5-shaped batch (whole arena and lengths); the decoder restores every packet, agrees with the
+host decoder on corrupted streams (which packets fail, and the bytes of those that do not), and a
+failing packet's slot and length are untouched."""
+import ctypes as C
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+import snappy_inputs as SI
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "snappy.json")
+DEV_MAX = 16384
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as T
+
+    if not T.cuda.is_available():
+        pytest.skip("no GPU")
+    return T
+
+
+def _lib():
+    from quantum_amd import _lib as L
+
+    return L.lib()
+
+
+def _host_compress(data: bytes) -> bytes:
+    L = _lib()
+    cap = L.qgcm_snappy_max_compressed_length(len(data))
+    dst = C.create_string_buffer(max(cap, 1))
+    n = L.qgcm_snappy_compress(data or None, len(data), dst, cap)
+    assert n > 0
+    return dst.raw[:n]
+
+
+def _host_uncompress(comp: bytes, cap: int):
+    dst = C.create_string_buffer(max(cap, 1))
+    n = _lib().qgcm_snappy_uncompress(comp, len(comp), dst, cap)
+    return None if n < 0 else dst.raw[:n]
+
+
+def _arena(torch, payloads, stride, fill=0xA5):
+    n = len(payloads)
+    host = np.full((n, stride), fill, dtype=np.uint8)
+    for i, p in enumerate(payloads):
+        host[i, 4:4 + len(p)] = np.frombuffer(p, np.uint8)
+    lens = np.array([len(p) for p in payloads], dtype=np.uint32)
+    return host, torch.from_numpy(host.reshape(-1).copy()).cuda(), torch.from_numpy(lens.view(np.int32).copy()).cuda()
+
+
+def _run(torch, ctx, compress, arena, stride, n, lens, max_len, limit):
+    from quantum_amd import batch
+
+    status = torch.full((n,), 7, dtype=torch.uint8, device="cuda")
+    fn = batch.snappy_compress if compress else batch.snappy_uncompress
+    fn(ctx, arena, stride, n, lens, max_len, limit, status)
+    torch.cuda.synchronize()
+    return (arena.cpu().numpy().reshape(n, stride), lens.cpu().numpy().view(np.uint32).copy(),
+            status.cpu().numpy())
+
+
+def _match(case, comp: bytes) -> bool:
+    if len(comp) != case["out_len"]:
+        return False
+    if "out_hex" in case:
+        return comp.hex() == case["out_hex"]
+    return hashlib.sha256(comp).hexdigest() == case["out_sha256"]
+
+
+def test_device_encoder_equals_libsnappy_golden(torch, ctx):
+    with open(GOLDEN) as f:
+        cases = [c for c in json.load(f)["cases"] if c["n"] <= DEV_MAX]
+    datas = [SI.make(c["kind"], c["n"]) for c in cases]
+    stride = (4 + max(_lib().qgcm_snappy_max_compressed_length(len(d)) for d in datas) + 3) // 4 * 4
+    host, arena, lens = _arena(torch, datas, stride)
+    out, ol, st = _run(torch, ctx, True, arena, stride, len(datas), lens, DEV_MAX, stride - 4)
+    assert (st == 1).all()
+    for i, (c, d) in enumerate(zip(cases, datas)):
+        comp = out[i, 4:4 + ol[i]].tobytes()
+        assert _match(c, comp), (c["kind"], c["n"])
+        assert (out[i, 4 + ol[i]:] == host[i, 4 + ol[i]:]).all()  # past the output: untouched
+        assert (out[i, :4] == host[i, :4]).all()
+    # and back: the device decoder restores every case
+    arena2 = torch.from_numpy(out.reshape(-1).copy()).cuda()
+    lens2 = torch.from_numpy(ol.view(np.int32).copy()).cuda()
+    back, bl, st2 = _run(torch, ctx, False, arena2, stride, len(datas), lens2, stride - 4, DEV_MAX)  # stride - 4
+    # = the longest stream of a 16-KiB input, the decoder's input limit
+    assert (st2 == 1).all()
+    for i, d in enumerate(datas):
+        assert bl[i] == len(d) and back[i, 4:4 + len(d)].tobytes() == d
+
+
+def test_device_codec_config5_batch_vs_host(torch, ctx):
+    """2^14 Payload.Raw slots (stride 1472): config 5's packet shape and a mix of lengths 0..1433
+    and contents; device compress == host encoder (whole arena incl. untouched bytes, lengths), then
+    device uncompress restores the plaintext arena."""
+    n, stride = 1 << 14, 1472
+    rng = np.random.default_rng(0x5EED0051)
+    kinds = SI.KINDS
+    payloads = []
+    for i in range(n):
+        L = 1350 if i % 2 == 0 else int(rng.integers(0, 1434))
+        payloads.append(SI.make(kinds[i % len(kinds)], L, seed=i))
+    host, arena, lens = _arena(torch, payloads, stride)
+    limit = stride - 4 - 28  # room for the tag and nonce (run_host_chain's max_plain)
+    out, ol, st = _run(torch, ctx, True, arena, stride, n, lens, stride - 4, limit)
+    # host reference: compress each slot in place with the host encoder
+    ref = host.copy()
+    for i, p in enumerate(payloads):
+        c = _host_compress(p)
+        assert len(c) <= limit
+        ref[i, 4:4 + len(c)] = np.frombuffer(c, np.uint8)
+        assert ol[i] == len(c), i
+    assert (st == 1).all()
+    assert np.array_equal(out, ref)
+    back, bl, st2 = _run(torch, ctx, False, torch.from_numpy(out.reshape(-1).copy()).cuda(), stride, n,
+                         torch.from_numpy(ol.view(np.int32).copy()).cuda(), stride - 4, stride - 4)
+    assert (st2 == 1).all()
+    assert np.array_equal(bl, np.array([len(p) for p in payloads], np.uint32))
+    plain = host.copy()
+    for i, p in enumerate(payloads):  # bytes past the plaintext keep the compressed stream's bytes
+        plain[i, 4 + len(p):] = out[i, 4 + len(p):]
+    assert np.array_equal(back, plain)
+
+
+def test_device_compress_failures_untouched(torch, ctx):
+    """Longer than max_len, or compressed form over limit: status 0, slot and length untouched."""
+    stride = 2048
+    payloads = [SI.make("random", 1500), SI.make("line", 1500), SI.make("random", 900), b"", SI.make("zeros", 40)]
+    host, arena, lens = _arena(torch, payloads, stride)
+    out, ol, st = _run(torch, ctx, True, arena, stride, len(payloads), lens, 1400, 1000)
+    assert list(st) == [0, 0, 1, 1, 1]  # 1500 > max_len; ...; 900 random -> 906 <= 1000
+    for i in (0, 1):
+        assert np.array_equal(out[i], host[i]) and ol[i] == 1500
+    for i in (2, 3, 4):
+        c = _host_compress(payloads[i])
+        assert ol[i] == len(c) and out[i, 4:4 + len(c)].tobytes() == c
+    _, arena, lens = _arena(torch, payloads, stride)
+    out, ol, st = _run(torch, ctx, True, arena, stride, len(payloads), lens, 2000, 800)
+    assert list(st) == [0, 1, 0, 1, 1]  # random 1500 / 900 do not fit 800; the line does
+
+
+def test_device_uncompress_corrupted_streams_vs_host(torch, ctx):
+    """Random corruption of valid streams (and truncations, bad varints, offsets before the output):
+    the device decoder fails exactly where the host decoder does, and otherwise writes its bytes."""
+    rng = np.random.default_rng(0x5EED0052)
+    goods = [_host_compress(SI.make(k, L, seed=j)) for j, (k, L) in
+             enumerate([("words", 1350), ("half", 1350), ("runs", 700), ("line", 300), ("words", 4096)])]
+    streams = [b"", b"\xff\xff\xff\xff\xff\xff", b"\x05\x02\xff", b"\x04\x0d\x01", b"\x03\x08abc",
+               b"\x10\x0cabcd\x01\x00", b"\x80\x80\x80\x80\x10", b"\x04\xf0\xff\xff\xff\xffabcd"]
+    for _ in range(3000):
+        g = bytearray(goods[int(rng.integers(0, len(goods)))])
+        r = rng.random()
+        if r < 0.2:
+            g = g[:int(rng.integers(0, len(g)))]
+        else:
+            for _ in range(int(rng.integers(1, 4))):
+                g[int(rng.integers(0, len(g)))] = int(rng.integers(0, 256))
+        streams.append(bytes(g))
+    streams += goods
+    cap = 4200
+    stride = (4 + max(max(len(s) for s in streams), cap) + 3) // 4 * 4
+    host, arena, lens = _arena(torch, streams, stride)
+    out, ol, st = _run(torch, ctx, False, arena, stride, len(streams), lens, stride - 4, cap)
+    for i, s in enumerate(streams):
+        want = _host_uncompress(s, cap)
+        if want is None:
+            assert st[i] == 0 and ol[i] == len(s) and np.array_equal(out[i], host[i]), i
+        else:
+            assert st[i] == 1 and ol[i] == len(want) and out[i, 4:4 + len(want)].tobytes() == want, i
+    assert st[-len(goods):].all()

@@ -1,15 +1,56 @@
 """CPU: the snappy block codec of the compression plugin (plugin/compression.go) and the plugin
-mirror.  golang/snappy (the reference's encoder) is absent, so its exact output bytes are parity-
-unpinned: the checks are round trips, cross-decoding with independent snappy implementations
-(Google's libsnappy 1.1.8 under /opt/conda and pyarrow's bundled snappy, when importable), and
-malformed-input rejection.  The reference's TestCompression / TestMulti shapes are restated."""
+mirror.  golang/snappy (the reference's encoder) is absent; its block algorithm is Google's C++
+snappy CompressFragment, and libsnappy 1.1.8 is in this image, so the encoder's exact output bytes are
+pinned to libsnappy's: tests/golden/snappy.json (270 cases, tests/golden/make_snappy_golden.py) holds
+them, and both libqgcm's host encoder and the pure-Python restatement oracle/snappy_oracle.py must
+reproduce them.  Also: round trips, cross-decoding with libsnappy and pyarrow's snappy, malformed-input
+rejection, and the reference's TestCompression shape."""
 import ctypes as C
+import hashlib
+import json
 import os
 import random
 
 import pytest
 
+from oracle import snappy_oracle
 from quantum_amd import _lib, common, plugin
+
+import snappy_inputs as SI
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "snappy.json")
+
+
+def _golden_match(case, comp: bytes) -> bool:
+    if len(comp) != case["out_len"]:
+        return False
+    if "out_hex" in case:
+        return comp.hex() == case["out_hex"]
+    return hashlib.sha256(comp).hexdigest() == case["out_sha256"]
+
+
+def test_host_encoder_bytes_equal_libsnappy_golden():
+    with open(GOLDEN) as f:
+        cases = json.load(f)["cases"]
+    assert len(cases) == len(SI.cases())
+    for case in cases:
+        data = SI.make(case["kind"], case["n"])
+        assert hashlib.sha256(data).hexdigest() == case["in_sha256"]
+        comp = _compress(data)
+        assert _golden_match(case, comp), (case["kind"], case["n"])
+        assert _uncompress(comp, len(data)) == data
+
+
+def test_oracle_restatement_equals_golden():
+    with open(GOLDEN) as f:
+        cases = json.load(f)["cases"]
+    for case in cases:
+        if case["n"] > 20000:  # pure-Python loops: the long cases are the host encoder's
+            continue
+        data = SI.make(case["kind"], case["n"])
+        comp = snappy_oracle.encode(data)
+        assert _golden_match(case, comp), (case["kind"], case["n"])
+        assert snappy_oracle.decode(comp) == data
 
 
 def _compress(data: bytes) -> bytes:
@@ -84,6 +125,7 @@ def test_cross_decode_with_libsnappy():
         m = C.c_size_t(cap)
         assert lib.snappy_compress(data, len(data), cbuf, C.byref(m)) == 0
         assert _uncompress(cbuf.raw[:m.value], len(data)) == data  # decode-compatible with Google's encoder
+        assert cbuf.raw[:m.value] == comp  # and the same bytes (the corpus here is not in the golden file)
 
 
 def test_cross_decode_with_pyarrow():

@@ -3,7 +3,7 @@
 # reference build, and the config-2 profile (trace + PMC).  Every GPU step has its own time limit;
 # the script stops at the first step that faults, aborts or times out (a plain test failure goes on).
 # Usage: bash tools/gpu_round.sh <tag> [steps...]
-#   steps: rtests tests smoke bench ab prof pp prof3 exp_res barreq align (default: tests smoke bench ab prof)
+#   steps: stests rtests tests smoke bench ab prof pp prof3 exp_res barreq align (default: tests smoke bench ab prof)
 set -u
 TAG=$1; shift
 STEPS=${*:-"tests smoke bench ab prof"}
@@ -44,6 +44,9 @@ for s in $STEPS; do
         timeout -k 10 120 tools/bin/per_packet_bench $t 1350 2 1 >> $OUT/per_packet.jsonl 2>> $OUT/per_packet.err
         check pp_bulk_$t $?
       done ;;
+    stests)
+      timeout -k 10 300 python3 -u -m pytest tests/test_gpu_snappy.py -x -v --timeout 120 --timeout-method thread > $OUT/snappy_tests.txt 2>&1
+      check stests $? ;;
     rtests)
       timeout -k 10 300 python3 -u -m pytest tests/test_gpu_resident.py -x -v --timeout 120 --timeout-method thread > $OUT/resident_tests.txt 2>&1
       check rtests $? ;;
