@@ -314,13 +314,8 @@ def extra_config5(key: bytes, threads: int, reps: int = 3) -> dict:
     a_ptr, n_ptr = Lb.qgcm_host_alloc(N * stride), Lb.qgcm_host_alloc(12 * N)
     host = np.frombuffer((C.c_uint8 * (N * stride)).from_address(a_ptr), np.uint8).reshape(N, stride)
     nons = np.frombuffer((C.c_uint8 * (12 * N)).from_address(n_ptr), np.uint8)
-    rng = np.random.default_rng(0x5EED0005)
-    host[:, :4] = np.frombuffer(AAD, np.uint8)
-    half = L // 2
-    host[:, 4:4 + half] = rng.integers(0, 256, (N, half), dtype=np.uint8)
-    line = np.frombuffer(b"GET /quantum/v1/peers HTTP/1.1\r\nHost: 10.99.0.1\r\n", np.uint8)
-    host[:, 4 + half:4 + L] = np.tile(line, (L - half) // len(line) + 1)[:L - half]
-    nons[:] = rng.integers(0, 256, 12 * N, dtype=np.uint8)
+    host[:] = config5_packets(N, L, stride)
+    nons[:] = np.random.default_rng(0x5EED0015).integers(0, 256, 12 * N, dtype=np.uint8)
     plain = host[:, :4 + L].copy()
     lens = np.full(N, L, np.uint32)
 
@@ -361,6 +356,72 @@ def extra_config5(key: bytes, threads: int, reps: int = 3) -> dict:
                      "with the gfx950 device codec taking the chunks they cannot keep up with (qgcm_chain_codec 1)",
             "chunks": (N * stride + (32 << 20) - 1) // (32 << 20), "by_codec_mode": modes,
             "status_ok": restored, "restored": restored, "reps": reps}
+
+
+def config5_packets(N: int, L: int, stride: int) -> np.ndarray:
+    """(N, stride) uint8 host slots of config 5: AAD, each packet's first half seeded random bytes, its
+    second half a repeated HTTP request line (the rest of the slot zero)."""
+    host = np.zeros((N, stride), np.uint8)
+    rng = np.random.default_rng(0x5EED0005)
+    host[:, :4] = np.frombuffer(AAD, np.uint8)
+    half = L // 2
+    host[:, 4:4 + half] = rng.integers(0, 256, (N, half), dtype=np.uint8)
+    line = np.frombuffer(b"GET /quantum/v1/peers HTTP/1.1\r\nHost: 10.99.0.1\r\n", np.uint8)
+    host[:, 4 + half:4 + L] = np.tile(line, (L - half) // len(line) + 1)[:L - half]
+    return host
+
+
+def extra_config5_resident(key: bytes, reps: int = 5, N: int = 1 << 20) -> dict:
+    """Config 5's chain with the codec on the GPU and the packets resident in HBM (no PCIe): device
+    snappy compress (writing the seal descriptors) -> seal, then open -> device uncompress, on config
+    5's packets; HIP events per stage, the arena checked against the plaintext after each rep."""
+    L, stride = 1350, 1472
+    ctx = Context(device=0, max_keys=4)
+    ctx.set_key(0, key)
+    plain = torch.from_numpy(config5_packets(N, L, stride).reshape(-1)).cuda()
+    arena = plain.clone()
+    nonces = torch.randint(0, 256, (12 * N,), dtype=torch.uint8, device="cuda")
+    lens = torch.empty(N, dtype=torch.int32, device="cuda")
+    descs = torch.empty(16 * N, dtype=torch.uint8, device="cuda")
+    status = torch.empty(N, dtype=torch.uint8, device="cuda")
+    limit = stride - 4 - 28
+    times = {k: [] for k in ("compress", "seal", "open", "uncompress")}
+    ok, sealed = True, 0
+    for r in range(reps + 1):
+        arena.copy_(plain)
+        lens.fill_(L)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
+        ev[0].record()
+        batch.snappy_compress(ctx, arena, stride, N, lens, stride - 4, limit, status, descs_out=descs, key_idx=0)
+        ev[1].record()
+        batch.seal_batch(ctx, arena, descs, N, nonces, status=status)
+        ev[2].record()
+        torch.cuda.synchronize()
+        ok &= bool((status == 1).all())
+        clen = lens.clone()
+        sealed = int(clen.sum()) + 28 * N
+        d = descs.view(torch.int32).view(N, 4)
+        d[:, 2] += 28  # the receiver's descriptors: sealed lengths (outside the timed stages)
+        ev[3].record()
+        batch.open_batch(ctx, arena, descs, N, status=status)
+        ev[4].record()
+        batch.snappy_uncompress(ctx, arena, stride, N, clen, limit, stride - 4, status)
+        ev[5].record()
+        torch.cuda.synchronize()
+        ok &= bool((status == 1).all()) and bool((clen == L).all())
+        ok &= bool(torch.equal(arena.view(N, stride)[:, :4 + L], plain.view(N, stride)[:, :4 + L]))
+        if r > 0:
+            for k, (a, b) in zip(times, ((0, 1), (1, 2), (3, 4), (4, 5))):
+                times[k].append(ev[a].elapsed_time(ev[b]))
+    med = {k: float(np.median(v)) for k, v in times.items()}
+    ctx.close()
+    total = sum(med.values())
+    return {"workload": f"config5 on device-resident slots: device snappy -> AES-256-GCM and back, {N} x {L} B",
+            "value": round(2 * N * L / (total * 1e-3) / 2**30, 2), "unit": "GiB/s of uncompressed payload (kernels only)",
+            **{f"{k}_ms": round(v, 3) for k, v in med.items()},
+            "compress_GBps": round(N * L / (med["compress"] * 1e-3) / 1e9, 1),
+            "uncompress_GBps": round(N * L / (med["uncompress"] * 1e-3) / 1e9, 1),
+            "sealed_over_plain": round(sealed / (N * L), 4), "status_ok_and_restored": ok, "reps": reps}
 
 
 def free_port() -> int:
@@ -578,6 +639,7 @@ def main() -> None:
             for name, fn in (("config3", lambda: extra_config3(verify=not args.no_verify)),
                              ("e2e_pinned_host", lambda: extra_e2e(key)),
                              ("config5", lambda: extra_config5(key, args.cpu_threads or host["share"])),
+                             ("config5_resident", lambda: extra_config5_resident(key)),
                              ("per_packet", extra_per_packet)):
                 t0 = time.perf_counter()
                 try:

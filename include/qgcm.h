@@ -233,10 +233,14 @@ int qgcm_snappy_uncompress_slots(uint8_t *arena, uint64_t stride, uint32_t n, ui
  * decode, or that decode to more than cap bytes fail.  A failed packet's slot and length are
  * untouched (d_status[i] = 0; 1 = ok; may be NULL).  All limits are at most stride - 4; compress's
  * max_len and uncompress's cap at most QGCM_SNAPPY_DEVICE_MAX, uncompress's max_len at most
- * qgcm_snappy_max_compressed_length(QGCM_SNAPPY_DEVICE_MAX).  Asynchronous on stream. */
+ * qgcm_snappy_max_compressed_length(QGCM_SNAPPY_DEVICE_MAX).  compress also writes, when d_descs_out is
+ * not NULL, the seal descriptor of each packet ({i*stride, compressed length, key_idx}; a failed packet
+ * gets length QGCM_MAX_PAYLOAD, which the seal rejects), so qgcm_seal_batch can follow on the stream
+ * (the chain main.go:50-51 sorts: compression, then encryption).  Asynchronous on stream. */
 #define QGCM_SNAPPY_DEVICE_MAX 16384
 int qgcm_snappy_compress_batch(qgcm_ctx *ctx, uint8_t *d_arena, uint64_t stride, uint32_t n, uint32_t *d_lens,
-                               uint32_t max_len, uint32_t limit, uint8_t *d_status, void *stream);
+                               uint32_t max_len, uint32_t limit, uint8_t *d_status, qgcm_desc *d_descs_out,
+                               uint32_t key_idx, void *stream);
 int qgcm_snappy_uncompress_batch(qgcm_ctx *ctx, uint8_t *d_arena, uint64_t stride, uint32_t n, uint32_t *d_lens,
                                  uint32_t max_len, uint32_t cap, uint8_t *d_status, void *stream);
 

@@ -114,7 +114,7 @@ def _bind(L: C.CDLL) -> None:
     L.qgcm_snappy_uncompress_slots.argtypes = [vp, u64, u32, vp, vp, C.c_int]
     L.qgcm_fill_uniform.argtypes = [vp, u64, u32, u32, u32, u64, vp, u64, vp]
     L.qgcm_snappy_compress_slots_limit.argtypes = [vp, u64, u32, vp, u64, vp, C.c_int]
-    L.qgcm_snappy_compress_batch.argtypes = [vp, vp, u64, u32, vp, u32, u32, vp, vp]
+    L.qgcm_snappy_compress_batch.argtypes = [vp, vp, u64, u32, vp, u32, u32, vp, vp, u32, vp]
     L.qgcm_snappy_uncompress_batch.argtypes = [vp, vp, u64, u32, vp, u32, u32, vp, vp]
     L.qgcm_chain_codec.argtypes = [vp, i32]
     L.qgcm_compress_seal_host.argtypes = [vp, vp, u64, u32, vp, u32, vp, u32, C.c_int, vp]

@@ -78,11 +78,14 @@ def fill_uniform(arena: torch.Tensor, stride: int, n: int, length: int, aad_word
 
 
 def snappy_compress(ctx: Context, arena: torch.Tensor, stride: int, n: int, lens: torch.Tensor, max_len: int,
-                    limit: int, status: torch.Tensor | None = None, stream: torch.cuda.Stream | None = None) -> None:
+                    limit: int, status: torch.Tensor | None = None, descs_out: torch.Tensor | None = None,
+                    key_idx: int = 0, stream: torch.cuda.Stream | None = None) -> None:
     """Device snappy Encode of each slot's packet in place (compression.go Outgoing); `lens` a device
-    int32/uint32 tensor, updated to the compressed lengths."""
+    int32/uint32 tensor, updated to the compressed lengths; `descs_out` (16 n bytes) receives the seal
+    descriptors of the compressed packets."""
     _lib.check(_lib.lib().qgcm_snappy_compress_batch(ctx.handle, _ptr(arena), stride, n, _ptr(lens), max_len, limit,
-                                                     _ptr(status), _stream_handle(stream)), "qgcm_snappy_compress_batch")
+                                                     _ptr(status), _ptr(descs_out), key_idx, _stream_handle(stream)),
+               "qgcm_snappy_compress_batch")
 
 
 def snappy_uncompress(ctx: Context, arena: torch.Tensor, stride: int, n: int, lens: torch.Tensor, max_len: int,

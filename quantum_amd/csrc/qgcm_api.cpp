@@ -1181,9 +1181,10 @@ static int run_snappy(qgcm_ctx *ctx, bool compress, uint8_t *d_arena, uint64_t s
 }
 
 int qgcm_snappy_compress_batch(qgcm_ctx *ctx, uint8_t *d_arena, uint64_t stride, uint32_t n, uint32_t *d_lens,
-                               uint32_t max_len, uint32_t limit, uint8_t *d_status, void *stream) {
-    return run_snappy(ctx, true, d_arena, stride, n, d_lens, max_len, limit, d_status, nullptr, nullptr, 0, 0,
-                      (hipStream_t)stream);
+                               uint32_t max_len, uint32_t limit, uint8_t *d_status, qgcm_desc *d_descs_out,
+                               uint32_t key_idx, void *stream) {
+    return run_snappy(ctx, true, d_arena, stride, n, d_lens, max_len, limit, d_status, nullptr, d_descs_out, key_idx,
+                      0, (hipStream_t)stream);
 }
 
 int qgcm_snappy_uncompress_batch(qgcm_ctx *ctx, uint8_t *d_arena, uint64_t stride, uint32_t n, uint32_t *d_lens,
