@@ -829,10 +829,10 @@ static int run_snappy(qgcm_ctx *ctx, bool compress, uint8_t *d_arena, uint64_t s
 // Each chunk's codec runs either on the host -- a pool of `threads` workers for the whole call,
 // 256-packet items -- or on the device (snappy_kernels.hip, the same bytes):
 //  * seal: host workers compress items ahead from the front of the batch; when a stream slot frees
-//    up and the next host chunk is not compressed yet, the device takes the LAST untouched chunk
-//    (whole chunks from the back, claimed against the workers' front by one atomic word), ships it
-//    uncompressed and compresses it in place before the seal.  The host codec and PCIe thus set the
-//    split themselves: the device takes what the host cores cannot keep up with.
+//    up and fewer than QGCM_CHAIN_DEV_AHEAD (2) compressed host chunks are waiting, the device takes
+//    the LAST untouched chunk (whole chunks from the back, claimed against the workers' front by one
+//    atomic word), ships it uncompressed and compresses it in place before the seal.  The host codec
+//    and PCIe thus set the split themselves: the device takes what the host cores cannot keep up with.
 //  * open: chunk by chunk in order; a chunk is decoded on the device when the host workers' backlog
 //    (released, not yet decoded items) exceeds QGCM_CHAIN_DEV_BACKLOG items (default one chunk),
 //    else after its D2H on the host.
@@ -1006,6 +1006,10 @@ static int run_host_chain(qgcm_ctx *ctx, bool seal, uint8_t *h_arena, uint64_t s
     };
     const int nt = (seal && dev_ok && dev_mode == 2) ? 0 : std::max(1, std::min(threads, 256));
     for (int t = 0; t < nt; ++t) pool.workers.emplace_back(work);
+    // seal: the device takes a chunk when fewer than ahead_min compressed host chunks are waiting as a
+    // stream slot frees up (the host codec is about to stall the pipeline); open: when more than
+    // backlog_max released items wait for the host decoder
+    const uint64_t ahead_min = (uint64_t)std::max(1, env_int("QGCM_CHAIN_DEV_AHEAD", 2));
     const uint64_t backlog_max = (uint64_t)env_int("QGCM_CHAIN_DEV_BACKLOG", (int)per_chunk);
     std::vector<int64_t> slot_chunk(nslots, -1);
     // a slot's previous chunk has landed: device chunks' lengths back to the caller; open: release
@@ -1040,12 +1044,16 @@ static int run_host_chain(qgcm_ctx *ctx, bool seal, uint8_t *h_arena, uint64_t s
             for (;;) {
                 const uint64_t dlo = pool.claim.load() & 0xffffffffull;
                 if (host_next >= dlo) break;
-                if (pool.done[host_next].load(std::memory_order_acquire) == items_in(host_next)) {
-                    c = (int64_t)host_next++;
+                uint64_t ready = 0;  // compressed host chunks waiting, up to ahead_min
+                while (ready < ahead_min && host_next + ready < dlo &&
+                       pool.done[host_next + ready].load(std::memory_order_acquire) == items_in(host_next + ready))
+                    ++ready;
+                if (dev_ok && ready < ahead_min && (c = claim_dev()) >= 0) {
+                    dev = true;
                     break;
                 }
-                if (dev_ok && (c = claim_dev()) >= 0) {
-                    dev = true;
+                if (ready) {
+                    c = (int64_t)host_next++;
                     break;
                 }
                 std::this_thread::yield();

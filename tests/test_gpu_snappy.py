@@ -96,8 +96,8 @@ def test_device_encoder_equals_libsnappy_golden(torch, ctx):
     # and back: the device decoder restores every case
     arena2 = torch.from_numpy(out.reshape(-1).copy()).cuda()
     lens2 = torch.from_numpy(ol.view(np.int32).copy()).cuda()
-    back, bl, st2 = _run(torch, ctx, False, arena2, stride, len(datas), lens2, stride - 4, DEV_MAX)  # stride - 4
-    # = the longest stream of a 16-KiB input, the decoder's input limit
+    in_max = _lib().qgcm_snappy_max_compressed_length(DEV_MAX)  # the decoder's input limit
+    back, bl, st2 = _run(torch, ctx, False, arena2, stride, len(datas), lens2, in_max, DEV_MAX)
     assert (st2 == 1).all()
     for i, d in enumerate(datas):
         assert bl[i] == len(d) and back[i, 4:4 + len(d)].tobytes() == d

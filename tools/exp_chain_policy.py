@@ -1,0 +1,62 @@
+"""Config 5 (bench.extra_config5's workload, host packets, copies included) under the chain's codec
+split knobs, one process: QGCM_CHAIN_DEV_AHEAD (seal) and QGCM_CHAIN_DEV_BACKLOG (open) are read per
+call, so each setting is timed in turn, interleaved over `rounds`.
+
+    python3 tools/exp_chain_policy.py [rounds]
+"""
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import numpy as np  # noqa: E402
+
+import bench  # noqa: E402
+from quantum_amd import _lib, batch  # noqa: E402
+from quantum_amd.crypto import Context  # noqa: E402
+
+
+def main() -> None:
+    rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+    N, L, stride = 1 << 20, 1350, 1472
+    ctx = Context(device=0, max_keys=4)
+    ctx.set_key(0, bench.derive_key(bench.SECRET, bench.SALT))
+    Lb = _lib.lib()
+    a_ptr, n_ptr = Lb.qgcm_host_alloc(N * stride), Lb.qgcm_host_alloc(12 * N)
+    host = np.frombuffer((C.c_uint8 * (N * stride)).from_address(a_ptr), np.uint8).reshape(N, stride)
+    nons = np.frombuffer((C.c_uint8 * (12 * N)).from_address(n_ptr), np.uint8)
+    host[:] = bench.config5_packets(N, L, stride)
+    nons[:] = np.random.default_rng(1).integers(0, 256, 12 * N, dtype=np.uint8)
+    plain = host[:, :4 + L].copy()
+    lens = np.full(N, L, np.uint32)
+    settings = [("host", 0, "2", "0"), ("ahead1", 1, "1", "999999"), ("ahead2", 1, "2", "999999"),
+                ("ahead3", 1, "3", "999999"), ("ahead4", 1, "4", "999999"), ("back0", 1, "2", "0"),
+                ("back45", 1, "2", "45"), ("back90", 1, "2", "90"), ("back180", 1, "2", "180")]
+    res = {name: {"seal": [], "open": [], "dev": []} for name, *_ in settings}
+    for _ in range(rounds):
+        for name, mode, ahead, back in settings:
+            os.environ["QGCM_CHAIN_DEV_AHEAD"], os.environ["QGCM_CHAIN_DEV_BACKLOG"] = ahead, back
+            batch.chain_codec(ctx, mode)
+            c0 = ctx.launch_counts()
+            lens[:] = L
+            t0 = time.perf_counter()
+            bad = batch.compress_seal_host(ctx, a_ptr, stride, N, lens, 0, n_ptr, threads=16)
+            t1 = time.perf_counter()
+            bad += batch.open_uncompress_host(ctx, a_ptr, stride, N, lens, 0, threads=16)
+            t2 = time.perf_counter()
+            c1 = ctx.launch_counts()
+            assert bad == 0 and np.array_equal(host[:, :4 + L], plain), name
+            res[name]["seal"].append(t1 - t0)
+            res[name]["open"].append(t2 - t1)
+            res[name]["dev"].append((c1["snappy_enc"] - c0["snappy_enc"], c1["snappy_dec"] - c0["snappy_dec"]))
+    for name, r in res.items():
+        s, o = float(np.median(r["seal"])), float(np.median(r["open"]))
+        print(json.dumps({"setting": name, "value": round(2 * N * L / (s + o) / 2**30, 2),
+                          "seal_ms": round(1e3 * s, 2), "open_ms": round(1e3 * o, 2), "device_chunks": r["dev"]}))
+
+
+if __name__ == "__main__":
+    main()

@@ -3,7 +3,7 @@
 # reference build, and the config-2 profile (trace + PMC).  Every GPU step has its own time limit;
 # the script stops at the first step that faults, aborts or times out (a plain test failure goes on).
 # Usage: bash tools/gpu_round.sh <tag> [steps...]
-#   steps: stests rtests tests smoke bench ab prof pp prof3 exp_res barreq align (default: tests smoke bench ab prof)
+#   steps: stests policy snapdev rtests tests smoke bench ab prof pp prof3 exp_res barreq align (default: tests smoke bench ab prof)
 set -u
 TAG=$1; shift
 STEPS=${*:-"tests smoke bench ab prof"}
@@ -47,6 +47,12 @@ for s in $STEPS; do
     stests)
       timeout -k 10 300 python3 -u -m pytest tests/test_gpu_snappy.py -x -v --timeout 120 --timeout-method thread > $OUT/snappy_tests.txt 2>&1
       check stests $? ;;
+    policy)
+      timeout -k 10 400 python3 tools/exp_chain_policy.py 3 > $OUT/chain_policy.jsonl 2> $OUT/chain_policy.err
+      check policy $? ;;
+    snapdev)
+      timeout -k 10 200 python3 tools/exp_snappy_dev.py 5 > $OUT/snappy_dev.json 2> $OUT/snappy_dev.err
+      check snapdev $? ;;
     rtests)
       timeout -k 10 300 python3 -u -m pytest tests/test_gpu_resident.py -x -v --timeout 120 --timeout-method thread > $OUT/resident_tests.txt 2>&1
       check rtests $? ;;
