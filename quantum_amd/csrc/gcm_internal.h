@@ -165,6 +165,7 @@ struct SnapArgs {
     uint32_t limit;             // compress: longest output kept; uncompress: output capacity
     uint32_t sub;               // uncompress: lens[i] - sub is the compressed length (28 after an open)
     uint32_t off_in, off_out, wave_bytes;
+    uint32_t serial;            // compress: probe one position at a time (A/B; default: batched probes)
 };
 hipError_t launch_snappy(bool compress, const SnapArgs &a, int waves_per_wg, int grid, hipStream_t s);
 

@@ -46,6 +46,11 @@ struct Wave {
         const uint32_t lo = w[o >> 2], hi = w[(o >> 2) + 1];
         return rfl(__builtin_amdgcn_alignbyte(hi, lo, o & 3));
     }
+    // the same, per lane (o differs across lanes)
+    __device__ __forceinline__ uint32_t load32v(uint32_t o) const {
+        const uint32_t *w = reinterpret_cast<const uint32_t *>(in);
+        return __builtin_amdgcn_alignbyte(w[(o >> 2) + 1], w[o >> 2], o & 3);
+    }
     __device__ __forceinline__ void put(uint32_t o, uint32_t v) const {
         if (lane == 0) out[o] = (uint8_t)v;
     }
@@ -112,19 +117,73 @@ struct Wave {
     }
 };
 
+// B probes of encodeBlock's miss loop at once, lane j = probe j, starting at position s with the
+// given skip.  Each lane rebuilds what the serial loop would have done: its position (the skip
+// recurrence), the table entry it would read -- the latest earlier probe of the batch with the same
+// hash, else the entry from before the batch -- and its 4-byte compare; a ballot finds the first
+// match, and the table receives the positions of the probes up to it (of probes sharing a hash, the
+// last one).  The serial chain of two dependent LDS round trips per probe becomes a few per batch.
+// Returns 0: match at s (cand set); 1: B misses (s, skip advanced); 2: the probes reached s_limit.
+__device__ __forceinline__ int probe_batch(const Wave &w, uint32_t B, uint32_t &s, uint32_t &skip, uint32_t &cand,
+                                           uint32_t s_limit, uint32_t shift) {
+    uint32_t my_p = 0, my_next = 0xffffffffu, p = s, sk = skip, nb = 0;
+    while (nb < B) {
+        const uint32_t step = sk >> 5, nx = p + step;
+        const bool mine = w.lane == nb;
+        my_p = mine ? p : my_p;
+        my_next = mine ? nx : my_next;
+        ++nb;
+        if (nx > s_limit) break;  // that probe is not made: the block's remainder follows
+        p = nx;
+        sk += step;
+    }
+    const bool valid = my_next <= s_limit;  // a prefix of the lanes
+    const uint32_t nvalid = (uint32_t)__builtin_popcountll(ballot(valid));
+    const uint32_t cur = valid ? w.load32v(my_p) : 0u;
+    const uint32_t h = hash4(cur, shift);
+    uint32_t c = valid ? (uint32_t)w.tab[h] : 0u;
+    uint32_t nextsame = 64;  // first later probe of the batch with the same hash (64: none)
+    for (uint32_t i = 0; i < nvalid; ++i) {
+        const uint32_t hi = __builtin_amdgcn_readlane(h, i), pi = __builtin_amdgcn_readlane(my_p, i);
+        const bool same = hi == h;
+        c = same && i < w.lane ? pi : c;
+        nextsame = same && i > w.lane && nextsame == 64 ? i : nextsame;
+    }
+    const uint64_t mm = ballot(valid && w.load32v(c) == cur);
+    const uint32_t last = mm ? (uint32_t)__builtin_ctzll(mm) : 63;  // the last probe made
+    if (valid && w.lane <= last && nextsame > last) w.tab[h] = (uint16_t)my_p;
+    wave_lds_sync();
+    if (mm) {
+        s = __builtin_amdgcn_readlane(my_p, last);
+        cand = __builtin_amdgcn_readlane(c, last);
+        return 0;
+    }
+    if (nvalid < nb || nb < B) return 2;
+    s = p;
+    skip = sk;
+    return 1;
+}
+
 // encode_other.go encodeBlock over the staged block in[0..n), kMinBlock <= n <= 65536; output
-// from out[op]; returns the end of the output.
+// from out[op]; returns the end of the output.  kBatch: the miss loop by probe_batch (the default),
+// else probe by probe (A/B: QGCM_SNAPPY_SERIAL=1).
+template <bool kBatch>
 __device__ uint32_t encode_block(const Wave &w, uint32_t op, uint32_t n, uint32_t bits) {
     const uint32_t shift = 32 - bits;
     for (uint32_t j = w.lane; j < (1u << bits); j += 64) w.tab[j] = 0;
     wave_lds_sync();
     const uint32_t s_limit = n - 15;
     uint32_t next_emit = 0, s = 1;
-    uint32_t next_val = w.load32(1);
+    uint32_t next_val = kBatch ? 0u : w.load32(1);
     uint32_t next_hash = hash4(next_val, shift);
     for (;;) {
         uint32_t skip = 32, next_s = s, cand = 0;
-        for (;;) {
+        if constexpr (kBatch) {
+            int r;
+            uint32_t B = 16;  // short first batch: after a copy the next match is often near
+            while ((r = probe_batch(w, B, s, skip, cand, s_limit, shift)) == 1) B = 64;
+            if (r == 2) goto remainder;
+        } else for (;;) {
             s = next_s;
             const uint32_t cur = next_val;  // load32(s)
             const uint32_t step = skip >> 5;
@@ -151,8 +210,10 @@ __device__ uint32_t encode_block(const Wave &w, uint32_t op, uint32_t n, uint32_
             cand = w.tab_get(h);
             w.tab_set(h, s);
             if (cur != w.load32(cand)) {
-                next_val = w.load32(s + 1);
-                next_hash = hash4(next_val, shift);
+                if constexpr (!kBatch) {
+                    next_val = w.load32(s + 1);
+                    next_hash = hash4(next_val, shift);
+                }
                 ++s;
                 break;
             }
@@ -212,7 +273,7 @@ __global__ void __launch_bounds__(256) snappy_compress_kernel(SnapArgs a) {
             } else {
                 uint32_t bits = 8;
                 while (bits < 14 && (1u << bits) < len) ++bits;
-                op = encode_block(w, op, len, bits);
+                op = a.serial ? encode_block<false>(w, op, len, bits) : encode_block<true>(w, op, len, bits);
             }
             d = op;
             ok = d <= a.limit;
