@@ -53,6 +53,9 @@ for s in $STEPS; do
     snapdev)
       timeout -k 10 200 python3 tools/exp_snappy_dev.py 5 > $OUT/snappy_dev.json 2> $OUT/snappy_dev.err
       check snapdev $? ;;
+    profsnap)
+      timeout -k 10 900 bash tools/profile_snappy.sh $TAG > $OUT/profile_snappy.log 2>&1
+      check profsnap $? ;;
     rtests)
       timeout -k 10 300 python3 -u -m pytest tests/test_gpu_resident.py -x -v --timeout 120 --timeout-method thread > $OUT/resident_tests.txt 2>&1
       check rtests $? ;;
