@@ -150,7 +150,8 @@ hipError_t launch_move_records(const RecMove *d_moves, uint32_t n, const uint8_t
 int ctx_device(const qgcm_ctx *ctx);
 bool ctx_key_ready(qgcm_ctx *ctx, uint32_t key_idx);
 // Device snappy codec (snappy_kernels.hip): one wave per Payload.Raw slot at i * stride.
-// LDS per wave: [hash table | staged input at off_in | output at off_out], wave_bytes in all.
+// LDS per wave: [hash table | staged input at off_in | output at off_out | lane scratch at off_sink],
+// wave_bytes in all.
 constexpr uint32_t kSnapDevMax = 16384;  // longest packet (in and out) the device codec takes
 struct SnapArgs {
     uint8_t *arena;
@@ -164,8 +165,7 @@ struct SnapArgs {
     uint32_t max_in;            // packets longer than this fail
     uint32_t limit;             // compress: longest output kept; uncompress: output capacity
     uint32_t sub;               // uncompress: lens[i] - sub is the compressed length (28 after an open)
-    uint32_t off_in, off_out, wave_bytes;
-    uint32_t serial;            // compress: probe one position at a time (A/B; default: batched probes)
+    uint32_t off_in, off_out, off_sink, wave_bytes;  // off_sink: 256 B of per-lane scratch
 };
 hipError_t launch_snappy(bool compress, const SnapArgs &a, int waves_per_wg, int grid, hipStream_t s);
 

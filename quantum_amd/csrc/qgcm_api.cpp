@@ -1168,7 +1168,6 @@ static int run_snappy(qgcm_ctx *ctx, bool compress, uint8_t *d_arena, uint64_t s
     a.max_in = max_in;
     a.limit = limit;
     a.sub = sub;
-    a.serial = env_int("QGCM_SNAPPY_SERIAL", 0) != 0;
     uint32_t tab = 0;
     if (compress) {
         uint32_t bits = 8;
@@ -1176,8 +1175,9 @@ static int run_snappy(qgcm_ctx *ctx, bool compress, uint8_t *d_arena, uint64_t s
         tab = 2u << bits;
     }
     a.off_in = tab;
-    a.off_out = a.off_in + a16(max_in + 12);  // + the two slack dwords of stage_in
-    a.wave_bytes = a.off_out + a16((compress ? (uint32_t)qgcm_snappy_max_compressed_length(max_in) : limit) + 8);
+    a.off_out = a.off_in + a16(max_in + 24);  // + the 16-B chunks' overhang and stage_in's slack dwords
+    a.off_sink = a.off_out + a16((compress ? (uint32_t)qgcm_snappy_max_compressed_length(max_in) : limit) + 8);
+    a.wave_bytes = a.off_sink + 256;
     int waves = 4;
     while (waves > 1 && (size_t)waves * a.wave_bytes > 64u * 1024u) --waves;
     int per_cu = (int)((160u * 1024u) / ((uint32_t)waves * a.wave_bytes));

@@ -38,6 +38,8 @@ struct Wave {
     uint8_t *in;    // staged packet (+8 B of slack)
     uint8_t *out;   // output staging
     uint16_t *tab;  // encoder hash table
+    uint8_t *sink;  // this lane's 4 scratch bytes: lanes other than 0 store there when lane 0 stores a
+                    // uniform value (one store instruction, no exec-mask branch around it)
     uint32_t lane;
 
     // 4 bytes at byte offset o of the staged input (two aligned dwords, uniform result)
@@ -46,17 +48,10 @@ struct Wave {
         const uint32_t lo = w[o >> 2], hi = w[(o >> 2) + 1];
         return rfl(__builtin_amdgcn_alignbyte(hi, lo, o & 3));
     }
-    // the same, per lane (o differs across lanes)
-    __device__ __forceinline__ uint32_t load32v(uint32_t o) const {
-        const uint32_t *w = reinterpret_cast<const uint32_t *>(in);
-        return __builtin_amdgcn_alignbyte(w[(o >> 2) + 1], w[o >> 2], o & 3);
-    }
-    __device__ __forceinline__ void put(uint32_t o, uint32_t v) const {
-        if (lane == 0) out[o] = (uint8_t)v;
-    }
+    __device__ __forceinline__ void put(uint32_t o, uint32_t v) const { *(lane ? sink : out + o) = (uint8_t)v; }
     __device__ __forceinline__ uint32_t tab_get(uint32_t h) const { return rfl(tab[h]); }
     __device__ __forceinline__ void tab_set(uint32_t h, uint32_t pos) const {
-        if (lane == 0) tab[h] = (uint16_t)pos;
+        *(lane ? reinterpret_cast<uint16_t *>(sink) : tab + h) = (uint16_t)pos;
     }
     // out[op..op+len) = in[from..from+len), all lanes
     __device__ __forceinline__ void copy_in(uint32_t op, uint32_t from, uint32_t len) const {
@@ -117,120 +112,90 @@ struct Wave {
     }
 };
 
-// B probes of encodeBlock's miss loop at once, lane j = probe j, starting at position s with the
-// given skip.  Each lane rebuilds what the serial loop would have done: its position (the skip
-// recurrence), the table entry it would read -- the latest earlier probe of the batch with the same
-// hash, else the entry from before the batch -- and its 4-byte compare; a ballot finds the first
-// match, and the table receives the positions of the probes up to it (of probes sharing a hash, the
-// last one).  The serial chain of two dependent LDS round trips per probe becomes a few per batch.
-// Returns 0: match at s (cand set); 1: B misses (s, skip advanced); 2: the probes reached s_limit.
-__device__ __forceinline__ int probe_batch(const Wave &w, uint32_t B, uint32_t &s, uint32_t &skip, uint32_t &cand,
-                                           uint32_t s_limit, uint32_t shift) {
-    uint32_t my_p = 0, my_next = 0xffffffffu, p = s, sk = skip, nb = 0;
-    while (nb < B) {
-        const uint32_t step = sk >> 5, nx = p + step;
-        const bool mine = w.lane == nb;
-        my_p = mine ? p : my_p;
-        my_next = mine ? nx : my_next;
-        ++nb;
-        if (nx > s_limit) break;  // that probe is not made: the block's remainder follows
-        p = nx;
-        sk += step;
-    }
-    const bool valid = my_next <= s_limit;  // a prefix of the lanes
-    const uint32_t nvalid = (uint32_t)__builtin_popcountll(ballot(valid));
-    const uint32_t cur = valid ? w.load32v(my_p) : 0u;
-    const uint32_t h = hash4(cur, shift);
-    uint32_t c = valid ? (uint32_t)w.tab[h] : 0u;
-    uint32_t nextsame = 64;  // first later probe of the batch with the same hash (64: none)
-    for (uint32_t i = 0; i < nvalid; ++i) {
-        const uint32_t hi = __builtin_amdgcn_readlane(h, i), pi = __builtin_amdgcn_readlane(my_p, i);
-        const bool same = hi == h;
-        c = same && i < w.lane ? pi : c;
-        nextsame = same && i > w.lane && nextsame == 64 ? i : nextsame;
-    }
-    const uint64_t mm = ballot(valid && w.load32v(c) == cur);
-    const uint32_t last = mm ? (uint32_t)__builtin_ctzll(mm) : 63;  // the last probe made
-    if (valid && w.lane <= last && nextsame > last) w.tab[h] = (uint16_t)my_p;
-    wave_lds_sync();
-    if (mm) {
-        s = __builtin_amdgcn_readlane(my_p, last);
-        cand = __builtin_amdgcn_readlane(c, last);
-        return 0;
-    }
-    if (nvalid < nb || nb < B) return 2;
-    s = p;
-    skip = sk;
-    return 1;
-}
-
 // encode_other.go encodeBlock over the staged block in[0..n), kMinBlock <= n <= 65536; output
-// from out[op]; returns the end of the output.  kBatch: the miss loop by probe_batch (the default),
-// else probe by probe (A/B: QGCM_SNAPPY_SERIAL=1).
-template <bool kBatch>
+// from out[op]; returns the end of the output.  One flat loop (the miss probes, and after a match the
+// literal and the run of back-to-back copies) keeps the wave-uniform control flow simple for the
+// compiler: every value that steers it lives in SGPRs.
 __device__ uint32_t encode_block(const Wave &w, uint32_t op, uint32_t n, uint32_t bits) {
     const uint32_t shift = 32 - bits;
     for (uint32_t j = w.lane; j < (1u << bits); j += 64) w.tab[j] = 0;
     wave_lds_sync();
     const uint32_t s_limit = n - 15;
-    uint32_t next_emit = 0, s = 1;
-    uint32_t next_val = kBatch ? 0u : w.load32(1);
-    uint32_t next_hash = hash4(next_val, shift);
+    uint32_t next_emit = 0, s = 1, skip = 32;
+    uint32_t cur = w.load32(1), h = hash4(cur, shift);
     for (;;) {
-        uint32_t skip = 32, next_s = s, cand = 0;
-        if constexpr (kBatch) {
-            int r;
-            uint32_t B = 16;  // short first batch: after a copy the next match is often near
-            while ((r = probe_batch(w, B, s, skip, cand, s_limit, shift)) == 1) B = 64;
-            if (r == 2) goto remainder;
-        } else for (;;) {
+        const uint32_t step = skip >> 5, next_s = s + step;
+        if (next_s > s_limit) break;
+        skip += step;
+        uint32_t cand = w.tab_get(h);
+        w.tab_set(h, s);
+        const uint32_t nv = w.load32(next_s);
+        if (cur != w.load32(cand)) {  // miss: probe further on
             s = next_s;
-            const uint32_t cur = next_val;  // load32(s)
-            const uint32_t step = skip >> 5;
-            next_s = s + step;
-            skip += step;
-            if (next_s > s_limit) goto remainder;
-            cand = w.tab_get(next_hash);
-            w.tab_set(next_hash, s);
-            next_val = w.load32(next_s);
-            next_hash = hash4(next_val, shift);
-            if (cur == w.load32(cand)) break;
+            cur = nv;
+            h = hash4(nv, shift);
+            continue;
         }
         op = w.emit_literal(op, next_emit, s - next_emit);
-        for (;;) {
+        bool more;
+        do {  // copies back to back while the position after one starts another
             const uint32_t base = s;
             s += 4 + w.match_len(cand + 4, s + 4, n);
             op = w.emit_copy(op, base - cand, s - base);
             next_emit = s;
-            if (s >= s_limit) goto remainder;
+            if (s >= s_limit) break;
             w.tab_set(hash4(w.load32(s - 1), shift), s - 1);
             wave_lds_sync();
-            const uint32_t cur = w.load32(s);
-            const uint32_t h = hash4(cur, shift);
+            cur = w.load32(s);
+            h = hash4(cur, shift);
             cand = w.tab_get(h);
             w.tab_set(h, s);
-            if (cur != w.load32(cand)) {
-                if constexpr (!kBatch) {
-                    next_val = w.load32(s + 1);
-                    next_hash = hash4(next_val, shift);
-                }
-                ++s;
-                break;
-            }
-        }
+            more = cur == w.load32(cand);
+        } while (more);
+        if (s >= s_limit) break;
+        ++s;  // the next probe, at s + 1, starts a new miss run
+        skip = 32;
+        cur = w.load32(s);
+        h = hash4(cur, shift);
     }
-remainder:
     if (next_emit < n) op = w.emit_literal(op, next_emit, n - next_emit);
     return op;
 }
 
-// slot bytes [4, 4 + len) -> LDS, whole dwords (the slot is 4-B aligned and at least 4 + len rounded
-// up to 4 bytes long, since stride is a multiple of 4)
-__device__ __forceinline__ void stage_in(uint8_t *dst, const uint8_t *slot, uint32_t len, uint32_t lane) {
+// The next packet of a wave is read while the wave codes the current one: its length (and input
+// status) and the first `cover` bytes of its slot, two 16-B loads per lane, so a packet's HBM
+// latencies overlap the previous packet's work instead of preceding its own.  The loads stay inside
+// the slot whatever the packet's length: cover = min(2 KiB, stride - 4 rounded down to 16).
+struct Prefetch {
+    uint32_t len, st;
+    uint4 r0, r1;
+};
+__device__ __forceinline__ uint32_t pf_cover(uint64_t stride) {
+    const uint64_t whole = (stride - 4) & ~15ull;
+    return whole < 2048 ? (uint32_t)whole : 2048u;
+}
+__device__ __forceinline__ void pf_issue(Prefetch &f, const SnapArgs &a, uint32_t q, uint32_t lane, uint32_t cover) {
+    const uint8_t *src = a.arena + (uint64_t)q * a.stride + 4;
+    f.len = a.lens[q];
+    f.st = a.status_in ? a.status_in[q] : 1u;
+    const uint32_t o0 = 16 * lane, o1 = 1024 + 16 * lane;
+    f.r0 = o0 < cover ? *reinterpret_cast<const uint4 *>(src + o0) : uint4{0, 0, 0, 0};
+    f.r1 = o1 < cover ? *reinterpret_cast<const uint4 *>(src + o1) : uint4{0, 0, 0, 0};
+}
+
+// slot bytes [4, 4 + len) -> LDS: the prefetched chunks, then whole dwords from cover on (the slot is
+// 4-B aligned and at least 4 + len rounded up to 4 bytes long, since stride is a multiple of 4); the
+// staging area holds len + 24 bytes
+__device__ __forceinline__ void stage_in(uint8_t *dst, const uint8_t *slot, uint32_t len, uint32_t lane,
+                                         uint32_t cover, const Prefetch &f) {
+    const uint32_t o0 = 16 * lane, o1 = 1024 + 16 * lane;
+    if (o0 < len && o0 < cover) *reinterpret_cast<uint4 *>(dst + o0) = f.r0;
+    if (o1 < len && o1 < cover) *reinterpret_cast<uint4 *>(dst + o1) = f.r1;
     const uint32_t *src = reinterpret_cast<const uint32_t *>(slot + 4);
     uint32_t *d = reinterpret_cast<uint32_t *>(dst);
     const uint32_t nw = (len + 3) >> 2;
-    for (uint32_t j = lane; j < nw; j += 64) d[j] = src[j];
+    for (uint32_t j = (cover >> 2) + lane; j < nw; j += 64) d[j] = src[j];
+    wave_lds_sync();  // the chunks' bytes past len, then the slack zeros over them
     if (lane < 2) d[nw + lane] = 0;  // slack read by load32 past the end
 }
 
@@ -254,18 +219,23 @@ __device__ __forceinline__ uint32_t put_varint(const Wave &w, uint32_t v) {
     return op;
 }
 
-__global__ void __launch_bounds__(256) snappy_compress_kernel(SnapArgs a) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) snappy_compress_kernel(SnapArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t lane = lane_id(), wv = threadIdx.x >> 6, waves = blockDim.x >> 6;
     uint8_t *base = smem + wv * a.wave_bytes;
-    Wave w{base + a.off_in, base + a.off_out, reinterpret_cast<uint16_t *>(base), lane};
-    for (uint32_t p = blockIdx.x * waves + wv; p < a.n; p += gridDim.x * waves) {
-        const uint32_t len = rfl(a.lens[p]);
+    Wave w{base + a.off_in, base + a.off_out, reinterpret_cast<uint16_t *>(base), base + a.off_sink + 4 * lane, lane};
+    const uint32_t cover = pf_cover(a.stride), step = gridDim.x * waves;
+    uint32_t p = blockIdx.x * waves + wv;
+    Prefetch f{};
+    if (p < a.n) pf_issue(f, a, p, lane, cover);
+    for (; p < a.n; p += step) {
+        const uint32_t len = rfl(f.len);
         uint8_t *slot = a.arena + (uint64_t)p * a.stride;
         bool ok = len <= a.max_in;
+        if (ok) stage_in(w.in, slot, len, lane, cover, f);
+        if (p + step < a.n) pf_issue(f, a, p + step, lane, cover);  // in flight while this packet is coded
         uint32_t d = 0;
         if (ok) {
-            stage_in(w.in, slot, len, lane);
             wave_lds_sync();
             uint32_t op = put_varint(w, len);
             if (len < 17) {
@@ -273,7 +243,7 @@ __global__ void __launch_bounds__(256) snappy_compress_kernel(SnapArgs a) {
             } else {
                 uint32_t bits = 8;
                 while (bits < 14 && (1u << bits) < len) ++bits;
-                op = a.serial ? encode_block<false>(w, op, len, bits) : encode_block<true>(w, op, len, bits);
+                op = encode_block(w, op, len, bits);
             }
             d = op;
             ok = d <= a.limit;
@@ -345,19 +315,26 @@ __device__ int decode(const Wave &w, uint32_t n, uint32_t cap) {
     return op == total ? (int)total : -1;
 }
 
-__global__ void __launch_bounds__(256) snappy_uncompress_kernel(SnapArgs a) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) snappy_uncompress_kernel(SnapArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t lane = lane_id(), wv = threadIdx.x >> 6, waves = blockDim.x >> 6;
     uint8_t *base = smem + wv * a.wave_bytes;
-    Wave w{base + a.off_in, base + a.off_out, nullptr, lane};
-    for (uint32_t p = blockIdx.x * waves + wv; p < a.n; p += gridDim.x * waves) {
-        if (a.status_in && rfl(a.status_in[p]) != 1) continue;  // not authentic: left to the caller
-        const uint32_t stored = rfl(a.lens[p]);
+    Wave w{base + a.off_in, base + a.off_out, nullptr, base + a.off_sink + 4 * lane, lane};
+    const uint32_t cover = pf_cover(a.stride), step = gridDim.x * waves;
+    uint32_t p = blockIdx.x * waves + wv;
+    Prefetch f{};
+    if (p < a.n) pf_issue(f, a, p, lane, cover);
+    for (; p < a.n; p += step) {
+        const bool auth = rfl(f.st) == 1;  // status_in: packets that failed to open are left to the caller
+        const uint32_t stored = rfl(f.len);
         const uint32_t len = stored >= a.sub ? stored - a.sub : stored;
         uint8_t *slot = a.arena + (uint64_t)p * a.stride;
+        const bool take = auth && stored >= a.sub && len <= a.max_in;
+        if (take) stage_in(w.in, slot, len, lane, cover, f);
+        if (p + step < a.n) pf_issue(f, a, p + step, lane, cover);  // in flight while this packet is decoded
+        if (!auth) continue;
         int u = -1;
-        if (stored >= a.sub && len <= a.max_in) {
-            stage_in(w.in, slot, len, lane);
+        if (take) {
             wave_lds_sync();
             u = decode(w, len, a.limit);
             wave_lds_sync();

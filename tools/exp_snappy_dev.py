@@ -20,9 +20,8 @@ def main() -> None:
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 1 << 20
     key = bench.derive_key(bench.SECRET, bench.SALT)
-    for serial in ("1", "0", "1", "0"):  # the encoder's miss loop probe by probe, then batched; twice
-        os.environ["QGCM_SNAPPY_SERIAL"] = serial
-        print(json.dumps(dict(serial=serial, **bench.extra_config5_resident(key, reps, n))), flush=True)
+    for _ in range(2):
+        print(json.dumps(bench.extra_config5_resident(key, reps, n)), flush=True)
 
 
 if __name__ == "__main__":
