@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "../../include/qgcm.h"
+#include "chain_claim.h"
 #include "gcm_internal.h"
 
 using namespace qgcm;
@@ -843,7 +844,7 @@ namespace {
 
 struct CodecPool {
     static constexpr uint32_t kItem = 256;  // packets per work item
-    std::atomic<uint64_t> claim{0};         // seal: front item << 32 | first device chunk
+    ChunkClaims claim;                      // seal: host items from the front, device chunks from the back
     std::atomic<uint64_t> next{0};          // open: next item to claim
     std::atomic<uint64_t> limit{0};         // open: items released to the workers
     std::atomic<bool> stop{false};
@@ -881,10 +882,8 @@ static int run_host_chain(qgcm_ctx *ctx, bool seal, uint8_t *h_arena, uint64_t s
     std::lock_guard<std::mutex> g(ctx->io_mu);
     if (hipSetDevice(ctx->device) != hipSuccess) return QGCM_E_HIP;
     auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
-    static const uint64_t chunk_bytes = [] {  // QGCM_CHAIN_CHUNK_MB: A/B knob for the chunk size
-        const char *v = getenv("QGCM_CHAIN_CHUNK_MB");
-        return v && *v ? (uint64_t)strtoull(v, nullptr, 10) << 20 : kPipeChunk;
-    }();
+    // QGCM_CHAIN_CHUNK_MB: A/B knob for the chunk size (read per call, like the split knobs below)
+    const uint64_t chunk_bytes = (uint64_t)std::max(1, env_int("QGCM_CHAIN_CHUNK_MB", (int)(kPipeChunk >> 20))) << 20;
     const int dev_mode = ctx->chain_codec.load();
     uint64_t cpk = (chunk_bytes / stride) & ~255ull;  // whole codec items per chunk
     if (cpk < 256) cpk = 256;
@@ -939,7 +938,7 @@ static int run_host_chain(qgcm_ctx *ctx, bool seal, uint8_t *h_arena, uint64_t s
         pool.done[c] = 0;
         pool.on_dev[c] = 0;
     }
-    pool.claim = nchunks;  // front item 0, no device chunk yet
+    pool.claim.reset(nchunks, total_items, per_chunk);
     auto process = [&](uint64_t it, std::vector<uint8_t> &tmp) {
         const uint64_t i0 = it * CodecPool::kItem, i1 = std::min<uint64_t>(n, i0 + CodecPool::kItem);
         for (uint64_t i = i0; i < i1; ++i) {
@@ -972,13 +971,9 @@ static int run_host_chain(qgcm_ctx *ctx, bool seal, uint8_t *h_arena, uint64_t s
         for (;;) {
             uint64_t it;
             if (seal) {  // claim the front item unless the device owns its chunk
-                uint64_t st = pool.claim.load();
-                for (;;) {
-                    const uint64_t f = st >> 32, dlo = st & 0xffffffffull;
-                    if (pool.stop || f >= total_items || f / per_chunk >= dlo) return;
-                    if (pool.claim.compare_exchange_weak(st, st + (1ull << 32))) break;
-                }
-                it = st >> 32;
+                const int64_t c = pool.stop ? -1 : pool.claim.claim_item();
+                if (c < 0) return;
+                it = (uint64_t)c;
             } else {
                 it = pool.next.load();
                 for (;;) {
@@ -993,15 +988,6 @@ static int run_host_chain(qgcm_ctx *ctx, bool seal, uint8_t *h_arena, uint64_t s
             }
             if (seal || !pool.on_dev[it / per_chunk].load(std::memory_order_acquire)) process(it, tmp);
             pool.done[it / per_chunk].fetch_add(1, std::memory_order_release);
-        }
-    };
-    // seal: the device takes the last chunk no worker has started
-    auto claim_dev = [&]() -> int64_t {
-        uint64_t st = pool.claim.load();
-        for (;;) {
-            const uint64_t f = st >> 32, dlo = st & 0xffffffffull;
-            if (dlo == 0 || (dlo - 1) * per_chunk < f) return -1;
-            if (pool.claim.compare_exchange_weak(st, (f << 32) | (dlo - 1))) return (int64_t)(dlo - 1);
         }
     };
     const int nt = (seal && dev_ok && dev_mode == 2) ? 0 : std::max(1, std::min(threads, 256));
@@ -1042,13 +1028,13 @@ static int run_host_chain(qgcm_ctx *ctx, bool seal, uint8_t *h_arena, uint64_t s
         bool dev = false;
         if (seal) {
             for (;;) {
-                const uint64_t dlo = pool.claim.load() & 0xffffffffull;
+                const uint64_t dlo = pool.claim.device_from();
                 if (host_next >= dlo) break;
                 uint64_t ready = 0;  // compressed host chunks waiting, up to ahead_min
                 while (ready < ahead_min && host_next + ready < dlo &&
                        pool.done[host_next + ready].load(std::memory_order_acquire) == items_in(host_next + ready))
                     ++ready;
-                if (dev_ok && ready < ahead_min && (c = claim_dev()) >= 0) {
+                if (dev_ok && ready < ahead_min && (c = pool.claim.claim_chunk()) >= 0) {
                     dev = true;
                     break;
                 }

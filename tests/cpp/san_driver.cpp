@@ -5,13 +5,19 @@
 //           EXACT-size heap buffers (an overrun is an ASan report); the multi-threaded slot
 //           compress/uncompress (TSan).
 //   keymath: PBKDF2-HMAC-SHA512 and X25519 on a fixed vector (UB / overruns).
+//   chain_claim.h: host workers claiming items from the front while the device claims chunks from
+//           the back (TSan): every item is taken exactly once, by one side, and a device chunk by
+//           no worker.
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
 #include <random>
+#include <thread>
 #include <vector>
 
+#include "../../quantum_amd/csrc/chain_claim.h"
 #include "qgcm.h"
 
 static int fail(const char *what) {
@@ -79,6 +85,38 @@ int main(int argc, char **argv) {
     for (uint32_t i = 0; i < n; ++i)
         if (lens[i] != orig[i] || memcmp(&arena[i * stride + 4], &plain[i * stride + 4], orig[i]))
             return fail("slot round trip");
+    // the chained codec's front/back claims (chain_claim.h) from 8 worker threads and a device thread
+    for (int round = 0; round < 200; ++round) {
+        const uint64_t per = 1 + rng() % 40, nchunks = 1 + rng() % 24;
+        const uint64_t items = (nchunks - 1) * per + 1 + rng() % per;  // a short last chunk
+        qgcm::ChunkClaims cl;
+        cl.reset(nchunks, items, per);
+        std::vector<std::atomic<int>> owner(items);
+        for (auto &o : owner) o = 0;
+        std::vector<std::atomic<int>> dev_chunk(nchunks);
+        for (auto &d : dev_chunk) d = 0;
+        std::vector<std::thread> ws;
+        for (int t = 0; t < 8; ++t)
+            ws.emplace_back([&] {
+                for (int64_t it; (it = cl.claim_item()) >= 0;) owner[it].fetch_add(1);
+            });
+        std::thread dev([&] {
+            for (int64_t c; (c = cl.claim_chunk()) >= 0;) {
+                dev_chunk[c].fetch_add(1);
+                for (uint64_t it = c * per; it < items && it < (c + 1) * per; ++it) owner[it].fetch_add(100);
+                std::this_thread::yield();
+            }
+        });
+        for (auto &w : ws) w.join();
+        dev.join();
+        const uint64_t dlo = cl.device_from();
+        for (uint64_t it = 0; it < items; ++it) {
+            const int o = owner[it].load();
+            if (o != (it / per >= dlo ? 100 : 1)) return fail("chain claims: an item taken twice, by both sides or never");
+        }
+        for (uint64_t c = 0; c < nchunks; ++c)
+            if (dev_chunk[c].load() != (c >= dlo ? 1 : 0)) return fail("chain claims: device chunks");
+    }
     printf("sanitizer driver ok\n");
     return 0;
 }

@@ -2,7 +2,7 @@
 split knobs, one process: QGCM_CHAIN_DEV_AHEAD (seal) and QGCM_CHAIN_DEV_BACKLOG (open) are read per
 call, so each setting is timed in turn, interleaved over `rounds`.
 
-    python3 tools/exp_chain_policy.py [rounds]
+    python3 tools/exp_chain_policy.py [rounds] [chunks]   (chunks: chunk size x codec threads sweep)
 """
 import ctypes as C
 import json
@@ -32,20 +32,30 @@ def main() -> None:
     nons[:] = np.random.default_rng(1).integers(0, 256, 12 * N, dtype=np.uint8)
     plain = host[:, :4 + L].copy()
     lens = np.full(N, L, np.uint32)
-    settings = [("host", 0, "2", "0"), ("ahead1", 1, "1", "999999"), ("ahead2", 1, "2", "999999"),
-                ("ahead3", 1, "3", "999999"), ("ahead4", 1, "4", "999999"), ("back0", 1, "2", "0"),
-                ("back45", 1, "2", "45"), ("back90", 1, "2", "90"), ("back180", 1, "2", "180")]
+    # (name, codec mode, QGCM_CHAIN_DEV_AHEAD, QGCM_CHAIN_DEV_BACKLOG, QGCM_CHAIN_CHUNK_MB, codec threads)
+    if len(sys.argv) > 2 and sys.argv[2] == "chunks":
+        settings = [(f"c{mb}t{t}", 1, "2", "", str(mb), t) for mb in (16, 32, 64) for t in (14, 15, 16)]
+    else:
+        settings = [("host", 0, "2", "0", "32", 16), ("ahead1", 1, "1", "999999", "32", 16),
+                    ("ahead2", 1, "2", "999999", "32", 16), ("ahead3", 1, "3", "999999", "32", 16),
+                    ("ahead4", 1, "4", "999999", "32", 16), ("back0", 1, "2", "0", "32", 16),
+                    ("back45", 1, "2", "45", "32", 16), ("back90", 1, "2", "90", "32", 16),
+                    ("back180", 1, "2", "180", "32", 16)]
     res = {name: {"seal": [], "open": [], "dev": []} for name, *_ in settings}
     for _ in range(rounds):
-        for name, mode, ahead, back in settings:
-            os.environ["QGCM_CHAIN_DEV_AHEAD"], os.environ["QGCM_CHAIN_DEV_BACKLOG"] = ahead, back
+        for name, mode, ahead, back, mb, threads in settings:
+            os.environ["QGCM_CHAIN_DEV_AHEAD"], os.environ["QGCM_CHAIN_CHUNK_MB"] = ahead, mb
+            if back:
+                os.environ["QGCM_CHAIN_DEV_BACKLOG"] = back
+            else:
+                os.environ.pop("QGCM_CHAIN_DEV_BACKLOG", None)
             batch.chain_codec(ctx, mode)
             c0 = ctx.launch_counts()
             lens[:] = L
             t0 = time.perf_counter()
-            bad = batch.compress_seal_host(ctx, a_ptr, stride, N, lens, 0, n_ptr, threads=16)
+            bad = batch.compress_seal_host(ctx, a_ptr, stride, N, lens, 0, n_ptr, threads=threads)
             t1 = time.perf_counter()
-            bad += batch.open_uncompress_host(ctx, a_ptr, stride, N, lens, 0, threads=16)
+            bad += batch.open_uncompress_host(ctx, a_ptr, stride, N, lens, 0, threads=threads)
             t2 = time.perf_counter()
             c1 = ctx.launch_counts()
             assert bad == 0 and np.array_equal(host[:, :4 + L], plain), name

@@ -50,6 +50,9 @@ for s in $STEPS; do
     policy)
       timeout -k 10 400 python3 tools/exp_chain_policy.py 3 > $OUT/chain_policy.jsonl 2> $OUT/chain_policy.err
       check policy $? ;;
+    chunks)
+      timeout -k 10 500 python3 tools/exp_chain_policy.py 3 chunks > $OUT/chain_chunks.jsonl 2> $OUT/chain_chunks.err
+      check chunks $? ;;
     snapdev)
       timeout -k 10 200 python3 tools/exp_snappy_dev.py 5 > $OUT/snappy_dev.json 2> $OUT/snappy_dev.err
       check snapdev $? ;;
