@@ -10,10 +10,12 @@
 // that steers it is wave-uniform and kept in SGPRs) and spends its 64 lanes where the work is
 // data-parallel -- staging the packet into LDS, extending a match 64 bytes per step (a ballot of
 // mismatching lanes), copying literals, writing the result back with dword stores.  The packet, the
-// hash table (2^8..2^14 uint16 positions) and the output are all in the wave's LDS, so the serial
-// chain is LDS latency, not HBM latency, and many waves per CU overlap their chains.  The decoder
-// parses tags uniformly and copies each literal / back-reference with all lanes (a copy of length
-// <= 64 is one step: lane j reads out[op - off + j % off], which is already written).
+// hash table (2^8..2^14 uint16 positions) and the output are all in the wave's LDS, and the next
+// packet is read while the current one is coded, so no HBM latency sits on the serial chain; 20
+// waves per CU then share the CU's one scalar unit, which bounds the encoder (~3.7 K
+// scalar instructions per 1350-B packet), so the loop is written for few scalar instructions.  The
+// decoder parses tags uniformly and copies each literal / back-reference with all lanes (a copy of
+// length <= 64 is one step: lane j reads out[op - off + j % off], which is already written).
 //
 // Byte-exact with the host encoder (tests/test_gpu_snappy.py): a packet whose output does not fit
 // `limit` (compress) or `cap` (uncompress), or that does not decode, fails: status 0, slot and
