@@ -260,8 +260,8 @@ int qgcm_open_uncompress_host(qgcm_ctx *ctx, uint8_t *h_arena, uint64_t stride, 
                               uint32_t key_idx, uint32_t aad_len, int threads, uint8_t *h_status);
 /* Where the chained calls run the snappy codec: 0 = host workers only; 1 = split (default): the device
  * codec takes the chunks the host workers cannot keep up with (seal: the last untouched chunks when a
- * stream slot is free and the next host chunk is not compressed yet; open: when the host decode backlog
- * exceeds a chunk); 2 = device only.  The bytes are the same either way.  Returns the previous mode
+ * stream slot is free and fewer than two compressed host chunks are waiting; open: when the host decode
+ * backlog exceeds two chunks); 2 = device only.  The bytes are the same either way.  Returns the previous mode
  * (mode -1: just read it) or QGCM_E_ARG.  QGCM_CHAIN_DEVICE sets the initial mode. */
 int qgcm_chain_codec(qgcm_ctx *ctx, int mode);
 

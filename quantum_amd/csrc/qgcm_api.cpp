@@ -835,7 +835,7 @@ static int run_snappy(qgcm_ctx *ctx, bool compress, uint8_t *d_arena, uint64_t s
 //    atomic word), ships it uncompressed and compresses it in place before the seal.  The host codec
 //    and PCIe thus set the split themselves: the device takes what the host cores cannot keep up with.
 //  * open: chunk by chunk in order; a chunk is decoded on the device when the host workers' backlog
-//    (released, not yet decoded items) exceeds QGCM_CHAIN_DEV_BACKLOG items (default one chunk),
+//    (released, not yet decoded items) exceeds QGCM_CHAIN_DEV_BACKLOG items (default two chunks),
 //    else after its D2H on the host.
 // A device chunk crosses PCIe at full width on the uncompressed side (the host cannot size the rows
 // before the kernel ran); a host chunk's rows are as wide as its longest record.  QGCM_CHAIN_DEVICE:
@@ -996,7 +996,7 @@ static int run_host_chain(qgcm_ctx *ctx, bool seal, uint8_t *h_arena, uint64_t s
     // stream slot frees up (the host codec is about to stall the pipeline); open: when more than
     // backlog_max released items wait for the host decoder
     const uint64_t ahead_min = (uint64_t)std::max(1, env_int("QGCM_CHAIN_DEV_AHEAD", 2));
-    const uint64_t backlog_max = (uint64_t)env_int("QGCM_CHAIN_DEV_BACKLOG", (int)per_chunk);
+    const uint64_t backlog_max = (uint64_t)env_int("QGCM_CHAIN_DEV_BACKLOG", (int)(2 * per_chunk));
     std::vector<int64_t> slot_chunk(nslots, -1);
     // a slot's previous chunk has landed: device chunks' lengths back to the caller; open: release
     // its items to the host workers (device chunks' items are skipped)
