@@ -89,6 +89,7 @@ struct qgcm_ctx {
     size_t side_cap = 0;
     qgcm_desc *h_desc = nullptr;  // pinned descriptor staging of the chained (snappy + GCM) path
     uint32_t *h_lens = nullptr;   // pinned length staging of its device-codec chunks (hdesc_cap entries)
+    std::vector<hipStream_t> chain_extra;  // chained path: streams past pipe[] (QGCM_CHAIN_SLOTS > 3)
     size_t hdesc_cap = 0;
 
     // orders reuse of the descriptor workspace across streams (guarded by ws_mu)
@@ -579,6 +580,7 @@ void qgcm_destroy(qgcm_ctx *ctx) {
     if (ctx->h_stat) hipHostFree(ctx->h_stat);
     if (ctx->h_desc) hipHostFree(ctx->h_desc);
     if (ctx->h_lens) hipHostFree(ctx->h_lens);
+    for (hipStream_t x : ctx->chain_extra) hipStreamDestroy(x);
     for (hipStream_t p : ctx->pipe)
         if (p) hipStreamDestroy(p);
     if (ctx->ws_done) hipEventDestroy(ctx->ws_done);
@@ -892,7 +894,15 @@ static int run_host_chain(qgcm_ctx *ctx, bool seal, uint8_t *h_arena, uint64_t s
     const bool non = seal && h_nonces;
     const uint64_t off_non = al(cpk * stride), off_st = off_non + (non ? al(12 * cpk) : 0);
     const uint64_t off_desc = off_st + al(cpk), off_lens = off_desc + al(16 * cpk), slot = off_lens + al(4 * cpk);
-    const int nslots = nchunks < (uint64_t)kPipeStreams ? (int)nchunks : kPipeStreams;
+    // chunks in flight, one stream and staging slot each (QGCM_CHAIN_SLOTS, A/B knob; default 3)
+    const int want_slots = std::max(1, std::min(16, env_int("QGCM_CHAIN_SLOTS", kPipeStreams)));
+    const int nslots = nchunks < (uint64_t)want_slots ? (int)nchunks : want_slots;
+    while ((int)ctx->chain_extra.size() + kPipeStreams < nslots) {
+        hipStream_t x = nullptr;
+        if (hipStreamCreateWithFlags(&x, hipStreamNonBlocking) != hipSuccess) return QGCM_E_HIP;
+        ctx->chain_extra.push_back(x);
+    }
+    auto stream_of = [&](int k) { return k < kPipeStreams ? ctx->pipe[k] : ctx->chain_extra[k - kPipeStreams]; };
     // every packet a slot can hold fits the device codec, so a chunk's result does not depend on where
     // its codec ran
     const bool dev_ok = dev_mode > 0 && stride - 4 <= kSnapDevMax;
@@ -1011,7 +1021,7 @@ static int run_host_chain(qgcm_ctx *ctx, bool seal, uint8_t *h_arena, uint64_t s
     uint64_t host_next = 0, released = 0;
     for (uint64_t e = 0; rc == QGCM_OK; ++e) {
         const int k = (int)(e % nslots);
-        hipStream_t s = ctx->pipe[k];
+        hipStream_t s = stream_of(k);
         if (slot_chunk[k] >= 0) {
             if (hipStreamSynchronize(s) != hipSuccess) {
                 rc = QGCM_E_HIP;
@@ -1109,7 +1119,7 @@ static int run_host_chain(qgcm_ctx *ctx, bool seal, uint8_t *h_arena, uint64_t s
             rc = QGCM_E_HIP;
     }
     for (int k = 0; k < nslots; ++k)
-        if (hipStreamSynchronize(ctx->pipe[k]) != hipSuccess) rc = QGCM_E_HIP;
+        if (hipStreamSynchronize(stream_of(k)) != hipSuccess) rc = QGCM_E_HIP;
     if (rc != QGCM_OK) {
         pool.join();
         return rc;

@@ -2,7 +2,8 @@
 split knobs, one process: QGCM_CHAIN_DEV_AHEAD (seal) and QGCM_CHAIN_DEV_BACKLOG (open) are read per
 call, so each setting is timed in turn, interleaved over `rounds`.
 
-    python3 tools/exp_chain_policy.py [rounds] [chunks]   (chunks: chunk size x codec threads sweep)
+    python3 tools/exp_chain_policy.py [rounds] [chunks|slots]   (chunk size x codec threads, or chunks in
+    flight x chunk size)
 """
 import ctypes as C
 import json
@@ -33,8 +34,17 @@ def main() -> None:
     plain = host[:, :4 + L].copy()
     lens = np.full(N, L, np.uint32)
     # (name, codec mode, QGCM_CHAIN_DEV_AHEAD, QGCM_CHAIN_DEV_BACKLOG, QGCM_CHAIN_CHUNK_MB, codec threads)
+    slots = {}
     if len(sys.argv) > 2 and sys.argv[2] == "chunks":
         settings = [(f"c{mb}t{t}", 1, "2", "", str(mb), t) for mb in (16, 32, 64) for t in (14, 15, 16)]
+    elif len(sys.argv) > 2 and sys.argv[2] == "slots":  # chunks in flight (QGCM_CHAIN_SLOTS) x chunk size
+        settings = []
+        for ns in (3, 4, 6, 8):
+            for mb in (16, 32):
+                settings.append((f"s{ns}c{mb}", 1, "2", "", str(mb), 16))
+                slots[f"s{ns}c{mb}"] = str(ns)
+        settings.append(("host_s6c16", 0, "2", "", "16", 16))
+        slots["host_s6c16"] = "6"
     else:
         settings = [("host", 0, "2", "0", "32", 16), ("ahead1", 1, "1", "999999", "32", 16),
                     ("ahead2", 1, "2", "999999", "32", 16), ("ahead3", 1, "3", "999999", "32", 16),
@@ -45,6 +55,7 @@ def main() -> None:
     for _ in range(rounds):
         for name, mode, ahead, back, mb, threads in settings:
             os.environ["QGCM_CHAIN_DEV_AHEAD"], os.environ["QGCM_CHAIN_CHUNK_MB"] = ahead, mb
+            os.environ["QGCM_CHAIN_SLOTS"] = slots.get(name, "3")
             if back:
                 os.environ["QGCM_CHAIN_DEV_BACKLOG"] = back
             else:

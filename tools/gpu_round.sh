@@ -53,6 +53,9 @@ for s in $STEPS; do
     chunks)
       timeout -k 10 500 python3 tools/exp_chain_policy.py 3 chunks > $OUT/chain_chunks.jsonl 2> $OUT/chain_chunks.err
       check chunks $? ;;
+    slots)
+      timeout -k 10 500 python3 tools/exp_chain_policy.py 3 slots > $OUT/chain_slots.jsonl 2> $OUT/chain_slots.err
+      check slots $? ;;
     snapdev)
       timeout -k 10 200 python3 tools/exp_snappy_dev.py 5 > $OUT/snappy_dev.json 2> $OUT/snappy_dev.err
       check snapdev $? ;;
