@@ -894,30 +894,13 @@ static int run_host_chain(qgcm_ctx *ctx, bool seal, uint8_t *h_arena, uint64_t s
     const bool non = seal && h_nonces;
     const uint64_t off_non = al(cpk * stride), off_st = off_non + (non ? al(12 * cpk) : 0);
     const uint64_t off_desc = off_st + al(cpk), off_lens = off_desc + al(16 * cpk), slot = off_lens + al(4 * cpk);
-    // Two pipeline forms (QGCM_CHAIN_PIPE, A/B knob): 0 = a stream per chunk in flight (H2D, kernels,
-    // D2H in order on it; QGCM_CHAIN_SLOTS slots, default 3); 1 = one stream per stage (copy-in,
-    // kernels, copy-out, as run_host) ordered by per-slot events over a ring of QGCM_CHAIN_RING
-    // staging slots (default 8), completed chunks drained in order without blocking.
-    const bool staged = env_int("QGCM_CHAIN_PIPE", 0) == 1;
-    const int want_slots = std::max(1, std::min(16, staged ? env_int("QGCM_CHAIN_RING", 8)
-                                                           : env_int("QGCM_CHAIN_SLOTS", kPipeStreams)));
+    // chunks in flight, one stream and staging slot each (QGCM_CHAIN_SLOTS, A/B knob; default 3)
+    const int want_slots = std::max(1, std::min(16, env_int("QGCM_CHAIN_SLOTS", kPipeStreams)));
     const int nslots = nchunks < (uint64_t)want_slots ? (int)nchunks : want_slots;
-    while (!staged && (int)ctx->chain_extra.size() + kPipeStreams < nslots) {
+    while ((int)ctx->chain_extra.size() + kPipeStreams < nslots) {
         hipStream_t x = nullptr;
         if (hipStreamCreateWithFlags(&x, hipStreamNonBlocking) != hipSuccess) return QGCM_E_HIP;
         ctx->chain_extra.push_back(x);
-    }
-    while (staged && ctx->ev_in.size() < (size_t)nslots) {
-        hipEvent_t e[3] = {};
-        for (hipEvent_t &x : e)
-            if (hipEventCreateWithFlags(&x, hipEventDisableTiming) != hipSuccess) {
-                for (hipEvent_t y : e)
-                    if (y) hipEventDestroy(y);
-                return QGCM_E_HIP;
-            }
-        ctx->ev_in.push_back(e[0]);
-        ctx->ev_kern.push_back(e[1]);
-        ctx->ev_out.push_back(e[2]);
     }
     auto stream_of = [&](int k) { return k < kPipeStreams ? ctx->pipe[k] : ctx->chain_extra[k - kPipeStreams]; };
     // every packet a slot can hold fits the device codec, so a chunk's result does not depend on where
@@ -1035,49 +1018,21 @@ static int run_host_chain(qgcm_ctx *ctx, bool seal, uint8_t *h_arena, uint64_t s
         slot_chunk[k] = -1;
     };
     int rc = QGCM_OK;
-    uint64_t host_next = 0, released = 0, drained = 0, enq = 0;
-    // the slot of enqueue e has landed (staged: its copy-out event; else its stream): finalize it, and on
-    // open release its items (chunks are enqueued in order on open) to the host decoders
-    auto land = [&](uint64_t e2, bool block) -> int {
-        const int k2 = (int)(e2 % nslots);
-        if (slot_chunk[k2] < 0) return 1;
-        if (staged) {
-            const hipError_t q = block ? hipEventSynchronize(ctx->ev_out[k2]) : hipEventQuery(ctx->ev_out[k2]);
-            if (q == hipErrorNotReady) return 0;
-            if (q != hipSuccess) return -1;
-        } else if (hipStreamSynchronize(stream_of(k2)) != hipSuccess) {
-            return -1;
-        }
-        const int64_t prev = slot_chunk[k2];
-        finalize(k2);
-        if (!seal) {
-            released = std::max<uint64_t>(released, (uint64_t)(prev + 1) * per_chunk);
-            pool.limit.store(std::min<uint64_t>(released, total_items), std::memory_order_release);
-        }
-        return 1;
-    };
-    auto drain = [&](uint64_t upto, bool block) {  // land enqueues [drained, upto) in order
-        for (; drained < upto; ++drained) {
-            const int r2 = land(drained, block);
-            if (r2 < 0) return false;
-            if (r2 == 0) break;
-        }
-        return true;
-    };
-    // staged seal: the copy-in engine has nothing queued (the last chunk's copy-in event has fired)
-    auto h2d_idle = [&]() {
-        return enq == 0 || hipEventQuery(ctx->ev_in[(enq - 1) % nslots]) == hipSuccess;
-    };
+    uint64_t host_next = 0, released = 0;
     for (uint64_t e = 0; rc == QGCM_OK; ++e) {
         const int k = (int)(e % nslots);
-        hipStream_t s = staged ? ctx->pipe[0] : stream_of(k);
-        if (staged && !drain(e, false)) {
-            rc = QGCM_E_HIP;
-            break;
-        }
-        if (e >= (uint64_t)nslots && !drain(e - nslots + 1, true)) {  // slot k is free once its chunk landed
-            rc = QGCM_E_HIP;
-            break;
+        hipStream_t s = stream_of(k);
+        if (slot_chunk[k] >= 0) {
+            if (hipStreamSynchronize(s) != hipSuccess) {
+                rc = QGCM_E_HIP;
+                break;
+            }
+            const int64_t prev = slot_chunk[k];
+            finalize(k);
+            if (!seal) {  // chunks are enqueued in order on open: release up to the one that landed
+                released = std::max<uint64_t>(released, (uint64_t)(prev + 1) * per_chunk);
+                pool.limit.store(std::min<uint64_t>(released, total_items), std::memory_order_release);
+            }
         }
         int64_t c = -1;
         bool dev = false;
@@ -1089,27 +1044,6 @@ static int run_host_chain(qgcm_ctx *ctx, bool seal, uint8_t *h_arena, uint64_t s
                 while (ready < ahead_min && host_next + ready < dlo &&
                        pool.done[host_next + ready].load(std::memory_order_acquire) == items_in(host_next + ready))
                     ++ready;
-                if (staged) {  // device chunks only while the copy-in engine would otherwise idle
-                    if (ready >= ahead_min || (ready && !dev_ok)) {
-                        c = (int64_t)host_next++;
-                        break;
-                    }
-                    const bool idle = h2d_idle();
-                    if (dev_ok && idle && (c = pool.claim.claim_chunk()) >= 0) {
-                        dev = true;
-                        break;
-                    }
-                    if (ready && idle) {
-                        c = (int64_t)host_next++;
-                        break;
-                    }
-                    if (!drain(e, false)) {  // keep finalizing landed chunks
-                        rc = QGCM_E_HIP;
-                        break;
-                    }
-                    std::this_thread::yield();
-                    continue;
-                }
                 if (dev_ok && ready < ahead_min && (c = pool.claim.claim_chunk()) >= 0) {
                     dev = true;
                     break;
@@ -1127,12 +1061,9 @@ static int run_host_chain(qgcm_ctx *ctx, bool seal, uint8_t *h_arena, uint64_t s
                 if (!pool.on_dev[q]) backlog += items_in(q) - pool.done[q].load(std::memory_order_acquire);
             dev = dev_ok && (dev_mode == 2 || backlog > backlog_max);
         }
-        if (c < 0 || rc != QGCM_OK) break;
+        if (c < 0) break;
         pool.on_dev[c].store(dev ? 1 : 0, std::memory_order_release);
         slot_chunk[k] = c;
-        ++enq;
-        // staged: copy-in on pipe[0], kernels on pipe[1], copy-out on pipe[2]
-        hipStream_t s_k = staged ? ctx->pipe[1] : s, s_out = staged ? ctx->pipe[2] : s;
         uint8_t *d = ctx->d_ring + k * slot, *d_non = d + off_non, *d_st = d + off_st;
         qgcm_desc *d_desc = reinterpret_cast<qgcm_desc *>(d + off_desc);
         uint32_t *d_lens = reinterpret_cast<uint32_t *>(d + off_lens);
@@ -1160,52 +1091,40 @@ static int run_host_chain(qgcm_ctx *ctx, bool seal, uint8_t *h_arena, uint64_t s
         }
         if (dev) width = stride;
         max_in = std::min<uint32_t>(max_in, max_plain);  // seal: longer packets fail, as on the host
-        auto copy = [&](void *dst, const void *src, uint64_t w, hipMemcpyKind kind, hipStream_t st) {
+        auto copy = [&](void *dst, const void *src, uint64_t w, hipMemcpyKind kind) {
             w = std::min<uint64_t>(stride, (w + 3) & ~3ull);
-            return w * 10 >= stride * 9 ? hipMemcpyAsync(dst, src, cn * stride, kind, st)
-                                        : hipMemcpy2DAsync(dst, stride, src, stride, w, cn, kind, st);
+            return w * 10 >= stride * 9 ? hipMemcpyAsync(dst, src, cn * stride, kind, s)
+                                        : hipMemcpy2DAsync(dst, stride, src, stride, w, cn, kind, s);
         };
         if (dev) {
             memcpy(hl, lens + c0, 4 * cn);
             if (hipMemcpyAsync(d_lens, hl, 4 * cn, hipMemcpyHostToDevice, s) != hipSuccess) rc = QGCM_E_HIP;
         }
         if (rc == QGCM_OK &&
-            (copy(d, h, width, hipMemcpyHostToDevice, s) != hipSuccess ||
+            (copy(d, h, width, hipMemcpyHostToDevice) != hipSuccess ||
              (!(seal && dev) &&
               hipMemcpyAsync(d_desc, hd, cn * sizeof(qgcm_desc), hipMemcpyHostToDevice, s) != hipSuccess) ||
              (non && hipMemcpyAsync(d_non, h_nonces + 12 * c0, 12 * cn, hipMemcpyHostToDevice, s) != hipSuccess)))
             rc = QGCM_E_HIP;
-        if (rc == QGCM_OK && staged &&
-            (hipEventRecord(ctx->ev_in[k], s) != hipSuccess || hipStreamWaitEvent(s_k, ctx->ev_in[k], 0) != hipSuccess))
-            rc = QGCM_E_HIP;
         if (rc == QGCM_OK && seal && dev)  // compress in place; failures get the sentinel length (seal skips them)
             rc = run_snappy(ctx, true, d, stride, (uint32_t)cn, d_lens, max_in, max_plain, nullptr, nullptr, d_desc,
-                            key_idx, 0, s_k);
-        if (rc == QGCM_OK) rc = run_descs(ctx, seal, d, d_desc, (uint32_t)cn, non ? d_non : nullptr, aad_len, d_st, s_k);
+                            key_idx, 0, s);
+        if (rc == QGCM_OK) rc = run_descs(ctx, seal, d, d_desc, (uint32_t)cn, non ? d_non : nullptr, aad_len, d_st, s);
         if (rc == QGCM_OK && !seal && dev)  // authentic packets only; a failed decode clears the status
             rc = run_snappy(ctx, false, d, stride, (uint32_t)cn, d_lens, max_in, (uint32_t)(stride - 4), d_st, d_st,
-                            nullptr, 0, QGCM_OVERHEAD, s_k);
-        if (rc == QGCM_OK && staged &&
-            (hipEventRecord(ctx->ev_kern[k], s_k) != hipSuccess || hipStreamWaitEvent(s_out, ctx->ev_kern[k], 0) != hipSuccess))
+                            nullptr, 0, QGCM_OVERHEAD, s);
+        if (rc == QGCM_OK && (copy(h, d, width, hipMemcpyDeviceToHost) != hipSuccess ||
+                              hipMemcpyAsync(ctx->h_stat + c0, d_st, cn, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                              (dev && hipMemcpyAsync(hl, d_lens, 4 * cn, hipMemcpyDeviceToHost, s) != hipSuccess)))
             rc = QGCM_E_HIP;
-        if (rc == QGCM_OK && (copy(h, d, width, hipMemcpyDeviceToHost, s_out) != hipSuccess ||
-                              hipMemcpyAsync(ctx->h_stat + c0, d_st, cn, hipMemcpyDeviceToHost, s_out) != hipSuccess ||
-                              (dev && hipMemcpyAsync(hl, d_lens, 4 * cn, hipMemcpyDeviceToHost, s_out) != hipSuccess)))
-            rc = QGCM_E_HIP;
-        if (rc == QGCM_OK && staged && hipEventRecord(ctx->ev_out[k], s_out) != hipSuccess) rc = QGCM_E_HIP;
     }
-    if (staged) {
-        for (int k = 0; k < kPipeStreams; ++k)
-            if (hipStreamSynchronize(ctx->pipe[k]) != hipSuccess) rc = QGCM_E_HIP;
-    } else {
-        for (int k = 0; k < nslots; ++k)
-            if (hipStreamSynchronize(stream_of(k)) != hipSuccess) rc = QGCM_E_HIP;
-    }
+    for (int k = 0; k < nslots; ++k)
+        if (hipStreamSynchronize(stream_of(k)) != hipSuccess) rc = QGCM_E_HIP;
     if (rc != QGCM_OK) {
         pool.join();
         return rc;
     }
-    for (int k = 0; k < nslots; ++k) finalize(k);  // everything has landed
+    for (int k = 0; k < nslots; ++k) finalize(k);
     if (!seal) pool.limit.store(total_items, std::memory_order_release);
     for (uint64_t c = 0; c < nchunks; ++c)
         if (!(seal && pool.on_dev[c])) pool.wait_chunk(c, items_in(c));

@@ -2,7 +2,7 @@
 split knobs, one process: QGCM_CHAIN_DEV_AHEAD (seal) and QGCM_CHAIN_DEV_BACKLOG (open) are read per
 call, so each setting is timed in turn, interleaved over `rounds`.
 
-    python3 tools/exp_chain_policy.py [rounds] [chunks|slots|pipe]   (chunk size x codec threads, or chunks in
+    python3 tools/exp_chain_policy.py [rounds] [chunks|slots]   (chunk size x codec threads, or chunks in
     flight x chunk size)
 """
 import ctypes as C
@@ -34,17 +34,9 @@ def main() -> None:
     plain = host[:, :4 + L].copy()
     lens = np.full(N, L, np.uint32)
     # (name, codec mode, QGCM_CHAIN_DEV_AHEAD, QGCM_CHAIN_DEV_BACKLOG, QGCM_CHAIN_CHUNK_MB, codec threads)
-    slots, pipes = {}, {}
+    slots = {}
     if len(sys.argv) > 2 and sys.argv[2] == "chunks":
         settings = [(f"c{mb}t{t}", 1, "2", "", str(mb), t) for mb in (16, 32, 64) for t in (14, 15, 16)]
-    elif len(sys.argv) > 2 and sys.argv[2] == "pipe":  # stream per chunk vs per-stage streams over a ring
-        settings, pipes = [], {}
-        for name, mode, mb, ring, pipe in (("chunk_c32", 1, 32, 3, 0), ("host_chunk_c32", 0, 32, 3, 0),
-                                           ("staged_r8c32", 1, 32, 8, 1), ("staged_r8c16", 1, 16, 8, 1),
-                                           ("staged_r16c16", 1, 16, 16, 1), ("host_staged_r8c32", 0, 32, 8, 1)):
-            settings.append((name, mode, "2", "", str(mb), 16))
-            slots[name] = str(ring)
-            pipes[name] = str(pipe)
     elif len(sys.argv) > 2 and sys.argv[2] == "slots":  # chunks in flight (QGCM_CHAIN_SLOTS) x chunk size
         settings = []
         for ns in (3, 4, 6, 8):
@@ -63,8 +55,7 @@ def main() -> None:
     for _ in range(rounds):
         for name, mode, ahead, back, mb, threads in settings:
             os.environ["QGCM_CHAIN_DEV_AHEAD"], os.environ["QGCM_CHAIN_CHUNK_MB"] = ahead, mb
-            os.environ["QGCM_CHAIN_SLOTS"] = os.environ["QGCM_CHAIN_RING"] = slots.get(name, "3")
-            os.environ["QGCM_CHAIN_PIPE"] = pipes.get(name, "0")
+            os.environ["QGCM_CHAIN_SLOTS"] = slots.get(name, "3")
             if back:
                 os.environ["QGCM_CHAIN_DEV_BACKLOG"] = back
             else:
