@@ -53,9 +53,6 @@ for s in $STEPS; do
     chunks)
       timeout -k 10 500 python3 tools/exp_chain_policy.py 3 chunks > $OUT/chain_chunks.jsonl 2> $OUT/chain_chunks.err
       check chunks $? ;;
-    pipe)
-      timeout -k 10 500 python3 tools/exp_chain_policy.py 3 pipe > $OUT/chain_pipe.jsonl 2> $OUT/chain_pipe.err
-      check pipe $? ;;
     ctests)
       timeout -k 10 300 python3 -u -m pytest tests/test_gpu_parity.py -k chain -x -v --timeout 120 --timeout-method thread > $OUT/chain_tests.txt 2>&1
       check ctests $? ;;
