@@ -50,7 +50,10 @@ struct Batch {
     uint8_t *done;              // gcm_one_kernel: done[0] (uniform form, one packet) or done[pkt] (descriptor
                                 // form) set to 1 after the slot is written
                                 // back and made system-visible (the host polls it instead of the stream)
+    const uint4 *pw_table;      // latency engine: [pw_keys][kPwPowers][512] comb tables of H^1..H^kPwPowers
+    uint32_t pw_keys;           // (NULL / 0: the Horner + Estrin GHASH for every packet)
 };
+constexpr uint32_t kPwPowers = 128;  // flat GHASH up to d + 2 = 128 exponents (payloads up to 2016 B)
 
 constexpr int kNumVariants = 15;     // ids as in round 2; only the three below are built
 constexpr int kVariantUniform = 12;  // single-key (uniform) batches: quad kernel (Tab2F), 32 waves/CU
@@ -169,6 +172,8 @@ struct SnapArgs {
 };
 hipError_t launch_snappy(bool compress, const SnapArgs &a, int waves_per_wg, int grid, hipStream_t s);
 
+hipError_t launch_pw_setup(uint32_t first, uint32_t count, const uint4 *gh_table, uint4 *pw, uint32_t pw_keys,
+                           hipStream_t s);
 hipError_t launch_key_setup(const uint8_t *d_keys, uint32_t first, uint32_t count, uint32_t *rk_table,
                             uint4 *gh_table, const uint8_t *d_sbox, hipStream_t s);
 hipError_t launch_fill_uniform(uint8_t *arena, uint64_t stride, uint32_t n, uint32_t len, uint32_t aad_word,

@@ -1229,7 +1229,9 @@ __device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_t
     constexpr int kGhIt = kOneTabs * 512 / kOneThreads;  // 7
     const uint4 *gh = b.gh_table + (size_t)key * kGhEntries;
     const uint32_t emax = ((L + 15u) >> 4) + 2u;  // GHASH exponents 1 .. d + 2 (step 3)
-    const uint32_t ntabs = emax >= 64u ? kOneTabs : 32u - __builtin_clz(emax);
+    // flat GHASH (step 3) from the key's global tables of H^1 .. H^kPwPowers: no comb tables in LDS
+    const bool flat = b.pw_table != nullptr && key < b.pw_keys && emax <= kPwPowers;  // workgroup-uniform
+    const uint32_t ntabs = flat ? 0u : emax >= 64u ? kOneTabs : 32u - __builtin_clz(emax);
     const uint32_t t0 = key == tab_key ? tab_n : 0u;  // tables [0, t0) already hold this key's
     if (fill_te) one_fill_te(b.te, tid);
     if (ntabs > t0) {
@@ -1368,7 +1370,62 @@ __device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_t
     // Y = sum_i B_i H^(N+1-i) is c + 2 mod 64 (the AAD block included): a Horner chain by H^64, then
     // sum_c Z_c H^c by radix-2 Estrin levels (multiply by H^(2^l), add chain c + 2^l's product through
     // LDS), then Y = S H^2 + [len(A)]||[len(C)] H.  Every thread calls it (it has workgroup barriers).
+    // the block of GHASH exponent ex in Y = sum_ex B_ex H^ex: the AAD block (ex = d + 2), the length
+    // block (ex = 1), else ciphertext block d + 1 - ex (the partial one masked)
+    auto gblock = [&](uint32_t ex) {
+        if (ex == d + 2u) return uint4{aad_len ? lds32(A) & (aad_len >= 4 ? 0xffffffffu : lowmask(aad_len)) : 0u, 0u, 0u, 0u};
+        if (ex == 1) return uint4{0u, bswap(aad_len * 8u), 0u, bswap(L * 8u)};
+        const uint32_t bi = d + 1u - ex;
+        uint4 cb = lds128(P + 16 * bi);
+        if (bi == nfull) {
+            cb.x &= m0;
+            cb.y &= m1;
+            cb.z &= m2;
+            cb.w &= m3;
+        }
+        return cb;
+    };
+    // Flat GHASH for packets with d + 2 <= kPwPowers exponents: every product B_ex H^ex is independent,
+    // looked up in the key's comb table of H^ex (global memory, L2-resident): chain c's 8 lanes take
+    // ex = c + 1 and c + 65, lane e the four windows of bytes 2e, 2e+1; the 512 partial products are
+    // XOR-reduced (shuffles in each wave, then LDS).  One round of independent table reads replaces the
+    // Horner step and the Estrin levels' dependent multiplies and barriers.
+    auto ghash_flat = [&]() {
+        const uint32_t c = tid >> 3, e = tid & 7u, w = e >> 1, k0 = 2u * (e & 1u);
+        const uint4 *pwk = b.pw_table + (size_t)key * kPwPowers * 512u;
+        uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+        for (uint32_t ex = c + 1u; ex <= emax; ex += 64u) {
+            const uint4 cb = gblock(ex);
+            const uint32_t y = w == 0 ? cb.x : w == 1 ? cb.y : w == 2 ? cb.z : cb.w;
+            const uint32_t y0 = (y >> (8 * k0)) & 0xffu, y1 = (y >> (8 * k0 + 8)) & 0xffu;
+            const uint4 *t = pwk + (ex - 1u) * 512u + 64u * e;  // rows 4e .. 4e+3
+            const uint4 t0 = t[y0 >> 4], t1 = t[16u + (y0 & 15u)], t2 = t[32u + (y1 >> 4)], t3 = t[48u + (y1 & 15u)];
+            a0 ^= xor3(t0.x, t1.x, t2.x) ^ t3.x;
+            a1 ^= xor3(t0.y, t1.y, t2.y) ^ t3.y;
+            a2 ^= xor3(t0.z, t1.z, t2.z) ^ t3.z;
+            a3 ^= xor3(t0.w, t1.w, t2.w) ^ t3.w;
+        }
+#pragma unroll
+        for (int sh = 1; sh < 64; sh <<= 1) {
+            a0 ^= __shfl_xor(a0, sh, 64);
+            a1 ^= __shfl_xor(a1, sh, 64);
+            a2 ^= __shfl_xor(a2, sh, 64);
+            a3 ^= __shfl_xor(a3, sh, 64);
+        }
+        if (lane == 0) lds_st128(kOneX + 16 * (tid >> 6), uint4{a0, a1, a2, a3});
+        lds_barrier();
+        if (tid == 0) {
+            uint4 y = lds128(kOneX);
+            for (uint32_t wv = 1; wv < kOneThreads / 64u; ++wv) {
+                const uint4 q = lds128(kOneX + 16 * wv);
+                y = uint4{y.x ^ q.x, y.y ^ q.y, y.z ^ q.z, y.w ^ q.w};
+            }
+            lds_st128(kOneScratch + 16, y);
+        }
+    };
+
     auto ghash = [&]() {
+        if (flat) return ghash_flat();
         const uint32_t c = tid >> 3, e = tid & 7u;
         uint32_t z0 = 0, z1 = 0, z2 = 0, z3 = 0;
         // Exponents 1 (the length block) .. d + 2 (the AAD block; zero without additional data), so
@@ -1943,6 +2000,64 @@ hipError_t launch_key_setup(const uint8_t *d_keys, uint32_t first, uint32_t coun
                             uint4 *gh_table, const uint8_t *d_sbox, hipStream_t s) {
     if (count == 0) return hipSuccess;
     hipLaunchKernelGGL(key_setup_kernel, dim3(count), dim3(256), 0, s, d_keys, first, rk_table, gh_table, d_sbox);
+    return hipGetLastError();
+}
+
+// The latency engine's flat GHASH tables (one_packet): the 4-bit comb tables of H^1 .. H^kPwPowers of
+// each key slot below pw_keys, 8 KiB each, in the key-setup layout (entry 16 p + v).  One 256-thread
+// workgroup per key, after key_setup_kernel (H is read back from the slot's comb table of H: entry
+// (p 0, v 8) = x^0 * H).  Powers by doubling levels, H^(t+1) = H^(t+1-2^l) * H^(2^l); then 16 powers at a
+// time, x^i * H^k for i < 128 in LDS and the comb entries from them.
+__global__ void __launch_bounds__(256) pw_setup_kernel(uint32_t first, const uint4 *gh_table, uint4 *pw,
+                                                       uint32_t pw_keys) {
+    __shared__ uint8_t hp[kPwPowers][16];  // H^1 .. H^128
+    __shared__ uint4 xs[16][128];          // x^i * H^k for 16 powers of a batch
+    const uint32_t slot = first + blockIdx.x, tid = threadIdx.x;
+    if (slot >= pw_keys) return;  // workgroup-uniform
+    if (tid == 0) {
+        const uint4 h = gh_table[(size_t)slot * kGhEntries + kGhH + 8];
+        const uint32_t w[4] = {h.x, h.y, h.z, h.w};
+        for (int i = 0; i < 16; ++i) hp[0][i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+    }
+    __syncthreads();
+    for (uint32_t span = 1; span < kPwPowers; span <<= 1) {
+        if (tid >= span && tid < 2 * span && tid < kPwPowers) gf128_mul_bytes(hp[tid - span], hp[span - 1], hp[tid]);
+        __syncthreads();
+    }
+    for (uint32_t b0 = 0; b0 < kPwPowers; b0 += 16) {
+        {
+            const uint32_t j = tid >> 4, i0 = 8 * (tid & 15u);
+            uint8_t v[16];
+            for (int i = 0; i < 16; ++i) v[i] = hp[b0 + j][i];
+            for (uint32_t i = 0; i < i0; ++i) shift_x(v);
+            for (uint32_t i = 0; i < 8; ++i) {
+                xs[j][i0 + i] = pack16(v);
+                shift_x(v);
+            }
+        }
+        __syncthreads();
+        for (uint32_t e = tid; e < 16u * 512u; e += 256) {
+            const uint32_t j = e >> 9, q = e & 511u, pp = q >> 4, v = q & 15u;
+            uint4 acc = {0, 0, 0, 0};
+            for (int k = 0; k < 4; ++k) {
+                if ((v >> (3 - k)) & 1u) {
+                    const uint4 t = xs[j][4 * pp + k];
+                    acc.x ^= t.x;
+                    acc.y ^= t.y;
+                    acc.z ^= t.z;
+                    acc.w ^= t.w;
+                }
+            }
+            pw[((size_t)slot * kPwPowers + b0 + j) * 512u + q] = acc;
+        }
+        __syncthreads();
+    }
+}
+
+hipError_t launch_pw_setup(uint32_t first, uint32_t count, const uint4 *gh_table, uint4 *pw, uint32_t pw_keys,
+                           hipStream_t s) {
+    if (count == 0 || !pw || first >= pw_keys) return hipSuccess;
+    hipLaunchKernelGGL(pw_setup_kernel, dim3(count), dim3(256), 0, s, first, gh_table, pw, pw_keys);
     return hipGetLastError();
 }
 

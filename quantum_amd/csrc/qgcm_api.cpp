@@ -47,6 +47,8 @@ struct qgcm_ctx {
                                                 // (QGCM_DESC_CHUNK, tuning; 0 = one launch)
     uint32_t *d_rk = nullptr;
     uint4 *d_gh = nullptr;
+    uint4 *d_pw = nullptr;   // per-packet flat GHASH: comb tables of H^1..H^kPwPowers, key slots < pw_keys
+    uint32_t pw_keys = 0;    // (1 MiB per key; QGCM_FLAT_GHASH_KEYS, default min(max_keys, 4096), 0 = off)
     uint32_t *d_te = nullptr;
     uint8_t *d_sbox = nullptr;
     uint8_t *d_key_valid = nullptr;  // device view of key_set (descriptor batches check it per packet)
@@ -114,6 +116,11 @@ namespace {
 
 thread_local bool tl_dummy;
 
+int env_int(const char *name, int dflt) {
+    const char *v = getenv(name);
+    return v && *v ? atoi(v) : dflt;
+}
+
 uint8_t gf8_mul(uint8_t a, uint8_t b) {
     uint8_t p = 0;
     for (int i = 0; i < 8; ++i) {
@@ -173,6 +180,8 @@ Batch base_batch(const qgcm_ctx *ctx) {
     Batch b{};
     b.rk_table = ctx->d_rk;
     b.gh_table = ctx->d_gh;
+    b.pw_table = ctx->d_pw;
+    b.pw_keys = ctx->pw_keys;
     b.te = ctx->d_te;
     b.key_valid = ctx->d_key_valid;
     b.max_keys = ctx->max_keys;
@@ -548,6 +557,14 @@ qgcm_ctx *qgcm_create(int device, uint32_t max_keys, char *err, int errlen) {
               hipMemcpy(ctx->d_te, te, sizeof te, hipMemcpyHostToDevice) == hipSuccess &&
               hipMemcpy(ctx->d_sbox, sbox, sizeof sbox, hipMemcpyHostToDevice) == hipSuccess &&
               hipEventCreateWithFlags(&ctx->ws_done, hipEventDisableTiming) == hipSuccess;
+    ctx->pw_keys = (uint32_t)std::min<int64_t>(max_keys, std::max(0, env_int("QGCM_FLAT_GHASH_KEYS", 4096)));
+    if (ok && ctx->pw_keys &&
+        (hipMalloc(&ctx->d_pw, (size_t)ctx->pw_keys * kPwPowers * 512 * 16) != hipSuccess ||
+         hipMemset(ctx->d_pw, 0, (size_t)ctx->pw_keys * kPwPowers * 512 * 16) != hipSuccess)) {
+        hipFree(ctx->d_pw);  // no room: the per-packet path keeps the Horner + Estrin GHASH
+        ctx->d_pw = nullptr;
+        ctx->pw_keys = 0;
+    }
     for (int k = 0; ok && k < kPipeStreams; ++k)
         ok = hipStreamCreateWithFlags(&ctx->pipe[k], hipStreamNonBlocking) == hipSuccess;
     if (!ok) {
@@ -565,6 +582,7 @@ void qgcm_destroy(qgcm_ctx *ctx) {
     hipDeviceSynchronize();
     hipFree(ctx->d_rk);
     hipFree(ctx->d_gh);
+    hipFree(ctx->d_pw);
     hipFree(ctx->d_te);
     hipFree(ctx->d_sbox);
     hipFree(ctx->d_key_valid);
@@ -601,6 +619,7 @@ int qgcm_set_keys(qgcm_ctx *ctx, uint32_t first_idx, uint32_t count, const uint8
     if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess ||
         hipMemcpyAsync(d_keys, keys, (size_t)count * 32, hipMemcpyHostToDevice, s) != hipSuccess ||
         launch_key_setup(d_keys, first_idx, count, ctx->d_rk, ctx->d_gh, ctx->d_sbox, s) != hipSuccess ||
+        launch_pw_setup(first_idx, count, ctx->d_gh, ctx->d_pw, ctx->pw_keys, s) != hipSuccess ||
         hipMemsetAsync(ctx->d_key_valid + first_idx, 1, count, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
         rc = QGCM_E_HIP;
@@ -866,11 +885,6 @@ struct CodecPool {
         if (!workers.empty()) join();
     }
 };
-
-int env_int(const char *name, int dflt) {
-    const char *v = getenv(name);
-    return v && *v ? atoi(v) : dflt;
-}
 
 }  // namespace
 
