@@ -1387,32 +1387,58 @@ __device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_t
     };
     // Flat GHASH for packets with d + 2 <= kPwPowers exponents: every product B_ex H^ex is independent,
     // looked up in the key's comb table of H^ex (global memory, L2-resident): chain c's 8 lanes take
-    // ex = c + 1 and c + 65, lane e the four windows of bytes 2e, 2e+1; the 512 partial products are
-    // XOR-reduced (shuffles in each wave, then LDS).  One round of independent table reads replaces the
-    // Horner step and the Estrin levels' dependent multiplies and barriers.
-    auto ghash_flat = [&]() {
+    // ex = c + 1 and c + 65, lane e the four windows of bytes 2e, 2e+1.  One round of independent table
+    // reads replaces the Horner step and the Estrin levels' dependent multiplies and barriers.  In
+    // three phases: flat_issue (the block reads and table loads), flat_consume (their XOR; it waits for
+    // the loads, so it comes before this thread's first global store -- vmcnt would wait for those too),
+    // flat_finish (the 512 partials XOR-reduced: DPP within rows, readlane across them, LDS across waves).
+    // An open issues the loads before its counter blocks (the ciphertext is staged) and consumes them
+    // before its first plaintext store, so the table latency hides behind the rounds.
+    uint4 f0{}, f1{}, f2{}, f3{}, f4{}, f5{}, f6{}, f7{};
+    uint32_t fa0 = 0, fa1 = 0, fa2 = 0, fa3 = 0;
+    bool fed = false;
+    auto flat_issue = [&]() {
         const uint32_t c = tid >> 3, e = tid & 7u, w = e >> 1, k0 = 2u * (e & 1u);
-        const uint4 *pwk = b.pw_table + (size_t)key * kPwPowers * 512u;
-        uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
-        for (uint32_t ex = c + 1u; ex <= emax; ex += 64u) {
-            const uint4 cb = gblock(ex);
-            const uint32_t y = w == 0 ? cb.x : w == 1 ? cb.y : w == 2 ? cb.z : cb.w;
-            const uint32_t y0 = (y >> (8 * k0)) & 0xffu, y1 = (y >> (8 * k0 + 8)) & 0xffu;
-            const uint4 *t = pwk + (ex - 1u) * 512u + 64u * e;  // rows 4e .. 4e+3
-            const uint4 t0 = t[y0 >> 4], t1 = t[16u + (y0 & 15u)], t2 = t[32u + (y1 >> 4)], t3 = t[48u + (y1 & 15u)];
-            a0 ^= xor3(t0.x, t1.x, t2.x) ^ t3.x;
-            a1 ^= xor3(t0.y, t1.y, t2.y) ^ t3.y;
-            a2 ^= xor3(t0.z, t1.z, t2.z) ^ t3.z;
-            a3 ^= xor3(t0.w, t1.w, t2.w) ^ t3.w;
+        const uint4 *pwk = b.pw_table + (size_t)key * kPwPowers * 512u + 64u * e;  // rows 4e .. 4e+3
+        const uint32_t xa = c + 1u, xb = c + 65u;
+        const bool va = xa <= emax, vb = xb <= emax;
+        const uint4 ca = va ? gblock(xa) : uint4{0, 0, 0, 0}, cb = vb ? gblock(xb) : uint4{0, 0, 0, 0};
+        const uint32_t ya = w == 0 ? ca.x : w == 1 ? ca.y : w == 2 ? ca.z : ca.w;
+        const uint32_t yb = w == 0 ? cb.x : w == 1 ? cb.y : w == 2 ? cb.z : cb.w;
+        const uint32_t a0b = (ya >> (8 * k0)) & 0xffu, a1b = (ya >> (8 * k0 + 8)) & 0xffu;
+        const uint32_t b0b = (yb >> (8 * k0)) & 0xffu, b1b = (yb >> (8 * k0 + 8)) & 0xffu;
+        const uint4 *ta = pwk + (xa - 1u) * 512u, *tb = pwk + (xb - 1u) * 512u;
+        if (va) {
+            f0 = ta[a0b >> 4];
+            f1 = ta[16u + (a0b & 15u)];
+            f2 = ta[32u + (a1b >> 4)];
+            f3 = ta[48u + (a1b & 15u)];
         }
-#pragma unroll
-        for (int sh = 1; sh < 64; sh <<= 1) {
-            a0 ^= __shfl_xor(a0, sh, 64);
-            a1 ^= __shfl_xor(a1, sh, 64);
-            a2 ^= __shfl_xor(a2, sh, 64);
-            a3 ^= __shfl_xor(a3, sh, 64);
+        if (vb) {
+            f4 = tb[b0b >> 4];
+            f5 = tb[16u + (b0b & 15u)];
+            f6 = tb[32u + (b1b >> 4)];
+            f7 = tb[48u + (b1b & 15u)];
         }
-        if (lane == 0) lds_st128(kOneX + 16 * (tid >> 6), uint4{a0, a1, a2, a3});
+    };
+    auto flat_consume = [&]() {
+        fa0 = xor3(xor3(f0.x, f1.x, f2.x), xor3(f3.x, f4.x, f5.x), f6.x ^ f7.x);
+        fa1 = xor3(xor3(f0.y, f1.y, f2.y), xor3(f3.y, f4.y, f5.y), f6.y ^ f7.y);
+        fa2 = xor3(xor3(f0.z, f1.z, f2.z), xor3(f3.z, f4.z, f5.z), f6.z ^ f7.z);
+        fa3 = xor3(xor3(f0.w, f1.w, f2.w), xor3(f3.w, f4.w, f5.w), f6.w ^ f7.w);
+        fed = true;
+    };
+    auto row_xor = [](uint32_t v) {  // XOR over the 16 lanes of each row, in every lane of it
+        v = quad_xor(v);
+        v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xf, 0xf, false);  // row_half_mirror
+        v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xf, 0xf, false);  // row_mirror
+        return __builtin_amdgcn_readlane(v, 0) ^ __builtin_amdgcn_readlane(v, 16) ^ __builtin_amdgcn_readlane(v, 32) ^
+               __builtin_amdgcn_readlane(v, 48);
+    };
+    auto flat_finish = [&]() {
+        if (!fed) flat_consume();
+        const uint32_t r0 = row_xor(fa0), r1 = row_xor(fa1), r2 = row_xor(fa2), r3 = row_xor(fa3);
+        if (lane == 0) lds_st128(kOneX + 16 * (tid >> 6), uint4{r0, r1, r2, r3});
         lds_barrier();
         if (tid == 0) {
             uint4 y = lds128(kOneX);
@@ -1425,7 +1451,7 @@ __device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_t
     };
 
     auto ghash = [&]() {
-        if (flat) return ghash_flat();
+        if (flat) return flat_finish();
         const uint32_t c = tid >> 3, e = tid & 7u;
         uint32_t z0 = 0, z1 = 0, z2 = 0, z3 = 0;
         // Exponents 1 (the length block) .. d + 2 (the AAD block; zero without additional data), so
@@ -1512,6 +1538,10 @@ __device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_t
 #ifdef QGCM_RES_TRACE
         if (kSys) res_stamp(2);
 #endif
+        if (flat) {  // the table reads before the early stores (see flat_issue)
+            flat_issue();
+            flat_consume();
+        }
         // the rows that end before the tag go out now; their stores complete while GHASH runs
         const uint32_t early = (4u + L) >> 4;
         for (uint32_t i = tid; i < early; i += kOneThreads) slot_st16<kSys>(out, i, row(i));
@@ -1542,8 +1572,10 @@ __device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_t
         // GHASH); on a tag mismatch it is overwritten with zeros below, once these stores have landed
         const __amdgpu_buffer_rsrc_t ro =
             __builtin_amdgcn_make_buffer_rsrc(out, 0, (int)(kSys ? kResSlotBytes : kOneCap), 0x00020000);
+        if (flat) flat_issue();  // the GHASH table reads run under the counter blocks
         ctr_run(
             [&](uint32_t j, uint32_t q, uint32_t w) {  // quads: four lanes store one block's 16 B together
+                if (flat && !fed) flat_consume();
                 const uint32_t off = 4 + 16 * j + 4 * q;
                 __builtin_amdgcn_raw_buffer_store_b32(lds32(P + 16 * j + 4 * q) ^ w, ro, (int)off, 0,
                                                       kSys ? kSc0Sc1 : 0);
