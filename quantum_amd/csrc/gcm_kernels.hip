@@ -1386,46 +1386,41 @@ __device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_t
         return cb;
     };
     // Flat GHASH for packets with d + 2 <= kPwPowers exponents: every product B_ex H^ex is independent,
-    // looked up in the key's comb table of H^ex (global memory, L2-resident): chain c's 8 lanes take
-    // ex = c + 1 and c + 65, lane e the four windows of bytes 2e, 2e+1.  One round of independent table
+    // looked up in the key's 8-bit comb table of H^ex (global memory): chain c's 8 lanes take
+    // ex = c + 1 and c + 65, lane e the entries of bytes 2e and 2e+1 (the 4-bit comb needed twice the
+    // reads, and a wave's random 16-B reads cost the texture path about a cycle each).  One round of independent table
     // reads replaces the Horner step and the Estrin levels' dependent multiplies and barriers.  In
     // three phases: flat_issue (the block reads and table loads), flat_consume (their XOR; it waits for
     // the loads, so it comes before this thread's first global store -- vmcnt would wait for those too),
     // flat_finish (the 512 partials XOR-reduced: DPP within rows, readlane across them, LDS across waves).
     // An open issues the loads before its counter blocks (the ciphertext is staged) and consumes them
     // before its first plaintext store, so the table latency hides behind the rounds.
-    uint4 f0{}, f1{}, f2{}, f3{}, f4{}, f5{}, f6{}, f7{};
+    uint4 f0{}, f1{}, f2{}, f3{};
     uint32_t fa0 = 0, fa1 = 0, fa2 = 0, fa3 = 0;
     bool fed = false;
     auto flat_issue = [&]() {
         const uint32_t c = tid >> 3, e = tid & 7u, w = e >> 1, k0 = 2u * (e & 1u);
-        const uint4 *pwk = b.pw_table + (size_t)key * kPwPowers * 512u + 64u * e;  // rows 4e .. 4e+3
+        const uint4 *pwk = b.pw_table + (size_t)key * kPwPowers * kPwEntries + 512u * e;  // bytes 2e, 2e+1
         const uint32_t xa = c + 1u, xb = c + 65u;
         const bool va = xa <= emax, vb = xb <= emax;
         const uint4 ca = va ? gblock(xa) : uint4{0, 0, 0, 0}, cb = vb ? gblock(xb) : uint4{0, 0, 0, 0};
         const uint32_t ya = w == 0 ? ca.x : w == 1 ? ca.y : w == 2 ? ca.z : ca.w;
         const uint32_t yb = w == 0 ? cb.x : w == 1 ? cb.y : w == 2 ? cb.z : cb.w;
-        const uint32_t a0b = (ya >> (8 * k0)) & 0xffu, a1b = (ya >> (8 * k0 + 8)) & 0xffu;
-        const uint32_t b0b = (yb >> (8 * k0)) & 0xffu, b1b = (yb >> (8 * k0 + 8)) & 0xffu;
-        const uint4 *ta = pwk + (xa - 1u) * 512u, *tb = pwk + (xb - 1u) * 512u;
+        const uint4 *ta = pwk + (xa - 1u) * kPwEntries, *tb = pwk + (xb - 1u) * kPwEntries;
         if (va) {
-            f0 = ta[a0b >> 4];
-            f1 = ta[16u + (a0b & 15u)];
-            f2 = ta[32u + (a1b >> 4)];
-            f3 = ta[48u + (a1b & 15u)];
+            f0 = ta[(ya >> (8 * k0)) & 0xffu];
+            f1 = ta[256u + ((ya >> (8 * k0 + 8)) & 0xffu)];
         }
         if (vb) {
-            f4 = tb[b0b >> 4];
-            f5 = tb[16u + (b0b & 15u)];
-            f6 = tb[32u + (b1b >> 4)];
-            f7 = tb[48u + (b1b & 15u)];
+            f2 = tb[(yb >> (8 * k0)) & 0xffu];
+            f3 = tb[256u + ((yb >> (8 * k0 + 8)) & 0xffu)];
         }
     };
     auto flat_consume = [&]() {
-        fa0 = xor3(xor3(f0.x, f1.x, f2.x), xor3(f3.x, f4.x, f5.x), f6.x ^ f7.x);
-        fa1 = xor3(xor3(f0.y, f1.y, f2.y), xor3(f3.y, f4.y, f5.y), f6.y ^ f7.y);
-        fa2 = xor3(xor3(f0.z, f1.z, f2.z), xor3(f3.z, f4.z, f5.z), f6.z ^ f7.z);
-        fa3 = xor3(xor3(f0.w, f1.w, f2.w), xor3(f3.w, f4.w, f5.w), f6.w ^ f7.w);
+        fa0 = xor3(f0.x, f1.x, f2.x) ^ f3.x;
+        fa1 = xor3(f0.y, f1.y, f2.y) ^ f3.y;
+        fa2 = xor3(f0.z, f1.z, f2.z) ^ f3.z;
+        fa3 = xor3(f0.w, f1.w, f2.w) ^ f3.w;
         fed = true;
     };
     auto row_xor = [](uint32_t v) {  // XOR over the 16 lanes of each row, in every lane of it
@@ -2035,11 +2030,12 @@ hipError_t launch_key_setup(const uint8_t *d_keys, uint32_t first, uint32_t coun
     return hipGetLastError();
 }
 
-// The latency engine's flat GHASH tables (one_packet): the 4-bit comb tables of H^1 .. H^kPwPowers of
-// each key slot below pw_keys, 8 KiB each, in the key-setup layout (entry 16 p + v).  One 256-thread
-// workgroup per key, after key_setup_kernel (H is read back from the slot's comb table of H: entry
-// (p 0, v 8) = x^0 * H).  Powers by doubling levels, H^(t+1) = H^(t+1-2^l) * H^(2^l); then 16 powers at a
-// time, x^i * H^k for i < 128 in LDS and the comb entries from them.
+// The latency engine's flat GHASH tables (one_packet): the 8-bit comb tables of H^1 .. H^kPwPowers of
+// each key slot below pw_keys -- entry (byte position B, byte value u) = sum over the set bits of u
+// (MSB = x^(8B)) of x^(8B + j) * H^k, 16 x 256 x 16 B = 64 KiB per power, 8 MiB per key.  One 256-thread
+// workgroup per key, after key_setup_kernel (H is read back from the slot's 4-bit comb table of H:
+// entry (p 0, v 8) = x^0 * H).  Powers by doubling levels, H^(t+1) = H^(t+1-2^l) * H^(2^l); then 16 powers
+// at a time, x^i * H^k for i < 128 in LDS and the comb entries from them.
 __global__ void __launch_bounds__(256) pw_setup_kernel(uint32_t first, const uint4 *gh_table, uint4 *pw,
                                                        uint32_t pw_keys) {
     __shared__ uint8_t hp[kPwPowers][16];  // H^1 .. H^128
@@ -2068,19 +2064,19 @@ __global__ void __launch_bounds__(256) pw_setup_kernel(uint32_t first, const uin
             }
         }
         __syncthreads();
-        for (uint32_t e = tid; e < 16u * 512u; e += 256) {
-            const uint32_t j = e >> 9, q = e & 511u, pp = q >> 4, v = q & 15u;
+        for (uint32_t e = tid; e < 16u * kPwEntries; e += 256) {
+            const uint32_t j = e / kPwEntries, q = e % kPwEntries, pos = q >> 8, u = q & 255u;
             uint4 acc = {0, 0, 0, 0};
-            for (int k = 0; k < 4; ++k) {
-                if ((v >> (3 - k)) & 1u) {
-                    const uint4 t = xs[j][4 * pp + k];
+            for (int k = 0; k < 8; ++k) {
+                if ((u >> (7 - k)) & 1u) {
+                    const uint4 t = xs[j][8 * pos + k];
                     acc.x ^= t.x;
                     acc.y ^= t.y;
                     acc.z ^= t.z;
                     acc.w ^= t.w;
                 }
             }
-            pw[((size_t)slot * kPwPowers + b0 + j) * 512u + q] = acc;
+            pw[((size_t)slot * kPwPowers + b0 + j) * kPwEntries + q] = acc;
         }
         __syncthreads();
     }

@@ -48,7 +48,7 @@ struct qgcm_ctx {
     uint32_t *d_rk = nullptr;
     uint4 *d_gh = nullptr;
     uint4 *d_pw = nullptr;   // per-packet flat GHASH: comb tables of H^1..H^kPwPowers, key slots < pw_keys
-    uint32_t pw_keys = 0;    // (1 MiB per key; QGCM_FLAT_GHASH_KEYS, default min(max_keys, 4096), 0 = off)
+    uint32_t pw_keys = 0;    // (8 MiB per key; QGCM_FLAT_GHASH_KEYS, default min(max_keys, 256), 0 = off)
     uint32_t *d_te = nullptr;
     uint8_t *d_sbox = nullptr;
     uint8_t *d_key_valid = nullptr;  // device view of key_set (descriptor batches check it per packet)
@@ -557,10 +557,10 @@ qgcm_ctx *qgcm_create(int device, uint32_t max_keys, char *err, int errlen) {
               hipMemcpy(ctx->d_te, te, sizeof te, hipMemcpyHostToDevice) == hipSuccess &&
               hipMemcpy(ctx->d_sbox, sbox, sizeof sbox, hipMemcpyHostToDevice) == hipSuccess &&
               hipEventCreateWithFlags(&ctx->ws_done, hipEventDisableTiming) == hipSuccess;
-    ctx->pw_keys = (uint32_t)std::min<int64_t>(max_keys, std::max(0, env_int("QGCM_FLAT_GHASH_KEYS", 4096)));
+    ctx->pw_keys = (uint32_t)std::min<int64_t>(max_keys, std::max(0, env_int("QGCM_FLAT_GHASH_KEYS", 256)));
     if (ok && ctx->pw_keys &&
-        (hipMalloc(&ctx->d_pw, (size_t)ctx->pw_keys * kPwPowers * 512 * 16) != hipSuccess ||
-         hipMemset(ctx->d_pw, 0, (size_t)ctx->pw_keys * kPwPowers * 512 * 16) != hipSuccess)) {
+        (hipMalloc(&ctx->d_pw, (size_t)ctx->pw_keys * kPwPowers * kPwEntries * 16) != hipSuccess ||
+         hipMemset(ctx->d_pw, 0, (size_t)ctx->pw_keys * kPwPowers * kPwEntries * 16) != hipSuccess)) {
         hipFree(ctx->d_pw);  // no room: the per-packet path keeps the Horner + Estrin GHASH
         ctx->d_pw = nullptr;
         ctx->pw_keys = 0;
