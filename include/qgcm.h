@@ -131,8 +131,12 @@ long qgcm_open_one(qgcm_ctx *ctx, uint32_t key_idx, uint8_t *data, long len, con
  * a request or QGCM_RESIDENT_LIFE_US (8000) of life, after serving what is pending (the next call starts
  * it again): work queued behind it on a shared hardware queue, or a device-wide synchronize, waits that
  * long at most.  qgcm_set_key(s) and qgcm_destroy end it too (it caches key tables).
- * qgcm_resident_stop ends it now; qgcm_resident_stats writes {requests served, instances launched,
- * request slots, workers running now} (min(n, 4) values, returns that number or -1). */
+ * A seal without a caller's nonce draws the nonce of its slot's NEXT seal too and hands it to the worker,
+ * which computes that nonce's counter blocks while idle (QGCM_RESIDENT_AHEAD=0: off); the next seal
+ * on the slot uses that nonce (drawn from getrandom like any other, used once) and skips the counter
+ * blocks.  qgcm_resident_stop ends it now; qgcm_resident_stats writes {requests served, instances
+ * launched, request slots, workers running now, seals served from a keystream computed ahead}
+ * (min(n, 5) values, returns that number or -1). */
 int qgcm_resident_stop(qgcm_ctx *ctx);
 int qgcm_resident_stats(const qgcm_ctx *ctx, uint64_t *out, int n);
 

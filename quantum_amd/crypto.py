@@ -67,10 +67,11 @@ class Context:
         return dict(zip(names, (int(x) for x in out)))
 
     def resident_stats(self) -> dict:
-        """The resident per-packet kernel: requests served, instances launched, slots, workers running."""
-        out = (C.c_uint64 * 4)()
-        _lib.check(_lib.lib().qgcm_resident_stats(self.handle, out, 4), "qgcm_resident_stats")
-        return dict(zip(("served", "launches", "slots", "running"), (int(x) for x in out)))
+        """The resident per-packet kernel: requests served, instances launched, slots, workers running,
+        seals served from a keystream computed ahead."""
+        out = (C.c_uint64 * 5)()
+        _lib.check(_lib.lib().qgcm_resident_stats(self.handle, out, 5), "qgcm_resident_stats")
+        return dict(zip(("served", "launches", "slots", "running", "ahead_hits"), (int(x) for x in out)))
 
     def resident_stop(self) -> None:
         _lib.check(_lib.lib().qgcm_resident_stop(self.handle), "qgcm_resident_stop")

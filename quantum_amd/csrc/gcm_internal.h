@@ -114,6 +114,7 @@ struct ResArgs {
     uint8_t *out;           // host: [S][kResSlotBytes] result bytes
     uint32_t *done;         // host: [S]
     uint32_t *over;         // host: generation of the last instance that ended
+    uint32_t *hits;         // host: worker w's count of seals served from a keystream ahead, at 16 w
     uint8_t *dev;           // device control words (kResDevBytes), zeroed per launch
     uint32_t workers, per_worker, gen, pad;
     uint64_t idle_ticks, life_ticks;
@@ -124,7 +125,7 @@ Resident *resident_create(int device, const Batch &base, int num_cus);  // nullp
 void resident_destroy(Resident *r);
 int resident_quiesce(Resident *r);
 int resident_workers_running(const Resident *r);
-void resident_stats(const Resident *r, uint64_t out[4]);  // served, launches, slots, workers running
+void resident_stats(const Resident *r, uint64_t out[5]);  // served, launches, slots, workers running, ahead hits
 constexpr long kResNotServed = -1000;  // resident_call: the request does not fit; take the launch path
 bool random_nonce(uint8_t out[12]);   // getrandom, buffered per thread, fork-safe (resident.cpp)
 long resident_call(Resident *r, bool seal, uint32_t key, uint8_t *data, long len, const uint8_t *aad,

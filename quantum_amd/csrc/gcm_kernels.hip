@@ -1198,18 +1198,72 @@ __device__ __forceinline__ void one_fill_te(const uint32_t *te, uint32_t tid) {
     }
 }
 
+// Word q of the counter block E_K(nonce || ctr), ctr < 256, column-sliced: the four lanes of a quad own
+// the four columns of one block's state, each looks up 4 table entries per round instead of 16 and
+// takes the other columns from its quad by DPP (a lone packet is bound by the rounds' latency, which
+// this cuts, not by the tables).  All four lanes of the quad call it together.
+__device__ __forceinline__ uint32_t ctr_sliced_word(const Keys &kk, uint32_t n0, uint32_t n1, uint32_t n2, uint32_t ctr,
+                                                    uint32_t q, uint32_t lb) {
+    uint32_t rq[11];
+#pragma unroll
+    for (int i = 0; i < 11; ++i) rq[i] = kk.rr[4 * (3 + i) + q];  // this column's round keys
+    const uint32_t rl = kk.rk[56 + q];
+    Ctr cc;
+    ctr_setup(cc, n0, n1, n2, 0u, kk, lb);  // every counter here is below 256: one segment
+    const uint32_t x = (ctr & 0xffu) ^ cc.x3;
+    const uint32_t tv = cc.K0 ^ rot16(lds32(((x << 8) | lb) + 128u));  // as ctr_block_t
+    const uint32_t kq = (4u - q) & 3u;  // byte of tv that column q looks up: 0, 3, 2, 1
+    uint32_t sv = lds32(perm(tv, lb, 0x0c0c0400u + (kq << 8)) + ((q & 1u) ? 128u : 0u));
+    if (q == 1 || q == 2) sv = rot16(sv);
+    sv ^= q == 0 ? cc.U0 : q == 1 ? cc.U1 : q == 2 ? cc.U2 : cc.U3;
+    const TT0 t{lb, 0};
+    // column q of round rr: Te0[s_q.b0] ^ Te1[s_q+1.b1] ^ rot16(Te0[s_q+2.b2] ^ Te1[s_q+3.b3] ^ rr)
+#pragma unroll
+    for (int i = 0; i < 11; ++i) {
+        const uint32_t s1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)sv, 0x39, 0xf, 0xf, false);
+        const uint32_t s2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)sv, 0x4E, 0xf, 0xf, false);
+        const uint32_t s3 = (uint32_t)__builtin_amdgcn_mov_dpp((int)sv, 0x93, 0xf, 0xf, false);
+        const uint32_t c0 = t.t0(sv, 0), c1 = t.t1(s1, 1), a0 = t.t0(s2, 2), a1 = t.t1(s3, 3);
+        asm volatile("" ::: "memory");
+        sv = xor3(c0, c1, rot16(xor3(a0, a1, rq[i])));
+    }
+    const uint32_t s1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)sv, 0x39, 0xf, 0xf, false);
+    const uint32_t s2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)sv, 0x4E, 0xf, 0xf, false);
+    const uint32_t s3 = (uint32_t)__builtin_amdgcn_mov_dpp((int)sv, 0x93, 0xf, 0xf, false);
+    const uint32_t a0 = t.t0(s1, 1), a1 = t.t0(sv, 0), a2 = t.t1(s3, 3), a3 = t.t0(s2, 2);
+    asm volatile("" ::: "memory");
+    return xor3(perm(a0, a1, 0x0c0c0501u), perm(a2, a3, 0x07020c0cu), rl);  // as round_last
+}
+
+// Keystream ahead (the resident kernel, seals): a worker that has been told the nonce of a slot's next
+// seal computes, while it has nothing else to do, that nonce's counter blocks into LDS -- kKsBlocks
+// blocks of 16 B, blocks 0 .. kKsBlocks-2 = E_K(inc32(J0) + j), the last E_K(J0) -- in the comb-table
+// area, which packets on the flat GHASH (every packet up to 2016 B of a key with flat tables) leave
+// unused; the seal that comes with that nonce then starts its GHASH right after staging.
+constexpr uint32_t kKsBlocks = kOneThreads / 4;           // one quad per block: 2032 B of payload + J0
+constexpr uint32_t kKsBytes = 16 * kKsBlocks;             // 2 KiB per slot
+constexpr uint32_t kKsSlots = kOneTabs * kGhBytes / kKsBytes;  // 28 slots of a worker can hold one
+__device__ __forceinline__ void ks_fill(const uint32_t *__restrict__ rk_table, uint32_t key, uint32_t n0, uint32_t n1,
+                                        uint32_t n2, uint32_t dst) {
+    const uint32_t tid = threadIdx.x, j = tid >> 2, q = tid & 3u, lb = (tid & 31u) << 2;
+    const Keys kk = {rk_table + (size_t)key * kRkWords, rk_table + (size_t)key * kRkWords + 64};
+    lds_st32(dst + 16u * j + 4u * q, ctr_sliced_word(kk, n0, n1, n2, j == kKsBlocks - 1u ? 1u : j + 2u, q, lb));
+}
+
 // One packet on one kOneThreads workgroup, tables already in LDS except (fill_te) the T-tables and the
 // comb tables of H^(2^l) that this packet needs beyond what `tab_key` / `tab_n` say is loaded (both
 // workgroup-uniform, updated here; a caller serving several packets puts a workgroup barrier
 // between two calls).  The slot (16-B aligned, (4 + Lin (+ 28 for seal) + 15) & ~15
 // bytes, checked by the caller) is staged in LDS, sealed or opened there and written back whole.
-// nonce: seal only, 12 B, or NULL for the nonce already in the slot.  Returns the verdict (1 ok, 0
-// authentication failure), the same on every thread.
+// nonce: seal only, 12 B, or NULL for the nonce already in the slot.  ks_tag / ks_lds (seal, resident
+// kernel): a keystream computed ahead (ks_fill), used when its tag names this key and nonce.  Returns
+// the verdict (bit 0: 1 ok, 0 authentication failure; bit 1: the keystream ahead was used), the same
+// on every thread.
 template <bool kSeal, bool kSys>
 __device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_table, const uint8_t *in, uint8_t *out,
                                uint32_t Lin,
                                uint32_t key, uint32_t aad_len, const uint8_t *nonce, bool fill_te, uint32_t &tab_key,
-                               uint32_t &tab_n) {
+                               uint32_t &tab_n, uint32_t ks_tag = 0, uint32_t ks_lds = 0) {
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
     const uint32_t n16 = (uint32_t)((4ull + Lin + (kSeal ? QGCM_OVERHEAD : 0) + 15) >> 4);
@@ -1292,6 +1346,10 @@ __device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_t
     uint32_t m0, m1, m2, m3;
     block_mask(r, m0, m1, m2, m3);
     const bool sliced = d + 1 <= kOneSliceMax;  // workgroup-uniform
+    // a seal whose nonce's keystream a resident worker computed ahead (ks_tag: {key + 1, nonce} in LDS,
+    // ks_lds: the blocks; see ks_fill); flat packets have d + 2 <= kPwPowers, so d < kKsBlocks - 1
+    const bool use_ks = kSeal && ks_tag && flat && lds32(ks_tag) == key + 1u && lds32(ks_tag + 4) == n0 &&
+                        lds32(ks_tag + 8) == n1 && lds32(ks_tag + 12) == n2;  // workgroup-uniform
 
     // 2. Counter blocks; block d is E_K(J0) (into scratch), and emit(j, q, w) takes word q of block j's
     // keystream (masked to the payload in the partial block).  Packets of up to kOneSliceMax blocks
@@ -1308,40 +1366,12 @@ __device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_t
                 emit(j, q, w);
             }
         };
-        if (sliced) {
+        if (use_ks) {  // the keystream computed ahead for this nonce (resident kernel): LDS reads
             const uint32_t j = tid >> 2, q = tid & 3u;
-            if (j <= d) {  // quad-uniform: the DPP exchanges stay within active quads
-                uint32_t rq[11];
-#pragma unroll
-                for (int i = 0; i < 11; ++i) rq[i] = kk.rr[4 * (3 + i) + q];  // this column's round keys
-                const uint32_t rl = kk.rk[56 + q];
-                Ctr cc;
-                ctr_setup(cc, n0, n1, n2, 0u, kk, lb);  // every counter here is below 256: one segment
-                const uint32_t ctr = j == d ? 1u : j + 2u;
-                const uint32_t x = (ctr & 0xffu) ^ cc.x3;
-                const uint32_t tv = cc.K0 ^ rot16(lds32(((x << 8) | lb) + 128u));  // as ctr_block_t
-                const uint32_t kq = (4u - q) & 3u;  // byte of tv that column q looks up: 0, 3, 2, 1
-                uint32_t sv = lds32(perm(tv, lb, 0x0c0c0400u + (kq << 8)) + ((q & 1u) ? 128u : 0u));
-                if (q == 1 || q == 2) sv = rot16(sv);
-                sv ^= q == 0 ? cc.U0 : q == 1 ? cc.U1 : q == 2 ? cc.U2 : cc.U3;
-                const TT0 t{lb, 0};
-                // column q of round rr: Te0[s_q.b0] ^ Te1[s_q+1.b1] ^ rot16(Te0[s_q+2.b2] ^ Te1[s_q+3.b3] ^ rr)
-#pragma unroll
-                for (int i = 0; i < 11; ++i) {
-                    const uint32_t s1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)sv, 0x39, 0xf, 0xf, false);
-                    const uint32_t s2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)sv, 0x4E, 0xf, 0xf, false);
-                    const uint32_t s3 = (uint32_t)__builtin_amdgcn_mov_dpp((int)sv, 0x93, 0xf, 0xf, false);
-                    const uint32_t c0 = t.t0(sv, 0), c1 = t.t1(s1, 1), a0 = t.t0(s2, 2), a1 = t.t1(s3, 3);
-                    asm volatile("" ::: "memory");
-                    sv = xor3(c0, c1, rot16(xor3(a0, a1, rq[i])));
-                }
-                const uint32_t s1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)sv, 0x39, 0xf, 0xf, false);
-                const uint32_t s2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)sv, 0x4E, 0xf, 0xf, false);
-                const uint32_t s3 = (uint32_t)__builtin_amdgcn_mov_dpp((int)sv, 0x93, 0xf, 0xf, false);
-                const uint32_t a0 = t.t0(s1, 1), a1 = t.t0(sv, 0), a2 = t.t1(s3, 3), a3 = t.t0(s2, 2);
-                asm volatile("" ::: "memory");
-                put(j, q, xor3(perm(a0, a1, 0x0c0c0501u), perm(a2, a3, 0x07020c0cu), rl));  // as round_last
-            }
+            if (j <= d) put(j, q, lds32(ks_lds + 16u * (j == d ? kKsBlocks - 1u : j) + 4u * q));
+        } else if (sliced) {
+            const uint32_t j = tid >> 2, q = tid & 3u;
+            if (j <= d) put(j, q, ctr_sliced_word(kk, n0, n1, n2, j == d ? 1u : j + 2u, q, lb));  // quad-uniform
         } else {
             for (uint32_t j = tid; j <= d; j += kOneThreads) {
                 const uint32_t ctr = j == d ? 1u : j + 2u;  // J0, or inc32(J0) + j
@@ -1562,6 +1592,7 @@ __device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_t
         if (kSys) res_stamp(1);
 #endif
         for (uint32_t i = early + tid; i < n16; i += kOneThreads) slot_st16<kSys>(out, i, row(i));
+        ok |= use_ks ? 2u : 0u;
     } else {
         // the plaintext goes straight from registers to the output (the staged ciphertext stays for
         // GHASH); on a tag mismatch it is overwritten with zeros below, once these stores have landed
@@ -1666,7 +1697,12 @@ __global__ void __launch_bounds__(kOneThreads) gcm_one_kernel(Batch b, const uin
 constexpr uint32_t kResCtl = (kOneLds + 15u) & ~15u;  // LDS: [0] command, [8,16) pending mask
 constexpr uint32_t kResDone = kResCtl + 64;           // the done sequence of each of the worker's slots
 constexpr uint32_t kResRec = kResDone + 4 * kResMaxPerWorker;  // the request records being served
-constexpr uint32_t kResLds = kResRec + 16 * kResMaxPerWorker;
+// keystream ahead (ks_fill), per slot below kKsSlots: {state, next nonce}; state 0: none, kKsPending |
+// (key + 1): the nonce of the slot's next seal is known, (key + 1): its keystream is in LDS
+constexpr uint32_t kResKs = kResRec + 16 * kResMaxPerWorker;
+constexpr uint32_t kResLds = kResKs + 16 * kResMaxPerWorker;
+constexpr uint32_t kKsPending = 0x80000000u;
+static_assert(kPwPowers - 2 < kKsBlocks - 1, "a flat packet's counter blocks fit the keystream ahead");
 static_assert(kResLds <= 160u * 1024u, "gfx950 LDS is 160 KiB per workgroup");
 #ifdef QGCM_RES_TRACE
 // per op (open 0, seal 1), sums of: poll -> staged, staged -> stamp 2, staged -> stamp 3, staged ->
@@ -1694,7 +1730,10 @@ __global__ void __launch_bounds__(kOneThreads) gcm_resident_kernel(Batch b, cons
     uint64_t *const ctl = reinterpret_cast<uint64_t *>(a.dev);  // [0] last activity, [1] shutdown, [2] left
     one_fill_te(b.te, tid);
     if (tid < P) lds_st32(kResDone + 4 * tid, ld_sys32(a.done + first + tid) >> 1);
+    if (tid < P) lds_st32(kResKs + 16 * tid, 0u);
     uint32_t tab_key = 0xffffffffu, tab_n = 0, idle = 0;  // idle: wave 0's count of empty polls
+    uint32_t hits = tid == 0 ? ld_sys32(a.hits + 16 * w) : 0u;  // seals served from a keystream ahead
+    const uint32_t nks = P < kKsSlots ? P : kKsSlots;
     const uint64_t t_start = wall_clock64();
     __syncthreads();
     for (;;) {
@@ -1737,7 +1776,21 @@ __global__ void __launch_bounds__(kOneThreads) gcm_resident_kernel(Batch b, cons
         uint64_t t_poll = wall_clock64();  // after the poll that found the requests
         uint64_t c_poll = clock64();       // shader clock, for the clock rate while serving
 #endif
-        if (cmd == 0) {
+        if (cmd == 0) {  // idle: compute one announced nonce's keystream ahead (ks_fill)
+            uint32_t jk = nks;
+            for (uint32_t k = 0; k < nks; ++k)
+                if (lds32(kResKs + 16 * k) & kKsPending) {
+                    jk = k;
+                    break;
+                }
+            if (jk < nks) {
+                const uint4 t = lds128(kResKs + 16 * jk);
+                ks_fill(rk_table, (t.x & ~kKsPending) - 1u, t.y, t.z, t.w, kTeBytes + kKsBytes * jk);
+                tab_key = 0xffffffffu;  // the comb-table area now holds keystreams
+                tab_n = 0;
+                lds_barrier();
+                if (tid == 0) lds_st32(kResKs + 16 * jk, t.x & ~kKsPending);
+            }
             __syncthreads();  // every thread has read the command before wave 0 writes the next
             continue;
         }
@@ -1746,7 +1799,8 @@ __global__ void __launch_bounds__(kOneThreads) gcm_resident_kernel(Batch b, cons
             mask &= mask - 1;
             const uint32_t sl = first + j;
             const uint4 m = lds128(kResRec + 16 * j);
-            const uint32_t q = m.x & 0x7fffffffu, op = m.y & 1u, aad = m.y >> 1, Lin = m.z, key = m.w;
+            const uint32_t q = m.x & 0x7fffffffu, op = m.y & 1u, aad = (m.y >> 1) & 0x7fu, Lin = m.z, key = m.w;
+            const bool ahead = (m.y >> 8) & 1u;  // a seal that announces the slot's next nonce
             const uint64_t stage = (4ull + Lin + (op ? QGCM_OVERHEAD : 0) + 15) & ~15ull;
             const bool valid = aad <= 4u && key < b.max_keys && b.key_valid[key] &&
                                (op ? Lin < QGCM_MAX_PAYLOAD : Lin >= (uint32_t)QGCM_OVERHEAD) &&
@@ -1754,11 +1808,26 @@ __global__ void __launch_bounds__(kOneThreads) gcm_resident_kernel(Batch b, cons
             uint32_t ok = 0;
             const uint8_t *in = a.in + (size_t)sl * kResSlotBytes;
             uint8_t *out = a.out + (size_t)sl * kResSlotBytes;
+            // the announced nonce (the slot's last 16 B), read before the packet so its load overlaps it
+            const bool announce = op && ahead && valid && j < nks && b.pw_table && key < b.pw_keys;
+            uint4 nn{0, 0, 0, 0};
+            if (announce && tid == 0) nn = host_ld16(in, kResSlotBytes, kResSlotBytes - 16);
+            const uint32_t kt = op && j < nks ? kResKs + 16 * j : 0u;
             if (valid)
-                ok = op ? one_packet<true, true>(b, rk_table, in, out, Lin, key, aad, nullptr, false, tab_key, tab_n)
+                ok = op ? one_packet<true, true>(b, rk_table, in, out, Lin, key, aad, nullptr, false, tab_key, tab_n, kt,
+                                                 kTeBytes + kKsBytes * j)
                         : one_packet<false, true>(b, rk_table, in, out, Lin, key, aad, nullptr, false, tab_key, tab_n);
+            const bool hit = (ok >> 1) & 1u;
+            ok &= 1u;
+            if (tab_n != 0 && tid < nks) {  // comb tables loaded over the keystreams ahead
+                const uint32_t st = lds32(kResKs + 16 * tid);
+                if (!(st & kKsPending)) lds_st32(kResKs + 16 * tid, 0u);
+            }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the result bytes have reached the host
             __syncthreads();
+            if (tid == 0 && kt)  // this seal used (or outdated) the slot's keystream ahead; the next one's
+                lds_st128(kt, announce ? uint4{kKsPending | (key + 1u), nn.x, nn.y, nn.z} : uint4{0, 0, 0, 0});
+            if (tid == 0 && hit) __hip_atomic_store(a.hits + 16 * w, ++hits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 #ifdef QGCM_RES_TRACE
             if (tid == 0 && valid) {
                 const uint64_t t_end = wall_clock64();

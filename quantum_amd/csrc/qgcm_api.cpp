@@ -673,18 +673,18 @@ long qgcm_seal_one(qgcm_ctx *ctx, uint32_t key_idx, uint8_t *data, long length, 
                    const uint8_t *nonce) {
     if (!ctx || !data || length < 0 || length >= (long)QGCM_MAX_PAYLOAD || aad_len > 4 || (aad_len && !aad)) return -1;
     if (!key_ok(ctx, key_idx)) return -1;
+    if (Resident *r = get_resident(ctx)) {  // no launch per call (and no HIP call); draws the nonce if NULL
+        const long rc = resident_call(r, true, key_idx, data, length, aad, aad_len, nonce);
+        if (rc != kResNotServed) {
+            ctx->count(QGCM_KERNEL_RESIDENT);
+            return rc;
+        }
+    }
     uint8_t nb[12];
     if (nonce) {
         memcpy(nb, nonce, 12);
     } else if (!random_nonce(nb)) {  // crypto/aes.go:44 rand.Read(nonce)
         return -1;
-    }
-    if (Resident *r = get_resident(ctx)) {  // no launch per call (and no HIP call)
-        const long rc = resident_call(r, true, key_idx, data, length, aad, aad_len, nb);
-        if (rc != kResNotServed) {
-            ctx->count(QGCM_KERNEL_RESIDENT);
-            return rc;
-        }
     }
     if (hipSetDevice(ctx->device) != hipSuccess) return -1;
     const uint64_t stride = ((uint64_t)length + 4 + QGCM_OVERHEAD + 15) & ~15ull;
@@ -1276,9 +1276,9 @@ int qgcm_resident_stop(qgcm_ctx *ctx) {
 
 int qgcm_resident_stats(const qgcm_ctx *ctx, uint64_t *out, int n) {
     if (!ctx || n < 0 || (n && !out)) return -1;
-    uint64_t v[4];
+    uint64_t v[5];
     resident_stats(ctx->res.load(std::memory_order_acquire), v);
-    const int m = n < 4 ? n : 4;
+    const int m = n < 5 ? n : 5;
     for (int i = 0; i < m; ++i) out[i] = v[i];
     return m;
 }

@@ -52,12 +52,19 @@ struct Resident {
     uint64_t idle_ticks = 200000, life_ticks = 800000;  // 100 MHz: 2 ms, 8 ms
     uint8_t *host = nullptr;  // pinned coherent region: done words, over, the result slots
     uint8_t *devm = nullptr;  // fine-grained device region the CPU writes: records, stop words, request slots
-    uint32_t *done = nullptr, *over = nullptr, *stop = nullptr;
+    uint32_t *done = nullptr, *over = nullptr, *stop = nullptr, *hits = nullptr;
     uint4 *req = nullptr;
     uint8_t *in = nullptr, *out = nullptr;
     uint8_t *d_ctl = nullptr;  // device control words (kResDevBytes)
     hipStream_t stream = nullptr;
     std::unique_ptr<uint32_t[]> seqh;                  // last sequence per slot (owned by the slot holder)
+    // keystream ahead (QGCM_RESIDENT_AHEAD, default on): each seal announces the nonce of its slot's
+    // next seal, whose counter blocks the worker then computes while idle (gcm_kernels.hip ks_fill).
+    // Per slot, owned by the slot holder: that nonce, and the fork generation + 1 it was drawn in (0:
+    // none) -- a forked child must not use its parent's announced nonce.
+    bool ahead = true;
+    std::unique_ptr<uint8_t[]> next_nonce;
+    std::unique_ptr<uint32_t[]> next_gen;
     std::unique_ptr<std::atomic<uint32_t>[]> busy;     // slot taken
     // per worker, each on its own cache line (every call updates them): requests served, callers
     // spinning now.  A caller's home worker is fixed per thread (quantum's workers are long-lived
@@ -129,6 +136,7 @@ int relaunch(Resident *r, uint32_t g) {
     a.out = r->out;
     a.done = r->done;
     a.over = r->over;
+    a.hits = r->hits;
     a.dev = r->d_ctl;
     a.workers = r->W;
     a.per_worker = r->P;
@@ -246,7 +254,8 @@ Resident *resident_create(int device, const Batch &base, int num_cus) {
     r->life_ticks = env_u64("QGCM_RESIDENT_LIFE_US", 8000) * 100;
     // host region: done, over, then the result slots; device region: the stop words (a 64-B line per
     // worker), the request records, then the request slots
-    const size_t o_over = (4ull * r->S + 63) & ~63ull, o_out = (o_over + 64 + 4095) & ~4095ull;
+    const size_t o_over = (4ull * r->S + 63) & ~63ull, o_hits = o_over + 64;
+    const size_t o_out = (o_hits + 64ull * r->W + 4095) & ~4095ull;
     const size_t host_bytes = o_out + (size_t)kResSlotBytes * r->S;
     const size_t o_req = 64ull * r->W, o_in = (o_req + 16ull * r->S + 4095) & ~4095ull;
     const size_t dev_bytes = o_in + (size_t)kResSlotBytes * r->S;
@@ -260,6 +269,7 @@ Resident *resident_create(int device, const Batch &base, int num_cus) {
     }
     r->done = reinterpret_cast<uint32_t *>(r->host);
     r->over = reinterpret_cast<uint32_t *>(r->host + o_over);
+    r->hits = reinterpret_cast<uint32_t *>(r->host + o_hits);
     r->out = r->host + o_out;
     r->stop = reinterpret_cast<uint32_t *>(r->devm);
     r->req = reinterpret_cast<uint4 *>(r->devm + o_req);
@@ -267,6 +277,9 @@ Resident *resident_create(int device, const Batch &base, int num_cus) {
     memset(r->devm, 0, o_in);  // stop words and records, through the BAR
     _mm_sfence();
     r->seqh.reset(new uint32_t[r->S]());
+    r->ahead = env_u64("QGCM_RESIDENT_AHEAD", 1) != 0;
+    r->next_nonce.reset(new uint8_t[12ull * r->S]());
+    r->next_gen.reset(new uint32_t[r->S]());
     r->busy.reset(new std::atomic<uint32_t>[r->S]);
     for (uint32_t i = 0; i < r->S; ++i) r->busy[i] = 0;
     r->wc.reset(new Resident::WorkerCounts[r->W]);
@@ -322,26 +335,23 @@ int resident_workers_running(const Resident *r) {
     return instance_over(r, g) ? 0 : (int)r->W;
 }
 
-void resident_stats(const Resident *r, uint64_t out[4]) {
-    uint64_t served = 0;
-    for (uint32_t w = 0; r && w < r->W; ++w) served += r->wc[w].served.load(std::memory_order_relaxed);
+void resident_stats(const Resident *r, uint64_t out[5]) {
+    uint64_t served = 0, hits = 0;
+    for (uint32_t w = 0; r && w < r->W; ++w) {
+        served += r->wc[w].served.load(std::memory_order_relaxed);
+        hits += __atomic_load_n(&r->hits[16 * w], __ATOMIC_RELAXED);
+    }
     out[0] = served;
     out[1] = r ? r->launches.load() : 0;
     out[2] = r ? r->W * (uint64_t)r->P : 0;
     out[3] = (uint64_t)resident_workers_running(r);
+    out[4] = hits;
 }
 
 long resident_call(Resident *r, bool seal, uint32_t key, uint8_t *data, long len, const uint8_t *aad,
                    uint32_t aad_len, const uint8_t *nonce) {
     const uint64_t stage = (4ull + (uint64_t)len + (seal ? QGCM_OVERHEAD : 0) + 15) & ~15ull;
     if (!r || r->broken || stage > kResSlotBytes || stage > kOneCap - 16) return kResNotServed;
-    uint8_t nb[12];
-    if (seal) {
-        if (nonce)
-            memcpy(nb, nonce, 12);
-        else if (!random_nonce(nb))  // crypto/aes.go:44 rand.Read(nonce)
-            return -1;
-    }
     // a free slot of this thread's home worker, else of the next workers in turn
     static std::atomic<uint32_t> next_thread{0};
     thread_local const uint32_t t_index = next_thread.fetch_add(1, std::memory_order_relaxed);
@@ -366,6 +376,28 @@ long resident_call(Resident *r, bool seal, uint32_t key, uint8_t *data, long len
         if (got) break;
         sched_yield();  // every slot in flight
     }
+    // the nonce: the caller's, else the one this slot's previous seal announced, else a fresh one
+    // (crypto/aes.go:44 rand.Read(nonce)); a seal without a caller's nonce announces the next one
+    uint8_t nb[12];
+    bool announce = false;
+    if (seal && nonce) {
+        memcpy(nb, nonce, 12);
+    } else if (seal) {
+        const uint32_t fg = g_fork_gen.load(std::memory_order_relaxed) + 1;
+        uint8_t *nx = &r->next_nonce[12ull * s];
+        const bool have = r->ahead && r->next_gen[s] == fg;
+        if (have)
+            memcpy(nb, nx, 12);
+        r->next_gen[s] = 0;  // used (or stale) either way
+        if (!have && !random_nonce(nb)) {
+            r->busy[s].store(0, std::memory_order_release);
+            return -1;
+        }
+        if (r->ahead && stage + 16 <= kResSlotBytes && random_nonce(nx)) {
+            r->next_gen[s] = fg;
+            announce = true;
+        }
+    }
     // the request into device memory (write-combined stores through the BAR) with its record's fields
     // under the old sequence (which the worker has served, so it ignores the record), then the new
     // sequence; sfence orders the first stores before it and pushes it out
@@ -375,12 +407,14 @@ long resident_call(Resident *r, bool seal, uint32_t key, uint8_t *data, long len
     memcpy(slot, &hdr, 4);
     memcpy(slot + 4, data, (size_t)len);
     if (seal) memcpy(slot + 4 + len + 16, nb, 12);
+    if (announce) memcpy(slot + kResSlotBytes - 16, &r->next_nonce[12ull * s], 12);
     const uint32_t q0 = r->seqh[s];
     uint32_t q = (q0 + 1) & 0x7fffffffu;
     if (q == 0) q = 1;
     r->seqh[s] = q;
     _mm_store_si128(reinterpret_cast<__m128i *>(&r->req[s]),
-                    _mm_set_epi32((int)key, (int)len, (int)((seal ? 1u : 0u) | aad_len << 1), (int)q0));
+                    _mm_set_epi32((int)key, (int)len, (int)((seal ? 1u : 0u) | aad_len << 1 | (announce ? 1u : 0u) << 8),
+                                  (int)q0));
     _mm_sfence();  // the slot bytes and the record's fields before the sequence
     __atomic_store_n(reinterpret_cast<uint32_t *>(&r->req[s]), q, __ATOMIC_RELAXED);
     _mm_sfence();

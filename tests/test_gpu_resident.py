@@ -365,3 +365,59 @@ def test_drawn_nonces_unique_and_open(torch):
         assert len(nonces) == 16000 and len(set(nonces)) == 16000
     finally:
         ctx.close()
+
+
+@pytest.mark.parametrize("ahead", [1, 0])
+def test_keystream_ahead_vs_oracle(torch, ahead, monkeypatch):
+    """Seals without a caller's nonce announce their slot's next nonce, whose counter blocks the worker
+    computes while idle (gcm_kernels.hip ks_fill); the next seal on the slot uses them.  4 threads x 400
+    seals and opens: two keys, lengths across the flat-GHASH limit (up to 2016 B the keystream ahead is
+    used; longer packets load comb tables over it, which must drop it) -- every sealed packet opens under
+    the oracle with its drawn nonce, and with QGCM_RESIDENT_AHEAD=0 nothing is served ahead."""
+    from quantum_amd.crypto import AES
+
+    monkeypatch.setenv("QGCM_RESIDENT_AHEAD", str(ahead))  # read when the first call starts the service
+    ctx = make_ctx()
+    try:
+        keys = [bytes(range(90 + 7 * i, 122 + 7 * i)) for i in range(2)]
+        aes_list = [AES(k, ctx=ctx) for k in keys]
+        errs, nonces, lock = [], [], threading.Lock()
+
+        def work(t):
+            rng = random.Random(0xA11E + t)
+            mine = []
+            for i in range(400):
+                k = 0 if i % 10 else 1
+                L = rng.choice([0, 1, 17, 1350, 1350, 1433, 2000, 2016, 2017, 2032, rng.randrange(0, 2017), 3000])
+                pt = rng.randbytes(L)
+                data = bytearray(pt + bytes(28))
+                n, err = aes_list[k].Encrypt(data, L, AAD)
+                if err is not None or n != L + 28:
+                    errs.append(f"seal t={t} i={i} L={L}")
+                    return
+                mine.append(bytes(data[L + 16:L + 28]))
+                ref = bytearray(data)
+                if O.aesgo_decrypt(keys[k], ref, AAD) != L or bytes(ref[:L]) != pt:
+                    errs.append(f"oracle open t={t} i={i} L={L} k={k}")
+                    return
+                n, err = aes_list[k].Decrypt(data, AAD)
+                if err is not None or n != L or bytes(data[:L]) != pt:
+                    errs.append(f"open t={t} i={i} L={L}")
+                    return
+            with lock:
+                nonces.extend(mine)
+
+        ths = [threading.Thread(target=work, args=(t,)) for t in range(4)]
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        assert not errs, errs[:5]
+        assert len(nonces) == 1600 and len(set(nonces)) == 1600
+        hits = ctx.resident_stats()["ahead_hits"]
+        if ahead:
+            assert hits > 400, hits  # most seals up to 2016 B after the first on a slot
+        else:
+            assert hits == 0
+    finally:
+        ctx.close()

@@ -3,7 +3,7 @@
 # reference build, and the config-2 profile (trace + PMC).  Every GPU step has its own time limit;
 # the script stops at the first step that faults, aborts or times out (a plain test failure goes on).
 # Usage: bash tools/gpu_round.sh <tag> [steps...]
-#   steps: stests policy snapdev rtests tests smoke bench ab prof pp prof3 exp_res barreq align (default: tests smoke bench ab prof)
+#   steps: stests policy snapdev rtests tests smoke bench ab prof pp prof3 exp_res res_trace ahead barreq align (default: tests smoke bench ab prof)
 set -u
 TAG=$1; shift
 STEPS=${*:-"tests smoke bench ab prof"}
@@ -86,6 +86,15 @@ for s in $STEPS; do
     barreq)
       timeout -k 10 400 bash tools/exp_barreq.sh $TAG
       check barreq $? ;;
+    ahead)  # keystream ahead on / off, interleaved: lone caller and 16 threads (per_packet_bench)
+      for rep in 1 2; do
+        for a in 1 0; do
+          for t in 1 16; do
+            QGCM_RESIDENT_AHEAD=$a timeout -k 10 60 tools/bin/per_packet_bench $t 1350 2 0 resident >> $OUT/ahead_$a.jsonl 2>> $OUT/ahead.err
+            check ahead_${a}_$t $?
+          done
+        done
+      done ;;
     align)  # config 3 packed vs 64-B aligned payloads: time, then WRITE_SIZE / FETCH_SIZE per layout
       timeout -k 10 300 python3 tools/exp_config3_align.py 9 > $OUT/align.json 2> $OUT/align.err
       check align $?

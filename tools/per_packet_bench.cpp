@@ -153,15 +153,16 @@ int main(int argc, char **argv) {
         const double wall = std::chrono::duration<double>(Clock::now() - tb).count();
         const double bulk_gibs = (bulk_calls.load() - b0) / 2.0 * 2.0 * bn * bl /
                                  std::chrono::duration<double>(Clock::now() - tb).count() / (1 << 30);
-        uint64_t st[4] = {0, 0, 0, 0}, lc[QGCM_KERNEL_COUNTERS] = {};
-        qgcm_resident_stats(ctx, st, 4);
+        uint64_t st[5] = {0, 0, 0, 0, 0}, lc[QGCM_KERNEL_COUNTERS] = {};
+        qgcm_resident_stats(ctx, st, 5);
         qgcm_launch_counts(ctx, lc, QGCM_KERNEL_COUNTERS);
         printf("{\"bench\": \"per_packet\", \"path\": \"%s\", \"threads\": %d, \"payload\": %d, \"bulk_alongside\": %s, "
                "\"round_trips_per_s\": %.0f, \"GiB_s\": %.3f, \"call_pair_p50_us\": %.1f, \"call_pair_p99_us\": %.1f, "
-               "\"failures\": %.0f, \"resident_served\": %llu, \"resident_launches\": %llu, \"one_kernel_launches\": %llu",
+               "\"failures\": %.0f, \"resident_served\": %llu, \"resident_launches\": %llu, \"one_kernel_launches\": %llu, "
+               "\"ahead_hits\": %llu",
                resident ? "resident" : "launch", threads, payload, bulk ? "true" : "false", r.rt_per_s,
                2.0 * r.rt_per_s * payload / (1 << 30), r.p50_us, r.p99_us, r.fail, (unsigned long long)st[0],
-               (unsigned long long)st[1], (unsigned long long)lc[QGCM_KERNEL_ONE]);
+               (unsigned long long)st[1], (unsigned long long)lc[QGCM_KERNEL_ONE], (unsigned long long)st[4]);
         if (bulk) printf(", \"bulk_GiB_s\": %.2f", bulk_gibs);
         if (trace && resident && trace(tr, 0) == 0) {
             for (int op = 1; op >= 0; --op) {
