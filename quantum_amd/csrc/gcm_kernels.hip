@@ -1738,23 +1738,33 @@ __global__ void __launch_bounds__(kOneThreads) gcm_resident_kernel(Batch b, cons
     __syncthreads();
     for (;;) {
         if (tid < 64) {  // one poll: every slot's record and the worker's stop word
+            // all of a poll's loads are issued before any is used: one memory latency per poll, not
+            // three or four in a row (records, stop word, shutdown word, last activity)
+            uint4 m{0, 0, 0, 0};
+            uint32_t stop = 0;
+            uint64_t shut = 0, act = 0;
+            if (lane < P) m = host_ld16(a.req, 16 * S, 16 * (first + lane));
+            if (lane == 0) {
+                stop = host_ld16(a.stop, 64u * a.workers, 64u * w).x;
+                shut = ld_agent(ctl + 1);
+                if (w == 0) act = ld_agent(ctl);  // last activity of any worker (0: none yet)
+            }
             bool pend = false;
             if (lane < P) {
-                const uint4 m = host_ld16(a.req, 16 * S, 16 * (first + lane));
                 pend = (m.x & 0x7fffffffu) != lds32(kResDone + 4 * lane);
                 if (pend) lds_st128(kResRec + 16 * lane, m);
             }
             const uint64_t pm = __ballot(pend);
-            uint32_t stop = 0;
             if (lane == 0) {
-                stop = host_ld16(a.stop, 64u * a.workers, 64u * w).x;
                 if (w == 0) {  // the instance's end: no request for idle_ticks, or life_ticks old
                     const uint64_t now = wall_clock64();
-                    const uint64_t act = ld_agent(ctl);  // last activity of any worker (0: none yet)
                     const int64_t q = (int64_t)(now - (act > t_start ? act : t_start));
-                    if (q > (int64_t)a.idle_ticks || now - t_start > a.life_ticks) st_agent(ctl + 1, (uint64_t)1);
+                    if (q > (int64_t)a.idle_ticks || now - t_start > a.life_ticks) {
+                        st_agent(ctl + 1, (uint64_t)1);
+                        shut = 1;
+                    }
                 }
-                stop |= ld_agent(ctl + 1) != 0 ? 1u : 0u;
+                stop |= shut != 0 ? 1u : 0u;
                 lds_st32(kResCtl, stop ? 2u : pm ? 1u : 0u);
                 lds_st32(kResCtl + 8, (uint32_t)pm);
                 lds_st32(kResCtl + 12, (uint32_t)(pm >> 32));

@@ -95,6 +95,19 @@ for s in $STEPS; do
           done
         done
       done ;;
+    poll)  # resident kernel A/B against the build in ablib/poll_old (LD_LIBRARY_PATH comes before RUNPATH)
+      for rep in 1 2; do
+        for lib in old new; do
+          for t in 1 16; do
+            if [ $lib = old ]; then
+              LD_LIBRARY_PATH=$PWD/ablib/poll_old timeout -k 10 60 tools/bin/per_packet_bench $t 1350 2 0 resident >> $OUT/poll_$lib.jsonl 2>> $OUT/poll.err
+            else
+              timeout -k 10 60 tools/bin/per_packet_bench $t 1350 2 0 resident >> $OUT/poll_$lib.jsonl 2>> $OUT/poll.err
+            fi
+            check poll_${lib}_$t $?
+          done
+        done
+      done ;;
     align)  # config 3 packed vs 64-B aligned payloads: time, then WRITE_SIZE / FETCH_SIZE per layout
       timeout -k 10 300 python3 tools/exp_config3_align.py 9 > $OUT/align.json 2> $OUT/align.err
       check align $?
