@@ -50,11 +50,14 @@ struct Batch {
     uint8_t *done;              // gcm_one_kernel: done[0] (uniform form, one packet) or done[pkt] (descriptor
                                 // form) set to 1 after the slot is written
                                 // back and made system-visible (the host polls it instead of the stream)
-    const uint4 *pw_table;      // latency engine: [pw_keys][kPwPowers][kPwEntries] 8-bit comb tables of
+    const uint4 *pw_table;      // latency engine: [pw_keys][kPwPowers][kPwEntries] kPwBits-bit comb tables of
     uint32_t pw_keys;           // H^1..H^kPwPowers (NULL / 0: the Horner + Estrin GHASH for every packet)
 };
 constexpr uint32_t kPwPowers = 128;    // flat GHASH up to d + 2 = 128 exponents (payloads up to 2016 B)
-constexpr uint32_t kPwEntries = 4096;  // 16 byte positions x 256 values, 64 KiB per power
+constexpr uint32_t kPwBits = 6;                                  // comb window of the flat GHASH tables
+constexpr uint32_t kPwWin = (128 + kPwBits - 1) / kPwBits;       // windows per block (22)
+constexpr uint32_t kPwEntries = kPwWin << kPwBits;               // entries per power (1408: 22 KiB)
+constexpr uint32_t kPwLaneWins = (kPwWin + 7) / 8;               // windows per lane of an 8-lane chain
 
 constexpr int kNumVariants = 15;     // ids as in round 2; only the three below are built
 constexpr int kVariantUniform = 12;  // single-key (uniform) batches: quad kernel (Tab2F), 32 waves/CU

@@ -188,21 +188,34 @@ __device__ __forceinline__ void round_last(uint32_t &s0, uint32_t &s1, uint32_t 
 // Precompute rounds 1-2 for counter blocks nonce || (ctr_hi << 8 | low byte).  Round 1: only
 // column 0 sees the varying byte (s3.b3, via Te3); round 2: each column sees exactly one byte
 // of that column 0.
+// the round-key words ctr_setup reads (rk[0..4], rk[9], rk[10]; rr[5..8], rr[11]), so a caller can
+// load them ahead (the latency engine does, before its staging barrier)
+struct SetupKeys {
+    uint32_t rk0, rk1, rk2, rk3, rk4, rr5, rr6, rr7, rr8, rk9, rk10, rr11;
+};
+__device__ __forceinline__ SetupKeys setup_keys(const Keys &k) {
+    return SetupKeys{k.rk[0], k.rk[1], k.rk[2], k.rk[3], k.rk[4], k.rr[5],
+                     k.rr[6], k.rr[7], k.rr[8], k.rk[9], k.rk[10], k.rr[11]};
+}
+template <class A>
+__device__ __forceinline__ void ctr_setup(Ctr &c, uint32_t n0, uint32_t n1, uint32_t n2, uint32_t ctr_hi,
+                                          const SetupKeys &k, const A &t) {
+    const uint32_t s0 = n0 ^ k.rk0, s1 = n1 ^ k.rk1, s2 = n2 ^ k.rk2;
+    const uint32_t s3 = bswap(ctr_hi << 8) ^ k.rk3;  // byte3 varies per block; unused below
+    c.x3 = k.rk3 >> 24;
+    c.K0 = xor3(t.t0(s0, 0), t.t1(s1, 1), rot16(t.t0(s2, 2))) ^ k.rk4;
+    const uint32_t t1 = xor3(t.t0(s1, 0), t.t1(s2, 1), rot16(xor3(t.t0(s3, 2), t.t1(s0, 3), k.rr5)));
+    const uint32_t t2 = xor3(t.t0(s2, 0), t.t1(s3, 1), rot16(xor3(t.t0(s0, 2), t.t1(s1, 3), k.rr6)));
+    const uint32_t t3 = xor3(t.t0(s3, 0), t.t1(s0, 1), rot16(xor3(t.t0(s1, 2), t.t1(s2, 3), k.rr7)));
+    c.U0 = t.t1(t1, 1) ^ rot16(xor3(t.t0(t2, 2), t.t1(t3, 3), k.rr8));
+    c.U1 = xor3(t.t0(t1, 0), t.t1(t2, 1), rot16(t.t0(t3, 2))) ^ k.rk9;
+    c.U2 = xor3(t.t0(t2, 0), t.t1(t3, 1), rot16(t.t1(t1, 3))) ^ k.rk10;
+    c.U3 = t.t0(t3, 0) ^ rot16(xor3(t.t0(t1, 2), t.t1(t2, 3), k.rr11));
+}
 template <class A>
 __device__ __forceinline__ void ctr_setup(Ctr &c, uint32_t n0, uint32_t n1, uint32_t n2, uint32_t ctr_hi,
                                           const Keys &k, const A &t) {
-    const uint32_t *rk = k.rk;
-    const uint32_t s0 = n0 ^ rk[0], s1 = n1 ^ rk[1], s2 = n2 ^ rk[2];
-    const uint32_t s3 = bswap(ctr_hi << 8) ^ rk[3];  // byte3 varies per block; unused below
-    c.x3 = rk[3] >> 24;
-    c.K0 = xor3(t.t0(s0, 0), t.t1(s1, 1), rot16(t.t0(s2, 2))) ^ rk[4];
-    const uint32_t t1 = xor3(t.t0(s1, 0), t.t1(s2, 1), rot16(xor3(t.t0(s3, 2), t.t1(s0, 3), k.rr[5])));
-    const uint32_t t2 = xor3(t.t0(s2, 0), t.t1(s3, 1), rot16(xor3(t.t0(s0, 2), t.t1(s1, 3), k.rr[6])));
-    const uint32_t t3 = xor3(t.t0(s3, 0), t.t1(s0, 1), rot16(xor3(t.t0(s1, 2), t.t1(s2, 3), k.rr[7])));
-    c.U0 = t.t1(t1, 1) ^ rot16(xor3(t.t0(t2, 2), t.t1(t3, 3), k.rr[8]));
-    c.U1 = xor3(t.t0(t1, 0), t.t1(t2, 1), rot16(t.t0(t3, 2))) ^ rk[9];
-    c.U2 = xor3(t.t0(t2, 0), t.t1(t3, 1), rot16(t.t1(t1, 3))) ^ rk[10];
-    c.U3 = t.t0(t3, 0) ^ rot16(xor3(t.t0(t1, 2), t.t1(t2, 3), k.rr[11]));
+    ctr_setup(c, n0, n1, n2, ctr_hi, setup_keys(k), t);
 }
 __device__ __forceinline__ void ctr_setup(Ctr &c, uint32_t n0, uint32_t n1, uint32_t n2, uint32_t ctr_hi,
                                           const Keys &k, uint32_t lb) {
@@ -1202,14 +1215,23 @@ __device__ __forceinline__ void one_fill_te(const uint32_t *te, uint32_t tid) {
 // the four columns of one block's state, each looks up 4 table entries per round instead of 16 and
 // takes the other columns from its quad by DPP (a lone packet is bound by the rounds' latency, which
 // this cuts, not by the tables).  All four lanes of the quad call it together.
-__device__ __forceinline__ uint32_t ctr_sliced_word(const Keys &kk, uint32_t n0, uint32_t n1, uint32_t n2, uint32_t ctr,
-                                                    uint32_t q, uint32_t lb) {
-    uint32_t rq[11];
+// Column q's round keys (rounds 3..13 and the last), loaded by the caller ahead of other memory reads:
+// a load's wait is in issue order, so round keys issued after a packet's table reads would wait for them.
+struct ColKeys {
+    uint32_t rq[11], rl;
+    SetupKeys sk;
+};
+__device__ __forceinline__ void col_keys(const Keys &kk, uint32_t q, ColKeys &ck) {
 #pragma unroll
-    for (int i = 0; i < 11; ++i) rq[i] = kk.rr[4 * (3 + i) + q];  // this column's round keys
-    const uint32_t rl = kk.rk[56 + q];
+    for (int i = 0; i < 11; ++i) ck.rq[i] = kk.rr[4 * (3 + i) + q];
+    ck.rl = kk.rk[56 + q];
+    ck.sk = setup_keys(kk);
+}
+__device__ __forceinline__ uint32_t ctr_sliced_word(const Keys &kk, const ColKeys &ck, uint32_t n0, uint32_t n1,
+                                                    uint32_t n2, uint32_t ctr, uint32_t q, uint32_t lb) {
+    const uint32_t *rq = ck.rq, rl = ck.rl;
     Ctr cc;
-    ctr_setup(cc, n0, n1, n2, 0u, kk, lb);  // every counter here is below 256: one segment
+    ctr_setup(cc, n0, n1, n2, 0u, ck.sk, TT0{lb, 0});  // every counter here is below 256: one segment
     const uint32_t x = (ctr & 0xffu) ^ cc.x3;
     const uint32_t tv = cc.K0 ^ rot16(lds32(((x << 8) | lb) + 128u));  // as ctr_block_t
     const uint32_t kq = (4u - q) & 3u;  // byte of tv that column q looks up: 0, 3, 2, 1
@@ -1247,7 +1269,9 @@ __device__ __forceinline__ void ks_fill(const uint32_t *__restrict__ rk_table, u
                                         uint32_t n2, uint32_t dst) {
     const uint32_t tid = threadIdx.x, j = tid >> 2, q = tid & 3u, lb = (tid & 31u) << 2;
     const Keys kk = {rk_table + (size_t)key * kRkWords, rk_table + (size_t)key * kRkWords + 64};
-    lds_st32(dst + 16u * j + 4u * q, ctr_sliced_word(kk, n0, n1, n2, j == kKsBlocks - 1u ? 1u : j + 2u, q, lb));
+    ColKeys ck;
+    col_keys(kk, q, ck);
+    lds_st32(dst + 16u * j + 4u * q, ctr_sliced_word(kk, ck, n0, n1, n2, j == kKsBlocks - 1u ? 1u : j + 2u, q, lb));
 }
 
 // One packet on one kOneThreads workgroup, tables already in LDS except (fill_te) the T-tables and the
@@ -1276,6 +1300,11 @@ __device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_t
         const uint32_t i = tid + k * kOneThreads;
         if (i < n16) v[k] = slot_ld16<kSys>(in, i);
     }
+    // the column-sliced counter blocks' round keys, before the table reads (see ColKeys)
+    const Keys kk = {rk_table + (size_t)key * kRkWords, rk_table + (size_t)key * kRkWords + 64};
+    const bool sliced = ((L + 15u) >> 4) + 1u <= kOneSliceMax;  // d + 1 blocks; workgroup-uniform
+    ColKeys ck{};
+    if (sliced) col_keys(kk, tid & 3u, ck);
     // The table fills load everything first and store after (one memory latency, not one per
     // iteration): Te0/Te1 words for 32 replicas per row, then the comb tables of H^(2^l) -- only the
     // ones this packet's GHASH reads (H^(2^l) for the Estrin levels up to bit-length(min(d + 2, 63)),
@@ -1328,7 +1357,6 @@ __device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_t
     if (kSys) res_stamp(0);
 #endif
 
-    const Keys kk = {rk_table + (size_t)key * kRkWords, rk_table + (size_t)key * kRkWords + 64};
     const uint32_t lb = (lane & 31u) << 2;
     const uint32_t nfull = L >> 4, r = L & 15u;
     const uint32_t d = nfull + (r ? 1u : 0u);
@@ -1345,7 +1373,6 @@ __device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_t
     }
     uint32_t m0, m1, m2, m3;
     block_mask(r, m0, m1, m2, m3);
-    const bool sliced = d + 1 <= kOneSliceMax;  // workgroup-uniform
     // a seal whose nonce's keystream a resident worker computed ahead (ks_tag: {key + 1, nonce} in LDS,
     // ks_lds: the blocks; see ks_fill); flat packets have d + 2 <= kPwPowers, so d < kKsBlocks - 1
     const bool use_ks = kSeal && ks_tag && flat && lds32(ks_tag) == key + 1u && lds32(ks_tag + 4) == n0 &&
@@ -1371,7 +1398,7 @@ __device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_t
             if (j <= d) put(j, q, lds32(ks_lds + 16u * (j == d ? kKsBlocks - 1u : j) + 4u * q));
         } else if (sliced) {
             const uint32_t j = tid >> 2, q = tid & 3u;
-            if (j <= d) put(j, q, ctr_sliced_word(kk, n0, n1, n2, j == d ? 1u : j + 2u, q, lb));  // quad-uniform
+            if (j <= d) put(j, q, ctr_sliced_word(kk, ck, n0, n1, n2, j == d ? 1u : j + 2u, q, lb));  // quad-uniform
         } else {
             for (uint32_t j = tid; j <= d; j += kOneThreads) {
                 const uint32_t ctr = j == d ? 1u : j + 2u;  // J0, or inc32(J0) + j
@@ -1416,41 +1443,54 @@ __device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_t
         return cb;
     };
     // Flat GHASH for packets with d + 2 <= kPwPowers exponents: every product B_ex H^ex is independent,
-    // looked up in the key's 8-bit comb table of H^ex (global memory): chain c's 8 lanes take
-    // ex = c + 1 and c + 65, lane e the entries of bytes 2e and 2e+1 (the 4-bit comb needed twice the
-    // reads, and a wave's random 16-B reads cost the texture path about a cycle each).  One round of independent table
-    // reads replaces the Horner step and the Estrin levels' dependent multiplies and barriers.  In
-    // three phases: flat_issue (the block reads and table loads), flat_consume (their XOR; it waits for
-    // the loads, so it comes before this thread's first global store -- vmcnt would wait for those too),
-    // flat_finish (the 512 partials XOR-reduced: DPP within rows, readlane across them, LDS across waves).
-    // An open issues the loads before its counter blocks (the ciphertext is staged) and consumes them
-    // before its first plaintext store, so the table latency hides behind the rounds.
-    uint4 f0{}, f1{}, f2{}, f3{};
+    // looked up in the key's kPwBits-bit comb table of H^ex (global memory, pw_setup_kernel): chain c's
+    // 8 lanes take ex = c + 1 and c + 65, lane e the windows e, e + 8, ... of the block (bits of the
+    // GHASH bit stream, x^0 first).  One round of independent table reads replaces the Horner step and
+    // the Estrin levels' dependent multiplies and barriers.  In three phases: flat_issue (the block reads
+    // and table loads), flat_consume (their XOR; it waits for the loads, so it comes before this thread's
+    // first global store -- vmcnt would wait for those too), flat_finish (the 512 partials XOR-reduced:
+    // DPP within rows, readlane across them, LDS across waves).  An open issues the loads before its
+    // counter blocks (the ciphertext is staged) and consumes them before its first plaintext store, so
+    // the table latency hides behind the rounds.
+    uint4 fr[2 * kPwLaneWins];
+#pragma unroll
+    for (int k = 0; k < 2 * (int)kPwLaneWins; ++k) fr[k] = uint4{0, 0, 0, 0};
     uint32_t fa0 = 0, fa1 = 0, fa2 = 0, fa3 = 0;
     bool fed = false;
     auto flat_issue = [&]() {
-        const uint32_t c = tid >> 3, e = tid & 7u, w = e >> 1, k0 = 2u * (e & 1u);
-        const uint4 *pwk = b.pw_table + (size_t)key * kPwPowers * kPwEntries + 512u * e;  // bytes 2e, 2e+1
-        const uint32_t xa = c + 1u, xb = c + 65u;
-        const bool va = xa <= emax, vb = xb <= emax;
-        const uint4 ca = va ? gblock(xa) : uint4{0, 0, 0, 0}, cb = vb ? gblock(xb) : uint4{0, 0, 0, 0};
-        const uint32_t ya = w == 0 ? ca.x : w == 1 ? ca.y : w == 2 ? ca.z : ca.w;
-        const uint32_t yb = w == 0 ? cb.x : w == 1 ? cb.y : w == 2 ? cb.z : cb.w;
-        const uint4 *ta = pwk + (xa - 1u) * kPwEntries, *tb = pwk + (xb - 1u) * kPwEntries;
-        if (va) {
-            f0 = ta[(ya >> (8 * k0)) & 0xffu];
-            f1 = ta[256u + ((ya >> (8 * k0 + 8)) & 0xffu)];
-        }
-        if (vb) {
-            f2 = tb[(yb >> (8 * k0)) & 0xffu];
-            f3 = tb[256u + ((yb >> (8 * k0 + 8)) & 0xffu)];
+        const uint32_t c = tid >> 3, e = tid & 7u;
+        const uint4 *pwk = b.pw_table + (size_t)key * kPwPowers * kPwEntries;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const uint32_t x = c + 1u + 64u * h;
+            if (x <= emax) {
+                const uint4 cb = gblock(x);
+                // the block as a big-endian bit stream: bit i of the stream is x^i
+                const uint32_t s0 = bswap(cb.x), s1 = bswap(cb.y), s2 = bswap(cb.z), s3 = bswap(cb.w);
+                const uint4 *t = pwk + (x - 1u) * kPwEntries;
+#pragma unroll
+                for (int k = 0; k < (int)kPwLaneWins; ++k) {
+                    const uint32_t w = e + 8u * k;
+                    if (w < kPwWin) {
+                        const uint32_t o = w * kPwBits, jw = o >> 5;
+                        const uint32_t hi = jw == 0 ? s0 : jw == 1 ? s1 : jw == 2 ? s2 : s3;
+                        const uint32_t lo = jw == 0 ? s1 : jw == 1 ? s2 : jw == 2 ? s3 : 0u;
+                        const uint64_t v = (uint64_t)hi << 32 | lo;
+                        const uint32_t u = (uint32_t)(v >> (64u - kPwBits - (o & 31u))) & ((1u << kPwBits) - 1u);
+                        fr[kPwLaneWins * h + k] = t[(w << kPwBits) + u];
+                    }
+                }
+            }
         }
     };
     auto flat_consume = [&]() {
-        fa0 = xor3(f0.x, f1.x, f2.x) ^ f3.x;
-        fa1 = xor3(f0.y, f1.y, f2.y) ^ f3.y;
-        fa2 = xor3(f0.z, f1.z, f2.z) ^ f3.z;
-        fa3 = xor3(f0.w, f1.w, f2.w) ^ f3.w;
+        uint4 a = fr[0];
+#pragma unroll
+        for (int k = 1; k < 2 * (int)kPwLaneWins; ++k) a = uint4{a.x ^ fr[k].x, a.y ^ fr[k].y, a.z ^ fr[k].z, a.w ^ fr[k].w};
+        fa0 = a.x;
+        fa1 = a.y;
+        fa2 = a.z;
+        fa3 = a.w;
         fed = true;
     };
     auto row_xor = [](uint32_t v) {  // XOR over the 16 lanes of each row, in every lane of it
@@ -2109,9 +2149,10 @@ hipError_t launch_key_setup(const uint8_t *d_keys, uint32_t first, uint32_t coun
     return hipGetLastError();
 }
 
-// The latency engine's flat GHASH tables (one_packet): the 8-bit comb tables of H^1 .. H^kPwPowers of
-// each key slot below pw_keys -- entry (byte position B, byte value u) = sum over the set bits of u
-// (MSB = x^(8B)) of x^(8B + j) * H^k, 16 x 256 x 16 B = 64 KiB per power, 8 MiB per key.  One 256-thread
+// The latency engine's flat GHASH tables (one_packet): the kPwBits-bit comb tables of H^1 .. H^kPwPowers
+// of each key slot below pw_keys -- entry (window W, value u) = sum over the set bits k of u (MSB first)
+// of x^(kPwBits W + k) * H^p, kPwEntries x 16 B per power (6 bits: 22 x 64 x 16 B = 22 KiB, 2.75 MiB
+// per key, which the L2 holds; 8 bits had 64 KiB per power and 8 MiB per key).  One 256-thread
 // workgroup per key, after key_setup_kernel (H is read back from the slot's 4-bit comb table of H:
 // entry (p 0, v 8) = x^0 * H).  Powers by doubling levels, H^(t+1) = H^(t+1-2^l) * H^(2^l); then 16 powers
 // at a time, x^i * H^k for i < 128 in LDS and the comb entries from them.
@@ -2144,11 +2185,12 @@ __global__ void __launch_bounds__(256) pw_setup_kernel(uint32_t first, const uin
         }
         __syncthreads();
         for (uint32_t e = tid; e < 16u * kPwEntries; e += 256) {
-            const uint32_t j = e / kPwEntries, q = e % kPwEntries, pos = q >> 8, u = q & 255u;
+            const uint32_t j = e / kPwEntries, q = e % kPwEntries, win = q >> kPwBits, u = q & ((1u << kPwBits) - 1u);
             uint4 acc = {0, 0, 0, 0};
-            for (int k = 0; k < 8; ++k) {
-                if ((u >> (7 - k)) & 1u) {
-                    const uint4 t = xs[j][8 * pos + k];
+            for (uint32_t k = 0; k < kPwBits; ++k) {
+                const uint32_t i = win * kPwBits + k;  // the window's bit k (its MSB first) is x^i
+                if (i < 128u && ((u >> (kPwBits - 1u - k)) & 1u)) {
+                    const uint4 t = xs[j][i];
                     acc.x ^= t.x;
                     acc.y ^= t.y;
                     acc.z ^= t.z;

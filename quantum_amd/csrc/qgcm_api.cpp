@@ -48,7 +48,7 @@ struct qgcm_ctx {
     uint32_t *d_rk = nullptr;
     uint4 *d_gh = nullptr;
     uint4 *d_pw = nullptr;   // per-packet flat GHASH: comb tables of H^1..H^kPwPowers, key slots < pw_keys
-    uint32_t pw_keys = 0;    // (8 MiB per key; QGCM_FLAT_GHASH_KEYS, default min(max_keys, 256), 0 = off)
+    uint32_t pw_keys = 0;    // (2.75 MiB per key; QGCM_FLAT_GHASH_KEYS, default min(max_keys, 256), 0 = off)
     uint32_t *d_te = nullptr;
     uint8_t *d_sbox = nullptr;
     uint8_t *d_key_valid = nullptr;  // device view of key_set (descriptor batches check it per packet)

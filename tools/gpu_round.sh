@@ -95,12 +95,12 @@ for s in $STEPS; do
           done
         done
       done ;;
-    poll)  # resident kernel A/B against the build in ablib/poll_old (LD_LIBRARY_PATH comes before RUNPATH)
+    poll)  # resident kernel A/B against the build in ${ABLIB:-ablib/poll_old} (LD_LIBRARY_PATH comes before RUNPATH)
       for rep in 1 2; do
         for lib in old new; do
           for t in 1 16; do
             if [ $lib = old ]; then
-              LD_LIBRARY_PATH=$PWD/ablib/poll_old timeout -k 10 60 tools/bin/per_packet_bench $t 1350 2 0 resident >> $OUT/poll_$lib.jsonl 2>> $OUT/poll.err
+              LD_LIBRARY_PATH=$PWD/${ABLIB:-ablib/poll_old} timeout -k 10 60 tools/bin/per_packet_bench $t 1350 2 0 resident >> $OUT/poll_$lib.jsonl 2>> $OUT/poll.err
             else
               timeout -k 10 60 tools/bin/per_packet_bench $t 1350 2 0 resident >> $OUT/poll_$lib.jsonl 2>> $OUT/poll.err
             fi
