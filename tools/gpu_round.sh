@@ -28,6 +28,9 @@ for s in $STEPS; do
     ab)
       timeout -k 10 300 python3 tools/ab_libs.py ablib/libqgcm_r2.so quantum_amd/libqgcm.so --rounds 15 > $OUT/ab.txt 2>&1
       check ab $? ;;
+    ab8)  # config 2 in-process A/B against the build in ${ABLIB:-ablib/flat8}
+      timeout -k 10 300 python3 tools/ab_libs.py ${ABLIB:-ablib/flat8}/libqgcm.so quantum_amd/libqgcm.so --rounds 9 > $OUT/ab8.txt 2>&1
+      check ab8 $? ;;
     prof)
       bash tools/profile.sh $TAG > $OUT/profile.log 2>&1
       check prof $?
