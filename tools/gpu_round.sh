@@ -28,6 +28,13 @@ for s in $STEPS; do
     ab)
       timeout -k 10 300 python3 tools/ab_libs.py ablib/libqgcm_r2.so quantum_amd/libqgcm.so --rounds 15 > $OUT/ab.txt 2>&1
       check ab $? ;;
+    spin)  # resident callers allowed to spin at once (QGCM_RESIDENT_SPINNERS; default half the CPU share)
+      for rep in 1 2; do
+        for sp in 8 12 16; do
+          QGCM_RESIDENT_SPINNERS=$sp timeout -k 10 60 tools/bin/per_packet_bench 16 1350 2 0 resident >> $OUT/spin_$sp.jsonl 2>> $OUT/spin.err
+          check spin_$sp $?
+        done
+      done ;;
     ab8)  # config 2 in-process A/B against the build in ${ABLIB:-ablib/flat8}
       timeout -k 10 300 python3 tools/ab_libs.py ${ABLIB:-ablib/flat8}/libqgcm.so quantum_amd/libqgcm.so --rounds 9 > $OUT/ab8.txt 2>&1
       check ab8 $? ;;
