@@ -131,6 +131,9 @@ long qgcm_open_one(qgcm_ctx *ctx, uint32_t key_idx, uint8_t *data, long len, con
  * a request or QGCM_RESIDENT_LIFE_US (8000) of life, after serving what is pending (the next call starts
  * it again): work queued behind it on a shared hardware queue, or a device-wide synchronize, waits that
  * long at most.  qgcm_set_key(s) and qgcm_destroy end it too (it caches key tables).
+ * Per-packet calls of up to 2016 B hash with per-key tables of H^1..H^128 (6-bit combs, 2.75 MiB of
+ * device memory per key slot, built by qgcm_set_key(s)) for the first QGCM_FLAT_GHASH_KEYS slots
+ * (default min(max_keys, 256); 0 = off: every packet takes the slower chained GHASH).
  * A seal without a caller's nonce draws the nonce of its slot's NEXT seal too and hands it to the worker,
  * which computes that nonce's counter blocks while idle (QGCM_RESIDENT_AHEAD=0: off); the next seal
  * on the slot uses that nonce (drawn from getrandom like any other, used once) and skips the counter
