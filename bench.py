@@ -62,7 +62,7 @@ def parse() -> argparse.Namespace:
     p.add_argument("--stride", type=int, default=0, help="slot stride (0 = smallest 64-B multiple)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extra", action="store_true", help="skip configs 3 / 5 and the host-memory rate (N=1)")
-    p.add_argument("--no-verify", action="store_true", help="skip config 3's arena digests")
+    p.add_argument("--no-verify", action="store_true", help="skip the golden arena digests of configs 3 and 5")
     p.add_argument("--cpu-threads", type=int, default=0, help="0 = the CPU share this job was given")
     p.add_argument("--dist-backend", default="nccl", help="nccl (RCCL, default) or gloo (rehearsal)")
     p.add_argument("--one-device", action="store_true",
@@ -299,27 +299,45 @@ def extra_e2e(key: bytes, reps: int = 3) -> dict:
             "matches_device_path": same, "status_ok": rc == 0, "reps": reps}
 
 
-def extra_config5(key: bytes, threads: int, reps: int = 3) -> dict:
+def _sha256_host(a: np.ndarray) -> str:
+    import hashlib
+
+    h = hashlib.sha256()
+    flat = a.reshape(-1)
+    for i in range(0, flat.size, 1 << 28):
+        h.update(memoryview(flat[i:i + (1 << 28)]))
+    return h.hexdigest()
+
+
+def _config5_golden() -> dict:
+    return json.load(open(os.path.join(ROOT, "tests", "golden", "config5_digest.json")))
+
+
+def extra_config5(key: bytes, threads: int, reps: int = 3, verify: bool = True) -> dict:
     """BASELINE config 5: snappy compress -> seal, then open -> uncompress, 2^20 x 1350 B packets in
-    pinned host memory (each packet's first half seeded random bytes, second half a repeated HTTP
-    request line), host codec workers overlapped with PCIe copies and the device
-    (qgcm_compress_seal_host / qgcm_open_uncompress_host; copies included)."""
+    pinned host memory (quantum_amd/workloads.py config5_*: each packet's first half seeded random bytes,
+    second half a repeated HTTP request line), host codec workers overlapped with PCIe copies and the
+    device (qgcm_compress_seal_host / qgcm_open_uncompress_host; copies included).  verify: after the timed
+    reps of each codec mode, one more compress+seal whose whole arena and lengths must hash to
+    tests/golden/config5_digest.json (libsnappy + OpenSSL), then open+uncompress back to the plaintext."""
     from quantum_amd import _lib
+    from quantum_amd import workloads as W
     import ctypes as C
 
-    N, L, stride = 1 << 20, 1350, 1472  # stride = common.MaxPacketLength (the Payload.Raw buffer)
+    N, L, stride = W.C5_N, W.C5_LEN, W.C5_STRIDE  # stride = common.MaxPacketLength (the Payload.Raw buffer)
+    gold = _config5_golden() if verify else None
     ctx = Context(device=0, max_keys=4)
     ctx.set_key(0, key)
     Lb = _lib.lib()
     a_ptr, n_ptr = Lb.qgcm_host_alloc(N * stride), Lb.qgcm_host_alloc(12 * N)
     host = np.frombuffer((C.c_uint8 * (N * stride)).from_address(a_ptr), np.uint8).reshape(N, stride)
     nons = np.frombuffer((C.c_uint8 * (12 * N)).from_address(n_ptr), np.uint8)
-    host[:] = config5_packets(N, L, stride)
-    nons[:] = np.random.default_rng(0x5EED0015).integers(0, 256, 12 * N, dtype=np.uint8)
+    host[:] = W.config5_packets(N, L, stride)
+    nons[:] = W.config5_nonces(N)
     plain = host[:, :4 + L].copy()
     lens = np.full(N, L, np.uint32)
 
-    def run(mode: int) -> tuple[float, float, int, int, tuple[int, int]]:
+    def run(mode: int) -> tuple[float, float, int, int, tuple[int, int], bool | None]:
         batch.chain_codec(ctx, mode)
         ts, to, bad, sealed = [], [], 0, 0
         c0 = ctx.launch_counts()
@@ -335,15 +353,24 @@ def extra_config5(key: bytes, threads: int, reps: int = 3) -> dict:
             to.append(t2 - t1)
         c1 = ctx.launch_counts()
         dev = (c1["snappy_enc"] - c0["snappy_enc"]) // reps, (c1["snappy_dec"] - c0["snappy_dec"]) // reps
-        return float(np.median(ts)), float(np.median(to)), bad, sealed, dev
+        digest_ok = None
+        if gold is not None:  # untimed: the sealed state against the golden digest, then back
+            lens[:] = L
+            bad += batch.compress_seal_host(ctx, a_ptr, stride, N, lens, 0, n_ptr, threads=threads)
+            digest_ok = (_sha256_host(host) == gold["sha256_sealed"] and
+                         _sha256_host(lens.astype("<u4")) == gold["sha256_sealed_lens"])
+            bad += batch.open_uncompress_host(ctx, a_ptr, stride, N, lens, 0, threads=threads)
+        return float(np.median(ts)), float(np.median(to)), bad, sealed, dev, digest_ok
 
     modes = {}
     for mode, name in ((0, "host"), (2, "device"), (1, "split")):  # the default (split) last: the value
-        s, o, bad, sealed, dev = run(mode)
+        s, o, bad, sealed, dev, digest_ok = run(mode)
         ok = bad == 0 and bool(np.array_equal(host[:, :4 + L], plain)) and bool((lens == L).all())
         modes[name] = {"value": round(2 * N * L / (s + o) / 2**30, 2), "compress_seal_s": round(s, 4),
-                       "open_uncompress_s": round(o, 4), "device_chunks_seal_open": dev, "restored": ok}
+                       "open_uncompress_s": round(o, 4), "device_chunks_seal_open": dev, "restored": ok,
+                       "sealed_digest_ok": digest_ok}
     restored = all(m["restored"] for m in modes.values())
+    digests = None if gold is None else all(m["sealed_digest_ok"] for m in modes.values())
     del host, nons, plain
     Lb.qgcm_host_free(a_ptr)
     Lb.qgcm_host_free(n_ptr)
@@ -355,38 +382,30 @@ def extra_config5(key: bytes, threads: int, reps: int = 3) -> dict:
             "codec": "snappy block codec (golang/snappy's algorithm, libsnappy-exact bytes): host C++ workers "
                      "with the gfx950 device codec taking the chunks they cannot keep up with (qgcm_chain_codec 1)",
             "chunks": (N * stride + (32 << 20) - 1) // (32 << 20), "by_codec_mode": modes,
+            "sealed_digest_ok": digests, "digest_source": "tests/golden/config5_digest.json",
             "status_ok": restored, "restored": restored, "reps": reps}
 
 
-def config5_packets(N: int, L: int, stride: int) -> np.ndarray:
-    """(N, stride) uint8 host slots of config 5: AAD, each packet's first half seeded random bytes, its
-    second half a repeated HTTP request line (the rest of the slot zero)."""
-    host = np.zeros((N, stride), np.uint8)
-    rng = np.random.default_rng(0x5EED0005)
-    host[:, :4] = np.frombuffer(AAD, np.uint8)
-    half = L // 2
-    host[:, 4:4 + half] = rng.integers(0, 256, (N, half), dtype=np.uint8)
-    line = np.frombuffer(b"GET /quantum/v1/peers HTTP/1.1\r\nHost: 10.99.0.1\r\n", np.uint8)
-    host[:, 4 + half:4 + L] = np.tile(line, (L - half) // len(line) + 1)[:L - half]
-    return host
-
-
-def extra_config5_resident(key: bytes, reps: int = 5, N: int = 1 << 20) -> dict:
+def extra_config5_resident(key: bytes, reps: int = 5, verify: bool = True) -> dict:
     """Config 5's chain with the codec on the GPU and the packets resident in HBM (no PCIe): device
     snappy compress (writing the seal descriptors) -> seal, then open -> device uncompress, on config
-    5's packets; HIP events per stage, the arena checked against the plaintext after each rep."""
-    L, stride = 1350, 1472
+    5's packets and nonces; HIP events per stage, the arena checked against the plaintext after each rep.
+    verify: the first rep's sealed arena and lengths against tests/golden/config5_digest.json."""
+    from quantum_amd import workloads as W
+
+    N, L, stride = W.C5_N, W.C5_LEN, W.C5_STRIDE
+    gold = _config5_golden() if verify else None
     ctx = Context(device=0, max_keys=4)
     ctx.set_key(0, key)
-    plain = torch.from_numpy(config5_packets(N, L, stride).reshape(-1)).cuda()
+    plain = torch.from_numpy(W.config5_packets(N, L, stride).reshape(-1)).cuda()
     arena = plain.clone()
-    nonces = torch.randint(0, 256, (12 * N,), dtype=torch.uint8, device="cuda")
+    nonces = torch.from_numpy(W.config5_nonces(N)).cuda()
     lens = torch.empty(N, dtype=torch.int32, device="cuda")
     descs = torch.empty(16 * N, dtype=torch.uint8, device="cuda")
     status = torch.empty(N, dtype=torch.uint8, device="cuda")
     limit = stride - 4 - 28
     times = {k: [] for k in ("compress", "seal", "open", "uncompress")}
-    ok, sealed = True, 0
+    ok, sealed, digest_ok = True, 0, None
     for r in range(reps + 1):
         arena.copy_(plain)
         lens.fill_(L)
@@ -400,6 +419,9 @@ def extra_config5_resident(key: bytes, reps: int = 5, N: int = 1 << 20) -> dict:
         ok &= bool((status == 1).all())
         clen = lens.clone()
         sealed = int(clen.sum()) + 28 * N
+        if r == 0 and gold is not None:  # untimed warm-up rep
+            digest_ok = (_sha256_device(arena) == gold["sha256_sealed"] and
+                         _sha256_host(clen.cpu().numpy().astype("<u4") + np.uint32(28)) == gold["sha256_sealed_lens"])
         d = descs.view(torch.int32).view(N, 4)
         d[:, 2] += 28  # the receiver's descriptors: sealed lengths (outside the timed stages)
         ev[3].record()
@@ -415,13 +437,59 @@ def extra_config5_resident(key: bytes, reps: int = 5, N: int = 1 << 20) -> dict:
                 times[k].append(ev[a].elapsed_time(ev[b]))
     med = {k: float(np.median(v)) for k, v in times.items()}
     ctx.close()
+    del arena, plain
+    torch.cuda.empty_cache()
     total = sum(med.values())
     return {"workload": f"config5 on device-resident slots: device snappy -> AES-256-GCM and back, {N} x {L} B",
             "value": round(2 * N * L / (total * 1e-3) / 2**30, 2), "unit": "GiB/s of uncompressed payload (kernels only)",
             **{f"{k}_ms": round(v, 3) for k, v in med.items()},
             "compress_GBps": round(N * L / (med["compress"] * 1e-3) / 1e9, 1),
             "uncompress_GBps": round(N * L / (med["uncompress"] * 1e-3) / 1e9, 1),
-            "sealed_over_plain": round(sealed / (N * L), 4), "status_ok_and_restored": ok, "reps": reps}
+            "sealed_over_plain": round(sealed / (N * L), 4), "status_ok_and_restored": ok,
+            "sealed_digest_ok": digest_ok, "reps": reps}
+
+
+def extra_config4_one_gpu(key: bytes, steps: int = 3, warmup: int = 1, settle_ms: float = 300.0) -> dict:
+    """BASELINE config 4's whole batch on ONE GPU: 64 x 2^20 x 1350 B (94.5 GB of 1408-B slots, one
+    MI355X holds it), seal then unseal, so the N-GPU lines (config 4 sharded over N ranks) have a
+    same-workload N = 1 anchor: per-GPU efficiency at N = value_N / (N x this value).  One step is the
+    same pair of uniform calls the headline makes (2^19-packet launches), timed between synchronizes."""
+    N, L = CONFIG4_PACKETS, 1350
+    stride = batch.slot_stride(L, align=64)
+    ctx = Context(device=0, max_keys=4)
+    ctx.set_key(0, key)
+    alloc = torch.empty(N * stride + 64, dtype=torch.uint8, device="cuda")
+    arena = alloc[60:]
+    nonces = torch.empty(12 * N, dtype=torch.uint8, device="cuda")
+    status = torch.zeros(N, dtype=torch.uint8, device="cuda")
+    batch.fill_uniform(arena, stride, N, L, int.from_bytes(AAD, "little"), 0x5EED0001, nonces, 0x5EED0002)
+    stream = torch.cuda.current_stream()
+
+    def step():
+        batch.seal_uniform(ctx, arena, stride, N, L, 0, nonces, status=None, stream=stream)
+        batch.open_uniform(ctx, arena, stride, N, L + 28, 0, status=status, stream=stream)
+
+    t0 = time.perf_counter()
+    while (time.perf_counter() - t0) * 1e3 < settle_ms:
+        step()
+        torch.cuda.synchronize()
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    ok = int(status.sum().item()) == N
+    del alloc, arena, nonces, status
+    ctx.close()
+    torch.cuda.empty_cache()
+    return {"workload": f"config4 on one GPU: {N} x {L} B packets (the whole 8-GPU batch), seal then unseal, 1 key",
+            "value": round(2 * N * L / (el / steps) / 2**30, 2), "unit": "GiB/s",
+            "ms_per_step": round(el * 1e3 / steps, 2), "steps": steps, "packets": N, "slot_stride": stride,
+            "arena_GB": round(N * stride / 1e9, 1), "status_ok": ok,
+            "use": "N = 1 anchor of the config-4 scaling curve (bench.py --gpus N runs config 4 sharded)"}
 
 
 def free_port() -> int:
@@ -500,7 +568,7 @@ def main() -> None:
     local = 0 if args.one_device else local
     torch.cuda.set_device(local)  # before the process group, so RCCL binds each rank to its GPU
     dev = torch.device("cuda", local)
-    if world > 1:
+    if world > 1 or "WORLD_SIZE" in os.environ:  # under a launcher: a process group even for one rank
         import torch.distributed as dist
 
         if args.dist_backend == "nccl":
@@ -568,10 +636,13 @@ def main() -> None:
     elapsed = time.perf_counter() - t0
     ok = int(status.sum().item()) == N  # the last timed open authenticated every packet
     # max over ranks, AND of the per-rank status (the only cross-rank traffic; no data collective)
-    elapsed, ok = shard.reduce_step_time(elapsed, ok, dist, dev if args.dist_backend == "nccl" else None)
-
     seal_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
     open_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
+    own_elapsed = elapsed
+    coll_dev = dev if args.dist_backend == "nccl" else None
+    elapsed, ok = shard.reduce_step_time(elapsed, ok, dist, coll_dev)
+    # every rank's own figures (after the timed region): per-GPU rates of the multi-GPU line
+    per_rank = shard.gather_rank_stats([own_elapsed, seal_ms, open_ms, N], dist, coll_dev)
     ms_step = elapsed * 1e3 / args.steps
     total_packets = CONFIG4_PACKETS if workload == "config4" and not args.packets else world * N
     total_bytes = 2 * total_packets * L  # each payload byte counted once sealed and once unsealed
@@ -626,8 +697,17 @@ def main() -> None:
                          "binding_unit": "LDS (T-table AES + comb GHASH lookups, DESIGN.md 4.1)",
                          "lds_array_busy": lds_busy},
             "kernels_ms": {"seal": round(seal_ms, 4), "open": round(open_ms, 4)},
+            "per_gpu": [{"rank": r, "packets": int(p[3]), "ms_per_step": round(p[0] * 1e3 / args.steps, 4),
+                         "GiB_s": round(2 * p[3] * L / (p[0] / args.steps) / 2**30, 2),
+                         "seal_ms": round(p[1], 4), "open_ms": round(p[2], 4)} for r, p in enumerate(per_rank)],
+            "dist_backend": args.dist_backend if dist is not None else None,
             "status_ok": ok,
         }
+        rates = [g["GiB_s"] for g in line["per_gpu"]]
+        line["per_gpu_GiB_s"] = {"min": min(rates), "max": max(rates), "mean": round(sum(rates) / len(rates), 2),
+                                 "aggregate_of_own_times": round(sum(rates), 2),
+                                 "note": "each rank's packets over its own step time; `value` uses the max over ranks"}
+        print(f"[bench] headline {line['value']} GiB/s", file=sys.stderr, flush=True)
         host = host_cpus()
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(key, L, args.cpu_threads or host["share"], host)
@@ -637,9 +717,10 @@ def main() -> None:
             torch.cuda.empty_cache()
             extra = {}
             for name, fn in (("config3", lambda: extra_config3(verify=not args.no_verify)),
+                             ("config4_one_gpu", lambda: extra_config4_one_gpu(key)),
                              ("e2e_pinned_host", lambda: extra_e2e(key)),
-                             ("config5", lambda: extra_config5(key, args.cpu_threads or host["share"])),
-                             ("config5_resident", lambda: extra_config5_resident(key)),
+                             ("config5", lambda: extra_config5(key, args.cpu_threads or host["share"], verify=not args.no_verify)),
+                             ("config5_resident", lambda: extra_config5_resident(key, verify=not args.no_verify)),
                              ("per_packet", extra_per_packet)):
                 t0 = time.perf_counter()
                 try:
@@ -647,6 +728,8 @@ def main() -> None:
                 except Exception as e:  # reported, and the run fails below: a broken config is not hidden
                     extra[name] = {"error": f"{type(e).__name__}: {e}"}
                 extra[name]["wall_s"] = round(time.perf_counter() - t0, 2)
+                print(f"[bench] extra {name}: {extra[name].get('value', extra[name].get('error', ''))} "
+                      f"({extra[name]['wall_s']} s)", file=sys.stderr, flush=True)  # progress for long runs
             line["extra_configs"] = extra
         print(json.dumps(line), flush=True)
         if any("error" in v for v in line.get("extra_configs", {}).values()):

@@ -980,7 +980,7 @@ static int run_host_chain(qgcm_ctx *ctx, bool seal, uint8_t *h_arena, uint64_t s
             } else if (ctx->h_stat[i] == 1) {  // compression.go:35-43, on authentic packets only
                 const uint32_t sl = lens[i] - QGCM_OVERHEAD;
                 const long u = qgcm_snappy_uncompress(pkt, sl, tmp.data(), stride - 4);
-                if (u < 0) {
+                if (u <= 0) {  // an empty result is Go's nil slice: compression.go:37-39 drops it
                     codec[i] = 0;
                     lens[i] = sl;
                 } else {

@@ -176,7 +176,9 @@ Result Compression::Apply(Direction direction, common::Payload *payload, common:
     if (direction == Incoming) {  // :35-43 decompress(); a decode error drops the packet
         const long n = qgcm_snappy_uncompressed_length(pkt.data, pkt.len);
         // a length that cannot fit Raw[PacketStart:] would make Go's re-slice panic: drop instead
-        if (n < 0 || (size_t)n > payload->Raw.cap - common::PacketStart) return {payload, mapping, false};
+        // n == 0: golang/snappy's Decode(nil, src) returns a nil slice for an empty result, and :37-39
+        // drops a nil packet
+        if (n <= 0 || (size_t)n > payload->Raw.cap - common::PacketStart) return {payload, mapping, false};
         out.resize((size_t)n + 1);
         length = qgcm_snappy_uncompress(pkt.data, pkt.len, out.data(), (size_t)n);
         if (length < 0) return {payload, mapping, false};

@@ -285,7 +285,8 @@ int qgcm_snappy_compress_slots(uint8_t *arena, uint64_t stride, uint32_t n, uint
 }
 
 // Inverse of qgcm_snappy_compress_slots (plugin/compression.go:35-38,41-47 Incoming): a packet that
-// does not decode, or would not fit its slot, fails (status 0, slot untouched).
+// does not decode, would not fit its slot, or decodes to nothing (golang/snappy returns a nil slice for
+// an empty result, which compression.go:37-39 treats as a failure) fails (status 0, slot untouched).
 int qgcm_snappy_uncompress_slots(uint8_t *arena, uint64_t stride, uint32_t n, uint32_t *lens, uint8_t *status,
                              int threads) {
     if ((n && (!arena || !lens)) || stride < 4) return -1;
@@ -300,7 +301,7 @@ int qgcm_snappy_uncompress_slots(uint8_t *arena, uint64_t stride, uint32_t n, ui
                 uint8_t *pkt = arena + (uint64_t)i * stride + 4;
                 const size_t L = std::min<uint64_t>(lens[i], stride - 4);
                 const long u = qgcm_snappy_uncompress(pkt, L, tmp.data(), stride - 4);
-                const bool ok = u >= 0;
+                const bool ok = u > 0;  // an empty result is a nil slice in Go: compression.go:37-39 drops it
                 if (ok) {
                     memcpy(pkt, tmp.data(), (size_t)u);
                     lens[i] = (uint32_t)u;

@@ -339,6 +339,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) s
         if (take) {
             wave_lds_sync();
             u = decode(w, len, a.limit);
+            // an empty result fails: golang/snappy's Decode(nil, src) returns a nil slice for it and
+            // compression.go:37-39 drops a nil packet
+            if (u == 0) u = -1;
             wave_lds_sync();
             if (u >= 0) write_out(slot, w.out, (uint32_t)u, lane);
         }

@@ -105,7 +105,8 @@ class Compression(Plugin):
         packet = bytes(payload.Packet)
         if direction == Incoming:  # :36-43 decompress; a decode error drops the packet
             n = _lib.lib().qgcm_snappy_uncompressed_length(packet, len(packet)) if packet else -1
-            out = _snappy("qgcm_snappy_uncompress", packet, n) if n >= 0 else None
+            # an empty result is golang/snappy's nil slice, which :37-39 treats as a failure
+            out = _snappy("qgcm_snappy_uncompress", packet, n) if n > 0 else None
         elif direction == Outgoing:  # :44-51 compress
             out = _snappy("qgcm_snappy_compress", packet, _lib.lib().qgcm_snappy_max_compressed_length(len(packet)))
         else:

@@ -51,6 +51,21 @@ def reduce_step_time(elapsed_s: float, ok: bool, dist=None, device=None) -> tupl
     return float(t[0].item()), t[1].item() == 0.0
 
 
+def gather_rank_stats(values, dist=None, device=None) -> list[list[float]]:
+    """Every rank's scalar measurements (its own step time, kernel times, packets), in rank order --
+    the per-GPU figures of a multi-GPU line.  One small all_gather after the
+    timed region; without a process group, [values]."""
+    vals = [float(v) for v in values]
+    if dist is None or not dist.is_initialized():
+        return [vals]
+    import torch
+
+    t = torch.tensor(vals, dtype=torch.float64, device=device)
+    out = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [[float(x) for x in o.cpu().tolist()] for o in out]
+
+
 class Group:
     """Several GPUs behind one process (qgcm_group_*, include/qgcm.h): quantum is one process
     (main.go:29-114) whose workers all call one Encryption plugin, so its drop-in drives every GPU of a

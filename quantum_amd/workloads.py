@@ -129,3 +129,31 @@ def device_arena(torch, size: int, offs: np.ndarray, kidx: np.ndarray, device="c
 def tail_index(offs: np.ndarray, lens: np.ndarray) -> np.ndarray:
     """(n, 28) byte indices of every slot's tag || nonce."""
     return (offs.astype(np.int64) + 4 + lens.astype(np.int64))[:, None] + np.arange(28, dtype=np.int64)
+
+
+# Config 5 (compression + encryption chain, plugin/compression.go then plugin/encryption.go in the
+# order main.go:50-51 sorts them): 2^20 Payload.Raw slots of common.MaxPacketLength = 1472 B, each
+# [AAD 10.99.0.1][1350-B packet][zeros]; a packet's first half is seeded random bytes, its second half a
+# repeated HTTP request line (compresses to ~0.64 with golang/snappy's block algorithm).  Nonces: 12 seeded
+# bytes per packet.  tests/golden/config5_digest.json pins the sealed arena and lengths
+# (tests/golden/make_config5_golden.py: libsnappy 1.1.8 + OpenSSL, cross-checked with the restatements).
+C5_N, C5_LEN, C5_STRIDE = 1 << 20, 1350, 1472
+C5_SEED_PAYLOAD, C5_SEED_NONCE = 0x5EED0005, 0x5EED0015
+C5_LINE = b"GET /quantum/v1/peers HTTP/1.1\r\nHost: 10.99.0.1\r\n"
+
+
+def config5_packets(n: int = C5_N, L: int = C5_LEN, stride: int = C5_STRIDE) -> np.ndarray:
+    """(n, stride) uint8 host slots of config 5 (the rest of each slot zero)."""
+    host = np.zeros((n, stride), np.uint8)
+    rng = np.random.default_rng(C5_SEED_PAYLOAD)
+    host[:, :4] = np.frombuffer(AAD_WORD.to_bytes(4, "little"), np.uint8)
+    half = L // 2
+    host[:, 4:4 + half] = rng.integers(0, 256, (n, half), dtype=np.uint8)
+    line = np.frombuffer(C5_LINE, np.uint8)
+    host[:, 4 + half:4 + L] = np.tile(line, (L - half) // len(line) + 1)[:L - half]
+    return host
+
+
+def config5_nonces(n: int = C5_N) -> np.ndarray:
+    """n * 12 seeded nonce bytes (production seals draw them from getrandom, qgcm_random_nonces)."""
+    return np.random.default_rng(C5_SEED_NONCE).integers(0, 256, 12 * n, dtype=np.uint8)

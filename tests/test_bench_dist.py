@@ -35,6 +35,10 @@ def test_bench_two_ranks_one_device():
     assert line["scaling"] == "weak" and line["config"]["packets_per_gpu"] == 65536
     assert "cpu_baseline" not in line  # rank 0 at N=1 only
     assert line["value"] > 0
+    per = line["per_gpu"]  # each rank's own rate, gathered after the timed region
+    assert [g["rank"] for g in per] == [0, 1] and all(g["packets"] == 65536 and g["GiB_s"] > 0 for g in per)
+    assert line["per_gpu_GiB_s"]["min"] <= line["per_gpu_GiB_s"]["max"]
+    assert line["dist_backend"] == "gloo"
 
 
 def test_bench_config4_two_ranks_one_device():
@@ -57,6 +61,29 @@ def test_bench_config4_two_ranks_one_device():
     assert line["status_ok"] is True and line["scaling"] == "strong"
     assert line["config"]["packets_total"] == 64 << 20 and line["config"]["packets_per_gpu"] == 32 << 20
     assert line["config"]["workload"].startswith("config4")
+    assert [g["packets"] for g in line["per_gpu"]] == [32 << 20, 32 << 20]
+
+
+def test_bench_rccl_process_group_one_rank():
+    """The RCCL branch of bench.py (init_process_group("nccl", device_id=...), the device-tensor
+    all_reduce of the step time and the all_gather of the per-rank figures) on real hardware: one rank
+    under torch.distributed.run, as the driver launches each rank of an N-GPU node."""
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr", "127.0.0.1", "--master-port", "29535", os.path.join(ROOT, "bench.py"),
+           "--gpus", "1", "--steps", "3", "--warmup", "1", "--packets", "65536", "--settle-ms", "0",
+           "--no-extra", "--no-cpu-baseline"]
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    line = json.loads(lines[0])
+    assert line["dist_backend"] == "nccl" and line["status_ok"] is True and line["n_gpus"] == 1
+    assert len(line["per_gpu"]) == 1 and line["per_gpu"][0]["packets"] == 65536
 
 
 def test_bench_gpus_flag_spawns_ranks():

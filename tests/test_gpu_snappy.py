@@ -177,8 +177,20 @@ def test_device_uncompress_corrupted_streams_vs_host(torch, ctx):
     out, ol, st = _run(torch, ctx, False, arena, stride, len(streams), lens, stride - 4, cap)
     for i, s in enumerate(streams):
         want = _host_uncompress(s, cap)
-        if want is None:
+        if want is None or len(want) == 0:  # an empty result is Go's nil slice: dropped (compression.go:37-39)
             assert st[i] == 0 and ol[i] == len(s) and np.array_equal(out[i], host[i]), i
         else:
             assert st[i] == 1 and ol[i] == len(want) and out[i, 4:4 + len(want)].tobytes() == want, i
     assert st[-len(goods):].all()
+
+
+def test_device_uncompress_empty_result_fails(torch, ctx):
+    """b"\\x00" decodes to 0 bytes: golang/snappy's Decode returns a nil slice and compression.go:37-39
+    drops the packet, so the device batch fails it (slot and length untouched), as the host slots do."""
+    streams = [b"\x00", _host_compress(b"abcabcabc"), b"\x00"]
+    stride = 64
+    host, arena, lens = _arena(torch, streams, stride)
+    out, ol, st = _run(torch, ctx, False, arena, stride, len(streams), lens, stride - 4, stride - 4)
+    assert list(st) == [0, 1, 0] and list(ol) == [1, 9, 1]
+    assert np.array_equal(out[0], host[0]) and np.array_equal(out[2], host[2])
+    assert out[1, 4:13].tobytes() == b"abcabcabc"

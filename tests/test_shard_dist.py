@@ -51,8 +51,9 @@ def _worker(rank, world, port, q):
         lo, hi = shard.packet_range(1000, world, rank)
         t, ok = shard.reduce_step_time(0.5 + rank, rank != 1 or True, dist)
         t2, ok2 = shard.reduce_step_time(1.0, rank == 0, dist)  # rank 1 reports failure
+        per = shard.gather_rank_stats([rank, 0.25 * (rank + 1), hi - lo], dist)
         dist.barrier()
-        q.put((rank, lo, hi, t, ok, t2, ok2))
+        q.put((rank, lo, hi, t, ok, t2, ok2, per))
     finally:
         dist.destroy_process_group()
 
@@ -70,7 +71,9 @@ def test_gloo_world2_reduction():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    (r0, lo0, hi0, t0, ok0, t20, ok20), (r1, lo1, hi1, t1, ok1, t21, ok21) = res
+    (r0, lo0, hi0, t0, ok0, t20, ok20, p0), (r1, lo1, hi1, t1, ok1, t21, ok21, p1) = res
     assert (lo0, hi0, lo1, hi1) == (0, 500, 500, 1000)
     assert t0 == t1 == 1.5 and ok0 and ok1  # max over ranks, all ok
     assert t20 == t21 == 1.0 and not ok20 and not ok21  # one failing rank fails the step
+    assert p0 == p1 == [[0.0, 0.25, 500.0], [1.0, 0.5, 500.0]]  # every rank's own figures, in rank order
+    assert shard.gather_rank_stats([1, 2]) == [[1.0, 2.0]]  # no process group: this rank only

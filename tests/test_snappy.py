@@ -205,3 +205,35 @@ def test_compression_plugin_roundtrip():
     m2 = common.Mapping(SupportedPlugins=["encryption"], AES=None)
     p = common.NewTunPayload(bytearray(64), 40)
     assert comp.Apply(plugin.Outgoing, p, m2)[2] and p.Length == 44
+
+
+def test_empty_result_is_dropped_by_the_plugin():
+    """golang/snappy's Decode(nil, src) returns a nil slice when the stream decodes to 0 bytes, and
+    plugin/compression.go:37-39 drops a nil packet: the empty stream b"\\x00" (what Encode gives for an
+    empty packet) decodes at codec level (0 bytes) but fails at plugin level -- Apply, the slot batch
+    and (GPU test) the device batch.  golang/snappy is not in the reference: parity unpinned, the
+    behaviour restated from its published decode.go."""
+    assert snappy_oracle.decode(b"\x00") == b""
+    assert snappy_oracle.encode(b"") == b"\x00" and _compress(b"") == b"\x00"
+    assert _uncompress(b"\x00", 16) == b""  # codec level: a valid, empty stream
+    comp, _ = plugin.New(plugin.CompressionPlugin)
+    mapping = common.Mapping(SupportedPlugins=["compression"], AES=None)
+    raw = bytearray(b"\x0a\x63\x00\x01\x00" + bytes(40))
+    p = common.NewSockPayload(raw, 5)
+    _, _, ok = comp.Apply(plugin.Incoming, p, mapping)
+    assert not ok and p.Length == 5
+    stride, n = 64, 3
+    arena = bytearray(stride * n)
+    streams = [b"\x00", _compress(b"abc"), b"\x00"]
+    lens = (C.c_uint32 * n)()
+    for i, s in enumerate(streams):
+        arena[i * stride + 4:i * stride + 4 + len(s)] = s
+        lens[i] = len(s)
+    before = bytes(arena)
+    buf = (C.c_uint8 * len(arena)).from_buffer(arena)
+    st = (C.c_uint8 * n)()
+    assert _lib.lib().qgcm_snappy_uncompress_slots(C.addressof(buf), stride, n, lens, st, 2) == 2
+    assert list(st) == [0, 1, 0] and list(lens) == [1, 3, 1]
+    assert arena[:stride] == before[:stride] and arena[2 * stride:] == before[2 * stride:]
+    assert bytes(arena[stride + 4:stride + 7]) == b"abc"
+    del buf

@@ -28,3 +28,31 @@ def test_nonces_and_lengths():
 def test_peer_keys_match_golden(kdf):
     """The 1024 peer keys through the product's host key math equal the golden table digest."""
     assert hashlib.sha256(W.peer_keys()).hexdigest() == kdf["peers"]["sha256_of_1024_keys"]
+
+
+def test_config5_workload_and_host_codec_match_golden():
+    """Config 5 at its stated size on the CPU: the workload definition hashes to the golden plaintext
+    digest, and libqgcm's host snappy encoder (compression.go Outgoing on every slot) produces exactly
+    libsnappy's compressed arena (tests/golden/config5_digest.json sha256_compressed)."""
+    import ctypes as C
+    import json
+    import os
+
+    from quantum_amd import _lib
+
+    gold = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "config5_digest.json")))
+    slots = W.config5_packets()
+    N, S = W.C5_N, W.C5_STRIDE
+
+    def sha(a):
+        h = hashlib.sha256()
+        flat = a.reshape(-1)
+        for i in range(0, flat.size, 1 << 28):
+            h.update(memoryview(flat[i:i + (1 << 28)]))
+        return h.hexdigest()
+
+    assert sha(slots) == gold["sha256_plain"]
+    lens = np.full(N, W.C5_LEN, np.uint32)
+    assert _lib.lib().qgcm_snappy_compress_slots(slots.ctypes.data, S, N, lens.ctypes.data, 8) == 0
+    assert int(lens.sum()) + 28 * N == gold["sealed_bytes"]
+    assert sha(slots) == gold["sha256_compressed"]

@@ -29,7 +29,7 @@ def main() -> None:
     a_ptr, n_ptr = Lb.qgcm_host_alloc(N * stride), Lb.qgcm_host_alloc(12 * N)
     host = np.frombuffer((C.c_uint8 * (N * stride)).from_address(a_ptr), np.uint8).reshape(N, stride)
     nons = np.frombuffer((C.c_uint8 * (12 * N)).from_address(n_ptr), np.uint8)
-    host[:] = bench.config5_packets(N, L, stride)
+    host[:] = __import__("quantum_amd.workloads", fromlist=["W"]).config5_packets(N, L, stride)
     nons[:] = np.random.default_rng(1).integers(0, 256, 12 * N, dtype=np.uint8)
     plain = host[:, :4 + L].copy()
     lens = np.full(N, L, np.uint32)
