@@ -254,6 +254,65 @@ def extra_config3(reps: int = 5, verify: bool = True) -> dict:
     return out
 
 
+def extra_config3_host(reps: int = 3, verify: bool = True) -> dict:
+    """Config 3's keyed batch from pinned HOST memory through the multi-GPU drop-in's entry point
+    (qgcm_group_seal_host / qgcm_group_open_host, one member on this GPU: the path quantum's multi-peer
+    traffic takes, worker/outgoing.go:55-80 with common/mapping.go:90-99 keys): PCIe included.  The
+    member's packets are one run of adjacent records, so they move by DMA in 64-MiB chunks (no gather).
+    verify: the opened arena after the timed reps and the sealed arena of one more seal against
+    tests/golden/config3_digest.json."""
+    from quantum_amd import _lib
+    from quantum_amd import workloads as W
+    import ctypes as C
+
+    keys = W.peer_keys()
+    lens, kidx = W.lengths(), W.key_indices()
+    offs, size = W.layout(lens)
+    grp = shard.Group([0], max_keys=W.NKEYS)
+    grp.set_keys(0, keys)
+    Lb = _lib.lib()
+    a_ptr, n_ptr = Lb.qgcm_host_alloc(size), Lb.qgcm_host_alloc(12 * W.N)
+    host = np.frombuffer((C.c_uint8 * size).from_address(a_ptr), np.uint8)
+    nons = np.frombuffer((C.c_uint8 * (12 * W.N)).from_address(n_ptr), np.uint8)
+    dev = W.device_arena(torch, size, offs, kidx)
+    host[:] = dev.cpu().numpy()
+    del dev
+    torch.cuda.empty_cache()
+    nons[:] = W.nonces()
+    d_seal = shard.host_descs(offs, lens, kidx)
+    d_open = shard.host_descs(offs, lens.astype(np.int64) + 28, kidx)
+    status = np.zeros(W.N, np.uint8)
+    bad = grp.seal_host(a_ptr, d_seal, W.N, n_ptr, 4, status.ctypes.data)  # warm-up pair (staging, streams)
+    bad += grp.open_host(a_ptr, d_open, W.N, 4, status.ctypes.data)
+    ts, to = [], []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        bad += grp.seal_host(a_ptr, d_seal, W.N, n_ptr, 4, status.ctypes.data)
+        t1 = time.perf_counter()
+        bad += grp.open_host(a_ptr, d_open, W.N, 4, status.ctypes.data)
+        t2 = time.perf_counter()
+        ts.append(t1 - t0)
+        to.append(t2 - t1)
+    path = grp.last_path(0)
+    out = {}
+    if verify:
+        gold = json.load(open(os.path.join(ROOT, "tests", "golden", "config3_digest.json")))
+        out["digest_opened_ok"] = _sha256_host(host) == gold["sha256_opened"]
+        bad += grp.seal_host(a_ptr, d_seal, W.N, n_ptr, 4, status.ctypes.data)
+        out["digest_sealed_ok"] = _sha256_host(host) == gold["sha256_sealed"]
+    s, o = float(np.median(ts)), float(np.median(to))
+    payload = int(lens.sum())
+    del host, nons
+    Lb.qgcm_host_free(a_ptr)
+    Lb.qgcm_host_free(n_ptr)
+    grp.close()
+    return {"workload": "config3 from pinned host memory: 2^20 x U{64..9000} B, 1024 peer keys, "
+                        "qgcm_group_seal_host / open_host (one member), H2D + seal/open + D2H",
+            "value": round(2 * payload / (s + o) / 2**30, 2), "unit": "GiB/s", "payload_bytes": payload,
+            "seal_s": round(s, 4), "open_s": round(o, 4), "member_path": path,
+            "pcie_GBps_each_way": round(size / ((s + o) / 2) / 1e9, 2), "status_ok": bad == 0, "reps": reps, **out}
+
+
 def extra_e2e(key: bytes, reps: int = 3) -> dict:
     """Config 2 from pinned HOST memory: qgcm_seal_host / qgcm_open_host (H2D + kernels + D2H,
     pipelined in 64 MiB chunks over three streams): the PCIe-inclusive rate (never `value`)."""
@@ -717,6 +776,7 @@ def main() -> None:
             torch.cuda.empty_cache()
             extra = {}
             for name, fn in (("config3", lambda: extra_config3(verify=not args.no_verify)),
+                             ("config3_host", lambda: extra_config3_host(verify=not args.no_verify)),
                              ("config4_one_gpu", lambda: extra_config4_one_gpu(key)),
                              ("e2e_pinned_host", lambda: extra_e2e(key)),
                              ("config5", lambda: extra_config5(key, args.cpu_threads or host["share"], verify=not args.no_verify)),

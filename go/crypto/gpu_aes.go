@@ -62,7 +62,6 @@ type GPUContext struct {
 	mu   sync.Mutex
 	next uint32
 	max  uint32
-	co   *C.qgcm_coalescer // optional: per-packet calls of all workers share device batches
 }
 
 // NewGPUContext opens device `device` with room for maxKeys peer keys.
@@ -76,28 +75,8 @@ func NewGPUContext(device int, maxKeys uint32) (*GPUContext, error) {
 	return &GPUContext{ctx: ctx, max: maxKeys}, nil
 }
 
-// EnableCoalescer routes every GPUAES of this context through one cross-thread coalescer
-// (qgcm_coalescer_*): the 2 x NumWorkers goroutines (main.go:72-75) keep the blocking per-packet
-// contract while their packets ride shared device batches of up to maxBatch packets, flushed after
-// maxWaitUs.  Call before the workers start.
-func (g *GPUContext) EnableCoalescer(maxBatch, maxWaitUs, maxPacket uint32) error {
-	buf := (*C.char)(C.malloc(C.QGCM_ERRLEN))
-	defer C.free(unsafe.Pointer(buf))
-	co := C.qgcm_coalescer_create(g.ctx, C.uint32_t(maxBatch), C.uint32_t(maxWaitUs), C.uint32_t(maxPacket), 4,
-		buf, C.QGCM_ERRLEN)
-	if co == nil {
-		return cError(buf)
-	}
-	g.co = co
-	return nil
-}
-
-// Close releases the coalescer and the device context (no call may be in flight).
+// Close releases the device context (no call may be in flight).
 func (g *GPUContext) Close() {
-	if g.co != nil {
-		C.qgcm_coalescer_destroy(g.co)
-		g.co = nil
-	}
 	if g.ctx != nil {
 		C.qgcm_destroy(g.ctx)
 		g.ctx = nil
@@ -157,14 +136,9 @@ func (a *GPUAES) Encrypt(data []byte, length int, additional []byte) (int, error
 	if len(additional) > 4 {
 		return -1, errAdditional
 	}
-	var n C.long
-	if a.g != nil && a.g.co != nil {
-		n = C.qgcm_coalescer_seal(a.g.co, C.uint32_t(a.idx), bytePtr(data), C.long(length), bytePtr(additional),
-			C.uint32_t(len(additional)))
-	} else {
-		n = C.qgcm_seal_one(a.ctx, C.uint32_t(a.idx), bytePtr(data), C.long(length), bytePtr(additional),
-			C.uint32_t(len(additional)), nil)
-	}
+	// one packet per call, served by libqgcm's resident kernel (no launch per call)
+	n := C.qgcm_seal_one(a.ctx, C.uint32_t(a.idx), bytePtr(data), C.long(length), bytePtr(additional),
+		C.uint32_t(len(additional)), nil)
 	if n < 0 {
 		return -1, errors.New("qgcm: seal failed")
 	}
@@ -177,14 +151,8 @@ func (a *GPUAES) Decrypt(data []byte, additional []byte) (int, error) {
 	if len(data) < overhead || len(additional) > 4 {
 		return a.DecryptedSize(data), errOpen
 	}
-	var n C.long
-	if a.g != nil && a.g.co != nil {
-		n = C.qgcm_coalescer_open(a.g.co, C.uint32_t(a.idx), bytePtr(data), C.long(len(data)), bytePtr(additional),
-			C.uint32_t(len(additional)))
-	} else {
-		n = C.qgcm_open_one(a.ctx, C.uint32_t(a.idx), bytePtr(data), C.long(len(data)), bytePtr(additional),
-			C.uint32_t(len(additional)))
-	}
+	n := C.qgcm_open_one(a.ctx, C.uint32_t(a.idx), bytePtr(data), C.long(len(data)), bytePtr(additional),
+		C.uint32_t(len(additional)))
 	if n < 0 {
 		return a.DecryptedSize(data), errOpen
 	}

@@ -2,7 +2,7 @@
 
 // gpu_aes_test.go -- crypto/crypto_test.go's TestAES and BenchmarkAES (crypto_test.go:54-131) run on
 // GPUAES, plus the edges the shim guards (nil additional data, short buffers, tampering, many
-// goroutines through the coalescer).  `go test -tags gpu ./crypto` on a machine with an MI355X.
+// goroutines calling one GPUAES at once).  `go test -tags gpu ./crypto` on a machine with an MI355X.
 // tests/cpp/go_replay.c replays the same C call sequence from C, which this image can build and the
 // GPU box can run (there is no Go toolchain in either).
 package crypto
@@ -93,12 +93,9 @@ func TestGPUAESEdges(t *testing.T) {
 	}
 }
 
-func TestGPUAESCoalescedGoroutines(t *testing.T) {
+func TestGPUAESConcurrentGoroutines(t *testing.T) {
 	g := newGPUContext(t)
 	defer g.Close()
-	if err := g.EnableCoalescer(256, 100, 1472); err != nil {
-		t.Fatal(err)
-	}
 	aes, err := g.NewGPUAES([]byte("AES256Key-32Characters1234567890"), make([]byte, SaltLength))
 	if err != nil {
 		t.Fatal(err)

@@ -10,8 +10,9 @@
  *   crypto/aes.go:57-62   (*AES).Decrypt(data, aad)           -> qgcm_open_one / qgcm_open_batch
  *   crypto/aes.go:29-36   EncryptedSize / DecryptedSize       -> QGCM_OVERHEAD (= 16 + 12)
  *   crypto/ecdh.go:13-31  GenerateECKeyPair / GenerateSharedSecret -> qgcm_x25519*
- *   plugin/encryption.go:16-40 Encryption.Apply calls Encrypt/Decrypt per packet; the batch
- *                         entry points are what a coalescing Apply shim drives.
+ *   plugin/encryption.go:16-40 Encryption.Apply calls Encrypt/Decrypt per packet (qgcm_seal_one /
+ *                         qgcm_open_one); workers that batch their packets call the host or device
+ *                         batch entry points instead.
  *
  * Error convention follows the reference's own cgo layer (crypto/dtls.go:37-40, dtls.h:43-48):
  * constructors return NULL and fill a caller-supplied error buffer; everything else returns
@@ -125,8 +126,12 @@ long qgcm_open_one(qgcm_ctx *ctx, uint32_t key_idx, uint8_t *data, long len, con
                    uint32_t aad_len);
 
 /* Per-packet calls are served by a RESIDENT kernel (16 workgroups by default, QGCM_RESIDENT_WORKERS;
- * 16 request slots each, QGCM_RESIDENT_SLOTS) that polls pinned host memory, so a call costs no
- * launch; payloads past ~16 KiB and QGCM_RESIDENT=0 take a gcm_one_kernel launch per call instead.
+ * 16 request slots each, QGCM_RESIDENT_SLOTS), so a call costs no launch: the caller writes its packet and
+ * a 16-B request record into fine-grained DEVICE memory through the PCIe BAR (the CPU agent is granted
+ * access with hsa_amd_agents_allow_access), the workers poll those records in their own HBM, and write
+ * the result and a done word into pinned host memory that the caller watches.  Without CPU access to that
+ * memory (or QGCM_RESIDENT=0), and for payloads past ~16 KiB, every call takes a gcm_one_kernel launch
+ * instead; qgcm_resident_stats says which served (requests served, instances launched).
  * The kernel is started by the first call and ends by itself after QGCM_RESIDENT_IDLE_US (2000) without
  * a request or QGCM_RESIDENT_LIFE_US (8000) of life, after serving what is pending (the next call starts
  * it again): work queued behind it on a shared hardware queue, or a device-wide synchronize, waits that
@@ -138,38 +143,25 @@ long qgcm_open_one(qgcm_ctx *ctx, uint32_t key_idx, uint8_t *data, long len, con
  * which computes that nonce's counter blocks while idle (QGCM_RESIDENT_AHEAD=0: off); the next seal
  * on the slot uses that nonce (drawn from getrandom like any other, used once) and skips the counter
  * blocks.  qgcm_resident_stop ends it now; qgcm_resident_stats writes {requests served, instances
- * launched, request slots, workers running now, seals served from a keystream computed ahead}
- * (min(n, 5) values, returns that number or -1). */
+ * launched, request slots, workers running now, seals served from a keystream computed ahead, callers
+ * asleep now, callers spinning now, 1 if the resident path has failed and every call takes the launch
+ * path} (min(n, 8) values, returns that number or -1).  qgcm_set_key(s) ends the instance before it
+ * changes the key tables and holds the next one back until the new keys are published; a per-packet call
+ * racing it waits (or, if the context's resident service was not started yet, starts it). */
 int qgcm_resident_stop(qgcm_ctx *ctx);
 int qgcm_resident_stats(const qgcm_ctx *ctx, uint64_t *out, int n);
 
 /* ---- host batches (end-to-end incl. PCIe) ---- */
 /* Slots in host memory at i*stride; copies in, runs the device batch, copies back, synchronously.
- * Pipelined in ~32 MiB chunks over 3 streams (H2D of chunk c+1 || kernel c || D2H of chunk c-1);
+ * Pipelined in 64 MiB chunks over 3 streams (H2D of chunk c+1 || kernel c || D2H of chunk c-1);
  * h_arena from qgcm_host_alloc (pinned) is DMA'd in place, pageable memory is staged by HIP.
  * Returns the number of packets that failed (0 = all ok) or a negative error.  status may be NULL.
  * Replaces the per-packet Apply loop of worker/outgoing.go:55-93 / worker/incoming.go:54-92 for a
- * coalesced batch. */
+ * batch of packets a worker has collected. */
 int qgcm_seal_host(qgcm_ctx *ctx, uint8_t *h_arena, uint64_t stride, uint32_t n, uint32_t len,
                    uint32_t key_idx, const uint8_t *h_nonces, uint32_t aad_len, uint8_t *h_status);
 int qgcm_open_host(qgcm_ctx *ctx, uint8_t *h_arena, uint64_t stride, uint32_t n, uint32_t len,
                    uint32_t key_idx, uint32_t aad_len, uint8_t *h_status);
-
-/* ---- coalescer: per-packet calls from many threads, batched on the device ---- */
-/* The exact Encrypt/Decrypt contract of crypto/aes.go:41-62 (blocking, in place, L+28 / len-28 or
- * -1, plaintext zeroed on auth failure), for the 2 x NumWorkers goroutines that call plugin.Apply
- * (worker/outgoing.go:55-93, worker/incoming.go:54-92): concurrent calls share one device batch,
- * flushed at max_batch packets or after max_wait_us.  Seal nonces come from one getrandom(2) per
- * batch.  Calls whose aad_len differs from the coalescer's go through qgcm_seal_one/open_one.
- * Thread-safe; destroy only when no call is in flight.  NULL + err on failure. */
-typedef struct qgcm_coalescer qgcm_coalescer;
-qgcm_coalescer *qgcm_coalescer_create(qgcm_ctx *ctx, uint32_t max_batch, uint32_t max_wait_us,
-                                      uint32_t max_packet, uint32_t aad_len, char *err, size_t errlen);
-void qgcm_coalescer_destroy(qgcm_coalescer *c);
-long qgcm_coalescer_seal(qgcm_coalescer *c, uint32_t key_idx, uint8_t *data, long length,
-                         const uint8_t *aad, uint32_t aad_len);
-long qgcm_coalescer_open(qgcm_coalescer *c, uint32_t key_idx, uint8_t *data, long len,
-                         const uint8_t *aad, uint32_t aad_len);
 
 /* ---- several GPUs behind one process (quantum is one process: main.go:29-114, 72-75) ---- */
 /* A group of `count` member contexts, member k on devices[k] (members may share a device).  Keyed
@@ -203,8 +195,22 @@ int qgcm_group_seal_host(qgcm_group *g, uint8_t *h_arena, const qgcm_desc *h_des
                          const uint8_t *h_nonces, uint32_t aad_len, uint8_t *h_status);
 int qgcm_group_open_host(qgcm_group *g, uint8_t *h_arena, const qgcm_desc *h_descs, uint32_t n, uint32_t aad_len,
                          uint8_t *h_status);
-/* 1 if the last qgcm_group_seal_host / open_host call took the zero-copy path, else 0. */
+/* 1 if the last qgcm_group_seal_host / open_host call took the zero-copy path on every member, else 0. */
 int qgcm_group_last_zerocopy(const qgcm_group *g);
+/* DMA runs: when the descriptors are in arena order (offsets nondecreasing, multiples of 4) and a member's
+ * packets form runs of adjacent records (consecutive packets, at most 256 B between one record's end and
+ * the next one's start) averaging 64 KiB or more, that member copies each run to and from its device with
+ * one DMA each way (64 MiB chunks, three streams), with no gather, scatter or shader-driven PCIe traffic;
+ * the gap bytes inside a run go back unchanged.  A batch laid out in qgcm_group_order's order, or any batch
+ * of a one-member group, takes it.  QGCM_GROUP_DMA=0 disables it.  qgcm_group_last_path: the path member
+ * took in the last call (0 host copies, 1 zero-copy, 2 DMA runs) or QGCM_E_ARG. */
+int qgcm_group_last_path(const qgcm_group *g, int member);
+/* The order in which to lay out a keyed batch so that each member's packets are contiguous (a stable
+ * counting sort by qgcm_group_shard): order[0..n) = input indices, member by member; member_counts
+ * (may be NULL) receives each member's packet count.  A caller that assembles its batch in this order
+ * gets the DMA-run path.  Returns QGCM_OK or QGCM_E_ARG. */
+int qgcm_group_order(const qgcm_group *g, const uint32_t *key_idx, uint32_t n, uint32_t *order,
+                     uint32_t *member_counts);
 
 /* Pinned (page-locked) host memory for arenas handed to the *_host calls; NULL on failure. */
 void *qgcm_host_alloc(size_t bytes);
@@ -306,8 +312,8 @@ int qgcm_tun_close(int fd);
 /* ---- introspection: which kernels served this context's calls ---- */
 /* Launch counts per kernel family since qgcm_create (uniform batches launch in chunks of 2^19
  * packets; a descriptor batch launches the segmented kernel and then the per-wave kernel for its
- * short keys; gcm_one_kernel serves per-packet calls, the coalescer's flushes and uniform batches of
- * up to 2048 packets).  Writes min(n, QGCM_KERNEL_COUNTERS) counters, returns that number or -1. */
+ * short keys; gcm_one_kernel serves per-packet calls the resident kernel does not take and uniform
+ * batches of up to 2048 packets).  Writes min(n, QGCM_KERNEL_COUNTERS) counters, returns that number or -1. */
 #define QGCM_KERNEL_QUAD 0      /* gcm_quad_kernel, single-key (uniform) batches */
 #define QGCM_KERNEL_SEGMENTED 1 /* gcm_seg_kernel, descriptor batches (long key runs) */
 #define QGCM_KERNEL_PER_WAVE 2  /* gcm_quad_kernel, descriptor batches (short key runs) */

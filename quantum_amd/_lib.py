@@ -20,7 +20,6 @@ EXPORTS = (
     "qgcm_seal_batch", "qgcm_open_batch", "qgcm_seal_uniform", "qgcm_open_uniform",
     "qgcm_seal_one", "qgcm_open_one", "qgcm_seal_host", "qgcm_open_host",
     "qgcm_random_nonces", "qgcm_fill_uniform", "qgcm_host_alloc", "qgcm_host_free",
-    "qgcm_coalescer_create", "qgcm_coalescer_destroy", "qgcm_coalescer_seal", "qgcm_coalescer_open",
     "qgcm_stream_copy",
     "qgcm_snappy_max_compressed_length", "qgcm_snappy_compress", "qgcm_snappy_uncompressed_length",
     "qgcm_snappy_uncompress", "qgcm_snappy_compress_slots", "qgcm_snappy_uncompress_slots",
@@ -31,7 +30,7 @@ EXPORTS = (
     "qgcm_tun_open", "qgcm_tun_up", "qgcm_tun_read_slots", "qgcm_tun_write_slots", "qgcm_tun_close",
     "qgcm_group_create", "qgcm_group_destroy", "qgcm_group_size", "qgcm_group_ctx", "qgcm_group_shard",
     "qgcm_group_set_keys", "qgcm_group_seal_host", "qgcm_group_open_host", "qgcm_group_member_cpus",
-    "qgcm_group_last_zerocopy", "qgcm_launch_counts", "qgcm_resident_stop", "qgcm_resident_stats",
+    "qgcm_group_last_zerocopy", "qgcm_group_last_path", "qgcm_group_order", "qgcm_launch_counts", "qgcm_resident_stop", "qgcm_resident_stats",
 )
 
 QGCM_OK = 0
@@ -87,14 +86,6 @@ def _bind(L: C.CDLL) -> None:
     L.qgcm_host_alloc.restype = vp
     L.qgcm_host_free.argtypes = [vp]
     L.qgcm_host_free.restype = None
-    L.qgcm_coalescer_create.argtypes = [vp, u32, u32, u32, u32, C.c_char_p, C.c_size_t]
-    L.qgcm_coalescer_create.restype = vp
-    L.qgcm_coalescer_destroy.argtypes = [vp]
-    L.qgcm_coalescer_destroy.restype = None
-    L.qgcm_coalescer_seal.argtypes = [vp, u32, vp, lng, vp, u32]
-    L.qgcm_coalescer_seal.restype = lng
-    L.qgcm_coalescer_open.argtypes = [vp, u32, vp, lng, vp, u32]
-    L.qgcm_coalescer_open.restype = lng
     L.qgcm_stream_copy.argtypes = [vp, vp, vp, u64, vp]
     if hasattr(L, "qgcm_launch_counts"):
         L.qgcm_launch_counts.argtypes = [vp, vp, i32]
@@ -141,6 +132,9 @@ def _bind(L: C.CDLL) -> None:
             L.qgcm_group_member_cpus.argtypes = [vp, i32]
         if hasattr(L, "qgcm_group_last_zerocopy"):
             L.qgcm_group_last_zerocopy.argtypes = [vp]
+        if hasattr(L, "qgcm_group_last_path"):
+            L.qgcm_group_last_path.argtypes = [vp, i32]
+            L.qgcm_group_order.argtypes = [vp, vp, u32, vp, vp]
     if hasattr(L, "qgcm_tun_open"):  # (older builds loaded by the A/B tools lack the TUN calls)
         L.qgcm_tun_open.argtypes = [C.c_char_p, C.c_int, vp, C.c_char_p, sz]
         L.qgcm_tun_up.argtypes = [C.c_char_p, C.c_char_p, C.c_int, C.c_int]

@@ -68,10 +68,12 @@ class Context:
 
     def resident_stats(self) -> dict:
         """The resident per-packet kernel: requests served, instances launched, slots, workers running,
-        seals served from a keystream computed ahead."""
-        out = (C.c_uint64 * 5)()
-        _lib.check(_lib.lib().qgcm_resident_stats(self.handle, out, 5), "qgcm_resident_stats")
-        return dict(zip(("served", "launches", "slots", "running", "ahead_hits"), (int(x) for x in out)))
+        seals served from a keystream computed ahead, callers asleep / spinning now, broken (1: every
+        call takes the launch path)."""
+        names = ("served", "launches", "slots", "running", "ahead_hits", "sleepers", "spinners", "broken")
+        out = (C.c_uint64 * len(names))()
+        n = _lib.check(_lib.lib().qgcm_resident_stats(self.handle, out, len(names)), "qgcm_resident_stats")
+        return dict(zip(names[:n], (int(x) for x in out)))
 
     def resident_stop(self) -> None:
         _lib.check(_lib.lib().qgcm_resident_stop(self.handle), "qgcm_resident_stop")
@@ -160,13 +162,11 @@ def _addr(data, offset: int = 0) -> tuple[int, int, object]:
 class AES:
     """crypto/aes.go:22-26 -- an AES-256-GCM AEAD bound to a device key slot."""
 
-    def __init__(self, key: bytes, salt: bytes | None = None, ctx: Context | None = None, coalescer=None):
+    def __init__(self, key: bytes, salt: bytes | None = None, ctx: Context | None = None):
         self.ctx = ctx or default_context()
         self.slot = self.ctx.alloc_slot()
         self.ctx.set_key(self.slot, key)
         self.salt = salt
-        # quantum_amd.coalescer.Coalescer: concurrent Encrypt/Decrypt calls share device batches
-        self.coalescer = coalescer
 
     def NonceSize(self) -> int:
         return NonceSize
@@ -189,10 +189,7 @@ class AES:
         if length < 0 or length + Overhead + NonceSize > cap:
             raise IndexError("slice bounds out of range")  # Go would panic in Seal/copy
         aad = bytes(additional) if additional is not None else b""
-        if self.coalescer is not None and nonce is None:
-            n = _lib.lib().qgcm_coalescer_seal(self.coalescer.handle, self.slot, addr, length, aad or None, len(aad))
-        else:
-            n = _lib.lib().qgcm_seal_one(self.ctx.handle, self.slot, addr, length, aad or None, len(aad), nonce)
+        n = _lib.lib().qgcm_seal_one(self.ctx.handle, self.slot, addr, length, aad or None, len(aad), nonce)
         del keep
         if n < 0:
             return -1, RuntimeError("qgcm_seal_one failed")
@@ -204,10 +201,7 @@ class AES:
         if length < NonceSize:
             raise IndexError("slice bounds out of range")  # the reference panics (negative slice)
         aad = bytes(additional) if additional is not None else b""
-        if self.coalescer is not None:
-            n = _lib.lib().qgcm_coalescer_open(self.coalescer.handle, self.slot, addr, length, aad or None, len(aad))
-        else:
-            n = _lib.lib().qgcm_open_one(self.ctx.handle, self.slot, addr, length, aad or None, len(aad))
+        n = _lib.lib().qgcm_open_one(self.ctx.handle, self.slot, addr, length, aad or None, len(aad))
         del keep
         return self.DecryptedSize(data) if n >= 0 else length - Overhead - NonceSize, (None if n >= 0 else ErrOpen())
 

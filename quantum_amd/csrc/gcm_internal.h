@@ -47,8 +47,7 @@ struct Batch {
     const uint32_t *nruns;
     const uint32_t *tile_list;  // per-wave descriptor kernels: NULL = every tile of the worklist, else
     const uint32_t *n_list;     // only these tiles (*n_list of them; the segmented kernel's short keys)
-    uint8_t *done;              // gcm_one_kernel: done[0] (uniform form, one packet) or done[pkt] (descriptor
-                                // form) set to 1 after the slot is written
+    uint8_t *done;              // gcm_one_kernel (a per-packet call): set to 1 after the slot is written
                                 // back and made system-visible (the host polls it instead of the stream)
     const uint4 *pw_table;      // latency engine: [pw_keys][kPwPowers][kPwEntries] kPwBits-bit comb tables of
     uint32_t pw_keys;           // H^1..H^kPwPowers (NULL / 0: the Horner + Estrin GHASH for every packet)
@@ -128,20 +127,18 @@ Resident *resident_create(int device, const Batch &base, int num_cus);  // nullp
 void resident_destroy(Resident *r);
 int resident_quiesce(Resident *r);
 int resident_workers_running(const Resident *r);
-void resident_stats(const Resident *r, uint64_t out[5]);  // served, launches, slots, workers running, ahead hits
+// served, launches, slots, workers running, ahead hits, callers asleep, callers spinning, broken
+constexpr int kResStats = 8;
+void resident_stats(const Resident *r, uint64_t out[kResStats]);
+int resident_pause(Resident *r);  // quiesce and hold new instances back (qgcm_set_keys) ...
+void resident_resume(Resident *r);  // ... until this
 constexpr long kResNotServed = -1000;  // resident_call: the request does not fit; take the launch path
 bool random_nonce(uint8_t out[12]);   // getrandom, buffered per thread, fork-safe (resident.cpp)
 long resident_call(Resident *r, bool seal, uint32_t key, uint8_t *data, long len, const uint8_t *aad,
                    uint32_t aad_len, const uint8_t *nonce);
-// Small descriptor batches through the latency kernel, one workgroup per packet, straight on the
-// caller's (pinned host or device) arena/descriptors/nonces/status -- the coalescer's flush path.
-constexpr uint32_t kOneBatchMax = 2048;
 constexpr uint32_t kOneUniformMax = 2048;    // measured cross-over with the quad kernel: 2048-4096 packets
 constexpr uint32_t kLaunchChunk = 1u << 19;  // packets per quad-kernel launch of a uniform batch
 constexpr uint32_t kDescChunk = 0;           // packets per sorted chunk of a descriptor batch (0 = all)
-int run_one_descs(qgcm_ctx *ctx, bool seal, uint8_t *arena, const qgcm_desc *descs, uint32_t n,
-                  const uint8_t *nonces, uint32_t aad_len, uint8_t *status, hipStream_t s,
-                  uint8_t *done = nullptr);
 bool ctx_one_kernel(const qgcm_ctx *ctx);
 hipError_t launch_stream_copy(void *dst, const void *src, uint64_t bytes, int num_cus, hipStream_t s);
 // one record move of the group dispatcher's zero-copy path: src/dst device-accessible addresses
@@ -154,9 +151,6 @@ struct RecMove {
 // exactly `bytes`, and only moves whose status byte is 1 when d_status is given
 hipError_t launch_move_records(const RecMove *d_moves, uint32_t n, const uint8_t *d_status, bool exact, int num_cus,
                                hipStream_t s);
-// context accessors for the coalescer (coalescer.cpp), defined in qgcm_api.cpp
-int ctx_device(const qgcm_ctx *ctx);
-bool ctx_key_ready(qgcm_ctx *ctx, uint32_t key_idx);
 // Device snappy codec (snappy_kernels.hip): one wave per Payload.Raw slot at i * stride.
 // LDS per wave: [hash table | staged input at off_in | output at off_out | lane scratch at off_sink],
 // wave_bytes in all.

@@ -1678,23 +1678,16 @@ __device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_t
     return ok;
 }
 
-// One workgroup per packet.  Uniform form (b.descs == NULL): slot i at b.arena + i * b.stride,
-// b.uniform_len = L (seal) or L + 28 (open), b.uniform_key.  Descriptor form (the coalescer's small
-// batches): packet blockIdx.x is b.descs[blockIdx.x] in b.arena.  Slots are 16-B aligned and
+// One workgroup per packet: slot i at b.arena + i * b.stride, b.uniform_len = L (seal) or L + 28
+// (open), b.uniform_key (a per-packet call is a batch of one).  Slots are 16-B aligned and
 // (4 + len (+ 28 for seal) + 15) & ~15 bytes long, at most kOneCap - 16; seal nonces come from
 // b.nonces (12 B per packet) when it is set, else from the slot.  b.status[packet] = verdict.
 template <bool kSeal>
 __global__ void __launch_bounds__(kOneThreads) gcm_one_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
     const uint32_t tid = threadIdx.x;
     const uint32_t pkt = blockIdx.x;
-    uint64_t off = (uint64_t)pkt * b.stride;  // uniform form: slot pkt of the batch
-    uint32_t Lin = b.uniform_len, key = b.uniform_key;
-    if (b.descs) {
-        const qgcm_desc dsc = b.descs[pkt];
-        off = dsc.offset;
-        Lin = dsc.len;
-        key = dsc.key_idx;
-    }
+    const uint64_t off = (uint64_t)pkt * b.stride;
+    const uint32_t Lin = b.uniform_len, key = b.uniform_key;
     const uint32_t n16 = (uint32_t)((4ull + Lin + (kSeal ? QGCM_OVERHEAD : 0) + 15) >> 4);
     // as the batch kernels: a key index out of range or an open shorter than 28 B fails the packet
     // (slot untouched); so does a slot past the LDS staging area or misaligned (the host never sends one)
@@ -1702,9 +1695,9 @@ __global__ void __launch_bounds__(kOneThreads) gcm_one_kernel(Batch b, const uin
         n16 * 16u > kOneCap - 16u || (off & 15u)) {
         if (tid == 0) {
             if (b.status) b.status[pkt] = 0;
-            if (b.done) {  // the host waits on every packet's flag
+            if (b.done) {  // the host waits on the flag
                 __threadfence_system();
-                *reinterpret_cast<volatile uint8_t *>(b.done + (b.descs ? pkt : 0u)) = 1;
+                *reinterpret_cast<volatile uint8_t *>(b.done) = 1;
             }
         }
         return;
@@ -1719,7 +1712,7 @@ __global__ void __launch_bounds__(kOneThreads) gcm_one_kernel(Batch b, const uin
         __syncthreads();
         if (tid == 0) {
             __threadfence_system();
-            *reinterpret_cast<volatile uint8_t *>(b.done + (b.descs ? pkt : 0u)) = 1;
+            *reinterpret_cast<volatile uint8_t *>(b.done) = 1;
         }
     }
 }

@@ -34,6 +34,16 @@
 // PCIe into device staging), runs the descriptor batch there and scatters the results back into the
 // slots -- the host only builds the per-record move lists (24 B per record).  QGCM_GROUP_ZEROCOPY=0
 // forces the CPU path.
+//
+// DMA-run path (the default when it applies): when a member's packets lie in the arena as long runs of
+// adjacent records -- the caller laid the batch out grouped by member (qgcm_group_order), or the group
+// has one member -- nothing is gathered at all.  Each run (records of consecutive input packets, gaps
+// of at most kRunGap bytes between them) is copied to device staging with one hipMemcpyAsync, the
+// descriptor batch runs on the staging with rebased offsets, and the run is copied back whole; a
+// record's gap bytes and untouched fields go back as they came.  Three streams per member (copy-in,
+// kernels, copy-out) ordered by per-slot events over kDmaSlots staging slots, as qgcm_seal_host's
+// pipeline does, so each PCIe direction sees a steady queue of large copies: the SDMA engines move the
+// bytes (shader-driven zero-copy reached ~25 GB/s each way; DMA ~45).  QGCM_GROUP_DMA=0 disables it.
 #include <hip/hip_runtime.h>
 #include <pthread.h>
 #include <ctype.h>
@@ -59,6 +69,10 @@ constexpr uint64_t kZcChunk = 256ull << 20; // zero-copy path (device staging): 
                                             // chunk to fill the GPU (a 32-MB chunk is ~1500 tiles)
 constexpr int kSlots = 2;                 // staging slots per member (double buffer)
 constexpr int kCopyThreads = 4;           // gather/scatter threads per member (QGCM_GROUP_THREADS)
+constexpr uint64_t kDmaChunk = 64ull << 20; // DMA-run path: staged bytes per chunk (qgcm_seal_host's size)
+constexpr int kDmaSlots = 4;              // DMA-run path: staging slots in flight per member
+constexpr uint64_t kRunGap = 256;         // largest gap between two records that still joins them in a run
+constexpr uint64_t kMinRun = 64ull << 10; // DMA-run path only when runs average at least this many bytes
 
 struct Stage {
     uint8_t *h = nullptr, *d = nullptr;  // pinned host / device: [records][descs][nonces][status]
@@ -147,12 +161,23 @@ struct ZC {
     uint64_t stage_cap = 0;  // bytes per staging slot
 };
 
+// DMA-run path state of a member (grow-only)
+struct DmaState {
+    hipStream_t s[3] = {};  // copy-in, kernels, copy-out
+    hipEvent_t ev_in[kDmaSlots] = {}, ev_k[kDmaSlots] = {}, ev_out[kDmaSlots] = {};
+    uint8_t *d_stage[kDmaSlots] = {};  // [records][descs][nonces][status] of one chunk
+    uint8_t *h_side[kDmaSlots] = {};   // pinned [descs][nonces][status] of one chunk
+    uint64_t stage_cap = 0, side_cap = 0;
+};
+
 struct Member {
     qgcm_ctx *ctx = nullptr;
     int device = 0;
     int num_cus = 0;
     Stage st[kSlots];
     ZC zc;
+    DmaState dma;
+    int last_path = 0;  // 0 copy, 1 zero-copy, 2 DMA runs (qgcm_group_last_path)
     cpu_set_t cpus;  // the GPU's local CPUs allowed to this process (empty: the thread is not pinned)
     int ncpus = 0;
     std::unique_ptr<CopyPool> pool;  // gather/scatter threads (created with the member)
@@ -215,6 +240,7 @@ struct qgcm_group {
     std::vector<Member> m;
     uint32_t max_keys = 0;
     bool zerocopy = true;  // QGCM_GROUP_ZEROCOPY=0: always gather/scatter on the CPU
+    bool dma = true;       // QGCM_GROUP_DMA=0: never the DMA-run path
     int last_zc = 0;       // the last call took the zero-copy path (qgcm_group_last_zerocopy)
     uint64_t zc_chunk = kZcChunk;  // zero-copy staging chunk bytes (QGCM_GROUP_ZC_CHUNK_MB, tuning)
     std::mutex call_mu;  // one batch call at a time (members' staging is reused per call)
@@ -472,6 +498,178 @@ int run_member_zc(Member &mb, bool seal, uint64_t v_arena, const qgcm_desc *desc
     return rc;
 }
 
+// ---- DMA-run path ----
+struct Piece {
+    uint64_t src, dst, bytes;  // arena offset, offset in the chunk's staging, length
+};
+struct DmaChunk {
+    size_t p0, p1, j0, j1;  // pieces [p0, p1), member packets [j0, j1)
+    uint64_t bytes;         // staging bytes the records occupy
+};
+struct DmaPlan {
+    std::vector<Piece> pieces;
+    std::vector<DmaChunk> chunks;
+    std::vector<uint64_t> at;  // staging offset of member packet j within its chunk
+    uint64_t piece_bytes = 0, max_bytes = 0;
+    size_t max_pk = 0;
+};
+
+inline uint64_t rec_in(bool seal, uint32_t len) {  // bytes of a slot the call reads and may write
+    return 4ull + len + (seal ? QGCM_OVERHEAD : 0);
+}
+
+// Runs of member packets idx[0..m) (input order, offsets nondecreasing over the whole batch): packet
+// idx[j] joins the run of idx[j-1] when it is the next input packet and its record starts at most
+// kRunGap bytes after the previous record ends.  Runs are cut into chunks of up to `chunk` staging
+// bytes at record boundaries; each piece keeps its arena offset mod 256 in staging (payload alignment).
+void plan_dma(bool seal, const qgcm_desc *descs, const uint32_t *idx, size_t m, uint64_t chunk, DmaPlan &pl) {
+    pl = DmaPlan{};
+    pl.at.resize(m);
+    uint64_t prev_end = 0;
+    size_t j0 = 0, p0 = 0;
+    for (size_t j = 0; j < m; ++j) {
+        const qgcm_desc &d = descs[idx[j]];
+        const uint64_t r0 = d.offset, r1 = r0 + rec_in(seal, d.len);
+        bool joined = false;
+        if (j > j0 && idx[j] == idx[j - 1] + 1 && r0 >= prev_end && r0 - prev_end <= kRunGap) {
+            Piece &pc = pl.pieces.back();
+            if (pc.dst + (r1 - pc.src) <= chunk) {
+                pc.bytes = r1 - pc.src;
+                joined = true;
+            }
+        }
+        if (!joined) {
+            uint64_t pos = pl.pieces.size() > p0 ? pl.pieces.back().dst + pl.pieces.back().bytes : 0;
+            pos += (r0 - pos) & 255;
+            if (j > j0 && pos + (r1 - r0) > chunk) {  // close the chunk
+                pl.chunks.push_back(DmaChunk{p0, pl.pieces.size(), j0, j, pos});
+                j0 = j;
+                p0 = pl.pieces.size();
+                pos = r0 & 255;
+            }
+            pl.pieces.push_back(Piece{r0, pos, r1 - r0});
+        }
+        const Piece &pc = pl.pieces.back();
+        pl.at[j] = pc.dst + (r0 - pc.src);
+        prev_end = r1;
+    }
+    if (m) {
+        const Piece &pc = pl.pieces.back();
+        pl.chunks.push_back(DmaChunk{p0, pl.pieces.size(), j0, m, pc.dst + pc.bytes});
+    }
+    for (const Piece &pc : pl.pieces) pl.piece_bytes += pc.bytes;
+    for (DmaChunk &c : pl.chunks) {
+        c.bytes = (pl.pieces[c.p1 - 1].dst + pl.pieces[c.p1 - 1].bytes + 255) & ~255ull;
+        pl.max_bytes = std::max(pl.max_bytes, c.bytes);
+        pl.max_pk = std::max(pl.max_pk, c.j1 - c.j0);
+    }
+}
+
+int dma_ready(DmaState &z, uint64_t stage, uint64_t side) {
+    for (hipStream_t &x : z.s)
+        if (!x && hipStreamCreateWithFlags(&x, hipStreamNonBlocking) != hipSuccess) return QGCM_E_HIP;
+    for (int k = 0; k < kDmaSlots; ++k)
+        for (hipEvent_t *e : {&z.ev_in[k], &z.ev_k[k], &z.ev_out[k]})
+            if (!*e && hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return QGCM_E_HIP;
+    if (stage + side > z.stage_cap) {
+        for (auto &p : z.d_stage) {
+            if (p) hipFree(p);
+            p = nullptr;
+        }
+        z.stage_cap = 0;
+        for (auto &p : z.d_stage)
+            if (hipMalloc(&p, stage + side) != hipSuccess) return QGCM_E_NOMEM;
+        z.stage_cap = stage + side;
+    }
+    if (side > z.side_cap) {
+        for (auto &p : z.h_side) {
+            if (p) hipHostFree(p);
+            p = nullptr;
+        }
+        z.side_cap = 0;
+        for (auto &p : z.h_side)
+            if (hipHostMalloc(&p, side, hipHostMallocDefault) != hipSuccess) return QGCM_E_NOMEM;
+        z.side_cap = side;
+    }
+    return QGCM_OK;
+}
+
+int run_member_dma(Member &mb, bool seal, uint8_t *h_arena, const qgcm_desc *descs, const uint32_t *idx,
+                   const DmaPlan &pl, const uint8_t *h_nonces, uint32_t aad_len, uint8_t *h_status, int *bad_out) {
+    DmaState &z = mb.dma;
+    const bool non = seal && h_nonces;
+    const uint64_t pk = pl.max_pk;
+    const uint64_t off_non = (16ull * pk + 255) & ~255ull, off_st = off_non + (non ? (12ull * pk + 255) & ~255ull : 0);
+    const uint64_t side = off_st + ((pk + 255) & ~255ull);
+    int rc = dma_ready(z, pl.max_bytes, side);
+    if (rc != QGCM_OK) return rc;
+    hipStream_t s_in = z.s[0], s_k = z.s[1], s_out = z.s[2];
+    int bad = 0;
+    // results of the chunk last staged in slot k (its copy-out has landed): statuses to the caller
+    auto retire = [&](int k, const DmaChunk &c) {
+        const uint8_t *st = z.h_side[k] + off_st;
+        for (size_t j = c.j0; j < c.j1; ++j) {
+            bad += st[j - c.j0] != 1;
+            if (h_status) h_status[idx[j]] = st[j - c.j0];
+        }
+    };
+    const size_t nc = pl.chunks.size();
+    size_t c = 0;
+    for (; c < nc && rc == QGCM_OK; ++c) {
+        const int k = (int)(c % kDmaSlots);
+        const DmaChunk &ch = pl.chunks[c];
+        if (c >= (size_t)kDmaSlots) {  // slot k's previous chunk must have landed before its side area is reused
+            if (hipEventSynchronize(z.ev_out[k]) != hipSuccess) {
+                rc = QGCM_E_HIP;
+                break;
+            }
+            retire(k, pl.chunks[c - kDmaSlots]);
+        }
+        uint8_t *hs = z.h_side[k], *ds = z.d_stage[k];
+        const uint64_t dside = pl.max_bytes;  // descs / nonces / status behind the records
+        const size_t cn = ch.j1 - ch.j0;
+        qgcm_desc *hd = reinterpret_cast<qgcm_desc *>(hs);
+        for (size_t j = ch.j0; j < ch.j1; ++j) {
+            const qgcm_desc &d = descs[idx[j]];
+            hd[j - ch.j0] = qgcm_desc{pl.at[j], d.len, d.key_idx};
+            if (non) memcpy(hs + off_non + 12 * (j - ch.j0), h_nonces + 12ull * idx[j], 12);
+        }
+        if (hipStreamWaitEvent(s_in, z.ev_out[k], 0) != hipSuccess) rc = QGCM_E_HIP;
+        for (size_t p = ch.p0; p < ch.p1 && rc == QGCM_OK; ++p) {
+            const Piece &pc = pl.pieces[p];
+            if (hipMemcpyAsync(ds + pc.dst, h_arena + pc.src, pc.bytes, hipMemcpyHostToDevice, s_in) != hipSuccess)
+                rc = QGCM_E_HIP;
+        }
+        if (rc == QGCM_OK &&
+            (hipMemcpyAsync(ds + dside, hs, off_st, hipMemcpyHostToDevice, s_in) != hipSuccess ||
+             hipEventRecord(z.ev_in[k], s_in) != hipSuccess || hipStreamWaitEvent(s_k, z.ev_in[k], 0) != hipSuccess))
+            rc = QGCM_E_HIP;
+        if (rc != QGCM_OK) break;
+        const qgcm_desc *dd = reinterpret_cast<const qgcm_desc *>(ds + dside);
+        rc = seal ? qgcm_seal_batch(mb.ctx, ds, dd, (uint32_t)cn, non ? ds + dside + off_non : nullptr, aad_len,
+                                    ds + dside + off_st, s_k)
+                  : qgcm_open_batch(mb.ctx, ds, dd, (uint32_t)cn, aad_len, ds + dside + off_st, s_k);
+        if (rc != QGCM_OK) break;
+        if (hipEventRecord(z.ev_k[k], s_k) != hipSuccess || hipStreamWaitEvent(s_out, z.ev_k[k], 0) != hipSuccess)
+            rc = QGCM_E_HIP;
+        for (size_t p = ch.p0; p < ch.p1 && rc == QGCM_OK; ++p) {
+            const Piece &pc = pl.pieces[p];
+            if (hipMemcpyAsync(h_arena + pc.src, ds + pc.dst, pc.bytes, hipMemcpyDeviceToHost, s_out) != hipSuccess)
+                rc = QGCM_E_HIP;
+        }
+        if (rc == QGCM_OK &&
+            (hipMemcpyAsync(hs + off_st, ds + dside + off_st, cn, hipMemcpyDeviceToHost, s_out) != hipSuccess ||
+             hipEventRecord(z.ev_out[k], s_out) != hipSuccess))
+            rc = QGCM_E_HIP;
+    }
+    for (hipStream_t x : z.s)
+        if (hipStreamSynchronize(x) != hipSuccess && rc == QGCM_OK) rc = QGCM_E_HIP;
+    if (rc == QGCM_OK)  // the chunks still in their slots
+        for (size_t q = c > (size_t)kDmaSlots ? c - kDmaSlots : 0; q < c; ++q) retire((int)(q % kDmaSlots), pl.chunks[q]);
+    *bad_out = bad;
+    return rc;
+}
+
 int run_group(qgcm_group *g, bool seal, uint8_t *h_arena, const qgcm_desc *descs, uint32_t n,
               const uint8_t *h_nonces, uint32_t aad_len, uint8_t *h_status) {
     if (!g || (n && (!h_arena || !descs)) || aad_len > 4 || n > QGCM_MAX_BATCH) return QGCM_E_ARG;
@@ -501,6 +699,11 @@ int run_group(qgcm_group *g, bool seal, uint8_t *h_arena, const qgcm_desc *descs
         zc = !(descs[i].offset & 3);
     }
     zc = zc && !((uintptr_t)h_arena & 3) && !(seal && h_nonces && ((uintptr_t)h_nonces & 3));
+    // DMA runs need the input in arena order (a run is consecutive input packets) and 4-B record offsets
+    bool sorted = g->dma;
+    for (uint32_t i = 1; sorted && i < n; ++i) sorted = descs[i].offset >= descs[i - 1].offset;
+    for (uint32_t i = 0; sorted && i < n; ++i) sorted = !(descs[i].offset & 3);
+    std::vector<DmaPlan> plan(G);
     std::vector<int> rc(G, QGCM_OK), bad(G, 0), used_zc(G, 1);
     std::vector<std::thread> thr;
     for (int k = 0; k < G; ++k) {
@@ -512,6 +715,17 @@ int run_group(qgcm_group *g, bool seal, uint8_t *h_arena, const qgcm_desc *descs
                 rc[k] = QGCM_E_HIP;
                 return;
             }
+            if (sorted) {
+                const size_t m = part[k].size();
+                plan_dma(seal, descs, part[k].data(), m, kDmaChunk, plan[k]);
+                if (plan[k].piece_bytes >= kMinRun * plan[k].pieces.size()) {
+                    mb.last_path = 2;
+                    used_zc[k] = 0;
+                    rc[k] = run_member_dma(mb, seal, h_arena, descs, part[k].data(), plan[k], h_nonces, aad_len,
+                                           h_status, &bad[k]);
+                    return;
+                }
+            }
             uint64_t va = 0, vn = 0;
             if (zc) {
                 va = pinned_view(h_arena, extent);
@@ -519,6 +733,7 @@ int run_group(qgcm_group *g, bool seal, uint8_t *h_arena, const qgcm_desc *descs
                 if ((va | vn) & 3) va = 0;
             }
             used_zc[k] = va ? 1 : 0;
+            mb.last_path = va ? 1 : 0;
             rc[k] = va ? run_member_zc(mb, seal, va, descs, part[k].data(), part[k].size(), vn, aad_len, h_status,
                                        &bad[k], g->zc_chunk)
                        : run_member(mb, seal, h_arena, descs, part[k].data(), part[k].size(), h_nonces, aad_len,
@@ -549,6 +764,7 @@ qgcm_group *qgcm_group_create(const int *devices, int count, uint32_t max_keys, 
     int threads = kCopyThreads;
     if (const char *v = getenv("QGCM_GROUP_THREADS")) threads = std::max(1, std::min(64, atoi(v)));
     if (const char *v = getenv("QGCM_GROUP_ZEROCOPY")) g->zerocopy = atoi(v) != 0;
+    if (const char *v = getenv("QGCM_GROUP_DMA")) g->dma = atoi(v) != 0;
     if (const char *v = getenv("QGCM_GROUP_ZC_CHUNK_MB")) g->zc_chunk = (uint64_t)std::max(1, atoi(v)) << 20;
     for (int k = 0; k < count; ++k) {
         Member mb;
@@ -586,6 +802,18 @@ void qgcm_group_destroy(qgcm_group *g) {
         hipFree(z.d_descs);
         hipFree(z.d_status);
         for (uint8_t *st : z.d_stage) hipFree(st);
+        DmaState &dm = mb.dma;
+        for (hipStream_t x : dm.s)
+            if (x) {
+                hipStreamSynchronize(x);
+                hipStreamDestroy(x);
+            }
+        for (int k = 0; k < kDmaSlots; ++k) {
+            for (hipEvent_t e : {dm.ev_in[k], dm.ev_k[k], dm.ev_out[k]})
+                if (e) hipEventDestroy(e);
+            if (dm.d_stage[k]) hipFree(dm.d_stage[k]);
+            if (dm.h_side[k]) hipHostFree(dm.h_side[k]);
+        }
         qgcm_destroy(mb.ctx);
     }
     delete g;
@@ -594,6 +822,28 @@ void qgcm_group_destroy(qgcm_group *g) {
 int qgcm_group_size(const qgcm_group *g) { return g ? (int)g->m.size() : 0; }
 
 int qgcm_group_last_zerocopy(const qgcm_group *g) { return g ? g->last_zc : QGCM_E_ARG; }
+
+int qgcm_group_last_path(const qgcm_group *g, int member) {
+    return g && member >= 0 && member < (int)g->m.size() ? g->m[member].last_path : QGCM_E_ARG;
+}
+
+int qgcm_group_order(const qgcm_group *g, const uint32_t *key_idx, uint32_t n, uint32_t *order,
+                     uint32_t *member_counts) {
+    if (!g || g->m.empty() || (n && (!key_idx || !order))) return QGCM_E_ARG;
+    const int G = (int)g->m.size();
+    std::vector<uint64_t> start(G + 1, 0);
+    std::vector<int> owner(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        owner[i] = qgcm_group_shard(g, key_idx[i]);
+        ++start[owner[i] + 1];
+    }
+    for (int k = 0; k < G; ++k) {
+        if (member_counts) member_counts[k] = (uint32_t)start[k + 1];
+        start[k + 1] += start[k];
+    }
+    for (uint32_t i = 0; i < n; ++i) order[start[owner[i]]++] = i;  // stable within a member
+    return QGCM_OK;
+}
 
 int qgcm_group_member_cpus(const qgcm_group *g, int member) {
     return g && member >= 0 && member < (int)g->m.size() ? g->m[member].ncpus : QGCM_E_ARG;

@@ -249,29 +249,7 @@ bool key_ok(qgcm_ctx *ctx, uint32_t k) {
 
 }  // namespace
 
-int qgcm::ctx_device(const qgcm_ctx *ctx) { return ctx->device; }
 bool qgcm::ctx_one_kernel(const qgcm_ctx *ctx) { return ctx->one_kernel; }
-
-int qgcm::run_one_descs(qgcm_ctx *ctx, bool seal, uint8_t *arena, const qgcm_desc *descs, uint32_t n,
-                        const uint8_t *nonces, uint32_t aad_len, uint8_t *status, hipStream_t s,
-                        uint8_t *done) {
-    if (!ctx || n == 0 || n > kOneBatchMax || !arena || !descs || aad_len > 4 || ((uintptr_t)arena & 15) ||
-        (nonces && ((uintptr_t)nonces & 3)))
-        return QGCM_E_ARG;
-    if (hipSetDevice(ctx->device) != hipSuccess) return QGCM_E_HIP;
-    Batch b = base_batch(ctx);
-    b.arena = arena;
-    b.descs = descs;
-    b.nonces = seal ? nonces : nullptr;
-    b.status = status;
-    b.n = n;
-    b.aad_len = aad_len;
-    b.done = done;
-    if (launch_one(seal, b, s) != hipSuccess) return QGCM_E_HIP;
-    ctx->count(QGCM_KERNEL_ONE);
-    return QGCM_OK;
-}
-bool qgcm::ctx_key_ready(qgcm_ctx *ctx, uint32_t key_idx) { return key_ok(ctx, key_idx); }
 
 namespace {
 
@@ -615,6 +593,10 @@ int qgcm_set_keys(qgcm_ctx *ctx, uint32_t first_idx, uint32_t count, const uint8
     uint8_t *d_keys = nullptr;
     if (hipMalloc(&d_keys, (size_t)count * 32) != hipSuccess) return QGCM_E_NOMEM;
     hipStream_t s = nullptr;
+    // a running resident instance holds key tables (and keystreams computed ahead, key-valid bytes) in
+    // its caches: end it BEFORE the tables change and start no new one until the new keys are published
+    Resident *res = ctx->res.load(std::memory_order_acquire);
+    (void)resident_pause(res);  // a failure marks the resident path broken: calls take the launch path
     int rc = QGCM_OK;
     if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess ||
         hipMemcpyAsync(d_keys, keys, (size_t)count * 32, hipMemcpyHostToDevice, s) != hipSuccess ||
@@ -629,9 +611,7 @@ int qgcm_set_keys(qgcm_ctx *ctx, uint32_t first_idx, uint32_t count, const uint8
         std::lock_guard<std::mutex> g(ctx->key_mu);
         for (uint32_t i = 0; i < count; ++i) __atomic_store_n(&ctx->key_set[first_idx + i], (uint8_t)1, __ATOMIC_RELEASE);
     }
-    // a running resident instance may hold the old key tables (and key-valid bytes) in its caches:
-    // end it; the next per-packet call starts a fresh one
-    if (rc == QGCM_OK && resident_quiesce(ctx->res.load(std::memory_order_acquire)) != QGCM_OK) rc = QGCM_E_HIP;
+    resident_resume(res);  // the next per-packet call starts a fresh instance
     return rc;
 }
 
@@ -1276,9 +1256,9 @@ int qgcm_resident_stop(qgcm_ctx *ctx) {
 
 int qgcm_resident_stats(const qgcm_ctx *ctx, uint64_t *out, int n) {
     if (!ctx || n < 0 || (n && !out)) return -1;
-    uint64_t v[5];
+    uint64_t v[kResStats];
     resident_stats(ctx->res.load(std::memory_order_acquire), v);
-    const int m = n < 5 ? n : 5;
+    const int m = n < kResStats ? n : kResStats;
     for (int i = 0; i < m; ++i) out[i] = v[i];
     return m;
 }

@@ -74,10 +74,11 @@ struct Resident {
         std::atomic<int32_t> spinners{0};
     };
     std::unique_ptr<WorkerCounts[]> wc;
-    std::mutex launch_mu;
+    std::mutex launch_mu;  // held across a launch, and by resident_pause until resident_resume
     std::atomic<uint32_t> gen{0};  // generation of the current (or last) instance; 0 = never launched
     std::atomic<bool> broken{false};
     std::atomic<uint64_t> launches{0};
+    uint64_t fail_after = ~0ull;  // QGCM_RESIDENT_FAIL_AFTER: test hook, launches after which relaunch fails
     // callers that stop spinning sleep on a futex; one completion thread watches their done words
     uint64_t spin_ns = 20000;                           // QGCM_RESIDENT_SPIN_US
     int32_t max_spinners = 8;  // QGCM_RESIDENT_SPINNERS (default: half the CPU share), spread over workers
@@ -122,7 +123,12 @@ int cpu_share() {
 // Launches instance g + 1 if instance g (0: none yet) has ended and nobody has launched since.
 int relaunch(Resident *r, uint32_t g) {
     std::lock_guard<std::mutex> lk(r->launch_mu);
+    if (r->broken.load(std::memory_order_acquire)) return QGCM_E_HIP;  // callers take the launch path now
     if (r->gen.load(std::memory_order_acquire) != g) return QGCM_OK;  // another caller did it
+    if (r->launches.load(std::memory_order_relaxed) >= r->fail_after) {  // the test hook's injected failure
+        r->broken = true;
+        return QGCM_E_HIP;
+    }
     if (hipSetDevice(r->device) != hipSuccess) return QGCM_E_HIP;
     // instance g has written `over` (its last worker is leaving): wait for the launch to retire
     if (g != 0 && hipStreamSynchronize(r->stream) != hipSuccess) {
@@ -172,7 +178,7 @@ void waker_loop(Resident *r) {
                 futex(&r->wake[s], FUTEX_WAKE_PRIVATE, 1, nullptr);
         }
         const uint32_t g = r->gen.load(std::memory_order_acquire);
-        if (instance_over(r, g)) relaunch(r, g);
+        if (!r->broken.load(std::memory_order_acquire) && instance_over(r, g)) relaunch(r, g);
         sched_yield();  // hand the CPU to a runnable caller when the job's CPUs are all busy
     }
 }
@@ -252,6 +258,7 @@ Resident *resident_create(int device, const Batch &base, int num_cus) {
     r->max_spinners = (int32_t)env_u64("QGCM_RESIDENT_SPINNERS", (uint64_t)std::max(1, cpu_share() / 2));
     r->idle_ticks = env_u64("QGCM_RESIDENT_IDLE_US", 2000) * 100;  // s_memrealtime: 100 MHz
     r->life_ticks = env_u64("QGCM_RESIDENT_LIFE_US", 8000) * 100;
+    r->fail_after = env_u64("QGCM_RESIDENT_FAIL_AFTER", ~0ull);
     // host region: done, over, then the result slots; device region: the stop words (a 64-B line per
     // worker), the request records, then the request slots
     const size_t o_over = (4ull * r->S + 63) & ~63ull, o_hits = o_over + 64;
@@ -297,10 +304,9 @@ Resident *resident_create(int device, const Batch &base, int num_cus) {
     return r.release();
 }
 
-// Ends the running instance (if any) after it has served what is pending; the next call relaunches.
-int resident_quiesce(Resident *r) {
-    if (!r) return QGCM_OK;
-    std::lock_guard<std::mutex> lk(r->launch_mu);
+// Ends the running instance (if any) after it has served what is pending (launch_mu held); the next call
+// relaunches.
+static int quiesce_locked(Resident *r) {
     const uint32_t g = r->gen.load(std::memory_order_acquire);
     if (g == 0) return QGCM_OK;
     for (uint32_t w = 0; w < r->W; ++w) __atomic_store_n(&r->stop[16 * w], 1u, __ATOMIC_RELEASE);
@@ -313,6 +319,24 @@ int resident_quiesce(Resident *r) {
         return QGCM_E_HIP;
     }
     return QGCM_OK;
+}
+
+int resident_quiesce(Resident *r) {
+    if (!r) return QGCM_OK;
+    std::lock_guard<std::mutex> lk(r->launch_mu);
+    return quiesce_locked(r);
+}
+
+// qgcm_set_keys: ends the running instance and keeps the next one from starting until resident_resume, so
+// no request is served from key tables (or keystreams computed ahead) cached across the key change.
+int resident_pause(Resident *r) {
+    if (!r) return QGCM_OK;
+    r->launch_mu.lock();
+    return quiesce_locked(r);
+}
+
+void resident_resume(Resident *r) {
+    if (r) r->launch_mu.unlock();
 }
 
 void resident_destroy(Resident *r) {
@@ -335,7 +359,7 @@ int resident_workers_running(const Resident *r) {
     return instance_over(r, g) ? 0 : (int)r->W;
 }
 
-void resident_stats(const Resident *r, uint64_t out[5]) {
+void resident_stats(const Resident *r, uint64_t out[kResStats]) {
     uint64_t served = 0, hits = 0;
     for (uint32_t w = 0; r && w < r->W; ++w) {
         served += r->wc[w].served.load(std::memory_order_relaxed);
@@ -346,7 +370,35 @@ void resident_stats(const Resident *r, uint64_t out[5]) {
     out[2] = r ? r->W * (uint64_t)r->P : 0;
     out[3] = (uint64_t)resident_workers_running(r);
     out[4] = hits;
+    int64_t spinning = 0;
+    for (uint32_t w = 0; r && w < r->W; ++w) spinning += r->wc[w].spinners.load(std::memory_order_relaxed);
+    out[5] = r ? r->sleepers.load(std::memory_order_relaxed) : 0;
+    out[6] = (uint64_t)std::max<int64_t>(0, spinning);
+    out[7] = r && r->broken.load() ? 1 : 0;
 }
+
+namespace {
+// A caller's waiting state: spinning (counted per worker) or asleep (want[s] set, counted in sleepers).
+// finish() undoes both; the destructor calls it on every early return (timeout, failed relaunch), so the
+// completion thread does not keep watching for a caller that has left.
+struct WaitState {
+    Resident *r;
+    uint32_t s, w;
+    bool spinning = false, asleep = false;
+    void finish() {
+        if (asleep) {
+            r->want[s].store(0, std::memory_order_relaxed);
+            r->sleepers.fetch_sub(1);
+            asleep = false;
+        }
+        if (spinning) {
+            r->wc[w].spinners.fetch_sub(1, std::memory_order_relaxed);
+            spinning = false;
+        }
+    }
+    ~WaitState() { finish(); }
+};
+}  // namespace
 
 long resident_call(Resident *r, bool seal, uint32_t key, uint8_t *data, long len, const uint8_t *aad,
                    uint32_t aad_len, const uint8_t *nonce) {
@@ -423,14 +475,14 @@ long resident_call(Resident *r, bool seal, uint32_t key, uint8_t *data, long len
     if (instance_over(r, g) && relaunch(r, g) != QGCM_OK) return -1;  // broken: the slot stays taken
     uint32_t v = 0;
     const auto t0 = std::chrono::steady_clock::now();
-    bool asleep = false;
-    bool spinning = r->wc[w].spinners.fetch_add(1, std::memory_order_relaxed) < r->max_spin_w;
-    if (!spinning) r->wc[w].spinners.fetch_sub(1, std::memory_order_relaxed);
-    const uint64_t spin_ns = spinning ? r->spin_ns : 0;
+    WaitState ws{r, s, w};
+    ws.spinning = r->wc[w].spinners.fetch_add(1, std::memory_order_relaxed) < r->max_spin_w;
+    if (!ws.spinning) r->wc[w].spinners.fetch_sub(1, std::memory_order_relaxed);
+    const uint64_t spin_ns = ws.spinning ? r->spin_ns : 0;
     for (uint32_t spins = 0;; ++spins) {
         v = __atomic_load_n(&r->done[s], __ATOMIC_ACQUIRE);
         if ((v >> 1) == q) break;
-        if ((spins & 63) == 63 || asleep || spin_ns == 0) {
+        if ((spins & 63) == 63 || ws.asleep || spin_ns == 0) {
             g = r->gen.load(std::memory_order_acquire);
             // the instance ended with this request still pending: launch the next one
             if (instance_over(r, g) && relaunch(r, g) != QGCM_OK) return -1;  // broken: the slot stays taken
@@ -441,10 +493,10 @@ long resident_call(Resident *r, bool seal, uint32_t key, uint8_t *data, long len
             }
             // past the spin budget: sleep until the completion thread sees the verdict (with many more
             // callers than CPUs, spinning ones would take the CPUs the posting ones need)
-            if (!asleep && (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(waited).count() >= spin_ns) {
-                if (spinning) {
+            if (!ws.asleep && (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(waited).count() >= spin_ns) {
+                if (ws.spinning) {
                     r->wc[w].spinners.fetch_sub(1, std::memory_order_relaxed);
-                    spinning = false;
+                    ws.spinning = false;
                 }
                 if (!r->waker.joinable()) {
                     std::lock_guard<std::mutex> lk(r->waker_mu);
@@ -453,22 +505,18 @@ long resident_call(Resident *r, bool seal, uint32_t key, uint8_t *data, long len
                 r->wake[s].store(0, std::memory_order_relaxed);
                 r->want[s].store(q, std::memory_order_release);
                 if (r->sleepers.fetch_add(1) == 0) futex(&r->sleepers, FUTEX_WAKE_PRIVATE, 1, nullptr);
-                asleep = true;
+                ws.asleep = true;
                 continue;  // re-check done before the first wait
             }
         }
-        if (asleep) {
+        if (ws.asleep) {
             const struct timespec ts = {0, 200 * 1000};
             futex(&r->wake[s], FUTEX_WAIT_PRIVATE, 0, &ts);
         } else {
             __builtin_ia32_pause();
         }
     }
-    if (asleep) {
-        r->want[s].store(0, std::memory_order_relaxed);
-        r->sleepers.fetch_sub(1);
-    }
-    if (spinning) r->wc[w].spinners.fetch_sub(1, std::memory_order_relaxed);
+    ws.finish();  // before the slot is released: its next holder may set want[s]
     r->wc[w].served.fetch_add(1, std::memory_order_relaxed);
     const uint8_t *res = r->out + (size_t)s * kResSlotBytes;
     if (seal) {

@@ -113,6 +113,27 @@ class Group:
 
         return _lib.check(_lib.lib().qgcm_group_member_cpus(self.handle, m), "qgcm_group_member_cpus")
 
+    def last_path(self, m: int) -> str:
+        """How member m moved its records in the last seal_host / open_host call: "copy" (host gather and
+        scatter through pinned staging), "zerocopy" (its GPU gathers over PCIe) or "dma" (whole runs of
+        adjacent records, one DMA each way)."""
+        from . import _lib
+
+        code = _lib.check(_lib.lib().qgcm_group_last_path(self.handle, m), "qgcm_group_last_path")
+        return ("copy", "zerocopy", "dma")[code]
+
+    def order(self, key_idx) -> tuple[np.ndarray, np.ndarray]:
+        """qgcm_group_order: the input indices member by member (stable) and each member's count -- the
+        layout in which a keyed batch takes the DMA-run path."""
+        from . import _lib
+
+        k = np.ascontiguousarray(key_idx, dtype=np.uint32)
+        order = np.empty(len(k), np.uint32)
+        counts = np.empty(len(self.devices), np.uint32)
+        _lib.check(_lib.lib().qgcm_group_order(self.handle, k.ctypes.data, len(k), order.ctypes.data,
+                                               counts.ctypes.data), "qgcm_group_order")
+        return order, counts
+
     def last_zerocopy(self) -> bool:
         """True if the last seal_host / open_host call ran the zero-copy path (pinned arena)."""
         from . import _lib

@@ -10,7 +10,7 @@
  *   TestGPUAESEdges   the shim's guards: no room for tag/nonce (never reaches C), empty payload,
  *                     Decrypt of 0/5/11/12/27 bytes (-> errOpen before C below 28; libqgcm also
  *                     returns -1 and leaves the bytes untouched when called), tamper -> zeroed plaintext
- *   TestGPUAESCoalesced  16 threads x 200 packets through qgcm_coalescer_seal/open with 4-B AAD
+ *   TestGPUAESConcurrent 16 threads x 200 packets through one key with qgcm_seal_one/open_one, 4-B AAD
  *   TestGPUGroup      NewGPUGroup + NewGPUAES: key installed on the owning member only, calls on it
  *   TestCreateError   qgcm_create on a device that does not exist: NULL + a message (cError)
  * Usage: go_replay [TestName ...] (default: all).  Prints "--- PASS: Name" per test.
@@ -113,12 +113,12 @@ static void TestGPUAESEdges(qgcm_ctx *ctx) {
 }
 
 struct worker {
-    qgcm_coalescer *co;
+    qgcm_ctx *ctx;
     const uint8_t *key;
     int w, ok;
 };
 
-static void *coalesced_worker(void *p) {
+static void *concurrent_worker(void *p) {
     struct worker *a = p;
     uint8_t buf[1472], plain[1472];
     const uint8_t ip[4] = {10, 99, 0, (uint8_t)a->w};
@@ -126,35 +126,31 @@ static void *coalesced_worker(void *p) {
     for (int i = 0; i < 200 && a->ok; ++i) {
         const long l = (a->w * 131 + i * 17) % 1433;
         for (long j = 0; j < l; ++j) plain[j] = buf[4 + j] = (uint8_t)(a->w + i + j);
-        const long n = qgcm_coalescer_seal(a->co, 2, buf + 4, l, ip, 4);
+        const long n = qgcm_seal_one(a->ctx, 2, buf + 4, l, ip, 4, NULL);
         if (n != l + 28 || !matches_oracle(a->key, plain, l, ip, 4, buf + 4)) a->ok = 0;
-        const long m = qgcm_coalescer_open(a->co, 2, buf + 4, n, ip, 4);
+        const long m = qgcm_open_one(a->ctx, 2, buf + 4, n, ip, 4);
         if (m != l || memcmp(buf + 4, plain, (size_t)l)) a->ok = 0;
     }
     return NULL;
 }
 
-static void TestGPUAESCoalesced(qgcm_ctx *ctx) {
+static void TestGPUAESConcurrent(qgcm_ctx *ctx) {
     uint8_t salt[32], key[32];
     for (int i = 0; i < 32; ++i) salt[i] = (uint8_t)(255 - i);
     CHECK(install_key(ctx, 2, salt, key) == QGCM_OK);
-    char err[QGCM_ERRLEN];
-    qgcm_coalescer *co = qgcm_coalescer_create(ctx, 256, 100, 1472, 4, err, sizeof err); /* EnableCoalescer */
-    CHECK(co != NULL);
     pthread_t th[16];
     struct worker a[16];
     for (int w = 0; w < 16; ++w) {
-        a[w] = (struct worker){co, key, w, 0};
-        pthread_create(&th[w], NULL, coalesced_worker, &a[w]);
+        a[w] = (struct worker){ctx, key, w, 0};
+        pthread_create(&th[w], NULL, concurrent_worker, &a[w]);
     }
     int ok = 1;
     for (int w = 0; w < 16; ++w) {
         pthread_join(th[w], NULL);
         ok &= a[w].ok;
     }
-    qgcm_coalescer_destroy(co);
     CHECK(ok);
-    printf("--- PASS: TestGPUAESCoalesced\n");
+    printf("--- PASS: TestGPUAESConcurrent\n");
 }
 
 static void TestGPUGroup(void) {
@@ -200,7 +196,7 @@ int main(int argc, char **argv) {
     char err[QGCM_ERRLEN];
     qgcm_ctx *ctx = NULL;
     if (want(argc, argv, "TestGPUAES") || want(argc, argv, "TestGPUAESEdges") ||
-        want(argc, argv, "TestGPUAESCoalesced")) {
+        want(argc, argv, "TestGPUAESConcurrent")) {
         ctx = qgcm_create(0, 64, err, sizeof err); /* NewGPUContext(0, 64) */
         if (!ctx) {
             fprintf(stderr, "qgcm_create: %s\n", err);
@@ -209,7 +205,7 @@ int main(int argc, char **argv) {
     }
     if (want(argc, argv, "TestGPUAES")) TestGPUAES(ctx);
     if (want(argc, argv, "TestGPUAESEdges")) TestGPUAESEdges(ctx);
-    if (want(argc, argv, "TestGPUAESCoalesced")) TestGPUAESCoalesced(ctx);
+    if (want(argc, argv, "TestGPUAESConcurrent")) TestGPUAESConcurrent(ctx);
     if (want(argc, argv, "TestGPUGroup")) TestGPUGroup();
     if (want(argc, argv, "TestCreateError")) TestCreateError();
     if (ctx) qgcm_destroy(ctx);

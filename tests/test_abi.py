@@ -141,10 +141,6 @@ def test_null_and_bad_args_rejected():
     assert L.qgcm_open_one(None, 0, None, 0, None, 0) == -1
     assert L.qgcm_strerror(_lib.QGCM_E_AUTH) == b"message authentication failed"
     err = C.create_string_buffer(_lib.ERRLEN)
-    assert not L.qgcm_coalescer_create(None, 64, 100, 1472, 4, err, _lib.ERRLEN) and err.value
-    assert L.qgcm_coalescer_seal(None, 0, None, 0, None, 0) == -1
-    assert L.qgcm_coalescer_open(None, 0, None, 0, None, 0) == -1
-    L.qgcm_coalescer_destroy(None)
     assert not L.qgcm_host_alloc(0)
 
 

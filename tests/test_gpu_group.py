@@ -45,15 +45,22 @@ def host_buffer(nbytes: int, pinned: bool):
     return arr, arr.ctypes.data, lambda: None
 
 
-@pytest.mark.parametrize("G,pinned,threads,zc", [(2, True, "4", "1"), (3, False, "7", "1"), (1, True, "1", "1"),
-                                                  (2, True, "3", "0")])
-def test_group_keyed_host_batch_vs_oracle(torch, G, pinned, threads, zc, monkeypatch):
+@pytest.mark.parametrize("G,pinned,threads,zc,dma,grouped", [
+    (2, True, "4", "1", "0", False), (3, False, "7", "1", "0", False), (1, True, "1", "1", "0", False),
+    (2, True, "3", "0", "0", False),
+    (1, True, "4", "1", "1", False), (2, True, "4", "1", "1", True), (3, False, "4", "1", "1", True),
+    (2, True, "4", "1", "1", False)])
+def test_group_keyed_host_batch_vs_oracle(torch, G, pinned, threads, zc, dma, grouped, monkeypatch):
     """threads: QGCM_GROUP_THREADS, the gather/scatter copy threads per member; zc: QGCM_GROUP_ZEROCOPY
-    (pinned arenas take the GPU gather/scatter path unless it is 0; pageable ones always the copy path)."""
+    (pinned arenas take the GPU gather/scatter path unless it is 0; pageable ones always the copy path);
+    dma: QGCM_GROUP_DMA -- a member whose packets form long runs of adjacent records (one member, or the
+    batch laid out member by member in qgcm_group_order's order: `grouped`) copies whole runs by DMA;
+    interleaved members fall back to the paths above."""
     from quantum_amd import shard
 
     monkeypatch.setenv("QGCM_GROUP_THREADS", threads)
     monkeypatch.setenv("QGCM_GROUP_ZEROCOPY", zc)
+    monkeypatch.setenv("QGCM_GROUP_DMA", dma)
     grp = shard.Group([0] * G, max_keys=256)
     try:
         rng = random.Random(0x6A0 + G)
@@ -66,6 +73,13 @@ def test_group_keyed_host_batch_vs_oracle(torch, G, pinned, threads, zc, monkeyp
         n = 3000
         kidx = [200 if i % 97 == 5 else rng.randrange(nkeys) for i in range(n)]  # key 200: no member has it
         lens = [rng.choice([0, 1, 15, 16, 17, 1350, 1433, 4081]) if i % 4 else rng.randint(0, 3000) for i in range(n)]
+        if grouped:  # the batch assembled member by member (qgcm_group_order)
+            order, counts = grp.order(kidx)
+            assert counts.tolist() == [int((shard.key_shard(np.array(kidx), G) == m).sum()) for m in range(G)]
+            assert np.array_equal(np.concatenate(shard.partition_by_key(kidx, G)), order)
+            kidx = [kidx[i] for i in order]
+            lens = [lens[i] for i in order]
+        want_path = "dma" if dma == "1" and (G == 1 or grouped) else ("zerocopy" if pinned and zc == "1" else "copy")
         offs, pos = [], 0
         for i, L in enumerate(lens):  # 4-B and 16-B aligned slots mixed
             offs.append(pos)
@@ -89,7 +103,8 @@ def test_group_keyed_host_batch_vs_oracle(torch, G, pinned, threads, zc, monkeyp
             status = np.full(n, 7, dtype=np.uint8)
             unset = sum(k >= nkeys for k in kidx)
             bad = grp.seal_host(aptr, descs, n, nonces.ctypes.data, 4, status.ctypes.data)
-            assert grp.last_zerocopy() == (pinned and zc == "1")
+            assert [grp.last_path(m) for m in range(G)] == [want_path] * G
+            assert grp.last_zerocopy() == (want_path == "zerocopy")
             assert bad == unset
             assert status.tolist() == [0 if k >= nkeys else 1 for k in kidx]
             assert np.array_equal(arena, ref)  # every slot in place, input order kept
@@ -101,7 +116,7 @@ def test_group_keyed_host_batch_vs_oracle(torch, G, pinned, threads, zc, monkeyp
             d_open = shard.host_descs(offs, [L + 28 for L in lens], kidx)
             status[:] = 7
             bad = grp.open_host(aptr, d_open, n, 4, status.ctypes.data)
-            assert grp.last_zerocopy() == (pinned and zc == "1")
+            assert [grp.last_path(m) for m in range(G)] == [want_path] * G
             assert bad == unset + len(tampered)
             for i, L in enumerate(lens):
                 o = offs[i]
@@ -116,6 +131,64 @@ def test_group_keyed_host_batch_vs_oracle(torch, G, pinned, threads, zc, monkeyp
             free_n()
         finally:
             free()
+    finally:
+        grp.close()
+
+
+def test_group_dma_runs_many_chunks_vs_oracle(torch):
+    """DMA-run path over more 64-MiB chunks than staging slots (slot reuse), two members on device 0 with
+    the batch laid out member by member: 2^19 packets, the first half of 1184..1440 B in 1472-B
+    Payload.Raw slots (gaps of up to 256 B inside a run; every 1000th slot 1 KiB further on, which breaks
+    the run), the second half of U{0..2000} B in 16-B packed slots; sealed against the oracle, then opened
+    back and every byte of the arena checked."""
+    from quantum_amd import shard
+
+    G, n = 2, 1 << 19  # ~660 MB of records: 5 chunks per member, more than its 4 staging slots
+    grp = shard.Group([0] * G, max_keys=64)
+    try:
+        rng = np.random.default_rng(0x6A05)
+        keys = rng.integers(0, 256, 32 * 16, dtype=np.uint8).tobytes()
+        grp.set_keys(0, keys)
+        kidx = rng.integers(0, 16, n).astype(np.uint32)
+        order, _ = grp.order(kidx)
+        kidx = kidx[order]
+        lens = rng.integers(0, 2001, n).astype(np.uint32)
+        lens[: n // 2] = 1184 + lens[: n // 2] % 257  # Raw slots: 4 + L + 28 <= 1472, gaps <= 256 B
+        rec = ((4 + lens.astype(np.uint64) + 28 + 15) & ~np.uint64(15))
+        offs = np.zeros(n, np.uint64)
+        # every 1000th slot starts 1 KiB further on: the runs break there
+        offs[: n // 2] = np.arange(n // 2, dtype=np.uint64) * np.uint64(1472) + \
+            np.uint64(1024) * (np.arange(n // 2, dtype=np.uint64) // np.uint64(1000))
+        base = offs[n // 2 - 1] + np.uint64(1472)
+        offs[n // 2:] = base + np.concatenate([[0], np.cumsum(rec[n // 2:])[:-1]]).astype(np.uint64)
+        size = int(offs[-1] + rec[-1]) + 64
+        arena, aptr, free = host_buffer(size, True)
+        nonces, nptr, free_n = host_buffer(12 * n, True)
+        try:
+            arena[:] = rng.integers(0, 256, size, dtype=np.uint8)
+            idx = offs.astype(np.int64)[:, None] + np.arange(4)
+            arena[idx] = np.frombuffer(AAD, np.uint8)
+            nonces[:] = rng.integers(0, 256, 12 * n, dtype=np.uint8)
+            plain = arena.copy()
+            ref = plain.copy()
+            O.aesgo_seal_descs(keys, ref, offs, lens, kidx, nonces, 4, 16)
+            status = np.zeros(n, np.uint8)
+            assert grp.seal_host(aptr, shard.host_descs(offs, lens, kidx), n, nptr, 4, status.ctypes.data) == 0
+            assert [grp.last_path(m) for m in range(G)] == ["dma", "dma"]
+            assert bool((status == 1).all()) and np.array_equal(arena, ref)
+            status[:] = 0
+            assert grp.open_host(aptr, shard.host_descs(offs, lens + 28, kidx), n, 4, status.ctypes.data) == 0
+            assert bool((status == 1).all())
+            pay = offs.astype(np.int64)
+            for i in range(0, n, 997):  # sampled plaintext restored (the full arena below)
+                assert np.array_equal(arena[pay[i]:pay[i] + 4 + lens[i]], plain[pay[i]:pay[i] + 4 + lens[i]])
+            tail = (offs.astype(np.int64) + 4 + lens.astype(np.int64))[:, None] + np.arange(28)
+            restored = arena.copy()
+            restored[tail] = plain[tail]  # Open leaves tag || nonce in the slot
+            assert np.array_equal(restored, plain)
+        finally:
+            free()
+            free_n()
     finally:
         grp.close()
 

@@ -421,3 +421,56 @@ def test_keystream_ahead_vs_oracle(torch, ahead, monkeypatch):
             assert hits == 0
     finally:
         ctx.close()
+
+
+def test_failed_relaunch_leaves_no_waiters(torch):
+    """A relaunch that fails (injected with the QGCM_RESIDENT_FAIL_AFTER test hook: every launch after the
+    first fails) marks the resident path broken: the callers whose requests were posted return -1, every
+    later call takes the launch path (bit-exact with the oracle), no caller stays counted asleep or
+    spinning, and no further instance is launched -- the completion thread stops relaunching."""
+    from quantum_amd.crypto import AES
+
+    ctx = make_ctx(QGCM_RESIDENT_FAIL_AFTER=1, QGCM_RESIDENT_LIFE_US=300, QGCM_RESIDENT_IDLE_US=100,
+                   QGCM_RESIDENT_SPIN_US=0)
+    try:
+        key = bytes(range(32))
+        ctx.set_key(0, key)
+        results, errors = [], []
+
+        def caller(t):
+            aes = AES(key, ctx=ctx)
+            rng = random.Random(t)
+            end = time.time() + 1.0
+            while time.time() < end:
+                L = rng.choice([64, 1350, 4000])
+                pt = rng.randbytes(L)
+                nonce = rng.randbytes(12)
+                data = bytearray(pt + bytes(28))
+                n, err = aes.Encrypt(data, L, AAD, nonce=nonce)
+                if err is not None:
+                    results.append("failed")
+                    continue
+                want = bytearray(pt + bytes(28))
+                O.aesgo_encrypt(key, want, L, AAD, nonce)
+                if n != L + 28 or bytes(data) != bytes(want):
+                    errors.append(L)
+                results.append("ok")
+
+        th = [threading.Thread(target=caller, args=(t,)) for t in range(8)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        assert not errors
+        st = ctx.resident_stats()
+        assert st["broken"] == 1 and st["launches"] == 1
+        assert st["sleepers"] == 0 and st["spinners"] == 0
+        assert results.count("ok") > 100  # the launch path served the calls after the failure
+        time.sleep(0.05)
+        st2 = ctx.resident_stats()
+        assert st2["launches"] == 1 and st2["sleepers"] == 0
+        before = ctx.launch_counts()["one"]
+        assert roundtrip(AES(key, ctx=ctx), key, 1350, random.Random(9)) is None
+        assert ctx.launch_counts()["one"] == before + 2
+    finally:
+        ctx.close()
