@@ -59,7 +59,7 @@ def open_(L, ctx):
     assert L.qgcm_open_batch(ctx, arena.data_ptr(), d_open.data_ptr(), N, 4, status.data_ptr(), stream) == 0
 
 
-ref = None
+ref = ref_open = None
 for path, (L, ctx) in libs.items():
     arena.copy_(plain)
     seal(L, ctx)
@@ -68,8 +68,12 @@ for path, (L, ctx) in libs.items():
         ref = arena.clone()
     same = bool(torch.equal(arena, ref))
     open_(L, ctx)
-    rt = int(status.sum()) == N and bool(torch.equal(arena[:64], plain[:64]))
-    print(f"{path}: status_ok={ok} sealed bytes same as first: {same}; round trip: {rt}", flush=True)
+    if ref_open is None:
+        ref_open = arena.clone()
+    rt = int(status.sum()) == N and bool(torch.equal(arena[:64], plain[:64])) and bool(torch.equal(arena, ref_open))
+    print(f"{path}: status_ok={ok} sealed bytes same as first: {same}; round trip (whole arena as first): {rt}",
+          flush=True)
+    assert ok and same and rt, f"{path} differs from {next(iter(libs))}"
 payload = int(lens.sum())
 res = {p: ([], []) for p in libs}
 for r in range(rounds + 1):
