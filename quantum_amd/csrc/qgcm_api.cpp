@@ -1167,16 +1167,19 @@ static int run_snappy(qgcm_ctx *ctx, bool compress, uint8_t *d_arena, uint64_t s
     a.off_in = tab;
     a.off_out = a.off_in + a16(max_in + 24);  // + the 16-B chunks' overhang and stage_in's slack dwords
     a.off_sink = a.off_out + a16((compress ? (uint32_t)qgcm_snappy_max_compressed_length(max_in) : limit) + 8);
-    a.wave_bytes = a.off_sink + 256;
-    int waves = 4;
+    // the encoder: four packets per wave (QGCM_SNAPPY_GROUP=0: one wave per packet, for A/Bs)
+    const bool group = compress && env_int("QGCM_SNAPPY_GROUP", 1) != 0;
+    a.wave_bytes = group ? kSnapGroup * a.off_sink : a.off_sink + 256;
+    const uint32_t per_wave = group ? kSnapGroup : 1;
+    int waves = group ? 1 : 4;
     while (waves > 1 && (size_t)waves * a.wave_bytes > 64u * 1024u) --waves;
     int per_cu = (int)((160u * 1024u) / ((uint32_t)waves * a.wave_bytes));
     per_cu = std::max(1, std::min(per_cu, 8));
-    const uint64_t need = (n + (uint64_t)waves - 1) / waves;
+    const uint64_t need = (n + (uint64_t)waves * per_wave - 1) / ((uint64_t)waves * per_wave);
     const int grid = (int)std::min<uint64_t>(need, (uint64_t)ctx->num_cus * per_cu);
     if (hipSetDevice(ctx->device) != hipSuccess) return QGCM_E_HIP;
     ctx->count(compress ? QGCM_KERNEL_SNAPPY_ENC : QGCM_KERNEL_SNAPPY_DEC);
-    return hip_fail(launch_snappy(compress, a, waves, grid, s));
+    return hip_fail(launch_snappy(compress, a, waves, grid, s, group));
 }
 
 int qgcm_snappy_compress_batch(qgcm_ctx *ctx, uint8_t *d_arena, uint64_t stride, uint32_t n, uint32_t *d_lens,

@@ -261,6 +261,208 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) s
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Group encoder: FOUR packets per wave, one per 16-lane group (QGCM_SNAPPY_GROUP, the default since
+// round 4).  The one-wave-per-packet encoder above is bound by the CU's single scalar unit: every
+// probe's control flow and wave-uniform values run there, ~3 K scalar instructions per 1350-B packet
+// (DESIGN.md 4.6).  Here a group's state lives in VGPRs (the same value in its 16 lanes), each lane
+// group runs encodeBlock on its own packet, and one instruction stream -- one set of scalar
+// instructions for the loop and its exec masks -- serves four packets.  Groups in different phases
+// (probing / emitting a copy run) diverge under exec masks; packets of a batch tend to move alike.
+// Every group lane stores the same byte to the same LDS address where the wave encoder let one lane
+// store (no exec branch per store).  Match extension compares 4 bytes per lane (64 B per group step);
+// literal copies move 4 bytes per lane.  Per packet: [hash table | staged input | output] in LDS
+// (a.off_in / a.off_out within a region of a.off_sink bytes), four regions per wave.
+constexpr uint32_t kGrp = 4, kGL = 64 / kGrp;
+
+struct GWave {
+    uint8_t *in, *out;
+    uint16_t *tab;
+    uint32_t gl, grp;  // lane within the group, group within the wave
+
+    __device__ __forceinline__ uint32_t load32(uint32_t o) const {
+        const uint32_t *w = reinterpret_cast<const uint32_t *>(in);
+        return __builtin_amdgcn_alignbyte(w[(o >> 2) + 1], w[o >> 2], o & 3);
+    }
+    __device__ __forceinline__ void put(uint32_t o, uint32_t v) const { out[o] = (uint8_t)v; }
+    // out[op..op+len) = in[from..from+len): lane gl moves bytes 4 gl .. 4 gl + 3 of every 64
+    __device__ __forceinline__ void copy_in(uint32_t op, uint32_t from, uint32_t len) const {
+        for (uint32_t j = 4 * gl; j < len; j += 4 * kGL) {
+            const uint32_t v = load32(from + j);
+            const uint32_t k = len - j < 4 ? len - j : 4;
+            out[op + j] = (uint8_t)v;
+            if (k > 1) out[op + j + 1] = (uint8_t)(v >> 8);
+            if (k > 2) out[op + j + 2] = (uint8_t)(v >> 16);
+            if (k > 3) out[op + j + 3] = (uint8_t)(v >> 24);
+        }
+    }
+    __device__ __forceinline__ uint32_t emit_literal(uint32_t op, uint32_t from, uint32_t len) const {
+        const uint32_t n = len - 1;
+        if (n < 60) {
+            put(op, n << 2);
+            op += 1;
+        } else if (n < 256) {
+            put(op, 60u << 2);
+            put(op + 1, n);
+            op += 2;
+        } else {
+            put(op, 61u << 2);
+            put(op + 1, n & 0xff);
+            put(op + 2, n >> 8);
+            op += 3;
+        }
+        copy_in(op, from, len);
+        return op + len;
+    }
+    __device__ __forceinline__ uint32_t copy2(uint32_t op, uint32_t off, uint32_t len) const {
+        put(op, ((len - 1) << 2) | 2);
+        put(op + 1, off & 0xff);
+        put(op + 2, off >> 8);
+        return op + 3;
+    }
+    __device__ __forceinline__ uint32_t emit_copy(uint32_t op, uint32_t off, uint32_t len) const {
+        while (len >= 68) {
+            op = copy2(op, off, 64);
+            len -= 64;
+        }
+        if (len > 64) {
+            op = copy2(op, off, 60);
+            len -= 60;
+        }
+        if (len >= 12 || off >= 2048) return copy2(op, off, len);
+        put(op, ((off >> 8) << 5) | ((len - 4) << 2) | 1);
+        put(op + 1, off & 0xff);
+        return op + 2;
+    }
+    // common run of in[a..) and in[b..), b < n: lane gl compares bytes 4 gl .. 4 gl + 3 of each 64
+    __device__ __forceinline__ uint32_t match_len(uint32_t a, uint32_t b, uint32_t n) const {
+        uint32_t m = 0;
+        for (;;) {
+            const uint32_t rem = n - (b + m);
+            if (rem == 0) return m;
+            const uint32_t k = rem < 4 * kGL ? rem : 4 * kGL;
+            const uint32_t o = 4 * gl;
+            uint32_t x = 0;
+            if (o < k) {
+                x = load32(a + m + o) ^ load32(b + m + o);
+                const uint32_t left = k - o;
+                if (left < 4) x &= 0xffffffffu >> (32 - 8 * left);
+            }
+            const uint64_t d = (__builtin_amdgcn_ballot_w64(x != 0) >> (kGL * grp)) & 0xffffull;
+            if (d) {
+                const uint32_t first = (uint32_t)__builtin_ctzll(d);  // the group's first differing dword
+                const uint32_t xf = __builtin_amdgcn_ds_bpermute((int)((kGL * grp + first) << 2), (int)x);
+                return m + 4 * first + ((uint32_t)__builtin_ctz(xf) >> 3);
+            }
+            m += k;
+        }
+    }
+};
+
+__device__ uint32_t gencode_block(const GWave &w, uint32_t op, uint32_t n, uint32_t bits) {
+    const uint32_t shift = 32 - bits;
+    uint4 *t16 = reinterpret_cast<uint4 *>(w.tab);  // 2 << bits bytes, a multiple of 256
+    for (uint32_t j = w.gl; j < (2u << bits) / 16; j += kGL) t16[j] = uint4{0, 0, 0, 0};
+    wave_lds_sync();
+    const uint32_t s_limit = n - 15;
+    uint32_t next_emit = 0, s = 1, skip = 32;
+    uint32_t cur = w.load32(1), h = hash4(cur, shift);
+    for (;;) {
+        const uint32_t step = skip >> 5, next_s = s + step;
+        if (next_s > s_limit) break;
+        skip += step;
+        uint32_t cand = w.tab[h];
+        w.tab[h] = (uint16_t)s;
+        const uint32_t nv = w.load32(next_s);
+        if (cur != w.load32(cand)) {  // miss: probe further on
+            s = next_s;
+            cur = nv;
+            h = hash4(nv, shift);
+            continue;
+        }
+        op = w.emit_literal(op, next_emit, s - next_emit);
+        bool more;
+        do {  // copies back to back while the position after one starts another
+            const uint32_t base = s;
+            s += 4 + w.match_len(cand + 4, s + 4, n);
+            op = w.emit_copy(op, base - cand, s - base);
+            next_emit = s;
+            if (s >= s_limit) break;
+            w.tab[hash4(w.load32(s - 1), shift)] = (uint16_t)(s - 1);
+            wave_lds_sync();
+            cur = w.load32(s);
+            h = hash4(cur, shift);
+            cand = w.tab[h];
+            w.tab[h] = (uint16_t)s;
+            more = cur == w.load32(cand);
+        } while (more);
+        if (s >= s_limit) break;
+        ++s;
+        skip = 32;
+        cur = w.load32(s);
+        h = hash4(cur, shift);
+    }
+    if (next_emit < n) op = w.emit_literal(op, next_emit, n - next_emit);
+    return op;
+}
+
+__global__ void __launch_bounds__(256) snappy_compress_group_kernel(SnapArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint32_t lane = lane_id(), wv = threadIdx.x >> 6, waves = blockDim.x >> 6;
+    const uint32_t grp = lane / kGL, gl = lane % kGL;
+    uint8_t *base = smem + (wv * kGrp + grp) * a.off_sink;
+    const GWave w{base + a.off_in, base + a.off_out, reinterpret_cast<uint16_t *>(base), gl, grp};
+    const uint32_t step = gridDim.x * waves * kGrp;
+    for (uint32_t p0 = (blockIdx.x * waves + wv) * kGrp; p0 < a.n; p0 += step) {
+        const uint32_t p = p0 + grp;
+        const bool have = p < a.n;
+        const uint32_t len = have ? a.lens[p] : 0u;
+        uint8_t *slot = a.arena + (uint64_t)(have ? p : 0u) * a.stride;
+        bool ok = have && len <= a.max_in;
+        if (ok) {  // slot bytes [4, 4 + len) -> LDS, whole dwords (the slot is 4-B aligned, stride a multiple of 4)
+            const uint32_t *src = reinterpret_cast<const uint32_t *>(slot + 4);
+            uint32_t *d = reinterpret_cast<uint32_t *>(w.in);
+            const uint32_t nw = (len + 3) >> 2;
+            for (uint32_t j = gl; j < nw; j += kGL) d[j] = src[j];
+            if (gl < 2) d[nw + gl] = 0;  // slack read by load32 past the end
+        }
+        wave_lds_sync();
+        uint32_t d = 0;
+        if (ok) {
+            uint32_t op = 0, v = len;  // put_varint
+            while (v >= 0x80) {
+                w.put(op++, (v & 0x7f) | 0x80);
+                v >>= 7;
+            }
+            w.put(op++, v);
+            if (len < 17) {
+                if (len) op = w.emit_literal(op, 0, len);
+            } else {
+                uint32_t bits = 8;
+                while (bits < 14 && (1u << bits) < len) ++bits;
+                op = gencode_block(w, op, len, bits);
+            }
+            d = op;
+            ok = d <= a.limit;
+        }
+        wave_lds_sync();
+        if (ok) {  // LDS [0, d) -> slot bytes [4, 4 + d)
+            uint32_t *dst = reinterpret_cast<uint32_t *>(slot + 4);
+            const uint32_t *srcw = reinterpret_cast<const uint32_t *>(w.out);
+            const uint32_t nw = d >> 2;
+            for (uint32_t j = gl; j < nw; j += kGL) dst[j] = srcw[j];
+            const uint32_t t = d & 3;
+            if (gl < t) slot[4 + 4 * nw + gl] = w.out[4 * nw + gl];
+        }
+        if (have && gl == 0) {
+            if (ok) a.lens[p] = d;
+            if (a.status) a.status[p] = ok ? 1 : 0;
+            if (a.descs) a.descs[p] = qgcm_desc{(uint64_t)p * a.stride, ok ? d : QGCM_MAX_PAYLOAD, a.key_idx};
+        }
+        wave_lds_sync();  // the next packets' staging overwrites these ones' LDS
+    }
+}
+
 // decode.go Decode of in[0..n) into out (at most cap bytes); returns the length or -1
 __device__ int decode(const Wave &w, uint32_t n, uint32_t cap) {
     uint32_t total = 0, ip = 0;
@@ -355,9 +557,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) s
 
 }  // namespace
 
-hipError_t launch_snappy(bool compress, const SnapArgs &a, int waves_per_wg, int grid, hipStream_t s) {
+hipError_t launch_snappy(bool compress, const SnapArgs &a, int waves_per_wg, int grid, hipStream_t s, bool group) {
     const size_t lds = (size_t)waves_per_wg * a.wave_bytes;
-    if (compress)
+    if (compress && group)
+        hipLaunchKernelGGL(snappy_compress_group_kernel, dim3(grid), dim3(64 * waves_per_wg), lds, s, a);
+    else if (compress)
         hipLaunchKernelGGL(snappy_compress_kernel, dim3(grid), dim3(64 * waves_per_wg), lds, s, a);
     else
         hipLaunchKernelGGL(snappy_uncompress_kernel, dim3(grid), dim3(64 * waves_per_wg), lds, s, a);

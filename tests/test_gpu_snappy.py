@@ -80,7 +80,15 @@ def _match(case, comp: bytes) -> bool:
     return hashlib.sha256(comp).hexdigest() == case["out_sha256"]
 
 
-def test_device_encoder_equals_libsnappy_golden(torch, ctx):
+@pytest.fixture(params=["1", "0"], ids=["group_encoder", "wave_encoder"])
+def encoder(request, monkeypatch):
+    """QGCM_SNAPPY_GROUP (read per call): 1 = four packets per wave (the default), 0 = one wave per
+    packet.  Both must give the host encoder's (and libsnappy's) bytes."""
+    monkeypatch.setenv("QGCM_SNAPPY_GROUP", request.param)
+    return request.param
+
+
+def test_device_encoder_equals_libsnappy_golden(torch, ctx, encoder):
     with open(GOLDEN) as f:
         cases = [c for c in json.load(f)["cases"] if c["n"] <= DEV_MAX]
     datas = [SI.make(c["kind"], c["n"]) for c in cases]
@@ -103,7 +111,7 @@ def test_device_encoder_equals_libsnappy_golden(torch, ctx):
         assert bl[i] == len(d) and back[i, 4:4 + len(d)].tobytes() == d
 
 
-def test_device_codec_config5_batch_vs_host(torch, ctx):
+def test_device_codec_config5_batch_vs_host(torch, ctx, encoder):
     """2^14 Payload.Raw slots (stride 1472): config 5's packet shape and a mix of lengths 0..1433
     and contents; device compress == host encoder (whole arena incl. untouched bytes, lengths), then
     device uncompress restores the plaintext arena."""
@@ -136,7 +144,7 @@ def test_device_codec_config5_batch_vs_host(torch, ctx):
     assert np.array_equal(back, plain)
 
 
-def test_device_compress_failures_untouched(torch, ctx):
+def test_device_compress_failures_untouched(torch, ctx, encoder):
     """Longer than max_len, or compressed form over limit: status 0, slot and length untouched."""
     stride = 2048
     payloads = [SI.make("random", 1500), SI.make("line", 1500), SI.make("random", 900), b"", SI.make("zeros", 40)]
