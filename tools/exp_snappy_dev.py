@@ -1,8 +1,11 @@
 """Device snappy codec rate on device-resident slots (config 5's packets: 2^20 x 1350 B, first half
 random, second half a repeated HTTP line, stride 1472): compress, seal, open, uncompress, each timed
-by HIP events; the result is checked against the plaintext arena.
+by HIP events; the sealed arena is checked against tests/golden/config5_digest.json and the result
+against the plaintext arena (bench.extra_config5_resident).  The encoder alternates between the
+four-packets-per-wave kernel (QGCM_SNAPPY_GROUP=1, the default) and one wave per packet (0), in one
+process, `rounds` times each.
 
-    python3 tools/exp_snappy_dev.py [reps] [n]
+    python3 tools/exp_snappy_dev.py [reps] [rounds]
 """
 import json
 import os
@@ -10,18 +13,19 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-import numpy as np  # noqa: E402
-import torch  # noqa: E402
-
 import bench  # noqa: E402
 
 
 def main() -> None:
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
-    n = int(sys.argv[2]) if len(sys.argv) > 2 else 1 << 20
+    rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 2
     key = bench.derive_key(bench.SECRET, bench.SALT)
-    for _ in range(2):
-        print(json.dumps(bench.extra_config5_resident(key, reps, n)), flush=True)
+    for r in range(rounds):
+        for grp in ("1", "0"):
+            os.environ["QGCM_SNAPPY_GROUP"] = grp
+            res = bench.extra_config5_resident(key, reps, verify=(r == 0))
+            print(json.dumps({"snappy_group": int(grp), **res}), flush=True)
+    os.environ.pop("QGCM_SNAPPY_GROUP", None)
 
 
 if __name__ == "__main__":

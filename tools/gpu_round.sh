@@ -3,7 +3,8 @@
 # reference build, and the config-2 profile (trace + PMC).  Every GPU step has its own time limit;
 # the script stops at the first step that faults, aborts or times out (a plain test failure goes on).
 # Usage: bash tools/gpu_round.sh <tag> [steps...]
-#   steps: stests policy snapdev rtests tests smoke bench ab prof pp prof3 exp_res res_trace ahead barreq align (default: tests smoke bench ab prof)
+#   steps: stests policy snapdev rtests tests smoke bench ab prof pp prof3 exp_res res_trace ahead barreq align
+#          r4tests abrealign snapab profsnap (default: tests smoke bench ab prof)
 set -u
 TAG=$1; shift
 STEPS=${*:-"tests smoke bench ab prof"}
@@ -129,6 +130,15 @@ for s in $STEPS; do
         mkdir -p $OUT/pmc_$form && cp -r $OUT/pmc_${form}_*/* $OUT/pmc_$form/ 2>/dev/null
         python3 tools/pmc_config3.py $OUT/pmc_$form > $OUT/traffic_$form.txt 2>&1
       done ;;
+    r4tests)  # the suites round 4 changed
+      timeout -k 10 900 python3 -u -m pytest tests/test_gpu_group.py tests/test_gpu_config5.py tests/test_gpu_snappy.py tests/test_bench_dist.py tests/test_gpu_resident.py -x -v --timeout 300 --timeout-method thread > $OUT/r4_tests.txt 2>&1
+      check r4tests $? ;;
+    abrealign)  # config 3: realigned segmented-kernel stores (side build in abt/realign) vs the product build
+      timeout -k 10 300 python3 tools/ab_libs_desc.py quantum_amd/libqgcm.so abt/realign/libqgcm.so --rounds 9 > $OUT/ab_realign.txt 2>&1
+      check abrealign $? ;;
+    snapab)  # device snappy encoder: four packets per wave vs one wave per packet, interleaved
+      timeout -k 10 300 python3 tools/exp_snappy_dev.py 5 2 > $OUT/snap_ab.jsonl 2> $OUT/snap_ab.err
+      check snapab $? ;;
   esac
 done
 echo all done | tee -a $OUT/steps.txt
