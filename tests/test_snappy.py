@@ -178,8 +178,12 @@ def test_slots_batch_threads():
         comp = bytes(arena[i * stride + 4:i * stride + 4 + lens[i]])
         assert _uncompress(comp, 1433) == plain[i]
     st = (C.c_uint8 * n)()
-    assert _lib.lib().qgcm_snappy_uncompress_slots(C.addressof(buf), stride, n, lens, st, 4) == 0
+    empty = sum(1 for p in plain if not p)  # decode to nothing: dropped (compression.go:37-39)
+    assert _lib.lib().qgcm_snappy_uncompress_slots(C.addressof(buf), stride, n, lens, st, 4) == empty
     for i in range(n):
+        if not plain[i]:
+            assert st[i] == 0 and lens[i] == 1
+            continue
         assert st[i] == 1 and lens[i] == len(plain[i])
         assert bytes(arena[i * stride + 4:i * stride + 4 + lens[i]]) == plain[i]
     del buf
