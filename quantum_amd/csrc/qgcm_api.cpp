@@ -1168,7 +1168,8 @@ static int run_snappy(qgcm_ctx *ctx, bool compress, uint8_t *d_arena, uint64_t s
     a.off_out = a.off_in + a16(max_in + 24);  // + the 16-B chunks' overhang and stage_in's slack dwords
     a.off_sink = a.off_out + a16((compress ? (uint32_t)qgcm_snappy_max_compressed_length(max_in) : limit) + 8);
     // the encoder: four packets per wave (QGCM_SNAPPY_GROUP=0: one wave per packet, for A/Bs)
-    const bool group = compress && env_int("QGCM_SNAPPY_GROUP", 1) != 0;
+    // (packets past ~5 KiB need more LDS than four regions per wave can have: one wave per packet)
+    const bool group = compress && env_int("QGCM_SNAPPY_GROUP", 1) != 0 && kSnapGroup * a.off_sink <= 160u * 1024u;
     a.wave_bytes = group ? kSnapGroup * a.off_sink : a.off_sink + 256;
     const uint32_t per_wave = group ? kSnapGroup : 1;
     int waves = group ? 1 : 4;

@@ -136,6 +136,22 @@ for s in $STEPS; do
     abrealign)  # config 3: realigned segmented-kernel stores (side build in abt/realign) vs the product build
       timeout -k 10 300 python3 tools/ab_libs_desc.py quantum_amd/libqgcm.so abt/realign/libqgcm.so --rounds 9 > $OUT/ab_realign.txt 2>&1
       check abrealign $? ;;
+    pmcrealign)  # config 3 HBM traffic of the segmented kernel: product build vs realigned stores (side build)
+      for lib in quantum_amd abt/realign; do
+        tagl=$(basename $lib)
+        for c in WRITE_SIZE FETCH_SIZE; do
+          timeout -k 10 300 rocprofv3 --pmc $c -d $OUT/pmcr_${tagl}_$c -o $c --output-format csv -- python3 tools/ab_libs_desc.py $lib/libqgcm.so --rounds 1 > $OUT/pmcr_${tagl}_$c.log 2>&1
+          check pmcr_${tagl}_$c $?
+        done
+        mkdir -p $OUT/pmcr_$tagl && cp -r $OUT/pmcr_${tagl}_*/* $OUT/pmcr_$tagl/ 2>/dev/null
+        PMC_PAYLOAD=4751969452 python3 tools/pmc_config3.py $OUT/pmcr_$tagl > $OUT/traffic_realign_$tagl.txt 2>&1
+      done ;;
+    profsnap2)  # device snappy counters, four-packets-per-wave encoder and one wave per packet
+      for g in 1 0; do
+        QGCM_SNAPPY_GROUP=$g bash tools/profile_snappy.sh ${TAG}_g$g > $OUT/profsnap_g$g.log 2>&1
+        check profsnap_g$g $?
+        python3 tools/pmc_kernels.py gpurun_out/prof_snappy_${TAG}_g$g 1048576 snappy_compress snappy_uncompress > $OUT/snappy_pmc_g$g.txt 2>&1
+      done ;;
     snapab)  # device snappy encoder: four packets per wave vs one wave per packet, interleaved
       timeout -k 10 300 python3 tools/exp_snappy_dev.py 5 2 > $OUT/snap_ab.jsonl 2> $OUT/snap_ab.err
       check snapab $? ;;

@@ -15,6 +15,8 @@ import statistics
 import sys
 
 PAYLOAD, N = 4751816686, 1 << 20  # quantum_amd/workloads.py (tools/bench_configs.py config3, bench.py extra_configs)
+# PMC_PAYLOAD: another workload's payload bytes (tools/ab_libs_desc.py's batch: 4751969452)
+PAYLOAD = int(os.environ.get("PMC_PAYLOAD", PAYLOAD))
 
 
 def per_kernel(prof: str, counter: str, sub: str) -> dict:
