@@ -58,7 +58,7 @@ constexpr uint32_t kPwWin = (128 + kPwBits - 1) / kPwBits;       // windows per 
 constexpr uint32_t kPwEntries = kPwWin << kPwBits;               // entries per power (1408: 22 KiB)
 constexpr uint32_t kPwLaneWins = (kPwWin + 7) / 8;               // windows per lane of an 8-lane chain
 
-constexpr int kNumVariants = 15;     // ids as in round 2; only the three below are built
+// kernel variant ids (QGCM_VARIANT / QGCM_DESC_VARIANT; the numbers the A/B logs under profiles/ use)
 constexpr int kVariantUniform = 12;  // single-key (uniform) batches: quad kernel (Tab2F), 32 waves/CU
 constexpr int kVariantDescWave = 13;  // descriptor batches, per-wave 4-bit tables (Tab2), 12 waves/CU
 constexpr int kVariantDescQuad = 14;  // default for descriptor batches: segmented Tab2F kernel (+ 13 for short keys)

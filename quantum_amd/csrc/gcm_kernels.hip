@@ -1981,8 +1981,8 @@ hipError_t launch_one(bool seal, const Batch &b, hipStream_t s) {
     return hipLaunchKernel(k, dim3(b.n), dim3(kOneThreads), args, kOneLds, s);
 }
 
-// Variant table: index = QGCM variant id (Batch-independent), see qgcm_api.cpp.  The ids are the
-// round-2 ones (the A/B variants measured then -- lane-per-packet, 4-bit-comb and four-table
+// Variant table: the three packet-kernel variants, named by their QGCM variant ids (qgcm_api.cpp).  The
+// ids are the round-2 ones (the A/B variants measured then -- lane-per-packet, 4-bit-comb and four-table
 // single-key kernels, folded J0, repeated-H recombination -- were removed in round 3; DESIGN.md keeps
 // their numbers): 12 = single-key quad kernel (Tab2F), 13 = per-wave descriptor kernel (Tab2),
 // 14 = segmented descriptor kernel (Tab2F) + 13 for the short keys.
@@ -1995,18 +1995,23 @@ struct Variant {
     int complement;  // segmented: the per-wave variant that takes the short keys' tiles after it
 };
 
-static Variant g_variants[kNumVariants];
+// the three kernels, by slot; variant ids (12, 13, 14: the numbering of the A/B logs under profiles/ and
+// of QGCM_VARIANT / QGCM_DESC_VARIANT) map onto them
+static Variant g_variants[3];
+static int variant_slot(int v) {
+    return v == kVariantUniform ? 0 : v == kVariantDescWave ? 1 : v == kVariantDescQuad ? 2 : -1;
+}
 
 hipError_t init_kernels() {
-    g_variants[kVariantUniform] = Variant{reinterpret_cast<const void *>(&gcm_quad_kernel<true, false>),
+    g_variants[0] = Variant{reinterpret_cast<const void *>(&gcm_quad_kernel<true, false>),
                                           reinterpret_cast<const void *>(&gcm_quad_kernel<false, false>),
                                           quad_waves<false>(), kG5Bytes + kTeBytes,
                                           quad_wpe<false>() * 4 / quad_waves<false>(), false, -1};
-    g_variants[kVariantDescWave] = Variant{reinterpret_cast<const void *>(&gcm_quad_kernel<true, true>),
+    g_variants[1] = Variant{reinterpret_cast<const void *>(&gcm_quad_kernel<true, true>),
                                            reinterpret_cast<const void *>(&gcm_quad_kernel<false, true>),
                                            quad_waves<true>(), kTeBytes + (uint32_t)quad_waves<true>() * kGhBytes,
                                            1, true, -1};
-    g_variants[kVariantDescQuad] = Variant{reinterpret_cast<const void *>(&gcm_seg_kernel<true>),
+    g_variants[2] = Variant{reinterpret_cast<const void *>(&gcm_seg_kernel<true>),
                                            reinterpret_cast<const void *>(&gcm_seg_kernel<false>), 16, kSegLds, 2, true,
                                            kVariantDescWave};
     for (const Variant &v : g_variants) {
@@ -2035,15 +2040,15 @@ hipError_t init_kernels() {
     return hipSuccess;
 }
 
-bool variant_valid(int v) { return v >= 0 && v < kNumVariants && g_variants[v].seal != nullptr; }
-int variant_waves(int v) { return g_variants[v].waves; }
-int variant_wgs_per_cu(int v) { return g_variants[v].wgs_per_cu; }
-bool variant_desc(int v) { return g_variants[v].desc; }
-int variant_complement(int v) { return g_variants[v].complement; }
+bool variant_valid(int v) { return variant_slot(v) >= 0 && g_variants[variant_slot(v)].seal != nullptr; }
+int variant_waves(int v) { return g_variants[variant_slot(v)].waves; }
+int variant_wgs_per_cu(int v) { return g_variants[variant_slot(v)].wgs_per_cu; }
+bool variant_desc(int v) { return g_variants[variant_slot(v)].desc; }
+int variant_complement(int v) { return g_variants[variant_slot(v)].complement; }
 
 hipError_t launch_packets(bool seal, int variant, const Batch &b, int grid, hipStream_t s) {
     if (!variant_valid(variant)) return hipErrorInvalidValue;
-    const Variant &v = g_variants[variant];
+    const Variant &v = g_variants[variant_slot(variant)];
     void *args[] = {const_cast<Batch *>(&b), const_cast<uint32_t **>(&b.rk_table)};
     return hipLaunchKernel(seal ? v.seal : v.open, dim3(grid), dim3(v.waves * 64), args, v.lds, s);
 }
