@@ -152,6 +152,9 @@ for s in $STEPS; do
         check profsnap_g$g $?
         python3 tools/pmc_kernels.py gpurun_out/prof_snappy_${TAG}_g$g 1048576 snappy_compress snappy_uncompress > $OUT/snappy_pmc_g$g.txt 2>&1
       done ;;
+    pcie)  # raw pinned-host <-> HBM hipMemcpyAsync rates of this box (the ceiling of every PCIe-inclusive figure)
+      timeout -k 10 200 python3 tools/microbench/pcie.py > $OUT/pcie.json 2> $OUT/pcie.err
+      check pcie $? ;;
     snapab)  # device snappy encoder: four packets per wave vs one wave per packet, interleaved
       timeout -k 10 300 python3 tools/exp_snappy_dev.py 5 2 > $OUT/snap_ab.jsonl 2> $OUT/snap_ab.err
       check snapab $? ;;
