@@ -11,6 +11,9 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libqgcm.so")
+# tools' A/B runs load another build of the same ABI in its place (never set by the product or the tests)
+if os.environ.get("QGCM_AB_LIB"):
+    LIB_PATH = os.path.abspath(os.environ["QGCM_AB_LIB"])
 
 # Every symbol include/qgcm.h declares (checked by tests/test_abi.py).
 EXPORTS = (

@@ -1167,9 +1167,11 @@ static int run_snappy(qgcm_ctx *ctx, bool compress, uint8_t *d_arena, uint64_t s
     a.off_in = tab;
     a.off_out = a.off_in + a16(max_in + 24);  // + the 16-B chunks' overhang and stage_in's slack dwords
     a.off_sink = a.off_out + a16((compress ? (uint32_t)qgcm_snappy_max_compressed_length(max_in) : limit) + 8);
-    // the encoder: four packets per wave (QGCM_SNAPPY_GROUP=0: one wave per packet, for A/Bs)
-    // (packets past ~5 KiB need more LDS than four regions per wave can have: one wave per packet)
-    const bool group = compress && env_int("QGCM_SNAPPY_GROUP", 1) != 0 && kSnapGroup * a.off_sink <= 160u * 1024u;
+    // the encoder: four packets per wave, miss probes pipelined (QGCM_SNAPPY_GROUP: 2, the default; 1 =
+    // not pipelined; 0 = one wave per packet -- A/B knobs).  Packets past ~5 KiB need more LDS than four
+    // regions per wave can have: one wave per packet.
+    int group = compress ? std::max(0, std::min(2, env_int("QGCM_SNAPPY_GROUP", 2))) : 0;
+    if (kSnapGroup * a.off_sink > 160u * 1024u) group = 0;
     a.wave_bytes = group ? kSnapGroup * a.off_sink : a.off_sink + 256;
     const uint32_t per_wave = group ? kSnapGroup : 1;
     int waves = group ? 1 : 4;

@@ -359,6 +359,13 @@ struct GWave {
     }
 };
 
+// kPipe: the miss probes are software-pipelined.  Probe positions do not depend on the data (each
+// miss moves on by skip >> 5, skip += step), so the word at the probe after next is loaded one probe
+// early and the next probe's table entry is read as soon as the current entry is written: a miss then
+// waits for one LDS round trip (the candidate's word) instead of two (the table entry, then the
+// candidate's word).  The early table read is issued after the current probe's table write (LDS
+// operations of a wave complete in order), so it sees that write; the bytes are those of encodeBlock.
+template <bool kPipe>
 __device__ uint32_t gencode_block(const GWave &w, uint32_t op, uint32_t n, uint32_t bits) {
     const uint32_t shift = 32 - bits;
     uint4 *t16 = reinterpret_cast<uint4 *>(w.tab);  // 2 << bits bytes, a multiple of 256
@@ -367,18 +374,38 @@ __device__ uint32_t gencode_block(const GWave &w, uint32_t op, uint32_t n, uint3
     const uint32_t s_limit = n - 15;
     uint32_t next_emit = 0, s = 1, skip = 32;
     uint32_t cur = w.load32(1), h = hash4(cur, shift);
+    uint32_t cand = 0, nv = 0;  // kPipe: tab[h] as of this probe, and the word at this probe's next_s
+    if (kPipe) {
+        cand = w.tab[h];
+        nv = w.load32(min(s + (skip >> 5), n));
+    }
     for (;;) {
         const uint32_t step = skip >> 5, next_s = s + step;
         if (next_s > s_limit) break;
         skip += step;
-        uint32_t cand = w.tab[h];
-        w.tab[h] = (uint16_t)s;
-        const uint32_t nv = w.load32(next_s);
-        if (cur != w.load32(cand)) {  // miss: probe further on
-            s = next_s;
-            cur = nv;
-            h = hash4(nv, shift);
-            continue;
+        if constexpr (kPipe) {
+            w.tab[h] = (uint16_t)s;
+            const uint32_t hn = hash4(nv, shift);
+            const uint32_t cn = w.tab[hn];  // after the write above: tab[hn] as the next probe sees it
+            const uint32_t nv2 = w.load32(min(next_s + (skip >> 5), n));  // the probe after next (clamped)
+            if (cur != w.load32(cand)) {  // miss: probe further on
+                s = next_s;
+                cur = nv;
+                h = hn;
+                cand = cn;
+                nv = nv2;
+                continue;
+            }
+        } else {
+            cand = w.tab[h];
+            w.tab[h] = (uint16_t)s;
+            nv = w.load32(next_s);
+            if (cur != w.load32(cand)) {  // miss: probe further on
+                s = next_s;
+                cur = nv;
+                h = hash4(nv, shift);
+                continue;
+            }
         }
         op = w.emit_literal(op, next_emit, s - next_emit);
         bool more;
@@ -401,11 +428,17 @@ __device__ uint32_t gencode_block(const GWave &w, uint32_t op, uint32_t n, uint3
         skip = 32;
         cur = w.load32(s);
         h = hash4(cur, shift);
+        if (kPipe) {
+            wave_lds_sync();
+            cand = w.tab[h];
+            nv = w.load32(min(s + (skip >> 5), n));
+        }
     }
     if (next_emit < n) op = w.emit_literal(op, next_emit, n - next_emit);
     return op;
 }
 
+template <bool kPipe>
 __global__ void __launch_bounds__(256) snappy_compress_group_kernel(SnapArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t lane = lane_id(), wv = threadIdx.x >> 6, waves = blockDim.x >> 6;
@@ -440,7 +473,7 @@ __global__ void __launch_bounds__(256) snappy_compress_group_kernel(SnapArgs a) 
             } else {
                 uint32_t bits = 8;
                 while (bits < 14 && (1u << bits) < len) ++bits;
-                op = gencode_block(w, op, len, bits);
+                op = gencode_block<kPipe>(w, op, len, bits);
             }
             d = op;
             ok = d <= a.limit;
@@ -557,10 +590,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) s
 
 }  // namespace
 
-hipError_t launch_snappy(bool compress, const SnapArgs &a, int waves_per_wg, int grid, hipStream_t s, bool group) {
+hipError_t launch_snappy(bool compress, const SnapArgs &a, int waves_per_wg, int grid, hipStream_t s, int group) {
     const size_t lds = (size_t)waves_per_wg * a.wave_bytes;
-    if (compress && group)
-        hipLaunchKernelGGL(snappy_compress_group_kernel, dim3(grid), dim3(64 * waves_per_wg), lds, s, a);
+    if (compress && group == 2)
+        hipLaunchKernelGGL(snappy_compress_group_kernel<true>, dim3(grid), dim3(64 * waves_per_wg), lds, s, a);
+    else if (compress && group)
+        hipLaunchKernelGGL(snappy_compress_group_kernel<false>, dim3(grid), dim3(64 * waves_per_wg), lds, s, a);
     else if (compress)
         hipLaunchKernelGGL(snappy_compress_kernel, dim3(grid), dim3(64 * waves_per_wg), lds, s, a);
     else

@@ -152,6 +152,9 @@ for s in $STEPS; do
         check profsnap_g$g $?
         python3 tools/pmc_kernels.py gpurun_out/prof_snappy_${TAG}_g$g 1048576 snappy_compress snappy_uncompress > $OUT/snappy_pmc_g$g.txt 2>&1
       done ;;
+    e2eab)  # config 2 from pinned host memory: this build vs the round-3 build (abt/r3), separate processes
+      timeout -k 10 400 python3 tools/exp_e2e_ab.py quantum_amd/libqgcm.so abt/r3/libqgcm.so 2 > $OUT/e2e_ab.jsonl 2> $OUT/e2e_ab.err
+      check e2eab $? ;;
     pcie)  # raw pinned-host <-> HBM hipMemcpyAsync rates of this box (the ceiling of every PCIe-inclusive figure)
       timeout -k 10 200 python3 tools/microbench/pcie.py > $OUT/pcie.json 2> $OUT/pcie.err
       check pcie $? ;;
