@@ -80,10 +80,11 @@ def _match(case, comp: bytes) -> bool:
     return hashlib.sha256(comp).hexdigest() == case["out_sha256"]
 
 
-@pytest.fixture(params=["1", "0"], ids=["group_encoder", "wave_encoder"])
+@pytest.fixture(params=["2", "1", "0"], ids=["group_pipelined", "group_encoder", "wave_encoder"])
 def encoder(request, monkeypatch):
-    """QGCM_SNAPPY_GROUP (read per call): 1 = four packets per wave (the default), 0 = one wave per
-    packet.  Both must give the host encoder's (and libsnappy's) bytes."""
+    """QGCM_SNAPPY_GROUP (read per call): 2 = four packets per wave with pipelined miss probes (the
+    default), 1 = four packets per wave, 0 = one wave per packet.  All must give the host encoder's (and
+    libsnappy's) bytes."""
     monkeypatch.setenv("QGCM_SNAPPY_GROUP", request.param)
     return request.param
 
