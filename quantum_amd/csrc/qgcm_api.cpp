@@ -1167,11 +1167,21 @@ static int run_snappy(qgcm_ctx *ctx, bool compress, uint8_t *d_arena, uint64_t s
     a.off_in = tab;
     a.off_out = a.off_in + a16(max_in + 24);  // + the 16-B chunks' overhang and stage_in's slack dwords
     a.off_sink = a.off_out + a16((compress ? (uint32_t)qgcm_snappy_max_compressed_length(max_in) : limit) + 8);
-    // the encoder: four packets per wave, miss probes pipelined (QGCM_SNAPPY_GROUP: 2, the default; 1 =
-    // not pipelined; 0 = one wave per packet -- A/B knobs).  Packets past ~5 KiB need more LDS than four
+    // the encoder (QGCM_SNAPPY_GROUP, A/B knob): 3 (default) = four packets per wave, miss probes
+    // pipelined, output straight into the slot (no LDS output area); 2 = the same with the output staged
+    // in LDS; 1 = not pipelined; 0 = one wave per packet.  Packets past ~5 KiB need more LDS than four
     // regions per wave can have: one wave per packet.
-    int group = compress ? std::max(0, std::min(2, env_int("QGCM_SNAPPY_GROUP", 2))) : 0;
+    int group = compress ? std::max(0, std::min(3, env_int("QGCM_SNAPPY_GROUP", 3))) : 0;
+    if (group == 3 && limit == 0) group = 2;
+    if (group == 3) {  // region: table + the input staged up to max(len, limit) bytes (the restore copy)
+        a.off_out = a.off_in + a16(std::max(max_in, limit) + 24);
+        a.off_sink = a.off_out;
+    }
     if (kSnapGroup * a.off_sink > 160u * 1024u) group = 0;
+    if (group == 0) {  // the wave encoder's layout
+        a.off_out = a.off_in + a16(max_in + 24);
+        a.off_sink = a.off_out + a16((compress ? (uint32_t)qgcm_snappy_max_compressed_length(max_in) : limit) + 8);
+    }
     a.wave_bytes = group ? kSnapGroup * a.off_sink : a.off_sink + 256;
     const uint32_t per_wave = group ? kSnapGroup : 1;
     int waves = group ? 1 : 4;

@@ -275,25 +275,29 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) s
 // (a.off_in / a.off_out within a region of a.off_sink bytes), four regions per wave.
 constexpr uint32_t kGrp = 4, kGL = 64 / kGrp;
 
+template <bool kDirect>
 struct GWave {
-    uint8_t *in, *out;
+    uint8_t *in, *out;  // kDirect: out = the slot's packet bytes in device memory, else LDS staging
     uint16_t *tab;
     uint32_t gl, grp;  // lane within the group, group within the wave
+    uint32_t olast;    // kDirect: last output index kept inside the packet's limit (writes past it land there)
 
     __device__ __forceinline__ uint32_t load32(uint32_t o) const {
         const uint32_t *w = reinterpret_cast<const uint32_t *>(in);
         return __builtin_amdgcn_alignbyte(w[(o >> 2) + 1], w[o >> 2], o & 3);
     }
-    __device__ __forceinline__ void put(uint32_t o, uint32_t v) const { out[o] = (uint8_t)v; }
+    __device__ __forceinline__ void put(uint32_t o, uint32_t v) const {
+        out[kDirect ? min(o, olast) : o] = (uint8_t)v;
+    }
     // out[op..op+len) = in[from..from+len): lane gl moves bytes 4 gl .. 4 gl + 3 of every 64
     __device__ __forceinline__ void copy_in(uint32_t op, uint32_t from, uint32_t len) const {
         for (uint32_t j = 4 * gl; j < len; j += 4 * kGL) {
             const uint32_t v = load32(from + j);
             const uint32_t k = len - j < 4 ? len - j : 4;
-            out[op + j] = (uint8_t)v;
-            if (k > 1) out[op + j + 1] = (uint8_t)(v >> 8);
-            if (k > 2) out[op + j + 2] = (uint8_t)(v >> 16);
-            if (k > 3) out[op + j + 3] = (uint8_t)(v >> 24);
+            put(op + j, v);
+            if (k > 1) put(op + j + 1, v >> 8);
+            if (k > 2) put(op + j + 2, v >> 16);
+            if (k > 3) put(op + j + 3, v >> 24);
         }
     }
     __device__ __forceinline__ uint32_t emit_literal(uint32_t op, uint32_t from, uint32_t len) const {
@@ -365,8 +369,8 @@ struct GWave {
 // waits for one LDS round trip (the candidate's word) instead of two (the table entry, then the
 // candidate's word).  The early table read is issued after the current probe's table write (LDS
 // operations of a wave complete in order), so it sees that write; the bytes are those of encodeBlock.
-template <bool kPipe>
-__device__ uint32_t gencode_block(const GWave &w, uint32_t op, uint32_t n, uint32_t bits) {
+template <bool kPipe, bool kDirect>
+__device__ uint32_t gencode_block(const GWave<kDirect> &w, uint32_t op, uint32_t n, uint32_t bits) {
     const uint32_t shift = 32 - bits;
     uint4 *t16 = reinterpret_cast<uint4 *>(w.tab);  // 2 << bits bytes, a multiple of 256
     for (uint32_t j = w.gl; j < (2u << bits) / 16; j += kGL) t16[j] = uint4{0, 0, 0, 0};
@@ -438,13 +442,18 @@ __device__ uint32_t gencode_block(const GWave &w, uint32_t op, uint32_t n, uint3
     return op;
 }
 
-template <bool kPipe>
+// kDirect: the output goes straight into the slot (its input is staged in LDS, so the slot is free to
+// overwrite), and a packet's LDS region holds only the hash table and the staged input -- 5.5 KiB
+// instead of 7.2 for a 1472-B slot, 7 waves (28 packets) per CU instead of 5.  Output bytes past the
+// packet's limit all land on its last kept byte; a packet whose output exceeds the limit gets its
+// first `limit` slot bytes back from the staged copy (staged up to max(len, limit) bytes for that).
+template <bool kPipe, bool kDirect>
 __global__ void __launch_bounds__(256) snappy_compress_group_kernel(SnapArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t lane = lane_id(), wv = threadIdx.x >> 6, waves = blockDim.x >> 6;
     const uint32_t grp = lane / kGL, gl = lane % kGL;
     uint8_t *base = smem + (wv * kGrp + grp) * a.off_sink;
-    const GWave w{base + a.off_in, base + a.off_out, reinterpret_cast<uint16_t *>(base), gl, grp};
+    GWave<kDirect> w{base + a.off_in, base + a.off_out, reinterpret_cast<uint16_t *>(base), gl, grp, 0u};
     const uint32_t step = gridDim.x * waves * kGrp;
     for (uint32_t p0 = (blockIdx.x * waves + wv) * kGrp; p0 < a.n; p0 += step) {
         const uint32_t p = p0 + grp;
@@ -452,12 +461,18 @@ __global__ void __launch_bounds__(256) snappy_compress_group_kernel(SnapArgs a) 
         const uint32_t len = have ? a.lens[p] : 0u;
         uint8_t *slot = a.arena + (uint64_t)(have ? p : 0u) * a.stride;
         bool ok = have && len <= a.max_in;
-        if (ok) {  // slot bytes [4, 4 + len) -> LDS, whole dwords (the slot is 4-B aligned, stride a multiple of 4)
+        // kDirect stages max(len, limit) bytes: the restore copy of a packet whose output overflows
+        const uint32_t sn = kDirect ? max(len, a.limit) : len;
+        if (ok) {  // slot bytes [4, 4 + sn) -> LDS, whole dwords (the slot is 4-B aligned, stride a multiple of 4)
             const uint32_t *src = reinterpret_cast<const uint32_t *>(slot + 4);
             uint32_t *d = reinterpret_cast<uint32_t *>(w.in);
-            const uint32_t nw = (len + 3) >> 2;
+            const uint32_t nw = (sn + 3) >> 2;
             for (uint32_t j = gl; j < nw; j += kGL) d[j] = src[j];
             if (gl < 2) d[nw + gl] = 0;  // slack read by load32 past the end
+        }
+        if constexpr (kDirect) {
+            w.out = slot + 4;
+            w.olast = a.limit - 1;
         }
         wave_lds_sync();
         uint32_t d = 0;
@@ -473,13 +488,21 @@ __global__ void __launch_bounds__(256) snappy_compress_group_kernel(SnapArgs a) 
             } else {
                 uint32_t bits = 8;
                 while (bits < 14 && (1u << bits) < len) ++bits;
-                op = gencode_block<kPipe>(w, op, len, bits);
+                op = gencode_block<kPipe, kDirect>(w, op, len, bits);
             }
             d = op;
             ok = d <= a.limit;
+            if (kDirect && !ok) {  // overflowed: the slot's first `limit` bytes back from the staged copy
+                uint32_t *dst = reinterpret_cast<uint32_t *>(slot + 4);
+                const uint32_t *srcw = reinterpret_cast<const uint32_t *>(w.in);
+                const uint32_t nw = a.limit >> 2;
+                for (uint32_t j = gl; j < nw; j += kGL) dst[j] = srcw[j];
+                const uint32_t t = a.limit & 3;
+                if (gl < t) slot[4 + 4 * nw + gl] = w.in[4 * nw + gl];
+            }
         }
         wave_lds_sync();
-        if (ok) {  // LDS [0, d) -> slot bytes [4, 4 + d)
+        if (!kDirect && ok) {  // LDS [0, d) -> slot bytes [4, 4 + d)
             uint32_t *dst = reinterpret_cast<uint32_t *>(slot + 4);
             const uint32_t *srcw = reinterpret_cast<const uint32_t *>(w.out);
             const uint32_t nw = d >> 2;
@@ -592,10 +615,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) s
 
 hipError_t launch_snappy(bool compress, const SnapArgs &a, int waves_per_wg, int grid, hipStream_t s, int group) {
     const size_t lds = (size_t)waves_per_wg * a.wave_bytes;
-    if (compress && group == 2)
-        hipLaunchKernelGGL(snappy_compress_group_kernel<true>, dim3(grid), dim3(64 * waves_per_wg), lds, s, a);
+    if (compress && group == 3)
+        hipLaunchKernelGGL((snappy_compress_group_kernel<true, true>), dim3(grid), dim3(64 * waves_per_wg), lds, s, a);
+    else if (compress && group == 2)
+        hipLaunchKernelGGL((snappy_compress_group_kernel<true, false>), dim3(grid), dim3(64 * waves_per_wg), lds, s, a);
     else if (compress && group)
-        hipLaunchKernelGGL(snappy_compress_group_kernel<false>, dim3(grid), dim3(64 * waves_per_wg), lds, s, a);
+        hipLaunchKernelGGL((snappy_compress_group_kernel<false, false>), dim3(grid), dim3(64 * waves_per_wg), lds, s, a);
     else if (compress)
         hipLaunchKernelGGL(snappy_compress_kernel, dim3(grid), dim3(64 * waves_per_wg), lds, s, a);
     else

@@ -80,11 +80,12 @@ def _match(case, comp: bytes) -> bool:
     return hashlib.sha256(comp).hexdigest() == case["out_sha256"]
 
 
-@pytest.fixture(params=["2", "1", "0"], ids=["group_pipelined", "group_encoder", "wave_encoder"])
+@pytest.fixture(params=["3", "2", "1", "0"], ids=["group_direct", "group_pipelined", "group_encoder", "wave_encoder"])
 def encoder(request, monkeypatch):
-    """QGCM_SNAPPY_GROUP (read per call): 2 = four packets per wave with pipelined miss probes (the
-    default), 1 = four packets per wave, 0 = one wave per packet.  All must give the host encoder's (and
-    libsnappy's) bytes."""
+    """QGCM_SNAPPY_GROUP (read per call): 3 = four packets per wave, pipelined miss probes, output
+    straight into the slot (the default); 2 = the same with the output staged in LDS; 1 = not pipelined;
+    0 = one wave per packet.  All must give the host encoder's (and libsnappy's) bytes, and leave a
+    failing packet's slot untouched."""
     monkeypatch.setenv("QGCM_SNAPPY_GROUP", request.param)
     return request.param
 
@@ -161,9 +162,15 @@ def test_device_compress_failures_untouched(torch, ctx, encoder):
     for i in (2, 3, 4):
         c = _host_compress(payloads[i])
         assert ol[i] == len(c) and out[i, 4:4 + len(c)].tobytes() == c
-    _, arena, lens = _arena(torch, payloads, stride)
+    host, arena, lens = _arena(torch, payloads, stride)
     out, ol, st = _run(torch, ctx, True, arena, stride, len(payloads), lens, 2000, 800)
     assert list(st) == [0, 1, 0, 1, 1]  # random 1500 / 900 do not fit 800; the line does
+    for i in (0, 2):  # encoded past the limit (the direct encoder wrote into the slot): restored whole
+        assert np.array_equal(out[i], host[i]) and ol[i] == len(payloads[i])
+    for i in (1, 3, 4):
+        c = _host_compress(payloads[i])
+        assert ol[i] == len(c) and out[i, 4:4 + len(c)].tobytes() == c
+        assert np.array_equal(out[i, 4 + len(c):], host[i, 4 + len(c):])  # past the output: untouched
 
 
 def test_device_uncompress_corrupted_streams_vs_host(torch, ctx):

@@ -2,8 +2,9 @@
 random, second half a repeated HTTP line, stride 1472): compress, seal, open, uncompress, each timed
 by HIP events; the sealed arena is checked against tests/golden/config5_digest.json and the result
 against the plaintext arena (bench.extra_config5_resident).  The encoder alternates between the
-four-packets-per-wave kernels (QGCM_SNAPPY_GROUP=2 and 1) and one wave per packet (0), in one
-process, `rounds` times each (2 = four packets per wave with pipelined miss probes, the default).
+four-packets-per-wave kernels (QGCM_SNAPPY_GROUP=3, 2, 1) and one wave per packet (0), in one process,
+`rounds` times each (3, the default: pipelined miss probes and the output written straight into the
+slot; 2: pipelined, output staged in LDS; 1: neither).
 
     python3 tools/exp_snappy_dev.py [reps] [rounds]
 """
@@ -21,7 +22,7 @@ def main() -> None:
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 2
     key = bench.derive_key(bench.SECRET, bench.SALT)
     for r in range(rounds):
-        for grp in ("2", "1", "0"):
+        for grp in ("3", "2", "1", "0"):
             os.environ["QGCM_SNAPPY_GROUP"] = grp
             res = bench.extra_config5_resident(key, reps, verify=(r == 0))
             print(json.dumps({"snappy_group": int(grp), **res}), flush=True)
