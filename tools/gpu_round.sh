@@ -155,6 +155,9 @@ for s in $STEPS; do
     e2eab)  # config 2 from pinned host memory: this build vs the round-3 build (abt/r3), separate processes
       timeout -k 10 400 python3 tools/exp_e2e_ab.py quantum_amd/libqgcm.so abt/r3/libqgcm.so 2 > $OUT/e2e_ab.jsonl 2> $OUT/e2e_ab.err
       check e2eab $? ;;
+    hostlegs)  # the PCIe-inclusive bench legs, each in a fresh process, with the NUMA nodes of their pinned arenas
+      timeout -k 10 600 python3 tools/exp_host_legs.py > $OUT/host_legs.jsonl 2> $OUT/host_legs.err
+      check hostlegs $? ;;
     pcie)  # raw pinned-host <-> HBM hipMemcpyAsync rates of this box (the ceiling of every PCIe-inclusive figure)
       timeout -k 10 200 python3 tools/microbench/pcie.py > $OUT/pcie.json 2> $OUT/pcie.err
       check pcie $? ;;
