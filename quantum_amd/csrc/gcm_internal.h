@@ -1,6 +1,8 @@
 // Internal interface between the C ABI (qgcm_api.cpp) and the gfx950 kernels (gcm_kernels.hip).
 #pragma once
 #include <hip/hip_runtime.h>
+
+#include <mutex>
 #include <stdint.h>
 
 #include "../../include/qgcm.h"
@@ -140,6 +142,10 @@ constexpr uint32_t kOneUniformMax = 2048;    // measured cross-over with the qua
 constexpr uint32_t kLaunchChunk = 1u << 19;  // packets per quad-kernel launch of a uniform batch
 constexpr uint32_t kDescChunk = 0;           // packets per sorted chunk of a descriptor batch (0 = all)
 bool ctx_one_kernel(const qgcm_ctx *ctx);
+// the context's host-pipeline streams (0 copy-in, 1 kernels, 2 copy-out) and the mutex that guards them
+// (group.cpp's DMA runs use them, as qgcm_seal_host does)
+hipStream_t ctx_pipe(qgcm_ctx *ctx, int k);
+std::mutex &ctx_io_mu(qgcm_ctx *ctx);
 hipError_t launch_stream_copy(void *dst, const void *src, uint64_t bytes, int num_cus, hipStream_t s);
 // one record move of the group dispatcher's zero-copy path: src/dst device-accessible addresses
 // (pinned host or device), 4-B aligned; status_idx: the record's status byte (scatter only)

@@ -565,9 +565,17 @@ void plan_dma(bool seal, const qgcm_desc *descs, const uint32_t *idx, size_t m, 
     }
 }
 
+bool own_streams() {
+    static const bool own = [] {
+        const char *v = getenv("QGCM_GROUP_DMA_OWN_STREAMS");
+        return v && atoi(v) != 0;
+    }();
+    return own;
+}
+
 int dma_ready(DmaState &z, uint64_t stage, uint64_t side) {
     for (hipStream_t &x : z.s)
-        if (!x && hipStreamCreateWithFlags(&x, hipStreamNonBlocking) != hipSuccess) return QGCM_E_HIP;
+        if (own_streams() && !x && hipStreamCreateWithFlags(&x, hipStreamNonBlocking) != hipSuccess) return QGCM_E_HIP;
     for (int k = 0; k < kDmaSlots; ++k)
         for (hipEvent_t *e : {&z.ev_in[k], &z.ev_k[k], &z.ev_out[k]})
             if (!*e && hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return QGCM_E_HIP;
@@ -603,7 +611,16 @@ int run_member_dma(Member &mb, bool seal, uint8_t *h_arena, const qgcm_desc *des
     const uint64_t side = off_st + ((pk + 255) & ~255ull);
     int rc = dma_ready(z, pl.max_bytes, side);
     if (rc != QGCM_OK) return rc;
+    // the member context's own pipeline streams (those qgcm_seal_host moves 46 GB/s each way with);
+    // QGCM_GROUP_DMA_OWN_STREAMS=1: streams of the group's own (A/B)
+    std::unique_lock<std::mutex> io(qgcm::ctx_io_mu(mb.ctx), std::defer_lock);
     hipStream_t s_in = z.s[0], s_k = z.s[1], s_out = z.s[2];
+    if (!own_streams()) {
+        io.lock();
+        s_in = qgcm::ctx_pipe(mb.ctx, 0);
+        s_k = qgcm::ctx_pipe(mb.ctx, 1);
+        s_out = qgcm::ctx_pipe(mb.ctx, 2);
+    }
     int bad = 0;
     // results of the chunk last staged in slot k (its copy-out has landed): statuses to the caller
     auto retire = [&](int k, const DmaChunk &c) {
@@ -662,7 +679,7 @@ int run_member_dma(Member &mb, bool seal, uint8_t *h_arena, const qgcm_desc *des
              hipEventRecord(z.ev_out[k], s_out) != hipSuccess))
             rc = QGCM_E_HIP;
     }
-    for (hipStream_t x : z.s)
+    for (hipStream_t x : {s_in, s_k, s_out})
         if (hipStreamSynchronize(x) != hipSuccess && rc == QGCM_OK) rc = QGCM_E_HIP;
     if (rc == QGCM_OK)  // the chunks still in their slots
         for (size_t q = c > (size_t)kDmaSlots ? c - kDmaSlots : 0; q < c; ++q) retire((int)(q % kDmaSlots), pl.chunks[q]);

@@ -250,6 +250,8 @@ bool key_ok(qgcm_ctx *ctx, uint32_t k) {
 }  // namespace
 
 bool qgcm::ctx_one_kernel(const qgcm_ctx *ctx) { return ctx->one_kernel; }
+hipStream_t qgcm::ctx_pipe(qgcm_ctx *ctx, int k) { return ctx->pipe[k]; }
+std::mutex &qgcm::ctx_io_mu(qgcm_ctx *ctx) { return ctx->io_mu; }
 
 namespace {
 
@@ -592,20 +594,22 @@ int qgcm_set_keys(qgcm_ctx *ctx, uint32_t first_idx, uint32_t count, const uint8
     if (hipSetDevice(ctx->device) != hipSuccess) return QGCM_E_HIP;
     uint8_t *d_keys = nullptr;
     if (hipMalloc(&d_keys, (size_t)count * 32) != hipSuccess) return QGCM_E_NOMEM;
-    hipStream_t s = nullptr;
+    // The key setup runs on the context's kernel stream (no stream created per call: every stream a
+    // process creates moves HIP's stream -> hardware-queue assignment on, and two pipeline stages that
+    // end up on one hardware queue serialize their copies).
+    std::lock_guard<std::mutex> io(ctx->io_mu);
+    hipStream_t s = ctx->pipe[1];
     // a running resident instance holds key tables (and keystreams computed ahead, key-valid bytes) in
     // its caches: end it BEFORE the tables change and start no new one until the new keys are published
     Resident *res = ctx->res.load(std::memory_order_acquire);
     (void)resident_pause(res);  // a failure marks the resident path broken: calls take the launch path
     int rc = QGCM_OK;
-    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess ||
-        hipMemcpyAsync(d_keys, keys, (size_t)count * 32, hipMemcpyHostToDevice, s) != hipSuccess ||
+    if (hipMemcpyAsync(d_keys, keys, (size_t)count * 32, hipMemcpyHostToDevice, s) != hipSuccess ||
         launch_key_setup(d_keys, first_idx, count, ctx->d_rk, ctx->d_gh, ctx->d_sbox, s) != hipSuccess ||
         launch_pw_setup(first_idx, count, ctx->d_gh, ctx->d_pw, ctx->pw_keys, s) != hipSuccess ||
         hipMemsetAsync(ctx->d_key_valid + first_idx, 1, count, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
         rc = QGCM_E_HIP;
-    if (s) hipStreamDestroy(s);
     hipFree(d_keys);
     if (rc == QGCM_OK) {
         std::lock_guard<std::mutex> g(ctx->key_mu);

@@ -158,6 +158,11 @@ for s in $STEPS; do
     hostlegs)  # the PCIe-inclusive bench legs, each in a fresh process, with the NUMA nodes of their pinned arenas
       timeout -k 10 600 python3 tools/exp_host_legs.py > $OUT/host_legs.jsonl 2> $OUT/host_legs.err
       check hostlegs $? ;;
+    dmaab)  # keyed host batch (DMA runs) on the member context's streams vs streams of its own, then e2e in the same process
+      for own in 0 1; do
+        QGCM_GROUP_DMA_OWN_STREAMS=$own timeout -k 10 400 python3 tools/exp_host_legs.py config3_host > $OUT/dmaab_own$own.jsonl 2>> $OUT/dmaab.err
+        check dmaab_own$own $?
+      done ;;
     pcie)  # raw pinned-host <-> HBM hipMemcpyAsync rates of this box (the ceiling of every PCIe-inclusive figure)
       timeout -k 10 200 python3 tools/microbench/pcie.py > $OUT/pcie.json 2> $OUT/pcie.err
       check pcie $? ;;
