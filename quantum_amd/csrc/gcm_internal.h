@@ -125,7 +125,13 @@ struct ResArgs {
 };
 hipError_t launch_resident(const Batch &b, const ResArgs &a, hipStream_t s);
 struct Resident;
-Resident *resident_create(int device, const Batch &base, int num_cus);  // nullptr: not available
+// the service's settings, read from the QGCM_RESIDENT_* environment when the context is created (like
+// every other QGCM_* knob), not when the service is first started by a per-packet call
+struct ResidentConfig {
+    uint64_t workers, slots, spin_us, spinners, idle_us, life_us, fail_after;
+};
+ResidentConfig resident_config_from_env();
+Resident *resident_create(int device, const Batch &base, int num_cus, const ResidentConfig &cfg);  // nullptr: not available
 void resident_destroy(Resident *r);
 int resident_quiesce(Resident *r);
 int resident_workers_running(const Resident *r);

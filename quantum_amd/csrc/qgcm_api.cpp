@@ -107,6 +107,7 @@ struct qgcm_ctx {
 
     // resident per-packet service (resident.cpp), created on the first per-packet call
     bool res_on = true;  // QGCM_RESIDENT=0: every per-packet call launches gcm_one_kernel
+    qgcm::ResidentConfig res_cfg{};  // QGCM_RESIDENT_*, read at qgcm_create
     std::atomic<qgcm::Resident *> res{nullptr};
     std::atomic<bool> res_failed{false};
     std::mutex res_mu;
@@ -233,7 +234,7 @@ Resident *get_resident(qgcm_ctx *ctx) {
     std::lock_guard<std::mutex> g(ctx->res_mu);
     r = ctx->res.load(std::memory_order_acquire);
     if (!r) {
-        r = resident_create(ctx->device, base_batch(ctx), ctx->num_cus);
+        r = resident_create(ctx->device, base_batch(ctx), ctx->num_cus, ctx->res_cfg);
         if (!r) ctx->res_failed = true;
         ctx->res.store(r, std::memory_order_release);
     }
@@ -513,6 +514,7 @@ qgcm_ctx *qgcm_create(int device, uint32_t max_keys, char *err, int errlen) {
     if (const char *v = getenv("QGCM_ONE_KERNEL")) ctx->one_kernel = atoi(v) != 0;
     if (const char *v = getenv("QGCM_CHAIN_DEVICE")) ctx->chain_codec = std::max(0, std::min(2, atoi(v)));
     if (const char *v = getenv("QGCM_RESIDENT")) ctx->res_on = atoi(v) != 0;
+    ctx->res_cfg = qgcm::resident_config_from_env();
     if (const char *v = getenv("QGCM_ONE_UNIFORM_MAX")) ctx->one_uniform_max = (uint32_t)std::max(0, atoi(v));
     if (const char *v = getenv("QGCM_LAUNCH_CHUNK"))  // rounded down to whole 64-packet tiles
         ctx->launch_chunk = (uint32_t)std::max(0, atoi(v)) & ~63u;

@@ -244,21 +244,33 @@ bool random_nonce(uint8_t out[12]) {
     return true;
 }
 
-Resident *resident_create(int device, const Batch &base, int num_cus) {
+ResidentConfig resident_config_from_env() {
+    ResidentConfig c;
+    c.workers = env_u64("QGCM_RESIDENT_WORKERS", 16);
+    c.slots = env_u64("QGCM_RESIDENT_SLOTS", 16);
+    c.spin_us = env_u64("QGCM_RESIDENT_SPIN_US", 20);
+    // callers beyond this many sleep at once instead of spinning: with many more callers than CPUs,
+    // spinning ones take the CPUs that posting callers, the completion thread and other host work need
+    c.spinners = env_u64("QGCM_RESIDENT_SPINNERS", (uint64_t)std::max(1, cpu_share() / 2));
+    c.idle_us = env_u64("QGCM_RESIDENT_IDLE_US", 2000);
+    c.life_us = env_u64("QGCM_RESIDENT_LIFE_US", 8000);
+    c.fail_after = env_u64("QGCM_RESIDENT_FAIL_AFTER", ~0ull);  // test hook
+    return c;
+}
+
+Resident *resident_create(int device, const Batch &base, int num_cus, const ResidentConfig &cfg) {
     auto r = std::make_unique<Resident>();
     r->device = device;
     r->base = base;
-    r->W = (uint32_t)env_u64("QGCM_RESIDENT_WORKERS", 16);
-    r->P = (uint32_t)env_u64("QGCM_RESIDENT_SLOTS", 16);
+    r->W = (uint32_t)cfg.workers;
+    r->P = (uint32_t)cfg.slots;
     if (r->W < 1 || (int)r->W > num_cus / 2 || r->P < 1 || r->P > kResMaxPerWorker) return nullptr;
     r->S = r->W * r->P;
-    r->spin_ns = env_u64("QGCM_RESIDENT_SPIN_US", 20) * 1000;
-    // callers beyond this many sleep at once instead of spinning: with many more callers than CPUs,
-    // spinning ones take the CPUs that posting callers, the completion thread and other host work need
-    r->max_spinners = (int32_t)env_u64("QGCM_RESIDENT_SPINNERS", (uint64_t)std::max(1, cpu_share() / 2));
-    r->idle_ticks = env_u64("QGCM_RESIDENT_IDLE_US", 2000) * 100;  // s_memrealtime: 100 MHz
-    r->life_ticks = env_u64("QGCM_RESIDENT_LIFE_US", 8000) * 100;
-    r->fail_after = env_u64("QGCM_RESIDENT_FAIL_AFTER", ~0ull);
+    r->spin_ns = cfg.spin_us * 1000;
+    r->max_spinners = (int32_t)cfg.spinners;
+    r->idle_ticks = cfg.idle_us * 100;  // s_memrealtime: 100 MHz
+    r->life_ticks = cfg.life_us * 100;
+    r->fail_after = cfg.fail_after;
     // host region: done, over, then the result slots; device region: the stop words (a 64-B line per
     // worker), the request records, then the request slots
     const size_t o_over = (4ull * r->S + 63) & ~63ull, o_hits = o_over + 64;

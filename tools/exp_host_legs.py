@@ -5,6 +5,8 @@ each leg the NUMA nodes of a sample of its pinned arena's pages (move_pages(2) q
 NUMA node (sysfs) are printed, to tell a slow box from a remote-node arena.
 
     python3 tools/exp_host_legs.py [leg ...]      (default: e2e config3_host config5 e2e)
+
+A leg written "config3_host+e2e" runs both legs in the same process, one after the other.
 """
 import ctypes as C
 import json
@@ -47,16 +49,18 @@ class Shim:
         return probe if k == "qgcm_host_alloc" else getattr(lib, k)
 _lib.lib = lambda: Shim()
 key = bench.derive_key(bench.SECRET, bench.SALT)
-leg = %(leg)r
-if leg == "e2e":
-    out = bench.extra_e2e(key)
-elif leg == "config3_host":
-    out = bench.extra_config3_host(verify=False)
-elif leg == "config5":
-    out = bench.extra_config5(key, bench.host_cpus()["share"], verify=False)
-out = {"leg": leg, "value": out.get("value"), "pcie_GBps_each_way": out.get("pcie_GBps_each_way"),
-       "pinned_arena_numa_nodes": nodes_seen, "affinity_cpus": len(os.sched_getaffinity(0))}
-print(json.dumps(out))
+outs = []
+for leg in %(leg)r.split("+"):  # legs joined by "+" run one after another in this one process
+    nodes_seen.clear()
+    if leg == "e2e":
+        out = bench.extra_e2e(key)
+    elif leg == "config3_host":
+        out = bench.extra_config3_host(verify=False)
+    elif leg == "config5":
+        out = bench.extra_config5(key, bench.host_cpus()["share"], verify=False)
+    outs.append({"leg": leg, "value": out.get("value"), "pcie_GBps_each_way": out.get("pcie_GBps_each_way"),
+                 "pinned_arena_numa_nodes": list(nodes_seen), "affinity_cpus": len(os.sched_getaffinity(0))})
+print(json.dumps(outs if len(outs) > 1 else outs[0]))
 '''
 
 

@@ -160,7 +160,7 @@ for s in $STEPS; do
       check hostlegs $? ;;
     dmaab)  # keyed host batch (DMA runs) on the member context's streams vs streams of its own, then e2e in the same process
       for own in 0 1; do
-        QGCM_GROUP_DMA_OWN_STREAMS=$own timeout -k 10 400 python3 tools/exp_host_legs.py config3_host > $OUT/dmaab_own$own.jsonl 2>> $OUT/dmaab.err
+        QGCM_GROUP_DMA_OWN_STREAMS=$own timeout -k 10 400 python3 tools/exp_host_legs.py config3_host config3_host+e2e > $OUT/dmaab_own$own.jsonl 2>> $OUT/dmaab.err
         check dmaab_own$own $?
       done ;;
     pcie)  # raw pinned-host <-> HBM hipMemcpyAsync rates of this box (the ceiling of every PCIe-inclusive figure)
