@@ -10,11 +10,11 @@ import torch
 TOTAL = 1 << 30  # 1 GiB per direction per measurement
 
 
-def rate(chunk: int, h2d: bool, d2h: bool, reps: int = 3, stream_host: bool = False) -> dict:
-    """stream_host: walk a 1 GiB pinned host buffer chunk by chunk (as qgcm_seal_host walks the
+def rate(chunk: int, h2d: bool, d2h: bool, reps: int = 3, stream_host: bool = False, total: int = TOTAL) -> dict:
+    """stream_host: walk a `total`-byte pinned host buffer chunk by chunk (as qgcm_seal_host walks the
     arena) instead of re-copying one chunk-sized buffer."""
-    n = TOTAL // chunk
-    hsz = TOTAL if stream_host else chunk
+    n = total // chunk
+    hsz = total if stream_host else chunk
     hs = [torch.empty(hsz, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
     ds = [torch.empty(chunk, dtype=torch.uint8, device="cuda") for _ in range(2)]
     s_in, s_out = torch.cuda.Stream(), torch.cuda.Stream()
@@ -50,3 +50,8 @@ if __name__ == "__main__":
             print(json.dumps(rate(chunk, h2d, d2h)), flush=True)
     for chunk in (32 << 20, 64 << 20):
         print(json.dumps(rate(chunk, True, True, stream_host=True)), flush=True)
+    # a 5 GiB walk (config 3's arena is 4.8 GB): does the rate depend on how much pinned memory a
+    # copy stream touches (IOMMU translation reach)?
+    for chunk in (64 << 20,):
+        print(json.dumps(rate(chunk, True, True, stream_host=True, total=5 << 30)), flush=True)
+        print(json.dumps(rate(chunk, True, False, stream_host=True, total=5 << 30)), flush=True)
