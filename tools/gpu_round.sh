@@ -163,6 +163,12 @@ for s in $STEPS; do
         QGCM_GROUP_DMA_OWN_STREAMS=$own timeout -k 10 400 python3 tools/exp_host_legs.py config3_host config3_host+e2e > $OUT/dmaab_own$own.jsonl 2>> $OUT/dmaab.err
         check dmaab_own$own $?
       done ;;
+    copytrace)  # copy / kernel timelines of the keyed host batch and the contiguous pipeline (is H2D overlapping D2H?)
+      for leg in config3_host e2e; do
+        timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $OUT/trace_$leg -o t -- python3 tools/run_leg.py $leg 2 > $OUT/trace_$leg.log 2>&1
+        check trace_$leg $?
+        python3 tools/copy_trace_summary.py $OUT/trace_$leg > $OUT/copy_summary_$leg.txt 2>&1
+      done ;;
     pcie)  # raw pinned-host <-> HBM hipMemcpyAsync rates of this box (the ceiling of every PCIe-inclusive figure)
       timeout -k 10 200 python3 tools/microbench/pcie.py > $OUT/pcie.json 2> $OUT/pcie.err
       check pcie $? ;;
