@@ -10,13 +10,15 @@ import torch
 TOTAL = 1 << 30  # 1 GiB per direction per measurement
 
 
-def rate(chunk: int, h2d: bool, d2h: bool, reps: int = 3, stream_host: bool = False, total: int = TOTAL) -> dict:
+def rate(chunk: int, h2d: bool, d2h: bool, reps: int = 3, stream_host: bool = False, total: int = TOTAL,
+         mis: int = 0) -> dict:
     """stream_host: walk a `total`-byte pinned host buffer chunk by chunk (as qgcm_seal_host walks the
-    arena) instead of re-copying one chunk-sized buffer."""
+    arena) instead of re-copying one chunk-sized buffer.  mis: both ends of every copy start `mis`
+    bytes past a 4 KiB boundary (a keyed batch's runs start wherever a record does)."""
     n = total // chunk
     hsz = total if stream_host else chunk
-    hs = [torch.empty(hsz, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
-    ds = [torch.empty(chunk, dtype=torch.uint8, device="cuda") for _ in range(2)]
+    hs = [torch.empty(hsz + 4096, dtype=torch.uint8, pin_memory=True)[mis:mis + hsz] for _ in range(2)]
+    ds = [torch.empty(chunk + 4096, dtype=torch.uint8, device="cuda")[mis:mis + chunk] for _ in range(2)]
     s_in, s_out = torch.cuda.Stream(), torch.cuda.Stream()
     best = None
     for _ in range(reps):
@@ -40,7 +42,7 @@ def rate(chunk: int, h2d: bool, d2h: bool, reps: int = 3, stream_host: bool = Fa
         ms = e0.elapsed_time(e1)
         best = ms if best is None else min(best, ms)
     gbs = n * chunk / (best * 1e-3) / 1e9
-    return {"chunk_MiB": chunk >> 20, "h2d": h2d, "d2h": d2h, "host_walk_GiB": hsz >> 30,
+    return {"chunk_MiB": chunk >> 20, "h2d": h2d, "d2h": d2h, "host_walk_GiB": hsz >> 30, "misalign": mis,
             "GB_per_s_each_direction": round(gbs, 1)}
 
 
@@ -55,3 +57,7 @@ if __name__ == "__main__":
     for chunk in (64 << 20,):
         print(json.dumps(rate(chunk, True, True, stream_host=True, total=5 << 30)), flush=True)
         print(json.dumps(rate(chunk, True, False, stream_host=True, total=5 << 30)), flush=True)
+    # copies whose ends are only 4-B aligned (where a keyed batch's DMA runs start), one way and both
+    for mis in (4, 64, 256):
+        for h2d, d2h in ((True, False), (False, True), (True, True)):
+            print(json.dumps(rate(64 << 20, h2d, d2h, mis=mis)), flush=True)
