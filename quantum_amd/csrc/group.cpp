@@ -521,8 +521,10 @@ inline uint64_t rec_in(bool seal, uint32_t len) {  // bytes of a slot the call r
 // Runs of member packets idx[0..m) (input order, offsets nondecreasing over the whole batch): packet
 // idx[j] joins the run of idx[j-1] when it is the next input packet and its record starts at most
 // kRunGap bytes after the previous record ends.  Runs are cut into chunks of up to `chunk` staging
-// bytes at record boundaries; each piece keeps its arena offset mod 256 in staging (payload alignment).
-void plan_dma(bool seal, const qgcm_desc *descs, const uint32_t *idx, size_t m, uint64_t chunk, DmaPlan &pl) {
+// bytes at record boundaries; each piece keeps its host address mod 256 (`mis` = the arena's) in
+// staging: the payloads keep their alignment, and a piece's host and staging ends share 256-B boundaries.
+void plan_dma(bool seal, const qgcm_desc *descs, const uint32_t *idx, size_t m, uint64_t chunk, uint32_t mis,
+              DmaPlan &pl) {
     pl = DmaPlan{};
     pl.at.resize(m);
     uint64_t prev_end = 0;
@@ -540,12 +542,12 @@ void plan_dma(bool seal, const qgcm_desc *descs, const uint32_t *idx, size_t m, 
         }
         if (!joined) {
             uint64_t pos = pl.pieces.size() > p0 ? pl.pieces.back().dst + pl.pieces.back().bytes : 0;
-            pos += (r0 - pos) & 255;
+            pos += (r0 + mis - pos) & 255;
             if (j > j0 && pos + (r1 - r0) > chunk) {  // close the chunk
                 pl.chunks.push_back(DmaChunk{p0, pl.pieces.size(), j0, j, pos});
                 j0 = j;
                 p0 = pl.pieces.size();
-                pos = r0 & 255;
+                pos = (r0 + mis) & 255;
             }
             pl.pieces.push_back(Piece{r0, pos, r1 - r0});
         }
@@ -565,17 +567,38 @@ void plan_dma(bool seal, const qgcm_desc *descs, const uint32_t *idx, size_t m, 
     }
 }
 
-bool own_streams() {
-    static const bool own = [] {
-        const char *v = getenv("QGCM_GROUP_DMA_OWN_STREAMS");
-        return v && atoi(v) != 0;
-    }();
-    return own;
+bool env_flag(const char *name) {  // read per call (A/B and tests switch it within one process)
+    const char *v = getenv(name);
+    return v && atoi(v) != 0;
 }
 
-int dma_ready(DmaState &z, uint64_t stage, uint64_t side) {
+bool own_streams() { return env_flag("QGCM_GROUP_DMA_OWN_STREAMS"); }
+
+// QGCM_GROUP_DMA_SPLIT=1: each piece moves as up to three copies, an unaligned head, a 256-B aligned
+// body and a tail (A/B: a run starts wherever a record does, only 4-B aligned)
+bool split_copies() { return env_flag("QGCM_GROUP_DMA_SPLIT"); }
+
+// one piece's copy; host and device ends share their address mod 256 (plan_dma)
+hipError_t piece_copy(void *dst, const void *src, uint64_t bytes, hipMemcpyKind kind, hipStream_t s) {
+    if (!split_copies()) return hipMemcpyAsync(dst, src, bytes, kind, s);
+    const uintptr_t host = (uintptr_t)(kind == hipMemcpyHostToDevice ? src : dst);
+    const uint64_t head = std::min<uint64_t>(bytes, (256 - (host & 255)) & 255);
+    const uint64_t body = (bytes - head) & ~255ull, tail = bytes - head - body;
+    uint64_t o = 0;
+    for (uint64_t part : {head, body, tail}) {
+        if (part) {
+            const hipError_t e = hipMemcpyAsync(static_cast<uint8_t *>(dst) + o, static_cast<const uint8_t *>(src) + o,
+                                                part, kind, s);
+            if (e != hipSuccess) return e;
+        }
+        o += part;
+    }
+    return hipSuccess;
+}
+
+int dma_ready(DmaState &z, uint64_t stage, uint64_t side, bool own) {
     for (hipStream_t &x : z.s)
-        if (own_streams() && !x && hipStreamCreateWithFlags(&x, hipStreamNonBlocking) != hipSuccess) return QGCM_E_HIP;
+        if (own && !x && hipStreamCreateWithFlags(&x, hipStreamNonBlocking) != hipSuccess) return QGCM_E_HIP;
     for (int k = 0; k < kDmaSlots; ++k)
         for (hipEvent_t *e : {&z.ev_in[k], &z.ev_k[k], &z.ev_out[k]})
             if (!*e && hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return QGCM_E_HIP;
@@ -609,13 +632,14 @@ int run_member_dma(Member &mb, bool seal, uint8_t *h_arena, const qgcm_desc *des
     const uint64_t pk = pl.max_pk;
     const uint64_t off_non = (16ull * pk + 255) & ~255ull, off_st = off_non + (non ? (12ull * pk + 255) & ~255ull : 0);
     const uint64_t side = off_st + ((pk + 255) & ~255ull);
-    int rc = dma_ready(z, pl.max_bytes, side);
+    const bool own = own_streams();
+    int rc = dma_ready(z, pl.max_bytes, side, own);
     if (rc != QGCM_OK) return rc;
     // the member context's own pipeline streams (those qgcm_seal_host moves 46 GB/s each way with);
     // QGCM_GROUP_DMA_OWN_STREAMS=1: streams of the group's own (A/B)
     std::unique_lock<std::mutex> io(qgcm::ctx_io_mu(mb.ctx), std::defer_lock);
     hipStream_t s_in = z.s[0], s_k = z.s[1], s_out = z.s[2];
-    if (!own_streams()) {
+    if (!own) {
         io.lock();
         s_in = qgcm::ctx_pipe(mb.ctx, 0);
         s_k = qgcm::ctx_pipe(mb.ctx, 1);
@@ -654,7 +678,7 @@ int run_member_dma(Member &mb, bool seal, uint8_t *h_arena, const qgcm_desc *des
         if (hipStreamWaitEvent(s_in, z.ev_out[k], 0) != hipSuccess) rc = QGCM_E_HIP;
         for (size_t p = ch.p0; p < ch.p1 && rc == QGCM_OK; ++p) {
             const Piece &pc = pl.pieces[p];
-            if (hipMemcpyAsync(ds + pc.dst, h_arena + pc.src, pc.bytes, hipMemcpyHostToDevice, s_in) != hipSuccess)
+            if (piece_copy(ds + pc.dst, h_arena + pc.src, pc.bytes, hipMemcpyHostToDevice, s_in) != hipSuccess)
                 rc = QGCM_E_HIP;
         }
         if (rc == QGCM_OK &&
@@ -671,7 +695,7 @@ int run_member_dma(Member &mb, bool seal, uint8_t *h_arena, const qgcm_desc *des
             rc = QGCM_E_HIP;
         for (size_t p = ch.p0; p < ch.p1 && rc == QGCM_OK; ++p) {
             const Piece &pc = pl.pieces[p];
-            if (hipMemcpyAsync(h_arena + pc.src, ds + pc.dst, pc.bytes, hipMemcpyDeviceToHost, s_out) != hipSuccess)
+            if (piece_copy(h_arena + pc.src, ds + pc.dst, pc.bytes, hipMemcpyDeviceToHost, s_out) != hipSuccess)
                 rc = QGCM_E_HIP;
         }
         if (rc == QGCM_OK &&
@@ -720,6 +744,7 @@ int run_group(qgcm_group *g, bool seal, uint8_t *h_arena, const qgcm_desc *descs
     bool sorted = g->dma;
     for (uint32_t i = 1; sorted && i < n; ++i) sorted = descs[i].offset >= descs[i - 1].offset;
     for (uint32_t i = 0; sorted && i < n; ++i) sorted = !(descs[i].offset & 3);
+    sorted = sorted && !((uintptr_t)h_arena & 3);
     std::vector<DmaPlan> plan(G);
     std::vector<int> rc(G, QGCM_OK), bad(G, 0), used_zc(G, 1);
     std::vector<std::thread> thr;
@@ -734,7 +759,7 @@ int run_group(qgcm_group *g, bool seal, uint8_t *h_arena, const qgcm_desc *descs
             }
             if (sorted) {
                 const size_t m = part[k].size();
-                plan_dma(seal, descs, part[k].data(), m, kDmaChunk, plan[k]);
+                plan_dma(seal, descs, part[k].data(), m, kDmaChunk, (uint32_t)((uintptr_t)h_arena & 255), plan[k]);
                 if (plan[k].piece_bytes >= kMinRun * plan[k].pieces.size()) {
                     mb.last_path = 2;
                     used_zc[k] = 0;

@@ -135,14 +135,19 @@ def test_group_keyed_host_batch_vs_oracle(torch, G, pinned, threads, zc, dma, gr
         grp.close()
 
 
-def test_group_dma_runs_many_chunks_vs_oracle(torch):
-    """DMA-run path over more 64-MiB chunks than staging slots (slot reuse), two members on device 0 with
+@pytest.mark.parametrize("split,shift", [("0", 0), ("1", 0), ("1", 68)])
+def test_group_dma_runs_many_chunks_vs_oracle(torch, split, shift, monkeypatch):
+    """split: QGCM_GROUP_DMA_SPLIT (each run moves as an unaligned head, a 256-B aligned body and a tail);
+    shift: the arena starts this many bytes past the pinned allocation's start (staging keeps host
+    addresses mod 256, so the head/body/tail cut moves).
+    DMA-run path over more 64-MiB chunks than staging slots (slot reuse), two members on device 0 with
     the batch laid out member by member: 2^19 packets, the first half of 1184..1440 B in 1472-B
     Payload.Raw slots (gaps of up to 256 B inside a run; every 1000th slot 1 KiB further on, which breaks
     the run), the second half of U{0..2000} B in 16-B packed slots; sealed against the oracle, then opened
     back and every byte of the arena checked."""
     from quantum_amd import shard
 
+    monkeypatch.setenv("QGCM_GROUP_DMA_SPLIT", split)
     G, n = 2, 1 << 19  # ~660 MB of records: 5 chunks per member, more than its 4 staging slots
     grp = shard.Group([0] * G, max_keys=64)
     try:
@@ -162,7 +167,8 @@ def test_group_dma_runs_many_chunks_vs_oracle(torch):
         base = offs[n // 2 - 1] + np.uint64(1472)
         offs[n // 2:] = base + np.concatenate([[0], np.cumsum(rec[n // 2:])[:-1]]).astype(np.uint64)
         size = int(offs[-1] + rec[-1]) + 64
-        arena, aptr, free = host_buffer(size, True)
+        whole, wptr, free = host_buffer(size + shift, True)
+        arena, aptr = whole[shift:], wptr + shift
         nonces, nptr, free_n = host_buffer(12 * n, True)
         try:
             arena[:] = rng.integers(0, 256, size, dtype=np.uint8)
