@@ -158,11 +158,15 @@ for s in $STEPS; do
     hostlegs)  # the PCIe-inclusive bench legs, each in a fresh process, with the NUMA nodes of their pinned arenas
       timeout -k 10 600 python3 tools/exp_host_legs.py > $OUT/host_legs.jsonl 2> $OUT/host_legs.err
       check hostlegs $? ;;
-    dmaab)  # keyed host batch (DMA runs) on the member context's streams vs streams of its own, then e2e in the same process
-      for own in 0 1; do
-        QGCM_GROUP_DMA_OWN_STREAMS=$own timeout -k 10 400 python3 tools/exp_host_legs.py config3_host config3_host+e2e > $OUT/dmaab_own$own.jsonl 2>> $OUT/dmaab.err
-        check dmaab_own$own $?
+    dmaab)  # keyed host batch (DMA runs): member context's streams vs own streams vs split copies; then e2e in the same process
+      for v in "0 0" "1 0" "0 1"; do
+        set -- $v
+        QGCM_GROUP_DMA_OWN_STREAMS=$1 QGCM_GROUP_DMA_SPLIT=$2 timeout -k 10 400 python3 tools/exp_host_legs.py config3_host config3_host+e2e > $OUT/dmaab_own$1_split$2.jsonl 2>> $OUT/dmaab.err
+        check dmaab_own$1_split$2 $?
       done ;;
+    gtests)  # the group (multi-GPU drop-in) suite
+      timeout -k 10 600 python3 -u -m pytest tests/test_gpu_group.py -x -v --timeout 300 --timeout-method thread > $OUT/group_tests.txt 2>&1
+      check gtests $? ;;
     copytrace)  # copy / kernel timelines of the keyed host batch and the contiguous pipeline (is H2D overlapping D2H?)
       for leg in config3_host e2e; do
         timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $OUT/trace_$leg -o t -- python3 tools/run_leg.py $leg 2 > $OUT/trace_$leg.log 2>&1
