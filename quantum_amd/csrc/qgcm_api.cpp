@@ -1177,9 +1177,12 @@ static int run_snappy(qgcm_ctx *ctx, bool compress, uint8_t *d_arena, uint64_t s
     // pipelined, output straight into the slot (no LDS output area); 2 = the same with the output staged
     // in LDS; 1 = not pipelined; 0 = one wave per packet.  Packets past ~5 KiB need more LDS than four
     // regions per wave can have: one wave per packet.
-    int group = compress ? std::max(0, std::min(3, env_int("QGCM_SNAPPY_GROUP", 3))) : 0;
-    if (group == 3 && limit == 0) group = 2;
-    if (group == 3) {  // region: table + the input staged up to max(len, limit) bytes (the restore copy)
+    // the decoder (QGCM_SNAPPY_DEC_GROUP, A/B knob): 1 (default) = four packets per wave, 0 = one wave
+    // per packet; the same [input | output] region either way
+    int group = compress ? std::max(0, std::min(3, env_int("QGCM_SNAPPY_GROUP", 3)))
+                         : std::max(0, std::min(1, env_int("QGCM_SNAPPY_DEC_GROUP", 1)));
+    if (compress && group == 3 && limit == 0) group = 2;
+    if (compress && group == 3) {  // region: table + the input staged up to max(len, limit) bytes (the restore copy)
         a.off_out = a.off_in + a16(std::max(max_in, limit) + 24);
         a.off_sink = a.off_out;
     }
@@ -1193,7 +1196,7 @@ static int run_snappy(qgcm_ctx *ctx, bool compress, uint8_t *d_arena, uint64_t s
     int waves = group ? 1 : 4;
     while (waves > 1 && (size_t)waves * a.wave_bytes > 64u * 1024u) --waves;
     int per_cu = (int)((160u * 1024u) / ((uint32_t)waves * a.wave_bytes));
-    per_cu = std::max(1, std::min(per_cu, 8));
+    per_cu = std::max(1, std::min(per_cu, group ? 16 : 8));
     const uint64_t need = (n + (uint64_t)waves * per_wave - 1) / ((uint64_t)waves * per_wave);
     const int grid = (int)std::min<uint64_t>(need, (uint64_t)ctx->num_cus * per_cu);
     if (hipSetDevice(ctx->device) != hipSuccess) return QGCM_E_HIP;

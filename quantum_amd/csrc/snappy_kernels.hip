@@ -611,6 +611,133 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) s
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Group decoder: FOUR packets per wave, one per 16-lane group (QGCM_SNAPPY_DEC_GROUP, default 1).  The
+// wave decoder above parses each element's tag with wave-uniform scalar code, so like the wave encoder
+// it is bound by the CU's one scalar unit (~660 scalar instructions per config-5 packet).  Here each
+// group parses its own packet's stream in VGPRs (the same value in its 16 lanes) and one instruction
+// stream serves four packets.  Literals move 4 bytes per lane (64 B per group step); a back-reference
+// of length <= 64 is one to four steps: lane j of the group writes out[op + i] for i = j, j + 16, ...,
+// reading out[op - off + i % off], which an earlier element wrote (LDS operations of a wave complete
+// in order, and the regions of the four groups are disjoint).  Per packet: [staged input | output]
+// in LDS, a.off_sink bytes, four per wave.
+struct GDec {
+    uint8_t *in, *out;
+    uint32_t gl;
+    __device__ __forceinline__ uint32_t load32(uint32_t o) const {
+        const uint32_t *w = reinterpret_cast<const uint32_t *>(in);
+        return __builtin_amdgcn_alignbyte(w[(o >> 2) + 1], w[o >> 2], o & 3);
+    }
+};
+
+// decode.go Decode of in[0..n) into out (at most cap bytes), per group; returns the length or -1
+__device__ int gdecode(const GDec &w, uint32_t n, uint32_t cap) {
+    uint32_t total = 0, ip = 0;
+    for (uint32_t sh = 0;; sh += 7) {
+        if (ip >= n || ip >= 5) return -1;
+        const uint32_t c = w.in[ip++];
+        if (sh == 28 && (c & 0x7f) > 15) return -1;  // > 32 bits
+        total |= (c & 0x7f) << sh;
+        if (c < 0x80) break;
+    }
+    if (total > cap) return -1;
+    uint32_t op = 0;
+    while (ip < n) {
+        const uint32_t tag = w.in[ip++];
+        uint32_t len, off;
+        if ((tag & 3) == 0) {
+            len = tag >> 2;
+            if (len >= 60) {
+                const uint32_t b = len - 59;  // 1..4 little-endian length bytes
+                if (ip + b > n) return -1;
+                len = w.load32(ip) & (0xffffffffu >> (32 - 8 * b));
+                ip += b;
+                if (len >= 0xffffffffu) return -1;
+            }
+            ++len;
+            if (len > n - ip || len > total - op) return -1;
+            for (uint32_t j = 4 * w.gl; j < len; j += 4 * kGL) {  // 4 bytes per lane
+                const uint32_t v = w.load32(ip + j), k = len - j < 4 ? len - j : 4;
+                w.out[op + j] = (uint8_t)v;
+                if (k > 1) w.out[op + j + 1] = (uint8_t)(v >> 8);
+                if (k > 2) w.out[op + j + 2] = (uint8_t)(v >> 16);
+                if (k > 3) w.out[op + j + 3] = (uint8_t)(v >> 24);
+            }
+            ip += len;
+            op += len;
+            continue;
+        }
+        if ((tag & 3) == 1) {
+            if (ip + 1 > n) return -1;
+            len = 4 + ((tag >> 2) & 7);
+            off = ((tag >> 5) << 8) | w.in[ip];
+            ip += 1;
+        } else if ((tag & 3) == 2) {
+            if (ip + 2 > n) return -1;
+            len = 1 + (tag >> 2);
+            off = w.load32(ip) & 0xffffu;
+            ip += 2;
+        } else {
+            if (ip + 4 > n) return -1;
+            len = 1 + (tag >> 2);
+            off = w.load32(ip);
+            ip += 4;
+        }
+        if (off == 0 || off > op || len > total - op) return -1;
+        for (uint32_t i = w.gl; i < len; i += kGL) w.out[op + i] = w.out[op - off + (i < off ? i : i % off)];
+        op += len;
+    }
+    return op == total ? (int)total : -1;
+}
+
+__global__ void __launch_bounds__(256) snappy_uncompress_group_kernel(SnapArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint32_t lane = lane_id(), wv = threadIdx.x >> 6, waves = blockDim.x >> 6;
+    const uint32_t grp = lane / kGL, gl = lane % kGL;
+    uint8_t *base = smem + (wv * kGrp + grp) * a.off_sink;
+    const GDec w{base + a.off_in, base + a.off_out, gl};
+    const uint32_t step = gridDim.x * waves * kGrp;
+    for (uint32_t p0 = (blockIdx.x * waves + wv) * kGrp; p0 < a.n; p0 += step) {
+        const uint32_t p = p0 + grp;
+        const bool have = p < a.n;
+        const uint32_t stored = have ? a.lens[p] : 0u;
+        // status_in: packets that failed to open are left to the caller
+        const bool auth = have && (a.status_in ? a.status_in[p] == 1 : true);
+        const uint32_t len = stored >= a.sub ? stored - a.sub : stored;
+        uint8_t *slot = a.arena + (uint64_t)(have ? p : 0u) * a.stride;
+        const bool take = auth && stored >= a.sub && len <= a.max_in;
+        if (take) {  // slot bytes [4, 4 + len) -> LDS, whole dwords, then 8 B of zero slack
+            const uint32_t *src = reinterpret_cast<const uint32_t *>(slot + 4);
+            uint32_t *d = reinterpret_cast<uint32_t *>(w.in);
+            const uint32_t nw = (len + 3) >> 2;
+            for (uint32_t j = gl; j < nw; j += kGL) d[j] = src[j];
+            if (gl < 2) d[nw + gl] = 0;
+        }
+        wave_lds_sync();
+        int u = -1;
+        if (take) {
+            u = gdecode(w, len, a.limit);
+            // an empty result fails: golang/snappy's Decode(nil, src) returns a nil slice for it and
+            // compression.go:37-39 drops a nil packet
+            if (u == 0) u = -1;
+        }
+        wave_lds_sync();
+        if (u > 0) {  // LDS [0, u) -> slot bytes [4, 4 + u)
+            uint32_t *dst = reinterpret_cast<uint32_t *>(slot + 4);
+            const uint32_t *srcw = reinterpret_cast<const uint32_t *>(w.out);
+            const uint32_t nw = (uint32_t)u >> 2;
+            for (uint32_t j = gl; j < nw; j += kGL) dst[j] = srcw[j];
+            const uint32_t t = (uint32_t)u & 3;
+            if (gl < t) slot[4 + 4 * nw + gl] = w.out[4 * nw + gl];
+        }
+        if (auth && gl == 0) {
+            a.lens[p] = u > 0 ? (uint32_t)u : len;  // failed: the compressed length (sub = 0: unchanged)
+            if (a.status) a.status[p] = u > 0 ? 1 : 0;
+        }
+        wave_lds_sync();  // the next packets' staging overwrites these ones' LDS
+    }
+}
+
 }  // namespace
 
 hipError_t launch_snappy(bool compress, const SnapArgs &a, int waves_per_wg, int grid, hipStream_t s, int group) {
@@ -623,6 +750,8 @@ hipError_t launch_snappy(bool compress, const SnapArgs &a, int waves_per_wg, int
         hipLaunchKernelGGL((snappy_compress_group_kernel<false, false>), dim3(grid), dim3(64 * waves_per_wg), lds, s, a);
     else if (compress)
         hipLaunchKernelGGL(snappy_compress_kernel, dim3(grid), dim3(64 * waves_per_wg), lds, s, a);
+    else if (group)
+        hipLaunchKernelGGL(snappy_uncompress_group_kernel, dim3(grid), dim3(64 * waves_per_wg), lds, s, a);
     else
         hipLaunchKernelGGL(snappy_uncompress_kernel, dim3(grid), dim3(64 * waves_per_wg), lds, s, a);
     return hipGetLastError();

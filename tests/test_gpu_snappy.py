@@ -90,6 +90,14 @@ def encoder(request, monkeypatch):
     return request.param
 
 
+@pytest.fixture(params=["1", "0"], ids=["group_decoder", "wave_decoder"])
+def decoder(request, monkeypatch):
+    """QGCM_SNAPPY_DEC_GROUP (read per call): 1 = four packets per wave (the default), 0 = one wave per
+    packet.  Both must restore every packet and fail exactly where the host decoder fails."""
+    monkeypatch.setenv("QGCM_SNAPPY_DEC_GROUP", request.param)
+    return request.param
+
+
 def test_device_encoder_equals_libsnappy_golden(torch, ctx, encoder):
     with open(GOLDEN) as f:
         cases = [c for c in json.load(f)["cases"] if c["n"] <= DEV_MAX]
@@ -115,7 +123,7 @@ def test_device_encoder_equals_libsnappy_golden(torch, ctx, encoder):
         assert st2[i] == 1 and bl[i] == len(d) and back[i, 4:4 + len(d)].tobytes() == d
 
 
-def test_device_codec_config5_batch_vs_host(torch, ctx, encoder):
+def test_device_codec_config5_batch_vs_host(torch, ctx, encoder, decoder):
     """2^14 Payload.Raw slots (stride 1472): config 5's packet shape and a mix of lengths 0..1433
     and contents; device compress == host encoder (whole arena incl. untouched bytes, lengths), then
     device uncompress restores the plaintext arena."""
@@ -173,7 +181,7 @@ def test_device_compress_failures_untouched(torch, ctx, encoder):
         assert np.array_equal(out[i, 4 + len(c):], host[i, 4 + len(c):])  # past the output: untouched
 
 
-def test_device_uncompress_corrupted_streams_vs_host(torch, ctx):
+def test_device_uncompress_corrupted_streams_vs_host(torch, ctx, decoder):
     """Random corruption of valid streams (and truncations, bad varints, offsets before the output):
     the device decoder fails exactly where the host decoder does, and otherwise writes its bytes."""
     rng = np.random.default_rng(0x5EED0052)
@@ -204,7 +212,7 @@ def test_device_uncompress_corrupted_streams_vs_host(torch, ctx):
     assert st[-len(goods):].all()
 
 
-def test_device_uncompress_empty_result_fails(torch, ctx):
+def test_device_uncompress_empty_result_fails(torch, ctx, decoder):
     """b"\\x00" decodes to 0 bytes: golang/snappy's Decode returns a nil slice and compression.go:37-39
     drops the packet, so the device batch fails it (slot and length untouched), as the host slots do."""
     streams = [b"\x00", _host_compress(b"abcabcabc"), b"\x00"]

@@ -1,12 +1,13 @@
 """Device snappy codec rate on device-resident slots (config 5's packets: 2^20 x 1350 B, first half
 random, second half a repeated HTTP line, stride 1472): compress, seal, open, uncompress, each timed
 by HIP events; the sealed arena is checked against tests/golden/config5_digest.json and the result
-against the plaintext arena (bench.extra_config5_resident).  The encoder alternates between the
-four-packets-per-wave kernels (QGCM_SNAPPY_GROUP=3, 2, 1) and one wave per packet (0), in one process,
-`rounds` times each (3, the default: pipelined miss probes and the output written straight into the
-slot; 2: pipelined, output staged in LDS; 1: neither).
+against the plaintext arena (bench.extra_config5_resident).  Encoder / decoder pairs alternate in one
+process, `rounds` times each.  Encoders (QGCM_SNAPPY_GROUP): 3 four packets per wave, pipelined miss
+probes, output straight into the slot (the default); 2 the same with the output staged in LDS; 1 not
+pipelined; 0 one wave per packet.  Decoders (QGCM_SNAPPY_DEC_GROUP): 1 four packets per wave (the
+default), 0 one wave per packet.
 
-    python3 tools/exp_snappy_dev.py [reps] [rounds]
+    python3 tools/exp_snappy_dev.py [reps] [rounds] [enc:dec,...]     (default 5 2 3:1,3:0)
 """
 import json
 import os
@@ -20,13 +21,16 @@ import bench  # noqa: E402
 def main() -> None:
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 2
+    pairs = [p.split(":") for p in (sys.argv[3] if len(sys.argv) > 3 else "3:1,3:0").split(",")]
     key = bench.derive_key(bench.SECRET, bench.SALT)
     for r in range(rounds):
-        for grp in ("3", "2", "1", "0"):
-            os.environ["QGCM_SNAPPY_GROUP"] = grp
+        for enc, dec in pairs:
+            os.environ["QGCM_SNAPPY_GROUP"] = enc
+            os.environ["QGCM_SNAPPY_DEC_GROUP"] = dec
             res = bench.extra_config5_resident(key, reps, verify=(r == 0))
-            print(json.dumps({"snappy_group": int(grp), **res}), flush=True)
+            print(json.dumps({"snappy_group": int(enc), "snappy_dec_group": int(dec), **res}), flush=True)
     os.environ.pop("QGCM_SNAPPY_GROUP", None)
+    os.environ.pop("QGCM_SNAPPY_DEC_GROUP", None)
 
 
 if __name__ == "__main__":

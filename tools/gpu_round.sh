@@ -176,7 +176,11 @@ for s in $STEPS; do
     pcie)  # raw pinned-host <-> HBM hipMemcpyAsync rates of this box (the ceiling of every PCIe-inclusive figure)
       timeout -k 10 200 python3 tools/microbench/pcie.py > $OUT/pcie.json 2> $OUT/pcie.err
       check pcie $? ;;
-    snapab)  # device snappy encoder: four packets per wave vs one wave per packet, interleaved
+    profsnap3)  # device snappy counters: group encoder, group decoder and wave decoder
+      bash tools/profile_snappy.sh ${TAG}_s3 > $OUT/profsnap3.log 2>&1
+      check profsnap3 $?
+      python3 tools/pmc_kernels.py gpurun_out/prof_snappy_${TAG}_s3 1048576 snappy_compress_group snappy_uncompress_group snappy_uncompress_kernel > $OUT/snappy_pmc_s3.txt 2>&1 ;;
+    snapab)  # device snappy codec: group vs wave decoder behind the default encoder, interleaved
       timeout -k 10 300 python3 tools/exp_snappy_dev.py 5 2 > $OUT/snap_ab.jsonl 2> $OUT/snap_ab.err
       check snapab $? ;;
   esac
