@@ -1201,7 +1201,10 @@ static int run_snappy(qgcm_ctx *ctx, bool compress, uint8_t *d_arena, uint64_t s
     const int grid = (int)std::min<uint64_t>(need, (uint64_t)ctx->num_cus * per_cu);
     if (hipSetDevice(ctx->device) != hipSuccess) return QGCM_E_HIP;
     ctx->count(compress ? QGCM_KERNEL_SNAPPY_ENC : QGCM_KERNEL_SNAPPY_DEC);
-    return hip_fail(launch_snappy(compress, a, waves, grid, s, group));
+    // QGCM_SNAPPY_PREFETCH (A/B knob, default 1): the four-packets-per-wave kernels load the next
+    // packets' bytes while coding the current ones (the direct encoder and the group decoder)
+    const bool prefetch = env_int("QGCM_SNAPPY_PREFETCH", 1) != 0;
+    return hip_fail(launch_snappy(compress, a, waves, grid, s, group, prefetch));
 }
 
 int qgcm_snappy_compress_batch(qgcm_ctx *ctx, uint8_t *d_arena, uint64_t stride, uint32_t n, uint32_t *d_lens,

@@ -275,6 +275,52 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) s
 // (a.off_in / a.off_out within a region of a.off_sink bytes), four regions per wave.
 constexpr uint32_t kGrp = 4, kGL = 64 / kGrp;
 
+// Group prefetch (kPf): the next packets' first bytes -- kGPf 16-B loads per lane, 1.5 KiB per packet
+// -- and lengths are loaded into registers before the current packets are coded, so a packet's HBM
+// latency overlaps the previous packet's work instead of preceding its own (the wave kernels'
+// Prefetch, per group).  The loads stay inside the slot: cover = min(1.5 KiB, stride - 4 rounded down
+// to 16); bytes from cover on are staged with dword loads.
+constexpr uint32_t kGPf = 6;
+struct GPrefetch {
+    uint32_t len, st;
+    uint4 r[kGPf];
+};
+__device__ __forceinline__ uint32_t gpf_cover(uint64_t stride) {
+    const uint64_t whole = (stride - 4) & ~15ull;
+    return whole < 256 * kGPf ? (uint32_t)whole : 256 * kGPf;
+}
+__device__ __forceinline__ void gpf_issue(GPrefetch &f, const SnapArgs &a, uint32_t q, uint32_t gl, uint32_t cover) {
+    if (q >= a.n) return;
+    const uint8_t *src = a.arena + (uint64_t)q * a.stride + 4;
+    f.len = a.lens[q];
+    f.st = a.status_in ? a.status_in[q] : 1u;
+#pragma unroll
+    for (uint32_t k = 0; k < kGPf; ++k) {
+        const uint32_t o = 16 * gl + 256 * k;
+        f.r[k] = o < cover ? *reinterpret_cast<const uint4 *>(src + o) : uint4{0, 0, 0, 0};
+    }
+}
+// slot bytes [4, 4 + sn) -> LDS (kPf: the prefetched part, then whole dwords from cover on), then
+// 8 B of zero slack for load32 past the end; the staging area holds sn + 24 bytes
+template <bool kPf>
+__device__ __forceinline__ void gstage(uint8_t *dst, const uint8_t *slot, uint32_t sn, uint32_t gl, uint32_t cover,
+                                       const GPrefetch &f) {
+    uint32_t from = 0;
+    if constexpr (kPf) {
+#pragma unroll
+        for (uint32_t k = 0; k < kGPf; ++k) {
+            const uint32_t o = 16 * gl + 256 * k;
+            if (o < sn && o < cover) *reinterpret_cast<uint4 *>(dst + o) = f.r[k];
+        }
+        from = cover >> 2;
+    }
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(slot + 4);
+    uint32_t *d = reinterpret_cast<uint32_t *>(dst);
+    const uint32_t nw = (sn + 3) >> 2;
+    for (uint32_t j = from + gl; j < nw; j += kGL) d[j] = src[j];
+    if (gl < 2) d[nw + gl] = 0;  // after the 16-B stores above that may cover it (a wave's LDS ops run in order)
+}
+
 template <bool kDirect>
 struct GWave {
     uint8_t *in, *out;  // kDirect: out = the slot's packet bytes in device memory, else LDS staging
@@ -447,29 +493,26 @@ __device__ uint32_t gencode_block(const GWave<kDirect> &w, uint32_t op, uint32_t
 // instead of 7.2 for a 1472-B slot, 7 waves (28 packets) per CU instead of 5.  Output bytes past the
 // packet's limit all land on its last kept byte; a packet whose output exceeds the limit gets its
 // first `limit` slot bytes back from the staged copy (staged up to max(len, limit) bytes for that).
-template <bool kPipe, bool kDirect>
+template <bool kPipe, bool kDirect, bool kPf>
 __global__ void __launch_bounds__(256) snappy_compress_group_kernel(SnapArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t lane = lane_id(), wv = threadIdx.x >> 6, waves = blockDim.x >> 6;
     const uint32_t grp = lane / kGL, gl = lane % kGL;
     uint8_t *base = smem + (wv * kGrp + grp) * a.off_sink;
     GWave<kDirect> w{base + a.off_in, base + a.off_out, reinterpret_cast<uint16_t *>(base), gl, grp, 0u};
-    const uint32_t step = gridDim.x * waves * kGrp;
+    const uint32_t step = gridDim.x * waves * kGrp, cover = gpf_cover(a.stride);
+    GPrefetch f{};
+    if (kPf) gpf_issue(f, a, (blockIdx.x * waves + wv) * kGrp + grp, gl, cover);
     for (uint32_t p0 = (blockIdx.x * waves + wv) * kGrp; p0 < a.n; p0 += step) {
         const uint32_t p = p0 + grp;
         const bool have = p < a.n;
-        const uint32_t len = have ? a.lens[p] : 0u;
+        const uint32_t len = have ? (kPf ? f.len : a.lens[p]) : 0u;
         uint8_t *slot = a.arena + (uint64_t)(have ? p : 0u) * a.stride;
         bool ok = have && len <= a.max_in;
         // kDirect stages max(len, limit) bytes: the restore copy of a packet whose output overflows
         const uint32_t sn = kDirect ? max(len, a.limit) : len;
-        if (ok) {  // slot bytes [4, 4 + sn) -> LDS, whole dwords (the slot is 4-B aligned, stride a multiple of 4)
-            const uint32_t *src = reinterpret_cast<const uint32_t *>(slot + 4);
-            uint32_t *d = reinterpret_cast<uint32_t *>(w.in);
-            const uint32_t nw = (sn + 3) >> 2;
-            for (uint32_t j = gl; j < nw; j += kGL) d[j] = src[j];
-            if (gl < 2) d[nw + gl] = 0;  // slack read by load32 past the end
-        }
+        if (ok) gstage<kPf>(w.in, slot, sn, gl, cover, f);  // the slot is 4-B aligned, stride a multiple of 4
+        if (kPf) gpf_issue(f, a, p + step, gl, cover);      // in flight while these packets are coded
         if constexpr (kDirect) {
             w.out = slot + 4;
             w.olast = a.limit - 1;
@@ -690,29 +733,27 @@ __device__ int gdecode(const GDec &w, uint32_t n, uint32_t cap) {
     return op == total ? (int)total : -1;
 }
 
+template <bool kPf>
 __global__ void __launch_bounds__(256) snappy_uncompress_group_kernel(SnapArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t lane = lane_id(), wv = threadIdx.x >> 6, waves = blockDim.x >> 6;
     const uint32_t grp = lane / kGL, gl = lane % kGL;
     uint8_t *base = smem + (wv * kGrp + grp) * a.off_sink;
     const GDec w{base + a.off_in, base + a.off_out, gl};
-    const uint32_t step = gridDim.x * waves * kGrp;
+    const uint32_t step = gridDim.x * waves * kGrp, cover = gpf_cover(a.stride);
+    GPrefetch f{};
+    if (kPf) gpf_issue(f, a, (blockIdx.x * waves + wv) * kGrp + grp, gl, cover);
     for (uint32_t p0 = (blockIdx.x * waves + wv) * kGrp; p0 < a.n; p0 += step) {
         const uint32_t p = p0 + grp;
         const bool have = p < a.n;
-        const uint32_t stored = have ? a.lens[p] : 0u;
+        const uint32_t stored = have ? (kPf ? f.len : a.lens[p]) : 0u;
         // status_in: packets that failed to open are left to the caller
-        const bool auth = have && (a.status_in ? a.status_in[p] == 1 : true);
+        const bool auth = have && (kPf ? f.st == 1 : (a.status_in ? a.status_in[p] == 1 : true));
         const uint32_t len = stored >= a.sub ? stored - a.sub : stored;
         uint8_t *slot = a.arena + (uint64_t)(have ? p : 0u) * a.stride;
         const bool take = auth && stored >= a.sub && len <= a.max_in;
-        if (take) {  // slot bytes [4, 4 + len) -> LDS, whole dwords, then 8 B of zero slack
-            const uint32_t *src = reinterpret_cast<const uint32_t *>(slot + 4);
-            uint32_t *d = reinterpret_cast<uint32_t *>(w.in);
-            const uint32_t nw = (len + 3) >> 2;
-            for (uint32_t j = gl; j < nw; j += kGL) d[j] = src[j];
-            if (gl < 2) d[nw + gl] = 0;
-        }
+        if (take) gstage<kPf>(w.in, slot, len, gl, cover, f);
+        if (kPf) gpf_issue(f, a, p + step, gl, cover);  // in flight while these packets are decoded
         wave_lds_sync();
         int u = -1;
         if (take) {
@@ -740,20 +781,26 @@ __global__ void __launch_bounds__(256) snappy_uncompress_group_kernel(SnapArgs a
 
 }  // namespace
 
-hipError_t launch_snappy(bool compress, const SnapArgs &a, int waves_per_wg, int grid, hipStream_t s, int group) {
+hipError_t launch_snappy(bool compress, const SnapArgs &a, int waves_per_wg, int grid, hipStream_t s, int group,
+                         bool prefetch) {
     const size_t lds = (size_t)waves_per_wg * a.wave_bytes;
-    if (compress && group == 3)
-        hipLaunchKernelGGL((snappy_compress_group_kernel<true, true>), dim3(grid), dim3(64 * waves_per_wg), lds, s, a);
+    const dim3 g(grid), b(64 * waves_per_wg);
+    if (compress && group == 3 && prefetch)
+        hipLaunchKernelGGL((snappy_compress_group_kernel<true, true, true>), g, b, lds, s, a);
+    else if (compress && group == 3)
+        hipLaunchKernelGGL((snappy_compress_group_kernel<true, true, false>), g, b, lds, s, a);
     else if (compress && group == 2)
-        hipLaunchKernelGGL((snappy_compress_group_kernel<true, false>), dim3(grid), dim3(64 * waves_per_wg), lds, s, a);
+        hipLaunchKernelGGL((snappy_compress_group_kernel<true, false, false>), g, b, lds, s, a);
     else if (compress && group)
-        hipLaunchKernelGGL((snappy_compress_group_kernel<false, false>), dim3(grid), dim3(64 * waves_per_wg), lds, s, a);
+        hipLaunchKernelGGL((snappy_compress_group_kernel<false, false, false>), g, b, lds, s, a);
     else if (compress)
-        hipLaunchKernelGGL(snappy_compress_kernel, dim3(grid), dim3(64 * waves_per_wg), lds, s, a);
+        hipLaunchKernelGGL(snappy_compress_kernel, g, b, lds, s, a);
+    else if (group && prefetch)
+        hipLaunchKernelGGL(snappy_uncompress_group_kernel<true>, g, b, lds, s, a);
     else if (group)
-        hipLaunchKernelGGL(snappy_uncompress_group_kernel, dim3(grid), dim3(64 * waves_per_wg), lds, s, a);
+        hipLaunchKernelGGL(snappy_uncompress_group_kernel<false>, g, b, lds, s, a);
     else
-        hipLaunchKernelGGL(snappy_uncompress_kernel, dim3(grid), dim3(64 * waves_per_wg), lds, s, a);
+        hipLaunchKernelGGL(snappy_uncompress_kernel, g, b, lds, s, a);
     return hipGetLastError();
 }
 

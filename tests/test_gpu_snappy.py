@@ -80,21 +80,27 @@ def _match(case, comp: bytes) -> bool:
     return hashlib.sha256(comp).hexdigest() == case["out_sha256"]
 
 
-@pytest.fixture(params=["3", "2", "1", "0"], ids=["group_direct", "group_pipelined", "group_encoder", "wave_encoder"])
+@pytest.fixture(params=["3", "3:0", "2", "1", "0"],
+                ids=["group_direct", "group_direct_noprefetch", "group_pipelined", "group_encoder", "wave_encoder"])
 def encoder(request, monkeypatch):
     """QGCM_SNAPPY_GROUP (read per call): 3 = four packets per wave, pipelined miss probes, output
-    straight into the slot (the default); 2 = the same with the output staged in LDS; 1 = not pipelined;
-    0 = one wave per packet.  All must give the host encoder's (and libsnappy's) bytes, and leave a
-    failing packet's slot untouched."""
-    monkeypatch.setenv("QGCM_SNAPPY_GROUP", request.param)
+    straight into the slot, the next packets prefetched (the default; ":0" sets QGCM_SNAPPY_PREFETCH=0);
+    2 = pipelined, output staged in LDS; 1 = not pipelined; 0 = one wave per packet.  All must give the
+    host encoder's (and libsnappy's) bytes, and leave a failing packet's slot untouched."""
+    grp, _, pf = request.param.partition(":")
+    monkeypatch.setenv("QGCM_SNAPPY_GROUP", grp)
+    monkeypatch.setenv("QGCM_SNAPPY_PREFETCH", pf or "1")
     return request.param
 
 
-@pytest.fixture(params=["1", "0"], ids=["group_decoder", "wave_decoder"])
+@pytest.fixture(params=["1", "1:0", "0"], ids=["group_decoder", "group_decoder_noprefetch", "wave_decoder"])
 def decoder(request, monkeypatch):
-    """QGCM_SNAPPY_DEC_GROUP (read per call): 1 = four packets per wave (the default), 0 = one wave per
-    packet.  Both must restore every packet and fail exactly where the host decoder fails."""
-    monkeypatch.setenv("QGCM_SNAPPY_DEC_GROUP", request.param)
+    """QGCM_SNAPPY_DEC_GROUP (read per call): 1 = four packets per wave, the next packets prefetched
+    (the default; ":0" sets QGCM_SNAPPY_PREFETCH=0), 0 = one wave per packet.  All must restore every
+    packet and fail exactly where the host decoder fails."""
+    grp, _, pf = request.param.partition(":")
+    monkeypatch.setenv("QGCM_SNAPPY_DEC_GROUP", grp)
+    monkeypatch.setenv("QGCM_SNAPPY_PREFETCH", pf or "1")
     return request.param
 
 
