@@ -8,7 +8,7 @@ pipelined; 0 one wave per packet.  Decoders (QGCM_SNAPPY_DEC_GROUP): 1 four pack
 default), 0 one wave per packet.  The third field sets QGCM_SNAPPY_PREFETCH (the group kernels load
 the next packets while coding the current ones; default 1).
 
-    python3 tools/exp_snappy_dev.py [reps] [rounds] [enc:dec:pf,...]   (default 5 2 3:1:1,3:1:0,3:0:0)
+    python3 tools/exp_snappy_dev.py [reps] [rounds] [enc:dec:pf,...]   (default 5 2 3:1:1,3:0:1,3:1:0)
 """
 import json
 import os
@@ -22,7 +22,7 @@ import bench  # noqa: E402
 def main() -> None:
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 2
-    pairs = [(p.split(":") + ["1"])[:3] for p in (sys.argv[3] if len(sys.argv) > 3 else "3:1:1,3:1:0,3:0:0").split(",")]
+    pairs = [(p.split(":") + ["1"])[:3] for p in (sys.argv[3] if len(sys.argv) > 3 else "3:1:1,3:0:1,3:1:0").split(",")]
     key = bench.derive_key(bench.SECRET, bench.SALT)
     for r in range(rounds):
         for enc, dec, pf in pairs:
