@@ -164,6 +164,9 @@ for s in $STEPS; do
         QGCM_GROUP_DMA_OWN_STREAMS=$1 QGCM_GROUP_DMA_SPLIT=$2 timeout -k 10 400 python3 tools/exp_host_legs.py config3_host config3_host+e2e > $OUT/dmaab_own$1_split$2.jsonl 2>> $OUT/dmaab.err
         check dmaab_own$1_split$2 $?
       done ;;
+    legorder)  # does a leg that ran before it slow the pinned-host e2e leg in one process (the bench's order)?
+      timeout -k 10 600 python3 tools/exp_host_legs.py e2e config4_one_gpu+e2e config3_host+config4_one_gpu+e2e > $OUT/legorder.jsonl 2> $OUT/legorder.err
+      check legorder $? ;;
     gtests)  # the group (multi-GPU drop-in) suite
       timeout -k 10 600 python3 -u -m pytest tests/test_gpu_group.py -x -v --timeout 300 --timeout-method thread > $OUT/group_tests.txt 2>&1
       check gtests $? ;;
