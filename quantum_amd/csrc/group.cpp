@@ -70,7 +70,7 @@ constexpr uint64_t kZcChunk = 256ull << 20; // zero-copy path (device staging): 
 constexpr int kSlots = 2;                 // staging slots per member (double buffer)
 constexpr int kCopyThreads = 4;           // gather/scatter threads per member (QGCM_GROUP_THREADS)
 constexpr uint64_t kDmaChunk = 64ull << 20; // DMA-run path: staged bytes per chunk (qgcm_seal_host's size)
-constexpr int kDmaSlots = 4;              // DMA-run path: staging slots in flight per member
+constexpr int kDmaSlots = 4;              // DMA-run path: staging slots in flight per member (QGCM_GROUP_DMA_SLOTS)
 constexpr uint64_t kRunGap = 256;         // largest gap between two records that still joins them in a run
 constexpr uint64_t kMinRun = 64ull << 10; // DMA-run path only when runs average at least this many bytes
 
@@ -164,9 +164,9 @@ struct ZC {
 // DMA-run path state of a member (grow-only)
 struct DmaState {
     hipStream_t s[3] = {};  // copy-in, kernels, copy-out
-    hipEvent_t ev_in[kDmaSlots] = {}, ev_k[kDmaSlots] = {}, ev_out[kDmaSlots] = {};
-    uint8_t *d_stage[kDmaSlots] = {};  // [records][descs][nonces][status] of one chunk
-    uint8_t *h_side[kDmaSlots] = {};   // pinned [descs][nonces][status] of one chunk
+    std::vector<hipEvent_t> ev_in, ev_k, ev_out;  // per staging slot
+    std::vector<uint8_t *> d_stage;  // [records][descs][nonces][status] of one chunk, stage_cap bytes each
+    std::vector<uint8_t *> h_side;   // pinned [descs][nonces][status] of one chunk, side_cap bytes each
     uint64_t stage_cap = 0, side_cap = 0;
 };
 
@@ -596,31 +596,40 @@ hipError_t piece_copy(void *dst, const void *src, uint64_t bytes, hipMemcpyKind 
     return hipSuccess;
 }
 
-int dma_ready(DmaState &z, uint64_t stage, uint64_t side, bool own) {
+int dma_ready(DmaState &z, uint64_t stage, uint64_t side, bool own, size_t slots) {
     for (hipStream_t &x : z.s)
         if (own && !x && hipStreamCreateWithFlags(&x, hipStreamNonBlocking) != hipSuccess) return QGCM_E_HIP;
-    for (int k = 0; k < kDmaSlots; ++k)
-        for (hipEvent_t *e : {&z.ev_in[k], &z.ev_k[k], &z.ev_out[k]})
-            if (!*e && hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return QGCM_E_HIP;
+    while (z.ev_in.size() < slots) {
+        hipEvent_t e[3] = {};
+        for (hipEvent_t &x : e)
+            if (hipEventCreateWithFlags(&x, hipEventDisableTiming) != hipSuccess) {
+                for (hipEvent_t y : e)
+                    if (y) hipEventDestroy(y);
+                return QGCM_E_HIP;
+            }
+        z.ev_in.push_back(e[0]);
+        z.ev_k.push_back(e[1]);
+        z.ev_out.push_back(e[2]);
+    }
     if (stage + side > z.stage_cap) {
-        for (auto &p : z.d_stage) {
-            if (p) hipFree(p);
-            p = nullptr;
-        }
-        z.stage_cap = 0;
-        for (auto &p : z.d_stage)
-            if (hipMalloc(&p, stage + side) != hipSuccess) return QGCM_E_NOMEM;
+        for (uint8_t *p : z.d_stage) hipFree(p);
+        z.d_stage.clear();
         z.stage_cap = stage + side;
     }
+    while (z.d_stage.size() < slots) {
+        uint8_t *p = nullptr;
+        if (hipMalloc(&p, z.stage_cap) != hipSuccess) return QGCM_E_NOMEM;
+        z.d_stage.push_back(p);
+    }
     if (side > z.side_cap) {
-        for (auto &p : z.h_side) {
-            if (p) hipHostFree(p);
-            p = nullptr;
-        }
-        z.side_cap = 0;
-        for (auto &p : z.h_side)
-            if (hipHostMalloc(&p, side, hipHostMallocDefault) != hipSuccess) return QGCM_E_NOMEM;
+        for (uint8_t *p : z.h_side) hipHostFree(p);
+        z.h_side.clear();
         z.side_cap = side;
+    }
+    while (z.h_side.size() < slots) {
+        uint8_t *p = nullptr;
+        if (hipHostMalloc(&p, z.side_cap, hipHostMallocDefault) != hipSuccess) return QGCM_E_NOMEM;
+        z.h_side.push_back(p);
     }
     return QGCM_OK;
 }
@@ -633,7 +642,10 @@ int run_member_dma(Member &mb, bool seal, uint8_t *h_arena, const qgcm_desc *des
     const uint64_t off_non = (16ull * pk + 255) & ~255ull, off_st = off_non + (non ? (12ull * pk + 255) & ~255ull : 0);
     const uint64_t side = off_st + ((pk + 255) & ~255ull);
     const bool own = own_streams();
-    int rc = dma_ready(z, pl.max_bytes, side, own);
+    const char *sv = getenv("QGCM_GROUP_DMA_SLOTS");  // A/B knob: staging slots (chunks in flight)
+    const size_t nc = pl.chunks.size();
+    const size_t S = std::min<size_t>(nc, (size_t)std::max(2, std::min(64, sv && *sv ? atoi(sv) : kDmaSlots)));
+    int rc = dma_ready(z, pl.max_bytes, side, own, S);
     if (rc != QGCM_OK) return rc;
     // the member context's own pipeline streams (those qgcm_seal_host moves 46 GB/s each way with);
     // QGCM_GROUP_DMA_OWN_STREAMS=1: streams of the group's own (A/B)
@@ -654,17 +666,16 @@ int run_member_dma(Member &mb, bool seal, uint8_t *h_arena, const qgcm_desc *des
             if (h_status) h_status[idx[j]] = st[j - c.j0];
         }
     };
-    const size_t nc = pl.chunks.size();
     size_t c = 0;
     for (; c < nc && rc == QGCM_OK; ++c) {
-        const int k = (int)(c % kDmaSlots);
+        const int k = (int)(c % S);
         const DmaChunk &ch = pl.chunks[c];
-        if (c >= (size_t)kDmaSlots) {  // slot k's previous chunk must have landed before its side area is reused
+        if (c >= S) {  // slot k's previous chunk must have landed before its side area is reused
             if (hipEventSynchronize(z.ev_out[k]) != hipSuccess) {
                 rc = QGCM_E_HIP;
                 break;
             }
-            retire(k, pl.chunks[c - kDmaSlots]);
+            retire(k, pl.chunks[c - S]);
         }
         uint8_t *hs = z.h_side[k], *ds = z.d_stage[k];
         const uint64_t dside = pl.max_bytes;  // descs / nonces / status behind the records
@@ -706,7 +717,7 @@ int run_member_dma(Member &mb, bool seal, uint8_t *h_arena, const qgcm_desc *des
     for (hipStream_t x : {s_in, s_k, s_out})
         if (hipStreamSynchronize(x) != hipSuccess && rc == QGCM_OK) rc = QGCM_E_HIP;
     if (rc == QGCM_OK)  // the chunks still in their slots
-        for (size_t q = c > (size_t)kDmaSlots ? c - kDmaSlots : 0; q < c; ++q) retire((int)(q % kDmaSlots), pl.chunks[q]);
+        for (size_t q = c > S ? c - S : 0; q < c; ++q) retire((int)(q % S), pl.chunks[q]);
     *bad_out = bad;
     return rc;
 }
@@ -850,12 +861,10 @@ void qgcm_group_destroy(qgcm_group *g) {
                 hipStreamSynchronize(x);
                 hipStreamDestroy(x);
             }
-        for (int k = 0; k < kDmaSlots; ++k) {
-            for (hipEvent_t e : {dm.ev_in[k], dm.ev_k[k], dm.ev_out[k]})
-                if (e) hipEventDestroy(e);
-            if (dm.d_stage[k]) hipFree(dm.d_stage[k]);
-            if (dm.h_side[k]) hipHostFree(dm.h_side[k]);
-        }
+        for (size_t k = 0; k < dm.ev_in.size(); ++k)
+            for (hipEvent_t e : {dm.ev_in[k], dm.ev_k[k], dm.ev_out[k]}) hipEventDestroy(e);
+        for (uint8_t *p : dm.d_stage) hipFree(p);
+        for (uint8_t *p : dm.h_side) hipHostFree(p);
         qgcm_destroy(mb.ctx);
     }
     delete g;

@@ -158,11 +158,11 @@ for s in $STEPS; do
     hostlegs)  # the PCIe-inclusive bench legs, each in a fresh process, with the NUMA nodes of their pinned arenas
       timeout -k 10 600 python3 tools/exp_host_legs.py > $OUT/host_legs.jsonl 2> $OUT/host_legs.err
       check hostlegs $? ;;
-    dmaab)  # keyed host batch (DMA runs): member context's streams vs own streams vs split copies; then e2e in the same process
-      for v in "0 0" "1 0" "0 1"; do
+    dmaab)  # keyed host batch (DMA runs): member context's streams vs own streams, split copies, staging slots; then e2e in the same process
+      for v in "0 0 4" "1 0 4" "0 1 4" "0 0 16" "0 0 64"; do
         set -- $v
-        QGCM_GROUP_DMA_OWN_STREAMS=$1 QGCM_GROUP_DMA_SPLIT=$2 timeout -k 10 400 python3 tools/exp_host_legs.py config3_host config3_host+e2e > $OUT/dmaab_own$1_split$2.jsonl 2>> $OUT/dmaab.err
-        check dmaab_own$1_split$2 $?
+        QGCM_GROUP_DMA_OWN_STREAMS=$1 QGCM_GROUP_DMA_SPLIT=$2 QGCM_GROUP_DMA_SLOTS=$3 timeout -k 10 400 python3 tools/exp_host_legs.py config3_host > $OUT/dmaab_own$1_split$2_slots$3.jsonl 2>> $OUT/dmaab.err
+        check dmaab_own$1_split$2_slots$3 $?
       done ;;
     legorder)  # does a leg that ran before it slow the pinned-host e2e leg in one process (the bench's order)?
       timeout -k 10 600 python3 tools/exp_host_legs.py e2e config4_one_gpu+e2e config3_host+config4_one_gpu+e2e > $OUT/legorder.jsonl 2> $OUT/legorder.err
