@@ -135,9 +135,11 @@ def test_group_keyed_host_batch_vs_oracle(torch, G, pinned, threads, zc, dma, gr
         grp.close()
 
 
-@pytest.mark.parametrize("split,shift", [("0", 0), ("1", 0), ("1", 68)])
-def test_group_dma_runs_many_chunks_vs_oracle(torch, split, shift, monkeypatch):
-    """split: QGCM_GROUP_DMA_SPLIT (each run moves as an unaligned head, a 256-B aligned body and a tail);
+@pytest.mark.parametrize("split,shift,slots", [("0", 0, "4"), ("1", 0, "4"), ("1", 68, "4"), ("0", 0, "2"),
+                                               ("0", 0, "16")])
+def test_group_dma_runs_many_chunks_vs_oracle(torch, split, shift, slots, monkeypatch):
+    """slots: QGCM_GROUP_DMA_SLOTS, staging slots in flight (2: every slot reused twice; 16: none reused);
+    split: QGCM_GROUP_DMA_SPLIT (each run moves as an unaligned head, a 256-B aligned body and a tail);
     shift: the arena starts this many bytes past the pinned allocation's start (staging keeps host
     addresses mod 256, so the head/body/tail cut moves).
     DMA-run path over more 64-MiB chunks than staging slots (slot reuse), two members on device 0 with
@@ -148,6 +150,7 @@ def test_group_dma_runs_many_chunks_vs_oracle(torch, split, shift, monkeypatch):
     from quantum_amd import shard
 
     monkeypatch.setenv("QGCM_GROUP_DMA_SPLIT", split)
+    monkeypatch.setenv("QGCM_GROUP_DMA_SLOTS", slots)
     G, n = 2, 1 << 19  # ~660 MB of records: 5 chunks per member, more than its 4 staging slots
     grp = shard.Group([0] * G, max_keys=64)
     try:
