@@ -69,7 +69,7 @@ constexpr uint64_t kZcChunk = 256ull << 20; // zero-copy path (device staging): 
                                             // chunk to fill the GPU (a 32-MB chunk is ~1500 tiles)
 constexpr int kSlots = 2;                 // staging slots per member (double buffer)
 constexpr int kCopyThreads = 4;           // gather/scatter threads per member (QGCM_GROUP_THREADS)
-constexpr uint64_t kDmaChunk = 64ull << 20; // DMA-run path: staged bytes per chunk (qgcm_seal_host's size)
+constexpr uint64_t kDmaChunk = 64ull << 20; // DMA-run path: staged bytes per chunk (QGCM_GROUP_DMA_CHUNK_MB)
 constexpr int kDmaSlots = 4;              // DMA-run path: staging slots in flight per member (QGCM_GROUP_DMA_SLOTS)
 constexpr uint64_t kRunGap = 256;         // largest gap between two records that still joins them in a run
 constexpr uint64_t kMinRun = 64ull << 10; // DMA-run path only when runs average at least this many bytes
@@ -757,6 +757,8 @@ int run_group(qgcm_group *g, bool seal, uint8_t *h_arena, const qgcm_desc *descs
     for (uint32_t i = 0; sorted && i < n; ++i) sorted = !(descs[i].offset & 3);
     sorted = sorted && !((uintptr_t)h_arena & 3);
     std::vector<DmaPlan> plan(G);
+    const char *cv = getenv("QGCM_GROUP_DMA_CHUNK_MB");  // A/B knob: staged bytes per DMA chunk
+    const uint64_t dma_chunk = cv && *cv ? (uint64_t)std::max(1, std::min(4096, atoi(cv))) << 20 : kDmaChunk;
     std::vector<int> rc(G, QGCM_OK), bad(G, 0), used_zc(G, 1);
     std::vector<std::thread> thr;
     for (int k = 0; k < G; ++k) {
@@ -770,7 +772,7 @@ int run_group(qgcm_group *g, bool seal, uint8_t *h_arena, const qgcm_desc *descs
             }
             if (sorted) {
                 const size_t m = part[k].size();
-                plan_dma(seal, descs, part[k].data(), m, kDmaChunk, (uint32_t)((uintptr_t)h_arena & 255), plan[k]);
+                plan_dma(seal, descs, part[k].data(), m, dma_chunk, (uint32_t)((uintptr_t)h_arena & 255), plan[k]);
                 if (plan[k].piece_bytes >= kMinRun * plan[k].pieces.size()) {
                     mb.last_path = 2;
                     used_zc[k] = 0;

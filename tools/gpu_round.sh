@@ -164,6 +164,12 @@ for s in $STEPS; do
         QGCM_GROUP_DMA_OWN_STREAMS=$1 QGCM_GROUP_DMA_SPLIT=$2 QGCM_GROUP_DMA_SLOTS=$3 timeout -k 10 400 python3 tools/exp_host_legs.py config3_host > $OUT/dmaab_own$1_split$2_slots$3.jsonl 2>> $OUT/dmaab.err
         check dmaab_own$1_split$2_slots$3 $?
       done ;;
+    dmachunk)  # keyed host batch (DMA runs): chunk size (per-chunk descriptor-batch overhead vs pipeline depth)
+      for v in "64 4" "128 4" "256 4" "512 4" "256 8"; do
+        set -- $v
+        QGCM_GROUP_DMA_CHUNK_MB=$1 QGCM_GROUP_DMA_SLOTS=$2 timeout -k 10 400 python3 tools/exp_host_legs.py config3_host > $OUT/dmachunk_$1_$2.jsonl 2>> $OUT/dmachunk.err
+        check dmachunk_$1_$2 $?
+      done ;;
     legorder)  # does a leg that ran before it slow the pinned-host e2e leg in one process (the bench's order)?
       timeout -k 10 600 python3 tools/exp_host_legs.py e2e config4_one_gpu+e2e config3_host+config4_one_gpu+e2e > $OUT/legorder.jsonl 2> $OUT/legorder.err
       check legorder $? ;;
@@ -176,6 +182,9 @@ for s in $STEPS; do
         check trace_$leg $?
         python3 tools/copy_trace_summary.py $OUT/trace_$leg > $OUT/copy_summary_$leg.txt 2>&1
       done ;;
+    pcieaf)  # PCIe copy rates before and after a 90-GB HBM allocation is freed in the same process
+      timeout -k 10 300 python3 tools/microbench/pcie.py --after-free 90 > $OUT/pcie_after_free.jsonl 2> $OUT/pcie_af.err
+      check pcieaf $? ;;
     pcie)  # raw pinned-host <-> HBM hipMemcpyAsync rates of this box (the ceiling of every PCIe-inclusive figure)
       timeout -k 10 200 python3 tools/microbench/pcie.py > $OUT/pcie.json 2> $OUT/pcie.err
       check pcie $? ;;

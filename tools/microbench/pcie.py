@@ -1,7 +1,7 @@
 """PCIe copy ceiling on the GPU box: pinned host <-> HBM hipMemcpyAsync rates, one direction at a time
 and both directions at once (two streams), for the chunk sizes qgcm_seal_host pipelines with.
 The e2e rows of DESIGN.md section 5 are read against these numbers.
-Usage: python tools/microbench/pcie.py
+Usage: python tools/microbench/pcie.py [--after-free GB]
 """
 import json
 
@@ -46,7 +46,26 @@ def rate(chunk: int, h2d: bool, d2h: bool, reps: int = 3, stream_host: bool = Fa
             "GB_per_s_each_direction": round(gbs, 1)}
 
 
+def after_free(gb: float) -> None:
+    """Allocate `gb` GB of HBM through torch, touch it, free it (empty_cache), then rerun a few rows:
+    does a huge allocation freed earlier in the process slow later PCIe copies (bench.py runs config 4's
+    94.5-GB arena before the pinned-host legs)?"""
+    x = torch.empty(int(gb * 1e9), dtype=torch.uint8, device="cuda")
+    x.fill_(1)
+    torch.cuda.synchronize()
+    del x
+    torch.cuda.empty_cache()
+    for h2d, d2h in ((True, False), (False, True), (True, True)):
+        print(json.dumps({"after_free_GB": gb, **rate(64 << 20, h2d, d2h)}), flush=True)
+
+
 if __name__ == "__main__":
+    import sys
+    if len(sys.argv) > 2 and sys.argv[1] == "--after-free":
+        for h2d, d2h in ((True, False), (False, True), (True, True)):
+            print(json.dumps({"after_free_GB": 0, **rate(64 << 20, h2d, d2h)}), flush=True)
+        after_free(float(sys.argv[2]))
+        sys.exit(0)
     for chunk in (8 << 20, 32 << 20, 128 << 20):
         for h2d, d2h in ((True, False), (False, True), (True, True)):
             print(json.dumps(rate(chunk, h2d, d2h)), flush=True)
