@@ -185,8 +185,7 @@ struct SnapArgs {
 // packet regions of a.off_sink bytes); 2 = the same with software-pipelined miss probes; 0 = one wave
 // per packet
 constexpr uint32_t kSnapGroup = 4;
-hipError_t launch_snappy(bool compress, const SnapArgs &a, int waves_per_wg, int grid, hipStream_t s, int group,
-                         bool prefetch);
+hipError_t launch_snappy(bool compress, const SnapArgs &a, int waves_per_wg, int grid, hipStream_t s, bool group);
 
 hipError_t launch_pw_setup(uint32_t first, uint32_t count, const uint4 *gh_table, uint4 *pw, uint32_t pw_keys,
                            hipStream_t s);

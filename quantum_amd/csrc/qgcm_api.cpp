@@ -1173,38 +1173,31 @@ static int run_snappy(qgcm_ctx *ctx, bool compress, uint8_t *d_arena, uint64_t s
     a.off_in = tab;
     a.off_out = a.off_in + a16(max_in + 24);  // + the 16-B chunks' overhang and stage_in's slack dwords
     a.off_sink = a.off_out + a16((compress ? (uint32_t)qgcm_snappy_max_compressed_length(max_in) : limit) + 8);
-    // the encoder (QGCM_SNAPPY_GROUP, A/B knob): 3 (default) = four packets per wave, miss probes
-    // pipelined, output straight into the slot (no LDS output area); 2 = the same with the output staged
-    // in LDS; 1 = not pipelined; 0 = one wave per packet.  Packets past ~5 KiB need more LDS than four
-    // regions per wave can have: one wave per packet.
-    // the decoder (QGCM_SNAPPY_DEC_GROUP, A/B knob): 1 (default) = four packets per wave, 0 = one wave
-    // per packet; the same [input | output] region either way
-    int group = compress ? std::max(0, std::min(3, env_int("QGCM_SNAPPY_GROUP", 3)))
-                         : std::max(0, std::min(1, env_int("QGCM_SNAPPY_DEC_GROUP", 1)));
-    if (compress && group == 3 && limit == 0) group = 2;
-    if (compress && group == 3) {  // region: table + the input staged up to max(len, limit) bytes (the restore copy)
+    // the encoder (QGCM_SNAPPY_GROUP, A/B knob): 1 (default) = four packets per wave, output straight
+    // into the slot (the region: table + the input staged up to max(len, limit) bytes, the restore
+    // copy); 0 = one wave per packet.  Packets past ~5 KiB need more LDS than four regions per wave can
+    // have, and limit 0 fails every packet: one wave per packet.  The decoder is one wave per packet.
+    bool group = compress && limit > 0 && env_int("QGCM_SNAPPY_GROUP", 1) != 0;
+    if (group) {
         a.off_out = a.off_in + a16(std::max(max_in, limit) + 24);
         a.off_sink = a.off_out;
-    }
-    if (kSnapGroup * a.off_sink > 160u * 1024u) group = 0;
-    if (group == 0) {  // the wave encoder's layout
-        a.off_out = a.off_in + a16(max_in + 24);
-        a.off_sink = a.off_out + a16((compress ? (uint32_t)qgcm_snappy_max_compressed_length(max_in) : limit) + 8);
+        if (kSnapGroup * a.off_sink > 160u * 1024u) {  // back to the wave encoder's layout
+            group = false;
+            a.off_out = a.off_in + a16(max_in + 24);
+            a.off_sink = a.off_out + a16((uint32_t)qgcm_snappy_max_compressed_length(max_in) + 8);
+        }
     }
     a.wave_bytes = group ? kSnapGroup * a.off_sink : a.off_sink + 256;
     const uint32_t per_wave = group ? kSnapGroup : 1;
     int waves = group ? 1 : 4;
     while (waves > 1 && (size_t)waves * a.wave_bytes > 64u * 1024u) --waves;
     int per_cu = (int)((160u * 1024u) / ((uint32_t)waves * a.wave_bytes));
-    per_cu = std::max(1, std::min(per_cu, group ? 16 : 8));
+    per_cu = std::max(1, std::min(per_cu, 8));
     const uint64_t need = (n + (uint64_t)waves * per_wave - 1) / ((uint64_t)waves * per_wave);
     const int grid = (int)std::min<uint64_t>(need, (uint64_t)ctx->num_cus * per_cu);
     if (hipSetDevice(ctx->device) != hipSuccess) return QGCM_E_HIP;
     ctx->count(compress ? QGCM_KERNEL_SNAPPY_ENC : QGCM_KERNEL_SNAPPY_DEC);
-    // QGCM_SNAPPY_PREFETCH (A/B knob, default 1): the four-packets-per-wave kernels load the next
-    // packets' bytes while coding the current ones (the direct encoder and the group decoder)
-    const bool prefetch = env_int("QGCM_SNAPPY_PREFETCH", 1) != 0;
-    return hip_fail(launch_snappy(compress, a, waves, grid, s, group, prefetch));
+    return hip_fail(launch_snappy(compress, a, waves, grid, s, group));
 }
 
 int qgcm_snappy_compress_batch(qgcm_ctx *ctx, uint8_t *d_arena, uint64_t stride, uint32_t n, uint32_t *d_lens,

@@ -269,13 +269,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) s
 // group runs encodeBlock on its own packet, and one instruction stream -- one set of scalar
 // instructions for the loop and its exec masks -- serves four packets.  Groups in different phases
 // (probing / emitting a copy run) diverge under exec masks; packets of a batch tend to move alike.
-// Every group lane stores the same byte to the same LDS address where the wave encoder let one lane
+// Every group lane stores the same byte to the same address where the wave encoder let one lane
 // store (no exec branch per store).  Match extension compares 4 bytes per lane (64 B per group step);
-// literal copies move 4 bytes per lane.  Per packet: [hash table | staged input | output] in LDS
-// (a.off_in / a.off_out within a region of a.off_sink bytes), four regions per wave.
+// literal copies move 4 bytes per lane.  Per packet: [hash table | staged input] in LDS (a.off_in
+// within a region of a.off_sink bytes), four regions per wave; the output goes straight into the slot.
+// The decoder stays one wave per packet: a four-packets-per-wave decoder measured no faster
+// (DESIGN.md 4.6).
 constexpr uint32_t kGrp = 4, kGL = 64 / kGrp;
 
-// Group prefetch (kPf): the next packets' first bytes -- kGPf 16-B loads per lane, 1.5 KiB per packet
+// Group prefetch: the next packets' first bytes -- kGPf 16-B loads per lane, 1.5 KiB per packet
 // -- and lengths are loaded into registers before the current packets are coded, so a packet's HBM
 // latency overlaps the previous packet's work instead of preceding its own (the wave kernels'
 // Prefetch, per group).  The loads stay inside the slot: cover = min(1.5 KiB, stride - 4 rounded down
@@ -300,40 +302,34 @@ __device__ __forceinline__ void gpf_issue(GPrefetch &f, const SnapArgs &a, uint3
         f.r[k] = o < cover ? *reinterpret_cast<const uint4 *>(src + o) : uint4{0, 0, 0, 0};
     }
 }
-// slot bytes [4, 4 + sn) -> LDS (kPf: the prefetched part, then whole dwords from cover on), then
-// 8 B of zero slack for load32 past the end; the staging area holds sn + 24 bytes
-template <bool kPf>
+// slot bytes [4, 4 + sn) -> LDS (the prefetched part, then whole dwords from cover on), then 8 B of
+// zero slack for load32 past the end; the staging area holds sn + 24 bytes
 __device__ __forceinline__ void gstage(uint8_t *dst, const uint8_t *slot, uint32_t sn, uint32_t gl, uint32_t cover,
                                        const GPrefetch &f) {
-    uint32_t from = 0;
-    if constexpr (kPf) {
 #pragma unroll
-        for (uint32_t k = 0; k < kGPf; ++k) {
-            const uint32_t o = 16 * gl + 256 * k;
-            if (o < sn && o < cover) *reinterpret_cast<uint4 *>(dst + o) = f.r[k];
-        }
-        from = cover >> 2;
+    for (uint32_t k = 0; k < kGPf; ++k) {
+        const uint32_t o = 16 * gl + 256 * k;
+        if (o < sn && o < cover) *reinterpret_cast<uint4 *>(dst + o) = f.r[k];
     }
     const uint32_t *src = reinterpret_cast<const uint32_t *>(slot + 4);
     uint32_t *d = reinterpret_cast<uint32_t *>(dst);
     const uint32_t nw = (sn + 3) >> 2;
-    for (uint32_t j = from + gl; j < nw; j += kGL) d[j] = src[j];
+    for (uint32_t j = (cover >> 2) + gl; j < nw; j += kGL) d[j] = src[j];
     if (gl < 2) d[nw + gl] = 0;  // after the 16-B stores above that may cover it (a wave's LDS ops run in order)
 }
 
-template <bool kDirect>
 struct GWave {
-    uint8_t *in, *out;  // kDirect: out = the slot's packet bytes in device memory, else LDS staging
+    uint8_t *in, *out;  // out = the slot's packet bytes in device memory
     uint16_t *tab;
     uint32_t gl, grp;  // lane within the group, group within the wave
-    uint32_t olast;    // kDirect: last output index kept inside the packet's limit (writes past it land there)
+    uint32_t olast;    // last output index kept inside the packet's limit (writes past it land there)
 
     __device__ __forceinline__ uint32_t load32(uint32_t o) const {
         const uint32_t *w = reinterpret_cast<const uint32_t *>(in);
         return __builtin_amdgcn_alignbyte(w[(o >> 2) + 1], w[o >> 2], o & 3);
     }
     __device__ __forceinline__ void put(uint32_t o, uint32_t v) const {
-        out[kDirect ? min(o, olast) : o] = (uint8_t)v;
+        out[min(o, olast)] = (uint8_t)v;
     }
     // out[op..op+len) = in[from..from+len): lane gl moves bytes 4 gl .. 4 gl + 3 of every 64
     __device__ __forceinline__ void copy_in(uint32_t op, uint32_t from, uint32_t len) const {
@@ -409,14 +405,14 @@ struct GWave {
     }
 };
 
-// kPipe: the miss probes are software-pipelined.  Probe positions do not depend on the data (each
-// miss moves on by skip >> 5, skip += step), so the word at the probe after next is loaded one probe
-// early and the next probe's table entry is read as soon as the current entry is written: a miss then
-// waits for one LDS round trip (the candidate's word) instead of two (the table entry, then the
-// candidate's word).  The early table read is issued after the current probe's table write (LDS
-// operations of a wave complete in order), so it sees that write; the bytes are those of encodeBlock.
-template <bool kPipe, bool kDirect>
-__device__ uint32_t gencode_block(const GWave<kDirect> &w, uint32_t op, uint32_t n, uint32_t bits) {
+// encodeBlock per group.  The miss probes are software-pipelined: probe positions do not depend on
+// the data (each miss moves on by skip >> 5, skip += step), so the word at the probe after next is
+// loaded one probe early and the next probe's table entry is read as soon as the current entry is
+// written.  A miss then waits for one LDS round trip (the candidate's word) instead of two (the table
+// entry, then the candidate's word).  The early table read is issued after the current probe's table
+// write (LDS operations of a wave complete in order), so it sees that write; the bytes are those of
+// encodeBlock.
+__device__ uint32_t gencode_block(const GWave &w, uint32_t op, uint32_t n, uint32_t bits) {
     const uint32_t shift = 32 - bits;
     uint4 *t16 = reinterpret_cast<uint4 *>(w.tab);  // 2 << bits bytes, a multiple of 256
     for (uint32_t j = w.gl; j < (2u << bits) / 16; j += kGL) t16[j] = uint4{0, 0, 0, 0};
@@ -424,38 +420,23 @@ __device__ uint32_t gencode_block(const GWave<kDirect> &w, uint32_t op, uint32_t
     const uint32_t s_limit = n - 15;
     uint32_t next_emit = 0, s = 1, skip = 32;
     uint32_t cur = w.load32(1), h = hash4(cur, shift);
-    uint32_t cand = 0, nv = 0;  // kPipe: tab[h] as of this probe, and the word at this probe's next_s
-    if (kPipe) {
-        cand = w.tab[h];
-        nv = w.load32(min(s + (skip >> 5), n));
-    }
+    uint32_t cand = w.tab[h];                       // tab[h] as of this probe
+    uint32_t nv = w.load32(min(s + (skip >> 5), n));  // the word at this probe's next_s
     for (;;) {
         const uint32_t step = skip >> 5, next_s = s + step;
         if (next_s > s_limit) break;
         skip += step;
-        if constexpr (kPipe) {
-            w.tab[h] = (uint16_t)s;
-            const uint32_t hn = hash4(nv, shift);
-            const uint32_t cn = w.tab[hn];  // after the write above: tab[hn] as the next probe sees it
-            const uint32_t nv2 = w.load32(min(next_s + (skip >> 5), n));  // the probe after next (clamped)
-            if (cur != w.load32(cand)) {  // miss: probe further on
-                s = next_s;
-                cur = nv;
-                h = hn;
-                cand = cn;
-                nv = nv2;
-                continue;
-            }
-        } else {
-            cand = w.tab[h];
-            w.tab[h] = (uint16_t)s;
-            nv = w.load32(next_s);
-            if (cur != w.load32(cand)) {  // miss: probe further on
-                s = next_s;
-                cur = nv;
-                h = hash4(nv, shift);
-                continue;
-            }
+        w.tab[h] = (uint16_t)s;
+        const uint32_t hn = hash4(nv, shift);
+        const uint32_t cn = w.tab[hn];  // after the write above: tab[hn] as the next probe sees it
+        const uint32_t nv2 = w.load32(min(next_s + (skip >> 5), n));  // the probe after next (clamped)
+        if (cur != w.load32(cand)) {  // miss: probe further on
+            s = next_s;
+            cur = nv;
+            h = hn;
+            cand = cn;
+            nv = nv2;
+            continue;
         }
         op = w.emit_literal(op, next_emit, s - next_emit);
         bool more;
@@ -478,45 +459,39 @@ __device__ uint32_t gencode_block(const GWave<kDirect> &w, uint32_t op, uint32_t
         skip = 32;
         cur = w.load32(s);
         h = hash4(cur, shift);
-        if (kPipe) {
-            wave_lds_sync();
-            cand = w.tab[h];
-            nv = w.load32(min(s + (skip >> 5), n));
-        }
+        wave_lds_sync();
+        cand = w.tab[h];
+        nv = w.load32(min(s + (skip >> 5), n));
     }
     if (next_emit < n) op = w.emit_literal(op, next_emit, n - next_emit);
     return op;
 }
 
-// kDirect: the output goes straight into the slot (its input is staged in LDS, so the slot is free to
-// overwrite), and a packet's LDS region holds only the hash table and the staged input -- 5.5 KiB
-// instead of 7.2 for a 1472-B slot, 7 waves (28 packets) per CU instead of 5.  Output bytes past the
-// packet's limit all land on its last kept byte; a packet whose output exceeds the limit gets its
-// first `limit` slot bytes back from the staged copy (staged up to max(len, limit) bytes for that).
-template <bool kPipe, bool kDirect, bool kPf>
+// The output goes straight into the slot (its input is staged in LDS, so the slot is free to
+// overwrite), and a packet's LDS region holds only the hash table and the staged input: 5.5 KiB for
+// a 1472-B slot, 7 waves (28 packets) per CU.  Output bytes past the packet's limit all land on its
+// last kept byte; a packet whose output exceeds the limit gets its first `limit` slot bytes back from
+// the staged copy (staged up to max(len, limit) bytes for that).  The next packets' first bytes are
+// prefetched into registers while these are coded (GPrefetch).
 __global__ void __launch_bounds__(256) snappy_compress_group_kernel(SnapArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t lane = lane_id(), wv = threadIdx.x >> 6, waves = blockDim.x >> 6;
     const uint32_t grp = lane / kGL, gl = lane % kGL;
     uint8_t *base = smem + (wv * kGrp + grp) * a.off_sink;
-    GWave<kDirect> w{base + a.off_in, base + a.off_out, reinterpret_cast<uint16_t *>(base), gl, grp, 0u};
+    GWave w{base + a.off_in, nullptr, reinterpret_cast<uint16_t *>(base), gl, grp, a.limit - 1};
     const uint32_t step = gridDim.x * waves * kGrp, cover = gpf_cover(a.stride);
     GPrefetch f{};
-    if (kPf) gpf_issue(f, a, (blockIdx.x * waves + wv) * kGrp + grp, gl, cover);
+    gpf_issue(f, a, (blockIdx.x * waves + wv) * kGrp + grp, gl, cover);
     for (uint32_t p0 = (blockIdx.x * waves + wv) * kGrp; p0 < a.n; p0 += step) {
         const uint32_t p = p0 + grp;
         const bool have = p < a.n;
-        const uint32_t len = have ? (kPf ? f.len : a.lens[p]) : 0u;
+        const uint32_t len = have ? f.len : 0u;
         uint8_t *slot = a.arena + (uint64_t)(have ? p : 0u) * a.stride;
         bool ok = have && len <= a.max_in;
-        // kDirect stages max(len, limit) bytes: the restore copy of a packet whose output overflows
-        const uint32_t sn = kDirect ? max(len, a.limit) : len;
-        if (ok) gstage<kPf>(w.in, slot, sn, gl, cover, f);  // the slot is 4-B aligned, stride a multiple of 4
-        if (kPf) gpf_issue(f, a, p + step, gl, cover);      // in flight while these packets are coded
-        if constexpr (kDirect) {
-            w.out = slot + 4;
-            w.olast = a.limit - 1;
-        }
+        // max(len, limit) bytes staged: the restore copy of a packet whose output overflows
+        if (ok) gstage(w.in, slot, max(len, a.limit), gl, cover, f);  // 4-B aligned slot, stride a multiple of 4
+        gpf_issue(f, a, p + step, gl, cover);                         // in flight while these packets are coded
+        w.out = slot + 4;
         wave_lds_sync();
         uint32_t d = 0;
         if (ok) {
@@ -531,11 +506,11 @@ __global__ void __launch_bounds__(256) snappy_compress_group_kernel(SnapArgs a) 
             } else {
                 uint32_t bits = 8;
                 while (bits < 14 && (1u << bits) < len) ++bits;
-                op = gencode_block<kPipe, kDirect>(w, op, len, bits);
+                op = gencode_block(w, op, len, bits);
             }
             d = op;
             ok = d <= a.limit;
-            if (kDirect && !ok) {  // overflowed: the slot's first `limit` bytes back from the staged copy
+            if (!ok) {  // overflowed: the slot's first `limit` bytes back from the staged copy
                 uint32_t *dst = reinterpret_cast<uint32_t *>(slot + 4);
                 const uint32_t *srcw = reinterpret_cast<const uint32_t *>(w.in);
                 const uint32_t nw = a.limit >> 2;
@@ -545,14 +520,6 @@ __global__ void __launch_bounds__(256) snappy_compress_group_kernel(SnapArgs a) 
             }
         }
         wave_lds_sync();
-        if (!kDirect && ok) {  // LDS [0, d) -> slot bytes [4, 4 + d)
-            uint32_t *dst = reinterpret_cast<uint32_t *>(slot + 4);
-            const uint32_t *srcw = reinterpret_cast<const uint32_t *>(w.out);
-            const uint32_t nw = d >> 2;
-            for (uint32_t j = gl; j < nw; j += kGL) dst[j] = srcw[j];
-            const uint32_t t = d & 3;
-            if (gl < t) slot[4 + 4 * nw + gl] = w.out[4 * nw + gl];
-        }
         if (have && gl == 0) {
             if (ok) a.lens[p] = d;
             if (a.status) a.status[p] = ok ? 1 : 0;
@@ -654,151 +621,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) s
     }
 }
 
-// ---------------------------------------------------------------------------------------------
-// Group decoder: FOUR packets per wave, one per 16-lane group (QGCM_SNAPPY_DEC_GROUP, default 1).  The
-// wave decoder above parses each element's tag with wave-uniform scalar code, so like the wave encoder
-// it is bound by the CU's one scalar unit (~660 scalar instructions per config-5 packet).  Here each
-// group parses its own packet's stream in VGPRs (the same value in its 16 lanes) and one instruction
-// stream serves four packets.  Literals move 4 bytes per lane (64 B per group step); a back-reference
-// of length <= 64 is one to four steps: lane j of the group writes out[op + i] for i = j, j + 16, ...,
-// reading out[op - off + i % off], which an earlier element wrote (LDS operations of a wave complete
-// in order, and the regions of the four groups are disjoint).  Per packet: [staged input | output]
-// in LDS, a.off_sink bytes, four per wave.
-struct GDec {
-    uint8_t *in, *out;
-    uint32_t gl;
-    __device__ __forceinline__ uint32_t load32(uint32_t o) const {
-        const uint32_t *w = reinterpret_cast<const uint32_t *>(in);
-        return __builtin_amdgcn_alignbyte(w[(o >> 2) + 1], w[o >> 2], o & 3);
-    }
-};
-
-// decode.go Decode of in[0..n) into out (at most cap bytes), per group; returns the length or -1
-__device__ int gdecode(const GDec &w, uint32_t n, uint32_t cap) {
-    uint32_t total = 0, ip = 0;
-    for (uint32_t sh = 0;; sh += 7) {
-        if (ip >= n || ip >= 5) return -1;
-        const uint32_t c = w.in[ip++];
-        if (sh == 28 && (c & 0x7f) > 15) return -1;  // > 32 bits
-        total |= (c & 0x7f) << sh;
-        if (c < 0x80) break;
-    }
-    if (total > cap) return -1;
-    uint32_t op = 0;
-    while (ip < n) {
-        const uint32_t tag = w.in[ip++];
-        uint32_t len, off;
-        if ((tag & 3) == 0) {
-            len = tag >> 2;
-            if (len >= 60) {
-                const uint32_t b = len - 59;  // 1..4 little-endian length bytes
-                if (ip + b > n) return -1;
-                len = w.load32(ip) & (0xffffffffu >> (32 - 8 * b));
-                ip += b;
-                if (len >= 0xffffffffu) return -1;
-            }
-            ++len;
-            if (len > n - ip || len > total - op) return -1;
-            for (uint32_t j = 4 * w.gl; j < len; j += 4 * kGL) {  // 4 bytes per lane
-                const uint32_t v = w.load32(ip + j), k = len - j < 4 ? len - j : 4;
-                w.out[op + j] = (uint8_t)v;
-                if (k > 1) w.out[op + j + 1] = (uint8_t)(v >> 8);
-                if (k > 2) w.out[op + j + 2] = (uint8_t)(v >> 16);
-                if (k > 3) w.out[op + j + 3] = (uint8_t)(v >> 24);
-            }
-            ip += len;
-            op += len;
-            continue;
-        }
-        if ((tag & 3) == 1) {
-            if (ip + 1 > n) return -1;
-            len = 4 + ((tag >> 2) & 7);
-            off = ((tag >> 5) << 8) | w.in[ip];
-            ip += 1;
-        } else if ((tag & 3) == 2) {
-            if (ip + 2 > n) return -1;
-            len = 1 + (tag >> 2);
-            off = w.load32(ip) & 0xffffu;
-            ip += 2;
-        } else {
-            if (ip + 4 > n) return -1;
-            len = 1 + (tag >> 2);
-            off = w.load32(ip);
-            ip += 4;
-        }
-        if (off == 0 || off > op || len > total - op) return -1;
-        for (uint32_t i = w.gl; i < len; i += kGL) w.out[op + i] = w.out[op - off + (i < off ? i : i % off)];
-        op += len;
-    }
-    return op == total ? (int)total : -1;
-}
-
-template <bool kPf>
-__global__ void __launch_bounds__(256) snappy_uncompress_group_kernel(SnapArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const uint32_t lane = lane_id(), wv = threadIdx.x >> 6, waves = blockDim.x >> 6;
-    const uint32_t grp = lane / kGL, gl = lane % kGL;
-    uint8_t *base = smem + (wv * kGrp + grp) * a.off_sink;
-    const GDec w{base + a.off_in, base + a.off_out, gl};
-    const uint32_t step = gridDim.x * waves * kGrp, cover = gpf_cover(a.stride);
-    GPrefetch f{};
-    if (kPf) gpf_issue(f, a, (blockIdx.x * waves + wv) * kGrp + grp, gl, cover);
-    for (uint32_t p0 = (blockIdx.x * waves + wv) * kGrp; p0 < a.n; p0 += step) {
-        const uint32_t p = p0 + grp;
-        const bool have = p < a.n;
-        const uint32_t stored = have ? (kPf ? f.len : a.lens[p]) : 0u;
-        // status_in: packets that failed to open are left to the caller
-        const bool auth = have && (kPf ? f.st == 1 : (a.status_in ? a.status_in[p] == 1 : true));
-        const uint32_t len = stored >= a.sub ? stored - a.sub : stored;
-        uint8_t *slot = a.arena + (uint64_t)(have ? p : 0u) * a.stride;
-        const bool take = auth && stored >= a.sub && len <= a.max_in;
-        if (take) gstage<kPf>(w.in, slot, len, gl, cover, f);
-        if (kPf) gpf_issue(f, a, p + step, gl, cover);  // in flight while these packets are decoded
-        wave_lds_sync();
-        int u = -1;
-        if (take) {
-            u = gdecode(w, len, a.limit);
-            // an empty result fails: golang/snappy's Decode(nil, src) returns a nil slice for it and
-            // compression.go:37-39 drops a nil packet
-            if (u == 0) u = -1;
-        }
-        wave_lds_sync();
-        if (u > 0) {  // LDS [0, u) -> slot bytes [4, 4 + u)
-            uint32_t *dst = reinterpret_cast<uint32_t *>(slot + 4);
-            const uint32_t *srcw = reinterpret_cast<const uint32_t *>(w.out);
-            const uint32_t nw = (uint32_t)u >> 2;
-            for (uint32_t j = gl; j < nw; j += kGL) dst[j] = srcw[j];
-            const uint32_t t = (uint32_t)u & 3;
-            if (gl < t) slot[4 + 4 * nw + gl] = w.out[4 * nw + gl];
-        }
-        if (auth && gl == 0) {
-            a.lens[p] = u > 0 ? (uint32_t)u : len;  // failed: the compressed length (sub = 0: unchanged)
-            if (a.status) a.status[p] = u > 0 ? 1 : 0;
-        }
-        wave_lds_sync();  // the next packets' staging overwrites these ones' LDS
-    }
-}
-
 }  // namespace
 
-hipError_t launch_snappy(bool compress, const SnapArgs &a, int waves_per_wg, int grid, hipStream_t s, int group,
-                         bool prefetch) {
+hipError_t launch_snappy(bool compress, const SnapArgs &a, int waves_per_wg, int grid, hipStream_t s, bool group) {
     const size_t lds = (size_t)waves_per_wg * a.wave_bytes;
     const dim3 g(grid), b(64 * waves_per_wg);
-    if (compress && group == 3 && prefetch)
-        hipLaunchKernelGGL((snappy_compress_group_kernel<true, true, true>), g, b, lds, s, a);
-    else if (compress && group == 3)
-        hipLaunchKernelGGL((snappy_compress_group_kernel<true, true, false>), g, b, lds, s, a);
-    else if (compress && group == 2)
-        hipLaunchKernelGGL((snappy_compress_group_kernel<true, false, false>), g, b, lds, s, a);
-    else if (compress && group)
-        hipLaunchKernelGGL((snappy_compress_group_kernel<false, false, false>), g, b, lds, s, a);
+    if (compress && group)
+        hipLaunchKernelGGL(snappy_compress_group_kernel, g, b, lds, s, a);
     else if (compress)
         hipLaunchKernelGGL(snappy_compress_kernel, g, b, lds, s, a);
-    else if (group && prefetch)
-        hipLaunchKernelGGL(snappy_uncompress_group_kernel<true>, g, b, lds, s, a);
-    else if (group)
-        hipLaunchKernelGGL(snappy_uncompress_group_kernel<false>, g, b, lds, s, a);
     else
         hipLaunchKernelGGL(snappy_uncompress_kernel, g, b, lds, s, a);
     return hipGetLastError();

@@ -80,27 +80,12 @@ def _match(case, comp: bytes) -> bool:
     return hashlib.sha256(comp).hexdigest() == case["out_sha256"]
 
 
-@pytest.fixture(params=["3", "3:0", "2", "1", "0"],
-                ids=["group_direct", "group_direct_noprefetch", "group_pipelined", "group_encoder", "wave_encoder"])
+@pytest.fixture(params=["1", "0"], ids=["group_encoder", "wave_encoder"])
 def encoder(request, monkeypatch):
-    """QGCM_SNAPPY_GROUP (read per call): 3 = four packets per wave, pipelined miss probes, output
-    straight into the slot, the next packets prefetched (the default; ":0" sets QGCM_SNAPPY_PREFETCH=0);
-    2 = pipelined, output staged in LDS; 1 = not pipelined; 0 = one wave per packet.  All must give the
-    host encoder's (and libsnappy's) bytes, and leave a failing packet's slot untouched."""
-    grp, _, pf = request.param.partition(":")
-    monkeypatch.setenv("QGCM_SNAPPY_GROUP", grp)
-    monkeypatch.setenv("QGCM_SNAPPY_PREFETCH", pf or "1")
-    return request.param
-
-
-@pytest.fixture(params=["1", "1:0", "0"], ids=["group_decoder", "group_decoder_noprefetch", "wave_decoder"])
-def decoder(request, monkeypatch):
-    """QGCM_SNAPPY_DEC_GROUP (read per call): 1 = four packets per wave, the next packets prefetched
-    (the default; ":0" sets QGCM_SNAPPY_PREFETCH=0), 0 = one wave per packet.  All must restore every
-    packet and fail exactly where the host decoder fails."""
-    grp, _, pf = request.param.partition(":")
-    monkeypatch.setenv("QGCM_SNAPPY_DEC_GROUP", grp)
-    monkeypatch.setenv("QGCM_SNAPPY_PREFETCH", pf or "1")
+    """QGCM_SNAPPY_GROUP (read per call): 1 = four packets per wave, pipelined miss probes, output
+    straight into the slot, the next packets prefetched (the default); 0 = one wave per packet.  Both
+    must give the host encoder's (and libsnappy's) bytes, and leave a failing packet's slot untouched."""
+    monkeypatch.setenv("QGCM_SNAPPY_GROUP", request.param)
     return request.param
 
 
@@ -129,7 +114,7 @@ def test_device_encoder_equals_libsnappy_golden(torch, ctx, encoder):
         assert st2[i] == 1 and bl[i] == len(d) and back[i, 4:4 + len(d)].tobytes() == d
 
 
-def test_device_codec_config5_batch_vs_host(torch, ctx, encoder, decoder):
+def test_device_codec_config5_batch_vs_host(torch, ctx, encoder):
     """2^14 Payload.Raw slots (stride 1472): config 5's packet shape and a mix of lengths 0..1433
     and contents; device compress == host encoder (whole arena incl. untouched bytes, lengths), then
     device uncompress restores the plaintext arena."""
@@ -187,7 +172,7 @@ def test_device_compress_failures_untouched(torch, ctx, encoder):
         assert np.array_equal(out[i, 4 + len(c):], host[i, 4 + len(c):])  # past the output: untouched
 
 
-def test_device_uncompress_corrupted_streams_vs_host(torch, ctx, decoder):
+def test_device_uncompress_corrupted_streams_vs_host(torch, ctx):
     """Random corruption of valid streams (and truncations, bad varints, offsets before the output):
     the device decoder fails exactly where the host decoder does, and otherwise writes its bytes."""
     rng = np.random.default_rng(0x5EED0052)
@@ -218,7 +203,7 @@ def test_device_uncompress_corrupted_streams_vs_host(torch, ctx, decoder):
     assert st[-len(goods):].all()
 
 
-def test_device_uncompress_empty_result_fails(torch, ctx, decoder):
+def test_device_uncompress_empty_result_fails(torch, ctx):
     """b"\\x00" decodes to 0 bytes: golang/snappy's Decode returns a nil slice and compression.go:37-39
     drops the packet, so the device batch fails it (slot and length untouched), as the host slots do."""
     streams = [b"\x00", _host_compress(b"abcabcabc"), b"\x00"]

@@ -147,7 +147,7 @@ for s in $STEPS; do
         PMC_PAYLOAD=4751969452 python3 tools/pmc_config3.py $OUT/pmcr_$tagl > $OUT/traffic_realign_$tagl.txt 2>&1
       done ;;
     profsnap2)  # device snappy counters, four-packets-per-wave encoder and one wave per packet
-      for g in 1 0; do
+      for g in 1 0; do  # (exp_snappy_dev alternates the encoders itself; pmc_kernels splits them by name)
         QGCM_SNAPPY_GROUP=$g bash tools/profile_snappy.sh ${TAG}_g$g > $OUT/profsnap_g$g.log 2>&1
         check profsnap_g$g $?
         python3 tools/pmc_kernels.py gpurun_out/prof_snappy_${TAG}_g$g 1048576 snappy_compress snappy_uncompress > $OUT/snappy_pmc_g$g.txt 2>&1
@@ -188,11 +188,11 @@ for s in $STEPS; do
     pcie)  # raw pinned-host <-> HBM hipMemcpyAsync rates of this box (the ceiling of every PCIe-inclusive figure)
       timeout -k 10 200 python3 tools/microbench/pcie.py > $OUT/pcie.json 2> $OUT/pcie.err
       check pcie $? ;;
-    profsnap3)  # device snappy counters: group encoder, group decoder and wave decoder
+    profsnap3)  # device snappy counters: group encoder (prefetching), wave encoder, decoder
       bash tools/profile_snappy.sh ${TAG}_s3 > $OUT/profsnap3.log 2>&1
       check profsnap3 $?
-      python3 tools/pmc_kernels.py gpurun_out/prof_snappy_${TAG}_s3 1048576 snappy_compress_group snappy_uncompress_group snappy_uncompress_kernel > $OUT/snappy_pmc_s3.txt 2>&1 ;;
-    snapab)  # device snappy codec: group vs wave decoder behind the default encoder, interleaved
+      python3 tools/pmc_kernels.py gpurun_out/prof_snappy_${TAG}_s3 1048576 snappy_compress_group snappy_compress_kernel snappy_uncompress_kernel > $OUT/snappy_pmc_s3.txt 2>&1 ;;
+    snapab)  # device snappy codec: group vs wave encoder, interleaved
       timeout -k 10 300 python3 tools/exp_snappy_dev.py 5 2 > $OUT/snap_ab.jsonl 2> $OUT/snap_ab.err
       check snapab $? ;;
   esac
