@@ -58,6 +58,10 @@ for leg in %(leg)r.split("+"):  # legs joined by "+" run one after another in th
         out = bench.extra_config3_host(verify=False)
     elif leg == "config5":
         out = bench.extra_config5(key, bench.host_cpus()["share"], verify=False)
+    elif leg.startswith("sleep"):  # e.g. sleep20: idle this many seconds between legs
+        import time
+        time.sleep(float(leg[5:]))
+        continue
     elif leg == "config4_one_gpu":  # device-resident (no pinned arena): what it leaves behind for the next leg
         out = bench.extra_config4_one_gpu(key)
     outs.append({"leg": leg, "value": out.get("value"), "pcie_GBps_each_way": out.get("pcie_GBps_each_way"),

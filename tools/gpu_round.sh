@@ -171,7 +171,7 @@ for s in $STEPS; do
         check dmachunk_$1_$2 $?
       done ;;
     legorder)  # does a leg that ran before it slow the pinned-host e2e leg in one process (the bench's order)?
-      timeout -k 10 600 python3 tools/exp_host_legs.py e2e config4_one_gpu+e2e config3_host+config4_one_gpu+e2e > $OUT/legorder.jsonl 2> $OUT/legorder.err
+      timeout -k 10 600 python3 tools/exp_host_legs.py e2e config4_one_gpu+e2e config4_one_gpu+sleep30+e2e > $OUT/legorder.jsonl 2> $OUT/legorder.err
       check legorder $? ;;
     gtests)  # the group (multi-GPU drop-in) suite
       timeout -k 10 600 python3 -u -m pytest tests/test_gpu_group.py -x -v --timeout 300 --timeout-method thread > $OUT/group_tests.txt 2>&1
@@ -185,6 +185,9 @@ for s in $STEPS; do
     pcieaf)  # PCIe copy rates before and after a 90-GB HBM allocation is freed in the same process
       timeout -k 10 300 python3 tools/microbench/pcie.py --after-free 90 > $OUT/pcie_after_free.jsonl 2> $OUT/pcie_af.err
       check pcieaf $? ;;
+    pcieaftrace)  # the same under a kernel + copy trace: which engine moves each direction before / after the free
+      timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $OUT/trace_pcieaf -o t -- python3 tools/microbench/pcie.py --after-free 90 > $OUT/trace_pcieaf.log 2>&1
+      check pcieaftrace $? ;;
     pcie)  # raw pinned-host <-> HBM hipMemcpyAsync rates of this box (the ceiling of every PCIe-inclusive figure)
       timeout -k 10 200 python3 tools/microbench/pcie.py > $OUT/pcie.json 2> $OUT/pcie.err
       check pcie $? ;;

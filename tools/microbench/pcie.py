@@ -55,8 +55,13 @@ def after_free(gb: float) -> None:
     torch.cuda.synchronize()
     del x
     torch.cuda.empty_cache()
-    for h2d, d2h in ((True, False), (False, True), (True, True)):
-        print(json.dumps({"after_free_GB": gb, **rate(64 << 20, h2d, d2h)}), flush=True)
+    import time
+    t0 = time.perf_counter()
+    for wait in (0, 5, 20, 60):  # does the slowdown wear off (a background clear of the freed HBM)?
+        while time.perf_counter() - t0 < wait:
+            time.sleep(0.1)
+        print(json.dumps({"after_free_GB": gb, "s_after_free": round(time.perf_counter() - t0, 1),
+                          **rate(64 << 20, True, True)}), flush=True)
 
 
 if __name__ == "__main__":
