@@ -248,9 +248,8 @@ def extra_config3(reps: int = 5, verify: bool = True) -> dict:
         out["digest_opened_ok"] = _sha256_device(arena) == gold["sha256_opened"]
         batch.seal_batch(ctx, arena, d_seal, W.N, nonces, status=status, stream=stream)
         out["digest_sealed_ok"] = _sha256_device(arena) == gold["sha256_sealed"]
-    del arena
+    del arena  # into torch's cache (config3_host reuses it; see the note there)
     ctx.close()
-    torch.cuda.empty_cache()
     return out
 
 
@@ -276,8 +275,10 @@ def extra_config3_host(reps: int = 3, verify: bool = True) -> dict:
     nons = np.frombuffer((C.c_uint8 * (12 * W.N)).from_address(n_ptr), np.uint8)
     dev = W.device_arena(torch, size, offs, kidx)
     host[:] = dev.cpu().numpy()
+    # freed into torch's cache, not to the driver: HBM released to the driver is cleared in the
+    # background, and while that runs concurrent H2D + D2H copies move at about half rate (a 90-GB free
+    # measured 29 vs 48 GB/s each way for a few seconds, profiles/r4_s9), which would land in the timing
     del dev
-    torch.cuda.empty_cache()
     nons[:] = W.nonces()
     d_seal = shard.host_descs(offs, lens, kidx)
     d_open = shard.host_descs(offs, lens.astype(np.int64) + 28, kidx)
@@ -775,13 +776,15 @@ def main() -> None:
             del arena_alloc, arena, nonces, status
             torch.cuda.empty_cache()
             extra = {}
+            # config4_one_gpu last: releasing its 94.5-GB arena halves concurrent H2D + D2H rates for a
+            # few seconds (the driver clears released HBM), which would otherwise hit the PCIe legs
             for name, fn in (("config3", lambda: extra_config3(verify=not args.no_verify)),
                              ("config3_host", lambda: extra_config3_host(verify=not args.no_verify)),
-                             ("config4_one_gpu", lambda: extra_config4_one_gpu(key)),
                              ("e2e_pinned_host", lambda: extra_e2e(key)),
                              ("config5", lambda: extra_config5(key, args.cpu_threads or host["share"], verify=not args.no_verify)),
                              ("config5_resident", lambda: extra_config5_resident(key, verify=not args.no_verify)),
-                             ("per_packet", extra_per_packet)):
+                             ("per_packet", extra_per_packet),
+                             ("config4_one_gpu", lambda: extra_config4_one_gpu(key))):
                 t0 = time.perf_counter()
                 try:
                     extra[name] = fn()
