@@ -170,6 +170,17 @@ for s in $STEPS; do
         QGCM_GROUP_DMA_CHUNK_MB=$1 QGCM_GROUP_DMA_SLOTS=$2 timeout -k 10 400 python3 tools/exp_host_legs.py config3_host > $OUT/dmachunk_$1_$2.jsonl 2>> $OUT/dmachunk.err
         check dmachunk_$1_$2 $?
       done ;;
+    blitwg)  # keyed host batch: the runtime's D2H blit kernels limited to N workgroups (do they crowd out the batch kernels?)
+      for v in "64 0" "64 16" "64 64" "512 0" "512 16" "512 64"; do
+        set -- $v
+        if [ "$2" = 0 ]; then unset DEBUG_CLR_LIMIT_BLIT_WG; else export DEBUG_CLR_LIMIT_BLIT_WG=$2; fi
+        QGCM_GROUP_DMA_CHUNK_MB=$1 timeout -k 10 400 python3 tools/exp_host_legs.py config3_host > $OUT/blitwg_$1_$2.jsonl 2>> $OUT/blitwg.err
+        check blitwg_$1_$2 $?
+      done
+      unset DEBUG_CLR_LIMIT_BLIT_WG ;;
+    trace512)  # copy / kernel timeline of the keyed host batch in 512-MiB DMA chunks
+      QGCM_GROUP_DMA_CHUNK_MB=512 timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $OUT/trace_c3_512 -o t -- python3 tools/run_leg.py config3_host 2 > $OUT/trace_c3_512.log 2>&1
+      check trace512 $? ;;
     legorder)  # does a leg that ran before it slow the pinned-host e2e leg in one process (the bench's order)?
       timeout -k 10 600 python3 tools/exp_host_legs.py e2e config4_one_gpu+e2e config4_one_gpu+sleep30+e2e > $OUT/legorder.jsonl 2> $OUT/legorder.err
       check legorder $? ;;
