@@ -69,8 +69,7 @@ constexpr uint64_t kZcChunk = 256ull << 20; // zero-copy path (device staging): 
                                             // chunk to fill the GPU (a 32-MB chunk is ~1500 tiles)
 constexpr int kSlots = 2;                 // staging slots per member (double buffer)
 constexpr int kCopyThreads = 4;           // gather/scatter threads per member (QGCM_GROUP_THREADS)
-constexpr uint64_t kDmaChunk = 512ull << 20;   // DMA-run path: largest chunk (QGCM_GROUP_DMA_CHUNK_MB)
-constexpr uint64_t kDmaChunkMin = 32ull << 20; // DMA-run path: first / last chunks (QGCM_GROUP_DMA_RAMP=0: flat)
+constexpr uint64_t kDmaChunk = 512ull << 20; // DMA-run path: staged bytes per chunk (QGCM_GROUP_DMA_CHUNK_MB)
 constexpr int kDmaSlots = 4;              // DMA-run path: staging slots in flight per member (QGCM_GROUP_DMA_SLOTS)
 constexpr uint64_t kRunGap = 256;         // largest gap between two records that still joins them in a run
 constexpr uint64_t kMinRun = 64ull << 10; // DMA-run path only when runs average at least this many bytes
@@ -521,26 +520,13 @@ inline uint64_t rec_in(bool seal, uint32_t len) {  // bytes of a slot the call r
 
 // Runs of member packets idx[0..m) (input order, offsets nondecreasing over the whole batch): packet
 // idx[j] joins the run of idx[j-1] when it is the next input packet and its record starts at most
-// kRunGap bytes after the previous record ends.  Runs are cut into chunks at record boundaries; each
-// piece keeps its host address mod 256 (`mis` = the arena's) in staging: the payloads keep their
-// alignment, and a piece's host and staging ends share 256-B boundaries.  Chunk sizes ramp: chunk c
-// holds up to min(chunk_max, chunk_min << c) bytes and at most half the bytes still to place (never
-// under chunk_min), so the pipeline fills and drains through small chunks (the first copy-in and the
-// last copy-out run alone) while the bulk moves in large ones (each chunk's descriptor batch has a
-// fixed cost: ~20 small launches for its worklist).  chunk_min = chunk_max: flat.
-void plan_dma(bool seal, const qgcm_desc *descs, const uint32_t *idx, size_t m, uint64_t chunk_max,
-              uint64_t chunk_min, uint32_t mis, DmaPlan &pl) {
+// kRunGap bytes after the previous record ends.  Runs are cut into chunks of up to `chunk` staging
+// bytes at record boundaries; each piece keeps its host address mod 256 (`mis` = the arena's) in
+// staging: the payloads keep their alignment, and a piece's host and staging ends share 256-B boundaries.
+void plan_dma(bool seal, const qgcm_desc *descs, const uint32_t *idx, size_t m, uint64_t chunk, uint32_t mis,
+              DmaPlan &pl) {
     pl = DmaPlan{};
     pl.at.resize(m);
-    chunk_min = std::min(chunk_min, chunk_max);
-    uint64_t total = 0, done = 0, placed = 0;  // record bytes: all, in closed chunks, in the open chunk
-    for (size_t j = 0; j < m; ++j) total += rec_in(seal, descs[idx[j]].len);
-    auto cap_for = [&](size_t c) {
-        const uint64_t up = c < 24 ? std::min(chunk_max, chunk_min << c) : chunk_max;
-        const uint64_t half = (total - done) / 2;
-        return std::max(chunk_min, std::min(up, half));
-    };
-    uint64_t chunk = cap_for(0);
     uint64_t prev_end = 0;
     size_t j0 = 0, p0 = 0;
     for (size_t j = 0; j < m; ++j) {
@@ -562,16 +548,12 @@ void plan_dma(bool seal, const qgcm_desc *descs, const uint32_t *idx, size_t m, 
                 j0 = j;
                 p0 = pl.pieces.size();
                 pos = (r0 + mis) & 255;
-                done += placed;
-                placed = 0;
-                chunk = cap_for(pl.chunks.size());
             }
             pl.pieces.push_back(Piece{r0, pos, r1 - r0});
         }
         const Piece &pc = pl.pieces.back();
         pl.at[j] = pc.dst + (r0 - pc.src);
         prev_end = r1;
-        placed += r1 - r0;
     }
     if (m) {
         const Piece &pc = pl.pieces.back();
@@ -775,10 +757,8 @@ int run_group(qgcm_group *g, bool seal, uint8_t *h_arena, const qgcm_desc *descs
     for (uint32_t i = 0; sorted && i < n; ++i) sorted = !(descs[i].offset & 3);
     sorted = sorted && !((uintptr_t)h_arena & 3);
     std::vector<DmaPlan> plan(G);
-    const char *cv = getenv("QGCM_GROUP_DMA_CHUNK_MB");  // A/B knobs: largest DMA chunk, ramp on / off
+    const char *cv = getenv("QGCM_GROUP_DMA_CHUNK_MB");  // A/B knob: staged bytes per DMA chunk
     const uint64_t dma_chunk = cv && *cv ? (uint64_t)std::max(1, std::min(4096, atoi(cv))) << 20 : kDmaChunk;
-    const char *rv = getenv("QGCM_GROUP_DMA_RAMP");
-    const uint64_t dma_min = rv && *rv && atoi(rv) == 0 ? dma_chunk : kDmaChunkMin;
     std::vector<int> rc(G, QGCM_OK), bad(G, 0), used_zc(G, 1);
     std::vector<std::thread> thr;
     for (int k = 0; k < G; ++k) {
@@ -792,7 +772,7 @@ int run_group(qgcm_group *g, bool seal, uint8_t *h_arena, const qgcm_desc *descs
             }
             if (sorted) {
                 const size_t m = part[k].size();
-                plan_dma(seal, descs, part[k].data(), m, dma_chunk, dma_min, (uint32_t)((uintptr_t)h_arena & 255), plan[k]);
+                plan_dma(seal, descs, part[k].data(), m, dma_chunk, (uint32_t)((uintptr_t)h_arena & 255), plan[k]);
                 if (plan[k].piece_bytes >= kMinRun * plan[k].pieces.size()) {
                     mb.last_path = 2;
                     used_zc[k] = 0;

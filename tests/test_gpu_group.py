@@ -142,8 +142,8 @@ def test_group_dma_runs_many_chunks_vs_oracle(torch, split, shift, slots, monkey
     split: QGCM_GROUP_DMA_SPLIT (each run moves as an unaligned head, a 256-B aligned body and a tail);
     shift: the arena starts this many bytes past the pinned allocation's start (staging keeps host
     addresses mod 256, so the head/body/tail cut moves).
-    DMA-run path over more chunks than staging slots (slot reuse; chunk sizes ramp 32 MiB up and down
-    again), two members on device 0 with
+    DMA-run path over more chunks than staging slots (slot reuse: 64-MiB chunks via
+    QGCM_GROUP_DMA_CHUNK_MB), two members on device 0 with
     the batch laid out member by member: 2^19 packets, the first half of 1184..1440 B in 1472-B
     Payload.Raw slots (gaps of up to 256 B inside a run; every 1000th slot 1 KiB further on, which breaks
     the run), the second half of U{0..2000} B in 16-B packed slots; sealed against the oracle, then opened
@@ -152,7 +152,8 @@ def test_group_dma_runs_many_chunks_vs_oracle(torch, split, shift, slots, monkey
 
     monkeypatch.setenv("QGCM_GROUP_DMA_SPLIT", split)
     monkeypatch.setenv("QGCM_GROUP_DMA_SLOTS", slots)
-    G, n = 2, 1 << 19  # ~660 MB of records: 6 chunks per member (32, 64, 128, 53, 32, ...), over 4 slots
+    monkeypatch.setenv("QGCM_GROUP_DMA_CHUNK_MB", "64")
+    G, n = 2, 1 << 19  # ~660 MB of records: 5 chunks of 64 MiB per member, more than its 4 staging slots
     grp = shard.Group([0] * G, max_keys=64)
     try:
         rng = np.random.default_rng(0x6A05)

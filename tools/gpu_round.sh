@@ -164,11 +164,10 @@ for s in $STEPS; do
         QGCM_GROUP_DMA_OWN_STREAMS=$1 QGCM_GROUP_DMA_SPLIT=$2 QGCM_GROUP_DMA_SLOTS=$3 timeout -k 10 400 python3 tools/exp_host_legs.py config3_host > $OUT/dmaab_own$1_split$2_slots$3.jsonl 2>> $OUT/dmaab.err
         check dmaab_own$1_split$2_slots$3 $?
       done ;;
-    dmachunk)  # keyed host batch (DMA runs): largest chunk and the 32-MiB ramp (per-chunk batch overhead vs pipeline fill/drain)
-      for v in "512 1" "512 0" "256 1" "1024 1" "64 0"; do
-        set -- $v
-        QGCM_GROUP_DMA_CHUNK_MB=$1 QGCM_GROUP_DMA_RAMP=$2 timeout -k 10 400 python3 tools/exp_host_legs.py config3_host > $OUT/dmachunk_$1_ramp$2.jsonl 2>> $OUT/dmachunk.err
-        check dmachunk_$1_ramp$2 $?
+    dmachunk)  # keyed host batch (DMA runs): chunk size (per-chunk descriptor-batch cost vs pipeline fill/drain)
+      for v in 64 256 384 512 768; do
+        QGCM_GROUP_DMA_CHUNK_MB=$v timeout -k 10 400 python3 tools/exp_host_legs.py config3_host > $OUT/dmachunk_$v.jsonl 2>> $OUT/dmachunk.err
+        check dmachunk_$v $?
       done ;;
     blitwg)  # keyed host batch: the runtime's D2H blit kernels limited to N workgroups (do they crowd out the batch kernels?)
       for v in "64 0" "64 16" "64 64" "512 0" "512 16" "512 64"; do
