@@ -30,7 +30,7 @@ constexpr uint64_t kPacketStart = 4;  // common.PacketStart
 
 void set_name(ifreq *r, const char *name) {
     memset(r, 0, sizeof *r);
-    if (name) strncpy(r->ifr_name, name, IFNAMSIZ - 1);
+    if (name) memcpy(r->ifr_name, name, strnlen(name, IFNAMSIZ - 1));  // stays NUL-terminated (memset above)
 }
 
 }  // namespace
