@@ -165,7 +165,7 @@ for s in $STEPS; do
         check dmaab_own$1_split$2_slots$3 $?
       done ;;
     dmachunk)  # keyed host batch (DMA runs): chunk size (per-chunk descriptor-batch cost vs pipeline fill/drain)
-      for v in 64 256 384 512 768; do
+      for v in ${DMACHUNKS:-64 256 384 512 768}; do
         QGCM_GROUP_DMA_CHUNK_MB=$v timeout -k 10 400 python3 tools/exp_host_legs.py config3_host > $OUT/dmachunk_$v.jsonl 2>> $OUT/dmachunk.err
         check dmachunk_$v $?
       done ;;
