@@ -177,9 +177,11 @@ for s in $STEPS; do
         check blitwg_$1_$2 $?
       done
       unset DEBUG_CLR_LIMIT_BLIT_WG ;;
-    trace512)  # copy / kernel timeline of the keyed host batch in 512-MiB DMA chunks
-      QGCM_GROUP_DMA_CHUNK_MB=512 timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $OUT/trace_c3_512 -o t -- python3 tools/run_leg.py config3_host 2 > $OUT/trace_c3_512.log 2>&1
-      check trace512 $? ;;
+    tracechunk)  # copy / kernel timelines of the keyed host batch at the DMA chunk sizes in TRACECHUNKS
+      for v in ${TRACECHUNKS:-512}; do
+        QGCM_GROUP_DMA_CHUNK_MB=$v timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $OUT/trace_c3_$v -o t -- python3 tools/run_leg.py config3_host 2 > $OUT/trace_c3_$v.log 2>&1
+        check tracechunk_$v $?
+      done ;;
     legorder)  # does a leg that ran before it slow the pinned-host e2e leg in one process (the bench's order)?
       timeout -k 10 600 python3 tools/exp_host_legs.py e2e config4_one_gpu+e2e config4_one_gpu+sleep30+e2e > $OUT/legorder.jsonl 2> $OUT/legorder.err
       check legorder $? ;;
