@@ -165,9 +165,11 @@ struct ZC {
 struct DmaState {
     hipStream_t s[3] = {};  // copy-in, kernels, copy-out
     std::vector<hipEvent_t> ev_in, ev_k, ev_out;  // per staging slot
-    std::vector<uint8_t *> d_stage;  // [records][descs][nonces][status] of one chunk, stage_cap bytes each
-    std::vector<uint8_t *> h_side;   // pinned [descs][nonces][status] of one chunk, side_cap bytes each
+    std::vector<uint8_t *> d_stage;  // [records][descs][nonces] of one chunk, stage_cap bytes each
+    std::vector<uint8_t *> h_side;   // pinned [descs][nonces] of one chunk, side_cap bytes each
     uint64_t stage_cap = 0, side_cap = 0;
+    uint8_t *d_stat = nullptr, *h_stat = nullptr;  // the member's statuses, all chunks (device, pinned)
+    size_t stat_cap = 0;
 };
 
 struct Member {
@@ -596,7 +598,16 @@ hipError_t piece_copy(void *dst, const void *src, uint64_t bytes, hipMemcpyKind 
     return hipSuccess;
 }
 
-int dma_ready(DmaState &z, uint64_t stage, uint64_t side, bool own, size_t slots) {
+int dma_ready(DmaState &z, uint64_t stage, uint64_t side, bool own, size_t slots, size_t m) {
+    if (m > z.stat_cap) {
+        if (z.d_stat) hipFree(z.d_stat);
+        if (z.h_stat) hipHostFree(z.h_stat);
+        z.d_stat = z.h_stat = nullptr;
+        z.stat_cap = 0;
+        if (hipMalloc(&z.d_stat, m) != hipSuccess || hipHostMalloc(&z.h_stat, m, hipHostMallocDefault) != hipSuccess)
+            return QGCM_E_NOMEM;
+        z.stat_cap = m;
+    }
     for (hipStream_t &x : z.s)
         if (own && !x && hipStreamCreateWithFlags(&x, hipStreamNonBlocking) != hipSuccess) return QGCM_E_HIP;
     while (z.ev_in.size() < slots) {
@@ -639,13 +650,14 @@ int run_member_dma(Member &mb, bool seal, uint8_t *h_arena, const qgcm_desc *des
     DmaState &z = mb.dma;
     const bool non = seal && h_nonces;
     const uint64_t pk = pl.max_pk;
-    const uint64_t off_non = (16ull * pk + 255) & ~255ull, off_st = off_non + (non ? (12ull * pk + 255) & ~255ull : 0);
-    const uint64_t side = off_st + ((pk + 255) & ~255ull);
+    const uint64_t off_non = (16ull * pk + 255) & ~255ull;
+    const uint64_t side = off_non + (non ? (12ull * pk + 255) & ~255ull : 0);  // [descs][nonces]
     const bool own = own_streams();
     const char *sv = getenv("QGCM_GROUP_DMA_SLOTS");  // A/B knob: staging slots (chunks in flight)
     const size_t nc = pl.chunks.size();
     const size_t S = std::min<size_t>(nc, (size_t)std::max(2, std::min(64, sv && *sv ? atoi(sv) : kDmaSlots)));
-    int rc = dma_ready(z, pl.max_bytes, side, own, S);
+    const size_t m = pl.at.size();
+    int rc = dma_ready(z, pl.max_bytes, side, own, S, m);
     if (rc != QGCM_OK) return rc;
     // the member context's own pipeline streams (those qgcm_seal_host moves 46 GB/s each way with);
     // QGCM_GROUP_DMA_OWN_STREAMS=1: streams of the group's own (A/B)
@@ -657,28 +669,19 @@ int run_member_dma(Member &mb, bool seal, uint8_t *h_arena, const qgcm_desc *des
         s_k = qgcm::ctx_pipe(mb.ctx, 1);
         s_out = qgcm::ctx_pipe(mb.ctx, 2);
     }
-    int bad = 0;
-    // results of the chunk last staged in slot k (its copy-out has landed): statuses to the caller
-    auto retire = [&](int k, const DmaChunk &c) {
-        const uint8_t *st = z.h_side[k] + off_st;
-        for (size_t j = c.j0; j < c.j1; ++j) {
-            bad += st[j - c.j0] != 1;
-            if (h_status) h_status[idx[j]] = st[j - c.j0];
-        }
-    };
+    // Statuses go to one member-wide device array and come back in ONE copy after the last kernel: a
+    // small copy-out per chunk costs a copy setup each, and the host never waits on a copy-out.
     size_t c = 0;
     for (; c < nc && rc == QGCM_OK; ++c) {
         const int k = (int)(c % S);
         const DmaChunk &ch = pl.chunks[c];
-        if (c >= S) {  // slot k's previous chunk must have landed before its side area is reused
-            if (hipEventSynchronize(z.ev_out[k]) != hipSuccess) {
-                rc = QGCM_E_HIP;
-                break;
-            }
-            retire(k, pl.chunks[c - S]);
+        // slot k's side area is rewritten below: the copy-in of its previous chunk must have read it
+        if (c >= S && hipEventSynchronize(z.ev_in[k]) != hipSuccess) {
+            rc = QGCM_E_HIP;
+            break;
         }
         uint8_t *hs = z.h_side[k], *ds = z.d_stage[k];
-        const uint64_t dside = pl.max_bytes;  // descs / nonces / status behind the records
+        const uint64_t dside = pl.max_bytes;  // descs / nonces behind the records
         const size_t cn = ch.j1 - ch.j0;
         qgcm_desc *hd = reinterpret_cast<qgcm_desc *>(hs);
         for (size_t j = ch.j0; j < ch.j1; ++j) {
@@ -686,6 +689,7 @@ int run_member_dma(Member &mb, bool seal, uint8_t *h_arena, const qgcm_desc *des
             hd[j - ch.j0] = qgcm_desc{pl.at[j], d.len, d.key_idx};
             if (non) memcpy(hs + off_non + 12 * (j - ch.j0), h_nonces + 12ull * idx[j], 12);
         }
+        // ... and its staging is overwritten once the copy-out of its previous chunk has landed
         if (hipStreamWaitEvent(s_in, z.ev_out[k], 0) != hipSuccess) rc = QGCM_E_HIP;
         for (size_t p = ch.p0; p < ch.p1 && rc == QGCM_OK; ++p) {
             const Piece &pc = pl.pieces[p];
@@ -693,14 +697,14 @@ int run_member_dma(Member &mb, bool seal, uint8_t *h_arena, const qgcm_desc *des
                 rc = QGCM_E_HIP;
         }
         if (rc == QGCM_OK &&
-            (hipMemcpyAsync(ds + dside, hs, off_st, hipMemcpyHostToDevice, s_in) != hipSuccess ||
+            (hipMemcpyAsync(ds + dside, hs, side, hipMemcpyHostToDevice, s_in) != hipSuccess ||
              hipEventRecord(z.ev_in[k], s_in) != hipSuccess || hipStreamWaitEvent(s_k, z.ev_in[k], 0) != hipSuccess))
             rc = QGCM_E_HIP;
         if (rc != QGCM_OK) break;
         const qgcm_desc *dd = reinterpret_cast<const qgcm_desc *>(ds + dside);
         rc = seal ? qgcm_seal_batch(mb.ctx, ds, dd, (uint32_t)cn, non ? ds + dside + off_non : nullptr, aad_len,
-                                    ds + dside + off_st, s_k)
-                  : qgcm_open_batch(mb.ctx, ds, dd, (uint32_t)cn, aad_len, ds + dside + off_st, s_k);
+                                    z.d_stat + ch.j0, s_k)
+                  : qgcm_open_batch(mb.ctx, ds, dd, (uint32_t)cn, aad_len, z.d_stat + ch.j0, s_k);
         if (rc != QGCM_OK) break;
         if (hipEventRecord(z.ev_k[k], s_k) != hipSuccess || hipStreamWaitEvent(s_out, z.ev_k[k], 0) != hipSuccess)
             rc = QGCM_E_HIP;
@@ -709,15 +713,19 @@ int run_member_dma(Member &mb, bool seal, uint8_t *h_arena, const qgcm_desc *des
             if (piece_copy(h_arena + pc.src, ds + pc.dst, pc.bytes, hipMemcpyDeviceToHost, s_out) != hipSuccess)
                 rc = QGCM_E_HIP;
         }
-        if (rc == QGCM_OK &&
-            (hipMemcpyAsync(hs + off_st, ds + dside + off_st, cn, hipMemcpyDeviceToHost, s_out) != hipSuccess ||
-             hipEventRecord(z.ev_out[k], s_out) != hipSuccess))
-            rc = QGCM_E_HIP;
+        if (rc == QGCM_OK && hipEventRecord(z.ev_out[k], s_out) != hipSuccess) rc = QGCM_E_HIP;
     }
+    // every kernel has run when s_k gets here
+    if (rc == QGCM_OK && hipMemcpyAsync(z.h_stat, z.d_stat, m, hipMemcpyDeviceToHost, s_k) != hipSuccess)
+        rc = QGCM_E_HIP;
     for (hipStream_t x : {s_in, s_k, s_out})
         if (hipStreamSynchronize(x) != hipSuccess && rc == QGCM_OK) rc = QGCM_E_HIP;
-    if (rc == QGCM_OK)  // the chunks still in their slots
-        for (size_t q = c > S ? c - S : 0; q < c; ++q) retire((int)(q % S), pl.chunks[q]);
+    int bad = 0;
+    if (rc == QGCM_OK)
+        for (size_t j = 0; j < m; ++j) {
+            bad += z.h_stat[j] != 1;
+            if (h_status) h_status[idx[j]] = z.h_stat[j];
+        }
     *bad_out = bad;
     return rc;
 }
@@ -867,6 +875,8 @@ void qgcm_group_destroy(qgcm_group *g) {
             for (hipEvent_t e : {dm.ev_in[k], dm.ev_k[k], dm.ev_out[k]}) hipEventDestroy(e);
         for (uint8_t *p : dm.d_stage) hipFree(p);
         for (uint8_t *p : dm.h_side) hipHostFree(p);
+        if (dm.d_stat) hipFree(dm.d_stat);
+        if (dm.h_stat) hipHostFree(dm.h_stat);
         qgcm_destroy(mb.ctx);
     }
     delete g;
