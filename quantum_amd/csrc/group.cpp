@@ -58,6 +58,7 @@
 #include <memory>
 #include <mutex>
 #include <thread>
+#include <string>
 #include <vector>
 
 #include "gcm_internal.h"
@@ -669,6 +670,16 @@ int run_member_dma(Member &mb, bool seal, uint8_t *h_arena, const qgcm_desc *des
         s_k = qgcm::ctx_pipe(mb.ctx, 1);
         s_out = qgcm::ctx_pipe(mb.ctx, 2);
     }
+    // QGCM_GROUP_DMA_TIMELINE=1 (diagnostics): timing events after each chunk's copy-in, kernels and
+    // copy-out, printed to stderr as ms since the call's first copy-in was queued (no profiler attached)
+    std::vector<hipEvent_t> tl;
+    hipEvent_t tl0 = nullptr;
+    if (env_flag("QGCM_GROUP_DMA_TIMELINE")) {
+        tl.assign(3 * nc, nullptr);
+        for (hipEvent_t &e : tl) hipEventCreate(&e);
+        hipEventCreate(&tl0);
+        hipEventRecord(tl0, s_in);
+    }
     // Statuses go to one member-wide device array and come back in ONE copy after the last kernel: a
     // small copy-out per chunk costs a copy setup each, and the host never waits on a copy-out.
     size_t c = 0;
@@ -703,11 +714,13 @@ int run_member_dma(Member &mb, bool seal, uint8_t *h_arena, const qgcm_desc *des
              hipEventRecord(z.ev_in[k], s_in) != hipSuccess || hipStreamWaitEvent(s_k, z.ev_in[k], 0) != hipSuccess))
             rc = QGCM_E_HIP;
         if (rc != QGCM_OK) break;
+        if (!tl.empty()) hipEventRecord(tl[3 * c], s_in);
         const qgcm_desc *dd = reinterpret_cast<const qgcm_desc *>(ds + dside);
         rc = seal ? qgcm_seal_batch(mb.ctx, ds, dd, (uint32_t)cn, non ? ds + dside + off_non : nullptr, aad_len,
                                     z.d_stat + ch.j0, s_k)
                   : qgcm_open_batch(mb.ctx, ds, dd, (uint32_t)cn, aad_len, z.d_stat + ch.j0, s_k);
         if (rc != QGCM_OK) break;
+        if (!tl.empty()) hipEventRecord(tl[3 * c + 1], s_k);
         if (hipEventRecord(z.ev_k[k], s_k) != hipSuccess || hipStreamWaitEvent(s_out, z.ev_k[k], 0) != hipSuccess)
             rc = QGCM_E_HIP;
         for (size_t p = ch.p0; p < ch.p1 && rc == QGCM_OK; ++p) {
@@ -716,12 +729,27 @@ int run_member_dma(Member &mb, bool seal, uint8_t *h_arena, const qgcm_desc *des
                 rc = QGCM_E_HIP;
         }
         if (rc == QGCM_OK && hipEventRecord(z.ev_out[k], s_out) != hipSuccess) rc = QGCM_E_HIP;
+        if (!tl.empty()) hipEventRecord(tl[3 * c + 2], s_out);
     }
     // every kernel has run when s_k gets here
     if (rc == QGCM_OK && hipMemcpyAsync(z.h_stat, z.d_stat, m, hipMemcpyDeviceToHost, s_k) != hipSuccess)
         rc = QGCM_E_HIP;
     for (hipStream_t x : {s_in, s_k, s_out})
         if (hipStreamSynchronize(x) != hipSuccess && rc == QGCM_OK) rc = QGCM_E_HIP;
+    if (!tl.empty()) {
+        std::string line = "{\"dma_timeline_ms\": [";
+        for (size_t q = 0; q < c; ++q) {
+            float t[3] = {};
+            for (int i = 0; i < 3; ++i) hipEventElapsedTime(&t[i], tl0, tl[3 * q + i]);
+            char buf[96];
+            snprintf(buf, sizeof buf, "%s[%.2f, %.2f, %.2f]", q ? ", " : "", t[0], t[1], t[2]);
+            line += buf;
+        }
+        line += "]}\n";
+        fputs(line.c_str(), stderr);
+        for (hipEvent_t e : tl) hipEventDestroy(e);
+        hipEventDestroy(tl0);
+    }
     int bad = 0;
     if (rc == QGCM_OK)
         for (size_t j = 0; j < m; ++j) {
