@@ -169,10 +169,12 @@ for s in $STEPS; do
         QGCM_GROUP_DMA_CHUNK_MB=$v timeout -k 10 400 python3 tools/exp_host_legs.py config3_host > $OUT/dmachunk_$v.jsonl 2>> $OUT/dmachunk.err
         check dmachunk_$v $?
       done ;;
-    dmatl)  # keyed host batch: per-chunk GPU timeline from timing events (no profiler), at the chunk sizes in DMACHUNKS
+    dmatl)  # keyed host batch: per-chunk GPU timeline from timing events (no profiler), at the chunk sizes in DMACHUNKS x slots in DMASLOTS
       for v in ${DMACHUNKS:-512 768}; do
-        QGCM_GROUP_DMA_TIMELINE=1 QGCM_GROUP_DMA_CHUNK_MB=$v timeout -k 10 300 python3 tools/run_leg.py config3_host 2 > $OUT/dmatl_$v.json 2> $OUT/dmatl_$v.err
-        check dmatl_$v $?
+        for sl in ${DMASLOTS:-4}; do
+          QGCM_GROUP_DMA_TIMELINE=1 QGCM_GROUP_DMA_CHUNK_MB=$v QGCM_GROUP_DMA_SLOTS=$sl timeout -k 10 300 python3 tools/run_leg.py config3_host 2 > $OUT/dmatl_${v}_s$sl.json 2> $OUT/dmatl_${v}_s$sl.err
+          check dmatl_${v}_s$sl $?
+        done
       done ;;
     blitwg)  # keyed host batch: the runtime's D2H blit kernels limited to N workgroups (do they crowd out the batch kernels?)
       for v in "64 0" "64 16" "64 64" "512 0" "512 16" "512 64"; do
