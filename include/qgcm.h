@@ -200,7 +200,8 @@ int qgcm_group_last_zerocopy(const qgcm_group *g);
 /* DMA runs: when the descriptors are in arena order (offsets nondecreasing, multiples of 4) and a member's
  * packets form runs of adjacent records (consecutive packets, at most 256 B between one record's end and
  * the next one's start) averaging 64 KiB or more, that member copies each run to and from its device with
- * one DMA each way (512 MiB chunks, three streams), with no gather, scatter or shader-driven PCIe traffic;
+ * one DMA each way (64 MiB chunks, three staging slots, three streams), with no gather, scatter or
+ * shader-driven PCIe traffic;
  * the gap bytes inside a run go back unchanged.  A batch laid out in qgcm_group_order's order, or any batch
  * of a one-member group, takes it.  QGCM_GROUP_DMA=0 disables it.  qgcm_group_last_path: the path member
  * took in the last call (0 host copies, 1 zero-copy, 2 DMA runs) or QGCM_E_ARG. */

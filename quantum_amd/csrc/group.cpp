@@ -70,8 +70,12 @@ constexpr uint64_t kZcChunk = 256ull << 20; // zero-copy path (device staging): 
                                             // chunk to fill the GPU (a 32-MB chunk is ~1500 tiles)
 constexpr int kSlots = 2;                 // staging slots per member (double buffer)
 constexpr int kCopyThreads = 4;           // gather/scatter threads per member (QGCM_GROUP_THREADS)
-constexpr uint64_t kDmaChunk = 512ull << 20; // DMA-run path: staged bytes per chunk (QGCM_GROUP_DMA_CHUNK_MB)
-constexpr int kDmaSlots = 4;              // DMA-run path: staging slots in flight per member (QGCM_GROUP_DMA_SLOTS)
+constexpr uint64_t kDmaChunk = 64ull << 20; // DMA-run path: staged bytes per chunk (QGCM_GROUP_DMA_CHUNK_MB)
+// DMA-run path: staging slots in flight per member (QGCM_GROUP_DMA_SLOTS).  Three, not more: config 3
+// from pinned host memory at 64-MiB chunks read 41.4 GiB/s with 3 slots, 25.7 with 4, 15.7 with 8 and
+// 13.2 with 16 (profiles/r4_dma: with more slots every S-th chunk's copy-out stalls 4-5 ms, by the
+// per-chunk timing events), and 34.2 with 2.
+constexpr int kDmaSlots = 3;
 constexpr uint64_t kRunGap = 256;         // largest gap between two records that still joins them in a run
 constexpr uint64_t kMinRun = 64ull << 10; // DMA-run path only when runs average at least this many bytes
 
