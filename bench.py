@@ -314,13 +314,14 @@ def extra_config3_host(reps: int = 3, verify: bool = True) -> dict:
             "pcie_GBps_each_way": round(size / ((s + o) / 2) / 1e9, 2), "status_ok": bad == 0, "reps": reps, **out}
 
 
-def extra_e2e(key: bytes, reps: int = 3) -> dict:
+def extra_e2e(key: bytes, reps: int = 3, n: int = 1 << 20) -> dict:
     """Config 2 from pinned HOST memory: qgcm_seal_host / qgcm_open_host (H2D + kernels + D2H,
-    pipelined in 64 MiB chunks over three streams): the PCIe-inclusive rate (never `value`)."""
+    pipelined in 64 MiB chunks over three streams): the PCIe-inclusive rate (never `value`).  n: packets
+    (tools/exp_host_legs.py runs batches past the 4-GiB staging ring, whose slots then rotate)."""
     from quantum_amd import _lib
     import ctypes as C
 
-    N, L = 1 << 20, 1350
+    N, L = n, 1350
     stride = batch.slot_stride(L, align=64)
     ctx = Context(device=0, max_keys=4)
     ctx.set_key(0, key)

@@ -54,6 +54,8 @@ for leg in %(leg)r.split("+"):  # legs joined by "+" run one after another in th
     nodes_seen.clear()
     if leg == "e2e":
         out = bench.extra_e2e(key)
+    elif leg == "e2e_big":  # 4.5 M packets, 6.3 GB: past qgcm_seal_host's 4-GiB staging ring (rotating slots)
+        out = bench.extra_e2e(key, reps=2, n=9 << 19)
     elif leg == "config3_host":
         out = bench.extra_config3_host(verify=False)
     elif leg == "config5":

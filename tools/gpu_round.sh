@@ -207,6 +207,9 @@ for s in $STEPS; do
     pcieaftrace)  # the same under a kernel + copy trace: which engine moves each direction before / after the free
       timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $OUT/trace_pcieaf -o t -- python3 tools/microbench/pcie.py --after-free 90 > $OUT/trace_pcieaf.log 2>&1
       check pcieaftrace $? ;;
+    e2ebig)  # qgcm_seal_host past its 4-GiB staging ring (slots rotate) vs within it
+      timeout -k 10 400 python3 tools/exp_host_legs.py e2e e2e_big > $OUT/e2e_big.jsonl 2> $OUT/e2e_big.err
+      check e2ebig $? ;;
     pcie)  # raw pinned-host <-> HBM hipMemcpyAsync rates of this box (the ceiling of every PCIe-inclusive figure)
       timeout -k 10 200 python3 tools/microbench/pcie.py > $OUT/pcie.json 2> $OUT/pcie.err
       check pcie $? ;;
