@@ -30,6 +30,7 @@ import "C"
 
 import (
 	"errors"
+	"fmt"
 	"sync"
 	"unsafe"
 )
@@ -40,6 +41,7 @@ var (
 	errShortBuffer = errors.New("qgcm: data buffer shorter than length + 28")
 	errAdditional  = errors.New("qgcm: additional data longer than 4 bytes")
 	errSlots       = errors.New("qgcm: out of key slots")
+	errBatch       = errors.New("qgcm: batch record outside the arena, or status shorter than the batch")
 )
 
 const overhead = C.QGCM_OVERHEAD // tag (16) + nonce (12): aead.Overhead() + aead.NonceSize()
@@ -166,6 +168,10 @@ type GPUGroup struct {
 	mu   sync.Mutex
 	next uint32
 	max  uint32
+
+	bmu    sync.Mutex     // one batch at a time (qgcm_group_seal_host serializes calls anyway)
+	nonces unsafe.Pointer // pinned nonce buffer of the last SealBatch (qgcm_host_alloc), 12 B per packet
+	ncap   int
 }
 
 // NewGPUGroup opens one context per device in `devices`.
@@ -214,4 +220,150 @@ func (gg *GPUGroup) Close() {
 		C.qgcm_group_destroy(gg.grp)
 		gg.grp = nil
 	}
+	if gg.nonces != nil {
+		C.qgcm_host_free(gg.nonces)
+		gg.nonces = nil
+	}
+}
+
+// ---- batched workers (INTEGRATION.md s2, s2b) ----
+// A worker that has read a batch of packets (recvmmsg / TUN reads) into one pinned Payload.Raw arena
+// seals or opens the whole batch with one call instead of one Encrypt / Decrypt per packet
+// (worker/outgoing.go:55-93, worker/incoming.go:54-92 loop over packets).  Laid out in Order's order,
+// each GPU's packets are adjacent and move by DMA (qgcm_group_last_path 2).
+
+// KeyIndex is the key slot of this peer: the Key field of its packets' Descs.
+func (a *GPUAES) KeyIndex() uint32 { return a.idx }
+
+// Arena is pinned host memory for a batch of Payload.Raw slots (qgcm_host_alloc), copied by DMA in
+// place.  Bytes aliases it until Free.
+type Arena struct {
+	Bytes []byte
+	p     unsafe.Pointer
+}
+
+// NewArena allocates size bytes of pinned host memory.
+func NewArena(size int) (*Arena, error) {
+	if size <= 0 || size > 1<<40 {
+		return nil, errors.New("qgcm: arena size out of range")
+	}
+	p := C.qgcm_host_alloc(C.size_t(size))
+	if p == nil {
+		return nil, errors.New("qgcm: pinned allocation failed")
+	}
+	return &Arena{Bytes: (*[1 << 40]byte)(p)[:size:size], p: p}, nil
+}
+
+// Free releases the arena (no batch call may be using it).
+func (a *Arena) Free() {
+	if a.p != nil {
+		C.qgcm_host_free(a.p)
+		a.p, a.Bytes = nil, nil
+	}
+}
+
+// Desc is one packet of a batch, laid out as qgcm_desc: the offset of its Payload.Raw slot in the
+// arena, its length (SealBatch: the payload length L; OpenBatch: the sealed length L+28) and its
+// peer's key slot (KeyIndex).  The slot is [4-B AAD (the IP header, Payload.Raw[0:4])][packet] with
+// room for the 28-B tag and nonce after a payload to be sealed.
+type Desc struct {
+	Offset uint64
+	Len    uint32
+	Key    uint32
+}
+
+// Desc and qgcm_desc have the same size (the two array lengths are non-negative only if equal).
+var _ [unsafe.Sizeof(Desc{}) - unsafe.Sizeof(C.qgcm_desc{})]byte
+var _ [unsafe.Sizeof(C.qgcm_desc{}) - unsafe.Sizeof(Desc{})]byte
+
+// Order returns the order in which to lay out a batch whose packet i belongs to peer keys[i] so that
+// each GPU's packets are adjacent (qgcm_group_order: stable, GPU by GPU), and each GPU's count.
+func (gg *GPUGroup) Order(keys []uint32) ([]uint32, []int, error) {
+	order := make([]uint32, len(keys))
+	counts := make([]C.uint32_t, int(C.qgcm_group_size(gg.grp)))
+	if len(keys) > 0 {
+		rc := C.qgcm_group_order(gg.grp, (*C.uint32_t)(unsafe.Pointer(&keys[0])), C.uint32_t(len(keys)),
+			(*C.uint32_t)(unsafe.Pointer(&order[0])), &counts[0])
+		if rc != C.QGCM_OK {
+			return nil, nil, errors.New(C.GoString(C.qgcm_strerror(rc)))
+		}
+	}
+	out := make([]int, len(counts))
+	for i, c := range counts {
+		out[i] = int(c)
+	}
+	return order, out, nil
+}
+
+func checkBatch(arena *Arena, descs []Desc, status []byte, seal bool) error {
+	if arena == nil || arena.p == nil || (status != nil && len(status) < len(descs)) {
+		return errBatch
+	}
+	extra := uint64(4)
+	if seal {
+		extra += overhead
+	}
+	for i := range descs {
+		if descs[i].Offset+extra+uint64(descs[i].Len) > uint64(len(arena.Bytes)) {
+			return errBatch
+		}
+	}
+	return nil
+}
+
+// SealBatch seals every packet of the batch in place, as Encrypt does one (crypto/aes.go:41-52):
+// slot [AAD][payload L] becomes [AAD][ciphertext L][tag 16][nonce 12], each nonce drawn from
+// getrandom(2).  status[i] (nil, or at least len(descs) bytes) is 1 for a sealed packet and 0 for one
+// that failed (a key slot that was never set, a length out of range), whose slot is left untouched.
+// Returns the number of failed packets.
+func (gg *GPUGroup) SealBatch(arena *Arena, descs []Desc, status []byte) (int, error) {
+	if err := checkBatch(arena, descs, status, true); err != nil {
+		return 0, err
+	}
+	n := len(descs)
+	if n == 0 {
+		return 0, nil
+	}
+	gg.bmu.Lock()
+	defer gg.bmu.Unlock()
+	if 12*n > gg.ncap {
+		if gg.nonces != nil {
+			C.qgcm_host_free(gg.nonces)
+		}
+		gg.nonces, gg.ncap = C.qgcm_host_alloc(C.size_t(12*n)), 12*n
+		if gg.nonces == nil {
+			gg.ncap = 0
+			return 0, errors.New("qgcm: pinned allocation failed")
+		}
+	}
+	if rc := C.qgcm_random_nonces((*C.uint8_t)(gg.nonces), C.uint32_t(n)); rc != C.QGCM_OK {
+		return 0, errors.New(C.GoString(C.qgcm_strerror(rc)))
+	}
+	rc := C.qgcm_group_seal_host(gg.grp, (*C.uint8_t)(arena.p), (*C.qgcm_desc)(unsafe.Pointer(&descs[0])),
+		C.uint32_t(n), (*C.uint8_t)(gg.nonces), 4, bytePtr(status))
+	if rc < 0 {
+		return 0, fmt.Errorf("qgcm: group seal: %s", C.GoString(C.qgcm_strerror(rc)))
+	}
+	return int(rc), nil
+}
+
+// OpenBatch opens every packet of the batch in place, as Decrypt does one (crypto/aes.go:57-62):
+// slot [AAD][ciphertext][tag][nonce] (Len = L+28) becomes [AAD][plaintext L]...; a packet whose tag
+// does not verify gets status 0 and its plaintext region zeroed, as Go's gcm Open leaves it.
+// Returns the number of failed packets.
+func (gg *GPUGroup) OpenBatch(arena *Arena, descs []Desc, status []byte) (int, error) {
+	if err := checkBatch(arena, descs, status, false); err != nil {
+		return 0, err
+	}
+	if len(descs) == 0 {
+		return 0, nil
+	}
+	gg.bmu.Lock()
+	defer gg.bmu.Unlock()
+	rc := C.qgcm_group_open_host(gg.grp, (*C.uint8_t)(arena.p), (*C.qgcm_desc)(unsafe.Pointer(&descs[0])),
+		C.uint32_t(len(descs)), 4, bytePtr(status))
+	if rc < 0 {
+		return 0, fmt.Errorf("qgcm: group open: %s", C.GoString(C.qgcm_strerror(rc)))
+	}
+	return int(rc), nil
 }

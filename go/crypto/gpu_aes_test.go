@@ -2,7 +2,7 @@
 
 // gpu_aes_test.go -- crypto/crypto_test.go's TestAES and BenchmarkAES (crypto_test.go:54-131) run on
 // GPUAES, plus the edges the shim guards (nil additional data, short buffers, tampering, many
-// goroutines calling one GPUAES at once).  `go test -tags gpu ./crypto` on a machine with an MI355X.
+// goroutines calling one GPUAES at once) and a batched worker's round trip over a GPUGroup.  `go test -tags gpu ./crypto` on a machine with an MI355X.
 // tests/cpp/go_replay.c replays the same C call sequence from C, which this image can build and the
 // GPU box can run (there is no Go toolchain in either).
 package crypto
@@ -152,5 +152,96 @@ func BenchmarkGPUAES(b *testing.B) {
 	for i := 0; i < b.N; i++ {
 		n, _ := aes.Encrypt(buf, dataLen, nil)
 		aes.Decrypt(buf[:n], nil)
+	}
+}
+
+// TestGPUGroupBatch: a batched worker's round trip over a two-member group (both on device 0 here):
+// 600 packets of 8 peers laid out in Order's order in a pinned arena, SealBatch, then OpenBatch
+// restores every payload; a tampered packet fails with its plaintext zeroed, and a peer whose key was
+// never installed fails with its slot untouched.  tests/cpp/go_replay.c TestGPUGroupBatch replays the
+// same calls and checks each sealed slot against the oracle.
+func TestGPUGroupBatch(t *testing.T) {
+	gg, err := NewGPUGroup([]int{0, 0}, 16)
+	if err != nil {
+		t.Fatal(err)
+	}
+	defer gg.Close()
+	const peers, n = 8, 600
+	var keyOf [peers]uint32
+	for k := 0; k < peers-1; k++ {
+		salt := make([]byte, SaltLength)
+		for i := range salt {
+			salt[i] = byte(0x40 + k)
+		}
+		a, err := gg.NewGPUAES([]byte("AES256Key-32Characters1234567890"), salt)
+		if err != nil {
+			t.Fatal(err)
+		}
+		keyOf[k] = a.KeyIndex()
+	}
+	keyOf[peers-1] = peers - 1 // a slot no NewGPUAES filled
+	peer := make([]uint32, n)
+	for i := range peer {
+		peer[i] = keyOf[(i*7+i/5)%peers]
+	}
+	order, counts, err := gg.Order(peer)
+	if err != nil || counts[0]+counts[1] != n {
+		t.Fatalf("Order: %v %v", counts, err)
+	}
+	descs := make([]Desc, n)
+	off := 0
+	for j, i := range order {
+		l := 1 + (int(i)*37)%1400
+		descs[j] = Desc{Offset: uint64(off), Len: uint32(l), Key: peer[i]}
+		off += (4 + l + 28 + 15) &^ 15
+	}
+	arena, err := NewArena(off)
+	if err != nil {
+		t.Fatal(err)
+	}
+	defer arena.Free()
+	for b := range arena.Bytes {
+		arena.Bytes[b] = byte(b*131 + 7)
+	}
+	plain := append([]byte(nil), arena.Bytes...)
+	status := make([]byte, n)
+	unset := 0
+	for _, d := range descs {
+		if d.Key == peers-1 {
+			unset++
+		}
+	}
+	if bad, err := gg.SealBatch(arena, descs, status); err != nil || bad != unset {
+		t.Fatalf("SealBatch: %d failed (want %d), %v", bad, unset, err)
+	}
+	victim := 0
+	for descs[victim].Key == peers-1 {
+		victim++
+	}
+	arena.Bytes[descs[victim].Offset+4] ^= 1
+	for j := range descs {
+		descs[j].Len += 28
+	}
+	if bad, err := gg.OpenBatch(arena, descs, status); err != nil || bad != unset+1 {
+		t.Fatalf("OpenBatch: %d failed (want %d), %v", bad, unset+1, err)
+	}
+	for j, d := range descs {
+		o, l := int(d.Offset), int(d.Len)-28
+		switch {
+		case d.Key == peers-1:
+			if status[j] != 0 || string(arena.Bytes[o:o+4+l+28]) != string(plain[o:o+4+l+28]) {
+				t.Fatalf("packet %d of the unset key was touched", j)
+			}
+		case j == victim:
+			for _, b := range arena.Bytes[o+4 : o+4+l] {
+				if status[j] != 0 || b != 0 {
+					t.Fatal("the tampered packet must fail with its plaintext zeroed")
+				}
+			}
+		default:
+			if status[j] != 1 || string(arena.Bytes[o:o+4+l]) != string(plain[o:o+4+l]) {
+				t.Fatalf("packet %d did not round-trip", j)
+			}
+		}
 	}
 }

@@ -12,6 +12,9 @@
  *                     returns -1 and leaves the bytes untouched when called), tamper -> zeroed plaintext
  *   TestGPUAESConcurrent 16 threads x 200 packets through one key with qgcm_seal_one/open_one, 4-B AAD
  *   TestGPUGroup      NewGPUGroup + NewGPUAES: key installed on the owning member only, calls on it
+ *   TestGPUGroupBatch GPUGroup.Order / NewArena / SealBatch / OpenBatch: 600 packets of 8 peers (one key
+ *                     slot never set) laid out in Order's order in a pinned arena; sealed against the
+ *                     oracle, opened back, a tampered packet zeroed, the unset key's packets untouched
  *   TestCreateError   qgcm_create on a device that does not exist: NULL + a message (cError)
  * Usage: go_replay [TestName ...] (default: all).  Prints "--- PASS: Name" per test.
  */
@@ -178,6 +181,75 @@ static void TestGPUGroup(void) {
     printf("--- PASS: TestGPUGroup\n");
 }
 
+static void TestGPUGroupBatch(void) {
+    const int devs[2] = {0, 0};
+    char err[QGCM_ERRLEN];
+    qgcm_group *g = qgcm_group_create(devs, 2, 16, err, sizeof err);
+    CHECK(g != NULL);
+    enum { kPeers = 8, kN = 600 };
+    uint8_t keys[kPeers][32];
+    for (uint32_t k = 0; k < kPeers - 1; ++k) { /* NewGPUAES on the owner; slot 7 is never set */
+        uint8_t salt[32];
+        memset(salt, (int)(0x40 + k), sizeof salt);
+        CHECK(install_key(qgcm_group_ctx(g, qgcm_group_shard(g, k)), k, salt, keys[k]) == QGCM_OK);
+    }
+    uint32_t peer[kN], order[kN], counts[2];
+    for (uint32_t i = 0; i < kN; ++i) peer[i] = (i * 7 + i / 5) % kPeers;
+    CHECK(qgcm_group_order(g, peer, kN, order, counts) == QGCM_OK); /* GPUGroup.Order */
+    CHECK(counts[0] + counts[1] == kN);
+    /* NewArena: slot j (the order[j]-th packet) = [AAD 4][L payload][28], 16-B aligned slots */
+    qgcm_desc d[kN];
+    uint64_t off = 0;
+    for (uint32_t j = 0; j < kN; ++j) {
+        const uint32_t i = order[j], L = 1 + (i * 37) % 1400;
+        d[j] = (qgcm_desc){off, L, peer[i]};
+        off += (4 + L + 28 + 15) & ~15ull;
+    }
+    uint8_t *arena = qgcm_host_alloc(off), *plain = malloc(off), *nonces = qgcm_host_alloc(12 * kN);
+    uint8_t status[kN];
+    CHECK(arena && plain && nonces);
+    for (uint64_t b = 0; b < off; ++b) arena[b] = (uint8_t)(b * 131 + 7);
+    memcpy(plain, arena, off);
+    int ok = qgcm_random_nonces(nonces, kN) == QGCM_OK; /* SealBatch */
+    int unset = 0;
+    for (uint32_t j = 0; j < kN; ++j) unset += d[j].key_idx == kPeers - 1;
+    ok &= qgcm_group_seal_host(g, arena, d, kN, nonces, 4, status) == unset;
+    for (uint32_t j = 0; j < kN && ok; ++j) {
+        const uint8_t *slot = arena + d[j].offset, *pslot = plain + d[j].offset;
+        if (d[j].key_idx == kPeers - 1) {
+            ok &= status[j] == 0 && !memcmp(slot, pslot, 4 + d[j].len + 28);
+        } else {
+            ok &= status[j] == 1 && !memcmp(slot + 4 + d[j].len + 16, nonces + 12 * j, 12);
+            ok &= matches_oracle(keys[d[j].key_idx], pslot + 4, d[j].len, pslot, 4, slot + 4);
+        }
+    }
+    uint32_t victim = 0;
+    while (d[victim].key_idx == kPeers - 1) ++victim;
+    arena[d[victim].offset + 4] ^= 1; /* tamper with one ciphertext */
+    for (uint32_t j = 0; j < kN; ++j) d[j].len += 28; /* OpenBatch: sealed lengths */
+    ok &= qgcm_group_open_host(g, arena, d, kN, 4, status) == unset + 1;
+    for (uint32_t j = 0; j < kN && ok; ++j) {
+        const uint32_t L = d[j].len - 28;
+        const uint8_t *slot = arena + d[j].offset, *pslot = plain + d[j].offset;
+        if (d[j].key_idx == kPeers - 1) { /* never set: status 0, the slot still as it came */
+            ok &= status[j] == 0 && !memcmp(slot, pslot, 4 + L + 28);
+            continue;
+        }
+        if (j == victim) {
+            ok &= status[j] == 0;
+            for (uint32_t b = 0; b < L; ++b) ok &= slot[4 + b] == 0;
+        } else {
+            ok &= status[j] == 1 && !memcmp(slot, pslot, 4 + L);
+        }
+    }
+    qgcm_host_free(arena);
+    qgcm_host_free(nonces);
+    free(plain);
+    qgcm_group_destroy(g);
+    CHECK(ok);
+    printf("--- PASS: TestGPUGroupBatch\n");
+}
+
 static void TestCreateError(void) {
     char err[QGCM_ERRLEN] = {0};
     CHECK(qgcm_create(4096, 16, err, sizeof err) == NULL);
@@ -207,6 +279,7 @@ int main(int argc, char **argv) {
     if (want(argc, argv, "TestGPUAESEdges")) TestGPUAESEdges(ctx);
     if (want(argc, argv, "TestGPUAESConcurrent")) TestGPUAESConcurrent(ctx);
     if (want(argc, argv, "TestGPUGroup")) TestGPUGroup();
+    if (want(argc, argv, "TestGPUGroupBatch")) TestGPUGroupBatch();
     if (want(argc, argv, "TestCreateError")) TestCreateError();
     if (ctx) qgcm_destroy(ctx);
     return failures ? 1 : 0;

@@ -54,4 +54,4 @@ def test_go_shim_replay_cpu():
 
 @pytest.mark.gpu
 def test_go_shim_replay_gpu():
-    run_go(["TestGPUAES", "TestGPUAESEdges", "TestGPUAESConcurrent", "TestGPUGroup"])
+    run_go(["TestGPUAES", "TestGPUAESEdges", "TestGPUAESConcurrent", "TestGPUGroup", "TestGPUGroupBatch"])
