@@ -168,7 +168,6 @@ struct ZC {
 
 // DMA-run path state of a member (grow-only)
 struct DmaState {
-    hipStream_t s[3] = {};  // copy-in, kernels, copy-out
     std::vector<hipEvent_t> ev_in, ev_k, ev_out;  // per staging slot
     std::vector<uint8_t *> d_stage;  // [records][descs][nonces] of one chunk, stage_cap bytes each
     std::vector<uint8_t *> h_side;   // pinned [descs][nonces] of one chunk, side_cap bytes each
@@ -579,31 +578,7 @@ bool env_flag(const char *name) {  // read per call (A/B and tests switch it wit
     return v && atoi(v) != 0;
 }
 
-bool own_streams() { return env_flag("QGCM_GROUP_DMA_OWN_STREAMS"); }
-
-// QGCM_GROUP_DMA_SPLIT=1: each piece moves as up to three copies, an unaligned head, a 256-B aligned
-// body and a tail (A/B: a run starts wherever a record does, only 4-B aligned)
-bool split_copies() { return env_flag("QGCM_GROUP_DMA_SPLIT"); }
-
-// one piece's copy; host and device ends share their address mod 256 (plan_dma)
-hipError_t piece_copy(void *dst, const void *src, uint64_t bytes, hipMemcpyKind kind, hipStream_t s) {
-    if (!split_copies()) return hipMemcpyAsync(dst, src, bytes, kind, s);
-    const uintptr_t host = (uintptr_t)(kind == hipMemcpyHostToDevice ? src : dst);
-    const uint64_t head = std::min<uint64_t>(bytes, (256 - (host & 255)) & 255);
-    const uint64_t body = (bytes - head) & ~255ull, tail = bytes - head - body;
-    uint64_t o = 0;
-    for (uint64_t part : {head, body, tail}) {
-        if (part) {
-            const hipError_t e = hipMemcpyAsync(static_cast<uint8_t *>(dst) + o, static_cast<const uint8_t *>(src) + o,
-                                                part, kind, s);
-            if (e != hipSuccess) return e;
-        }
-        o += part;
-    }
-    return hipSuccess;
-}
-
-int dma_ready(DmaState &z, uint64_t stage, uint64_t side, bool own, size_t slots, size_t m) {
+int dma_ready(DmaState &z, uint64_t stage, uint64_t side, size_t slots, size_t m) {
     if (m > z.stat_cap) {
         if (z.d_stat) hipFree(z.d_stat);
         if (z.h_stat) hipHostFree(z.h_stat);
@@ -613,8 +588,6 @@ int dma_ready(DmaState &z, uint64_t stage, uint64_t side, bool own, size_t slots
             return QGCM_E_NOMEM;
         z.stat_cap = m;
     }
-    for (hipStream_t &x : z.s)
-        if (own && !x && hipStreamCreateWithFlags(&x, hipStreamNonBlocking) != hipSuccess) return QGCM_E_HIP;
     while (z.ev_in.size() < slots) {
         hipEvent_t e[3] = {};
         for (hipEvent_t &x : e)
@@ -657,23 +630,16 @@ int run_member_dma(Member &mb, bool seal, uint8_t *h_arena, const qgcm_desc *des
     const uint64_t pk = pl.max_pk;
     const uint64_t off_non = (16ull * pk + 255) & ~255ull;
     const uint64_t side = off_non + (non ? (12ull * pk + 255) & ~255ull : 0);  // [descs][nonces]
-    const bool own = own_streams();
     const char *sv = getenv("QGCM_GROUP_DMA_SLOTS");  // A/B knob: staging slots (chunks in flight)
     const size_t nc = pl.chunks.size();
     const size_t S = std::min<size_t>(nc, (size_t)std::max(2, std::min(64, sv && *sv ? atoi(sv) : kDmaSlots)));
     const size_t m = pl.at.size();
-    int rc = dma_ready(z, pl.max_bytes, side, own, S, m);
+    int rc = dma_ready(z, pl.max_bytes, side, S, m);
     if (rc != QGCM_OK) return rc;
-    // the member context's own pipeline streams (those qgcm_seal_host moves 46 GB/s each way with);
-    // QGCM_GROUP_DMA_OWN_STREAMS=1: streams of the group's own (A/B)
-    std::unique_lock<std::mutex> io(qgcm::ctx_io_mu(mb.ctx), std::defer_lock);
-    hipStream_t s_in = z.s[0], s_k = z.s[1], s_out = z.s[2];
-    if (!own) {
-        io.lock();
-        s_in = qgcm::ctx_pipe(mb.ctx, 0);
-        s_k = qgcm::ctx_pipe(mb.ctx, 1);
-        s_out = qgcm::ctx_pipe(mb.ctx, 2);
-    }
+    // the member context's own pipeline streams, those qgcm_seal_host moves 46 GB/s each way with
+    // (streams of the group's own measured the same, profiles/r4_s6)
+    std::lock_guard<std::mutex> io(qgcm::ctx_io_mu(mb.ctx));
+    hipStream_t s_in = qgcm::ctx_pipe(mb.ctx, 0), s_k = qgcm::ctx_pipe(mb.ctx, 1), s_out = qgcm::ctx_pipe(mb.ctx, 2);
     // QGCM_GROUP_DMA_TIMELINE=1 (diagnostics): timing events after each chunk's copy-in, kernels and
     // copy-out, printed to stderr as ms since the call's first copy-in was queued (no profiler attached)
     std::vector<hipEvent_t> tl;
@@ -710,7 +676,7 @@ int run_member_dma(Member &mb, bool seal, uint8_t *h_arena, const qgcm_desc *des
 
         for (size_t p = ch.p0; p < ch.p1 && rc == QGCM_OK; ++p) {
             const Piece &pc = pl.pieces[p];
-            if (piece_copy(ds + pc.dst, h_arena + pc.src, pc.bytes, hipMemcpyHostToDevice, s_in) != hipSuccess)
+            if (hipMemcpyAsync(ds + pc.dst, h_arena + pc.src, pc.bytes, hipMemcpyHostToDevice, s_in) != hipSuccess)
                 rc = QGCM_E_HIP;
         }
         if (rc == QGCM_OK &&
@@ -729,7 +695,7 @@ int run_member_dma(Member &mb, bool seal, uint8_t *h_arena, const qgcm_desc *des
             rc = QGCM_E_HIP;
         for (size_t p = ch.p0; p < ch.p1 && rc == QGCM_OK; ++p) {
             const Piece &pc = pl.pieces[p];
-            if (piece_copy(h_arena + pc.src, ds + pc.dst, pc.bytes, hipMemcpyDeviceToHost, s_out) != hipSuccess)
+            if (hipMemcpyAsync(h_arena + pc.src, ds + pc.dst, pc.bytes, hipMemcpyDeviceToHost, s_out) != hipSuccess)
                 rc = QGCM_E_HIP;
         }
         if (rc == QGCM_OK && hipEventRecord(z.ev_out[k], s_out) != hipSuccess) rc = QGCM_E_HIP;
@@ -900,11 +866,6 @@ void qgcm_group_destroy(qgcm_group *g) {
         hipFree(z.d_status);
         for (uint8_t *st : z.d_stage) hipFree(st);
         DmaState &dm = mb.dma;
-        for (hipStream_t x : dm.s)
-            if (x) {
-                hipStreamSynchronize(x);
-                hipStreamDestroy(x);
-            }
         for (size_t k = 0; k < dm.ev_in.size(); ++k)
             for (hipEvent_t e : {dm.ev_in[k], dm.ev_k[k], dm.ev_out[k]}) hipEventDestroy(e);
         for (uint8_t *p : dm.d_stage) hipFree(p);

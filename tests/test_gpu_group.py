@@ -135,13 +135,11 @@ def test_group_keyed_host_batch_vs_oracle(torch, G, pinned, threads, zc, dma, gr
         grp.close()
 
 
-@pytest.mark.parametrize("split,shift,slots", [("0", 0, "3"), ("1", 0, "3"), ("1", 68, "3"), ("0", 0, "2"),
-                                               ("0", 0, "16")])
-def test_group_dma_runs_many_chunks_vs_oracle(torch, split, shift, slots, monkeypatch):
-    """slots: QGCM_GROUP_DMA_SLOTS, staging slots in flight (2: every slot reused twice; 16: none reused);
-    split: QGCM_GROUP_DMA_SPLIT (each run moves as an unaligned head, a 256-B aligned body and a tail);
-    shift: the arena starts this many bytes past the pinned allocation's start (staging keeps host
-    addresses mod 256, so the head/body/tail cut moves).
+@pytest.mark.parametrize("shift,slots", [(0, "3"), (68, "3"), (0, "2"), (0, "16")])
+def test_group_dma_runs_many_chunks_vs_oracle(torch, shift, slots, monkeypatch):
+    """slots: QGCM_GROUP_DMA_SLOTS, staging slots in flight (3, the default; 2: every slot reused twice; 16:
+    none reused); shift: the arena starts this many bytes past the pinned allocation's start (staging
+    keeps host addresses mod 256).
     DMA-run path over more chunks than staging slots (slot reuse: 64-MiB chunks via
     QGCM_GROUP_DMA_CHUNK_MB), two members on device 0 with
     the batch laid out member by member: 2^19 packets, the first half of 1184..1440 B in 1472-B
@@ -150,7 +148,6 @@ def test_group_dma_runs_many_chunks_vs_oracle(torch, split, shift, slots, monkey
     back and every byte of the arena checked."""
     from quantum_amd import shard
 
-    monkeypatch.setenv("QGCM_GROUP_DMA_SPLIT", split)
     monkeypatch.setenv("QGCM_GROUP_DMA_SLOTS", slots)
     monkeypatch.setenv("QGCM_GROUP_DMA_CHUNK_MB", "64")
     G, n = 2, 1 << 19  # ~660 MB of records: 5 chunks of 64 MiB per member, more than its 3 staging slots
