@@ -158,11 +158,10 @@ for s in $STEPS; do
     hostlegs)  # the PCIe-inclusive bench legs, each in a fresh process, with the NUMA nodes of their pinned arenas
       timeout -k 10 600 python3 tools/exp_host_legs.py > $OUT/host_legs.jsonl 2> $OUT/host_legs.err
       check hostlegs $? ;;
-    dmaab)  # keyed host batch (DMA runs): member context's streams vs own streams, split copies, staging slots; then e2e in the same process
-      for v in "0 0 4" "1 0 4" "0 1 4" "0 0 16" "0 0 64"; do
-        set -- $v
-        QGCM_GROUP_DMA_OWN_STREAMS=$1 QGCM_GROUP_DMA_SPLIT=$2 QGCM_GROUP_DMA_SLOTS=$3 timeout -k 10 400 python3 tools/exp_host_legs.py config3_host > $OUT/dmaab_own$1_split$2_slots$3.jsonl 2>> $OUT/dmaab.err
-        check dmaab_own$1_split$2_slots$3 $?
+    dmaab)  # keyed host batch (DMA runs): staging slots (3 is the default), each in a fresh process
+      for sl in ${DMASLOTS:-3 4}; do
+        QGCM_GROUP_DMA_SLOTS=$sl timeout -k 10 400 python3 tools/exp_host_legs.py config3_host > $OUT/dmaab_slots$sl.jsonl 2>> $OUT/dmaab.err
+        check dmaab_slots$sl $?
       done ;;
     dmachunk)  # keyed host batch (DMA runs): chunk size (per-chunk descriptor-batch cost vs pipeline fill/drain)
       for v in ${DMACHUNKS:-64 256 384 512 768}; do
@@ -176,14 +175,6 @@ for s in $STEPS; do
           check dmatl_${v}_s$sl $?
         done
       done ;;
-    blitwg)  # keyed host batch: the runtime's D2H blit kernels limited to N workgroups (do they crowd out the batch kernels?)
-      for v in "64 0" "64 16" "64 64" "512 0" "512 16" "512 64"; do
-        set -- $v
-        if [ "$2" = 0 ]; then unset DEBUG_CLR_LIMIT_BLIT_WG; else export DEBUG_CLR_LIMIT_BLIT_WG=$2; fi
-        QGCM_GROUP_DMA_CHUNK_MB=$1 timeout -k 10 400 python3 tools/exp_host_legs.py config3_host > $OUT/blitwg_$1_$2.jsonl 2>> $OUT/blitwg.err
-        check blitwg_$1_$2 $?
-      done
-      unset DEBUG_CLR_LIMIT_BLIT_WG ;;
     tracechunk)  # copy / kernel timelines of the keyed host batch at the DMA chunk sizes in TRACECHUNKS
       for v in ${TRACECHUNKS:-512}; do
         QGCM_GROUP_DMA_CHUNK_MB=$v timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $OUT/trace_c3_$v -o t -- python3 tools/run_leg.py config3_host 2 > $OUT/trace_c3_$v.log 2>&1
@@ -204,9 +195,6 @@ for s in $STEPS; do
     pcieaf)  # PCIe copy rates before and after a 90-GB HBM allocation is freed in the same process
       timeout -k 10 300 python3 tools/microbench/pcie.py --after-free 90 > $OUT/pcie_after_free.jsonl 2> $OUT/pcie_af.err
       check pcieaf $? ;;
-    pcieaftrace)  # the same under a kernel + copy trace: which engine moves each direction before / after the free
-      timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $OUT/trace_pcieaf -o t -- python3 tools/microbench/pcie.py --after-free 90 > $OUT/trace_pcieaf.log 2>&1
-      check pcieaftrace $? ;;
     e2ebig)  # qgcm_seal_host past its 4-GiB staging ring (slots rotate) vs within it
       timeout -k 10 400 python3 tools/exp_host_legs.py e2e e2e_big > $OUT/e2e_big.jsonl 2> $OUT/e2e_big.err
       check e2ebig $? ;;
