@@ -1,4 +1,5 @@
-"""Device-resident packet batches: the throughput path behind a coalescing Encryption.Apply.
+"""Device-resident packet batches: the throughput path for workers that hand over whole batches
+(worker/outgoing.go:55-93 and worker/incoming.go:54-92 loop over packets).
 
 Slots are common.Payload.Raw buffers laid end to end in one HBM arena (include/qgcm.h).  Torch
 is used only as the device allocator and for stream handles; the work is done by libqgcm.
