@@ -133,28 +133,12 @@ for s in $STEPS; do
     r4tests)  # the suites round 4 changed
       timeout -k 10 900 python3 -u -m pytest tests/test_gpu_group.py tests/test_gpu_config5.py tests/test_gpu_snappy.py tests/test_bench_dist.py tests/test_gpu_resident.py -x -v --timeout 300 --timeout-method thread > $OUT/r4_tests.txt 2>&1
       check r4tests $? ;;
-    abrealign)  # config 3: realigned segmented-kernel stores (side build in abt/realign) vs the product build
-      timeout -k 10 300 python3 tools/ab_libs_desc.py quantum_amd/libqgcm.so abt/realign/libqgcm.so --rounds 9 > $OUT/ab_realign.txt 2>&1
-      check abrealign $? ;;
-    pmcrealign)  # config 3 HBM traffic of the segmented kernel: product build vs realigned stores (side build)
-      for lib in quantum_amd abt/realign; do
-        tagl=$(basename $lib)
-        for c in WRITE_SIZE FETCH_SIZE; do
-          timeout -k 10 300 rocprofv3 --pmc $c -d $OUT/pmcr_${tagl}_$c -o $c --output-format csv -- python3 tools/ab_libs_desc.py $lib/libqgcm.so --rounds 1 > $OUT/pmcr_${tagl}_$c.log 2>&1
-          check pmcr_${tagl}_$c $?
-        done
-        mkdir -p $OUT/pmcr_$tagl && cp -r $OUT/pmcr_${tagl}_*/* $OUT/pmcr_$tagl/ 2>/dev/null
-        PMC_PAYLOAD=4751969452 python3 tools/pmc_config3.py $OUT/pmcr_$tagl > $OUT/traffic_realign_$tagl.txt 2>&1
-      done ;;
     profsnap2)  # device snappy counters, four-packets-per-wave encoder and one wave per packet
       for g in 1 0; do  # (exp_snappy_dev alternates the encoders itself; pmc_kernels splits them by name)
         QGCM_SNAPPY_GROUP=$g bash tools/profile_snappy.sh ${TAG}_g$g > $OUT/profsnap_g$g.log 2>&1
         check profsnap_g$g $?
         python3 tools/pmc_kernels.py gpurun_out/prof_snappy_${TAG}_g$g 1048576 snappy_compress snappy_uncompress > $OUT/snappy_pmc_g$g.txt 2>&1
       done ;;
-    e2eab)  # config 2 from pinned host memory: this build vs the round-3 build (abt/r3), separate processes
-      timeout -k 10 400 python3 tools/exp_e2e_ab.py quantum_amd/libqgcm.so abt/r3/libqgcm.so 2 > $OUT/e2e_ab.jsonl 2> $OUT/e2e_ab.err
-      check e2eab $? ;;
     hostlegs)  # the PCIe-inclusive bench legs, each in a fresh process, with the NUMA nodes of their pinned arenas
       timeout -k 10 600 python3 tools/exp_host_legs.py > $OUT/host_legs.jsonl 2> $OUT/host_legs.err
       check hostlegs $? ;;
