@@ -182,6 +182,11 @@ for s in $STEPS; do
     e2ebig)  # qgcm_seal_host past its 4-GiB staging ring (slots rotate) vs within it
       timeout -k 10 400 python3 tools/exp_host_legs.py e2e e2e_big > $OUT/e2e_big.jsonl 2> $OUT/e2e_big.err
       check e2ebig $? ;;
+    e2echunk)  # qgcm_seal_host / open_host chunk size (QGCM_PIPE_CHUNK_MB), each in a fresh process
+      for v in ${E2ECHUNKS:-32 64 128 256}; do
+        QGCM_PIPE_CHUNK_MB=$v timeout -k 10 300 python3 tools/exp_host_legs.py e2e > $OUT/e2echunk_$v.jsonl 2>> $OUT/e2echunk.err
+        check e2echunk_$v $?
+      done ;;
     pcie)  # raw pinned-host <-> HBM hipMemcpyAsync rates of this box (the ceiling of every PCIe-inclusive figure)
       timeout -k 10 200 python3 tools/microbench/pcie.py > $OUT/pcie.json 2> $OUT/pcie.err
       check pcie $? ;;
