@@ -578,7 +578,7 @@ bool env_flag(const char *name) {  // read per call (A/B and tests switch it wit
     return v && atoi(v) != 0;
 }
 
-int dma_ready(DmaState &z, uint64_t stage, uint64_t side, size_t slots, size_t m) {
+int dma_ready(DmaState &z, uint64_t stage, uint64_t side, size_t slots, size_t m, size_t nev) {
     if (m > z.stat_cap) {
         if (z.d_stat) hipFree(z.d_stat);
         if (z.h_stat) hipHostFree(z.h_stat);
@@ -588,7 +588,7 @@ int dma_ready(DmaState &z, uint64_t stage, uint64_t side, size_t slots, size_t m
             return QGCM_E_NOMEM;
         z.stat_cap = m;
     }
-    while (z.ev_in.size() < slots) {
+    while (z.ev_in.size() < nev) {
         hipEvent_t e[3] = {};
         for (hipEvent_t &x : e)
             if (hipEventCreateWithFlags(&x, hipEventDisableTiming) != hipSuccess) {
@@ -634,7 +634,9 @@ int run_member_dma(Member &mb, bool seal, uint8_t *h_arena, const qgcm_desc *des
     const size_t nc = pl.chunks.size();
     const size_t S = std::min<size_t>(nc, (size_t)std::max(2, std::min(64, sv && *sv ? atoi(sv) : kDmaSlots)));
     const size_t m = pl.at.size();
-    int rc = dma_ready(z, pl.max_bytes, side, S, m);
+    // QGCM_GROUP_DMA_FRESH_EVENTS=1 (diagnostics): one event triple per chunk instead of per slot
+    const bool fresh = env_flag("QGCM_GROUP_DMA_FRESH_EVENTS");
+    int rc = dma_ready(z, pl.max_bytes, side, S, m, fresh ? std::max(nc, S) : S);
     if (rc != QGCM_OK) return rc;
     // the member context's own pipeline streams, those qgcm_seal_host moves 46 GB/s each way with
     // (streams of the group's own measured the same, profiles/r4_s6)
@@ -650,8 +652,8 @@ int run_member_dma(Member &mb, bool seal, uint8_t *h_arena, const qgcm_desc *des
         hipEventCreate(&tl0);
         hipEventRecord(tl0, s_in);
     }
-    // Statuses go to one member-wide device array and come back in ONE copy after the last kernel: a
-    // small copy-out per chunk costs a copy setup each, and the host never waits on a copy-out.
+    // Statuses go to one member-wide device array and come back in ONE copy after the last kernel (a
+    // small copy-out per chunk would cost a copy setup each).
     size_t c = 0;
     for (; c < nc && rc == QGCM_OK; ++c) {
         const int k = (int)(c % S);
@@ -660,7 +662,8 @@ int run_member_dma(Member &mb, bool seal, uint8_t *h_arena, const qgcm_desc *des
         // (which also covers the side area's copy-in) rather than leaving the wait to the copy-in
         // stream: a copy-in queued behind a GPU-side wait for the copy-out stream's blit kernels took
         // the keyed host batch from 25.8 to 13.0 GiB/s at 64-MiB chunks (profiles/r4_s16)
-        if (c >= S && hipEventSynchronize(z.ev_out[k]) != hipSuccess) {
+        const size_t e = fresh ? c : (size_t)k;  // this chunk's events
+        if (c >= S && hipEventSynchronize(z.ev_out[fresh ? c - S : (size_t)k]) != hipSuccess) {
             rc = QGCM_E_HIP;
             break;
         }
@@ -681,7 +684,7 @@ int run_member_dma(Member &mb, bool seal, uint8_t *h_arena, const qgcm_desc *des
         }
         if (rc == QGCM_OK &&
             (hipMemcpyAsync(ds + dside, hs, side, hipMemcpyHostToDevice, s_in) != hipSuccess ||
-             hipEventRecord(z.ev_in[k], s_in) != hipSuccess || hipStreamWaitEvent(s_k, z.ev_in[k], 0) != hipSuccess))
+             hipEventRecord(z.ev_in[e], s_in) != hipSuccess || hipStreamWaitEvent(s_k, z.ev_in[e], 0) != hipSuccess))
             rc = QGCM_E_HIP;
         if (rc != QGCM_OK) break;
         if (!tl.empty()) hipEventRecord(tl[3 * c], s_in);
@@ -691,14 +694,14 @@ int run_member_dma(Member &mb, bool seal, uint8_t *h_arena, const qgcm_desc *des
                   : qgcm_open_batch(mb.ctx, ds, dd, (uint32_t)cn, aad_len, z.d_stat + ch.j0, s_k);
         if (rc != QGCM_OK) break;
         if (!tl.empty()) hipEventRecord(tl[3 * c + 1], s_k);
-        if (hipEventRecord(z.ev_k[k], s_k) != hipSuccess || hipStreamWaitEvent(s_out, z.ev_k[k], 0) != hipSuccess)
+        if (hipEventRecord(z.ev_k[e], s_k) != hipSuccess || hipStreamWaitEvent(s_out, z.ev_k[e], 0) != hipSuccess)
             rc = QGCM_E_HIP;
         for (size_t p = ch.p0; p < ch.p1 && rc == QGCM_OK; ++p) {
             const Piece &pc = pl.pieces[p];
             if (hipMemcpyAsync(h_arena + pc.src, ds + pc.dst, pc.bytes, hipMemcpyDeviceToHost, s_out) != hipSuccess)
                 rc = QGCM_E_HIP;
         }
-        if (rc == QGCM_OK && hipEventRecord(z.ev_out[k], s_out) != hipSuccess) rc = QGCM_E_HIP;
+        if (rc == QGCM_OK && hipEventRecord(z.ev_out[e], s_out) != hipSuccess) rc = QGCM_E_HIP;
         if (!tl.empty()) hipEventRecord(tl[3 * c + 2], s_out);
     }
     // every kernel has run when s_k gets here
