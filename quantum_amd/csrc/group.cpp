@@ -634,9 +634,7 @@ int run_member_dma(Member &mb, bool seal, uint8_t *h_arena, const qgcm_desc *des
     const size_t nc = pl.chunks.size();
     const size_t S = std::min<size_t>(nc, (size_t)std::max(2, std::min(64, sv && *sv ? atoi(sv) : kDmaSlots)));
     const size_t m = pl.at.size();
-    // QGCM_GROUP_DMA_FRESH_EVENTS=1 (diagnostics): one event triple per chunk instead of per slot
-    const bool fresh = env_flag("QGCM_GROUP_DMA_FRESH_EVENTS");
-    int rc = dma_ready(z, pl.max_bytes, side, S, m, fresh ? std::max(nc, S) : S);
+    int rc = dma_ready(z, pl.max_bytes, side, S, m, S);
     if (rc != QGCM_OK) return rc;
     // the member context's own pipeline streams, those qgcm_seal_host moves 46 GB/s each way with
     // (streams of the group's own measured the same, profiles/r4_s6)
@@ -662,8 +660,8 @@ int run_member_dma(Member &mb, bool seal, uint8_t *h_arena, const qgcm_desc *des
         // (which also covers the side area's copy-in) rather than leaving the wait to the copy-in
         // stream: a copy-in queued behind a GPU-side wait for the copy-out stream's blit kernels took
         // the keyed host batch from 25.8 to 13.0 GiB/s at 64-MiB chunks (profiles/r4_s16)
-        const size_t e = fresh ? c : (size_t)k;  // this chunk's events
-        if (c >= S && hipEventSynchronize(z.ev_out[fresh ? c - S : (size_t)k]) != hipSuccess) {
+        const size_t e = (size_t)k;  // this chunk's events: its slot's
+        if (c >= S && hipEventSynchronize(z.ev_out[e]) != hipSuccess) {
             rc = QGCM_E_HIP;
             break;
         }
