@@ -46,7 +46,8 @@ def main() -> None:
         settings.append(("host_s6c16", 0, "2", "", "16", 16))
         slots["host_s6c16"] = "6"
     else:
-        settings = [("host", 0, "2", "0", "32", 16), ("ahead1", 1, "1", "999999", "32", 16),
+        settings = [("host", 0, "2", "0", "32", 16), ("device", 2, "2", "", "32", 16),
+                    ("ahead1", 1, "1", "999999", "32", 16),
                     ("ahead2", 1, "2", "999999", "32", 16), ("ahead3", 1, "3", "999999", "32", 16),
                     ("ahead4", 1, "4", "999999", "32", 16), ("back0", 1, "2", "0", "32", 16),
                     ("back45", 1, "2", "45", "32", 16), ("back90", 1, "2", "90", "32", 16),
