@@ -155,9 +155,9 @@ for s in $STEPS; do
     dmatl)  # keyed host batch: per-chunk GPU timeline from timing events (no profiler), at the chunk sizes in DMACHUNKS x slots in DMASLOTS
       for v in ${DMACHUNKS:-512 768}; do
         for sl in ${DMASLOTS:-4}; do
-          f=0
-          QGCM_GROUP_DMA_TIMELINE=1 QGCM_GROUP_DMA_CHUNK_MB=$v QGCM_GROUP_DMA_SLOTS=$sl timeout -k 10 300 python3 tools/run_leg.py config3_host 2 > $OUT/dmatl_${v}_s${sl}_f$f.json 2> $OUT/dmatl_${v}_s${sl}_f$f.err
-          check dmatl_${v}_s${sl}_f$f $?
+          q=${HWQ:-4}  # hardware queues per process (HIP's default 4; at most 32 here)
+          GPU_MAX_HW_QUEUES=$q QGCM_GROUP_DMA_TIMELINE=1 QGCM_GROUP_DMA_CHUNK_MB=$v QGCM_GROUP_DMA_SLOTS=$sl timeout -k 10 300 python3 tools/run_leg.py config3_host 2 > $OUT/dmatl_${v}_s${sl}_q$q.json 2> $OUT/dmatl_${v}_s${sl}_q$q.err
+          check dmatl_${v}_s${sl}_q$q $?
         done
       done ;;
     tracechunk)  # copy / kernel timelines of the keyed host batch at the DMA chunk sizes in TRACECHUNKS
