@@ -126,8 +126,8 @@ __global__ void qwl_scatter_kernel(const uint32_t *sorted_keys, const uint32_t *
     if ((w & 15u) == 0) tile_keys[w >> 4] = k;
 }
 
-// Counting sort (the default for up to kCountMaxKeys key slots; QGCM_WORKLIST_SORT=radix forces the
-// radix sort below): one bucket per (key, 8-block length class), longest class first within a key,
+// Counting sort (QGCM_WORKLIST_SORT=count, up to kCountMaxKeys key slots; the radix sort below is the
+// default): one bucket per (key, 8-block length class), longest class first within a key,
 // the excluded entries in a last bucket.  A histogram, a one-workgroup scan and a scatter replace the
 // radix sort's ~7 launches and fills; entries of one bucket land in arbitrary order (lengths within
 // 128 B of one another), which only decides which packets share a tile.
@@ -238,8 +238,8 @@ hipError_t launch_quad_worklist(const qgcm_desc *descs, uint32_t n, uint32_t max
     if (n) hipLaunchKernelGGL(qwl_keys_kernel, dim3(g), dim3(bs), 0, s, descs, n, max_keys, key_valid, seal, k_in,
                                  v_in);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    const char *sv = getenv("QGCM_WORKLIST_SORT");  // "radix": the radix sort (A/B knob)
-    if (max_keys <= kCountMaxKeys && !(sv && !strcmp(sv, "radix"))) {
+    const char *sv = getenv("QGCM_WORKLIST_SORT");  // "count": the counting sort (A/B knob)
+    if (max_keys <= kCountMaxKeys && sv && !strcmp(sv, "count")) {
         const uint32_t nb = max_keys * kLenClasses + 1;
         uint32_t *hist = static_cast<uint32_t *>(cub_tmp);
         if ((e = hipMemsetAsync(hist, 0, 4ull * nb, s)) != hipSuccess) return e;

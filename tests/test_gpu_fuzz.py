@@ -95,12 +95,11 @@ def draw_case(case: int):
 @pytest.mark.parametrize("variant", ["default", 13])
 @pytest.mark.parametrize("seed", range(len(SIZES)))
 def test_descriptor_fuzz_vs_oracle(torch, fuzz_ctxs, fuzz_keys, variant, seed, sort, monkeypatch):
-    """sort: the worklist's key grouping -- the counting sort (the default up to 4096 key slots) or the
-    radix sort (QGCM_WORKLIST_SORT=radix; the default past 4096)."""
+    """sort: the worklist's key grouping -- the radix sort (the default) or the counting sort
+    (QGCM_WORKLIST_SORT=count, up to 4096 key slots)."""
     from quantum_amd import batch
 
-    if sort == "radix":
-        monkeypatch.setenv("QGCM_WORKLIST_SORT", "radix")
+    monkeypatch.setenv("QGCM_WORKLIST_SORT", sort)
 
     ctx = fuzz_ctxs[variant]
     rng, n, kidx, lens, offs, slot, size, aad_len, valid = draw_case(seed)
