@@ -11,10 +11,6 @@
 #include <hip/hip_runtime.h>
 #include <rocprim/device/device_radix_sort.hpp>
 #include <stdint.h>
-#include <stdlib.h>
-#include <string.h>
-
-#include <algorithm>
 
 #include "gcm_internal.h"
 
@@ -126,58 +122,6 @@ __global__ void qwl_scatter_kernel(const uint32_t *sorted_keys, const uint32_t *
     if ((w & 15u) == 0) tile_keys[w >> 4] = k;
 }
 
-// Counting sort (QGCM_WORKLIST_SORT=count, up to kCountMaxKeys key slots; the radix sort below is the
-// default): one bucket per (key, 8-block length class), longest class first within a key,
-// the excluded entries in a last bucket.  A histogram, a one-workgroup scan and a scatter replace the
-// radix sort's ~7 launches and fills; entries of one bucket land in arbitrary order (lengths within
-// 128 B of one another), which only decides which packets share a tile.
-constexpr uint32_t kLenClasses = 128;  // 8-block classes: lengths up to 16 KiB told apart
-constexpr uint32_t kCountMaxKeys = 4096;
-
-__device__ __forceinline__ uint32_t count_bucket(uint32_t sk, uint32_t max_keys) {
-    if (sk == 0xffffffffu) return max_keys * kLenClasses;
-    const uint32_t nb = (1u << kLenBits) - 1u - (sk & ((1u << kLenBits) - 1u));
-    return (sk >> kLenBits) * kLenClasses + (kLenClasses - 1u - min(nb >> 3, kLenClasses - 1u));
-}
-
-__global__ void qwl_hist_kernel(const uint32_t *sk, uint32_t n, uint32_t max_keys, uint32_t *hist) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) atomicAdd(&hist[count_bucket(sk[i], max_keys)], 1u);
-}
-
-// Single workgroup: hist[0..nb) -> exclusive prefix sums in place
-__global__ void __launch_bounds__(1024) qwl_offsets_kernel(uint32_t *hist, uint32_t nb) {
-    __shared__ uint32_t part[1024];
-    const uint32_t t = threadIdx.x, per = (nb + 1023) / 1024;
-    const uint32_t lo = min(t * per, nb), hi = min(lo + per, nb);
-    uint32_t sum = 0;
-    for (uint32_t k = lo; k < hi; ++k) sum += hist[k];
-    part[t] = sum;
-    __syncthreads();
-    for (uint32_t d = 1; d < 1024; d <<= 1) {
-        const uint32_t a = t >= d ? part[t - d] : 0;
-        __syncthreads();
-        part[t] += a;
-        __syncthreads();
-    }
-    uint32_t run = part[t] - sum;
-    for (uint32_t k = lo; k < hi; ++k) {
-        const uint32_t c = hist[k];
-        hist[k] = run;
-        run += c;
-    }
-}
-
-__global__ void qwl_place_kernel(const uint32_t *sk, uint32_t n, uint32_t max_keys, uint32_t *next, uint32_t *k_out,
-                                 uint32_t *v_out) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t key = sk[i];
-    const uint32_t pos = atomicAdd(&next[count_bucket(key, max_keys)], 1u);
-    k_out[pos] = key;
-    v_out[pos] = i;
-}
-
 // rocprim's radix sort takes its merge-sort path up to 2^20 items by default (a block sort and ~20
 // merge launches, ~150 us for a 2^20-packet batch); Onesweep (a histogram, a scan and one pass per
 // 8-bit digit) is used for every size here.
@@ -194,7 +138,6 @@ size_t quad_worklist_bytes(uint32_t n, uint32_t max_keys, uint32_t *n_items_out)
     const uint32_t items = (uint32_t)((cap + 15) & ~15ull);
     size_t cub = 0;
     sort_pairs(nullptr, cub, nullptr, nullptr, nullptr, nullptr, n, 32, 0);
-    if (max_keys <= kCountMaxKeys) cub = std::max<size_t>(cub, 4ull * (max_keys * kLenClasses + 1));  // the counting sort's buckets
     if (n_items_out) *n_items_out = items;
     // keys in/out, vals in/out, counts, start, pstart, run counters, runs, worklist, tile keys, short
     // tiles, tile counter + run count + short count, sort temp (256-B aligned pieces)
@@ -238,21 +181,10 @@ hipError_t launch_quad_worklist(const qgcm_desc *descs, uint32_t n, uint32_t max
     if (n) hipLaunchKernelGGL(qwl_keys_kernel, dim3(g), dim3(bs), 0, s, descs, n, max_keys, key_valid, seal, k_in,
                                  v_in);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    const char *sv = getenv("QGCM_WORKLIST_SORT");  // "count": the counting sort (A/B knob)
-    if (max_keys <= kCountMaxKeys && sv && !strcmp(sv, "count")) {
-        const uint32_t nb = max_keys * kLenClasses + 1;
-        uint32_t *hist = static_cast<uint32_t *>(cub_tmp);
-        if ((e = hipMemsetAsync(hist, 0, 4ull * nb, s)) != hipSuccess) return e;
-        if (n) hipLaunchKernelGGL(qwl_hist_kernel, dim3(g), dim3(bs), 0, s, k_in, n, max_keys, hist);
-        hipLaunchKernelGGL(qwl_offsets_kernel, dim3(1), dim3(1024), 0, s, hist, nb);
-        if (n) hipLaunchKernelGGL(qwl_place_kernel, dim3(g), dim3(bs), 0, s, k_in, n, max_keys, hist, k_out, v_out);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-    } else {
-        // only the bits a valid key can use, plus one so that excluded entries (all ones) sort last
-        int end_bit = kLenBits + 1;
-        while (end_bit < 32 && (1ull << (end_bit - kLenBits - 1)) < max_keys) ++end_bit;
-        if ((e = sort_pairs(cub_tmp, cub_bytes, k_in, k_out, v_in, v_out, n, end_bit, s)) != hipSuccess) return e;
-    }
+    // only the bits a valid key can use, plus one so that excluded entries (all ones) sort last
+    int end_bit = kLenBits + 1;
+    while (end_bit < 32 && (1ull << (end_bit - kLenBits - 1)) < max_keys) ++end_bit;
+    if ((e = sort_pairs(cub_tmp, cub_bytes, k_in, k_out, v_in, v_out, n, end_bit, s)) != hipSuccess) return e;
     if (n) {
         hipLaunchKernelGGL(qwl_first_kernel, dim3(g), dim3(bs), 0, s, k_out, n, start);
         hipLaunchKernelGGL(qwl_count_kernel, dim3(g), dim3(bs), 0, s, k_out, n, start, counts);

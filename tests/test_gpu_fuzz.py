@@ -91,15 +91,10 @@ def draw_case(case: int):
     return rng, n, kidx, lens, offs, slot, size, aad_len, ~bad_key
 
 
-@pytest.mark.parametrize("sort", ["count", "radix"])
 @pytest.mark.parametrize("variant", ["default", 13])
 @pytest.mark.parametrize("seed", range(len(SIZES)))
-def test_descriptor_fuzz_vs_oracle(torch, fuzz_ctxs, fuzz_keys, variant, seed, sort, monkeypatch):
-    """sort: the worklist's key grouping -- the radix sort (the default) or the counting sort
-    (QGCM_WORKLIST_SORT=count, up to 4096 key slots)."""
+def test_descriptor_fuzz_vs_oracle(torch, fuzz_ctxs, fuzz_keys, variant, seed):
     from quantum_amd import batch
-
-    monkeypatch.setenv("QGCM_WORKLIST_SORT", sort)
 
     ctx = fuzz_ctxs[variant]
     rng, n, kidx, lens, offs, slot, size, aad_len, valid = draw_case(seed)

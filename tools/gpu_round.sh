@@ -188,10 +188,7 @@ for s in $STEPS; do
         QGCM_PIPE_CHUNK_MB=$v timeout -k 10 300 python3 tools/exp_host_legs.py e2e > $OUT/e2echunk_$v.jsonl 2>> $OUT/e2echunk.err
         check e2echunk_$v $?
       done ;;
-    wlab)  # config 3: the worklist's counting sort vs the radix sort, alternating in one process
-      timeout -k 10 600 python3 tools/ab_worklist.py 4 > $OUT/worklist_ab.jsonl 2> $OUT/worklist_ab.err
-      check wlab $? ;;
-    ftests)  # the descriptor-batch fuzz suite (both worklist sorts)
+    ftests)  # the descriptor-batch fuzz and config-3 suites
       timeout -k 10 600 python3 -u -m pytest tests/test_gpu_fuzz.py tests/test_gpu_config3.py -x -v --timeout 300 --timeout-method thread > $OUT/fuzz_tests.txt 2>&1
       check ftests $? ;;
     pcie)  # raw pinned-host <-> HBM hipMemcpyAsync rates of this box (the ceiling of every PCIe-inclusive figure)
