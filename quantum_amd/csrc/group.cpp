@@ -578,7 +578,7 @@ bool env_flag(const char *name) {  // read per call (A/B and tests switch it wit
     return v && atoi(v) != 0;
 }
 
-int dma_ready(DmaState &z, uint64_t stage, uint64_t side, size_t slots, size_t m, size_t nev) {
+int dma_ready(DmaState &z, uint64_t stage, uint64_t side, size_t slots, size_t m) {
     if (m > z.stat_cap) {
         if (z.d_stat) hipFree(z.d_stat);
         if (z.h_stat) hipHostFree(z.h_stat);
@@ -588,7 +588,7 @@ int dma_ready(DmaState &z, uint64_t stage, uint64_t side, size_t slots, size_t m
             return QGCM_E_NOMEM;
         z.stat_cap = m;
     }
-    while (z.ev_in.size() < nev) {
+    while (z.ev_in.size() < slots) {
         hipEvent_t e[3] = {};
         for (hipEvent_t &x : e)
             if (hipEventCreateWithFlags(&x, hipEventDisableTiming) != hipSuccess) {
@@ -634,7 +634,7 @@ int run_member_dma(Member &mb, bool seal, uint8_t *h_arena, const qgcm_desc *des
     const size_t nc = pl.chunks.size();
     const size_t S = std::min<size_t>(nc, (size_t)std::max(2, std::min(64, sv && *sv ? atoi(sv) : kDmaSlots)));
     const size_t m = pl.at.size();
-    int rc = dma_ready(z, pl.max_bytes, side, S, m, S);
+    int rc = dma_ready(z, pl.max_bytes, side, S, m);
     if (rc != QGCM_OK) return rc;
     // the member context's own pipeline streams, those qgcm_seal_host moves 46 GB/s each way with
     // (streams of the group's own measured the same, profiles/r4_s6)
@@ -660,7 +660,7 @@ int run_member_dma(Member &mb, bool seal, uint8_t *h_arena, const qgcm_desc *des
         // (which also covers the side area's copy-in) rather than leaving the wait to the copy-in
         // stream: a copy-in queued behind a GPU-side wait for the copy-out stream's blit kernels took
         // the keyed host batch from 25.8 to 13.0 GiB/s at 64-MiB chunks (profiles/r4_s16)
-        const size_t e = (size_t)k;  // this chunk's events: its slot's
+        const size_t e = (size_t)k;  // the slot's events
         if (c >= S && hipEventSynchronize(z.ev_out[e]) != hipSuccess) {
             rc = QGCM_E_HIP;
             break;
@@ -674,7 +674,6 @@ int run_member_dma(Member &mb, bool seal, uint8_t *h_arena, const qgcm_desc *des
             hd[j - ch.j0] = qgcm_desc{pl.at[j], d.len, d.key_idx};
             if (non) memcpy(hs + off_non + 12 * (j - ch.j0), h_nonces + 12ull * idx[j], 12);
         }
-
         for (size_t p = ch.p0; p < ch.p1 && rc == QGCM_OK; ++p) {
             const Piece &pc = pl.pieces[p];
             if (hipMemcpyAsync(ds + pc.dst, h_arena + pc.src, pc.bytes, hipMemcpyHostToDevice, s_in) != hipSuccess)
