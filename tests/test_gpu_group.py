@@ -201,6 +201,51 @@ def test_group_dma_runs_many_chunks_vs_oracle(torch, shift, slots, monkeypatch):
         grp.close()
 
 
+@pytest.mark.parametrize("G,grouped", [(1, False), (2, True), (2, False)])
+def test_group_seal_with_nonces_in_the_slots(torch, G, grouped):
+    """qgcm_group_seal_host with h_nonces NULL: each packet's nonce is already in its slot (the 12 bytes
+    after the tag's place), as a caller that draws nonces into the slots itself lays them out.  Paths:
+    one member (DMA runs), two members in qgcm_group_order's order (DMA runs) and interleaved (zero-copy);
+    sealed bytes against the oracle with those nonces, then opened back."""
+    from quantum_amd import shard
+
+    grp = shard.Group([0] * G, max_keys=32)
+    try:
+        rng = np.random.default_rng(0x6A07 + G + 10 * grouped)
+        keys = rng.integers(0, 256, 32 * 8, dtype=np.uint8).tobytes()
+        grp.set_keys(0, keys)
+        n = 2000
+        kidx = rng.integers(0, 8, n).astype(np.uint32)
+        if grouped:
+            kidx = kidx[grp.order(kidx)[0]]
+        lens = rng.integers(0, 3000, n).astype(np.uint32)
+        rec = (4 + lens.astype(np.uint64) + 28 + 3) & ~np.uint64(3)
+        offs = np.concatenate([[0], np.cumsum(rec)[:-1]]).astype(np.uint64)
+        size = int(offs[-1] + rec[-1])
+        arena, aptr, free = host_buffer(size, True)
+        try:
+            arena[:] = rng.integers(0, 256, size, dtype=np.uint8)
+            idx = offs.astype(np.int64)[:, None] + np.arange(4)
+            arena[idx] = np.frombuffer(AAD, np.uint8)
+            nonce_at = (offs.astype(np.int64) + 4 + lens.astype(np.int64) + 16)[:, None] + np.arange(12)
+            nonces = np.ascontiguousarray(arena[nonce_at].reshape(-1))
+            plain = arena.copy()
+            ref = plain.copy()
+            O.aesgo_seal_descs(keys, ref, offs, lens, kidx, nonces, 4, 8)
+            status = np.zeros(n, np.uint8)
+            assert grp.seal_host(aptr, shard.host_descs(offs, lens, kidx), n, None, 4, status.ctypes.data) == 0
+            want = "dma" if (G == 1 or grouped) else "zerocopy"
+            assert [grp.last_path(m) for m in range(G)] == [want] * G
+            assert bool((status == 1).all()) and np.array_equal(arena, ref)
+            assert grp.open_host(aptr, shard.host_descs(offs, lens + 28, kidx), n, 4, status.ctypes.data) == 0
+            pay = np.concatenate([np.arange(int(o), int(o) + 4 + int(L)) for o, L in zip(offs, lens)])
+            assert np.array_equal(arena[pay], plain[pay])
+        finally:
+            free()
+    finally:
+        grp.close()
+
+
 def test_group_zerocopy_records_at_the_allocation_end(torch):
     """Zero-copy path: records whose last byte is the last bytes of a one-page pinned allocation, with
     lengths that are not multiples of 4 or 16 (the gather reads whole dwords up to the next 4-B
