@@ -246,6 +246,47 @@ def test_group_seal_with_nonces_in_the_slots(torch, G, grouped):
         grp.close()
 
 
+def test_group_unaligned_records_take_the_copy_path(torch):
+    """Records packed back to back with no alignment (offsets not multiples of 4): neither DMA runs nor
+    zero-copy apply (both move records dword-wise), so the member gathers them through pinned staging;
+    sealed bytes against the oracle, opened back."""
+    from quantum_amd import shard
+
+    grp = shard.Group([0], max_keys=8)
+    try:
+        rng = np.random.default_rng(0x6A08)
+        keys = rng.integers(0, 256, 32 * 4, dtype=np.uint8).tobytes()
+        grp.set_keys(0, keys)
+        n = 1500
+        kidx = rng.integers(0, 4, n).astype(np.uint32)
+        lens = rng.integers(0, 2000, n).astype(np.uint32)
+        rec = 4 + lens.astype(np.uint64) + 28
+        offs = np.concatenate([[0], np.cumsum(rec)[:-1]]).astype(np.uint64)
+        assert bool((offs % 4 != 0).any())
+        size = int(offs[-1] + rec[-1])
+        arena, aptr, free = host_buffer(size, True)
+        try:
+            arena[:] = rng.integers(0, 256, size, dtype=np.uint8)
+            arena[offs.astype(np.int64)[:, None] + np.arange(4)] = np.frombuffer(AAD, np.uint8)
+            nonces, nptr, free_n = host_buffer(12 * n, True)
+            nonces[:] = rng.integers(0, 256, 12 * n, dtype=np.uint8)
+            plain, ref = arena.copy(), arena.copy()
+            O.aesgo_seal_descs(keys, ref, offs, lens, kidx, np.ascontiguousarray(nonces), 4, 8)
+            status = np.zeros(n, np.uint8)
+            assert grp.seal_host(aptr, shard.host_descs(offs, lens, kidx), n, nptr, 4, status.ctypes.data) == 0
+            assert grp.last_path(0) == "copy"
+            assert bool((status == 1).all()) and np.array_equal(arena, ref)
+            assert grp.open_host(aptr, shard.host_descs(offs, lens + 28, kidx), n, 4, status.ctypes.data) == 0
+            pay = np.concatenate([np.arange(int(o), int(o) + 4 + int(L)) for o, L in zip(offs, lens)])
+            assert np.array_equal(arena[pay], plain[pay])
+            del nonces
+            free_n()
+        finally:
+            free()
+    finally:
+        grp.close()
+
+
 def test_group_zerocopy_records_at_the_allocation_end(torch):
     """Zero-copy path: records whose last byte is the last bytes of a one-page pinned allocation, with
     lengths that are not multiples of 4 or 16 (the gather reads whole dwords up to the next 4-B
