@@ -180,10 +180,10 @@ struct SnapArgs {
     uint32_t limit;             // compress: longest output kept; uncompress: output capacity
     uint32_t sub;               // uncompress: lens[i] - sub is the compressed length (28 after an open)
     uint32_t off_in, off_out, off_sink, wave_bytes;  // off_sink: 256 B of per-lane scratch
+    uint32_t dec_sync;  // uncompress: 1 = drain the wave's LDS operations before each back-reference (A/B)
 };
-// group (compress only): 1 = snappy_compress_group_kernel, four packets per wave (a.wave_bytes = four
-// packet regions of a.off_sink bytes); 2 = the same with software-pipelined miss probes; 0 = one wave
-// per packet
+// group (compress only): true = snappy_compress_group_kernel, four packets per wave (a.wave_bytes = four
+// packet regions of a.off_sink bytes); false = one wave per packet
 constexpr uint32_t kSnapGroup = 4;
 hipError_t launch_snappy(bool compress, const SnapArgs &a, int waves_per_wg, int grid, hipStream_t s, bool group);
 
