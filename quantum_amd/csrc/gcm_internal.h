@@ -180,7 +180,6 @@ struct SnapArgs {
     uint32_t limit;             // compress: longest output kept; uncompress: output capacity
     uint32_t sub;               // uncompress: lens[i] - sub is the compressed length (28 after an open)
     uint32_t off_in, off_out, off_sink, wave_bytes;  // off_sink: 256 B of per-lane scratch
-    uint32_t dec_sync;  // uncompress: 1 = drain the wave's LDS operations before each back-reference (A/B)
 };
 // group (compress only): true = snappy_compress_group_kernel, four packets per wave (a.wave_bytes = four
 // packet regions of a.off_sink bytes); false = one wave per packet

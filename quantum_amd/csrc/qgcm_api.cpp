@@ -1164,7 +1164,6 @@ static int run_snappy(qgcm_ctx *ctx, bool compress, uint8_t *d_arena, uint64_t s
     a.max_in = max_in;
     a.limit = limit;
     a.sub = sub;
-    a.dec_sync = env_int("QGCM_SNAPPY_DEC_SYNC", 0) != 0;  // A/B knob (decoder)
     uint32_t tab = 0;
     if (compress) {
         uint32_t bits = 8;

@@ -530,7 +530,7 @@ __global__ void __launch_bounds__(256) snappy_compress_group_kernel(SnapArgs a) 
 }
 
 // decode.go Decode of in[0..n) into out (at most cap bytes); returns the length or -1
-__device__ int decode(const Wave &w, uint32_t n, uint32_t cap, bool sync) {
+__device__ int decode(const Wave &w, uint32_t n, uint32_t cap) {
     uint32_t total = 0, ip = 0;
     for (uint32_t sh = 0;; sh += 7) {
         if (ip >= n || ip >= 5) return -1;
@@ -578,9 +578,7 @@ __device__ int decode(const Wave &w, uint32_t n, uint32_t cap, bool sync) {
             ip += 4;
         }
         if (off == 0 || off > op || len > total - op) return -1;
-        // earlier elements' bytes are read back by other lanes: a wave's LDS operations complete in
-        // order, so the reads below see them without draining the queue first (dec_sync: drain, A/B)
-        if (sync) wave_lds_sync();
+        wave_lds_sync();  // earlier elements' bytes are in LDS before lanes read them back
         if (w.lane < len) w.out[op + w.lane] = w.out[op - off + w.lane % off];  // len <= 64
         op += len;
     }
@@ -608,7 +606,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) s
         int u = -1;
         if (take) {
             wave_lds_sync();
-            u = decode(w, len, a.limit, a.dec_sync != 0);
+            u = decode(w, len, a.limit);
             // an empty result fails: golang/snappy's Decode(nil, src) returns a nil slice for it and
             // compression.go:37-39 drops a nil packet
             if (u == 0) u = -1;

@@ -3,8 +3,7 @@ random, second half a repeated HTTP line, stride 1472): compress, seal, open, un
 by HIP events; the sealed arena is checked against tests/golden/config5_digest.json and the result
 against the plaintext arena (bench.extra_config5_resident).  The encoders alternate in one process,
 `rounds` times each: QGCM_SNAPPY_GROUP=1, four packets per wave (the default), and 0, one wave per
-packet; then the decoder with and without draining its LDS queue before each back-reference
-(QGCM_SNAPPY_DEC_SYNC=1 / 0).
+packet.
 
     python3 tools/exp_snappy_dev.py [reps] [rounds]
 """
@@ -22,13 +21,11 @@ def main() -> None:
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 2
     key = bench.derive_key(bench.SECRET, bench.SALT)
     for r in range(rounds):
-        for grp, sync in (("1", "0"), ("0", "0"), ("1", "1")):
+        for grp in ("1", "0"):
             os.environ["QGCM_SNAPPY_GROUP"] = grp
-            os.environ["QGCM_SNAPPY_DEC_SYNC"] = sync
             res = bench.extra_config5_resident(key, reps, verify=(r == 0))
-            print(json.dumps({"snappy_group": int(grp), "dec_sync": int(sync), **res}), flush=True)
+            print(json.dumps({"snappy_group": int(grp), **res}), flush=True)
     os.environ.pop("QGCM_SNAPPY_GROUP", None)
-    os.environ.pop("QGCM_SNAPPY_DEC_SYNC", None)
 
 
 if __name__ == "__main__":
