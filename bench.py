@@ -253,22 +253,28 @@ def extra_config3(reps: int = 5, verify: bool = True) -> dict:
     return out
 
 
-def extra_config3_host(reps: int = 3, verify: bool = True) -> dict:
+def extra_config3_host(reps: int = 3, verify: bool = True, members: int = 1) -> dict:
     """Config 3's keyed batch from pinned HOST memory through the multi-GPU drop-in's entry point
     (qgcm_group_seal_host / qgcm_group_open_host, one member on this GPU: the path quantum's multi-peer
     traffic takes, worker/outgoing.go:55-80 with common/mapping.go:90-99 keys): PCIe included.  The
     member's packets are one run of adjacent records, so they move by DMA in 64-MiB chunks (no gather).
     verify: the opened arena after the timed reps and the sealed arena of one more seal against
-    tests/golden/config3_digest.json."""
+    tests/golden/config3_digest.json.  members > 1 (tools/exp_host_legs.py only): that many member
+    contexts on this GPU, the batch laid out in qgcm_group_order's order (each member's packets one run;
+    the digests then do not apply)."""
     from quantum_amd import _lib
     from quantum_amd import workloads as W
     import ctypes as C
 
     keys = W.peer_keys()
     lens, kidx = W.lengths(), W.key_indices()
-    offs, size = W.layout(lens)
-    grp = shard.Group([0], max_keys=W.NKEYS)
+    grp = shard.Group([0] * members, max_keys=W.NKEYS)
     grp.set_keys(0, keys)
+    if members > 1:
+        order = grp.order(kidx)[0]
+        lens, kidx = lens[order], kidx[order]
+        verify = False
+    offs, size = W.layout(lens)
     Lb = _lib.lib()
     a_ptr, n_ptr = Lb.qgcm_host_alloc(size), Lb.qgcm_host_alloc(12 * W.N)
     host = np.frombuffer((C.c_uint8 * size).from_address(a_ptr), np.uint8)
@@ -294,7 +300,7 @@ def extra_config3_host(reps: int = 3, verify: bool = True) -> dict:
         t2 = time.perf_counter()
         ts.append(t1 - t0)
         to.append(t2 - t1)
-    path = grp.last_path(0)
+    path = ",".join(grp.last_path(m) for m in range(members))
     out = {}
     if verify:
         gold = json.load(open(os.path.join(ROOT, "tests", "golden", "config3_digest.json")))

@@ -58,6 +58,8 @@ for leg in %(leg)r.split("+"):  # legs joined by "+" run one after another in th
         out = bench.extra_e2e(key, reps=2, n=9 << 19)
     elif leg == "config3_host":
         out = bench.extra_config3_host(verify=False)
+    elif leg == "config3_host2":  # two member contexts on this GPU, the batch in qgcm_group_order's order
+        out = bench.extra_config3_host(verify=False, members=2)
     elif leg == "config5":
         out = bench.extra_config5(key, bench.host_cpus()["share"], verify=False)
     elif leg.startswith("sleep"):  # e.g. sleep20: idle this many seconds between legs
