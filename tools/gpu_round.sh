@@ -184,8 +184,10 @@ for s in $STEPS; do
       timeout -k 10 400 python3 tools/exp_host_legs.py e2e e2e_big > $OUT/e2e_big.jsonl 2> $OUT/e2e_big.err
       check e2ebig $? ;;
     members2)  # keyed host batch with two member contexts on this GPU (grouped layout): per-member DMA pipelines side by side, with per-chunk timelines
-      QGCM_GROUP_DMA_TIMELINE=1 timeout -k 10 400 python3 tools/exp_host_legs.py config3_host config3_host2 > $OUT/members2.jsonl 2> $OUT/members2.err
-      check members2 $? ;;
+      for q in ${HWQS:-4}; do
+        GPU_MAX_HW_QUEUES=$q timeout -k 10 400 python3 tools/exp_host_legs.py config3_host config3_host2 > $OUT/members2_q$q.jsonl 2> $OUT/members2_q$q.err
+        check members2_q$q $?
+      done ;;
     e2echunk)  # qgcm_seal_host / open_host chunk size (QGCM_PIPE_CHUNK_MB), each in a fresh process
       for v in ${E2ECHUNKS:-32 64 128 256}; do
         QGCM_PIPE_CHUNK_MB=$v timeout -k 10 300 python3 tools/exp_host_legs.py e2e > $OUT/e2echunk_$v.jsonl 2>> $OUT/e2echunk.err
