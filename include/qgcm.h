@@ -164,7 +164,8 @@ int qgcm_open_host(qgcm_ctx *ctx, uint8_t *h_arena, uint64_t stride, uint32_t n,
                    uint32_t key_idx, uint32_t aad_len, uint8_t *h_status);
 
 /* ---- several GPUs behind one process (quantum is one process: main.go:29-114, 72-75) ---- */
-/* A group of `count` member contexts, member k on devices[k] (members may share a device).  Keyed
+/* A group of `count` member contexts, member k on devices[k] (members may share a device, but then share
+ * its hardware queues and PCIe link: one member per GPU is the intended layout).  Keyed
  * traffic is hash-sharded: key index k belongs to member qgcm_group_shard(k) = ((k * 0x9E3779B97F4A7C15)
  * mod 2^64 >> 32) mod count (quantum_amd/shard.py key_shard), so a peer's packets stay on
  * one GPU and each member holds only its peers' keys.  No collective, no GPU-to-GPU traffic.
