@@ -188,6 +188,9 @@ for s in $STEPS; do
         GPU_MAX_HW_QUEUES=$q timeout -k 10 400 python3 tools/exp_host_legs.py config3_host config3_host2 > $OUT/members2_q$q.jsonl 2> $OUT/members2_q$q.err
         check members2_q$q $?
       done ;;
+    hostsizes)  # worker-sized host batches: seal+open pair latency and rate vs batch size (qgcm_seal_host and a one-member group)
+      timeout -k 10 400 python3 tools/exp_host_batch_sizes.py 30 > $OUT/host_batch_sizes.jsonl 2> $OUT/host_batch_sizes.err
+      check hostsizes $? ;;
     e2echunk)  # qgcm_seal_host / open_host chunk size (QGCM_PIPE_CHUNK_MB), each in a fresh process
       for v in ${E2ECHUNKS:-32 64 128 256}; do
         QGCM_PIPE_CHUNK_MB=$v timeout -k 10 300 python3 tools/exp_host_legs.py e2e > $OUT/e2echunk_$v.jsonl 2>> $OUT/e2echunk.err
