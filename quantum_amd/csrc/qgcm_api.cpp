@@ -786,8 +786,14 @@ static int run_host(qgcm_ctx *ctx, bool seal, uint8_t *h_arena, uint64_t stride,
         if (hipHostMalloc(&ctx->h_stat, n, hipHostMallocDefault) != hipSuccess) return QGCM_E_NOMEM;
         ctx->hstat_cap = n;
     }
-    // one copy-in stream: alternating two (two SDMA queues) measured 27.3 vs 38.0 GiB/s
-    hipStream_t s_in = ctx->pipe[0], s_k = ctx->pipe[1], s_out = ctx->pipe[2];
+    // one copy-in stream: alternating two (two SDMA queues) measured 27.3 vs 38.0 GiB/s.  A batch of one
+    // chunk (a worker's recvmmsg batch) has nothing to overlap: copy-in, kernel and copy-out go on one
+    // stream, with no cross-stream events and one synchronize
+    const bool one = nchunks == 1;
+    hipStream_t s_in = ctx->pipe[0], s_k = one ? s_in : ctx->pipe[1], s_out = one ? s_in : ctx->pipe[2];
+    auto link = [&](hipEvent_t e, hipStream_t from, hipStream_t to) {  // `to` waits for `from`'s work so far
+        return from == to || (hipEventRecord(e, from) == hipSuccess && hipStreamWaitEvent(to, e, 0) == hipSuccess);
+    };
     int rc = QGCM_OK;
     if (non && hipMemcpyAsync(d_non_all, h_nonces, 12ull * n, hipMemcpyHostToDevice, s_in) != hipSuccess)
         rc = QGCM_E_HIP;
@@ -799,7 +805,7 @@ static int run_host(qgcm_ctx *ctx, bool seal, uint8_t *h_arena, uint64_t stride,
         // slot k is free once the copy-out of chunk c - nslots has landed
         if ((c >= (uint64_t)nslots && hipStreamWaitEvent(s_in, ctx->ev_out[k], 0) != hipSuccess) ||
             hipMemcpyAsync(d, h, cn * stride, hipMemcpyHostToDevice, s_in) != hipSuccess ||
-            hipEventRecord(ctx->ev_in[k], s_in) != hipSuccess || hipStreamWaitEvent(s_k, ctx->ev_in[k], 0) != hipSuccess) {
+            !link(ctx->ev_in[k], s_in, s_k)) {
             rc = QGCM_E_HIP;
             break;
         }
@@ -809,16 +815,18 @@ static int run_host(qgcm_ctx *ctx, bool seal, uint8_t *h_arena, uint64_t stride,
             rc = run_uniform(ctx, seal, d, stride, (uint32_t)cn, len, key_idx, non ? d_non_all + 12 * c0 : nullptr,
                              aad_len, d_stat_all + c0, s_k);
         if (rc == QGCM_OK &&
-            (hipEventRecord(ctx->ev_kern[k], s_k) != hipSuccess || hipStreamWaitEvent(s_out, ctx->ev_kern[k], 0) != hipSuccess ||
+            (!link(ctx->ev_kern[k], s_k, s_out) ||
              hipMemcpyAsync(h, d, cn * stride, hipMemcpyDeviceToHost, s_out) != hipSuccess ||
-             hipEventRecord(ctx->ev_out[k], s_out) != hipSuccess))
+             (!one && hipEventRecord(ctx->ev_out[k], s_out) != hipSuccess)))
             rc = QGCM_E_HIP;
     }
-    if (rc == QGCM_OK && (hipStreamWaitEvent(s_out, ctx->ev_kern[(nchunks - 1) % nslots], 0) != hipSuccess ||
+    if (rc == QGCM_OK && ((!one && hipStreamWaitEvent(s_out, ctx->ev_kern[(nchunks - 1) % nslots], 0) != hipSuccess) ||
                           hipMemcpyAsync(ctx->h_stat, d_stat_all, n, hipMemcpyDeviceToHost, s_out) != hipSuccess))
         rc = QGCM_E_HIP;
-    for (hipStream_t p : {s_in, s_k, s_out})
+    for (hipStream_t p : {s_in, s_k, s_out}) {
+        if (one && p != s_in) continue;
         if (hipStreamSynchronize(p) != hipSuccess) rc = QGCM_E_HIP;
+    }
     if (rc != QGCM_OK) return rc;
     int bad = 0;
     for (uint32_t i = 0; i < n; ++i) bad += ctx->h_stat[i] != 1;
