@@ -11,6 +11,8 @@
 #include <hip/hip_runtime.h>
 #include <rocprim/device/device_radix_sort.hpp>
 #include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
 
 #include "gcm_internal.h"
 
@@ -122,6 +124,151 @@ __global__ void qwl_scatter_kernel(const uint32_t *sorted_keys, const uint32_t *
     if ((w & 15u) == 0) tile_keys[w >> 4] = k;
 }
 
+// ---- small batches (n <= kSmallWl): the whole worklist in ONE workgroup ----
+// A worker-sized batch (a recvmmsg batch, a few thousand packets) spent ~0.15 ms in the ~15 launches
+// of the path below (keys, radix sort, per-key counts, scan, scatter, their fills), more than its
+// kernels.  Here one 1024-thread workgroup sorts (sort key, index) pairs in LDS (bitonic, so ties keep
+// arena order: the key's packets in input order within a length rank, as the stable radix sort leaves
+// them), finds each key's segment, and writes the same worklist, tile keys, run table, short-tile list
+// and counters the multi-launch path does.
+constexpr uint32_t kSmallWl = 4096;
+constexpr uint32_t kSmallThreads = 1024;
+
+// exclusive scan of v[0..m) in place (m <= 4 * kSmallThreads); returns the total.  part: kSmallThreads words
+__device__ uint32_t wg_exclusive_scan(uint32_t *v, uint32_t m, uint32_t *part) {
+    const uint32_t t = threadIdx.x, per = (m + kSmallThreads - 1) / kSmallThreads;
+    const uint32_t lo = min(t * per, m), hi = min(lo + per, m);
+    uint32_t sum = 0;
+    for (uint32_t k = lo; k < hi; ++k) sum += v[k];
+    part[t] = sum;
+    __syncthreads();
+    for (uint32_t d = 1; d < kSmallThreads; d <<= 1) {
+        const uint32_t a = t >= d ? part[t - d] : 0u;
+        __syncthreads();
+        part[t] += a;
+        __syncthreads();
+    }
+    uint32_t run = part[t] - sum;
+    const uint32_t total = part[kSmallThreads - 1];
+    for (uint32_t k = lo; k < hi; ++k) {
+        const uint32_t c = v[k];
+        v[k] = run;
+        run += c;
+    }
+    __syncthreads();
+    return total;
+}
+
+__global__ void __launch_bounds__(kSmallThreads)
+qwl_small_kernel(const qgcm_desc *descs, uint32_t n, uint32_t max_keys, const uint8_t *key_valid, bool seal,
+                 uint32_t items, uint32_t *worklist, uint32_t *tile_keys, uint2 *runs, uint32_t *run_next,
+                 uint32_t *short_tiles, uint32_t *counter) {
+    __shared__ uint64_t e[kSmallWl];                   // (sort key << 32 | index), sorted ascending
+    __shared__ uint32_t seg[kSmallWl], aux[kSmallWl];  // per entry, then per segment
+    __shared__ uint32_t part[kSmallThreads];
+    __shared__ uint32_t nvalid_s;
+    const uint32_t t = threadIdx.x;
+    uint32_t P = 64;
+    while (P < n) P <<= 1;
+    for (uint32_t i = t; i < P; i += kSmallThreads) {
+        uint32_t sk = 0xffffffffu;
+        if (i < n) {
+            const qgcm_desc d = descs[i];
+            const bool ok = d.key_idx < max_keys && key_valid[d.key_idx] && (seal || d.len >= (uint32_t)QGCM_OVERHEAD) &&
+                            d.len - (seal ? 0u : (uint32_t)QGCM_OVERHEAD) < QGCM_MAX_PAYLOAD;
+            if (ok) {
+                const uint32_t L = seal ? d.len : d.len - QGCM_OVERHEAD;
+                const uint32_t nb = min((L + 15u) >> 4, (1u << kLenBits) - 1u);
+                sk = (d.key_idx << kLenBits) | ((1u << kLenBits) - 1u - nb);
+            }
+        }
+        e[i] = ((uint64_t)sk << 32) | (i < n ? i : 0xffffffffu);
+    }
+    for (uint32_t i = t; i < items; i += kSmallThreads) worklist[i] = 0xffffffffu;  // padding entries
+    __syncthreads();
+    for (uint32_t k = 2; k <= P; k <<= 1)  // bitonic sort, ascending
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = t; i < P; i += kSmallThreads) {
+                const uint32_t l = i ^ j;
+                if (l > i) {
+                    const uint64_t a = e[i], b = e[l];
+                    if (((i & k) == 0) == (a > b)) {
+                        e[i] = b;
+                        e[l] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    // valid entries (sort key != all ones) come first; a segment starts where the key index changes
+    for (uint32_t i = t; i < P; i += kSmallThreads) {
+        const uint32_t sk = (uint32_t)(e[i] >> 32);
+        const bool valid = sk != 0xffffffffu;
+        if (valid && (i + 1 == P || (uint32_t)(e[i + 1] >> 32) == 0xffffffffu)) nvalid_s = i + 1;
+        seg[i] = valid && (i == 0 || (uint32_t)(e[i - 1] >> 32) >> kLenBits != sk >> kLenBits) ? 1u : 0u;
+    }
+    if (t == 0 && (uint32_t)(e[0] >> 32) == 0xffffffffu) nvalid_s = 0;
+    __syncthreads();
+    const uint32_t nv = nvalid_s;
+    const uint32_t S = wg_exclusive_scan(seg, nv, part);  // seg[i]: segment ordinal of i's segment start
+    // per segment: start entry (aux), then tiles; entries keep their segment via seg[] after this pass
+    for (uint32_t i = t; i < nv; i += kSmallThreads) {
+        const bool start = i == 0 || (uint32_t)(e[i - 1] >> 32) >> kLenBits != (uint32_t)(e[i] >> 32) >> kLenBits;
+        if (start) aux[seg[i]] = i;
+    }
+    __syncthreads();
+    for (uint32_t i = t; i < nv; i += kSmallThreads) {  // seg[i] = the segment of entry i (its start's ordinal)
+        const bool start = i == 0 || (uint32_t)(e[i - 1] >> 32) >> kLenBits != (uint32_t)(e[i] >> 32) >> kLenBits;
+        if (!start) {
+            uint32_t lo = 0, hi = S;  // the last segment whose start is <= i
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (aux[mid] <= i) lo = mid; else hi = mid;
+            }
+            seg[i] = lo;
+        }
+    }
+    __syncthreads();
+    // segment s: count = next start - start, tiles = ceil(count / 16); tile bases by an exclusive scan
+    __shared__ uint32_t tiles[kSmallWl], rflag[kSmallWl], sflag[kSmallWl];
+    for (uint32_t q = t; q < S; q += kSmallThreads) {
+        const uint32_t cnt = (q + 1 < S ? aux[q + 1] : nv) - aux[q];
+        const uint32_t nt = (cnt + 15u) >> 4;
+        tiles[q] = nt;
+        rflag[q] = nt >= kSegMinTiles ? 1u : 0u;
+        sflag[q] = nt >= kSegMinTiles ? 0u : nt;
+    }
+    __syncthreads();
+    // keep the counts: rflag / sflag are scanned in place, tiles too (copied first for the run ends)
+    __shared__ uint32_t ntile[kSmallWl];
+    for (uint32_t q = t; q < S; q += kSmallThreads) ntile[q] = tiles[q];
+    __syncthreads();
+    wg_exclusive_scan(tiles, S, part);
+    const uint32_t nruns = wg_exclusive_scan(rflag, S, part);
+    const uint32_t nshort = wg_exclusive_scan(sflag, S, part);
+    for (uint32_t q = t; q < S; q += kSmallThreads) {
+        const uint32_t base = tiles[q], nt = ntile[q];
+        if (nt >= kSegMinTiles) {
+            runs[rflag[q]] = uint2{base, base + nt};
+            run_next[rflag[q]] = 0u;
+        } else {
+            for (uint32_t j = 0; j < nt; ++j) short_tiles[sflag[q] + j] = base + j;
+        }
+    }
+    for (uint32_t i = t; i < nv; i += kSmallThreads) {
+        const uint32_t q = seg[i];
+        const uint32_t w = tiles[q] * 16u + (i - aux[q]);
+        worklist[w] = (uint32_t)e[i];
+        if ((w & 15u) == 0) tile_keys[w >> 4] = (uint32_t)(e[i] >> 32) >> kLenBits;
+    }
+    if (t == 0) {
+        counter[0] = 0u;
+        counter[1] = nruns;
+        counter[2] = nshort;
+        counter[3] = 0u;
+    }
+}
+
 // rocprim's radix sort takes its merge-sort path up to 2^20 items by default (a block sort and ~20
 // merge launches, ~150 us for a 2^20-packet batch); Onesweep (a histogram, a scan and one pass per
 // 8-bit digit) is used for every size here.
@@ -175,6 +322,22 @@ hipError_t launch_quad_worklist(const qgcm_desc *descs, uint32_t n, uint32_t max
     void *cub_tmp = p;
     size_t cub_bytes = need - (size_t)(p - static_cast<char *>(ws));
     hipError_t e;
+    const char *sv = getenv("QGCM_SMALL_WORKLIST");  // "0": small batches take the multi-launch path too (A/B)
+    if (n && n <= kSmallWl && !(sv && !strcmp(sv, "0"))) {
+        hipLaunchKernelGGL(qwl_small_kernel, dim3(1), dim3(kSmallThreads), 0, s, descs, n, max_keys, key_valid, seal,
+                           items, worklist, tile_keys, runs, run_next, short_tiles, counter);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        out->worklist = worklist;
+        out->tile_keys = tile_keys;
+        out->runs = runs;
+        out->run_next = run_next;
+        out->nruns = counter + 1;
+        out->short_tiles = short_tiles;
+        out->nshort = counter + 2;
+        out->tile_counter = counter;
+        out->n_items = items;
+        return hipSuccess;
+    }
     if ((e = hipMemsetAsync(zero0, 0, zero_bytes, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(ones0, 0xff, ones_bytes, s)) != hipSuccess) return e;
     const int bs = 256, g = (int)((n + bs - 1) / bs);

@@ -91,10 +91,16 @@ def draw_case(case: int):
     return rng, n, kidx, lens, offs, slot, size, aad_len, ~bad_key
 
 
+@pytest.mark.parametrize("small", ["1", "0"])
 @pytest.mark.parametrize("variant", ["default", 13])
 @pytest.mark.parametrize("seed", range(len(SIZES)))
-def test_descriptor_fuzz_vs_oracle(torch, fuzz_ctxs, fuzz_keys, variant, seed):
+def test_descriptor_fuzz_vs_oracle(torch, fuzz_ctxs, fuzz_keys, variant, seed, small, monkeypatch):
+    """small: QGCM_SMALL_WORKLIST -- batches of up to 4096 packets build their worklist in one workgroup
+    ("1", the default) or through the multi-launch radix-sort path ("0"); larger batches always take
+    the latter."""
     from quantum_amd import batch
+
+    monkeypatch.setenv("QGCM_SMALL_WORKLIST", small)
 
     ctx = fuzz_ctxs[variant]
     rng, n, kidx, lens, offs, slot, size, aad_len, valid = draw_case(seed)

@@ -191,6 +191,9 @@ for s in $STEPS; do
     hostsizes)  # worker-sized host batches: seal+open pair latency and rate vs batch size (qgcm_seal_host and a one-member group)
       timeout -k 10 400 python3 tools/exp_host_batch_sizes.py 30 > $OUT/host_batch_sizes.jsonl 2> $OUT/host_batch_sizes.err
       check hostsizes $? ;;
+    smallwl)  # small keyed batches: worklist in one workgroup vs the multi-launch path, alternating
+      timeout -k 10 300 python3 tools/exp_small_worklist.py 30 > $OUT/small_worklist.jsonl 2> $OUT/small_worklist.err
+      check smallwl $? ;;
     e2echunk)  # qgcm_seal_host / open_host chunk size (QGCM_PIPE_CHUNK_MB), each in a fresh process
       for v in ${E2ECHUNKS:-32 64 128 256}; do
         QGCM_PIPE_CHUNK_MB=$v timeout -k 10 300 python3 tools/exp_host_legs.py e2e > $OUT/e2echunk_$v.jsonl 2>> $OUT/e2echunk.err
