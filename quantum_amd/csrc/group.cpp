@@ -638,8 +638,11 @@ int run_member_dma(Member &mb, bool seal, uint8_t *h_arena, const qgcm_desc *des
     if (rc != QGCM_OK) return rc;
     // the member context's own pipeline streams, those qgcm_seal_host moves 46 GB/s each way with
     // (streams of the group's own measured the same, profiles/r4_s6)
+    // one chunk (a worker-sized batch) has nothing to overlap: one stream, no events, one synchronize
     std::lock_guard<std::mutex> io(qgcm::ctx_io_mu(mb.ctx));
-    hipStream_t s_in = qgcm::ctx_pipe(mb.ctx, 0), s_k = qgcm::ctx_pipe(mb.ctx, 1), s_out = qgcm::ctx_pipe(mb.ctx, 2);
+    const bool one = nc == 1;
+    hipStream_t s_in = qgcm::ctx_pipe(mb.ctx, 0);
+    hipStream_t s_k = one ? s_in : qgcm::ctx_pipe(mb.ctx, 1), s_out = one ? s_in : qgcm::ctx_pipe(mb.ctx, 2);
     // QGCM_GROUP_DMA_TIMELINE=1 (diagnostics): timing events after each chunk's copy-in, kernels and
     // copy-out, printed to stderr as ms since the call's first copy-in was queued (no profiler attached)
     std::vector<hipEvent_t> tl;
@@ -681,7 +684,8 @@ int run_member_dma(Member &mb, bool seal, uint8_t *h_arena, const qgcm_desc *des
         }
         if (rc == QGCM_OK &&
             (hipMemcpyAsync(ds + dside, hs, side, hipMemcpyHostToDevice, s_in) != hipSuccess ||
-             hipEventRecord(z.ev_in[e], s_in) != hipSuccess || hipStreamWaitEvent(s_k, z.ev_in[e], 0) != hipSuccess))
+             (!one && (hipEventRecord(z.ev_in[e], s_in) != hipSuccess ||
+                       hipStreamWaitEvent(s_k, z.ev_in[e], 0) != hipSuccess))))
             rc = QGCM_E_HIP;
         if (rc != QGCM_OK) break;
         if (!tl.empty()) hipEventRecord(tl[3 * c], s_in);
@@ -691,21 +695,23 @@ int run_member_dma(Member &mb, bool seal, uint8_t *h_arena, const qgcm_desc *des
                   : qgcm_open_batch(mb.ctx, ds, dd, (uint32_t)cn, aad_len, z.d_stat + ch.j0, s_k);
         if (rc != QGCM_OK) break;
         if (!tl.empty()) hipEventRecord(tl[3 * c + 1], s_k);
-        if (hipEventRecord(z.ev_k[e], s_k) != hipSuccess || hipStreamWaitEvent(s_out, z.ev_k[e], 0) != hipSuccess)
+        if (!one && (hipEventRecord(z.ev_k[e], s_k) != hipSuccess || hipStreamWaitEvent(s_out, z.ev_k[e], 0) != hipSuccess))
             rc = QGCM_E_HIP;
         for (size_t p = ch.p0; p < ch.p1 && rc == QGCM_OK; ++p) {
             const Piece &pc = pl.pieces[p];
             if (hipMemcpyAsync(h_arena + pc.src, ds + pc.dst, pc.bytes, hipMemcpyDeviceToHost, s_out) != hipSuccess)
                 rc = QGCM_E_HIP;
         }
-        if (rc == QGCM_OK && hipEventRecord(z.ev_out[e], s_out) != hipSuccess) rc = QGCM_E_HIP;
+        if (rc == QGCM_OK && !one && hipEventRecord(z.ev_out[e], s_out) != hipSuccess) rc = QGCM_E_HIP;
         if (!tl.empty()) hipEventRecord(tl[3 * c + 2], s_out);
     }
     // every kernel has run when s_k gets here
     if (rc == QGCM_OK && hipMemcpyAsync(z.h_stat, z.d_stat, m, hipMemcpyDeviceToHost, s_k) != hipSuccess)
         rc = QGCM_E_HIP;
-    for (hipStream_t x : {s_in, s_k, s_out})
+    for (hipStream_t x : {s_in, s_k, s_out}) {
+        if (one && x != s_in) continue;
         if (hipStreamSynchronize(x) != hipSuccess && rc == QGCM_OK) rc = QGCM_E_HIP;
+    }
     if (!tl.empty()) {
         std::string line = "{\"dma_timeline_ms\": [";
         for (size_t q = 0; q < c; ++q) {
@@ -769,11 +775,17 @@ int run_group(qgcm_group *g, bool seal, uint8_t *h_arena, const qgcm_desc *descs
     const uint64_t dma_chunk = cv && *cv ? (uint64_t)std::max(1, std::min(4096, atoi(cv))) << 20 : kDmaChunk;
     std::vector<int> rc(G, QGCM_OK), bad(G, 0), used_zc(G, 1);
     std::vector<std::thread> thr;
+    int active = 0;
+    for (int k = 0; k < G; ++k) active += part[k].empty() ? 0 : 1;
+    // A batch for one member whose records move by DMA runs on the calling thread: a thread per call
+    // costs tens of microseconds, a worker-sized batch's whole budget.  (Other paths keep the member
+    // thread: it is pinned to the GPU's NUMA node before it allocates or touches host staging.)
+    const bool inline_one = active == 1 && sorted;
     for (int k = 0; k < G; ++k) {
         if (part[k].empty()) continue;
-        thr.emplace_back([&, k] {
+        auto work = [&, k](bool pin) {
             Member &mb = g->m[k];
-            if (mb.ncpus > 0) pthread_setaffinity_np(pthread_self(), sizeof(mb.cpus), &mb.cpus);
+            if (pin && mb.ncpus > 0) pthread_setaffinity_np(pthread_self(), sizeof(mb.cpus), &mb.cpus);
             if (hipSetDevice(mb.device) != hipSuccess) {
                 rc[k] = QGCM_E_HIP;
                 return;
@@ -801,7 +813,30 @@ int run_group(qgcm_group *g, bool seal, uint8_t *h_arena, const qgcm_desc *descs
                                        &bad[k], g->zc_chunk)
                        : run_member(mb, seal, h_arena, descs, part[k].data(), part[k].size(), h_nonces, aad_len,
                                     h_status, &bad[k]);
-        });
+        };
+        if (!inline_one) {
+            thr.emplace_back(work, true);
+            continue;
+        }
+        // inline: the DMA plan decides first; a member that would take another path gets its thread
+        const size_t m = part[k].size();
+        plan_dma(seal, descs, part[k].data(), m, dma_chunk, (uint32_t)((uintptr_t)h_arena & 255), plan[k]);
+        if (plan[k].piece_bytes < kMinRun * plan[k].pieces.size()) {
+            thr.emplace_back(work, true);
+            continue;
+        }
+        int dev0 = 0;
+        const bool had = hipGetDevice(&dev0) == hipSuccess;
+        Member &mb = g->m[k];
+        if (hipSetDevice(mb.device) != hipSuccess) {
+            rc[k] = QGCM_E_HIP;
+        } else {
+            mb.last_path = 2;
+            used_zc[k] = 0;
+            rc[k] = run_member_dma(mb, seal, h_arena, descs, part[k].data(), plan[k], h_nonces, aad_len, h_status,
+                                   &bad[k]);
+        }
+        if (had) hipSetDevice(dev0);  // the caller's current device, as it was
     }
     for (auto &t : thr) t.join();
     g->last_zc = zc && std::all_of(used_zc.begin(), used_zc.end(), [](int u) { return u == 1; }) ? 1 : 0;
