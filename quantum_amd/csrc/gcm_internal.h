@@ -86,8 +86,12 @@ struct QuadWorklist {
     uint32_t *tile_counter;  // zeroed
     uint32_t n_items;
 };
+// status (may be NULL): the batch's status bytes; the one-workgroup path for small batches zeroes them
+// itself (small_worklist(n)), the caller fills them otherwise
 hipError_t launch_quad_worklist(const qgcm_desc *descs, uint32_t n, uint32_t max_keys, const uint8_t *key_valid,
-                                bool seal, void *ws, size_t ws_bytes, QuadWorklist *out, hipStream_t s);
+                                bool seal, void *ws, size_t ws_bytes, QuadWorklist *out, hipStream_t s,
+                                uint8_t *status);
+bool small_worklist(uint32_t n);  // a batch of n packets builds its worklist in one workgroup
 hipError_t launch_packets(bool seal, int variant, const Batch &b, int grid, hipStream_t s);
 // One packet, one 512-thread workgroup (qgcm_seal_one / qgcm_open_one): the slot (b.stride bytes,
 // a multiple of 16, at most kOneCap - 16) is staged in LDS; b.n must be 1.

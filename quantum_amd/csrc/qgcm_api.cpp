@@ -313,7 +313,9 @@ int run_descs(qgcm_ctx *ctx, bool seal, uint8_t *arena, const qgcm_desc *descs, 
     if (((uintptr_t)arena & 3) || (nonces && ((uintptr_t)nonces & 3))) return QGCM_E_ARG;
     if (n == 0) return QGCM_OK;
     if (hipSetDevice(ctx->device) != hipSuccess) return QGCM_E_HIP;
-    if (status && hipMemsetAsync(status, 0, n, s) != hipSuccess) return QGCM_E_HIP;
+    // statuses start at 0 (packets left out of the worklist keep it); small batches' worklist kernel
+    // zeroes them itself
+    if (status && !small_worklist(n) && hipMemsetAsync(status, 0, n, s) != hipSuccess) return QGCM_E_HIP;
     // The workspace is reused by the next call on any stream: serialize descriptor batches per ctx.
     std::lock_guard<std::mutex> g(ctx->ws_mu);
     // ...and on the device: this batch's worklist build must not start before the previous batch's
@@ -358,8 +360,8 @@ int run_descs_locked(qgcm_ctx *ctx, bool seal, const qgcm_desc *descs, uint32_t 
             ctx->qws_cap = need;
         }
         QuadWorklist q{};
-        if (launch_quad_worklist(descs, n, ctx->max_keys, ctx->d_key_valid, seal, ctx->d_qws, ctx->qws_cap, &q, s) !=
-            hipSuccess)
+        if (launch_quad_worklist(descs, n, ctx->max_keys, ctx->d_key_valid, seal, ctx->d_qws, ctx->qws_cap, &q, s,
+                                 status) != hipSuccess)
             return QGCM_E_HIP;
         b.worklist = q.worklist;
         b.tile_keys = q.tile_keys;
@@ -368,9 +370,13 @@ int run_descs_locked(qgcm_ctx *ctx, bool seal, const qgcm_desc *descs, uint32_t 
         b.nruns = q.nruns;
         b.tile_counter = q.tile_counter;
         b.n_items = q.n_items;
-        if (launch_packets(seal, v, b, grid_for(ctx, b.n_items, v), s) != hipSuccess) return QGCM_E_HIP;
-        ctx->count(v == kVariantDescQuad ? QGCM_KERNEL_SEGMENTED : QGCM_KERNEL_PER_WAVE);
+        // fewer than kSegMinTiles * 16 packets cannot give a key a run: the segmented kernel would find
+        // none, so only its complement (the per-wave kernel) is launched
         const int vc = variant_complement(v);
+        if (vc < 0 || n >= kSegMinTiles * 16u) {
+            if (launch_packets(seal, v, b, grid_for(ctx, b.n_items, v), s) != hipSuccess) return QGCM_E_HIP;
+            ctx->count(v == kVariantDescQuad ? QGCM_KERNEL_SEGMENTED : QGCM_KERNEL_PER_WAVE);
+        }
         if (vc < 0) return QGCM_OK;
         // the short keys' tiles (fewer than kSegMinTiles per key) through the per-wave kernel; its
         // dynamic tile counter is the next word of the zeroed counter block

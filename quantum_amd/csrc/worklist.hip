@@ -162,7 +162,7 @@ __device__ uint32_t wg_exclusive_scan(uint32_t *v, uint32_t m, uint32_t *part) {
 __global__ void __launch_bounds__(kSmallThreads)
 qwl_small_kernel(const qgcm_desc *descs, uint32_t n, uint32_t max_keys, const uint8_t *key_valid, bool seal,
                  uint32_t items, uint32_t *worklist, uint32_t *tile_keys, uint2 *runs, uint32_t *run_next,
-                 uint32_t *short_tiles, uint32_t *counter) {
+                 uint32_t *short_tiles, uint32_t *counter, uint8_t *status) {
     __shared__ uint64_t e[kSmallWl];                   // (sort key << 32 | index), sorted ascending
     __shared__ uint32_t seg[kSmallWl], aux[kSmallWl];  // per entry, then per segment
     __shared__ uint32_t part[kSmallThreads];
@@ -185,6 +185,8 @@ qwl_small_kernel(const qgcm_desc *descs, uint32_t n, uint32_t max_keys, const ui
         e[i] = ((uint64_t)sk << 32) | (i < n ? i : 0xffffffffu);
     }
     for (uint32_t i = t; i < items; i += kSmallThreads) worklist[i] = 0xffffffffu;  // padding entries
+    if (status)  // the batch's statuses start at 0 (excluded packets keep it), in place of a separate fill
+        for (uint32_t i = t; i < n; i += kSmallThreads) status[i] = 0;
     __syncthreads();
     for (uint32_t k = 2; k <= P; k <<= 1)  // bitonic sort, ascending
         for (uint32_t j = k >> 1; j > 0; j >>= 1) {
@@ -293,8 +295,14 @@ size_t quad_worklist_bytes(uint32_t n, uint32_t max_keys, uint32_t *n_items_out)
            al(16) + al(cub);
 }
 
+bool small_worklist(uint32_t n) {
+    const char *sv = getenv("QGCM_SMALL_WORKLIST");  // "0": small batches take the multi-launch path too (A/B)
+    return n && n <= kSmallWl && !(sv && !strcmp(sv, "0"));
+}
+
 hipError_t launch_quad_worklist(const qgcm_desc *descs, uint32_t n, uint32_t max_keys, const uint8_t *key_valid,
-                                bool seal, void *ws, size_t ws_bytes, QuadWorklist *out, hipStream_t s) {
+                                bool seal, void *ws, size_t ws_bytes, QuadWorklist *out, hipStream_t s,
+                                uint8_t *status) {
     uint32_t items = 0;
     const size_t need = quad_worklist_bytes(n, max_keys, &items);
     if (ws_bytes < need) return hipErrorInvalidValue;
@@ -322,10 +330,9 @@ hipError_t launch_quad_worklist(const qgcm_desc *descs, uint32_t n, uint32_t max
     void *cub_tmp = p;
     size_t cub_bytes = need - (size_t)(p - static_cast<char *>(ws));
     hipError_t e;
-    const char *sv = getenv("QGCM_SMALL_WORKLIST");  // "0": small batches take the multi-launch path too (A/B)
-    if (n && n <= kSmallWl && !(sv && !strcmp(sv, "0"))) {
+    if (small_worklist(n)) {
         hipLaunchKernelGGL(qwl_small_kernel, dim3(1), dim3(kSmallThreads), 0, s, descs, n, max_keys, key_valid, seal,
-                           items, worklist, tile_keys, runs, run_next, short_tiles, counter);
+                           items, worklist, tile_keys, runs, run_next, short_tiles, counter, status);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         out->worklist = worklist;
         out->tile_keys = tile_keys;
