@@ -62,7 +62,7 @@ def fuzz_ctxs(torch, fuzz_keys):
         c.close()
 
 
-SIZES = (1, 17, 700, 3000, 9000, 24000, 16000, 5000)
+SIZES = (1, 17, 700, 3000, 9000, 24000, 16000, 5000, 768, 4096)  # 768: the smallest batch a key can fill a run in; 4096: the largest one-workgroup worklist
 
 
 def draw_case(case: int):
@@ -115,7 +115,8 @@ def test_descriptor_fuzz_vs_oracle(torch, fuzz_ctxs, fuzz_keys, variant, seed, s
                            np.ascontiguousarray(kidx[vi]), np.ascontiguousarray(nonces.reshape(n, 12)[vi]).reshape(-1),
                            aad_len, 8)
     arena = torch.from_numpy(plain.copy()).cuda()
-    status = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    # statuses start as junk: the call itself must clear those of packets it leaves out
+    status = torch.full((n,), 0x5A, dtype=torch.uint8, device="cuda")
     batch.seal_batch(ctx, arena, batch.make_descs(offs, lens, kidx, "cuda"), n, torch.from_numpy(nonces).cuda(),
                      aad_len=aad_len, status=status)
     st = status.cpu().numpy()
@@ -149,6 +150,7 @@ def test_descriptor_fuzz_vs_oracle(torch, fuzz_ctxs, fuzz_keys, variant, seed, s
         ost[oi] = sub
     assert not np.any(ost[ok & ~tam] == 0), "oracle rejected an untampered packet"
     arena.copy_(torch.from_numpy(tampered).cuda())
+    status.fill_(0x5A)
     batch.open_batch(ctx, arena, batch.make_descs(offs, olens, kidx, "cuda"), n, aad_len=aad_len, status=status)
     assert np.array_equal(status.cpu().numpy(), ost)
     assert np.array_equal(arena.cpu().numpy(), exp)
