@@ -204,7 +204,9 @@ int qgcm_group_last_zerocopy(const qgcm_group *g);
  * one DMA each way (64 MiB chunks, three staging slots, three streams), with no gather, scatter or
  * shader-driven PCIe traffic;
  * the gap bytes inside a run go back unchanged.  A batch laid out in qgcm_group_order's order, or any batch
- * of a one-member group, takes it.  QGCM_GROUP_DMA=0 disables it.  qgcm_group_last_path: the path member
+ * of a one-member group, takes it.  A chunk of at most 8192 packets whose records all start 16-B aligned
+ * runs one workgroup per packet instead of the sorted worklist (QGCM_DESC_ONE=0 disables that).
+ * QGCM_GROUP_DMA=0 disables the DMA runs.  qgcm_group_last_path: the path member
  * took in the last call (0 host copies, 1 zero-copy, 2 DMA runs) or QGCM_E_ARG. */
 int qgcm_group_last_path(const qgcm_group *g, int member);
 /* The order in which to lay out a keyed batch so that each member's packets are contiguous (a stable

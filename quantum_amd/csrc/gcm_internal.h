@@ -149,6 +149,10 @@ bool random_nonce(uint8_t out[12]);   // getrandom, buffered per thread, fork-sa
 long resident_call(Resident *r, bool seal, uint32_t key, uint8_t *data, long len, const uint8_t *aad,
                    uint32_t aad_len, const uint8_t *nonce);
 constexpr uint32_t kOneUniformMax = 2048;    // measured cross-over with the quad kernel: 2048-4096 packets
+// keyed batches of up to this many packets run one workgroup per packet when their records allow it:
+// against the worklist + per-wave kernel it wins up to 8192 (1395 vs 1442 us a seal+open pair at 8192,
+// 754 vs 921 at 4096: profiles/r4_s46_s49); the uniform kernel's cross-over is lower
+constexpr uint32_t kDescOneMax = 8192;
 constexpr uint32_t kLaunchChunk = 1u << 19;  // packets per quad-kernel launch of a uniform batch
 constexpr uint32_t kDescChunk = 0;           // packets per sorted chunk of a descriptor batch (0 = all)
 bool ctx_one_kernel(const qgcm_ctx *ctx);
@@ -156,6 +160,16 @@ bool ctx_one_kernel(const qgcm_ctx *ctx);
 // (group.cpp's DMA runs use them, as qgcm_seal_host does)
 hipStream_t ctx_pipe(qgcm_ctx *ctx, int k);
 std::mutex &ctx_io_mu(qgcm_ctx *ctx);
+// Small keyed batches whose records the caller has checked (group.cpp's DMA staging): one workgroup
+// per descriptor (gcm_one_kernel), no worklist.  descs_one_max: the largest batch that takes it (0:
+// off; kDescOneMax, QGCM_DESC_ONE_MAX at qgcm_create; QGCM_VARIANT and QGCM_ONE_KERNEL turn it off as
+// for uniform batches, and so does QGCM_DESC_ONE=0, read per call).  run_descs_one needs every record 16-B aligned in
+// device memory, no other record inside its 16-B-rounded area (4 + len (+ 28 on seal), rounded up),
+// and that area at most kOneCap - 16 bytes; keys, short opens and statuses behave as in the batch
+// kernels.
+uint32_t descs_one_max(const qgcm_ctx *ctx);
+int run_descs_one(qgcm_ctx *ctx, bool seal, uint8_t *d_arena, const qgcm_desc *d_descs, uint32_t n,
+                  const uint8_t *d_nonces, uint32_t aad_len, uint8_t *d_status, hipStream_t s);
 hipError_t launch_stream_copy(void *dst, const void *src, uint64_t bytes, int num_cus, hipStream_t s);
 // one record move of the group dispatcher's zero-copy path: src/dst device-accessible addresses
 // (pinned host or device), 4-B aligned; status_idx: the record's status byte (scatter only)

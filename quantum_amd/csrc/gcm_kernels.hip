@@ -1722,12 +1722,20 @@ __device__ uint32_t one_packet(const Batch &b, const uint32_t *__restrict__ rk_t
 // (open), b.uniform_key (a per-packet call is a batch of one).  Slots are 16-B aligned and
 // (4 + len (+ 28 for seal) + 15) & ~15 bytes long, at most kOneCap - 16; seal nonces come from
 // b.nonces (12 B per packet) when it is set, else from the slot.  b.status[packet] = verdict.
+// With b.descs set (small keyed batches, run_descs_one), packet i is descs[i] instead: its record
+// at a 16-B-aligned offset, no other record inside its 16-B-rounded staging area.
 template <bool kSeal>
 __global__ void __launch_bounds__(kOneThreads) gcm_one_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
     const uint32_t tid = threadIdx.x;
     const uint32_t pkt = blockIdx.x;
-    const uint64_t off = (uint64_t)pkt * b.stride;
-    const uint32_t Lin = b.uniform_len, key = b.uniform_key;
+    uint64_t off = (uint64_t)pkt * b.stride;
+    uint32_t Lin = b.uniform_len, key = b.uniform_key;
+    if (b.descs) {
+        const qgcm_desc d = b.descs[pkt];
+        off = d.offset;
+        Lin = d.len;
+        key = d.key_idx;
+    }
     const uint32_t n16 = (uint32_t)((4ull + Lin + (kSeal ? QGCM_OVERHEAD : 0) + 15) >> 4);
     // as the batch kernels: a key index out of range or an open shorter than 28 B fails the packet
     // (slot untouched); so does a slot past the LDS staging area or misaligned (the host never sends one)

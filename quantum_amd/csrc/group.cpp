@@ -641,6 +641,7 @@ int run_member_dma(Member &mb, bool seal, uint8_t *h_arena, const qgcm_desc *des
     // one chunk (a worker-sized batch) has nothing to overlap: one stream, no events, one synchronize
     std::lock_guard<std::mutex> io(qgcm::ctx_io_mu(mb.ctx));
     const bool one = nc == 1;
+    const uint32_t one_max = qgcm::descs_one_max(mb.ctx);
     hipStream_t s_in = qgcm::ctx_pipe(mb.ctx, 0);
     hipStream_t s_k = one ? s_in : qgcm::ctx_pipe(mb.ctx, 1), s_out = one ? s_in : qgcm::ctx_pipe(mb.ctx, 2);
     // QGCM_GROUP_DMA_TIMELINE=1 (diagnostics): timing events after each chunk's copy-in, kernels and
@@ -672,10 +673,15 @@ int run_member_dma(Member &mb, bool seal, uint8_t *h_arena, const qgcm_desc *des
         const uint64_t dside = pl.max_bytes;  // descs / nonces behind the records
         const size_t cn = ch.j1 - ch.j0;
         qgcm_desc *hd = reinterpret_cast<qgcm_desc *>(hs);
+        // a worker-sized chunk whose records all sit at 16-B-aligned staging offsets runs one workgroup
+        // per packet (no worklist sort, every CU busy); staging keeps the host layout, so a record's
+        // 16-B-rounded area holds no other record, and the chunk's staging bytes are 256-B rounded
+        bool one_ok = cn <= one_max;
         for (size_t j = ch.j0; j < ch.j1; ++j) {
             const qgcm_desc &d = descs[idx[j]];
             hd[j - ch.j0] = qgcm_desc{pl.at[j], d.len, d.key_idx};
             if (non) memcpy(hs + off_non + 12 * (j - ch.j0), h_nonces + 12ull * idx[j], 12);
+            one_ok = one_ok && !(pl.at[j] & 15) && ((rec_in(seal, d.len) + 15) & ~15ull) <= qgcm::kOneCap - 16;
         }
         for (size_t p = ch.p0; p < ch.p1 && rc == QGCM_OK; ++p) {
             const Piece &pc = pl.pieces[p];
@@ -690,9 +696,13 @@ int run_member_dma(Member &mb, bool seal, uint8_t *h_arena, const qgcm_desc *des
         if (rc != QGCM_OK) break;
         if (!tl.empty()) hipEventRecord(tl[3 * c], s_in);
         const qgcm_desc *dd = reinterpret_cast<const qgcm_desc *>(ds + dside);
-        rc = seal ? qgcm_seal_batch(mb.ctx, ds, dd, (uint32_t)cn, non ? ds + dside + off_non : nullptr, aad_len,
-                                    z.d_stat + ch.j0, s_k)
-                  : qgcm_open_batch(mb.ctx, ds, dd, (uint32_t)cn, aad_len, z.d_stat + ch.j0, s_k);
+        if (one_ok)
+            rc = qgcm::run_descs_one(mb.ctx, seal, ds, dd, (uint32_t)cn, non ? ds + dside + off_non : nullptr, aad_len,
+                                     z.d_stat + ch.j0, s_k);
+        else
+            rc = seal ? qgcm_seal_batch(mb.ctx, ds, dd, (uint32_t)cn, non ? ds + dside + off_non : nullptr, aad_len,
+                                        z.d_stat + ch.j0, s_k)
+                      : qgcm_open_batch(mb.ctx, ds, dd, (uint32_t)cn, aad_len, z.d_stat + ch.j0, s_k);
         if (rc != QGCM_OK) break;
         if (!tl.empty()) hipEventRecord(tl[3 * c + 1], s_k);
         if (!one && (hipEventRecord(z.ev_k[e], s_k) != hipSuccess || hipStreamWaitEvent(s_out, z.ev_k[e], 0) != hipSuccess))

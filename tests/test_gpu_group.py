@@ -22,6 +22,7 @@ from oracle import oracle as O
 pytestmark = pytest.mark.gpu
 
 AAD = bytes([10, 99, 0, 1])
+DESC_ONE_MAX = 8192  # gcm_internal.h kDescOneMax
 
 
 @pytest.fixture(scope="module")
@@ -279,6 +280,98 @@ def test_group_unaligned_records_take_the_copy_path(torch):
             assert grp.open_host(aptr, shard.host_descs(offs, lens + 28, kidx), n, 4, status.ctypes.data) == 0
             pay = np.concatenate([np.arange(int(o), int(o) + 4 + int(L)) for o, L in zip(offs, lens)])
             assert np.array_equal(arena[pay], plain[pay])
+            del nonces
+            free_n()
+        finally:
+            free()
+    finally:
+        grp.close()
+
+
+@pytest.mark.parametrize("n,one,align", [(1, "1", 16), (64, "1", 16), (700, "1", 16), (8192, "1", 16),
+                                         (8193, "1", 16), (700, "0", 16), (64, "1", 4)])
+def test_group_small_batches_one_workgroup_per_packet(torch, n, one, align, monkeypatch):
+    """A one-member batch of up to 8192 packets (kDescOneMax) whose records all start 16-B aligned runs one workgroup
+    per packet (gcm_one_kernel reading descriptors) instead of the worklist + per-wave kernel; larger
+    batches, 4-B-aligned records or QGCM_DESC_ONE=0 take the latter.  Records packed at `align` with
+    random bytes in the gaps; seal against the oracle over the whole arena (gaps untouched), statuses
+    start as junk, a key no member holds and opens shorter than 28 B fail with the slot untouched,
+    tampered packets are zeroed."""
+    from quantum_amd import shard
+
+    monkeypatch.setenv("QGCM_DESC_ONE", one)
+    grp = shard.Group([0], max_keys=256)
+    try:
+        rng = np.random.default_rng(0x6A10 + n + align)
+        nkeys = 8
+        keys = rng.integers(0, 256, 32 * nkeys, dtype=np.uint8).tobytes()
+        grp.set_keys(0, keys)
+        kidx = rng.integers(0, nkeys, n).astype(np.uint32)
+        if n > 1:
+            kidx[n - max(1, n // 40):] = 200  # no member holds key 200 (at the end: the others stay one run)
+        lens = rng.choice([0, 1, 15, 16, 17, 100, 1350, 1433, 4081, 9000], n).astype(np.uint32)
+        mix = rng.random(n) < 0.5
+        lens[mix] = rng.integers(0, 1500, int(mix.sum()))
+        rec = 4 + lens.astype(np.uint64) + 28
+        step = (rec + align - 1) // align * align + align * rng.integers(0, 2, n).astype(np.uint64)
+        offs = np.concatenate([[0], np.cumsum(step)[:-1]]).astype(np.uint64)
+        size = int(offs[-1] + step[-1])
+        arena, aptr, free = host_buffer(size, True)
+        ctx = grp.member(0)
+        try:
+            arena[:] = rng.integers(0, 256, size, dtype=np.uint8)
+            arena[offs.astype(np.int64)[:, None] + np.arange(4)] = np.frombuffer(AAD, np.uint8)
+            nonces, nptr, free_n = host_buffer(12 * n, True)
+            nonces[:] = rng.integers(0, 256, 12 * n, dtype=np.uint8)
+            plain, ref = arena.copy(), arena.copy()
+            ok = kidx < nkeys
+            vi = np.flatnonzero(ok)
+            if len(vi):
+                O.aesgo_seal_descs(keys, ref, np.ascontiguousarray(offs[vi]), np.ascontiguousarray(lens[vi]),
+                                   np.ascontiguousarray(kidx[vi]),
+                                   np.ascontiguousarray(nonces.reshape(n, 12)[vi]).reshape(-1), 4, 8)
+            c0 = ctx.launch_counts()
+            status = np.full(n, 7, np.uint8)
+            bad = grp.seal_host(aptr, shard.host_descs(offs, lens, kidx), n, nptr, 4, status.ctypes.data)
+            c1 = ctx.launch_counts()
+            path = grp.last_path(0)  # one run under kMinRun (64 KiB) goes zero-copy instead
+            assert path == ("dma" if int(offs[-max(1, n // 40)]) >= 64 << 10 else "zerocopy")
+            want_one = one == "1" and n <= DESC_ONE_MAX and align == 16 and path == "dma"
+            assert c1["one"] - c0["one"] == (1 if want_one else 0), (c0, c1)
+            assert bad == int((~ok).sum()) and np.array_equal(status, ok.astype(np.uint8))
+            assert np.array_equal(arena, ref)
+
+            tam = np.zeros(n, bool)
+            tam[rng.choice(vi, size=max(1, len(vi) // 20), replace=False)] = len(vi) > 1
+            for i in np.flatnonzero(tam):
+                arena[int(offs[i]) + 4 + int(rng.integers(0, int(lens[i]) + 28))] ^= 0x10
+            olens = lens + 28
+            short = (rng.random(n) < 0.02) & ~tam
+            olens[short] = rng.integers(0, 28, int(short.sum()))
+            before = arena.copy()
+            exp = before.copy()
+            good = ok & ~short
+            ost = np.zeros(n, np.uint8)
+            gi = np.flatnonzero(good)
+            if len(gi):
+                sub = np.zeros(len(gi), np.uint8)
+                O.aesgo_open_descs(keys, exp, np.ascontiguousarray(offs[gi]), np.ascontiguousarray(olens[gi]),
+                                   np.ascontiguousarray(kidx[gi]), sub, 4, 8)
+                ost[gi] = sub
+            assert np.array_equal(ost[good], (~tam[good]).astype(np.uint8))
+            status[:] = 7
+            bad = grp.open_host(aptr, shard.host_descs(offs, olens, kidx), n, 4, status.ctypes.data)
+            # shortened opens are rejected before the member (its batch is smaller) and can split the run
+            # (gaps past kRunGap), so the open's path is its own
+            m = int((olens >= 28).sum())
+            want_one = one == "1" and m <= DESC_ONE_MAX and align == 16 and grp.last_path(0) == "dma"
+            assert ctx.launch_counts()["one"] - c1["one"] == (1 if want_one else 0)
+            assert bad == int((ost == 0).sum()) and np.array_equal(status, ost)
+            assert np.array_equal(arena, exp)
+            pay = [i for i in gi if not tam[i]]
+            for i in pay[:: max(1, len(pay) // 200)]:
+                o, L = int(offs[i]), int(lens[i])
+                assert np.array_equal(arena[o:o + 4 + L], plain[o:o + 4 + L]), i
             del nonces
             free_n()
         finally:

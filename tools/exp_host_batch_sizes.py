@@ -3,7 +3,7 @@ Payload.Raw slots (1350 B, 1472-B stride), and the same through a one-member gro
 (qgcm_group_seal_host / open_host), for n from one recvmmsg batch (64) up to 2^18: median microseconds
 per seal+open pair and the payload rate, so a batched worker can pick its batch size.
 
-    python3 tools/exp_host_batch_sizes.py [reps]
+    python3 tools/exp_host_batch_sizes.py [reps] [sizes, comma-separated]
 """
 import ctypes as C
 import json
@@ -33,7 +33,8 @@ def main() -> None:
     host = np.frombuffer((C.c_uint8 * (nmax * stride)).from_address(a_ptr), np.uint8)
     host[:] = np.random.default_rng(1).integers(0, 256, host.size, dtype=np.uint8)
     Lb.qgcm_random_nonces(n_ptr, nmax)
-    for n in (64, 256, 1024, 4096, 16384, 65536, nmax):
+    sizes = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [64, 256, 1024, 4096, 16384, 65536, nmax]
+    for n in sizes:
         d_seal = shard.host_descs(np.arange(n, dtype=np.uint64) * stride, np.full(n, L, np.uint32),
                                   np.zeros(n, np.uint32))
         d_open = shard.host_descs(np.arange(n, dtype=np.uint64) * stride, np.full(n, L + 28, np.uint32),

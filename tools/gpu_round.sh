@@ -191,6 +191,9 @@ for s in $STEPS; do
     hostsizes)  # worker-sized host batches: seal+open pair latency and rate vs batch size (qgcm_seal_host and a one-member group)
       timeout -k 10 400 python3 tools/exp_host_batch_sizes.py 30 > $OUT/host_batch_sizes.jsonl 2> $OUT/host_batch_sizes.err
       check hostsizes $? ;;
+    smalltrace)  # kernel + copy timeline of 64-packet host and group pairs (where a small call's time goes)
+      timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $OUT/trace_small -o t -- python3 tools/exp_host_batch_sizes.py 40 64 > $OUT/trace_small.log 2>&1
+      check smalltrace $? ;;
     smallwl)  # small keyed batches: worklist in one workgroup vs the multi-launch path, alternating
       timeout -k 10 300 python3 tools/exp_small_worklist.py 30 > $OUT/small_worklist.jsonl 2> $OUT/small_worklist.err
       check smallwl $? ;;
