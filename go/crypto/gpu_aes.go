@@ -230,7 +230,9 @@ func (gg *GPUGroup) Close() {
 // A worker that has read a batch of packets (recvmmsg / TUN reads) into one pinned Payload.Raw arena
 // seals or opens the whole batch with one call instead of one Encrypt / Decrypt per packet
 // (worker/outgoing.go:55-93, worker/incoming.go:54-92 loop over packets).  Laid out in Order's order,
-// each GPU's packets are adjacent and move by DMA (qgcm_group_last_path 2).
+// each GPU's packets are adjacent and move by DMA (qgcm_group_last_path 2); a worker-sized batch (up to
+// 32768 packets in one 64-MiB chunk) whose slots start 16-B aligned, e.g. the 1472-B MaxPacketLength
+// stride, is sealed in place in the arena instead (qgcm_group_last_path 3).
 
 // KeyIndex is the key slot of this peer: the Key field of its packets' Descs.
 func (a *GPUAES) KeyIndex() uint32 { return a.idx }

@@ -153,6 +153,10 @@ constexpr uint32_t kOneUniformMax = 2048;    // measured cross-over with the qua
 // against the worklist + per-wave kernel it wins up to 8192 (1395 vs 1442 us a seal+open pair at 8192,
 // 754 vs 921 at 4096: profiles/r4_s46_s49); the uniform kernel's cross-over is lower
 constexpr uint32_t kDescOneMax = 8192;
+// a batch sealed in place in pinned host memory (group.cpp run_member_direct) takes that kernel up to
+// this many packets: 1.57-1.65 ms a pair at 16384 against 2.38 by DMA runs, 3.11 against 4.28 at 32768
+// (profiles/r4_s52_s53); 65536 packets are two DMA chunks, where the DMA pipeline wins
+constexpr uint32_t kDirectMax = 32768;
 constexpr uint32_t kLaunchChunk = 1u << 19;  // packets per quad-kernel launch of a uniform batch
 constexpr uint32_t kDescChunk = 0;           // packets per sorted chunk of a descriptor batch (0 = all)
 bool ctx_one_kernel(const qgcm_ctx *ctx);
@@ -168,6 +172,7 @@ std::mutex &ctx_io_mu(qgcm_ctx *ctx);
 // and that area at most kOneCap - 16 bytes; keys, short opens and statuses behave as in the batch
 // kernels.
 uint32_t descs_one_max(const qgcm_ctx *ctx);
+uint32_t direct_max(const qgcm_ctx *ctx);  // kDirectMax (QGCM_DIRECT_MAX at qgcm_create), 0 when the above is off
 int run_descs_one(qgcm_ctx *ctx, bool seal, uint8_t *d_arena, const qgcm_desc *d_descs, uint32_t n,
                   const uint8_t *d_nonces, uint32_t aad_len, uint8_t *d_status, hipStream_t s);
 hipError_t launch_stream_copy(void *dst, const void *src, uint64_t bytes, int num_cus, hipStream_t s);

@@ -183,7 +183,7 @@ struct Member {
     Stage st[kSlots];
     ZC zc;
     DmaState dma;
-    int last_path = 0;  // 0 copy, 1 zero-copy, 2 DMA runs (qgcm_group_last_path)
+    int last_path = 0;  // 0 copy, 1 zero-copy, 2 DMA runs, 3 direct (qgcm_group_last_path)
     cpu_set_t cpus;  // the GPU's local CPUs allowed to this process (empty: the thread is not pinned)
     int ncpus = 0;
     std::unique_ptr<CopyPool> pool;  // gather/scatter threads (created with the member)
@@ -623,8 +623,67 @@ int dma_ready(DmaState &z, uint64_t stage, uint64_t side, size_t slots, size_t m
     return QGCM_OK;
 }
 
+bool direct_on() {  // QGCM_GROUP_DIRECT=0: worker-sized batches copy by DMA as larger ones (A/B; read per call)
+    const char *v = getenv("QGCM_GROUP_DIRECT");
+    return !(v && !strcmp(v, "0"));
+}
+
+// Direct: a worker-sized batch (one DMA chunk, at most direct_max packets) whose records all start
+// 16-B aligned in a pinned arena that holds each record's 16-B-rounded area runs one workgroup per
+// packet on the records in place, over PCIe: no copies and one launch.  Descriptors, nonces and
+// statuses stay in pinned host memory as well.  Returns 1 when it ran (rc in *rc), 0 when the batch
+// does not qualify (nothing done).
+int run_member_direct(Member &mb, bool seal, uint8_t *h_arena, const qgcm_desc *descs, const uint32_t *idx,
+                      const DmaPlan &pl, const uint8_t *h_nonces, uint32_t aad_len, uint8_t *h_status, int *bad_out,
+                      int *rc) {
+    const size_t m = pl.at.size();
+    if (!direct_on() || pl.chunks.size() != 1 || !m || m > qgcm::direct_max(mb.ctx)) return 0;
+    uint64_t ext = 0;
+    for (size_t j = 0; j < m; ++j) {
+        const qgcm_desc &d = descs[idx[j]];
+        const uint64_t area = (rec_in(seal, d.len) + 15) & ~15ull;
+        if (((uintptr_t)(h_arena + d.offset) & 15) || area > qgcm::kOneCap - 16) return 0;
+        ext = std::max(ext, d.offset + area);
+    }
+    const uint64_t va = pinned_view(h_arena, ext);
+    if (!va || (va & 15)) return 0;
+    DmaState &z = mb.dma;
+    const bool non = seal && h_nonces;
+    const uint64_t off_non = (16ull * m + 255) & ~255ull;
+    const uint64_t side = off_non + (non ? (12ull * m + 255) & ~255ull : 0);  // [descs][nonces]
+    *rc = dma_ready(z, pl.max_bytes, side, 1, m);
+    if (*rc != QGCM_OK) return 1;
+    uint8_t *hs = z.h_side[0];
+    const uint64_t vs = pinned_view(hs, side), vst = pinned_view(z.h_stat, m);
+    if (!vs || !vst) return 0;
+    qgcm_desc *hd = reinterpret_cast<qgcm_desc *>(hs);
+    for (size_t j = 0; j < m; ++j) {
+        hd[j] = descs[idx[j]];
+        if (non) memcpy(hs + off_non + 12 * j, h_nonces + 12ull * idx[j], 12);
+    }
+    std::lock_guard<std::mutex> io(qgcm::ctx_io_mu(mb.ctx));
+    hipStream_t s = qgcm::ctx_pipe(mb.ctx, 0);
+    *rc = qgcm::run_descs_one(mb.ctx, seal, reinterpret_cast<uint8_t *>(va), reinterpret_cast<const qgcm_desc *>(vs),
+                              (uint32_t)m, non ? reinterpret_cast<const uint8_t *>(vs + off_non) : nullptr, aad_len,
+                              reinterpret_cast<uint8_t *>(vst), s);
+    if (hipStreamSynchronize(s) != hipSuccess && *rc == QGCM_OK) *rc = QGCM_E_HIP;
+    int bad = 0;
+    if (*rc == QGCM_OK)
+        for (size_t j = 0; j < m; ++j) {
+            bad += z.h_stat[j] != 1;
+            if (h_status) h_status[idx[j]] = z.h_stat[j];
+        }
+    *bad_out = bad;
+    mb.last_path = 3;
+    return 1;
+}
+
 int run_member_dma(Member &mb, bool seal, uint8_t *h_arena, const qgcm_desc *descs, const uint32_t *idx,
                    const DmaPlan &pl, const uint8_t *h_nonces, uint32_t aad_len, uint8_t *h_status, int *bad_out) {
+    {
+        int rc = QGCM_OK;
+        if (run_member_direct(mb, seal, h_arena, descs, idx, pl, h_nonces, aad_len, h_status, bad_out, &rc)) return rc;
+    }
     DmaState &z = mb.dma;
     const bool non = seal && h_nonces;
     const uint64_t pk = pl.max_pk;
@@ -781,6 +840,15 @@ int run_group(qgcm_group *g, bool seal, uint8_t *h_arena, const qgcm_desc *descs
     for (uint32_t i = 0; sorted && i < n; ++i) sorted = !(descs[i].offset & 3);
     sorted = sorted && !((uintptr_t)h_arena & 3);
     std::vector<DmaPlan> plan(G);
+    // worker-sized batches from a pinned arena may go direct (run_member_direct checks the rest), so a
+    // run under kMinRun still takes the DMA branch for them
+    const bool pinned = sorted && direct_on() && pinned_view(h_arena, 1) != 0;
+    auto dma_pays = [&](int k) {
+        const DmaPlan &pl = plan[k];
+        if (pl.piece_bytes >= kMinRun * pl.pieces.size()) return true;
+        if (!pinned || pl.chunks.size() != 1 || pl.at.size() > qgcm::direct_max(g->m[k].ctx)) return false;
+        return std::all_of(pl.at.begin(), pl.at.end(), [](uint64_t a) { return !(a & 15); });
+    };
     const char *cv = getenv("QGCM_GROUP_DMA_CHUNK_MB");  // A/B knob: staged bytes per DMA chunk
     const uint64_t dma_chunk = cv && *cv ? (uint64_t)std::max(1, std::min(4096, atoi(cv))) << 20 : kDmaChunk;
     std::vector<int> rc(G, QGCM_OK), bad(G, 0), used_zc(G, 1);
@@ -803,7 +871,7 @@ int run_group(qgcm_group *g, bool seal, uint8_t *h_arena, const qgcm_desc *descs
             if (sorted) {
                 const size_t m = part[k].size();
                 plan_dma(seal, descs, part[k].data(), m, dma_chunk, (uint32_t)((uintptr_t)h_arena & 255), plan[k]);
-                if (plan[k].piece_bytes >= kMinRun * plan[k].pieces.size()) {
+                if (dma_pays(k)) {
                     mb.last_path = 2;
                     used_zc[k] = 0;
                     rc[k] = run_member_dma(mb, seal, h_arena, descs, part[k].data(), plan[k], h_nonces, aad_len,
@@ -831,7 +899,7 @@ int run_group(qgcm_group *g, bool seal, uint8_t *h_arena, const qgcm_desc *descs
         // inline: the DMA plan decides first; a member that would take another path gets its thread
         const size_t m = part[k].size();
         plan_dma(seal, descs, part[k].data(), m, dma_chunk, (uint32_t)((uintptr_t)h_arena & 255), plan[k]);
-        if (plan[k].piece_bytes < kMinRun * plan[k].pieces.size()) {
+        if (!dma_pays(k)) {
             thr.emplace_back(work, true);
             continue;
         }

@@ -40,6 +40,7 @@ struct qgcm_ctx {
     bool one_kernel = true;                 // seal_one/open_one use the latency kernel (QGCM_ONE_KERNEL)
     bool variant_forced = false;            // QGCM_VARIANT given: uniform batches always run that variant
     uint32_t desc_one_max = kDescOneMax;        // small keyed batches (run_descs_one), QGCM_DESC_ONE_MAX
+    uint32_t direct_max = kDirectMax;           // ... sealed in place in pinned host memory, QGCM_DIRECT_MAX
     uint32_t one_uniform_max = kOneUniformMax;  // uniform batches up to this many packets take the
                                                 // latency kernel (QGCM_ONE_UNIFORM_MAX, tuning)
     uint32_t launch_chunk = kLaunchChunk;       // uniform batches launch at most this many packets per
@@ -260,9 +261,12 @@ uint32_t qgcm::descs_one_max(const qgcm_ctx *ctx) {
     return ctx->one_kernel && !ctx->variant_forced && !(v && !strcmp(v, "0")) ? ctx->desc_one_max : 0u;
 }
 
+uint32_t qgcm::direct_max(const qgcm_ctx *ctx) { return descs_one_max(ctx) ? ctx->direct_max : 0u; }
+
 int qgcm::run_descs_one(qgcm_ctx *ctx, bool seal, uint8_t *d_arena, const qgcm_desc *d_descs, uint32_t n,
                         const uint8_t *d_nonces, uint32_t aad_len, uint8_t *d_status, hipStream_t s) {
-    if (!ctx || !n || !d_arena || !d_descs || aad_len > 4 || n > descs_one_max(ctx) || ((uintptr_t)d_arena & 15))
+    if (!ctx || !n || !d_arena || !d_descs || aad_len > 4 || n > QGCM_MAX_BATCH || !descs_one_max(ctx) ||
+        ((uintptr_t)d_arena & 15))
         return QGCM_E_ARG;
     if (hipSetDevice(ctx->device) != hipSuccess) return QGCM_E_HIP;
     Batch b = base_batch(ctx);
@@ -547,6 +551,7 @@ qgcm_ctx *qgcm_create(int device, uint32_t max_keys, char *err, int errlen) {
     ctx->res_cfg = qgcm::resident_config_from_env();
     if (const char *v = getenv("QGCM_ONE_UNIFORM_MAX")) ctx->one_uniform_max = (uint32_t)std::max(0, atoi(v));
     if (const char *v = getenv("QGCM_DESC_ONE_MAX")) ctx->desc_one_max = (uint32_t)std::max(0, atoi(v));
+    if (const char *v = getenv("QGCM_DIRECT_MAX")) ctx->direct_max = (uint32_t)std::max(0, atoi(v));
     if (const char *v = getenv("QGCM_LAUNCH_CHUNK"))  // rounded down to whole 64-packet tiles
         ctx->launch_chunk = (uint32_t)std::max(0, atoi(v)) & ~63u;
     if (const char *v = getenv("QGCM_DESC_CHUNK")) ctx->desc_chunk = (uint32_t)std::max(0, atoi(v));

@@ -115,12 +115,13 @@ class Group:
 
     def last_path(self, m: int) -> str:
         """How member m moved its records in the last seal_host / open_host call: "copy" (host gather and
-        scatter through pinned staging), "zerocopy" (its GPU gathers over PCIe) or "dma" (whole runs of
-        adjacent records, one DMA each way)."""
+        scatter through pinned staging), "zerocopy" (its GPU gathers over PCIe), "dma" (whole runs of
+        adjacent records, one DMA each way) or "direct" (a worker-sized batch of 16-B-aligned records in a
+        pinned arena, sealed in place over PCIe by one workgroup per packet)."""
         from . import _lib
 
         code = _lib.check(_lib.lib().qgcm_group_last_path(self.handle, m), "qgcm_group_last_path")
-        return ("copy", "zerocopy", "dma")[code]
+        return ("copy", "zerocopy", "dma", "direct")[code]
 
     def order(self, key_idx) -> tuple[np.ndarray, np.ndarray]:
         """qgcm_group_order: the input indices member by member (stable) and each member's count -- the

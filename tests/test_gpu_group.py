@@ -23,6 +23,7 @@ pytestmark = pytest.mark.gpu
 
 AAD = bytes([10, 99, 0, 1])
 DESC_ONE_MAX = 8192  # gcm_internal.h kDescOneMax
+DIRECT_MAX = 32768  # gcm_internal.h kDirectMax
 
 
 @pytest.fixture(scope="module")
@@ -288,18 +289,24 @@ def test_group_unaligned_records_take_the_copy_path(torch):
         grp.close()
 
 
-@pytest.mark.parametrize("n,one,align", [(1, "1", 16), (64, "1", 16), (700, "1", 16), (8192, "1", 16),
-                                         (8193, "1", 16), (700, "0", 16), (64, "1", 4)])
-def test_group_small_batches_one_workgroup_per_packet(torch, n, one, align, monkeypatch):
+@pytest.mark.parametrize("n,one,align,direct", [(1, "1", 16, "1"), (64, "1", 16, "1"), (700, "1", 16, "1"),
+                                                (8192, "1", 16, "0"), (8193, "1", 16, "0"), (8193, "1", 16, "1"),
+                                                (32768, "1", 16, "1"), (32769, "1", 16, "1"), (700, "0", 16, "1"),
+                                                (64, "1", 4, "1"), (64, "1", 16, "0"), (700, "1", 16, "0"),
+                                                (700, "1", 16, "slot")])
+def test_group_small_batches_one_workgroup_per_packet(torch, n, one, align, direct, monkeypatch):
     """A one-member batch of up to 8192 packets (kDescOneMax) whose records all start 16-B aligned runs one workgroup
     per packet (gcm_one_kernel reading descriptors) instead of the worklist + per-wave kernel; larger
     batches, 4-B-aligned records or QGCM_DESC_ONE=0 take the latter.  Records packed at `align` with
     random bytes in the gaps; seal against the oracle over the whole arena (gaps untouched), statuses
     start as junk, a key no member holds and opens shorter than 28 B fail with the slot untouched,
-    tampered packets are zeroed."""
+    tampered packets are zeroed.  direct: QGCM_GROUP_DIRECT -- such a batch in a pinned arena is sealed in
+    place over PCIe ("1", path "direct"), or copied by DMA ("0"); "slot": direct with each nonce already in
+    its slot (h_nonces NULL)."""
     from quantum_amd import shard
 
     monkeypatch.setenv("QGCM_DESC_ONE", one)
+    monkeypatch.setenv("QGCM_GROUP_DIRECT", "0" if direct == "0" else "1")
     grp = shard.Group([0], max_keys=256)
     try:
         rng = np.random.default_rng(0x6A10 + n + align)
@@ -323,6 +330,10 @@ def test_group_small_batches_one_workgroup_per_packet(torch, n, one, align, monk
             arena[offs.astype(np.int64)[:, None] + np.arange(4)] = np.frombuffer(AAD, np.uint8)
             nonces, nptr, free_n = host_buffer(12 * n, True)
             nonces[:] = rng.integers(0, 256, 12 * n, dtype=np.uint8)
+            if direct == "slot":  # the nonce sits after the tag's place; the call gets no nonce array
+                at = (offs.astype(np.int64) + 4 + lens.astype(np.int64) + 16)[:, None] + np.arange(12)
+                arena[at] = nonces.reshape(n, 12)
+                nptr = None
             plain, ref = arena.copy(), arena.copy()
             ok = kidx < nkeys
             vi = np.flatnonzero(ok)
@@ -334,9 +345,13 @@ def test_group_small_batches_one_workgroup_per_packet(torch, n, one, align, monk
             status = np.full(n, 7, np.uint8)
             bad = grp.seal_host(aptr, shard.host_descs(offs, lens, kidx), n, nptr, 4, status.ctypes.data)
             c1 = ctx.launch_counts()
-            path = grp.last_path(0)  # one run under kMinRun (64 KiB) goes zero-copy instead
-            assert path == ("dma" if int(offs[-max(1, n // 40)]) >= 64 << 10 else "zerocopy")
-            want_one = one == "1" and n <= DESC_ONE_MAX and align == 16 and path == "dma"
+            path = grp.last_path(0)
+            if one == "1" and align == 16 and direct != "0" and n <= DIRECT_MAX:
+                assert path == "direct"
+                want_one = True
+            else:  # one run under kMinRun (64 KiB) goes zero-copy instead
+                assert path == ("dma" if int(offs[-max(1, n // 40)]) >= 64 << 10 else "zerocopy")
+                want_one = one == "1" and n <= DESC_ONE_MAX and align == 16 and path == "dma"
             assert c1["one"] - c0["one"] == (1 if want_one else 0), (c0, c1)
             assert bad == int((~ok).sum()) and np.array_equal(status, ok.astype(np.uint8))
             assert np.array_equal(arena, ref)
@@ -364,7 +379,11 @@ def test_group_small_batches_one_workgroup_per_packet(torch, n, one, align, monk
             # shortened opens are rejected before the member (its batch is smaller) and can split the run
             # (gaps past kRunGap), so the open's path is its own
             m = int((olens >= 28).sum())
-            want_one = one == "1" and m <= DESC_ONE_MAX and align == 16 and grp.last_path(0) == "dma"
+            if one == "1" and align == 16 and direct != "0" and m <= DIRECT_MAX:
+                assert grp.last_path(0) == "direct"
+                want_one = True
+            else:
+                want_one = one == "1" and m <= DESC_ONE_MAX and align == 16 and grp.last_path(0) == "dma"
             assert ctx.launch_counts()["one"] - c1["one"] == (1 if want_one else 0)
             assert bad == int((ost == 0).sum()) and np.array_equal(status, ost)
             assert np.array_equal(arena, exp)
