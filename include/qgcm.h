@@ -154,7 +154,9 @@ int qgcm_resident_stats(const qgcm_ctx *ctx, uint64_t *out, int n);
 /* ---- host batches (end-to-end incl. PCIe) ---- */
 /* Slots in host memory at i*stride; copies in, runs the device batch, copies back, synchronously.
  * Pipelined in 64 MiB chunks over 3 streams (H2D of chunk c+1 || kernel c || D2H of chunk c-1);
- * h_arena from qgcm_host_alloc (pinned) is DMA'd in place, pageable memory is staged by HIP.
+ * h_arena from qgcm_host_alloc (pinned) is DMA'd in place, pageable memory is staged by HIP.  A pinned
+ * batch of up to 32768 packets with 16-B-aligned slots (stride a multiple of 16) is sealed in place
+ * instead: one kernel on the arena's device view, no copies (QGCM_HOST_DIRECT=0 disables it).
  * Returns the number of packets that failed (0 = all ok) or a negative error.  status may be NULL.
  * Replaces the per-packet Apply loop of worker/outgoing.go:55-93 / worker/incoming.go:54-92 for a
  * batch of packets a worker has collected. */

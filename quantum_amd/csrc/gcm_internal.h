@@ -173,6 +173,8 @@ std::mutex &ctx_io_mu(qgcm_ctx *ctx);
 // kernels.
 uint32_t descs_one_max(const qgcm_ctx *ctx);
 uint32_t direct_max(const qgcm_ctx *ctx);  // kDirectMax (QGCM_DIRECT_MAX at qgcm_create), 0 when the above is off
+// Device-accessible address of pinned host memory [p, p + bytes) inside one allocation, or 0.
+uint64_t pinned_view(const void *p, uint64_t bytes);
 int run_descs_one(qgcm_ctx *ctx, bool seal, uint8_t *d_arena, const qgcm_desc *d_descs, uint32_t n,
                   const uint8_t *d_nonces, uint32_t aad_len, uint8_t *d_status, hipStream_t s);
 hipError_t launch_stream_copy(void *dst, const void *src, uint64_t bytes, int num_cus, hipStream_t s);

@@ -385,22 +385,7 @@ bool grow_pinned(T *&h, T *&d, size_t count) {
            hipMalloc(reinterpret_cast<void **>(&d), sizeof(T) * count) == hipSuccess;
 }
 
-// Device-accessible address of pinned host memory [p, p + bytes) inside one allocation, or 0.
-uint64_t pinned_view(const void *p, uint64_t bytes) {
-    hipPointerAttribute_t a;
-    if (hipPointerGetAttributes(&a, p) != hipSuccess || a.type != hipMemoryTypeHost || !a.devicePointer) {
-        (void)hipGetLastError();  // pageable memory reports an error: clear it
-        return 0;
-    }
-    hipDeviceptr_t base = nullptr;
-    size_t size = 0;
-    if (hipMemGetAddressRange(&base, &size, a.devicePointer) != hipSuccess || !base) {
-        (void)hipGetLastError();
-        return 0;
-    }
-    const uint64_t dv = reinterpret_cast<uint64_t>(a.devicePointer), b = reinterpret_cast<uint64_t>(base);
-    return dv >= b && dv + bytes <= b + size ? dv : 0;
-}
+using qgcm::pinned_view;
 
 // Zero-copy form of run_member: the member's GPU gathers its records from the pinned arena itself.
 // v_arena / v_nonces: the arena's and nonces' device views resolved on this member's device.

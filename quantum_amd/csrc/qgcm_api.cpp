@@ -261,6 +261,23 @@ uint32_t qgcm::descs_one_max(const qgcm_ctx *ctx) {
     return ctx->one_kernel && !ctx->variant_forced && !(v && !strcmp(v, "0")) ? ctx->desc_one_max : 0u;
 }
 
+// Device-accessible address of pinned host memory [p, p + bytes) inside one allocation, or 0.
+uint64_t qgcm::pinned_view(const void *p, uint64_t bytes) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess || a.type != hipMemoryTypeHost || !a.devicePointer) {
+        (void)hipGetLastError();  // pageable memory reports an error: clear it
+        return 0;
+    }
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    if (hipMemGetAddressRange(&base, &size, a.devicePointer) != hipSuccess || !base) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    const uint64_t dv = reinterpret_cast<uint64_t>(a.devicePointer), b = reinterpret_cast<uint64_t>(base);
+    return dv >= b && dv + bytes <= b + size ? dv : 0;
+}
+
 uint32_t qgcm::direct_max(const qgcm_ctx *ctx) { return descs_one_max(ctx) ? ctx->direct_max : 0u; }
 
 int qgcm::run_descs_one(qgcm_ctx *ctx, bool seal, uint8_t *d_arena, const qgcm_desc *d_descs, uint32_t n,
@@ -766,6 +783,8 @@ long qgcm_open_one(qgcm_ctx *ctx, uint32_t key_idx, uint8_t *data, long len, con
 // stream wait behind its copy-out: 30.5 GiB/s; per-stage streams with 4 rotating 32 MiB slots: 35.6).
 // Pinned caller memory (qgcm_host_alloc, hipHostMalloc/Register) is DMA'd in place; pageable memory
 // still works but HIP stages it, which serializes the copies.
+static bool non_ok(bool seal, const uint8_t *h_nonces) { return seal && h_nonces; }
+
 static int run_host(qgcm_ctx *ctx, bool seal, uint8_t *h_arena, uint64_t stride, uint32_t n, uint32_t len,
                     uint32_t key_idx, const uint8_t *h_nonces, uint32_t aad_len, uint8_t *h_status) {
     if (!ctx || (n && !h_arena) || aad_len > 4 || (stride & 3)) return QGCM_E_ARG;
@@ -776,6 +795,46 @@ static int run_host(qgcm_ctx *ctx, bool seal, uint8_t *h_arena, uint64_t stride,
     if (n == 0) return 0;
     std::lock_guard<std::mutex> g(ctx->io_mu);
     if (hipSetDevice(ctx->device) != hipSuccess) return QGCM_E_HIP;
+    if (n > ctx->hstat_cap) {
+        if (ctx->h_stat) hipHostFree(ctx->h_stat);
+        ctx->h_stat = nullptr;
+        ctx->hstat_cap = 0;
+        if (hipHostMalloc(&ctx->h_stat, n, hipHostMallocDefault) != hipSuccess) return QGCM_E_NOMEM;
+        ctx->hstat_cap = n;
+    }
+    {
+        // Direct: a worker-sized batch in a pinned arena with 16-B-aligned slots that hold the rounded
+        // staging area is sealed in place over PCIe, one workgroup per packet (gcm_one_kernel on the
+        // arena's device view), nonces and statuses in pinned memory too: one launch, no copies
+        // (QGCM_HOST_DIRECT=0: off, read per call)
+        const char *dv = getenv("QGCM_HOST_DIRECT");
+        const uint64_t area = (4ull + len + (seal ? QGCM_OVERHEAD : 0) + 15) & ~15ull;
+        uint64_t va = 0, vn = 0, vst = 0;
+        if (!(dv && !strcmp(dv, "0")) && n <= direct_max(ctx) && !ctx->variant_forced && !(stride & 15) &&
+            area <= stride && area <= kOneCap - 16 && (seal || len >= QGCM_OVERHEAD) &&
+            (va = pinned_view(h_arena, (uint64_t)n * stride)) && !(va & 15) &&
+            (!non_ok(seal, h_nonces) || (vn = pinned_view(h_nonces, 12ull * n))) && !(vn & 3) &&
+            (vst = pinned_view(ctx->h_stat, n))) {
+            Batch b = base_batch(ctx);
+            b.arena = reinterpret_cast<uint8_t *>(va);
+            b.nonces = reinterpret_cast<const uint8_t *>(vn);
+            b.status = reinterpret_cast<uint8_t *>(vst);
+            b.stride = stride;
+            b.uniform_len = len;
+            b.uniform_key = key_idx;
+            b.n = n;
+            b.n_items = (uint32_t)(((uint64_t)n + 63) & ~63ull);
+            b.aad_len = aad_len;
+            hipStream_t s = ctx->pipe[0];
+            if (launch_one(seal, b, s) != hipSuccess) return QGCM_E_HIP;
+            ctx->count(QGCM_KERNEL_ONE);
+            if (hipStreamSynchronize(s) != hipSuccess) return QGCM_E_HIP;
+            int bad = 0;
+            for (uint32_t i = 0; i < n; ++i) bad += ctx->h_stat[i] != 1;
+            if (h_status) memcpy(h_status, ctx->h_stat, n);
+            return bad;
+        }
+    }
     uint64_t cpk = (ctx->host_chunk / stride) & ~63ull;  // packets per chunk, whole 64-packet tiles
     if (cpk < 64) cpk = 64;
     if (cpk > n) cpk = n;
@@ -815,13 +874,6 @@ static int run_host(qgcm_ctx *ctx, bool seal, uint8_t *h_arena, uint64_t stride,
         ctx->side_cap = side;
     }
     uint8_t *d_non_all = ctx->d_side, *d_stat_all = ctx->d_side + non_bytes;
-    if (n > ctx->hstat_cap) {
-        if (ctx->h_stat) hipHostFree(ctx->h_stat);
-        ctx->h_stat = nullptr;
-        ctx->hstat_cap = 0;
-        if (hipHostMalloc(&ctx->h_stat, n, hipHostMallocDefault) != hipSuccess) return QGCM_E_NOMEM;
-        ctx->hstat_cap = n;
-    }
     // one copy-in stream: alternating two (two SDMA queues) measured 27.3 vs 38.0 GiB/s.  A batch of one
     // chunk (a worker's recvmmsg batch) has nothing to overlap: copy-in, kernel and copy-out go on one
     // stream, with no cross-stream events and one synchronize
