@@ -209,7 +209,8 @@ int qgcm_group_last_zerocopy(const qgcm_group *g);
  * of a one-member group, takes it.  A chunk of at most 8192 packets whose records all start 16-B aligned
  * runs one workgroup per packet instead of the sorted worklist (QGCM_DESC_ONE=0 disables that).  Direct:
  * when such a batch is a single chunk in a pinned arena that also holds each record's 16-B-rounded area,
- * that kernel seals the records in place over PCIe, with no copies (QGCM_GROUP_DIRECT=0 disables it).
+ * that kernel seals the records in place over PCIe, with no copies (QGCM_GROUP_DIRECT=0 disables it);
+ * so does each member's share of up to 32768 such records when members are interleaved in the arena.
  * QGCM_GROUP_DMA=0 disables the DMA runs.  qgcm_group_last_path: the path member
  * took in the last call (0 host copies, 1 zero-copy, 2 DMA runs, 3 direct) or QGCM_E_ARG. */
 int qgcm_group_last_path(const qgcm_group *g, int member);

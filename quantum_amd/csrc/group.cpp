@@ -613,16 +613,16 @@ bool direct_on() {  // QGCM_GROUP_DIRECT=0: worker-sized batches copy by DMA as 
     return !(v && !strcmp(v, "0"));
 }
 
-// Direct: a worker-sized batch (one DMA chunk, at most direct_max packets) whose records all start
-// 16-B aligned in a pinned arena that holds each record's 16-B-rounded area runs one workgroup per
-// packet on the records in place, over PCIe: no copies and one launch.  Descriptors, nonces and
-// statuses stay in pinned host memory as well.  Returns 1 when it ran (rc in *rc), 0 when the batch
-// does not qualify (nothing done).
+// Direct: a member's worker-sized batch (at most direct_max packets; by DMA runs: one chunk) whose
+// records all start 16-B aligned in a pinned arena that holds each record's 16-B-rounded area runs one
+// workgroup per packet on the records in place, over PCIe: no copies and one launch.  The member's
+// records need not be adjacent: no record shares another's rounded area, so members interleaved in one
+// arena each seal their own in place at once.  Descriptors, nonces and statuses stay in pinned host
+// memory as well.  Returns 1 when it ran (rc in *rc), 0 when the batch does not qualify (nothing done).
 int run_member_direct(Member &mb, bool seal, uint8_t *h_arena, const qgcm_desc *descs, const uint32_t *idx,
-                      const DmaPlan &pl, const uint8_t *h_nonces, uint32_t aad_len, uint8_t *h_status, int *bad_out,
+                      size_t m, const uint8_t *h_nonces, uint32_t aad_len, uint8_t *h_status, int *bad_out,
                       int *rc) {
-    const size_t m = pl.at.size();
-    if (!direct_on() || pl.chunks.size() != 1 || !m || m > qgcm::direct_max(mb.ctx)) return 0;
+    if (!direct_on() || !m || m > qgcm::direct_max(mb.ctx)) return 0;
     uint64_t ext = 0;
     for (size_t j = 0; j < m; ++j) {
         const qgcm_desc &d = descs[idx[j]];
@@ -636,7 +636,7 @@ int run_member_direct(Member &mb, bool seal, uint8_t *h_arena, const qgcm_desc *
     const bool non = seal && h_nonces;
     const uint64_t off_non = (16ull * m + 255) & ~255ull;
     const uint64_t side = off_non + (non ? (12ull * m + 255) & ~255ull : 0);  // [descs][nonces]
-    *rc = dma_ready(z, pl.max_bytes, side, 1, m);
+    *rc = dma_ready(z, 0, side, 1, m);
     if (*rc != QGCM_OK) return 1;
     uint8_t *hs = z.h_side[0];
     const uint64_t vs = pinned_view(hs, side), vst = pinned_view(z.h_stat, m);
@@ -667,7 +667,9 @@ int run_member_dma(Member &mb, bool seal, uint8_t *h_arena, const qgcm_desc *des
                    const DmaPlan &pl, const uint8_t *h_nonces, uint32_t aad_len, uint8_t *h_status, int *bad_out) {
     {
         int rc = QGCM_OK;
-        if (run_member_direct(mb, seal, h_arena, descs, idx, pl, h_nonces, aad_len, h_status, bad_out, &rc)) return rc;
+        if (pl.chunks.size() == 1 &&
+            run_member_direct(mb, seal, h_arena, descs, idx, pl.at.size(), h_nonces, aad_len, h_status, bad_out, &rc))
+            return rc;
     }
     DmaState &z = mb.dma;
     const bool non = seal && h_nonces;
@@ -827,7 +829,8 @@ int run_group(qgcm_group *g, bool seal, uint8_t *h_arena, const qgcm_desc *descs
     std::vector<DmaPlan> plan(G);
     // worker-sized batches from a pinned arena may go direct (run_member_direct checks the rest), so a
     // run under kMinRun still takes the DMA branch for them
-    const bool pinned = sorted && direct_on() && pinned_view(h_arena, 1) != 0;
+    const bool pinned_arena = direct_on() && pinned_view(h_arena, 1) != 0;
+    const bool pinned = sorted && pinned_arena;
     auto dma_pays = [&](int k) {
         const DmaPlan &pl = plan[k];
         if (pl.piece_bytes >= kMinRun * pl.pieces.size()) return true;
@@ -861,6 +864,15 @@ int run_group(qgcm_group *g, bool seal, uint8_t *h_arena, const qgcm_desc *descs
                     used_zc[k] = 0;
                     rc[k] = run_member_dma(mb, seal, h_arena, descs, part[k].data(), plan[k], h_nonces, aad_len,
                                            h_status, &bad[k]);
+                    return;
+                }
+            }
+            {  // a worker-sized share of an interleaved batch: in place, as by DMA runs above
+                int drc = QGCM_OK;
+                if (pinned_arena && run_member_direct(mb, seal, h_arena, descs, part[k].data(), part[k].size(),
+                                                      h_nonces, aad_len, h_status, &bad[k], &drc)) {
+                    used_zc[k] = 0;
+                    rc[k] = drc;
                     return;
                 }
             }

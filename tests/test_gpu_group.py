@@ -399,6 +399,64 @@ def test_group_small_batches_one_workgroup_per_packet(torch, n, one, align, dire
         grp.close()
 
 
+@pytest.mark.parametrize("G,direct,pinned_nonces", [(2, "1", True), (3, "1", False), (2, "0", True)])
+def test_group_interleaved_members_seal_in_place(torch, G, direct, pinned_nonces, monkeypatch):
+    """Several members with their packets interleaved in one pinned arena (no DMA runs): each member's
+    worker-sized share of 16-B-aligned records is sealed in place by its own GPU ("direct"), the members
+    at once; QGCM_GROUP_DIRECT=0: zero-copy gather/scatter.  Against the oracle over the whole arena,
+    nonces from pinned or pageable memory, then tampered packets fail and the rest open back."""
+    from quantum_amd import shard
+
+    monkeypatch.setenv("QGCM_GROUP_DIRECT", direct)
+    grp = shard.Group([0] * G, max_keys=64)
+    try:
+        rng = np.random.default_rng(0x6A20 + G)
+        nkeys = 24
+        keys = rng.integers(0, 256, 32 * nkeys, dtype=np.uint8).tobytes()
+        grp.set_keys(0, keys)
+        n = 900
+        kidx = rng.integers(0, nkeys, n).astype(np.uint32)
+        assert len(set(shard.key_shard(kidx, G).tolist())) == G
+        lens = rng.integers(0, 1500, n).astype(np.uint32)
+        step = (4 + lens.astype(np.uint64) + 28 + 15) // 16 * 16
+        offs = np.concatenate([[0], np.cumsum(step)[:-1]]).astype(np.uint64)
+        size = int(offs[-1] + step[-1])
+        arena, aptr, free = host_buffer(size, True)
+        nonces, nptr, free_n = host_buffer(12 * n, pinned_nonces)
+        try:
+            arena[:] = rng.integers(0, 256, size, dtype=np.uint8)
+            arena[offs.astype(np.int64)[:, None] + np.arange(4)] = np.frombuffer(AAD, np.uint8)
+            nonces[:] = rng.integers(0, 256, 12 * n, dtype=np.uint8)
+            plain, ref = arena.copy(), arena.copy()
+            O.aesgo_seal_descs(keys, ref, offs, lens, kidx, np.ascontiguousarray(nonces), 4, 8)
+            status = np.full(n, 7, np.uint8)
+            assert grp.seal_host(aptr, shard.host_descs(offs, lens, kidx), n, nptr, 4, status.ctypes.data) == 0
+            want = "direct" if direct == "1" else "zerocopy"
+            assert [grp.last_path(m) for m in range(G)] == [want] * G
+            assert bool((status == 1).all()) and np.array_equal(arena, ref)
+            tam = rng.choice(n, size=30, replace=False)
+            for i in tam:
+                arena[int(offs[i]) + 4 + int(rng.integers(0, int(lens[i]) + 28))] ^= 0x08
+            status[:] = 7
+            assert grp.open_host(aptr, shard.host_descs(offs, lens + 28, kidx), n, 4, status.ctypes.data) == len(tam)
+            assert [grp.last_path(m) for m in range(G)] == [want] * G
+            ok = np.ones(n, bool)
+            ok[tam] = False
+            assert np.array_equal(status, ok.astype(np.uint8))
+            for i in range(n):
+                o, L = int(offs[i]), int(lens[i])
+                if ok[i]:
+                    assert np.array_equal(arena[o:o + 4 + L], plain[o:o + 4 + L]), i
+                else:
+                    assert not arena[o + 4:o + 4 + L].any(), i
+        finally:
+            del nonces
+            free_n()
+            free()
+    finally:
+        grp.close()
+
+
 def test_group_zerocopy_records_at_the_allocation_end(torch):
     """Zero-copy path: records whose last byte is the last bytes of a one-page pinned allocation, with
     lengths that are not multiples of 4 or 16 (the gather reads whole dwords up to the next 4-B

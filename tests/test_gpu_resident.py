@@ -139,13 +139,14 @@ def test_instance_ends_and_relaunches(torch):
         l0 = ctx.resident_stats()["launches"]
         assert roundtrip(aes, key, 1350, rng) is None
         assert ctx.resident_stats()["launches"] == l0 + 1
-        # back-to-back traffic from 8 threads for ~60 ms: the 3-ms lifetime cap ends ~20 instances
+        # back-to-back traffic from 8 threads until the 3-ms lifetime cap has ended 5 instances (~15 ms of
+        # traffic; at most 2 s, so a slow box cannot turn a timing margin into a failure)
         errors = []
-        stop = time.time() + 0.06
+        done = threading.Event()
 
         def work(t):
             r = random.Random(100 + t)
-            while time.time() < stop:
+            while not done.is_set():
                 e = roundtrip(aes, key, r.randrange(0, 3000), r)
                 if e:
                     errors.append(e)
@@ -154,6 +155,10 @@ def test_instance_ends_and_relaunches(torch):
         ths = [threading.Thread(target=work, args=(t,)) for t in range(8)]
         for th in ths:
             th.start()
+        deadline = time.time() + 2.0
+        while time.time() < deadline and ctx.resident_stats()["launches"] < l0 + 5 and not errors:
+            time.sleep(0.01)
+        done.set()
         for th in ths:
             th.join()
         assert not errors, errors[:3]
