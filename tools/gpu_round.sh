@@ -4,7 +4,8 @@
 # the script stops at the first step that faults, aborts or times out (a plain test failure goes on).
 # Usage: bash tools/gpu_round.sh <tag> [steps...]
 #   steps: stests policy snapdev rtests tests smoke bench ab prof pp prof3 exp_res res_trace ahead barreq align
-#          r4tests abrealign snapab profsnap (default: tests smoke bench ab prof)
+#          r4tests abrealign snapab profsnap gtests ftests hostsizes smallwl smalltrace copytrace
+#          (default: tests smoke bench ab prof)
 set -u
 TAG=$1; shift
 STEPS=${*:-"tests smoke bench ab prof"}
