@@ -783,8 +783,6 @@ long qgcm_open_one(qgcm_ctx *ctx, uint32_t key_idx, uint8_t *data, long len, con
 // stream wait behind its copy-out: 30.5 GiB/s; per-stage streams with 4 rotating 32 MiB slots: 35.6).
 // Pinned caller memory (qgcm_host_alloc, hipHostMalloc/Register) is DMA'd in place; pageable memory
 // still works but HIP stages it, which serializes the copies.
-static bool non_ok(bool seal, const uint8_t *h_nonces) { return seal && h_nonces; }
-
 static int run_host(qgcm_ctx *ctx, bool seal, uint8_t *h_arena, uint64_t stride, uint32_t n, uint32_t len,
                     uint32_t key_idx, const uint8_t *h_nonces, uint32_t aad_len, uint8_t *h_status) {
     if (!ctx || (n && !h_arena) || aad_len > 4 || (stride & 3)) return QGCM_E_ARG;
@@ -813,7 +811,7 @@ static int run_host(qgcm_ctx *ctx, bool seal, uint8_t *h_arena, uint64_t stride,
         if (!(dv && !strcmp(dv, "0")) && n <= direct_max(ctx) && !ctx->variant_forced && !(stride & 15) &&
             area <= stride && area <= kOneCap - 16 && (seal || len >= QGCM_OVERHEAD) &&
             (va = pinned_view(h_arena, (uint64_t)n * stride)) && !(va & 15) &&
-            (!non_ok(seal, h_nonces) || (vn = pinned_view(h_nonces, 12ull * n))) && !(vn & 3) &&
+            (!(seal && h_nonces) || (vn = pinned_view(h_nonces, 12ull * n))) && !(vn & 3) &&
             (vst = pinned_view(ctx->h_stat, n))) {
             Batch b = base_batch(ctx);
             b.arena = reinterpret_cast<uint8_t *>(va);
