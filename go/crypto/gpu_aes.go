@@ -231,7 +231,7 @@ func (gg *GPUGroup) Close() {
 // seals or opens the whole batch with one call instead of one Encrypt / Decrypt per packet
 // (worker/outgoing.go:55-93, worker/incoming.go:54-92 loop over packets).  Laid out in Order's order,
 // each GPU's packets are adjacent and move by DMA (qgcm_group_last_path 2); a worker-sized batch (up to
-// 32768 packets in one 64-MiB chunk) whose slots start 16-B aligned, e.g. the 1472-B MaxPacketLength
+// 65536 packets and 128 MiB) whose slots start 16-B aligned, e.g. the 1472-B MaxPacketLength
 // stride, is sealed in place in the arena instead (qgcm_group_last_path 3).
 
 // KeyIndex is the key slot of this peer: the Key field of its packets' Descs.

@@ -155,7 +155,7 @@ int qgcm_resident_stats(const qgcm_ctx *ctx, uint64_t *out, int n);
 /* Slots in host memory at i*stride; copies in, runs the device batch, copies back, synchronously.
  * Pipelined in 64 MiB chunks over 3 streams (H2D of chunk c+1 || kernel c || D2H of chunk c-1);
  * h_arena from qgcm_host_alloc (pinned) is DMA'd in place, pageable memory is staged by HIP.  A pinned
- * batch of up to 32768 packets with 16-B-aligned slots (stride a multiple of 16) is sealed in place
+ * batch of up to 65536 packets (128 MiB) with 16-B-aligned slots (stride a multiple of 16) is sealed in place
  * instead: one kernel on the arena's device view, no copies (QGCM_HOST_DIRECT=0 disables it).
  * Returns the number of packets that failed (0 = all ok) or a negative error.  status may be NULL.
  * Replaces the per-packet Apply loop of worker/outgoing.go:55-93 / worker/incoming.go:54-92 for a
@@ -208,9 +208,9 @@ int qgcm_group_last_zerocopy(const qgcm_group *g);
  * the gap bytes inside a run go back unchanged.  A batch laid out in qgcm_group_order's order, or any batch
  * of a one-member group, takes it.  A chunk of at most 8192 packets whose records all start 16-B aligned
  * runs one workgroup per packet instead of the sorted worklist (QGCM_DESC_ONE=0 disables that).  Direct:
- * when such a batch is a single chunk in a pinned arena that also holds each record's 16-B-rounded area,
+ * when such a batch (up to 65536 packets, 128 MiB) is in a pinned arena that also holds each record's 16-B-rounded area,
  * that kernel seals the records in place over PCIe, with no copies (QGCM_GROUP_DIRECT=0 disables it);
- * so does each member's share of up to 32768 such records when members are interleaved in the arena.
+ * so does each member's share of up to 65536 such records when members are interleaved in the arena.
  * QGCM_GROUP_DMA=0 disables the DMA runs.  qgcm_group_last_path: the path member
  * took in the last call (0 host copies, 1 zero-copy, 2 DMA runs, 3 direct) or QGCM_E_ARG. */
 int qgcm_group_last_path(const qgcm_group *g, int member);

@@ -151,12 +151,15 @@ long resident_call(Resident *r, bool seal, uint32_t key, uint8_t *data, long len
 constexpr uint32_t kOneUniformMax = 2048;    // measured cross-over with the quad kernel: 2048-4096 packets
 // keyed batches of up to this many packets run one workgroup per packet when their records allow it:
 // against the worklist + per-wave kernel it wins up to 8192 (1395 vs 1442 us a seal+open pair at 8192,
-// 754 vs 921 at 4096: profiles/r4_s46_s49); the uniform kernel's cross-over is lower
+// 754 vs 921 at 4096: profiles/r4_s46_s51); the uniform kernel's cross-over is lower
 constexpr uint32_t kDescOneMax = 8192;
-// a batch sealed in place in pinned host memory (group.cpp run_member_direct) takes that kernel up to
-// this many packets: 1.57-1.65 ms a pair at 16384 against 2.38 by DMA runs, 3.11 against 4.28 at 32768
-// (profiles/r4_s52_s53); 65536 packets are two DMA chunks, where the DMA pipeline wins
-constexpr uint32_t kDirectMax = 32768;
+// a batch sealed in place in pinned host memory (group.cpp run_member_direct, qgcm_seal_host) takes
+// that kernel up to this many packets and kDirectMaxBytes of slots: keyed 1.57-1.65 ms a pair at 16384
+// against 2.38 by DMA runs, 3.11 against 4.28 at 32768, 6.28-6.30 against 7.23 at 65536, but 12.3
+// against 11.7 at 131072; uniform 5.92-5.97 against 6.30 at 65536 (profiles/r4_s52_s54, r4_s55_s56,
+// r4_s62)
+constexpr uint32_t kDirectMax = 65536;
+constexpr uint64_t kDirectMaxBytes = 128ull << 20;
 constexpr uint32_t kLaunchChunk = 1u << 19;  // packets per quad-kernel launch of a uniform batch
 constexpr uint32_t kDescChunk = 0;           // packets per sorted chunk of a descriptor batch (0 = all)
 bool ctx_one_kernel(const qgcm_ctx *ctx);

@@ -613,7 +613,7 @@ bool direct_on() {  // QGCM_GROUP_DIRECT=0: worker-sized batches copy by DMA as 
     return !(v && !strcmp(v, "0"));
 }
 
-// Direct: a member's worker-sized batch (at most direct_max packets; by DMA runs: one chunk) whose
+// Direct: a member's worker-sized batch (at most direct_max packets and kDirectMaxBytes) whose
 // records all start 16-B aligned in a pinned arena that holds each record's 16-B-rounded area runs one
 // workgroup per packet on the records in place, over PCIe: no copies and one launch.  The member's
 // records need not be adjacent: no record shares another's rounded area, so members interleaved in one
@@ -630,6 +630,9 @@ int run_member_direct(Member &mb, bool seal, uint8_t *h_arena, const qgcm_desc *
         if (((uintptr_t)(h_arena + d.offset) & 15) || area > qgcm::kOneCap - 16) return 0;
         ext = std::max(ext, d.offset + area);
     }
+    uint64_t bytes = 0;  // the records' rounded areas: past kDirectMaxBytes the DMA pipeline is faster
+    for (size_t j = 0; j < m; ++j) bytes += (rec_in(seal, descs[idx[j]].len) + 15) & ~15ull;
+    if (bytes > qgcm::kDirectMaxBytes) return 0;
     const uint64_t va = pinned_view(h_arena, ext);
     if (!va || (va & 15)) return 0;
     DmaState &z = mb.dma;
@@ -667,8 +670,7 @@ int run_member_dma(Member &mb, bool seal, uint8_t *h_arena, const qgcm_desc *des
                    const DmaPlan &pl, const uint8_t *h_nonces, uint32_t aad_len, uint8_t *h_status, int *bad_out) {
     {
         int rc = QGCM_OK;
-        if (pl.chunks.size() == 1 &&
-            run_member_direct(mb, seal, h_arena, descs, idx, pl.at.size(), h_nonces, aad_len, h_status, bad_out, &rc))
+        if (run_member_direct(mb, seal, h_arena, descs, idx, pl.at.size(), h_nonces, aad_len, h_status, bad_out, &rc))
             return rc;
     }
     DmaState &z = mb.dma;
@@ -834,7 +836,8 @@ int run_group(qgcm_group *g, bool seal, uint8_t *h_arena, const qgcm_desc *descs
     auto dma_pays = [&](int k) {
         const DmaPlan &pl = plan[k];
         if (pl.piece_bytes >= kMinRun * pl.pieces.size()) return true;
-        if (!pinned || pl.chunks.size() != 1 || pl.at.size() > qgcm::direct_max(g->m[k].ctx)) return false;
+        if (!pinned || pl.at.size() > qgcm::direct_max(g->m[k].ctx) || pl.piece_bytes > qgcm::kDirectMaxBytes)
+            return false;
         return std::all_of(pl.at.begin(), pl.at.end(), [](uint64_t a) { return !(a & 15); });
     };
     const char *cv = getenv("QGCM_GROUP_DMA_CHUNK_MB");  // A/B knob: staged bytes per DMA chunk

@@ -808,7 +808,8 @@ static int run_host(qgcm_ctx *ctx, bool seal, uint8_t *h_arena, uint64_t stride,
         const char *dv = getenv("QGCM_HOST_DIRECT");
         const uint64_t area = (4ull + len + (seal ? QGCM_OVERHEAD : 0) + 15) & ~15ull;
         uint64_t va = 0, vn = 0, vst = 0;
-        if (!(dv && !strcmp(dv, "0")) && n <= direct_max(ctx) && !ctx->variant_forced && !(stride & 15) &&
+        if (!(dv && !strcmp(dv, "0")) && n <= direct_max(ctx) && (uint64_t)n * stride <= kDirectMaxBytes &&
+            !ctx->variant_forced && !(stride & 15) &&
             area <= stride && area <= kOneCap - 16 && (seal || len >= QGCM_OVERHEAD) &&
             (va = pinned_view(h_arena, (uint64_t)n * stride)) && !(va & 15) &&
             (!(seal && h_nonces) || (vn = pinned_view(h_nonces, 12ull * n))) && !(vn & 3) &&

@@ -23,7 +23,7 @@ pytestmark = pytest.mark.gpu
 
 AAD = bytes([10, 99, 0, 1])
 DESC_ONE_MAX = 8192  # gcm_internal.h kDescOneMax
-DIRECT_MAX = 32768  # gcm_internal.h kDirectMax
+DIRECT_MAX = 65536  # gcm_internal.h kDirectMax
 
 
 @pytest.fixture(scope="module")
@@ -291,7 +291,7 @@ def test_group_unaligned_records_take_the_copy_path(torch):
 
 @pytest.mark.parametrize("n,one,align,direct", [(1, "1", 16, "1"), (64, "1", 16, "1"), (700, "1", 16, "1"),
                                                 (8192, "1", 16, "0"), (8193, "1", 16, "0"), (8193, "1", 16, "1"),
-                                                (32768, "1", 16, "1"), (32769, "1", 16, "1"), (700, "0", 16, "1"),
+                                                (65536, "1", 16, "1"), (65537, "1", 16, "1"), (700, "0", 16, "1"),
                                                 (64, "1", 4, "1"), (64, "1", 16, "0"), (700, "1", 16, "0"),
                                                 (700, "1", 16, "slot")])
 def test_group_small_batches_one_workgroup_per_packet(torch, n, one, align, direct, monkeypatch):
