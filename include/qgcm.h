@@ -207,10 +207,11 @@ int qgcm_group_last_zerocopy(const qgcm_group *g);
  * shader-driven PCIe traffic;
  * the gap bytes inside a run go back unchanged.  A batch laid out in qgcm_group_order's order, or any batch
  * of a one-member group, takes it.  A chunk of at most 8192 packets whose records all start 16-B aligned
- * runs one workgroup per packet instead of the sorted worklist (QGCM_DESC_ONE=0 disables that).  Direct:
- * when such a batch (up to 65536 packets, 128 MiB) is in a pinned arena that also holds each record's 16-B-rounded area,
- * that kernel seals the records in place over PCIe, with no copies (QGCM_GROUP_DIRECT=0 disables it);
- * so does each member's share of up to 65536 such records when members are interleaved in the arena.
+ * runs one workgroup per packet instead of the sorted worklist (QGCM_DESC_ONE=0 disables that).
+ * Direct: a member's share of up to 65536 packets (128 MiB) whose records all start 16-B aligned, in a
+ * pinned arena that also holds each record's 16-B-rounded area, is sealed in place by that kernel over
+ * PCIe with no copies, whether the members' records are adjacent or interleaved (QGCM_GROUP_DIRECT=0
+ * disables it).
  * QGCM_GROUP_DMA=0 disables the DMA runs.  qgcm_group_last_path: the path member
  * took in the last call (0 host copies, 1 zero-copy, 2 DMA runs, 3 direct) or QGCM_E_ARG. */
 int qgcm_group_last_path(const qgcm_group *g, int member);
