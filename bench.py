@@ -366,6 +366,83 @@ def extra_e2e(key: bytes, reps: int = 3, n: int = 1 << 20) -> dict:
             "matches_device_path": same, "status_ok": rc == 0, "reps": reps}
 
 
+def extra_worker_batches(key: bytes, reps: int = 30, sizes=(64, 1024, 16384)) -> dict:
+    """Worker-sized batches (a recvmmsg batch of Payload.Raw slots, 1350 B in 1472-B slots, pinned):
+    median microseconds per seal + open pair through qgcm_seal_host (one peer) and through a one-member
+    group (qgcm_group_seal_host, 8 peers, packet i of peer i % 8), both sealed in place.
+    Checked in the run: the first host seal equals the device path's bytes (qgcm_seal_uniform), the
+    first group seal the device descriptor batch's (qgcm_seal_batch); every open restores the plaintext."""
+    from quantum_amd import _lib
+    import ctypes as C
+
+    L, stride, nmax = 1350, 1472, max(sizes)
+    keys = b"".join(bytes((b + 7 * k) & 0xFF for b in key) for k in range(8))  # 8 distinct peer keys
+    ctx = Context(device=0, max_keys=8)
+    ctx.set_key(0, keys[:32])
+    grp = shard.Group([0], max_keys=8)
+    grp.set_keys(0, keys)
+    dctx = Context(device=0, max_keys=8)
+    for k in range(8):
+        dctx.set_key(k, keys[32 * k:32 * k + 32])
+    Lb = _lib.lib()
+    a_ptr, n_ptr = Lb.qgcm_host_alloc(nmax * stride), Lb.qgcm_host_alloc(12 * nmax)
+    host = np.frombuffer((C.c_uint8 * (nmax * stride)).from_address(a_ptr), np.uint8)
+    nons = np.frombuffer((C.c_uint8 * (12 * nmax)).from_address(n_ptr), np.uint8)
+    rng = np.random.default_rng(0x5EED0077)
+    host[:] = rng.integers(0, 256, host.size, dtype=np.uint8)
+    host.reshape(nmax, stride)[:, :4] = np.frombuffer(AAD, np.uint8)
+    Lb.qgcm_random_nonces(n_ptr, nmax)
+    plain = host.copy()
+    out, ok = {}, True
+    for n in sizes:
+        offs = np.arange(n, dtype=np.uint64) * stride
+        kidx = (np.arange(n) % 8).astype(np.uint32)
+        d_seal = shard.host_descs(offs, np.full(n, L, np.uint32), kidx)
+        d_open = shard.host_descs(offs, np.full(n, L + 28, np.uint32), kidx)
+        row = {}
+        for path in ("host", "group"):
+            # the device path's bytes for this batch, from the same plaintext and nonces
+            dev = torch.from_numpy(plain[:n * stride].copy()).cuda()
+            dn = torch.from_numpy(nons[:12 * n].copy()).cuda()
+            if path == "host":
+                batch.seal_uniform(ctx, dev, stride, n, L, 0, dn)
+            else:
+                batch.seal_batch(dctx, dev, batch.make_descs(offs, [L] * n, kidx.tolist(), "cuda"), n, dn)
+            want = dev.cpu().numpy()
+            ts = []
+            for r in range(reps + 1):
+                t0 = time.perf_counter()
+                if path == "host":
+                    bad = Lb.qgcm_seal_host(ctx.handle, a_ptr, stride, n, L, 0, n_ptr, 4, None)
+                    if r == 0:
+                        ok &= bool(np.array_equal(host[:n * stride], want))
+                    bad += Lb.qgcm_open_host(ctx.handle, a_ptr, stride, n, L + 28, 0, 4, None)
+                else:
+                    bad = grp.seal_host(a_ptr, d_seal, n, n_ptr, 4)
+                    if r == 0:
+                        ok &= bool(np.array_equal(host[:n * stride], want))
+                    bad += grp.open_host(a_ptr, d_open, n, 4)
+                if r:
+                    ts.append(time.perf_counter() - t0)
+                ok &= bad == 0
+            ok &= bool(np.array_equal(host[:n * stride].reshape(n, stride)[:, :4 + L],
+                                      plain[:n * stride].reshape(n, stride)[:, :4 + L]))
+            row[f"{path}_pair_us"] = round(float(np.median(ts)) * 1e6, 1)
+            row[f"{path}_path"] = "seal_host" if path == "host" else grp.last_path(0)
+            del dev, dn
+        out[str(n)] = row
+    del host, nons
+    Lb.qgcm_host_free(a_ptr)
+    Lb.qgcm_host_free(n_ptr)
+    grp.close()
+    dctx.close()
+    ctx.close()
+    return {"workload": f"worker-sized batches from pinned host memory: {list(sizes)} x {L} B in {stride}-B slots, "
+                        "seal + open pair, qgcm_seal_host (1 peer) and a one-member group (8 peers)",
+            "value": out[str(sizes[0])]["group_pair_us"], "unit": f"us per seal+open pair of {sizes[0]} keyed packets",
+            "higher_is_better": False, "by_packets": out, "matches_device_path": ok, "status_ok": ok, "reps": reps}
+
+
 def _sha256_host(a: np.ndarray) -> str:
     import hashlib
 
@@ -791,6 +868,7 @@ def main() -> None:
                              ("config5", lambda: extra_config5(key, args.cpu_threads or host["share"], verify=not args.no_verify)),
                              ("config5_resident", lambda: extra_config5_resident(key, verify=not args.no_verify)),
                              ("per_packet", extra_per_packet),
+                             ("worker_batches", lambda: extra_worker_batches(key)),
                              ("config4_one_gpu", lambda: extra_config4_one_gpu(key))):
                 t0 = time.perf_counter()
                 try:
