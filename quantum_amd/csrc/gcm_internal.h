@@ -90,8 +90,11 @@ struct QuadWorklist {
 // itself (small_worklist(n)), the caller fills them otherwise
 hipError_t launch_quad_worklist(const qgcm_desc *descs, uint32_t n, uint32_t max_keys, const uint8_t *key_valid,
                                 bool seal, void *ws, size_t ws_bytes, QuadWorklist *out, hipStream_t s,
-                                uint8_t *status);
-bool small_worklist(uint32_t n);  // a batch of n packets builds its worklist in one workgroup
+                                uint8_t *status, bool small);
+// a batch of n packets builds its worklist in one workgroup (on: the context's QGCM_SMALL_WORKLIST
+// setting); computed once per batch and passed to launch_quad_worklist, so the status fill and the
+// worklist build always agree
+bool small_worklist(uint32_t n, bool on);
 hipError_t launch_packets(bool seal, int variant, const Batch &b, int grid, hipStream_t s);
 // One packet, one 512-thread workgroup (qgcm_seal_one / qgcm_open_one): the slot (b.stride bytes,
 // a multiple of 16, at most kOneCap - 16) is staged in LDS; b.n must be 1.
@@ -170,7 +173,7 @@ std::mutex &ctx_io_mu(qgcm_ctx *ctx);
 // Small keyed batches whose records the caller has checked (group.cpp's DMA staging): one workgroup
 // per descriptor (gcm_one_kernel), no worklist.  descs_one_max: the largest batch that takes it (0:
 // off; kDescOneMax, QGCM_DESC_ONE_MAX at qgcm_create; QGCM_VARIANT and QGCM_ONE_KERNEL turn it off as
-// for uniform batches, and so does QGCM_DESC_ONE=0, read per call).  run_descs_one needs every record 16-B aligned in
+// for uniform batches, and so does QGCM_DESC_ONE=0 at qgcm_create).  run_descs_one needs every record 16-B aligned in
 // device memory, no other record inside its 16-B-rounded area (4 + len (+ 28 on seal), rounded up),
 // and that area at most kOneCap - 16 bytes; keys, short opens and statuses behave as in the batch
 // kernels.

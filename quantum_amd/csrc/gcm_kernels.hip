@@ -581,20 +581,8 @@ __device__ __forceinline__ uint32_t quad_xor(uint32_t v) {
     return v;
 }
 
-// QGCM_REALIGN (side builds, A/B only): the segmented kernel stores a payload that
-// is not 16-B aligned (packed 4-B slots) as aligned 16-B chunks -- lane m's chunk is the last dl
-// dwords of block b - 1 (from lane m - 1 by DPP; lane 0 carries lane 3's from the previous step) and
-// the first 4 - dl of block b -- with exact dword stores for the head of block 0 and the tail of the
-// last full block, so no byte outside the payload is written.
-#ifndef QGCM_REALIGN
-#define QGCM_REALIGN 0
-#endif
-__device__ __forceinline__ uint32_t quad_prev(uint32_t v) {  // lane m <- lane (m - 1) mod 4
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x93, 0xf, 0xf, false);  // quad_perm [3,0,1,2]
-}
-
 // One packet of a quad tile (4 lanes, lane m owns blocks b = m mod 4): CTR + GHASH + tag, in place.
-template <bool kSeal, class Eng, bool kRealign = false>
+template <bool kSeal, class Eng>
 __device__ __forceinline__ void quad_packet(const Batch &b, const Eng &eng, uint32_t pkt, uint64_t off, uint32_t L,
                                             uint32_t wkey, uint32_t m, uint32_t gH4) {
     const uint4 *Hg = b.gh_table + (size_t)wkey * kGhEntries;  // comb tables of H^k (global)
@@ -621,9 +609,6 @@ __device__ __forceinline__ void quad_packet(const Batch &b, const Eng &eng, uint
 
     uint32_t e0 = 0, e1 = 0, e2 = 0, e3 = 0;  // E_K(J0)
     uint32_t prefix = 0;
-    // kRealign: dwords the payload lies past a 16-B boundary, and lane 3's previous block (lane 0)
-    const uint32_t dl = kRealign ? (uint32_t)((reinterpret_cast<uintptr_t>(data) >> 2) & 3u) : 0u;
-    W4 carry = {0, 0, 0, 0};
     {
     Ctr cc;
     uint32_t hi = 0;
@@ -640,32 +625,7 @@ __device__ __forceinline__ void quad_packet(const Batch &b, const Eng &eng, uint
         uint32_t k0, k1, k2, k3;
         eng.block(cc, ctr & 0xffu, k0, k1, k2, k3);
         const W4 out = {in.x ^ k0, in.y ^ k1, in.z ^ k2, in.w ^ k3};
-        if constexpr (kRealign) {
-            const W4 rot = {quad_prev(out.x), quad_prev(out.y), quad_prev(out.z), quad_prev(out.w)};
-            const W4 pv = m == 0 ? carry : rot;  // block bi - 1
-            carry = rot;
-            uint32_t *pw = reinterpret_cast<uint32_t *>(p);
-            if (dl == 0) {
-                store_block(p, out);
-            } else {
-                if (bi == 0) {  // head: the first 4 - dl dwords of block 0, at the payload start
-                    pw[0] = out.x;
-                    if (dl < 3) pw[1] = out.y;
-                    if (dl < 2) pw[2] = out.z;
-                } else {  // the aligned 16 B that end 4 dl bytes into block bi
-                    const W4 a = {dl == 1 ? pv.w : (dl == 2 ? pv.z : pv.y), dl == 1 ? out.x : (dl == 2 ? pv.w : pv.z),
-                                  dl == 1 ? out.y : (dl == 2 ? out.x : pv.w), dl == 1 ? out.z : (dl == 2 ? out.y : out.x)};
-                    store_block(reinterpret_cast<W4 *>(pw - dl), a);
-                }
-                if (bi + 1 == nfull) {  // tail: the last dl dwords of the last full block
-                    if (dl > 2) pw[1] = out.y;
-                    if (dl > 1) pw[2] = out.z;
-                    pw[3] = out.w;
-                }
-            }
-        } else {
-            store_block(p, out);
-        }
+        store_block(p, out);
         const W4 &c = kSeal ? out : in;
         eng.ghash(z0, z1, z2, z3, gH4);
         z0 ^= c.x;
@@ -1070,7 +1030,7 @@ gcm_seg_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
             if (pkt != 0xffffffffu) {  // the padding of a key run's last tile
                 const qgcm_desc dsc = b.descs[pkt];
                 const uint32_t L = kSeal ? dsc.len : dsc.len - QGCM_OVERHEAD;  // open: len >= 28 here
-                quad_packet<kSeal, Tab2F, QGCM_REALIGN != 0>(b, e3, pkt, dsc.offset, L, key, m, 0u);
+                quad_packet<kSeal, Tab2F>(b, e3, pkt, dsc.offset, L, key, m, 0u);
             }
             ++ntile_stat;
         }

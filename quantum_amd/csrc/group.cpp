@@ -249,6 +249,12 @@ struct qgcm_group {
     bool dma = true;       // QGCM_GROUP_DMA=0: never the DMA-run path
     int last_zc = 0;       // the last call took the zero-copy path (qgcm_group_last_zerocopy)
     uint64_t zc_chunk = kZcChunk;  // zero-copy staging chunk bytes (QGCM_GROUP_ZC_CHUNK_MB, tuning)
+    // A/B and diagnostic knobs, read once at qgcm_group_create like the ones above (a getenv per call
+    // would race a setenv from another thread)
+    bool direct = true;             // QGCM_GROUP_DIRECT=0: worker-sized batches copy by DMA as larger ones
+    int dma_slots = kDmaSlots;      // QGCM_GROUP_DMA_SLOTS: staging slots (chunks in flight) per member
+    uint64_t dma_chunk = kDmaChunk; // QGCM_GROUP_DMA_CHUNK_MB: staged bytes per DMA chunk
+    bool dma_timeline = false;      // QGCM_GROUP_DMA_TIMELINE=1: per-chunk timing events to stderr
     std::mutex call_mu;  // one batch call at a time (members' staging is reused per call)
 };
 
@@ -558,11 +564,6 @@ void plan_dma(bool seal, const qgcm_desc *descs, const uint32_t *idx, size_t m, 
     }
 }
 
-bool env_flag(const char *name) {  // read per call (A/B and tests switch it within one process)
-    const char *v = getenv(name);
-    return v && atoi(v) != 0;
-}
-
 int dma_ready(DmaState &z, uint64_t stage, uint64_t side, size_t slots, size_t m) {
     if (m > z.stat_cap) {
         if (z.d_stat) hipFree(z.d_stat);
@@ -608,21 +609,19 @@ int dma_ready(DmaState &z, uint64_t stage, uint64_t side, size_t slots, size_t m
     return QGCM_OK;
 }
 
-bool direct_on() {  // QGCM_GROUP_DIRECT=0: worker-sized batches copy by DMA as larger ones (A/B; read per call)
-    const char *v = getenv("QGCM_GROUP_DIRECT");
-    return !(v && !strcmp(v, "0"));
-}
-
 // Direct: a member's worker-sized batch (at most direct_max packets and kDirectMaxBytes) whose
 // records all start 16-B aligned in a pinned arena that holds each record's 16-B-rounded area runs one
-// workgroup per packet on the records in place, over PCIe: no copies and one launch.  The member's
-// records need not be adjacent: no record shares another's rounded area, so members interleaved in one
-// arena each seal their own in place at once.  Descriptors, nonces and statuses stay in pinned host
-// memory as well.  Returns 1 when it ran (rc in *rc), 0 when the batch does not qualify (nothing done).
-int run_member_direct(Member &mb, bool seal, uint8_t *h_arena, const qgcm_desc *descs, const uint32_t *idx,
-                      size_t m, const uint8_t *h_nonces, uint32_t aad_len, uint8_t *h_status, int *bad_out,
-                      int *rc) {
-    if (!direct_on() || !m || m > qgcm::direct_max(mb.ctx)) return 0;
+// workgroup per packet on the records in place, over PCIe: no copies and one launch.  The kernel
+// writes each record's whole 16-B-rounded area back, so `allowed` (run_group) is false unless EVERY
+// record of the batch -- any member's, rejected ones included -- starts 16-B aligned: then no record
+// begins inside another's rounded area, and members interleaved in one arena each seal their own in
+// place at once without one member's write-back overwriting another's results.  Descriptors, nonces
+// and statuses stay in pinned host memory as well.  Returns 1 when it ran (rc in *rc), 0 when the
+// batch does not qualify (nothing done).
+int run_member_direct(Member &mb, bool allowed, bool seal, uint8_t *h_arena, const qgcm_desc *descs,
+                      const uint32_t *idx, size_t m, const uint8_t *h_nonces, uint32_t aad_len, uint8_t *h_status,
+                      int *bad_out, int *rc) {
+    if (!allowed || !m || m > qgcm::direct_max(mb.ctx)) return 0;
     uint64_t ext = 0;
     for (size_t j = 0; j < m; ++j) {
         const qgcm_desc &d = descs[idx[j]];
@@ -666,11 +665,13 @@ int run_member_direct(Member &mb, bool seal, uint8_t *h_arena, const qgcm_desc *
     return 1;
 }
 
-int run_member_dma(Member &mb, bool seal, uint8_t *h_arena, const qgcm_desc *descs, const uint32_t *idx,
-                   const DmaPlan &pl, const uint8_t *h_nonces, uint32_t aad_len, uint8_t *h_status, int *bad_out) {
+int run_member_dma(const qgcm_group *g, Member &mb, bool direct_ok, bool seal, uint8_t *h_arena,
+                   const qgcm_desc *descs, const uint32_t *idx, const DmaPlan &pl, const uint8_t *h_nonces,
+                   uint32_t aad_len, uint8_t *h_status, int *bad_out) {
     {
         int rc = QGCM_OK;
-        if (run_member_direct(mb, seal, h_arena, descs, idx, pl.at.size(), h_nonces, aad_len, h_status, bad_out, &rc))
+        if (run_member_direct(mb, direct_ok, seal, h_arena, descs, idx, pl.at.size(), h_nonces, aad_len, h_status,
+                              bad_out, &rc))
             return rc;
     }
     DmaState &z = mb.dma;
@@ -678,9 +679,8 @@ int run_member_dma(Member &mb, bool seal, uint8_t *h_arena, const qgcm_desc *des
     const uint64_t pk = pl.max_pk;
     const uint64_t off_non = (16ull * pk + 255) & ~255ull;
     const uint64_t side = off_non + (non ? (12ull * pk + 255) & ~255ull : 0);  // [descs][nonces]
-    const char *sv = getenv("QGCM_GROUP_DMA_SLOTS");  // A/B knob: staging slots (chunks in flight)
     const size_t nc = pl.chunks.size();
-    const size_t S = std::min<size_t>(nc, (size_t)std::max(2, std::min(64, sv && *sv ? atoi(sv) : kDmaSlots)));
+    const size_t S = std::min<size_t>(nc, (size_t)g->dma_slots);
     const size_t m = pl.at.size();
     int rc = dma_ready(z, pl.max_bytes, side, S, m);
     if (rc != QGCM_OK) return rc;
@@ -696,7 +696,7 @@ int run_member_dma(Member &mb, bool seal, uint8_t *h_arena, const qgcm_desc *des
     // copy-out, printed to stderr as ms since the call's first copy-in was queued (no profiler attached)
     std::vector<hipEvent_t> tl;
     hipEvent_t tl0 = nullptr;
-    if (env_flag("QGCM_GROUP_DMA_TIMELINE")) {
+    if (g->dma_timeline) {
         tl.assign(3 * nc, nullptr);
         for (hipEvent_t &e : tl) hipEventCreate(&e);
         hipEventCreate(&tl0);
@@ -830,8 +830,11 @@ int run_group(qgcm_group *g, bool seal, uint8_t *h_arena, const qgcm_desc *descs
     sorted = sorted && !((uintptr_t)h_arena & 3);
     std::vector<DmaPlan> plan(G);
     // worker-sized batches from a pinned arena may go direct (run_member_direct checks the rest), so a
-    // run under kMinRun still takes the DMA branch for them
-    const bool pinned_arena = direct_on() && pinned_view(h_arena, 1) != 0;
+    // run under kMinRun still takes the DMA branch for them.  Direct writes whole 16-B-rounded areas
+    // back, so it needs every record of the batch 16-B aligned (run_member_direct)
+    bool all16 = g->direct;
+    for (uint32_t i = 0; all16 && i < n; ++i) all16 = !(((uintptr_t)h_arena + descs[i].offset) & 15);
+    const bool pinned_arena = all16 && pinned_view(h_arena, 1) != 0;
     const bool pinned = sorted && pinned_arena;
     auto dma_pays = [&](int k) {
         const DmaPlan &pl = plan[k];
@@ -840,8 +843,7 @@ int run_group(qgcm_group *g, bool seal, uint8_t *h_arena, const qgcm_desc *descs
             return false;
         return std::all_of(pl.at.begin(), pl.at.end(), [](uint64_t a) { return !(a & 15); });
     };
-    const char *cv = getenv("QGCM_GROUP_DMA_CHUNK_MB");  // A/B knob: staged bytes per DMA chunk
-    const uint64_t dma_chunk = cv && *cv ? (uint64_t)std::max(1, std::min(4096, atoi(cv))) << 20 : kDmaChunk;
+    const uint64_t dma_chunk = g->dma_chunk;
     std::vector<int> rc(G, QGCM_OK), bad(G, 0), used_zc(G, 1);
     std::vector<std::thread> thr;
     int active = 0;
@@ -865,15 +867,15 @@ int run_group(qgcm_group *g, bool seal, uint8_t *h_arena, const qgcm_desc *descs
                 if (dma_pays(k)) {
                     mb.last_path = 2;
                     used_zc[k] = 0;
-                    rc[k] = run_member_dma(mb, seal, h_arena, descs, part[k].data(), plan[k], h_nonces, aad_len,
-                                           h_status, &bad[k]);
+                    rc[k] = run_member_dma(g, mb, pinned_arena, seal, h_arena, descs, part[k].data(), plan[k],
+                                           h_nonces, aad_len, h_status, &bad[k]);
                     return;
                 }
             }
             {  // a worker-sized share of an interleaved batch: in place, as by DMA runs above
                 int drc = QGCM_OK;
-                if (pinned_arena && run_member_direct(mb, seal, h_arena, descs, part[k].data(), part[k].size(),
-                                                      h_nonces, aad_len, h_status, &bad[k], &drc)) {
+                if (run_member_direct(mb, pinned_arena, seal, h_arena, descs, part[k].data(), part[k].size(),
+                                      h_nonces, aad_len, h_status, &bad[k], &drc)) {
                     used_zc[k] = 0;
                     rc[k] = drc;
                     return;
@@ -911,8 +913,8 @@ int run_group(qgcm_group *g, bool seal, uint8_t *h_arena, const qgcm_desc *descs
         } else {
             mb.last_path = 2;
             used_zc[k] = 0;
-            rc[k] = run_member_dma(mb, seal, h_arena, descs, part[k].data(), plan[k], h_nonces, aad_len, h_status,
-                                   &bad[k]);
+            rc[k] = run_member_dma(g, mb, pinned_arena, seal, h_arena, descs, part[k].data(), plan[k], h_nonces,
+                                   aad_len, h_status, &bad[k]);
         }
         if (had) hipSetDevice(dev0);  // the caller's current device, as it was
     }
@@ -942,6 +944,11 @@ qgcm_group *qgcm_group_create(const int *devices, int count, uint32_t max_keys, 
     if (const char *v = getenv("QGCM_GROUP_ZEROCOPY")) g->zerocopy = atoi(v) != 0;
     if (const char *v = getenv("QGCM_GROUP_DMA")) g->dma = atoi(v) != 0;
     if (const char *v = getenv("QGCM_GROUP_ZC_CHUNK_MB")) g->zc_chunk = (uint64_t)std::max(1, atoi(v)) << 20;
+    if (const char *v = getenv("QGCM_GROUP_DIRECT")) g->direct = strcmp(v, "0") != 0;
+    if (const char *v = getenv("QGCM_GROUP_DMA_SLOTS"); v && *v) g->dma_slots = std::max(2, std::min(64, atoi(v)));
+    if (const char *v = getenv("QGCM_GROUP_DMA_CHUNK_MB"); v && *v)
+        g->dma_chunk = (uint64_t)std::max(1, std::min(4096, atoi(v))) << 20;
+    if (const char *v = getenv("QGCM_GROUP_DMA_TIMELINE")) g->dma_timeline = atoi(v) != 0;
     for (int k = 0; k < count; ++k) {
         Member mb;
         mb.device = devices[k];

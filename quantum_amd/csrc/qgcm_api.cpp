@@ -47,6 +47,11 @@ struct qgcm_ctx {
                                                 // kernel (QGCM_LAUNCH_CHUNK, tuning; 0 = one launch)
     uint32_t desc_chunk = kDescChunk;           // descriptor batches: packets per sorted chunk
                                                 // (QGCM_DESC_CHUNK, tuning; 0 = one launch)
+    // A/B switches, read once at qgcm_create like every other knob (a getenv per call would race a
+    // setenv from another thread): QGCM_DESC_ONE=0 sends small keyed batches to the worklist path,
+    // QGCM_HOST_DIRECT=0 stops qgcm_seal_host sealing worker-sized pinned arenas in place,
+    // QGCM_SMALL_WORKLIST=0 builds small batches' worklists by the multi-launch path
+    bool desc_one_on = true, host_direct = true, small_wl = true;
     uint32_t *d_rk = nullptr;
     uint4 *d_gh = nullptr;
     uint4 *d_pw = nullptr;   // per-packet flat GHASH: comb tables of H^1..H^kPwPowers, key slots < pw_keys
@@ -257,8 +262,7 @@ hipStream_t qgcm::ctx_pipe(qgcm_ctx *ctx, int k) { return ctx->pipe[k]; }
 std::mutex &qgcm::ctx_io_mu(qgcm_ctx *ctx) { return ctx->io_mu; }
 
 uint32_t qgcm::descs_one_max(const qgcm_ctx *ctx) {
-    const char *v = getenv("QGCM_DESC_ONE");  // "0": small keyed batches take the worklist path (A/B)
-    return ctx->one_kernel && !ctx->variant_forced && !(v && !strcmp(v, "0")) ? ctx->desc_one_max : 0u;
+    return ctx->one_kernel && !ctx->variant_forced && ctx->desc_one_on ? ctx->desc_one_max : 0u;
 }
 
 // Device-accessible address of pinned host memory [p, p + bytes) inside one allocation, or 0.
@@ -360,7 +364,7 @@ int run_descs(qgcm_ctx *ctx, bool seal, uint8_t *arena, const qgcm_desc *descs, 
     if (hipSetDevice(ctx->device) != hipSuccess) return QGCM_E_HIP;
     // statuses start at 0 (packets left out of the worklist keep it); small batches' worklist kernel
     // zeroes them itself
-    if (status && !small_worklist(n) && hipMemsetAsync(status, 0, n, s) != hipSuccess) return QGCM_E_HIP;
+    if (status && !small_worklist(n, ctx->small_wl) && hipMemsetAsync(status, 0, n, s) != hipSuccess) return QGCM_E_HIP;
     // The workspace is reused by the next call on any stream: serialize descriptor batches per ctx.
     std::lock_guard<std::mutex> g(ctx->ws_mu);
     // ...and on the device: this batch's worklist build must not start before the previous batch's
@@ -406,7 +410,7 @@ int run_descs_locked(qgcm_ctx *ctx, bool seal, const qgcm_desc *descs, uint32_t 
         }
         QuadWorklist q{};
         if (launch_quad_worklist(descs, n, ctx->max_keys, ctx->d_key_valid, seal, ctx->d_qws, ctx->qws_cap, &q, s,
-                                 status) != hipSuccess)
+                                 status, small_worklist(n, ctx->small_wl)) != hipSuccess)
             return QGCM_E_HIP;
         b.worklist = q.worklist;
         b.tile_keys = q.tile_keys;
@@ -415,10 +419,11 @@ int run_descs_locked(qgcm_ctx *ctx, bool seal, const qgcm_desc *descs, uint32_t 
         b.nruns = q.nruns;
         b.tile_counter = q.tile_counter;
         b.n_items = q.n_items;
-        // fewer than kSegMinTiles * 16 packets cannot give a key a run: the segmented kernel would find
-        // none, so only its complement (the per-wave kernel) is launched
+        // a key is a run once it has kSegMinTiles tiles, i.e. (kSegMinTiles - 1) * 16 + 1 packets (the
+        // worklist's ceil(count / 16)); a smaller batch cannot give any key a run, so only the segmented
+        // kernel's complement (the per-wave kernel) is launched
         const int vc = variant_complement(v);
-        if (vc < 0 || n >= kSegMinTiles * 16u) {
+        if (vc < 0 || n > (kSegMinTiles - 1) * 16u) {
             if (launch_packets(seal, v, b, grid_for(ctx, b.n_items, v), s) != hipSuccess) return QGCM_E_HIP;
             ctx->count(v == kVariantDescQuad ? QGCM_KERNEL_SEGMENTED : QGCM_KERNEL_PER_WAVE);
         }
@@ -578,6 +583,13 @@ qgcm_ctx *qgcm_create(int device, uint32_t max_keys, char *err, int errlen) {
         const int iv = atoi(v);
         if (variant_valid(iv) && variant_desc(iv)) ctx->desc_variant = iv;
     }
+    auto off = [](const char *name) {
+        const char *v = getenv(name);
+        return v && !strcmp(v, "0");
+    };
+    ctx->desc_one_on = !off("QGCM_DESC_ONE");
+    ctx->host_direct = !off("QGCM_HOST_DIRECT");
+    ctx->small_wl = !off("QGCM_SMALL_WORKLIST");
     uint8_t sbox[256];
     uint32_t te[512];
     build_tables(sbox, te);
@@ -655,7 +667,11 @@ int qgcm_set_keys(qgcm_ctx *ctx, uint32_t first_idx, uint32_t count, const uint8
     std::lock_guard<std::mutex> io(ctx->io_mu);
     hipStream_t s = ctx->pipe[1];
     // a running resident instance holds key tables (and keystreams computed ahead, key-valid bytes) in
-    // its caches: end it BEFORE the tables change and start no new one until the new keys are published
+    // its caches: end it BEFORE the tables change and start no new one until the new keys are published.
+    // res_mu is held for the whole update, so a per-packet call that finds no service cannot create one
+    // meanwhile (get_resident takes res_mu to create; an instance created mid-update would cache the
+    // tables being rewritten, and nothing would end it)
+    std::lock_guard<std::mutex> res_lk(ctx->res_mu);
     Resident *res = ctx->res.load(std::memory_order_acquire);
     (void)resident_pause(res);  // a failure marks the resident path broken: calls take the launch path
     int rc = QGCM_OK;
@@ -804,11 +820,10 @@ static int run_host(qgcm_ctx *ctx, bool seal, uint8_t *h_arena, uint64_t stride,
         // Direct: a worker-sized batch in a pinned arena with 16-B-aligned slots that hold the rounded
         // staging area is sealed in place over PCIe, one workgroup per packet (gcm_one_kernel on the
         // arena's device view), nonces and statuses in pinned memory too: one launch, no copies
-        // (QGCM_HOST_DIRECT=0: off, read per call)
-        const char *dv = getenv("QGCM_HOST_DIRECT");
+        // (QGCM_HOST_DIRECT=0 at qgcm_create: off)
         const uint64_t area = (4ull + len + (seal ? QGCM_OVERHEAD : 0) + 15) & ~15ull;
         uint64_t va = 0, vn = 0, vst = 0;
-        if (!(dv && !strcmp(dv, "0")) && n <= direct_max(ctx) && (uint64_t)n * stride <= kDirectMaxBytes &&
+        if (ctx->host_direct && n <= direct_max(ctx) && (uint64_t)n * stride <= kDirectMaxBytes &&
             !ctx->variant_forced && !(stride & 15) &&
             area <= stride && area <= kOneCap - 16 && (seal || len >= QGCM_OVERHEAD) &&
             (va = pinned_view(h_arena, (uint64_t)n * stride)) && !(va & 15) &&

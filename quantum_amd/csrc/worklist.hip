@@ -295,14 +295,11 @@ size_t quad_worklist_bytes(uint32_t n, uint32_t max_keys, uint32_t *n_items_out)
            al(16) + al(cub);
 }
 
-bool small_worklist(uint32_t n) {
-    const char *sv = getenv("QGCM_SMALL_WORKLIST");  // "0": small batches take the multi-launch path too (A/B)
-    return n && n <= kSmallWl && !(sv && !strcmp(sv, "0"));
-}
+bool small_worklist(uint32_t n, bool on) { return on && n && n <= kSmallWl; }
 
 hipError_t launch_quad_worklist(const qgcm_desc *descs, uint32_t n, uint32_t max_keys, const uint8_t *key_valid,
                                 bool seal, void *ws, size_t ws_bytes, QuadWorklist *out, hipStream_t s,
-                                uint8_t *status) {
+                                uint8_t *status, bool small) {
     uint32_t items = 0;
     const size_t need = quad_worklist_bytes(n, max_keys, &items);
     if (ws_bytes < need) return hipErrorInvalidValue;
@@ -330,7 +327,7 @@ hipError_t launch_quad_worklist(const qgcm_desc *descs, uint32_t n, uint32_t max
     void *cub_tmp = p;
     size_t cub_bytes = need - (size_t)(p - static_cast<char *>(ws));
     hipError_t e;
-    if (small_worklist(n)) {
+    if (small) {
         hipLaunchKernelGGL(qwl_small_kernel, dim3(1), dim3(kSmallThreads), 0, s, descs, n, max_keys, key_valid, seal,
                            items, worklist, tile_keys, runs, run_next, short_tiles, counter, status);
         if ((e = hipGetLastError()) != hipSuccess) return e;

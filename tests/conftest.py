@@ -41,6 +41,11 @@ def batch_digests():
 
 
 @pytest.fixture(scope="session")
+def headline_digest():
+    return golden("headline_digest.json")
+
+
+@pytest.fixture(scope="session")
 def config3_digest():
     return golden("config3_digest.json")
 

@@ -39,24 +39,28 @@ def fuzz_keys():
 
 @pytest.fixture(scope="module")
 def fuzz_ctxs(torch, fuzz_keys):
+    """One context per (kernel variant, QGCM_SMALL_WORKLIST): both knobs are read at qgcm_create."""
     from quantum_amd.crypto import Context
 
     out = {}
-    old = os.environ.get("QGCM_DESC_VARIANT")
+    saved = {k: os.environ.get(k) for k in ("QGCM_DESC_VARIANT", "QGCM_SMALL_WORKLIST")}
     try:
         for v in (None, 13):
-            if v is None:
-                os.environ.pop("QGCM_DESC_VARIANT", None)
-            else:
-                os.environ["QGCM_DESC_VARIANT"] = str(v)
-            c = Context(device=0, max_keys=MAX_KEYS)
-            c.set_keys(0, fuzz_keys[:32 * SET_KEYS])
-            out["default" if v is None else v] = c
+            for small in ("1", "0"):
+                if v is None:
+                    os.environ.pop("QGCM_DESC_VARIANT", None)
+                else:
+                    os.environ["QGCM_DESC_VARIANT"] = str(v)
+                os.environ["QGCM_SMALL_WORKLIST"] = small
+                c = Context(device=0, max_keys=MAX_KEYS)
+                c.set_keys(0, fuzz_keys[:32 * SET_KEYS])
+                out[("default" if v is None else v, small)] = c
     finally:
-        if old is None:
-            os.environ.pop("QGCM_DESC_VARIANT", None)
-        else:
-            os.environ["QGCM_DESC_VARIANT"] = old
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     yield out
     for c in out.values():
         c.close()
@@ -94,15 +98,13 @@ def draw_case(case: int):
 @pytest.mark.parametrize("small", ["1", "0"])
 @pytest.mark.parametrize("variant", ["default", 13])
 @pytest.mark.parametrize("seed", range(len(SIZES)))
-def test_descriptor_fuzz_vs_oracle(torch, fuzz_ctxs, fuzz_keys, variant, seed, small, monkeypatch):
+def test_descriptor_fuzz_vs_oracle(torch, fuzz_ctxs, fuzz_keys, variant, seed, small):
     """small: QGCM_SMALL_WORKLIST -- batches of up to 4096 packets build their worklist in one workgroup
     ("1", the default) or through the multi-launch radix-sort path ("0"); larger batches always take
     the latter."""
     from quantum_amd import batch
 
-    monkeypatch.setenv("QGCM_SMALL_WORKLIST", small)
-
-    ctx = fuzz_ctxs[variant]
+    ctx = fuzz_ctxs[(variant, small)]
     rng, n, kidx, lens, offs, slot, size, aad_len, valid = draw_case(seed)
     plain = np.frombuffer(rng.bytes(size), dtype=np.uint8).copy()
     nonces = np.frombuffer(rng.bytes(12 * n), dtype=np.uint8).copy()
@@ -163,7 +165,7 @@ def test_descriptor_batch_4m_packets(torch, fuzz_ctxs, fuzz_keys):
     authenticate and the sampled payloads must be back to their plaintext."""
     from quantum_amd import batch
 
-    ctx = fuzz_ctxs["default"]
+    ctx = fuzz_ctxs[("default", "1")]
     n = 1 << 22
     rng = np.random.default_rng(0xF0224000)
     kidx = rng.integers(0, 64, size=n).astype(np.uint32)
@@ -198,3 +200,40 @@ def test_descriptor_batch_4m_packets(torch, fuzz_ctxs, fuzz_keys):
         assert np.array_equal(got, plain[i][:4 + L])
     del arena, nonces, status
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("small", ["1", "0"])
+@pytest.mark.parametrize("n", [752, 753, 760, 767, 768, 769])
+def test_single_key_run_threshold(torch, fuzz_ctxs, fuzz_keys, n, small):
+    """A key becomes a segmented-kernel run at kSegMinTiles = 48 tiles, i.e. 753 packets (ceil(n / 16)
+    = 48).  Batches of 753..767 packets of ONE key are a run, so the segmented kernel must launch for
+    them (it was skipped below 768 packets, leaving the key's packets unsealed with status 0).  Both
+    worklist builds (one workgroup, small = "1"; multi-launch radix sort, "0"); 4-B-aligned packed slots
+    so the one-workgroup-per-packet path does not take them; seal against the oracle, open back."""
+    from quantum_amd import batch
+
+    ctx = fuzz_ctxs[("default", small)]
+    rng = np.random.default_rng(0xF0230000 + n)
+    kidx = np.full(n, 17, dtype=np.uint32)
+    lens = rng.integers(0, 1500, size=n).astype(np.uint32)
+    slot = (4 + lens.astype(np.int64) + 28 + 3) & ~3
+    offs = np.zeros(n, dtype=np.uint64)
+    offs[1:] = np.cumsum(slot)[:-1].astype(np.uint64)
+    offs += 4  # 4 mod 16: never the one-workgroup-per-packet path
+    size = int(offs[-1]) + int(slot[-1]) + 64
+    plain = np.frombuffer(rng.bytes(size), dtype=np.uint8).copy()
+    nonces = np.frombuffer(rng.bytes(12 * n), dtype=np.uint8).copy()
+    ref = plain.copy()
+    O.aesgo_seal_descs(fuzz_keys, ref, offs, lens, kidx, nonces, 4, 8)
+    arena = torch.from_numpy(plain.copy()).cuda()
+    status = torch.full((n,), 0x5A, dtype=torch.uint8, device="cuda")
+    batch.seal_batch(ctx, arena, batch.make_descs(offs, lens, kidx, "cuda"), n, torch.from_numpy(nonces).cuda(),
+                     aad_len=4, status=status)
+    assert bool((status == 1).all()), f"{int((status != 1).sum())} packets unsealed"
+    assert np.array_equal(arena.cpu().numpy(), ref)
+    batch.open_batch(ctx, arena, batch.make_descs(offs, lens + 28, kidx, "cuda"), n, aad_len=4, status=status)
+    assert bool((status == 1).all())
+    got = arena.cpu().numpy()
+    for i in range(n):
+        o, L = int(offs[i]), int(lens[i])
+        assert np.array_equal(got[o:o + 4 + L], plain[o:o + 4 + L]), i

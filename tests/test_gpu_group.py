@@ -457,6 +457,55 @@ def test_group_interleaved_members_seal_in_place(torch, G, direct, pinned_nonces
         grp.close()
 
 
+@pytest.mark.parametrize("G", [2, 3])
+def test_group_mixed_alignment_members_never_overwrite(torch, G):
+    """the direct (in place) path writes each record's 16-B-rounded area back, so a record
+    of ANOTHER member that starts inside that rounded tail (4-B packed, right behind the record) would
+    get stale bytes written over its result while both members run at once.  Records are interleaved
+    over the members in one pinned arena, packed at 4-B alignment so every record starts in the
+    previous one's rounded tail; a few of them 16-B aligned.  No member may go direct, and sealed and
+    opened bytes must equal the oracle over the whole arena, several rounds (the race was timing-bound)."""
+    from quantum_amd import shard
+
+    grp = shard.Group([0] * G, max_keys=64)
+    try:
+        rng = np.random.default_rng(0x6A30 + G)
+        nkeys = 24
+        keys = rng.integers(0, 256, 32 * nkeys, dtype=np.uint8).tobytes()
+        grp.set_keys(0, keys)
+        n = 1200
+        kidx = rng.integers(0, nkeys, n).astype(np.uint32)
+        assert len(set(shard.key_shard(kidx, G).tolist())) == G
+        lens = rng.integers(0, 1500, n).astype(np.uint32)
+        step = (4 + lens.astype(np.uint64) + 28 + 3) // 4 * 4  # packed: 4-B aligned records
+        step[rng.random(n) < 0.1] += 12  # some records end up 16-B aligned, most not
+        offs = np.concatenate([[0], np.cumsum(step)[:-1]]).astype(np.uint64)
+        assert (offs % 16 == 0).any() and (offs % 16 != 0).any()
+        size = int(offs[-1] + step[-1]) + 16
+        arena, aptr, free = host_buffer(size, True)
+        nonces, nptr, free_n = host_buffer(12 * n, True)
+        try:
+            for rnd in range(4):
+                arena[:] = rng.integers(0, 256, size, dtype=np.uint8)
+                arena[offs.astype(np.int64)[:, None] + np.arange(4)] = np.frombuffer(AAD, np.uint8)
+                nonces[:] = rng.integers(0, 256, 12 * n, dtype=np.uint8)
+                plain, ref = arena.copy(), arena.copy()
+                O.aesgo_seal_descs(keys, ref, offs, lens, kidx, np.ascontiguousarray(nonces), 4, 8)
+                status = np.full(n, 7, np.uint8)
+                assert grp.seal_host(aptr, shard.host_descs(offs, lens, kidx), n, nptr, 4, status.ctypes.data) == 0
+                assert "direct" not in [grp.last_path(m) for m in range(G)]
+                assert bool((status == 1).all()) and np.array_equal(arena, ref), rnd
+                assert grp.open_host(aptr, shard.host_descs(offs, lens + 28, kidx), n, 4, status.ctypes.data) == 0
+                assert "direct" not in [grp.last_path(m) for m in range(G)]
+                assert bool((status == 1).all()) and np.array_equal(arena, plain), rnd
+        finally:
+            del nonces
+            free_n()
+            free()
+    finally:
+        grp.close()
+
+
 def test_group_zerocopy_records_at_the_allocation_end(torch):
     """Zero-copy path: records whose last byte is the last bytes of a one-page pinned allocation, with
     lengths that are not multiples of 4 or 16 (the gather reads whole dwords up to the next 4-B

@@ -181,6 +181,9 @@ for s in $STEPS; do
     pcieaf)  # PCIe copy rates before and after a 90-GB HBM allocation is freed in the same process
       timeout -k 10 300 python3 tools/microbench/pcie.py --after-free 90 > $OUT/pcie_after_free.jsonl 2> $OUT/pcie_af.err
       check pcieaf $? ;;
+    pcieaftrace)  # the after-free rows under the copy tracer: r4_s9 crashed in __cxa_finalize at exit here (pcie.py teardown)
+      timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $OUT/trace_pcieaf -o t -- python3 tools/microbench/pcie.py --after-free 90 > $OUT/trace_pcieaf.log 2>&1
+      check pcieaftrace $? ;;
     e2ebig)  # qgcm_seal_host past its 4-GiB staging ring (slots rotate) vs within it
       timeout -k 10 400 python3 tools/exp_host_legs.py e2e e2e_big > $OUT/e2e_big.jsonl 2> $OUT/e2e_big.err
       check e2ebig $? ;;

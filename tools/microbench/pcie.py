@@ -64,12 +64,33 @@ def after_free(gb: float) -> None:
                           **rate(64 << 20, True, True)}), flush=True)
 
 
+def teardown() -> None:
+    """Release every device and pinned-host block torch still caches BEFORE the interpreter exits.
+
+    Under `rocprofv3 --memory-copy-trace` (profiles/r4_s9: SIGSEGV, rc 139, in __cxa_finalize after
+    every row had printed) the pinned buffers of rate() -- returned to torch's caching host allocator,
+    not freed -- were released by that allocator's static destructor at exit, i.e. a hipHostFree issued
+    from __cxa_finalize after the profiler's tool library had already been finalized by its own exit
+    handler: the intercepted HIP call jumps into torn-down tracing state.  Freeing the caches here, while
+    the runtime and the profiler are both alive, leaves no HIP call for exit time (tools/README.md)."""
+    import gc
+
+    torch.cuda.synchronize()
+    gc.collect()  # the rate() buffers and streams
+    torch.cuda.empty_cache()
+    host_empty = getattr(torch._C, "_host_emptyCache", None)
+    if host_empty is not None:
+        host_empty()  # the caching host (pinned) allocator's free blocks -> hipHostFree now
+    torch.cuda.synchronize()
+
+
 if __name__ == "__main__":
     import sys
     if len(sys.argv) > 2 and sys.argv[1] == "--after-free":
         for h2d, d2h in ((True, False), (False, True), (True, True)):
             print(json.dumps({"after_free_GB": 0, **rate(64 << 20, h2d, d2h)}), flush=True)
         after_free(float(sys.argv[2]))
+        teardown()
         sys.exit(0)
     for chunk in (8 << 20, 32 << 20, 128 << 20):
         for h2d, d2h in ((True, False), (False, True), (True, True)):
@@ -85,3 +106,4 @@ if __name__ == "__main__":
     for mis in (4, 64, 256):
         for h2d, d2h in ((True, False), (False, True), (True, True)):
             print(json.dumps(rate(64 << 20, h2d, d2h, mis=mis)), flush=True)
+    teardown()
