@@ -2,16 +2,31 @@
 
 // +build gpu
 
-// gpu_aes.go -- the MI355X drop-in for quantum's crypto.AES (crypto/aes.go), over libqgcm's C ABI
-// (include/qgcm.h).  A maintainer copies this file into quantum's crypto/ directory and builds with
-// `go build -tags gpu`; without the tag the package builds exactly as before.  The cgo preamble,
-// the prebuilt-library LDFLAGS and the "NULL plus a 120-byte error string" convention follow
+// aes_gpu.go -- the MI355X drop-in for quantum's crypto.AES (crypto/aes.go), over libqgcm's C ABI
+// (include/qgcm.h).  A maintainer copies this file into quantum's crypto/ directory, adds the line
+// `// +build !gpu` to crypto/aes.go, and builds with `go build -tags gpu`.  Nothing else changes:
+// this file defines the same package-level names crypto/aes.go does -- SaltLength, type AES with
+// EncryptedSize / DecryptedSize / Encrypt / Decrypt, and NewAES(secret, salt) (*AES, error) with the
+// signatures of crypto/aes.go:15-83 -- so common.Mapping.AES (*crypto.AES, common/mapping.go:54),
+// ParseMapping (common/mapping.go:90-99) and plugin.Encryption.Apply (plugin/encryption.go:16-40)
+// compile and run unchanged, and crypto_test.go's own TestAES / BenchmarkAES (crypto/crypto_test.go:54-131)
+// exercise the GPU path.  Without the tag the package builds exactly as before.  The cgo preamble, the
+// prebuilt-library LDFLAGS and the "NULL plus a 120-byte error string" convention follow
 // crypto/dtls.go:6-40, the reference's own cgo layer.
 //
-// GPUAES has crypto.AES's method set -- EncryptedSize, DecryptedSize, Encrypt, Decrypt
-// (crypto/aes.go:29-62) -- with the same sizes, buffer layout (ct || tag || nonce, in place) and errors,
-// so plugin/encryption.go:16-40 calls it unchanged once common.Mapping.AES (common/mapping.go:54) is
-// typed by that method set (INTEGRATION.md s1).  Differences, all where the reference would panic:
+// Device state is process-wide, created by the first NewAES (quantum is one process per node,
+// main.go:29-114, and every Mapping's AES of that process shares it):
+//   - QGCM_DEVICES: the GPUs to use, e.g. "0,1,2,3,4,5,6,7" (default: every device the process sees);
+//   - QGCM_MAX_PEERS: key slots (default 4096; a slot is recycled when its AES is garbage-collected).
+// The set is a qgcm_group of one member context per device (one member on a 1-GPU box); NewAES installs
+// a peer's key on member hash(key slot) mod G only, where that peer's Encrypt / Decrypt calls then run
+// (SURVEY.md s8e: packets are independent, no GPU-to-GPU traffic).
+//
+// Encrypt / Decrypt are one packet per call (worker/outgoing.go:83-93 calls Apply per packet), served
+// by libqgcm's resident kernel with no launch per call.  Batched workers use the extra API below
+// (Devices, GPUGroup.Order / SealBatch / OpenBatch, Arena, Desc; INTEGRATION.md s2).
+//
+// Differences from crypto/aes.go, all where the reference would panic:
 //   - Encrypt with length < 0 or len(data) < length + 28 returns (-1, errShortBuffer);
 //   - Decrypt of fewer than 28 bytes returns errOpen (the reference panics below 12 bytes,
 //     crypto/aes.go:58-59, and returns errOpen from 12 to 27);
@@ -31,8 +46,18 @@ import "C"
 import (
 	"errors"
 	"fmt"
+	"os"
+	"runtime"
+	"strconv"
+	"strings"
 	"sync"
 	"unsafe"
+)
+
+const (
+	// SaltLength is the length that the passed in salt slice should be for AES objects (crypto/aes.go:16-17).
+	SaltLength = 32
+	iterations = C.QGCM_PBKDF2_ITERS // crypto/aes.go:18, applied by qgcm_derive_key
 )
 
 var (
@@ -40,7 +65,7 @@ var (
 	errOpen        = errors.New("cipher: message authentication failed")
 	errShortBuffer = errors.New("qgcm: data buffer shorter than length + 28")
 	errAdditional  = errors.New("qgcm: additional data longer than 4 bytes")
-	errSlots       = errors.New("qgcm: out of key slots")
+	errSlots       = errors.New("qgcm: out of key slots (QGCM_MAX_PEERS)")
 	errBatch       = errors.New("qgcm: batch record outside the arena, or status shorter than the batch")
 )
 
@@ -57,124 +82,148 @@ func bytePtr(b []byte) *C.uint8_t {
 // cError turns a C error buffer into a Go error (crypto/dtls.go:37-40).
 func cError(buf *C.char) error { return errors.New(C.GoString(buf)) }
 
-// GPUContext owns one MI355X device's key tables (qgcm_ctx): the device-side state of every
-// crypto.AES object of the process.
-type GPUContext struct {
-	ctx  *C.qgcm_ctx
-	mu   sync.Mutex
-	next uint32
-	max  uint32
-}
-
-// NewGPUContext opens device `device` with room for maxKeys peer keys.
-func NewGPUContext(device int, maxKeys uint32) (*GPUContext, error) {
-	buf := (*C.char)(C.malloc(C.QGCM_ERRLEN))
-	defer C.free(unsafe.Pointer(buf))
-	ctx := C.qgcm_create(C.int(device), C.uint32_t(maxKeys), buf, C.QGCM_ERRLEN)
-	if ctx == nil {
-		return nil, cError(buf)
-	}
-	return &GPUContext{ctx: ctx, max: maxKeys}, nil
-}
-
-// Close releases the device context (no call may be in flight).
-func (g *GPUContext) Close() {
-	if g.ctx != nil {
-		C.qgcm_destroy(g.ctx)
-		g.ctx = nil
-	}
-}
-
-// GPUAES is a drop-in for *crypto.AES (crypto/aes.go:22-26): one key slot of a GPUContext.
-type GPUAES struct {
-	g    *GPUContext
-	ctx  *C.qgcm_ctx // the context that holds the key (a group member's, see GPUGroup)
+// AES represents an aes-256-gcm AEAD cipher object (crypto/aes.go:22-26): one key slot of the
+// process's GPU set.  The slot holds the expanded key schedule and GHASH tables on the GPU that owns it.
+type AES struct {
+	g    *GPUGroup
+	ctx  *C.qgcm_ctx // the member context that holds the key
 	idx  uint32
 	salt []byte
 }
 
-// NewGPUAES replaces NewAES (crypto/aes.go:65-83): PBKDF2-HMAC-SHA512(secret, salt, 10000, 32) on
-// the host (qgcm_derive_key), then aes.NewCipher + cipher.NewGCM as a device key schedule and GHASH
-// tables (qgcm_set_key).
-func (g *GPUContext) NewGPUAES(secret, salt []byte) (*GPUAES, error) {
-	g.mu.Lock()
-	idx := g.next
-	if idx >= g.max {
-		g.mu.Unlock()
-		return nil, errSlots
-	}
-	g.next++
-	g.mu.Unlock()
-	if err := installKey(g.ctx, idx, secret, salt); err != nil {
-		return nil, err
-	}
-	return &GPUAES{g: g, ctx: g.ctx, idx: idx, salt: salt}, nil
-}
+// EncryptedSize returns the minimum size of the data buffer for encryption, which includes the gcm
+// tag size + nonce size (crypto/aes.go:29-31).
+func (crypt *AES) EncryptedSize(data []byte) int { return len(data) + overhead }
 
-func installKey(ctx *C.qgcm_ctx, idx uint32, secret, salt []byte) error {
-	var key [C.QGCM_KEY_BYTES]C.uint8_t
-	if rc := C.qgcm_derive_key(bytePtr(secret), C.size_t(len(secret)), bytePtr(salt), C.size_t(len(salt)),
-		&key[0]); rc != C.QGCM_OK {
-		return errors.New(C.GoString(C.qgcm_strerror(rc)))
-	}
-	if rc := C.qgcm_set_key(ctx, C.uint32_t(idx), &key[0]); rc != C.QGCM_OK {
-		return errors.New(C.GoString(C.qgcm_strerror(rc)))
-	}
-	return nil
-}
+// DecryptedSize returns the size of the data once decrypted (crypto/aes.go:34-36).
+func (crypt *AES) DecryptedSize(data []byte) int { return len(data) - overhead }
 
-// EncryptedSize == crypto/aes.go:29-31.
-func (a *GPUAES) EncryptedSize(data []byte) int { return len(data) + overhead }
-
-// DecryptedSize == crypto/aes.go:34-36.
-func (a *GPUAES) DecryptedSize(data []byte) int { return len(data) - overhead }
-
-// Encrypt == crypto/aes.go:41-52: seals data[:length] in place, then the 16-byte tag and the 12-byte
-// nonce (drawn by libqgcm from getrandom(2), crypto/rand's source); returns length + 28.
-func (a *GPUAES) Encrypt(data []byte, length int, additional []byte) (int, error) {
+// Encrypt takes the data buffer and encrypts up to length bytes in place, while injecting the nonce and
+// gcm tag at the end and signing the additional data (crypto/aes.go:41-52): data[:length] becomes the
+// ciphertext, then the 16-byte tag and the 12-byte nonce (drawn by libqgcm from getrandom(2),
+// crypto/rand's source); returns length + 28.
+//
+// additional may be nil.
+func (crypt *AES) Encrypt(data []byte, length int, additional []byte) (int, error) {
 	if length < 0 || length+overhead > len(data) {
 		return -1, errShortBuffer
 	}
 	if len(additional) > 4 {
 		return -1, errAdditional
 	}
-	// one packet per call, served by libqgcm's resident kernel (no launch per call)
-	n := C.qgcm_seal_one(a.ctx, C.uint32_t(a.idx), bytePtr(data), C.long(length), bytePtr(additional),
+	n := C.qgcm_seal_one(crypt.ctx, C.uint32_t(crypt.idx), bytePtr(data), C.long(length), bytePtr(additional),
 		C.uint32_t(len(additional)), nil)
+	runtime.KeepAlive(crypt) // the slot is not recycled while a call on it runs
 	if n < 0 {
 		return -1, errors.New("qgcm: seal failed")
 	}
 	return int(n), nil
 }
 
-// Decrypt == crypto/aes.go:57-62: opens data in place (nonce = the last 12 bytes, tag the 16 before);
-// returns len(data) - 28.  On a tag mismatch the plaintext region is zeroed, as Go 1.9's gcm Open does.
-func (a *GPUAES) Decrypt(data []byte, additional []byte) (int, error) {
+// Decrypt takes the data buffer and decrypts it and verifies the additional data (crypto/aes.go:57-62):
+// the nonce is the last 12 bytes, the tag the 16 before; returns len(data) - 28.  On a tag mismatch the
+// plaintext region is zeroed, as Go 1.9's gcm Open does, and errOpen is returned.
+//
+// additional and data must be the same buffers passed to Encrypt.
+func (crypt *AES) Decrypt(data []byte, additional []byte) (int, error) {
 	if len(data) < overhead || len(additional) > 4 {
-		return a.DecryptedSize(data), errOpen
+		return crypt.DecryptedSize(data), errOpen
 	}
-	n := C.qgcm_open_one(a.ctx, C.uint32_t(a.idx), bytePtr(data), C.long(len(data)), bytePtr(additional),
+	n := C.qgcm_open_one(crypt.ctx, C.uint32_t(crypt.idx), bytePtr(data), C.long(len(data)), bytePtr(additional),
 		C.uint32_t(len(additional)))
+	runtime.KeepAlive(crypt)
 	if n < 0 {
-		return a.DecryptedSize(data), errOpen
+		return crypt.DecryptedSize(data), errOpen
 	}
 	return int(n), nil
 }
 
+// KeyIndex is this peer's key slot: the Key field of its packets' Descs in a batch (extra API).  Keep
+// the AES reachable while batches name its slot: the slot is recycled once the AES is collected.
+func (crypt *AES) KeyIndex() uint32 { return crypt.idx }
+
+// Member is the index of the group member (GPU) that holds this peer's key and serves its calls.
+func (crypt *AES) Member() int { return int(C.qgcm_group_shard(crypt.g.grp, C.uint32_t(crypt.idx))) }
+
+// NewAES returns a new AEAD based cipher object based on the passed in secret and salt
+// (crypto/aes.go:65-83): PBKDF2-HMAC-SHA512(secret, salt, 10000, 32) on the host (qgcm_derive_key),
+// then aes.NewCipher + cipher.NewGCM as a device key schedule and GHASH tables (qgcm_set_key) on the GPU
+// that owns the new key slot.  The first call creates the process's device set (Devices).
+func NewAES(secret, salt []byte) (*AES, error) {
+	gg, err := Devices()
+	if err != nil {
+		return nil, err
+	}
+	return gg.NewAES(secret, salt)
+}
+
+var process struct {
+	once sync.Once
+	g    *GPUGroup
+	err  error
+}
+
+// Devices returns the process-wide GPU set every NewAES installs its key in, created on first use
+// from QGCM_DEVICES and QGCM_MAX_PEERS (see the file comment).  Batched workers seal and open through it.
+func Devices() (*GPUGroup, error) {
+	process.once.Do(func() {
+		devs, err := deviceList(os.Getenv("QGCM_DEVICES"), int(C.qgcm_device_count()))
+		if err != nil {
+			process.err = err
+			return
+		}
+		peers := uint32(4096)
+		if v := os.Getenv("QGCM_MAX_PEERS"); v != "" {
+			p, err := strconv.ParseUint(v, 10, 32)
+			if err != nil || p == 0 || p > uint64(C.QGCM_MAX_KEYS) {
+				process.err = fmt.Errorf("qgcm: QGCM_MAX_PEERS=%q", v)
+				return
+			}
+			peers = uint32(p)
+		}
+		process.g, process.err = NewGPUGroup(devs, peers)
+	})
+	return process.g, process.err
+}
+
+// deviceList parses QGCM_DEVICES ("0,1,2,3"; empty: devices 0..visible-1).
+func deviceList(spec string, visible int) ([]int, error) {
+	if strings.TrimSpace(spec) == "" {
+		if visible < 1 {
+			return nil, errors.New("qgcm: no HIP device visible")
+		}
+		out := make([]int, visible)
+		for i := range out {
+			out[i] = i
+		}
+		return out, nil
+	}
+	var out []int
+	for _, f := range strings.Split(spec, ",") {
+		d, err := strconv.Atoi(strings.TrimSpace(f))
+		if err != nil || d < 0 {
+			return nil, fmt.Errorf("qgcm: QGCM_DEVICES=%q", spec)
+		}
+		out = append(out, d)
+	}
+	return out, nil
+}
+
 // GPUGroup drives every GPU of a node from quantum's one process (qgcm_group_*): a peer's key lives on
-// GPU hash(key index) mod G, and that peer's per-packet calls go to that GPU (SURVEY.md s8e).
+// GPU hash(key slot) mod G, and that peer's per-packet calls go to that GPU (SURVEY.md s8e).
 type GPUGroup struct {
 	grp  *C.qgcm_group
 	mu   sync.Mutex
 	next uint32
 	max  uint32
+	free []uint32 // key slots of garbage-collected AES objects, reused first
 
 	bmu    sync.Mutex     // one batch at a time (qgcm_group_seal_host serializes calls anyway)
 	nonces unsafe.Pointer // pinned nonce buffer of the last SealBatch (qgcm_host_alloc), 12 B per packet
 	ncap   int
 }
 
-// NewGPUGroup opens one context per device in `devices`.
+// NewGPUGroup opens one context per device in `devices` (a device may repeat).
 func NewGPUGroup(devices []int, maxKeys uint32) (*GPUGroup, error) {
 	if len(devices) == 0 {
 		return nil, errors.New("qgcm: no devices")
@@ -192,29 +241,62 @@ func NewGPUGroup(devices []int, maxKeys uint32) (*GPUGroup, error) {
 	return &GPUGroup{grp: grp, max: maxKeys}, nil
 }
 
-// NewGPUAES derives the key and installs it on its owning GPU only; the returned object seals and
-// opens there.
-func (gg *GPUGroup) NewGPUAES(secret, salt []byte) (*GPUAES, error) {
+// NewAES derives the key (crypto/aes.go:66) and installs it on the GPU that owns the next free key
+// slot only; the returned object seals and opens there.  quantum's datastore watch calls ParseMapping,
+// and with it NewAES, again on every mapping update (datastore/etcdv2.go:236-276), so a slot whose AES
+// has become unreachable is returned to the group by a finalizer and reused.
+func (gg *GPUGroup) NewAES(secret, salt []byte) (*AES, error) {
 	gg.mu.Lock()
-	idx := gg.next
-	if idx >= gg.max {
+	var idx uint32
+	switch {
+	case len(gg.free) > 0:
+		idx = gg.free[len(gg.free)-1]
+		gg.free = gg.free[:len(gg.free)-1]
+	case gg.next < gg.max:
+		idx = gg.next
+		gg.next++
+	default:
 		gg.mu.Unlock()
 		return nil, errSlots
 	}
-	gg.next++
 	gg.mu.Unlock()
 	owner := C.qgcm_group_shard(gg.grp, C.uint32_t(idx))
 	ctx := C.qgcm_group_ctx(gg.grp, owner)
 	if ctx == nil {
+		gg.release(idx)
 		return nil, errors.New("qgcm: no owner context")
 	}
 	if err := installKey(ctx, idx, secret, salt); err != nil {
+		gg.release(idx)
 		return nil, err
 	}
-	return &GPUAES{ctx: ctx, idx: idx, salt: salt}, nil
+	a := &AES{g: gg, ctx: ctx, idx: idx, salt: salt}
+	runtime.SetFinalizer(a, func(a *AES) { a.g.release(a.idx) })
+	return a, nil
 }
 
-// Close releases every member context.
+func (gg *GPUGroup) release(idx uint32) {
+	gg.mu.Lock()
+	gg.free = append(gg.free, idx)
+	gg.mu.Unlock()
+}
+
+func installKey(ctx *C.qgcm_ctx, idx uint32, secret, salt []byte) error {
+	var key [C.QGCM_KEY_BYTES]C.uint8_t
+	if rc := C.qgcm_derive_key(bytePtr(secret), C.size_t(len(secret)), bytePtr(salt), C.size_t(len(salt)),
+		&key[0]); rc != C.QGCM_OK {
+		return errors.New(C.GoString(C.qgcm_strerror(rc)))
+	}
+	if rc := C.qgcm_set_key(ctx, C.uint32_t(idx), &key[0]); rc != C.QGCM_OK {
+		return errors.New(C.GoString(C.qgcm_strerror(rc)))
+	}
+	return nil
+}
+
+// Size is the number of members (one context per listed device).
+func (gg *GPUGroup) Size() int { return int(C.qgcm_group_size(gg.grp)) }
+
+// Close releases every member context (no call may be in flight; the process-wide set is never closed).
 func (gg *GPUGroup) Close() {
 	if gg.grp != nil {
 		C.qgcm_group_destroy(gg.grp)
@@ -231,11 +313,8 @@ func (gg *GPUGroup) Close() {
 // seals or opens the whole batch with one call instead of one Encrypt / Decrypt per packet
 // (worker/outgoing.go:55-93, worker/incoming.go:54-92 loop over packets).  Laid out in Order's order,
 // each GPU's packets are adjacent and move by DMA (qgcm_group_last_path 2); a worker-sized batch (up to
-// 65536 packets and 128 MiB) whose slots start 16-B aligned, e.g. the 1472-B MaxPacketLength
+// 65536 packets and 128 MiB) whose slots all start 16-B aligned, e.g. the 1472-B MaxPacketLength
 // stride, is sealed in place in the arena instead (qgcm_group_last_path 3).
-
-// KeyIndex is the key slot of this peer: the Key field of its packets' Descs.
-func (a *GPUAES) KeyIndex() uint32 { return a.idx }
 
 // Arena is pinned host memory for a batch of Payload.Raw slots (qgcm_host_alloc), copied by DMA in
 // place.  Bytes aliases it until Free.
@@ -266,7 +345,7 @@ func (a *Arena) Free() {
 
 // Desc is one packet of a batch, laid out as qgcm_desc: the offset of its Payload.Raw slot in the
 // arena, its length (SealBatch: the payload length L; OpenBatch: the sealed length L+28) and its
-// peer's key slot (KeyIndex).  The slot is [4-B AAD (the IP header, Payload.Raw[0:4])][packet] with
+// peer's key slot (AES.KeyIndex).  The slot is [4-B AAD (the IP header, Payload.Raw[0:4])][packet] with
 // room for the 28-B tag and nonce after a payload to be sealed.
 type Desc struct {
 	Offset uint64

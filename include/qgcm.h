@@ -78,6 +78,9 @@ qgcm_ctx *qgcm_create(int device, uint32_t max_keys, char *err, int errlen);
 void qgcm_destroy(qgcm_ctx *ctx);
 const char *qgcm_strerror(int code);
 const char *qgcm_version(void);
+/* HIP devices this process sees (0 when there are none or the runtime fails).  The Go drop-in's
+ * process-wide device set (go/crypto/aes_gpu.go, QGCM_DEVICES unset) is every one of them. */
+int qgcm_device_count(void);
 
 /* ---- key setup: crypto/aes.go:65-83 NewAES, common/mapping.go:90-99 ---- */
 /* key = PBKDF2-HMAC-SHA512(secret, salt, 10000, 32)  (crypto/aes.go:66) -- host */

@@ -19,11 +19,14 @@
 // syscall (what libqgcm's per-packet path does), to separate the kernel's RNG from the cipher when
 // threads do not scale.  Prints one JSON line: packets sealed and opened per second, GiB/s (each
 // payload byte counted once sealed and once opened), the process's user / system CPU seconds over the
-// timed part, and whether every payload came back intact.
+// timed part, and whether every payload came back intact.  QGCM_CHAIN_CPUS="a,b,c": thread t runs
+// pinned on the t-th listed CPU (mod the list), e.g. one CPU per physical core (bench.py's sweep).
 #include <openssl/evp.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <pthread.h>
+#include <sched.h>
 #include <sys/random.h>
 #include <sys/resource.h>
 
@@ -117,6 +120,13 @@ int main(int argc, char **argv) {
     const int L = argc > 3 ? atoi(argv[3]) : 1350;
     const double seconds = argc > 4 ? atof(argv[4]) : 2.0;
     g_buffered = argc > 5 && !strcmp(argv[5], "buffered");
+    std::vector<int> pin;
+    if (const char *cl = getenv("QGCM_CHAIN_CPUS"))
+        for (const char *p = cl; *p;) {
+            pin.push_back(atoi(p));
+            while (*p && *p != ',') ++p;
+            if (*p == ',') ++p;
+        }
     if (threads < 1 || payloads < 1 || L < 0 || L + 4 + 28 > common::MaxPacketLength) return 2;
     uint8_t key[32];
     const char *secret = "AES256Key-32Characters1234567890";
@@ -130,6 +140,12 @@ int main(int argc, char **argv) {
     std::vector<std::thread> ths;
     for (int t = 0; t < threads; ++t) {
         ths.emplace_back([&, t] {
+            if (!pin.empty()) {
+                cpu_set_t one;
+                CPU_ZERO(&one);
+                CPU_SET(pin[t % pin.size()], &one);
+                pthread_setaffinity_np(pthread_self(), sizeof one, &one);
+            }
             // one Encryption and one Mock plugin per worker, sorted as main.go:50-51 does
             auto enc = plugin::New(plugin::EncryptionPlugin).first;
             auto mock = plugin::New(plugin::MockPlugin).first;
@@ -187,9 +203,9 @@ int main(int argc, char **argv) {
     const double us = cpu_seconds(false) - u0, ss = cpu_seconds(true) - s0;
     const double pps = done.load() / dt;
     printf("{\"threads\": %d, \"payloads_per_thread\": %d, \"payload_len\": %d, \"nonces\": \"%s\", "
-           "\"seconds\": %.3f, \"packets_per_s\": %.0f, \"GiB_s\": %.4f, \"user_s\": %.3f, \"sys_s\": %.3f, "
+           "\"pinned\": %s, \"seconds\": %.3f, \"packets_per_s\": %.0f, \"GiB_s\": %.4f, \"user_s\": %.3f, \"sys_s\": %.3f, "
            "\"cpus_busy\": %.2f, \"intact\": %s}\n",
-           threads, payloads, L, g_buffered ? "buffered" : "syscall", dt, pps, 2.0 * pps * L / (1 << 30), us, ss,
+           threads, payloads, L, g_buffered ? "buffered" : "syscall", pin.empty() ? "false" : "true", dt, pps, 2.0 * pps * L / (1 << 30), us, ss,
            (us + ss) / dt, bad.load() ? "false" : "true");
     return bad.load() ? 1 : 0;
 }

@@ -17,7 +17,7 @@ if os.environ.get("QGCM_AB_LIB"):
 
 # Every symbol include/qgcm.h declares (checked by tests/test_abi.py).
 EXPORTS = (
-    "qgcm_create", "qgcm_destroy", "qgcm_strerror", "qgcm_version",
+    "qgcm_create", "qgcm_destroy", "qgcm_strerror", "qgcm_version", "qgcm_device_count",
     "qgcm_derive_key", "qgcm_derive_keys", "qgcm_set_key", "qgcm_set_keys",
     "qgcm_x25519_base", "qgcm_x25519",
     "qgcm_seal_batch", "qgcm_open_batch", "qgcm_seal_uniform", "qgcm_open_uniform",
@@ -68,6 +68,8 @@ def _bind(L: C.CDLL) -> None:
     L.qgcm_strerror.argtypes = [i32]
     L.qgcm_strerror.restype = C.c_char_p
     L.qgcm_version.restype = C.c_char_p
+    L.qgcm_device_count.argtypes = []
+    L.qgcm_device_count.restype = i32
     L.qgcm_derive_key.argtypes = [u8p, sz, u8p, sz, u8p]
     L.qgcm_derive_keys.argtypes = [u8p, u8p, u32, u8p]
     L.qgcm_set_key.argtypes = [vp, u32, u8p]

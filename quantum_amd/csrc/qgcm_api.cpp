@@ -506,6 +506,15 @@ extern "C" {
 
 const char *qgcm_version(void) { return "qgcm 0.1.0 (gfx950)"; }
 
+int qgcm_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return n;
+}
+
 const char *qgcm_strerror(int code) {
     switch (code) {
         case QGCM_OK: return "ok";

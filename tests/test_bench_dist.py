@@ -103,3 +103,29 @@ def test_bench_gpus_flag_spawns_ranks():
     assert len(lines) == 1, out.stdout
     line = json.loads(lines[0])
     assert line["n_gpus"] == 2 and line["status_ok"] is True and line["config"]["packets_per_gpu"] == 65536
+
+
+def test_bench_eight_ranks_one_device():
+    """The driver's N = 8 launch rehearsed on one GPU: eight ranks (torch.distributed.run
+    --nproc-per-node 8, the driver's command with --one-device --dist-backend gloo) each seal and open
+    their own 2^18-packet shard; barrier + max-over-ranks timing, per-GPU figures from all eight ranks,
+    one JSON line from rank 0 (main.go:72-75: quantum's independent workers; here one rank per GPU)."""
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=8",
+           "--master-addr", "127.0.0.1", "--master-port", "29536", os.path.join(ROOT, "bench.py"),
+           "--gpus", "8", "--steps", "3", "--warmup", "1", "--packets", "262144", "--settle-ms", "0",
+           "--dist-backend", "gloo", "--one-device"]
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 8 and line["status_ok"] is True and line["scaling"] == "weak"
+    assert line["config"]["packets_per_gpu"] == 262144 and line["config"]["packets_total"] == 8 * 262144
+    per = line["per_gpu"]
+    assert [g["rank"] for g in per] == list(range(8)) and all(g["packets"] == 262144 and g["GiB_s"] > 0 for g in per)
+    assert line["value"] > 0 and line["dist_backend"] == "gloo"

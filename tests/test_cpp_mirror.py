@@ -38,7 +38,8 @@ GO_BIN = os.path.join(ROOT, "tests", "cpp", "go_replay")
 
 
 def run_go(names, timeout=120):
-    """tests/cpp/go_replay.c: the C calls go/crypto/gpu_aes.go makes under go/crypto/gpu_aes_test.go."""
+    """tests/cpp/go_replay.c: the C calls go/crypto/aes_gpu.go makes under crypto_test.go's TestAES and
+    go/crypto/aes_gpu_test.go."""
     if not os.path.exists(GO_BIN):
         pytest.fail(f"{GO_BIN} is missing: build it with __graft_entry__.build()")
     r = subprocess.run([GO_BIN, *names], capture_output=True, text=True, timeout=timeout)
@@ -54,4 +55,5 @@ def test_go_shim_replay_cpu():
 
 @pytest.mark.gpu
 def test_go_shim_replay_gpu():
-    run_go(["TestGPUAES", "TestGPUAESEdges", "TestGPUAESConcurrent", "TestGPUGroup", "TestGPUGroupBatch"])
+    run_go(["TestAES", "TestAESEdges", "TestAESConcurrentGoroutines", "TestNewAESAcrossMembers", "TestSlotsRecycled",
+            "TestGPUGroupBatch"])

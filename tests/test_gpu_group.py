@@ -497,7 +497,13 @@ def test_group_mixed_alignment_members_never_overwrite(torch, G):
                 assert bool((status == 1).all()) and np.array_equal(arena, ref), rnd
                 assert grp.open_host(aptr, shard.host_descs(offs, lens + 28, kidx), n, 4, status.ctypes.data) == 0
                 assert "direct" not in [grp.last_path(m) for m in range(G)]
-                assert bool((status == 1).all()) and np.array_equal(arena, plain), rnd
+                # opened: the plaintext back, each slot's tag || nonce left as sealed (Open never writes them)
+                want = ref.copy()
+                pay = np.zeros(size, bool)
+                for o, L in zip(offs.astype(np.int64), lens.astype(np.int64)):
+                    pay[o + 4:o + 4 + L] = True
+                want[pay] = plain[pay]
+                assert bool((status == 1).all()) and np.array_equal(arena, want), rnd
         finally:
             del nonces
             free_n()
@@ -618,3 +624,63 @@ def test_config4_one_gpu_shard(torch, batch_digests):
     del arena, ref, a2, r2, nonces
     ctx.close()
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("layout", ["ordered", "interleaved"])
+def test_group_eight_members_vs_oracle(torch, layout):
+    """G = 8, the node's GPU count (all members on device 0 here): a keyed batch of 40 000 packets of 96
+    peers.  "ordered": laid out member by member (qgcm_group_order), so every member moves its packets
+    by DMA runs; "interleaved": input order, 4-B-packed records, so members gather their shares (zero-copy
+    path).  Keys installed on their owners only; sealed against the oracle over the whole arena, then
+    opened back (a tampered packet per member fails with its plaintext zeroed)."""
+    from quantum_amd import shard
+
+    G, n, nkeys = 8, 40000, 96
+    grp = shard.Group([0] * G, max_keys=128)
+    try:
+        rng = np.random.default_rng(0x6A80 + (layout == "ordered"))
+        keys = rng.integers(0, 256, 32 * nkeys, dtype=np.uint8).tobytes()
+        grp.set_keys(0, keys)
+        kidx = rng.integers(0, nkeys, n).astype(np.uint32)
+        assert len(set(shard.key_shard(kidx, G).tolist())) == G
+        if layout == "ordered":
+            order, counts = grp.order(kidx)
+            kidx = kidx[order]
+            assert int(counts.sum()) == n and (counts > 0).all()
+        lens = rng.integers(0, 1500, n).astype(np.uint32)
+        step = (4 + lens.astype(np.uint64) + 28 + 3) // 4 * 4
+        offs = np.concatenate([[0], np.cumsum(step)[:-1]]).astype(np.uint64)
+        size = int(offs[-1] + step[-1]) + 64
+        arena, aptr, free = host_buffer(size, True)
+        nonces, nptr, free_n = host_buffer(12 * n, True)
+        try:
+            arena[:] = rng.integers(0, 256, size, dtype=np.uint8)
+            arena[offs.astype(np.int64)[:, None] + np.arange(4)] = np.frombuffer(AAD, np.uint8)
+            nonces[:] = rng.integers(0, 256, 12 * n, dtype=np.uint8)
+            plain, ref = arena.copy(), arena.copy()
+            O.aesgo_seal_descs(keys, ref, offs, lens, kidx, np.ascontiguousarray(nonces), 4, 8)
+            status = np.full(n, 7, np.uint8)
+            assert grp.seal_host(aptr, shard.host_descs(offs, lens, kidx), n, nptr, 4, status.ctypes.data) == 0
+            paths = {grp.last_path(m) for m in range(G)}
+            assert paths == ({"dma"} if layout == "ordered" else {"zerocopy"}), paths
+            assert bool((status == 1).all()) and np.array_equal(arena, ref)
+            owner = shard.key_shard(kidx, G)
+            tam = np.array([int(np.nonzero((owner == m) & (lens > 0))[0][0]) for m in range(G)])
+            for i in tam:
+                arena[int(offs[i]) + 4] ^= 0x10
+            assert grp.open_host(aptr, shard.host_descs(offs, lens + 28, kidx), n, 4, status.ctypes.data) == G
+            ok = np.ones(n, bool)
+            ok[tam] = False
+            assert np.array_equal(status, ok.astype(np.uint8))
+            for i in range(n):
+                o, L = int(offs[i]), int(lens[i])
+                if ok[i]:
+                    assert np.array_equal(arena[o:o + 4 + L], plain[o:o + 4 + L]), i
+                else:
+                    assert not arena[o + 4:o + 4 + L].any(), i
+        finally:
+            del nonces
+            free_n()
+            free()
+    finally:
+        grp.close()

@@ -181,6 +181,14 @@ for s in $STEPS; do
     pcieaf)  # PCIe copy rates before and after a 90-GB HBM allocation is freed in the same process
       timeout -k 10 300 python3 tools/microbench/pcie.py --after-free 90 > $OUT/pcie_after_free.jsonl 2> $OUT/pcie_af.err
       check pcieaf $? ;;
+    r5tests)  # the suites round 5 changed
+      timeout -k 10 900 python3 -u -m pytest tests/test_gpu_group.py tests/test_gpu_parity.py tests/test_cpp_mirror.py tests/test_bench_dist.py tests/test_gpu_fuzz.py -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/r5_tests.txt 2>&1
+      check r5tests $? ;;
+    crashmaps)  # the exit-time crash under the copy tracer, short form, with the process's maps for resolve_crash.py
+      PCIE_MAPS=$OUT/maps_${CRASHTAG:-q}.txt timeout -k 10 120 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $OUT/trace_${CRASHTAG:-q} -o t -- python3 tools/microbench/pcie.py --quick ${CRASHARGS:-} > $OUT/trace_${CRASHTAG:-q}.log 2>&1
+      rc=$?
+      python3 tools/resolve_crash.py $OUT/trace_${CRASHTAG:-q}.log $OUT/maps_${CRASHTAG:-q}.txt > $OUT/resolved_${CRASHTAG:-q}.txt 2>&1
+      check crashmaps $rc ;;
     pcieaftrace)  # the after-free rows under the copy tracer: r4_s9 crashed in __cxa_finalize at exit here (pcie.py teardown)
       timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $OUT/trace_pcieaf -o t -- python3 tools/microbench/pcie.py --after-free 90 > $OUT/trace_pcieaf.log 2>&1
       check pcieaftrace $? ;;

@@ -84,8 +84,29 @@ def teardown() -> None:
     torch.cuda.synchronize()
 
 
+def dump_maps_at_exit(path: str) -> None:
+    """Write /proc/self/maps when the interpreter exits (before the C-level finalizers run), so the
+    addresses of an exit-time crash report can be resolved to library + offset (tools/resolve_crash.py)."""
+    import atexit
+
+    def dump():
+        with open(path, "w") as f:
+            f.write(open("/proc/self/maps").read())
+
+    atexit.register(dump)
+
+
 if __name__ == "__main__":
+    import os
     import sys
+    if os.environ.get("PCIE_MAPS"):
+        dump_maps_at_exit(os.environ["PCIE_MAPS"])
+    if len(sys.argv) > 1 and sys.argv[1] == "--quick":  # three rows: the exit-time crash reproduction
+        for h2d, d2h in ((True, False), (False, True), (True, True)):
+            print(json.dumps(rate(64 << 20, h2d, d2h)), flush=True)
+        if "--no-teardown" not in sys.argv:
+            teardown()
+        sys.exit(0)
     if len(sys.argv) > 2 and sys.argv[1] == "--after-free":
         for h2d, d2h in ((True, False), (False, True), (True, True)):
             print(json.dumps({"after_free_GB": 0, **rate(64 << 20, h2d, d2h)}), flush=True)
