@@ -123,14 +123,41 @@ def cgroup_cpu_stat() -> dict:
 SWEEP_THREADS = (1, 2, 4, 8, 12, 15, 16)
 
 
-def core_cpus() -> list[int]:
-    """One CPU per physical core of this process's affinity set (the lowest SMT sibling allowed), in
-    CPU order: the list the pinned sweep points place their threads on."""
+def cpu_busy(sample_s: float = 0.25) -> dict[int, float]:
+    """Busy fraction of every CPU of the host over `sample_s` (/proc/stat), i.e. what the GPU box's
+    other tenants are running right now."""
+    def snap():
+        out = {}
+        for ln in open("/proc/stat"):
+            if ln.startswith("cpu") and ln[3:4].isdigit():
+                f = ln.split()
+                v = [int(x) for x in f[1:]]
+                idle = v[3] + (v[4] if len(v) > 4 else 0)
+                out[int(f[0][3:])] = (sum(v), idle)
+        return out
+    try:
+        a = snap()
+        time.sleep(sample_s)
+        b = snap()
+    except (OSError, ValueError):
+        return {}
+    busy = {}
+    for c, (t1, i1) in b.items():
+        t0, i0 = a.get(c, (t1, i1))
+        dt = t1 - t0
+        busy[c] = 1.0 - (i1 - i0) / dt if dt > 0 else 0.0
+    return busy
+
+
+def core_cpus(busy: dict[int, float] | None = None) -> list[int]:
+    """One CPU per physical core of this process's affinity set (the lowest SMT sibling allowed), the
+    cores whose hardware threads the host's other work uses least first (`busy`, cpu_busy()): the
+    list the pinned sweep points place their threads on."""
     try:
         allowed = sorted(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         return []
-    seen, out = set(), []
+    seen, cores = set(), []
     for c in allowed:
         try:
             sib = open(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list").read().strip()
@@ -138,8 +165,13 @@ def core_cpus() -> list[int]:
             sib = str(c)
         if sib not in seen:
             seen.add(sib)
-            out.append(c)
-    return out
+            sibs = []
+            for part in sib.split(","):
+                lo, _, hi = part.partition("-")
+                sibs.extend(range(int(lo), int(hi or lo) + 1))
+            load = max((busy or {}).get(x, 0.0) for x in sibs)
+            cores.append((round(load, 2), c))
+    return [c for _, c in sorted(cores)]
 
 
 def cpu_baseline(key: bytes, L: int, threads: int, host: dict, seconds: float = 1.0) -> dict:
@@ -160,7 +192,8 @@ def cpu_baseline(key: bytes, L: int, threads: int, host: dict, seconds: float = 
 
     exe = os.path.join(ROOT, "oracle", "_build", "cpu_chain")
 
-    cores = core_cpus()
+    busy = cpu_busy()
+    cores = core_cpus(busy)
 
     def chain(t: int, nonces: str, pinned: bool) -> dict:
         env = dict(os.environ)
@@ -202,6 +235,8 @@ def cpu_baseline(key: bytes, L: int, threads: int, host: dict, seconds: float = 
         kernel = ""
     return {"value": best["GiB_s"], "unit": "GiB/s", "cores": best["threads"], "kind": "port",
             "best_point_pinned": best["pinned"], "physical_cores_allowed": len(cores),
+            "host_cpus_busy_before": {"over_50pct": sum(1 for v in busy.values() if v > 0.5),
+                                      "sum": round(sum(busy.values()), 1), "sampled_s": 0.25},
             "one_core": one["GiB_s"], "nproc": host["nproc"],
             "per_thread_efficiency": round(eff, 3),
             "at_share": {"threads": full["threads"], "GiB_s": full["GiB_s"], "cpus_busy": full["cpus_busy"],
@@ -218,7 +253,8 @@ def cpu_baseline(key: bytes, L: int, threads: int, host: dict, seconds: float = 
                        f"10000 payloads x {L} B per thread looped {seconds} s per point, threads "
                        f"{'/'.join(map(str, counts))} (this job's CPU share of a {host['nproc']}-CPU host: "
                        f"{threads}), each point a fresh child process run before the GPU is initialised, "
-                       f"threads left to the scheduler and pinned one per physical core; "
+                       f"threads left to the scheduler and pinned one per physical core (least-loaded cores "
+                       f"first); "
                        f"C++ mirror of the Go plugins (oracle/cpu_chain.cpp) over OpenSSL EVP aes-256-gcm with "
                        f"crypto/aes.go semantics (getrandom nonce per packet, in place); value = best point "
                        f"({best['threads']} threads, {best['packets_per_s']:.0f} packets/s sealed and opened, "

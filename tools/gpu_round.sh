@@ -189,6 +189,25 @@ for s in $STEPS; do
       rc=$?
       python3 tools/resolve_crash.py $OUT/trace_${CRASHTAG:-q}.log $OUT/maps_${CRASHTAG:-q}.txt > $OUT/resolved_${CRASHTAG:-q}.txt 2>&1
       check crashmaps $rc ;;
+    c3traffic)  # config 3's read excess by form (1024 keys vs one key, packed vs 64-B aligned), separate PMC passes
+      for form in packed packed_onekey aligned aligned_onekey; do
+        i=0
+        for P in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
+          i=$((i+1))
+          timeout -s KILL 120 rocprofv3 --pmc $P -d $OUT/c3t/${form}_p$i -o p --output-format csv -- python3 tools/exp_config3_traffic.py run $form > $OUT/c3t_${form}_p$i.log 2>&1
+          check c3t_${form}_p$i $?
+        done
+      done
+      python3 tools/exp_config3_traffic.py summarize $OUT/c3t > $OUT/c3_traffic.json 2>&1 ;;
+    crashmin)  # exit-time crash under the copy tracer: which minimal script crashes (steps stop at the first crash)
+      for m in ${CRASHMODES:-kernel:kt copy:kt kernel:mc copy_reset:mc copy:mc}; do
+        mode=${m%%:*}; tr=${m##*:}
+        if [ $tr = kt ]; then TRACE="--kernel-trace"; else TRACE="--kernel-trace --memory-copy-trace"; fi
+        timeout -k 10 120 rocprofv3 $TRACE --output-format csv -d $OUT/cm_${mode}_$tr -o t -- python3 tools/microbench/crash_min.py $mode > $OUT/cm_${mode}_$tr.log 2>&1
+        rc=$?
+        ls -R $OUT/cm_${mode}_$tr 2>/dev/null | grep -c csv > $OUT/cm_${mode}_$tr.csvcount
+        check cm_${mode}_$tr $rc
+      done ;;
     pcieaftrace)  # the after-free rows under the copy tracer: r4_s9 crashed in __cxa_finalize at exit here (pcie.py teardown)
       timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $OUT/trace_pcieaf -o t -- python3 tools/microbench/pcie.py --after-free 90 > $OUT/trace_pcieaf.log 2>&1
       check pcieaftrace $? ;;
