@@ -7,7 +7,12 @@
 // the first packet, then drain what the queue already holds without blocking", straight into the
 // Payload.Raw slots of a (pinned) host arena -- slot i at arena + i * stride, the packet at
 // Raw[4:], the 4 leading bytes left for the private IP (common/payload.go:22-36) -- which is the
-// layout qgcm_seal_host and qgcm_compress_seal_host consume.  The link set-up of initTun
+// layout qgcm_seal_host and qgcm_compress_seal_host consume.  The drain is one io_uring submission
+// per batch: a READ per slot with RWF_NOWAIT (the TUN driver honours IOCB_NOWAIT), so every read
+// completes inline -- with a packet, or -EAGAIN once the queue is empty -- and a batch of n packets
+// costs one poll and one io_uring_enter instead of a poll and a read per packet.  Where io_uring is
+// unavailable (a kernel or seccomp that refuses io_uring_setup) each packet is one
+// preadv2(RWF_NOWAIT), and without that one poll + read, as before.  The link set-up of initTun
 // (device/tun.go:121-150: up, MTU, address + route by netlink) is done here with the classic
 // interface ioctls; the route of the address's prefix comes with the address.
 #include <arpa/inet.h>
@@ -17,16 +22,149 @@
 #include <linux/if_tun.h>
 #include <netinet/in.h>
 #include <poll.h>
+#include <stdlib.h>
 #include <string.h>
+#include <linux/io_uring.h>
 #include <sys/ioctl.h>
+#include <sys/mman.h>
 #include <sys/socket.h>
+#include <sys/syscall.h>
+#include <sys/uio.h>
 #include <unistd.h>
+
+#include <atomic>
 
 #include "../../include/qgcm.h"
 
 namespace {
 
 constexpr uint64_t kPacketStart = 4;  // common.PacketStart
+
+// One io_uring per calling thread (a worker thread owns its queues, worker/outgoing.go:83-93), created
+// on the first batched read; kRingEntries reads per submission.
+constexpr unsigned kRingEntries = 256;
+
+struct Ring {
+    int fd = -1;
+    unsigned *sq_tail = nullptr, *sq_mask = nullptr, *sq_array = nullptr;
+    unsigned *cq_head = nullptr, *cq_tail = nullptr, *cq_mask = nullptr;
+    io_uring_sqe *sqes = nullptr;
+    io_uring_cqe *cqes = nullptr;
+    void *sq_ptr = nullptr, *cq_ptr = nullptr;
+    size_t sq_len = 0, cq_len = 0, sqe_len = 0;
+
+    bool init() {
+        io_uring_params p{};
+        fd = (int)syscall(__NR_io_uring_setup, kRingEntries, &p);
+        if (fd < 0) return false;
+        sq_len = p.sq_off.array + p.sq_entries * sizeof(unsigned);
+        cq_len = p.cq_off.cqes + p.cq_entries * sizeof(io_uring_cqe);
+        const bool single = p.features & IORING_FEAT_SINGLE_MMAP;
+        if (single) sq_len = cq_len = sq_len > cq_len ? sq_len : cq_len;
+        sq_ptr = mmap(nullptr, sq_len, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_POPULATE, fd, IORING_OFF_SQ_RING);
+        if (sq_ptr == MAP_FAILED) return fail();
+        cq_ptr = single ? sq_ptr
+                        : mmap(nullptr, cq_len, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_POPULATE, fd, IORING_OFF_CQ_RING);
+        if (cq_ptr == MAP_FAILED) return fail();
+        sqe_len = p.sq_entries * sizeof(io_uring_sqe);
+        void *sq = mmap(nullptr, sqe_len, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_POPULATE, fd, IORING_OFF_SQES);
+        if (sq == MAP_FAILED) return fail();
+        sqes = static_cast<io_uring_sqe *>(sq);
+        auto at = [](void *base, unsigned off) { return reinterpret_cast<unsigned *>(static_cast<char *>(base) + off); };
+        sq_tail = at(sq_ptr, p.sq_off.tail);
+        sq_mask = at(sq_ptr, p.sq_off.ring_mask);
+        sq_array = at(sq_ptr, p.sq_off.array);
+        cq_head = at(cq_ptr, p.cq_off.head);
+        cq_tail = at(cq_ptr, p.cq_off.tail);
+        cq_mask = at(cq_ptr, p.cq_off.ring_mask);
+        cqes = reinterpret_cast<io_uring_cqe *>(static_cast<char *>(cq_ptr) + p.cq_off.cqes);
+        return true;
+    }
+    bool fail() {
+        close(fd);
+        fd = -1;
+        return false;
+    }
+    ~Ring() {
+        if (fd < 0) return;
+        munmap(sqes, sqe_len);
+        if (cq_ptr != sq_ptr) munmap(cq_ptr, cq_len);
+        munmap(sq_ptr, sq_len);
+        close(fd);
+    }
+};
+
+thread_local Ring tl_ring;
+thread_local int tl_ring_state = 0;  // 0 not tried, 1 ready, -1 unavailable
+// QGCM_TUN_URING=0 at the first batched read of the process: the preadv2 / read fallback (A/B)
+std::atomic<int> g_uring_allowed{-1};
+
+Ring *ring() {
+    int allowed = g_uring_allowed.load(std::memory_order_relaxed);
+    if (allowed < 0) {
+        const char *v = getenv("QGCM_TUN_URING");
+        allowed = !(v && !strcmp(v, "0"));
+        g_uring_allowed.store(allowed, std::memory_order_relaxed);
+    }
+    if (!allowed) return nullptr;
+    if (tl_ring_state == 0) tl_ring_state = tl_ring.init() ? 1 : -1;
+    return tl_ring_state > 0 ? &tl_ring : nullptr;
+}
+
+// Up to k (<= kRingEntries) non-blocking reads into slots [first, first + k), one submission; the
+// packets that were queued land in those slots, holes (a read that found the queue empty while a
+// later one found a packet that had just arrived) are closed up.  Returns how many landed (lens set),
+// or -1 when the ring failed (nothing consumed: the caller falls back).
+int uring_drain(Ring &r, int fd, uint8_t *arena, uint64_t stride, uint32_t first, uint32_t k, uint32_t *lens) {
+    unsigned tail = *r.sq_tail;
+    for (uint32_t j = 0; j < k; ++j) {
+        const unsigned idx = tail & *r.sq_mask;
+        io_uring_sqe &e = r.sqes[idx];
+        memset(&e, 0, sizeof e);
+        e.opcode = IORING_OP_READ;
+        e.fd = fd;
+        e.addr = reinterpret_cast<uint64_t>(arena + (uint64_t)(first + j) * stride + kPacketStart);
+        e.len = (uint32_t)(stride - kPacketStart);
+        e.off = (uint64_t)-1;  // the file position (a character device: none)
+        e.rw_flags = RWF_NOWAIT;
+        e.user_data = j;
+        r.sq_array[idx] = idx;
+        ++tail;
+    }
+    __atomic_store_n(r.sq_tail, tail, __ATOMIC_RELEASE);
+    int sub;
+    do {
+        sub = (int)syscall(__NR_io_uring_enter, r.fd, k, k, IORING_ENTER_GETEVENTS, nullptr, 0);
+    } while (sub < 0 && errno == EINTR);
+    if (sub != (int)k) return -1;
+    // every read completed inline (RWF_NOWAIT): reap k completions
+    static thread_local int32_t res[kRingEntries];
+    unsigned head = *r.cq_head, seen = 0;
+    while (seen < k) {
+        const unsigned ctail = __atomic_load_n(r.cq_tail, __ATOMIC_ACQUIRE);
+        for (; head != ctail && seen < k; ++head, ++seen) {
+            const io_uring_cqe &c = r.cqes[head & *r.cq_mask];
+            res[c.user_data] = c.res;
+        }
+        __atomic_store_n(r.cq_head, head, __ATOMIC_RELEASE);
+        if (seen < k) {
+            int w;
+            do {
+                w = (int)syscall(__NR_io_uring_enter, r.fd, 0, k - seen, IORING_ENTER_GETEVENTS, nullptr, 0);
+            } while (w < 0 && errno == EINTR);
+            if (w < 0) return -1;
+        }
+    }
+    uint32_t got = 0;
+    for (uint32_t j = 0; j < k; ++j) {
+        if (res[j] < 0) continue;
+        if (got != j)
+            memmove(arena + (uint64_t)(first + got) * stride + kPacketStart,
+                    arena + (uint64_t)(first + j) * stride + kPacketStart, (size_t)res[j]);
+        lens[first + got++] = (uint32_t)res[j];
+    }
+    return (int)got;
+}
 
 void set_name(ifreq *r, const char *name) {
     memset(r, 0, sizeof *r);
@@ -126,6 +264,33 @@ int qgcm_tun_read_slots(int fd, uint8_t *arena, uint64_t stride, uint32_t max_n,
     if (pr < 0) return -1;
     if (pr == 0) return 0;
     uint32_t got = 0;
+    if (Ring *r = ring()) {
+        // one submission per kRingEntries slots; the next only while the queue kept every read busy
+        while (got < max_n) {
+            const uint32_t k = max_n - got < kRingEntries ? max_n - got : kRingEntries;
+            const int n = uring_drain(*r, fd, arena, stride, got, k, lens);
+            if (n < 0) break;  // the ring failed: the loop below takes over
+            got += (uint32_t)n;
+            if ((uint32_t)n < k) return (int)got;
+        }
+        if (got == max_n) return (int)got;
+    }
+    // no io_uring: one preadv2(RWF_NOWAIT) per packet (a poll + read where that is refused too)
+    static std::atomic<int> nowait_ok{1};
+    while (got < max_n && nowait_ok.load(std::memory_order_relaxed)) {
+        iovec v{arena + (uint64_t)got * stride + kPacketStart, (size_t)(stride - kPacketStart)};
+        const ssize_t n = preadv2(fd, &v, 1, -1, RWF_NOWAIT);
+        if (n < 0) {
+            if (errno == EINTR) continue;
+            if (errno == EAGAIN || errno == EWOULDBLOCK) return (int)got;
+            if (errno == EOPNOTSUPP || errno == EINVAL || errno == ENOSYS) {
+                nowait_ok.store(0, std::memory_order_relaxed);
+                break;
+            }
+            return got ? (int)got : -1;
+        }
+        lens[got++] = (uint32_t)n;
+    }
     while (got < max_n) {
         if (got) {  // drain without blocking: only what is already queued joins this batch
             p.revents = 0;

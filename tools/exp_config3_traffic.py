@@ -15,6 +15,7 @@ whose workgroups work on the key); packed - aligned is what 4-B slot offsets cos
 4-B offset touches an extra line).  Each form: one warmup pair, then 3 seal+open pairs.
 
   python3 tools/exp_config3_traffic.py run <form>          (under rocprofv3 --pmc ...)
+  python3 tools/exp_config3_traffic.py time [reps]         (all four forms in one process, interleaved)
   python3 tools/exp_config3_traffic.py summarize <dir>     (one sub-directory per form x pass)
 """
 import collections
@@ -64,6 +65,48 @@ def run(form: str) -> None:
     ctx.close()
 
 
+def time_forms(reps: int = 7) -> None:
+    """Seal+open pairs of the four forms interleaved in one process, HIP events, median GiB/s."""
+    import torch
+
+    from exp_config3_align import aligned_layout
+    from quantum_amd import batch, workloads as W
+    from quantum_amd.crypto import Context
+
+    keys = W.peer_keys()
+    ctx = Context(device=0, max_keys=W.NKEYS)
+    ctx.set_keys(0, keys)
+    lens, kidx0 = W.lengths(), W.key_indices()
+    nonces = torch.from_numpy(W.nonces()).cuda()
+    status = torch.zeros(W.N, dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.current_stream()
+    forms = {}
+    for form in FORMS:
+        kidx = np.zeros_like(kidx0) if form.endswith("onekey") else kidx0
+        offs, size = aligned_layout(lens) if form.startswith("aligned") else W.layout(lens)
+        forms[form] = (W.device_arena(torch, size, offs, kidx), batch.make_descs(offs, lens, kidx, "cuda"),
+                       batch.make_descs(offs, lens.astype(np.int64) + 28, kidx, "cuda"))
+    times = {f: [] for f in FORMS}
+    ok = True
+    for r in range(reps + 1):
+        for form, (arena, ds, do) in forms.items():
+            e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            e[0].record(stream)
+            batch.seal_batch(ctx, arena, ds, W.N, nonces, status=status, stream=stream)
+            batch.open_batch(ctx, arena, do, W.N, status=status, stream=stream)
+            e[1].record(stream)
+            torch.cuda.synchronize()
+            ok &= int(status.sum()) == W.N
+            if r:
+                times[form].append(e[0].elapsed_time(e[1]))
+    payload = int(lens.sum())
+    print(json.dumps({"exp": "config3 forms, seal+open pair", "reps": reps, "status_ok": ok,
+                      **{f: {"pair_ms": round(float(np.median(t)), 3),
+                             "GiB_s": round(2 * payload / (float(np.median(t)) * 1e-3) / 2**30, 1)}
+                         for f, t in times.items()}}))
+    ctx.close()
+
+
 def summarize(root: str) -> None:
     """<root>/<form>_<pass>/...counter_collection.csv -> per form and direction: every counter summed
     over the call's packet kernels (gcm_*: the segmented kernel and its per-wave complement), median
@@ -75,7 +118,7 @@ def summarize(root: str) -> None:
     out = {"payload_bytes": payload, "packets": W.N, "forms": {}}
     for form in FORMS:
         per = collections.defaultdict(lambda: collections.defaultdict(list))  # kind -> counter -> per-call sums
-        for f in glob.glob(os.path.join(root, f"{form}_*", "**", "*counter_collection.csv"), recursive=True):
+        for f in glob.glob(os.path.join(root, f"{form}_p[0-9]*", "**", "*counter_collection.csv"), recursive=True):
             calls = collections.defaultdict(lambda: collections.defaultdict(float))
             seq = {"seal": -1, "open": -1}
             last = None
@@ -128,5 +171,7 @@ def summarize(root: str) -> None:
 if __name__ == "__main__":
     if sys.argv[1] == "run":
         run(sys.argv[2])
+    elif sys.argv[1] == "time":
+        time_forms(int(sys.argv[2]) if len(sys.argv) > 2 else 7)
     else:
         summarize(sys.argv[2])

@@ -208,6 +208,9 @@ for s in $STEPS; do
         ls -R $OUT/cm_${mode}_$tr 2>/dev/null | grep -c csv > $OUT/cm_${mode}_$tr.csvcount
         check cm_${mode}_$tr $rc
       done ;;
+    c3time)  # config 3's four forms timed in one process, interleaved
+      timeout -k 10 300 python3 tools/exp_config3_traffic.py time 7 > $OUT/c3_forms_time.json 2> $OUT/c3_forms_time.err
+      check c3time $? ;;
     pcieaftrace)  # the after-free rows under the copy tracer: r4_s9 crashed in __cxa_finalize at exit here (pcie.py teardown)
       timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $OUT/trace_pcieaf -o t -- python3 tools/microbench/pcie.py --after-free 90 > $OUT/trace_pcieaf.log 2>&1
       check pcieaftrace $? ;;

@@ -6,6 +6,11 @@ __cxa_finalize -> librocprofiler-sdk -> libhsa-runtime64).  Modes:
   kernel      a device-only op (no copy), then a normal exit
   copy_reset  as copy, then hipDeviceReset() before the exit (every stream, allocation and HSA queue
               the runtime holds released while the profiler is still alive)
+  many        pcie.py's traffic: 64-MiB pinned copies on two side streams, 1 GiB each way x 3
+  many_reset  as many, then hipDeviceReset() before the exit
+
+profiles/r5_s3: copy, kernel and copy_reset exit cleanly under --memory-copy-trace (the crash needs more
+than one copy).
 
 Usage: python3 tools/microbench/crash_min.py <mode>   (run under rocprofv3 ... -- python3 ...)"""
 import ctypes
@@ -14,6 +19,33 @@ import sys
 import torch
 
 mode = sys.argv[1]
+if mode in ("many", "many_reset"):
+    chunk, n = 64 << 20, 16
+    hs = [torch.empty(chunk, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
+    ds = [torch.empty(chunk, dtype=torch.uint8, device="cuda") for _ in range(2)]
+    s_in, s_out = torch.cuda.Stream(), torch.cuda.Stream()
+    for rep in range(3):
+        e0 = torch.cuda.Event()
+        e0.record()
+        s_in.wait_event(e0)
+        s_out.wait_event(e0)
+        for i in range(n):
+            with torch.cuda.stream(s_in):
+                ds[0].copy_(hs[0], non_blocking=True)
+            with torch.cuda.stream(s_out):
+                hs[1].copy_(ds[1], non_blocking=True)
+        torch.cuda.current_stream().wait_stream(s_in)
+        torch.cuda.current_stream().wait_stream(s_out)
+        torch.cuda.synchronize()
+    print({"mode": mode, "copies": 2 * 3 * n}, flush=True)
+    if mode == "many_reset":
+        del hs, ds, s_in, s_out
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        torch._C._host_emptyCache()
+        hip = ctypes.CDLL("libamdhip64.so")
+        print({"hipDeviceReset": hip.hipDeviceReset()}, flush=True)
+    sys.exit(0)
 if mode in ("copy", "copy_reset"):
     h = torch.ones(1 << 20, dtype=torch.uint8, pin_memory=True)
     d = h.to("cuda", non_blocking=True)
