@@ -7,12 +7,11 @@
 // the first packet, then drain what the queue already holds without blocking", straight into the
 // Payload.Raw slots of a (pinned) host arena -- slot i at arena + i * stride, the packet at
 // Raw[4:], the 4 leading bytes left for the private IP (common/payload.go:22-36) -- which is the
-// layout qgcm_seal_host and qgcm_compress_seal_host consume.  The drain is one io_uring submission
-// per batch: a READ per slot with RWF_NOWAIT (the TUN driver honours IOCB_NOWAIT), so every read
-// completes inline -- with a packet, or -EAGAIN once the queue is empty -- and a batch of n packets
-// costs one poll and one io_uring_enter instead of a poll and a read per packet.  Where io_uring is
-// unavailable (a kernel or seccomp that refuses io_uring_setup) each packet is one
-// preadv2(RWF_NOWAIT), and without that one poll + read, as before.  The link set-up of initTun
+// layout qgcm_seal_host and qgcm_compress_seal_host consume.  After the poll for the first packet the
+// drain is one preadv2(RWF_NOWAIT) per packet (the TUN driver honours IOCB_NOWAIT: a packet, or
+// -EAGAIN once the queue is empty), one syscall per packet instead of a poll and a read.  One io_uring
+// submission of RWF_NOWAIT reads per batch (QGCM_TUN_URING=1) was built and measured slower (read_mode
+// below).  The link set-up of initTun
 // (device/tun.go:121-150: up, MTU, address + route by netlink) is done here with the classic
 // interface ioctls; the route of the address's prefix comes with the address.
 #include <arpa/inet.h>
@@ -96,17 +95,27 @@ struct Ring {
 
 thread_local Ring tl_ring;
 thread_local int tl_ring_state = 0;  // 0 not tried, 1 ready, -1 unavailable
-// QGCM_TUN_URING=0 at the first batched read of the process: the preadv2 / read fallback (A/B)
-std::atomic<int> g_uring_allowed{-1};
+// The read path, fixed at the first batched read of the process: 0 preadv2(RWF_NOWAIT) per packet (the
+// default), 1 one io_uring submission per batch (QGCM_TUN_URING=1), 2 poll + read per packet, the
+// round-4 form (QGCM_TUN_URING=-1).  tools/tun_rate.py, 400 000 packets of 1378 B through a TUN queue,
+// time inside the read calls per packet, three interleaved runs: preadv2 0.68 / 0.80 / 0.68 us,
+// io_uring 0.83 / 0.91 / 1.11, poll + read 0.93 / 0.97 / 1.09 -- the kernel's per-packet work (the
+// skb copy-out and free), not the syscall entry, is most of the cost, and io_uring's per-request
+// set-up and completion cost more than the syscall it saves.
+std::atomic<int> g_read_mode{-1};
+
+int read_mode() {
+    int m = g_read_mode.load(std::memory_order_relaxed);
+    if (m < 0) {
+        const char *v = getenv("QGCM_TUN_URING");
+        m = !v ? 0 : !strcmp(v, "1") ? 1 : !strcmp(v, "-1") ? 2 : 0;
+        g_read_mode.store(m, std::memory_order_relaxed);
+    }
+    return m;
+}
 
 Ring *ring() {
-    int allowed = g_uring_allowed.load(std::memory_order_relaxed);
-    if (allowed < 0) {
-        const char *v = getenv("QGCM_TUN_URING");
-        allowed = !(v && !strcmp(v, "0"));
-        g_uring_allowed.store(allowed, std::memory_order_relaxed);
-    }
-    if (!allowed) return nullptr;
+    if (read_mode() != 1) return nullptr;
     if (tl_ring_state == 0) tl_ring_state = tl_ring.init() ? 1 : -1;
     return tl_ring_state > 0 ? &tl_ring : nullptr;
 }
@@ -275,8 +284,10 @@ int qgcm_tun_read_slots(int fd, uint8_t *arena, uint64_t stride, uint32_t max_n,
         }
         if (got == max_n) return (int)got;
     }
-    // no io_uring: one preadv2(RWF_NOWAIT) per packet (a poll + read where that is refused too)
+    // no io_uring: one preadv2(RWF_NOWAIT) per packet (a poll + read where that is refused too, or
+    // with QGCM_TUN_URING=-1: the round-4 form, for A/Bs)
     static std::atomic<int> nowait_ok{1};
+    if (read_mode() == 2) nowait_ok.store(0, std::memory_order_relaxed);
     while (got < max_n && nowait_ok.load(std::memory_order_relaxed)) {
         iovec v{arena + (uint64_t)got * stride + kPacketStart, (size_t)(stride - kPacketStart)};
         const ssize_t n = preadv2(fd, &v, 1, -1, RWF_NOWAIT);

@@ -160,3 +160,23 @@ def test_tun_multi_queue_keeps_flows_in_order(tun):
     for f, recs in seen.items():
         assert len({q for q, _ in recs}) == 1, f"flow {f} split over queues"
         assert [s for _, s in recs] == list(range(per)), f"flow {f} out of order"
+
+
+@pytest.mark.parametrize("mode", ["1", "-1"])
+def test_tun_read_paths(mode):
+    """The other two drain forms of qgcm_tun_read_slots, each in a fresh process (the form is fixed at a
+    process's first batched read): one io_uring submission of RWF_NOWAIT reads per batch
+    (QGCM_TUN_URING=1) and poll + read per packet (-1); the default preadv2 form runs in this process."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, QGCM_TUN_URING=mode)
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider",
+                        os.path.join(root, "tests", "test_tun_batch.py"), "-k", "read_slots_gets_routed"],
+                       cwd=root, env=env, capture_output=True, text=True, timeout=120)
+    if "1 skipped" in r.stdout:
+        pytest.skip("TUN device refused in the child")
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "1 passed" in r.stdout, r.stdout[-1000:]

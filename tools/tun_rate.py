@@ -44,14 +44,16 @@ def main() -> None:
         # drain link-up chatter
         while L.qgcm_tun_read_slots(fd, arena.ctypes.data, STRIDE, BATCH, rl.ctypes.data, 20) > 0:
             pass
-        got, calls = 0, 0
+        got, calls, t_read = 0, 0, 0.0
         t0 = time.perf_counter()
         while got < total:
             # bursts of 256: the device's transmit queue (txqueuelen) holds 500 packets
             assert L.qgcm_udp_send_slots(tx, src.ctypes.data, STRIDE, 256, lens.ctypes.data, PEER_IP.encode(), 9000) == 256
             batch_got = 0
             while batch_got < 256:
+                tr = time.perf_counter()
                 r = L.qgcm_tun_read_slots(fd, arena.ctypes.data, STRIDE, BATCH, rl.ctypes.data, 5)
+                t_read += time.perf_counter() - tr
                 if r <= 0:
                     break  # the kernel dropped the rest (queue full): count what arrived
                 batch_got += r
@@ -61,7 +63,10 @@ def main() -> None:
         print(json.dumps({"direction": "udp -> tun -> qgcm_tun_read_slots", "packets": got,
                           "packet_bytes": PAYLOAD + 28, "Mpps": round(got / dt / 1e6, 3),
                           "GiB_s": round(got * (PAYLOAD + 28) / dt / 2**30, 3),
-                          "packets_per_call": round(got / max(calls, 1), 1)}), flush=True)
+                          "packets_per_call": round(got / max(calls, 1), 1),
+                          "read_calls_us_per_packet": round(t_read / max(got, 1) * 1e6, 3),
+                          "read_calls_Mpps": round(got / max(t_read, 1e-9) / 1e6, 2),
+                          "io_uring": os.environ.get("QGCM_TUN_URING", "1") != "0"}), flush=True)
         L.qgcm_udp_close(tx)
 
         rx = L.qgcm_udp_socket(HOST_IP.encode(), 0, 1 << 26)
