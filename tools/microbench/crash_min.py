@@ -9,8 +9,13 @@ __cxa_finalize -> librocprofiler-sdk -> libhsa-runtime64).  Modes:
   many        pcie.py's traffic: 64-MiB pinned copies on two side streams, 1 GiB each way x 3
   many_reset  as many, then hipDeviceReset() before the exit
 
-profiles/r5_s3: copy, kernel and copy_reset exit cleanly under --memory-copy-trace (the crash needs more
-than one copy).
+  many_default  as many, all copies on the current (default) stream, no side streams
+  ext_streams   as many, on two streams made with hipStreamCreate (torch.cuda.ExternalStream) and
+                destroyed with hipStreamDestroy before the exit
+  streams_only  two torch.cuda.Stream() side streams, one small copy on each
+
+profiles/r5_s3: copy, kernel and copy_reset exit cleanly under --memory-copy-trace; profiles/r5_s4:
+many_reset crashes (hipDeviceReset does not avoid it).
 
 Usage: python3 tools/microbench/crash_min.py <mode>   (run under rocprofv3 ... -- python3 ...)"""
 import ctypes
@@ -19,6 +24,36 @@ import sys
 import torch
 
 mode = sys.argv[1]
+hip = ctypes.CDLL("libamdhip64.so")
+if mode in ("many_default", "ext_streams", "streams_only"):
+    chunk, n = 64 << 20, 16
+    hs = [torch.empty(chunk, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
+    ds = [torch.empty(chunk, dtype=torch.uint8, device="cuda") for _ in range(2)]
+    raw = []
+    if mode == "ext_streams":
+        for _ in range(2):
+            h = ctypes.c_void_p()
+            assert hip.hipStreamCreateWithFlags(ctypes.byref(h), 1) == 0  # hipStreamNonBlocking
+            raw.append(h)
+        streams = [torch.cuda.ExternalStream(h.value) for h in raw]
+    elif mode == "streams_only":
+        streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+        n = 1
+    else:
+        streams = [torch.cuda.current_stream()] * 2
+    for rep in range(3 if mode != "streams_only" else 1):
+        for i in range(n):
+            with torch.cuda.stream(streams[0]):
+                ds[0].copy_(hs[0], non_blocking=True)
+            with torch.cuda.stream(streams[1]):
+                hs[1].copy_(ds[1], non_blocking=True)
+        torch.cuda.synchronize()
+    print({"mode": mode, "copies": 2 * n * (3 if mode != "streams_only" else 1)}, flush=True)
+    if raw:
+        del streams
+        torch.cuda.synchronize()
+        print({"hipStreamDestroy": [hip.hipStreamDestroy(h) for h in raw]}, flush=True)
+    sys.exit(0)
 if mode in ("many", "many_reset"):
     chunk, n = 64 << 20, 16
     hs = [torch.empty(chunk, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
@@ -43,7 +78,6 @@ if mode in ("many", "many_reset"):
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
         torch._C._host_emptyCache()
-        hip = ctypes.CDLL("libamdhip64.so")
         print({"hipDeviceReset": hip.hipDeviceReset()}, flush=True)
     sys.exit(0)
 if mode in ("copy", "copy_reset"):
@@ -61,5 +95,4 @@ if mode == "copy_reset":
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
     torch._C._host_emptyCache()
-    hip = ctypes.CDLL("libamdhip64.so")
     print({"hipDeviceReset": hip.hipDeviceReset()}, flush=True)
