@@ -211,8 +211,9 @@ for s in $STEPS; do
     c3time)  # config 3's four forms timed in one process, interleaved
       timeout -k 10 300 python3 tools/exp_config3_traffic.py time 7 > $OUT/c3_forms_time.json 2> $OUT/c3_forms_time.err
       check c3time $? ;;
-    pcieaftrace)  # the after-free rows under the copy tracer: r4_s9 crashed in __cxa_finalize at exit here (pcie.py teardown)
-      timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $OUT/trace_pcieaf -o t -- python3 tools/microbench/pcie.py --after-free 90 > $OUT/trace_pcieaf.log 2>&1
+    pcieaftrace)  # the after-free rows under the profiler, kernel trace only: with --memory-copy-trace rocprofv3's own
+                  # finalization faults at exit for torch copies on side streams (tools/README.md, crashmin)
+      timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/trace_pcieaf -o t -- python3 tools/microbench/pcie.py --after-free 90 > $OUT/trace_pcieaf.log 2>&1
       check pcieaftrace $? ;;
     e2ebig)  # qgcm_seal_host past its 4-GiB staging ring (slots rotate) vs within it
       timeout -k 10 400 python3 tools/exp_host_legs.py e2e e2e_big > $OUT/e2e_big.jsonl 2> $OUT/e2e_big.err
