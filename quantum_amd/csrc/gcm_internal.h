@@ -2,8 +2,11 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <sched.h>
+
 #include <mutex>
 #include <stdint.h>
+#include <vector>
 
 #include "../../include/qgcm.h"
 
@@ -216,6 +219,13 @@ struct SnapArgs {
 // packet regions of a.off_sink bytes); false = one wave per packet
 constexpr uint32_t kSnapGroup = 4;
 hipError_t launch_snappy(bool compress, const SnapArgs &a, int waves_per_wg, int grid, hipStream_t s, bool group);
+
+// Host worker placement (cpu_topo.cpp): the device's NUMA-local CPUs this process may use (count; 0 when
+// sysfs has no answer), one CPU per physical core ordered preferred-first then least busy over a
+// sample_ms window, and pinning the calling thread to one CPU.
+int gpu_local_cpus(int device, cpu_set_t *out);
+std::vector<int> spread_cpus(const cpu_set_t *prefer, int sample_ms);
+void pin_to_cpu(int cpu);
 
 hipError_t launch_pw_setup(uint32_t first, uint32_t count, const uint4 *gh_table, uint4 *pw, uint32_t pw_keys,
                            hipStream_t s);

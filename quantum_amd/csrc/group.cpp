@@ -195,46 +195,7 @@ inline void slice(size_t n, int i, int k, size_t &lo, size_t &hi) {
     hi = n * (size_t)(i + 1) / (size_t)k;
 }
 
-// "0-31,64-95" -> set bits (sysfs cpulist format)
-void parse_cpulist(const char *txt, cpu_set_t *set) {
-    CPU_ZERO(set);
-    const char *p = txt;
-    while (*p) {
-        char *e;
-        const long a = strtol(p, &e, 10);
-        if (e == p) break;
-        long b = a;
-        p = e;
-        if (*p == '-') {
-            b = strtol(p + 1, &e, 10);
-            p = e;
-        }
-        for (long c = a; c <= b && c < CPU_SETSIZE; ++c)
-            if (c >= 0) CPU_SET((int)c, set);
-        while (*p == ',' || *p == '\n' || *p == ' ') ++p;
-    }
-}
-
-// CPUs of the device's NUMA node that this process may run on; 0 when sysfs has no answer
-int gpu_local_cpus(int device, cpu_set_t *out) {
-    CPU_ZERO(out);
-    char bus[64] = {0};
-    if (hipDeviceGetPCIBusId(bus, (int)sizeof(bus), device) != hipSuccess) return 0;
-    for (char *c = bus; *c; ++c) *c = (char)tolower(*c);
-    char path[160];
-    snprintf(path, sizeof(path), "/sys/bus/pci/devices/%s/local_cpulist", bus);
-    FILE *f = fopen(path, "r");
-    if (!f) return 0;
-    char txt[4096] = {0};
-    const size_t got = fread(txt, 1, sizeof(txt) - 1, f);
-    fclose(f);
-    if (got == 0) return 0;
-    cpu_set_t local, allowed;
-    parse_cpulist(txt, &local);
-    if (sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return 0;
-    CPU_AND(out, &local, &allowed);
-    return CPU_COUNT(out);
-}
+using qgcm::gpu_local_cpus;
 
 inline uint64_t rec_bytes(bool seal, uint32_t len) {  // AAD word + packet (+ tag || nonce), 16-B aligned
     return (4ull + len + (seal ? QGCM_OVERHEAD : 0) + 15) & ~15ull;

@@ -52,6 +52,19 @@ struct qgcm_ctx {
     // QGCM_HOST_DIRECT=0 stops qgcm_seal_host sealing worker-sized pinned arenas in place,
     // QGCM_SMALL_WORKLIST=0 builds small batches' worklists by the multi-launch path
     bool desc_one_on = true, host_direct = true, small_wl = true;
+    // the snappy + GCM chain's A/B knobs, read at qgcm_create too: QGCM_CHAIN_CHUNK_MB (bytes of slots
+    // per chunk), QGCM_CHAIN_SLOTS (chunks in flight), QGCM_CHAIN_DEV_AHEAD / QGCM_CHAIN_DEV_BACKLOG
+    // (the host/device codec split; backlog -1 = two chunks' items), QGCM_SNAPPY_GROUP (the device
+    // encoder: four packets per wave, or one wave per packet)
+    uint64_t chain_chunk = kPipeChunk;
+    int chain_slots = kPipeStreams, chain_dev_ahead = 2, chain_dev_backlog = -1;
+    bool snappy_group = true;
+    // the chain's host codec workers run one per physical core, the GPU's NUMA-local cores and the least
+    // busy first (cpu_topo.cpp; QGCM_CHAIN_PIN=0 at qgcm_create: left to the scheduler).  The core list
+    // is taken at the first chained call (a 30-ms sample of the host's load) and kept.
+    bool chain_pin = true;
+    std::once_flag codec_cpus_once;
+    std::vector<int> codec_cpus;
     uint32_t *d_rk = nullptr;
     uint4 *d_gh = nullptr;
     uint4 *d_pw = nullptr;   // per-packet flat GHASH: comb tables of H^1..H^kPwPowers, key slots < pw_keys
@@ -596,6 +609,12 @@ qgcm_ctx *qgcm_create(int device, uint32_t max_keys, char *err, int errlen) {
         const char *v = getenv(name);
         return v && !strcmp(v, "0");
     };
+    ctx->chain_chunk = (uint64_t)std::max(1, env_int("QGCM_CHAIN_CHUNK_MB", (int)(kPipeChunk >> 20))) << 20;
+    ctx->chain_slots = std::max(1, std::min(16, env_int("QGCM_CHAIN_SLOTS", kPipeStreams)));
+    ctx->chain_dev_ahead = std::max(1, env_int("QGCM_CHAIN_DEV_AHEAD", 2));
+    ctx->chain_dev_backlog = env_int("QGCM_CHAIN_DEV_BACKLOG", -1);
+    ctx->snappy_group = env_int("QGCM_SNAPPY_GROUP", 1) != 0;
+    ctx->chain_pin = env_int("QGCM_CHAIN_PIN", 1) != 0;
     ctx->desc_one_on = !off("QGCM_DESC_ONE");
     ctx->host_direct = !off("QGCM_HOST_DIRECT");
     ctx->small_wl = !off("QGCM_SMALL_WORKLIST");
@@ -1003,8 +1022,7 @@ static int run_host_chain(qgcm_ctx *ctx, bool seal, uint8_t *h_arena, uint64_t s
     std::lock_guard<std::mutex> g(ctx->io_mu);
     if (hipSetDevice(ctx->device) != hipSuccess) return QGCM_E_HIP;
     auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
-    // QGCM_CHAIN_CHUNK_MB: A/B knob for the chunk size (read per call, like the split knobs below)
-    const uint64_t chunk_bytes = (uint64_t)std::max(1, env_int("QGCM_CHAIN_CHUNK_MB", (int)(kPipeChunk >> 20))) << 20;
+    const uint64_t chunk_bytes = ctx->chain_chunk;  // QGCM_CHAIN_CHUNK_MB at qgcm_create
     const int dev_mode = ctx->chain_codec.load();
     uint64_t cpk = (chunk_bytes / stride) & ~255ull;  // whole codec items per chunk
     if (cpk < 256) cpk = 256;
@@ -1013,8 +1031,8 @@ static int run_host_chain(qgcm_ctx *ctx, bool seal, uint8_t *h_arena, uint64_t s
     const bool non = seal && h_nonces;
     const uint64_t off_non = al(cpk * stride), off_st = off_non + (non ? al(12 * cpk) : 0);
     const uint64_t off_desc = off_st + al(cpk), off_lens = off_desc + al(16 * cpk), slot = off_lens + al(4 * cpk);
-    // chunks in flight, one stream and staging slot each (QGCM_CHAIN_SLOTS, A/B knob; default 3)
-    const int want_slots = std::max(1, std::min(16, env_int("QGCM_CHAIN_SLOTS", kPipeStreams)));
+    // chunks in flight, one stream and staging slot each (QGCM_CHAIN_SLOTS at qgcm_create; default 3)
+    const int want_slots = ctx->chain_slots;
     const int nslots = nchunks < (uint64_t)want_slots ? (int)nchunks : want_slots;
     while ((int)ctx->chain_extra.size() + kPipeStreams < nslots) {
         hipStream_t x = nullptr;
@@ -1120,12 +1138,23 @@ static int run_host_chain(qgcm_ctx *ctx, bool seal, uint8_t *h_arena, uint64_t s
         }
     };
     const int nt = (seal && dev_ok && dev_mode == 2) ? 0 : std::max(1, std::min(threads, 256));
-    for (int t = 0; t < nt; ++t) pool.workers.emplace_back(work);
+    if (ctx->chain_pin && nt > 0)
+        std::call_once(ctx->codec_cpus_once, [ctx] {
+            cpu_set_t local;
+            const bool have = qgcm::gpu_local_cpus(ctx->device, &local) > 0;
+            ctx->codec_cpus = qgcm::spread_cpus(have ? &local : nullptr, 30);
+        });
+    const std::vector<int> *pin = ctx->chain_pin && !ctx->codec_cpus.empty() ? &ctx->codec_cpus : nullptr;
+    for (int t = 0; t < nt; ++t)
+        pool.workers.emplace_back([&work, pin, t] {
+            if (pin) qgcm::pin_to_cpu((*pin)[(size_t)t % pin->size()]);
+            work();
+        });
     // seal: the device takes a chunk when fewer than ahead_min compressed host chunks are waiting as a
     // stream slot frees up (the host codec is about to stall the pipeline); open: when more than
     // backlog_max released items wait for the host decoder
-    const uint64_t ahead_min = (uint64_t)std::max(1, env_int("QGCM_CHAIN_DEV_AHEAD", 2));
-    const uint64_t backlog_max = (uint64_t)env_int("QGCM_CHAIN_DEV_BACKLOG", (int)(2 * per_chunk));
+    const uint64_t ahead_min = (uint64_t)ctx->chain_dev_ahead;
+    const uint64_t backlog_max = ctx->chain_dev_backlog >= 0 ? (uint64_t)ctx->chain_dev_backlog : 2ull * per_chunk;
     std::vector<int64_t> slot_chunk(nslots, -1);
     // a slot's previous chunk has landed: device chunks' lengths back to the caller; open: release
     // its items to the host workers (device chunks' items are skipped)
@@ -1292,11 +1321,11 @@ static int run_snappy(qgcm_ctx *ctx, bool compress, uint8_t *d_arena, uint64_t s
     a.off_in = tab;
     a.off_out = a.off_in + a16(max_in + 24);  // + the 16-B chunks' overhang and stage_in's slack dwords
     a.off_sink = a.off_out + a16((compress ? (uint32_t)qgcm_snappy_max_compressed_length(max_in) : limit) + 8);
-    // the encoder (QGCM_SNAPPY_GROUP, A/B knob): 1 (default) = four packets per wave, output straight
+    // the encoder (QGCM_SNAPPY_GROUP at qgcm_create, A/B knob): 1 (default) = four packets per wave, output straight
     // into the slot (the region: table + the input staged up to max(len, limit) bytes, the restore
     // copy); 0 = one wave per packet.  Packets past ~5 KiB need more LDS than four regions per wave can
     // have, and limit 0 fails every packet: one wave per packet.  The decoder is one wave per packet.
-    bool group = compress && limit > 0 && env_int("QGCM_SNAPPY_GROUP", 1) != 0;
+    bool group = compress && limit > 0 && ctx->snappy_group;
     if (group) {
         a.off_out = a.off_in + a16(std::max(max_in, limit) + 24);
         a.off_sink = a.off_out;

@@ -80,16 +80,37 @@ def _match(case, comp: bytes) -> bool:
     return hashlib.sha256(comp).hexdigest() == case["out_sha256"]
 
 
+@pytest.fixture(scope="module")
+def encoder_ctxs(torch):
+    """One context per QGCM_SNAPPY_GROUP setting (read at qgcm_create)."""
+    from quantum_amd.crypto import Context
+
+    out, old = {}, os.environ.get("QGCM_SNAPPY_GROUP")
+    try:
+        for g in ("1", "0"):
+            os.environ["QGCM_SNAPPY_GROUP"] = g
+            out[g] = Context(device=0, max_keys=16)
+    finally:
+        if old is None:
+            os.environ.pop("QGCM_SNAPPY_GROUP", None)
+        else:
+            os.environ["QGCM_SNAPPY_GROUP"] = old
+    yield out
+    for c in out.values():
+        c.close()
+
+
 @pytest.fixture(params=["1", "0"], ids=["group_encoder", "wave_encoder"])
-def encoder(request, monkeypatch):
-    """QGCM_SNAPPY_GROUP (read per call): 1 = four packets per wave, pipelined miss probes, output
+def encoder(request, encoder_ctxs):
+    """QGCM_SNAPPY_GROUP (at qgcm_create): 1 = four packets per wave, pipelined miss probes, output
     straight into the slot, the next packets prefetched (the default); 0 = one wave per packet.  Both
-    must give the host encoder's (and libsnappy's) bytes, and leave a failing packet's slot untouched."""
-    monkeypatch.setenv("QGCM_SNAPPY_GROUP", request.param)
-    return request.param
+    must give the host encoder's (and libsnappy's) bytes, and leave a failing packet's slot untouched.
+    The value is the context built with that setting."""
+    return encoder_ctxs[request.param]
 
 
-def test_device_encoder_equals_libsnappy_golden(torch, ctx, encoder):
+def test_device_encoder_equals_libsnappy_golden(torch, encoder):
+    ctx = encoder
     with open(GOLDEN) as f:
         cases = [c for c in json.load(f)["cases"] if c["n"] <= DEV_MAX]
     datas = [SI.make(c["kind"], c["n"]) for c in cases]
@@ -114,10 +135,11 @@ def test_device_encoder_equals_libsnappy_golden(torch, ctx, encoder):
         assert st2[i] == 1 and bl[i] == len(d) and back[i, 4:4 + len(d)].tobytes() == d
 
 
-def test_device_codec_config5_batch_vs_host(torch, ctx, encoder):
+def test_device_codec_config5_batch_vs_host(torch, encoder):
     """2^14 Payload.Raw slots (stride 1472): config 5's packet shape and a mix of lengths 0..1433
     and contents; device compress == host encoder (whole arena incl. untouched bytes, lengths), then
     device uncompress restores the plaintext arena."""
+    ctx = encoder
     n, stride = 1 << 14, 1472
     rng = np.random.default_rng(0x5EED0051)
     kinds = SI.KINDS
@@ -149,8 +171,9 @@ def test_device_codec_config5_batch_vs_host(torch, ctx, encoder):
     assert np.array_equal(back, plain)
 
 
-def test_device_compress_failures_untouched(torch, ctx, encoder):
+def test_device_compress_failures_untouched(torch, encoder):
     """Longer than max_len, or compressed form over limit: status 0, slot and length untouched."""
+    ctx = encoder
     stride = 2048
     payloads = [SI.make("random", 1500), SI.make("line", 1500), SI.make("random", 900), b"", SI.make("zeros", 40)]
     host, arena, lens = _arena(torch, payloads, stride)

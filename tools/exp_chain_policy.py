@@ -1,6 +1,7 @@
 """Config 5 (bench.extra_config5's workload, host packets, copies included) under the chain's codec
-split knobs, one process: QGCM_CHAIN_DEV_AHEAD (seal) and QGCM_CHAIN_DEV_BACKLOG (open) are read per
-call, so each setting is timed in turn, interleaved over `rounds`.
+split knobs, one process: QGCM_CHAIN_DEV_AHEAD (seal), QGCM_CHAIN_DEV_BACKLOG (open), QGCM_CHAIN_SLOTS
+and QGCM_CHAIN_CHUNK_MB are read at qgcm_create, so each setting gets a context of its own, timed in
+turn, interleaved over `rounds`.
 
     python3 tools/exp_chain_policy.py [rounds] [chunks|slots]   (chunk size x codec threads, or chunks in
     flight x chunk size)
@@ -23,8 +24,7 @@ from quantum_amd.crypto import Context  # noqa: E402
 def main() -> None:
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 3
     N, L, stride = 1 << 20, 1350, 1472
-    ctx = Context(device=0, max_keys=4)
-    ctx.set_key(0, bench.derive_key(bench.SECRET, bench.SALT))
+    key = bench.derive_key(bench.SECRET, bench.SALT)
     Lb = _lib.lib()
     a_ptr, n_ptr = Lb.qgcm_host_alloc(N * stride), Lb.qgcm_host_alloc(12 * N)
     host = np.frombuffer((C.c_uint8 * (N * stride)).from_address(a_ptr), np.uint8).reshape(N, stride)
@@ -61,6 +61,8 @@ def main() -> None:
                 os.environ["QGCM_CHAIN_DEV_BACKLOG"] = back
             else:
                 os.environ.pop("QGCM_CHAIN_DEV_BACKLOG", None)
+            ctx = Context(device=0, max_keys=4)
+            ctx.set_key(0, key)
             batch.chain_codec(ctx, mode)
             c0 = ctx.launch_counts()
             lens[:] = L
@@ -74,6 +76,7 @@ def main() -> None:
             res[name]["seal"].append(t1 - t0)
             res[name]["open"].append(t2 - t1)
             res[name]["dev"].append((c1["snappy_enc"] - c0["snappy_enc"], c1["snappy_dec"] - c0["snappy_dec"]))
+            ctx.close()
     for name, r in res.items():
         s, o = float(np.median(r["seal"])), float(np.median(r["open"]))
         print(json.dumps({"setting": name, "value": round(2 * N * L / (s + o) / 2**30, 2),

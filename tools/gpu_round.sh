@@ -211,6 +211,12 @@ for s in $STEPS; do
     c3time)  # config 3's four forms timed in one process, interleaved
       timeout -k 10 300 python3 tools/exp_config3_traffic.py time 7 > $OUT/c3_forms_time.json 2> $OUT/c3_forms_time.err
       check c3time $? ;;
+    chainpin)  # config 5 from host memory, codec workers pinned per physical core vs left to the scheduler
+      timeout -k 10 400 python3 tools/exp_chain_pin.py 2 > $OUT/chain_pin.jsonl 2> $OUT/chain_pin.err
+      check chainpin $? ;;
+    sntests)  # the snappy / config-5 suites
+      timeout -k 10 600 python3 -u -m pytest tests/test_gpu_snappy.py tests/test_gpu_config5.py -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/sn_tests.txt 2>&1
+      check sntests $? ;;
     pcieaftrace)  # the after-free rows under the profiler, kernel trace only: with --memory-copy-trace rocprofv3's own
                   # finalization faults at exit for torch copies on side streams (tools/README.md, crashmin)
       timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/trace_pcieaf -o t -- python3 tools/microbench/pcie.py --after-free 90 > $OUT/trace_pcieaf.log 2>&1
