@@ -100,13 +100,37 @@ class GPUContext {
     std::mutex mu_;
 };
 
+// The process-wide device set of the reference-signature NewAES(secret, salt) below, as
+// go/crypto/aes_gpu.go's Devices(): created on first use from QGCM_DEVICES ("0,1,...", default every
+// visible device) and QGCM_MAX_PEERS (default 4096) as a qgcm_group, one member context per device;
+// a key lives on member hash(slot) mod G.  A slot goes back to the set when its AES is destroyed.
+class DeviceSet {
+  public:
+    static std::pair<std::shared_ptr<DeviceSet>, Error> Get();
+    ~DeviceSet();
+    qgcm_group *handle() const { return grp_; }
+    std::pair<uint32_t, Error> AllocSlot();
+    void Release(uint32_t slot);
+
+  private:
+    DeviceSet(qgcm_group *g, uint32_t max_keys) : grp_(g), max_(max_keys) {}
+    qgcm_group *grp_;
+    uint32_t max_;
+    uint32_t next_ = 0;
+    std::vector<uint32_t> free_;
+    std::mutex mu_;
+};
+
 // crypto/aes.go:22-26, bound to a device key slot.  Encrypt / Decrypt are virtual so that a test or
 // baseline harness can run the same plugin chain over another AES-GCM (oracle/cpu_chain.cpp: the
 // reference's CPU configuration with OpenSSL standing in for Go's crypto/cipher).
 class AES {
   public:
-    AES(std::shared_ptr<GPUContext> g, uint32_t slot) : g_(std::move(g)), slot_(slot) {}
-    virtual ~AES() = default;
+    AES(std::shared_ptr<GPUContext> g, uint32_t slot) : g_(std::move(g)), ctx_(g_->handle()), slot_(slot) {}
+    AES(std::shared_ptr<DeviceSet> d, qgcm_ctx *member, uint32_t slot) : d_(std::move(d)), ctx_(member), slot_(slot) {}
+    virtual ~AES() {
+        if (d_) d_->Release(slot_);
+    }
     int EncryptedSize(common::Slice data) const { return (int)data.len + Overhead + NonceSize; }  // :29-31
     int DecryptedSize(common::Slice data) const { return (int)data.len - Overhead - NonceSize; }  // :34-36
     // crypto/aes.go:41-52: seals data[0:length] in place with a fresh random nonce, appends tag and
@@ -122,11 +146,15 @@ class AES {
 
   private:
     std::shared_ptr<GPUContext> g_;
+    std::shared_ptr<DeviceSet> d_;
+    qgcm_ctx *ctx_ = nullptr;
     uint32_t slot_ = 0;
 };
 
 // crypto/aes.go:65-83: PBKDF2-HMAC-SHA512(secret, salt, 10000, 32) on the host, key schedule and
-// GHASH tables on the device.
+// GHASH tables on the device.  NewAES(secret, salt) is the reference's signature, on the process-wide
+// DeviceSet; the other form installs the key in a given context.
+std::pair<std::shared_ptr<AES>, Error> NewAES(common::Slice secret, common::Slice salt);
 std::pair<std::shared_ptr<AES>, Error> NewAES(const std::shared_ptr<GPUContext> &g, common::Slice secret,
                                               common::Slice salt);
 
@@ -148,6 +176,11 @@ struct Mapping {
 // node's private ones; {nullptr, nil} when the peer published no keys.
 std::pair<std::shared_ptr<crypto::AES>, Error> MappingAES(const std::shared_ptr<crypto::GPUContext> &g,
                                                           const std::vector<uint8_t> &publicKey,
+                                                          const std::vector<uint8_t> &publicSalt,
+                                                          const std::vector<uint8_t> &privateKey,
+                                                          const std::vector<uint8_t> &privateSalt);
+// the same through crypto::NewAES(secret, salt), as ParseMapping calls it
+std::pair<std::shared_ptr<crypto::AES>, Error> MappingAES(const std::vector<uint8_t> &publicKey,
                                                           const std::vector<uint8_t> &publicSalt,
                                                           const std::vector<uint8_t> &privateKey,
                                                           const std::vector<uint8_t> &privateSalt);

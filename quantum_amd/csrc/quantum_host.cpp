@@ -3,6 +3,7 @@
 #include "../../include/quantum.hpp"
 
 #include <errno.h>
+#include <stdlib.h>
 #include <sys/random.h>
 
 #include <algorithm>
@@ -68,7 +69,7 @@ std::pair<uint32_t, Error> GPUContext::AllocSlot() {
 std::pair<int, Error> AES::Encrypt(common::Slice data, int length, common::Slice additional) const {
     if (length < 0 || (size_t)length + Overhead + NonceSize > data.cap)
         return {-1, Error{"crypto: buffer too small for the tag and nonce"}};
-    const long n = qgcm_seal_one(g_->handle(), slot_, data.data, length, additional.len ? additional.data : nullptr,
+    const long n = qgcm_seal_one(ctx_, slot_, data.data, length, additional.len ? additional.data : nullptr,
                                  (uint32_t)additional.len, nullptr);
     if (n < 0) return {-1, Error{"qgcm_seal_one failed"}};
     return {(int)n, Error{}};
@@ -76,10 +77,84 @@ std::pair<int, Error> AES::Encrypt(common::Slice data, int length, common::Slice
 
 // crypto/aes.go:57-62: returns DecryptedSize(data) together with the error, as Go does.
 std::pair<int, Error> AES::Decrypt(common::Slice data, common::Slice additional) const {
-    const long n = qgcm_open_one(g_->handle(), slot_, data.data, (long)data.len,
+    const long n = qgcm_open_one(ctx_, slot_, data.data, (long)data.len,
                                  additional.len ? additional.data : nullptr, (uint32_t)additional.len);
     if (n < 0) return {DecryptedSize(data), Error{"cipher: message authentication failed"}};
     return {(int)n, Error{}};
+}
+
+std::pair<std::shared_ptr<DeviceSet>, Error> DeviceSet::Get() {
+    static std::mutex mu;
+    static std::shared_ptr<DeviceSet> set;
+    static Error failed;
+    std::lock_guard<std::mutex> lk(mu);
+    if (set || !failed.ok()) return {set, failed};
+    std::vector<int> devs;
+    const char *spec = getenv("QGCM_DEVICES");
+    if (spec && *spec) {
+        for (const char *p = spec; *p;) {
+            char *e;
+            const long d = strtol(p, &e, 10);
+            if (e == p || d < 0) {
+                failed = Error{std::string("qgcm: QGCM_DEVICES=") + spec};
+                return {nullptr, failed};
+            }
+            devs.push_back((int)d);
+            p = *e == ',' ? e + 1 : e;
+        }
+    } else {
+        for (int d = 0; d < qgcm_device_count(); ++d) devs.push_back(d);
+    }
+    uint32_t peers = 4096;
+    if (const char *v = getenv("QGCM_MAX_PEERS"); v && *v) peers = (uint32_t)strtoul(v, nullptr, 10);
+    if (devs.empty() || peers == 0 || peers > QGCM_MAX_KEYS) {
+        failed = Error{"qgcm: no device set (QGCM_DEVICES / QGCM_MAX_PEERS)"};
+        return {nullptr, failed};
+    }
+    char err[QGCM_ERRLEN] = {0};
+    qgcm_group *g = qgcm_group_create(devs.data(), (int)devs.size(), peers, err, (int)sizeof(err));
+    if (!g) {
+        failed = Error{err[0] ? err : "qgcm_group_create failed"};
+        return {nullptr, failed};
+    }
+    set.reset(new DeviceSet(g, peers));
+    return {set, Error{}};
+}
+
+DeviceSet::~DeviceSet() { qgcm_group_destroy(grp_); }
+
+std::pair<uint32_t, Error> DeviceSet::AllocSlot() {
+    std::lock_guard<std::mutex> g(mu_);
+    if (!free_.empty()) {
+        const uint32_t s = free_.back();
+        free_.pop_back();
+        return {s, Error{}};
+    }
+    if (next_ >= max_) return {0, Error{"qgcm: out of key slots (QGCM_MAX_PEERS)"}};
+    return {next_++, Error{}};
+}
+
+void DeviceSet::Release(uint32_t slot) {
+    std::lock_guard<std::mutex> g(mu_);
+    free_.push_back(slot);
+}
+
+// crypto/aes.go:65-83, the reference's signature: the process-wide DeviceSet, the key on its owner
+std::pair<std::shared_ptr<AES>, Error> NewAES(common::Slice secret, common::Slice salt) {
+    auto [d, derr] = DeviceSet::Get();
+    if (!derr.ok()) return {nullptr, derr};
+    uint8_t key[QGCM_KEY_BYTES];
+    if (qgcm_derive_key(secret.data, secret.len, salt.data, salt.len, key) != QGCM_OK)
+        return {nullptr, Error{"qgcm_derive_key failed"}};
+    auto [slot, err] = d->AllocSlot();
+    if (!err.ok()) return {nullptr, err};
+    qgcm_ctx *member = qgcm_group_ctx(d->handle(), qgcm_group_shard(d->handle(), slot));
+    const int rc = member ? qgcm_set_key(member, slot, key) : QGCM_E_ARG;
+    if (rc != QGCM_OK) {
+        d->Release(slot);
+        return {nullptr, Error{qgcm_strerror(rc)}};
+    }
+    return {std::make_shared<AES>(d, member, slot), Error{}};
 }
 
 // crypto/aes.go:65-83
@@ -134,6 +209,16 @@ std::pair<std::shared_ptr<crypto::AES>, Error> MappingAES(const std::shared_ptr<
     std::vector<uint8_t> secret = crypto::GenerateSharedSecret(publicKey, privateKey);
     std::vector<uint8_t> salt = crypto::GenerateSharedSecret(publicSalt, privateSalt);
     return crypto::NewAES(g, MakeSlice(secret), MakeSlice(salt));
+}
+
+std::pair<std::shared_ptr<crypto::AES>, Error> MappingAES(const std::vector<uint8_t> &publicKey,
+                                                          const std::vector<uint8_t> &publicSalt,
+                                                          const std::vector<uint8_t> &privateKey,
+                                                          const std::vector<uint8_t> &privateSalt) {
+    if (publicKey.empty() || publicSalt.empty()) return {nullptr, Error{}};
+    std::vector<uint8_t> secret = crypto::GenerateSharedSecret(publicKey, privateKey);
+    std::vector<uint8_t> salt = crypto::GenerateSharedSecret(publicSalt, privateSalt);
+    return crypto::NewAES(MakeSlice(secret), MakeSlice(salt));
 }
 
 }  // namespace common

@@ -8,6 +8,7 @@
 // (common/mapping.go:94-103: two peers derive the same key).
 // Usage: mirror_test [TestName ...]  (no names: all).  Exit status = number of failed tests.
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 #include <sys/random.h>
 
@@ -71,12 +72,13 @@ common::Mapping *testMapping() {
     return &m;
 }
 
+// crypto/crypto_test.go TestAES, with the reference's own call: NewAES(key, salt) on the process-wide
+// device set (QGCM_DEVICES, QGCM_MAX_PEERS; main() defaults them to "0,0" and 4)
 void TestAES() {
     const int tagLen = 16, nonceLen = 12, bufLen = 1500, dataLen = bufLen - tagLen - nonceLen;
-    if (!gpu()) FATAL("no GPU context");
     std::vector<uint8_t> key = asciiKey(), salt(crypto::SaltLength);
     randfill(salt.data(), salt.size());
-    auto [aes, err] = crypto::NewAES(gpu(), MakeSlice(key), MakeSlice(salt));
+    auto [aes, err] = crypto::NewAES(MakeSlice(key), MakeSlice(salt));
     if (!err.ok()) FATAL("Unable to create the AES object: " + err.msg);
     std::vector<uint8_t> buf(bufLen), expected(dataLen, 1);
     memset(buf.data(), 1, dataLen);
@@ -270,15 +272,91 @@ void TestMappingAES() {
     if (!e5.ok() || m != 1400 || !testEq(buf.data(), plain.data(), 1400)) FATAL("B cannot open A's packet");
 }
 
+// The device set hands out QGCM_MAX_PEERS slots; an AES gives its slot back when the last reference
+// to it goes, so a process that makes and drops peers forever never runs out.  A key sealed through
+// the device set opens through a plain context holding the same derived key (same salt, same slot
+// independence: the bytes depend on the key only).
+void TestNewAESSlotsRecycled() {
+    std::vector<uint8_t> key = asciiKey(), salt(crypto::SaltLength);
+    randfill(salt.data(), salt.size());
+    std::vector<std::shared_ptr<crypto::AES>> live;
+    for (int i = 0; i < 4; ++i) {
+        auto [a, err] = crypto::NewAES(MakeSlice(key), MakeSlice(salt));
+        if (!err.ok() || !a) FATAL("NewAES " + std::to_string(i) + ": " + err.msg);
+        live.push_back(a);
+    }
+    {
+        auto [a, err] = crypto::NewAES(MakeSlice(key), MakeSlice(salt));
+        if (a || err.ok()) FATAL("a fifth live AES must fail with QGCM_MAX_PEERS=4");
+    }
+    std::vector<uint8_t> buf(1500), plain;
+    randfill(buf.data(), buf.size());
+    plain = buf;
+    uint8_t ip[4] = {10, 0, 0, 7};
+    const Slice aad{ip, 4, 4};
+    for (int round = 0; round < 3; ++round) {
+        live.clear();  // every slot back
+        for (int i = 0; i < 4; ++i) {
+            auto [a, err] = crypto::NewAES(MakeSlice(key), MakeSlice(salt));
+            if (!err.ok() || !a) FATAL("recycled NewAES: " + err.msg);
+            live.push_back(a);
+        }
+    }
+    auto [ref, e0] = crypto::NewAES(gpu(), MakeSlice(key), MakeSlice(salt));
+    if (!e0.ok() || !ref) FATAL("context NewAES: " + e0.msg);
+    for (const auto &a : live) {
+        auto [n, e1] = a->Encrypt(MakeSlice(buf), 1400, aad);
+        if (!e1.ok() || n != 1428) FATAL("seal through the device set");
+        auto [m, e2] = ref->Decrypt(MakeSlice(buf).sub(0, 1428), aad);
+        if (!e2.ok() || m != 1400 || !testEq(buf.data(), plain.data(), 1400)) FATAL("context cannot open it");
+    }
+}
+
+// common/mapping.go:94-103 through the reference-signature NewAES: two peers, one on the device set and
+// one on a context, derive the same key
+void TestMappingAESDeviceSet() {
+    if (!gpu()) FATAL("no GPU context");
+    auto [apub, apriv] = crypto::GenerateECKeyPair();
+    auto [aspub, aspriv] = crypto::GenerateECKeyPair();
+    auto [bpub, bpriv] = crypto::GenerateECKeyPair();
+    auto [bspub, bspriv] = crypto::GenerateECKeyPair();
+    auto [ab, e1] = common::MappingAES(bpub, bspub, apriv, aspriv);
+    auto [ba, e2] = common::MappingAES(gpu(), apub, aspub, bpriv, bspriv);
+    if (!e1.ok() || !e2.ok() || !ab || !ba) FATAL("MappingAES: " + e1.msg + e2.msg);
+    auto [none, e3] = common::MappingAES({}, bspub, apriv, aspriv);
+    if (none || !e3.ok()) FATAL("a peer without keys must give a nil AES and no error");
+    std::vector<uint8_t> buf(900), plain;
+    randfill(buf.data(), buf.size());
+    plain = buf;
+    auto [n, e4] = ab->Encrypt(MakeSlice(buf), 800, Slice{});
+    if (!e4.ok() || n != 828) FATAL("seal with the A->B key");
+    auto [m, e5] = ba->Decrypt(MakeSlice(buf).sub(0, 828), Slice{});
+    if (!e5.ok() || m != 800 || !testEq(buf.data(), plain.data(), 800)) FATAL("B cannot open A's packet");
+}
+
+// no device set (a bad QGCM_DEVICES, or no GPU): NewAES returns the error, every time, and never a
+// half-made AES
+void TestNewAESNoDevices() {
+    std::vector<uint8_t> key = asciiKey(), salt(crypto::SaltLength, 3);
+    for (int i = 0; i < 2; ++i) {
+        auto [a, err] = crypto::NewAES(MakeSlice(key), MakeSlice(salt));
+        if (a || err.ok()) FATAL("NewAES must fail without a device set");
+    }
+}
+
 }  // namespace
 
 int main(int argc, char **argv) {
+    setenv("QGCM_DEVICES", "0,0", 0);  // two members on one GPU: the sharding is exercised on one card
+    setenv("QGCM_MAX_PEERS", "4", 0);
     const std::vector<std::pair<std::string, std::function<void()>>> tests = {
         {"TestAES", TestAES},         {"TestEcdh", TestEcdh},
         {"TestSorter", TestSorter},   {"TestEncryption", TestEncryption},
         {"TestCompression", TestCompression}, {"TestMulti", TestMulti},
         {"TestMock", TestMock},       {"TestPayload", TestPayload},
         {"TestEncryptionTamper", TestEncryptionTamper}, {"TestMappingAES", TestMappingAES},
+        {"TestNewAESSlotsRecycled", TestNewAESSlotsRecycled}, {"TestMappingAESDeviceSet", TestMappingAESDeviceSet},
+        {"TestNewAESNoDevices", TestNewAESNoDevices},
     };
     std::vector<std::string> want(argv + 1, argv + argc);
     int failed = 0, ran = 0;

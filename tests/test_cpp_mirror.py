@@ -11,13 +11,15 @@ from conftest import ROOT
 
 BIN = os.path.join(ROOT, "tests", "cpp", "mirror_test")
 CPU_TESTS = ["TestEcdh", "TestSorter", "TestCompression", "TestMock", "TestPayload"]
-GPU_TESTS = ["TestAES", "TestEncryption", "TestMulti", "TestEncryptionTamper", "TestMappingAES"]
+GPU_TESTS = ["TestAES", "TestEncryption", "TestMulti", "TestEncryptionTamper", "TestMappingAES",
+             "TestNewAESSlotsRecycled", "TestMappingAESDeviceSet"]
 
 
-def run(names, timeout=120):
+def run(names, timeout=120, env=None):
     if not os.path.exists(BIN):
         pytest.fail(f"{BIN} is missing: build it with __graft_entry__.build()")
-    r = subprocess.run([BIN, *names], capture_output=True, text=True, timeout=timeout)
+    r = subprocess.run([BIN, *names], capture_output=True, text=True, timeout=timeout,
+                       env=None if env is None else {**os.environ, **env})
     out = r.stdout + r.stderr
     assert r.returncode == 0, out
     for n in names:
@@ -27,6 +29,11 @@ def run(names, timeout=120):
 @pytest.mark.parametrize("name", CPU_TESTS)
 def test_cpp_mirror_cpu(name):
     run([name])
+
+
+def test_cpp_mirror_no_device_set():
+    """crypto::NewAES(secret, salt) with an unusable QGCM_DEVICES returns the error (no GPU is touched)."""
+    run(["TestNewAESNoDevices"], env={"QGCM_DEVICES": "x"})
 
 
 @pytest.mark.gpu
