@@ -139,6 +139,7 @@ struct Resident;
 // every other QGCM_* knob), not when the service is first started by a per-packet call
 struct ResidentConfig {
     uint64_t workers, slots, spin_us, spinners, idle_us, life_us, fail_after;
+    bool ahead;  // QGCM_RESIDENT_AHEAD: draw the next nonce and keystream ahead (default on)
 };
 ResidentConfig resident_config_from_env();
 Resident *resident_create(int device, const Batch &base, int num_cus, const ResidentConfig &cfg);  // nullptr: not available

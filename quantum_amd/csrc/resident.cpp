@@ -255,6 +255,7 @@ ResidentConfig resident_config_from_env() {
     c.idle_us = env_u64("QGCM_RESIDENT_IDLE_US", 2000);
     c.life_us = env_u64("QGCM_RESIDENT_LIFE_US", 8000);
     c.fail_after = env_u64("QGCM_RESIDENT_FAIL_AFTER", ~0ull);  // test hook
+    c.ahead = env_u64("QGCM_RESIDENT_AHEAD", 1) != 0;
     return c;
 }
 
@@ -296,7 +297,7 @@ Resident *resident_create(int device, const Batch &base, int num_cus, const Resi
     memset(r->devm, 0, o_in);  // stop words and records, through the BAR
     _mm_sfence();
     r->seqh.reset(new uint32_t[r->S]());
-    r->ahead = env_u64("QGCM_RESIDENT_AHEAD", 1) != 0;
+    r->ahead = cfg.ahead;
     r->next_nonce.reset(new uint8_t[12ull * r->S]());
     r->next_gen.reset(new uint32_t[r->S]());
     r->busy.reset(new std::atomic<uint32_t>[r->S]);

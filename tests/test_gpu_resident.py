@@ -381,7 +381,7 @@ def test_keystream_ahead_vs_oracle(torch, ahead, monkeypatch):
     the oracle with its drawn nonce, and with QGCM_RESIDENT_AHEAD=0 nothing is served ahead."""
     from quantum_amd.crypto import AES
 
-    monkeypatch.setenv("QGCM_RESIDENT_AHEAD", str(ahead))  # read when the first call starts the service
+    monkeypatch.setenv("QGCM_RESIDENT_AHEAD", str(ahead))  # read at qgcm_create
     ctx = make_ctx()
     try:
         keys = [bytes(range(90 + 7 * i, 122 + 7 * i)) for i in range(2)]
