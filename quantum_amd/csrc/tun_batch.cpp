@@ -45,12 +45,13 @@ constexpr unsigned kRingEntries = 256;
 
 struct Ring {
     int fd = -1;
-    unsigned *sq_tail = nullptr, *sq_mask = nullptr, *sq_array = nullptr;
+    unsigned *sq_head = nullptr, *sq_tail = nullptr, *sq_mask = nullptr, *sq_array = nullptr;
     unsigned *cq_head = nullptr, *cq_tail = nullptr, *cq_mask = nullptr;
     io_uring_sqe *sqes = nullptr;
     io_uring_cqe *cqes = nullptr;
     void *sq_ptr = nullptr, *cq_ptr = nullptr;
     size_t sq_len = 0, cq_len = 0, sqe_len = 0;
+    bool broken = false;
 
     bool init() {
         io_uring_params p{};
@@ -70,6 +71,7 @@ struct Ring {
         if (sq == MAP_FAILED) return fail();
         sqes = static_cast<io_uring_sqe *>(sq);
         auto at = [](void *base, unsigned off) { return reinterpret_cast<unsigned *>(static_cast<char *>(base) + off); };
+        sq_head = at(sq_ptr, p.sq_off.head);
         sq_tail = at(sq_ptr, p.sq_off.tail);
         sq_mask = at(sq_ptr, p.sq_off.ring_mask);
         sq_array = at(sq_ptr, p.sq_off.array);
@@ -117,15 +119,18 @@ int read_mode() {
 Ring *ring() {
     if (read_mode() != 1) return nullptr;
     if (tl_ring_state == 0) tl_ring_state = tl_ring.init() ? 1 : -1;
-    return tl_ring_state > 0 ? &tl_ring : nullptr;
+    return tl_ring_state > 0 && !tl_ring.broken ? &tl_ring : nullptr;
 }
 
 // Up to k (<= kRingEntries) non-blocking reads into slots [first, first + k), one submission; the
 // packets that were queued land in those slots, holes (a read that found the queue empty while a
 // later one found a packet that had just arrived) are closed up.  Returns how many landed (lens set),
-// or -1 when the ring failed (nothing consumed: the caller falls back).
+// or -1 when the ring took no read (nothing consumed: the caller falls back).  What was submitted is
+// read off the kernel's SQ head, not the return value: an io_uring_enter interrupted while it waits
+// for completions has still submitted its reads, and a partial submission leaves the rest queued.
 int uring_drain(Ring &r, int fd, uint8_t *arena, uint64_t stride, uint32_t first, uint32_t k, uint32_t *lens) {
-    unsigned tail = *r.sq_tail;
+    const unsigned tail0 = *r.sq_tail;  // == the SQ head: every earlier entry was taken or withdrawn
+    unsigned tail = tail0;
     for (uint32_t j = 0; j < k; ++j) {
         const unsigned idx = tail & *r.sq_mask;
         io_uring_sqe &e = r.sqes[idx];
@@ -145,27 +150,34 @@ int uring_drain(Ring &r, int fd, uint8_t *arena, uint64_t stride, uint32_t first
     do {
         sub = (int)syscall(__NR_io_uring_enter, r.fd, k, k, IORING_ENTER_GETEVENTS, nullptr, 0);
     } while (sub < 0 && errno == EINTR);
-    if (sub != (int)k) return -1;
-    // every read completed inline (RWF_NOWAIT): reap k completions
+    const unsigned took = __atomic_load_n(r.sq_head, __ATOMIC_ACQUIRE) - tail0;
+    if (took < k) __atomic_store_n(r.sq_tail, tail0 + took, __ATOMIC_RELEASE);  // withdraw the rest
+    if (took == 0) return -1;
+    // the taken reads (entries 0 .. took-1, in order) complete inline under RWF_NOWAIT: reap them all,
+    // waiting if need be -- a completion left behind would be read as the next batch's
     static thread_local int32_t res[kRingEntries];
+    for (uint32_t j = 0; j < took; ++j) res[j] = -EAGAIN;
     unsigned head = *r.cq_head, seen = 0;
-    while (seen < k) {
+    while (seen < took) {
         const unsigned ctail = __atomic_load_n(r.cq_tail, __ATOMIC_ACQUIRE);
-        for (; head != ctail && seen < k; ++head, ++seen) {
+        for (; head != ctail && seen < took; ++head, ++seen) {
             const io_uring_cqe &c = r.cqes[head & *r.cq_mask];
-            res[c.user_data] = c.res;
+            if (c.user_data < kRingEntries) res[c.user_data] = c.res;
         }
         __atomic_store_n(r.cq_head, head, __ATOMIC_RELEASE);
-        if (seen < k) {
+        if (seen < took) {
             int w;
             do {
-                w = (int)syscall(__NR_io_uring_enter, r.fd, 0, k - seen, IORING_ENTER_GETEVENTS, nullptr, 0);
+                w = (int)syscall(__NR_io_uring_enter, r.fd, 0, took - seen, IORING_ENTER_GETEVENTS, nullptr, 0);
             } while (w < 0 && errno == EINTR);
-            if (w < 0) return -1;
+            if (w < 0) {  // cannot wait: keep what completed; the ring is not used again (late completions)
+                r.broken = true;
+                break;
+            }
         }
     }
     uint32_t got = 0;
-    for (uint32_t j = 0; j < k; ++j) {
+    for (uint32_t j = 0; j < took; ++j) {
         if (res[j] < 0) continue;
         if (got != j)
             memmove(arena + (uint64_t)(first + got) * stride + kPacketStart,
