@@ -131,6 +131,9 @@ class AES {
     virtual ~AES() {
         if (d_) d_->Release(slot_);
     }
+    // one owner per key slot: a copy would give the slot back twice
+    AES(const AES &) = delete;
+    AES &operator=(const AES &) = delete;
     int EncryptedSize(common::Slice data) const { return (int)data.len + Overhead + NonceSize; }  // :29-31
     int DecryptedSize(common::Slice data) const { return (int)data.len - Overhead - NonceSize; }  // :34-36
     // crypto/aes.go:41-52: seals data[0:length] in place with a fresh random nonce, appends tag and
