@@ -408,8 +408,8 @@ struct GWave {
 // encodeBlock per group.  The miss probes are software-pipelined: probe positions do not depend on
 // the data (each miss moves on by skip >> 5, skip += step), so the word at the probe after next is
 // loaded one probe early and the next probe's table entry is read as soon as the current entry is
-// written.  A miss then waits for one LDS round trip (the candidate's word) instead of two (the table
-// entry, then the candidate's word).  The early table read is issued after the current probe's table
+// written, together with the candidate's word.  A miss then waits for one LDS round trip instead of
+// two (the table entry, then the candidate's word).  The early table read is issued after the current probe's table
 // write (LDS operations of a wave complete in order), so it sees that write; the bytes are those of
 // encodeBlock.
 __device__ uint32_t gencode_block(const GWave &w, uint32_t op, uint32_t n, uint32_t bits) {
@@ -428,9 +428,21 @@ __device__ uint32_t gencode_block(const GWave &w, uint32_t op, uint32_t n, uint3
         skip += step;
         w.tab[h] = (uint16_t)s;
         const uint32_t hn = hash4(nv, shift);
-        const uint32_t cn = w.tab[hn];  // after the write above: tab[hn] as the next probe sees it
-        const uint32_t nv2 = w.load32(min(next_s + (skip >> 5), n));  // the probe after next (clamped)
-        if (cur != w.load32(cand)) {  // miss: probe further on
+        // Every LDS read of the probe -- tab[hn] (after the write above, so as the next probe sees
+        // it), the word at the probe after next (clamped) and the candidate's word -- is issued
+        // before any result is used, so a probe costs one LDS round trip.  Without the fence the
+        // compiler sinks the next probe's reads (used on the miss path only) below the compare, and
+        // each miss waited for two: compress 4.05-4.10 -> 3.67-3.75 ms per 2^20 config-5 packets
+        // (profiles/r5_s11, interleaved A/B).
+        const uint32_t *iw = reinterpret_cast<const uint32_t *>(w.in);
+        const uint32_t o2 = min(next_s + (skip >> 5), n);
+        const uint32_t cn = w.tab[hn];
+        const uint32_t a0 = iw[o2 >> 2], a1 = iw[(o2 >> 2) + 1];
+        const uint32_t b0 = iw[cand >> 2], b1 = iw[(cand >> 2) + 1];
+        asm volatile("" ::: "memory");
+        const uint32_t nv2 = __builtin_amdgcn_alignbyte(a1, a0, o2 & 3);
+        const uint32_t cw = __builtin_amdgcn_alignbyte(b1, b0, cand & 3);
+        if (cur != cw) {  // miss: probe further on
             s = next_s;
             cur = nv;
             h = hn;
