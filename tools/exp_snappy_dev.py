@@ -3,7 +3,7 @@ random, second half a repeated HTTP line, stride 1472): compress, seal, open, un
 by HIP events; the sealed arena is checked against tests/golden/config5_digest.json and the result
 against the plaintext arena (bench.extra_config5_resident).  The encoders alternate in one process,
 `rounds` times each: QGCM_SNAPPY_GROUP=1, four packets per wave (the default), and 0, one wave per
-packet.
+packet (SNAP_GROUPS="1,2" compares other settings, e.g. a temporary variant wired to 2 for an A/B).
 
     python3 tools/exp_snappy_dev.py [reps] [rounds]
 """
@@ -21,7 +21,7 @@ def main() -> None:
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 2
     key = bench.derive_key(bench.SECRET, bench.SALT)
     for r in range(rounds):
-        for grp in ("1", "0"):
+        for grp in os.environ.get("SNAP_GROUPS", "1,0").split(","):
             os.environ["QGCM_SNAPPY_GROUP"] = grp
             res = bench.extra_config5_resident(key, reps, verify=(r == 0))
             print(json.dumps({"snappy_group": int(grp), **res}), flush=True)
