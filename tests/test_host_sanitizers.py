@@ -1,7 +1,8 @@
 """Host code under sanitizers (SURVEY.md §5 "use TSan/ASan on host lib tests"): the snappy codec and
 the key math of libqgcm (host-only C++, no HIP) built with g++ -fsanitize=address,undefined and with
 -fsanitize=thread, driven by tests/cpp/san_driver.cpp (round trips, malformed streams into
-exact-size buffers, the threaded slot codec).  Any report fails the test."""
+exact-size buffers, the threaded slot codec); the batched TUN and UDP I/O under ASan/UBSan
+(tests/cpp/tun_san_driver.cpp, udp_san_driver.cpp).  Any report fails the test."""
 import os
 import shutil
 import subprocess
@@ -57,4 +58,20 @@ def test_asan_ubsan_tun_reads(tmp_path, mode):
     if r.returncode == 77:
         pytest.skip("TUN device refused")
     assert r.returncode == 0 and "tun driver ok" in r.stdout, r.stdout + r.stderr
+    assert "runtime error" not in r.stderr and "ERROR: AddressSanitizer" not in r.stderr, r.stderr
+
+
+def test_asan_ubsan_udp_batches(tmp_path):
+    """quantum_amd/csrc/udp_batch.cpp under ASan/UBSan (tests/cpp/udp_san_driver.cpp): 2000 loopback
+    datagrams of 1..1472 B through sendmmsg / recvmmsg slot batches, back in order and intact."""
+    if shutil.which("g++") is None:
+        pytest.skip("no g++")
+    exe = tmp_path / "udp_san_driver"
+    cmd = ["g++", "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined",
+           "-fno-sanitize-recover=undefined", f"-I{ROOT}/include", os.path.join(ROOT, "tests", "cpp", "udp_san_driver.cpp"),
+           os.path.join(CSRC, "udp_batch.cpp"), "-o", str(exe)]
+    subprocess.run(cmd, check=True, capture_output=True, timeout=300)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0"))
+    assert r.returncode == 0 and "udp driver ok" in r.stdout, r.stdout + r.stderr
     assert "runtime error" not in r.stderr and "ERROR: AddressSanitizer" not in r.stderr, r.stderr
