@@ -15,6 +15,8 @@
 #include <atomic>
 #include <chrono>
 #include <memory>
+#include <future>
+#include <map>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -61,8 +63,10 @@ struct qgcm_ctx {
     bool snappy_group = true;
     // the chain's host codec workers run one per physical core, the GPU's NUMA-local cores and the least
     // busy first (cpu_topo.cpp; QGCM_CHAIN_PIN=0 at qgcm_create: left to the scheduler).  The core list
-    // is taken at the first chained call (a 30-ms sample of the host's load) and kept.
+    // comes from a 30-ms sample of the host's load, taken once per device and process in the background
+    // from the first qgcm_create on (codec_cpu_list), and is kept from the context's first chained call.
     bool chain_pin = true;
+    std::shared_future<std::vector<int>> codec_cpus_pending;
     std::once_flag codec_cpus_once;
     std::vector<int> codec_cpus;
     uint32_t *d_rk = nullptr;
@@ -515,6 +519,23 @@ struct BigRelease {
 
 }  // namespace
 
+// The chain's codec core list for a device (qgcm_ctx::chain_pin): sampled once per process, off the
+// caller's path -- the first context of a device starts the 30-ms load sample, later ones share it.
+static std::shared_future<std::vector<int>> codec_cpu_list(int device) {
+    static std::mutex mu;
+    static std::map<int, std::shared_future<std::vector<int>>> lists;
+    std::lock_guard<std::mutex> g(mu);
+    auto it = lists.find(device);
+    if (it != lists.end()) return it->second;
+    auto f = std::async(std::launch::async, [device] {
+                 cpu_set_t local;
+                 const bool have = qgcm::gpu_local_cpus(device, &local) > 0;
+                 return qgcm::spread_cpus(have ? &local : nullptr, 30);
+             }).share();
+    lists.emplace(device, f);
+    return f;
+}
+
 extern "C" {
 
 const char *qgcm_version(void) { return "qgcm 0.1.0 (gfx950)"; }
@@ -647,6 +668,7 @@ qgcm_ctx *qgcm_create(int device, uint32_t max_keys, char *err, int errlen) {
         qgcm_destroy(ctx);
         return nullptr;
     }
+    if (ctx->chain_pin) ctx->codec_cpus_pending = codec_cpu_list(ctx->device);
     return ctx;
 }
 
@@ -1140,9 +1162,7 @@ static int run_host_chain(qgcm_ctx *ctx, bool seal, uint8_t *h_arena, uint64_t s
     const int nt = (seal && dev_ok && dev_mode == 2) ? 0 : std::max(1, std::min(threads, 256));
     if (ctx->chain_pin && nt > 0)
         std::call_once(ctx->codec_cpus_once, [ctx] {
-            cpu_set_t local;
-            const bool have = qgcm::gpu_local_cpus(ctx->device, &local) > 0;
-            ctx->codec_cpus = qgcm::spread_cpus(have ? &local : nullptr, 30);
+            if (ctx->codec_cpus_pending.valid()) ctx->codec_cpus = ctx->codec_cpus_pending.get();
         });
     const std::vector<int> *pin = ctx->chain_pin && !ctx->codec_cpus.empty() ? &ctx->codec_cpus : nullptr;
     for (int t = 0; t < nt; ++t)
@@ -1321,11 +1341,25 @@ static int run_snappy(qgcm_ctx *ctx, bool compress, uint8_t *d_arena, uint64_t s
     a.off_in = tab;
     a.off_out = a.off_in + a16(max_in + 24);  // + the 16-B chunks' overhang and stage_in's slack dwords
     a.off_sink = a.off_out + a16((compress ? (uint32_t)qgcm_snappy_max_compressed_length(max_in) : limit) + 8);
-    // the encoder (QGCM_SNAPPY_GROUP at qgcm_create, A/B knob): 1 (default) = four packets per wave, output straight
-    // into the slot (the region: table + the input staged up to max(len, limit) bytes, the restore
-    // copy); 0 = one wave per packet.  Packets past ~5 KiB need more LDS than four regions per wave can
-    // have, and limit 0 fails every packet: one wave per packet.  The decoder is one wave per packet.
+    // the codec (QGCM_SNAPPY_GROUP at qgcm_create, A/B knob): 1 (default) = four packets per wave --
+    // the encoder's output straight into the slot (the region: table + the input staged up to max(len,
+    // limit) bytes, the restore copy), the decoder's region [input | output | lane scratch]; 0 = one
+    // wave per packet.  Packets past ~5 KiB (encoder) or whose regions pass 16 KiB (decoder) need more
+    // LDS than four regions per wave can have, and limit 0 fails every packet: one wave per packet.
     bool group = compress && limit > 0 && ctx->snappy_group;
+    bool gdec = !compress && ctx->snappy_group;  // the four-packets-per-wave decoder
+    uint32_t gregion = 0;
+    if (gdec) {  // [staged input | output | 64 B of lane scratch] per packet, four per wave
+        a.off_in = 0;
+        a.off_out = a16(max_in + 24);
+        a.off_sink = a.off_out + a16(limit + 8);
+        gregion = a.off_sink + 64;
+        if (kSnapGroup * gregion > 64u * 1024u) {  // back to the wave decoder's layout
+            gdec = false;
+            a.off_out = a.off_in + a16(max_in + 24);
+            a.off_sink = a.off_out + a16(limit + 8);
+        }
+    }
     if (group) {
         a.off_out = a.off_in + a16(std::max(max_in, limit) + 24);
         a.off_sink = a.off_out;
@@ -1335,8 +1369,8 @@ static int run_snappy(qgcm_ctx *ctx, bool compress, uint8_t *d_arena, uint64_t s
             a.off_sink = a.off_out + a16((uint32_t)qgcm_snappy_max_compressed_length(max_in) + 8);
         }
     }
-    a.wave_bytes = group ? kSnapGroup * a.off_sink : a.off_sink + 256;
-    const uint32_t per_wave = group ? kSnapGroup : 1;
+    a.wave_bytes = group ? kSnapGroup * a.off_sink : gdec ? kSnapGroup * gregion : a.off_sink + 256;
+    const uint32_t per_wave = group || gdec ? kSnapGroup : 1;
     int waves = group ? 1 : 4;
     while (waves > 1 && (size_t)waves * a.wave_bytes > 64u * 1024u) --waves;
     int per_cu = (int)((160u * 1024u) / ((uint32_t)waves * a.wave_bytes));
@@ -1345,7 +1379,7 @@ static int run_snappy(qgcm_ctx *ctx, bool compress, uint8_t *d_arena, uint64_t s
     const int grid = (int)std::min<uint64_t>(need, (uint64_t)ctx->num_cus * per_cu);
     if (hipSetDevice(ctx->device) != hipSuccess) return QGCM_E_HIP;
     ctx->count(compress ? QGCM_KERNEL_SNAPPY_ENC : QGCM_KERNEL_SNAPPY_DEC);
-    return hip_fail(launch_snappy(compress, a, waves, grid, s, group));
+    return hip_fail(launch_snappy(compress, a, waves, grid, s, group ? 1 : gdec ? 2 : 0));
 }
 
 int qgcm_snappy_compress_batch(qgcm_ctx *ctx, uint8_t *d_arena, uint64_t stride, uint32_t n, uint32_t *d_lens,

@@ -4,6 +4,10 @@
 // payload.Packet) and the copy back into Payload.Raw[4:] that Apply does (compression.go:39-51), for
 // a batch of Payload.Raw slots at i * stride in device memory.
 //
+// The default codec (QGCM_SNAPPY_GROUP=1) codes four packets per wave, one per 16-lane group: the
+// group encoder and the group decoder below.  The forms with one wave per packet come first; they
+// also serve packets too long for four LDS regions per wave.
+//
 // One wave per packet.  The encoder is the block algorithm of golang/snappy's encodeBlock (restated
 // in snappy_codec.cpp and oracle/snappy_oracle.py, pinned to libsnappy 1.1.8's bytes): its probe /
 // insert sequence is inherently serial, so the wave runs it as one uniform control flow (every value
@@ -288,8 +292,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) s
 // store (no exec branch per store).  Match extension compares 4 bytes per lane (64 B per group step);
 // literal copies move 4 bytes per lane.  Per packet: [hash table | staged input] in LDS (a.off_in
 // within a region of a.off_sink bytes), four regions per wave; the output goes straight into the slot.
-// The decoder stays one wave per packet: a four-packets-per-wave decoder measured no faster
-// (DESIGN.md 4.6).
+// The group decoder is at the end of the file.
 constexpr uint32_t kGrp = 4, kGL = 64 / kGrp;
 
 // Group prefetch: the next packets' first bytes -- kGPf 16-B loads per lane, 1.5 KiB per packet
@@ -662,15 +665,163 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) s
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Group decoder: four packets per wave, one per 16-lane group.  The wave decoder above runs each
+// element's parse as wave-uniform scalar code for one packet, and the CU's one scalar unit is its
+// bound; here each group parses its own packet in VGPRs (the same values in its 16 lanes), so one
+// instruction stream serves four packets.  An element header comes from one two-dword window; a
+// literal moves 4 bytes per lane per step; a back-reference (<= 64 bytes) is four reads then four
+// writes per lane (i = gl, gl + 16, ...: out[op - off + i mod off], bytes earlier elements wrote), the
+// lanes past the element writing into their scratch word.  Per packet: [staged input | output |
+// 64 B of scratch] in LDS, wave_bytes / 4 bytes, four per wave.
+struct GDec {
+    uint8_t *in, *out, *sink;  // sink: this lane's scratch word
+    uint32_t gl;
+    __device__ __forceinline__ uint32_t load32(uint32_t o) const {
+        const uint32_t *w = reinterpret_cast<const uint32_t *>(in);
+        return __builtin_amdgcn_alignbyte(w[(o >> 2) + 1], w[o >> 2], o & 3);
+    }
+};
+
+// i % off for i < 64 and off >= 1 without a division: off >= 64 leaves i; below that the quotient of a
+// float reciprocal with a half-step margin ((i + 0.5) / off is at least 1/128 from an integer, far more
+// than the reciprocal's error; every (i, off) pair checked exhaustively), corrected once each way
+__device__ __forceinline__ uint32_t mod64(uint32_t i, uint32_t off) {
+    if (off >= 64) return i;
+    const uint32_t q = (uint32_t)(((float)i + 0.5f) * __builtin_amdgcn_rcpf((float)off));
+    int m = (int)i - (int)(q * off);
+    m = m < 0 ? m + (int)off : m;
+    return (uint32_t)(m >= (int)off ? m - (int)off : m);
+}
+
+// decode.go Decode of in[0..n) into out (at most cap bytes), per group; returns the length or -1
+__device__ int gdecode(const GDec &w, uint32_t n, uint32_t cap) {
+    const uint32_t *iw = reinterpret_cast<const uint32_t *>(w.in);
+    uint32_t total = 0, ip = 0;
+    {
+        const uint64_t x = ((uint64_t)iw[1] << 32) | iw[0];  // the staging's 8 B of slack cover n < 8
+        for (uint32_t sh = 0;; sh += 7) {
+            if (ip >= n || ip >= 5) return -1;
+            const uint32_t c = (uint32_t)(x >> (8 * ip)) & 0xffu;
+            ++ip;
+            if (sh == 28 && (c & 0x7f) > 15) return -1;  // > 32 bits
+            total |= (c & 0x7f) << sh;
+            if (c < 0x80) break;
+        }
+    }
+    if (total > cap) return -1;
+    uint32_t op = 0;
+    while (ip < n) {
+        const uint32_t q = ip >> 2;
+        const uint64_t x = (((uint64_t)iw[q + 1] << 32) | iw[q]) >> (8 * (ip & 3));
+        const uint32_t tag = (uint32_t)x & 0xffu;
+        ++ip;
+        uint32_t len, off;
+        if ((tag & 3) == 0) {
+            len = tag >> 2;
+            if (len >= 60) {
+                const uint32_t b = len - 59;  // 1..4 little-endian length bytes
+                if (ip + b > n) return -1;
+                len = (uint32_t)(x >> 8) & (0xffffffffu >> (32 - 8 * b));
+                ip += b;
+                if (len >= 0xffffffffu) return -1;
+            }
+            ++len;
+            if (len > n - ip || len > total - op) return -1;
+            for (uint32_t j = 4 * w.gl; j < len; j += 4 * kGL) {  // 4 bytes per lane, the tail to the sink
+                const uint32_t v = w.load32(ip + j);
+#pragma unroll
+                for (uint32_t t = 0; t < 4; ++t) *(j + t < len ? w.out + op + j + t : w.sink) = (uint8_t)(v >> (8 * t));
+            }
+            ip += len;
+            op += len;
+            continue;
+        }
+        if ((tag & 3) == 1) {
+            if (ip + 1 > n) return -1;
+            len = 4 + ((tag >> 2) & 7);
+            off = ((tag >> 5) << 8) | ((uint32_t)(x >> 8) & 0xffu);
+            ip += 1;
+        } else if ((tag & 3) == 2) {
+            if (ip + 2 > n) return -1;
+            len = 1 + (tag >> 2);
+            off = (uint32_t)(x >> 8) & 0xffffu;
+            ip += 2;
+        } else {
+            if (ip + 4 > n) return -1;
+            len = 1 + (tag >> 2);
+            off = (uint32_t)(x >> 8);
+            ip += 4;
+        }
+        if (off == 0 || off > op || len > total - op) return -1;
+        uint8_t v[4];
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) v[k] = w.out[op - off + mod64(w.gl + kGL * k, off)];
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+            const uint32_t i = w.gl + kGL * k;
+            *(i < len ? w.out + op + i : w.sink) = v[k];
+        }
+        op += len;
+    }
+    return op == total ? (int)total : -1;
+}
+
+__global__ void __launch_bounds__(256) snappy_uncompress_group_kernel(SnapArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint32_t lane = lane_id(), wv = threadIdx.x >> 6, waves = blockDim.x >> 6;
+    const uint32_t grp = lane / kGL, gl = lane % kGL, region = a.wave_bytes / kGrp;
+    uint8_t *base = smem + (wv * kGrp + grp) * region;
+    const GDec w{base + a.off_in, base + a.off_out, base + a.off_sink + 4 * gl, gl};
+    const uint32_t step = gridDim.x * waves * kGrp, cover = gpf_cover(a.stride);
+    GPrefetch f{};
+    gpf_issue(f, a, (blockIdx.x * waves + wv) * kGrp + grp, gl, cover);
+    for (uint32_t p0 = (blockIdx.x * waves + wv) * kGrp; p0 < a.n; p0 += step) {
+        const uint32_t p = p0 + grp;
+        const bool have = p < a.n;
+        const uint32_t stored = have ? f.len : 0u;
+        const bool auth = have && f.st == 1;  // status_in: packets that failed to open are left to the caller
+        const uint32_t len = stored >= a.sub ? stored - a.sub : stored;
+        uint8_t *slot = a.arena + (uint64_t)(have ? p : 0u) * a.stride;
+        const bool take = auth && stored >= a.sub && len <= a.max_in;
+        if (take) gstage(w.in, slot, len, gl, cover, f);
+        gpf_issue(f, a, p + step, gl, cover);  // in flight while these packets are decoded
+        wave_lds_sync();
+        int u = -1;
+        if (take) {
+            u = gdecode(w, len, a.limit);
+            // an empty result fails: golang/snappy's Decode(nil, src) returns a nil slice for it and
+            // compression.go:37-39 drops a nil packet
+            if (u == 0) u = -1;
+        }
+        wave_lds_sync();
+        if (u > 0) {  // LDS [0, u) -> slot bytes [4, 4 + u)
+            uint32_t *dst = reinterpret_cast<uint32_t *>(slot + 4);
+            const uint32_t *srcw = reinterpret_cast<const uint32_t *>(w.out);
+            const uint32_t nw = (uint32_t)u >> 2;
+            for (uint32_t j = gl; j < nw; j += kGL) dst[j] = srcw[j];
+            const uint32_t t = (uint32_t)u & 3;
+            if (gl < t) slot[4 + 4 * nw + gl] = w.out[4 * nw + gl];
+        }
+        if (auth && gl == 0) {
+            a.lens[p] = u > 0 ? (uint32_t)u : len;  // failed: the compressed length (sub = 0: unchanged)
+            if (a.status) a.status[p] = u > 0 ? 1 : 0;
+        }
+        wave_lds_sync();  // the next packets' staging overwrites these ones' LDS
+    }
+}
+
 }  // namespace
 
-hipError_t launch_snappy(bool compress, const SnapArgs &a, int waves_per_wg, int grid, hipStream_t s, bool group) {
+hipError_t launch_snappy(bool compress, const SnapArgs &a, int waves_per_wg, int grid, hipStream_t s, int group) {
     const size_t lds = (size_t)waves_per_wg * a.wave_bytes;
     const dim3 g(grid), b(64 * waves_per_wg);
     if (compress && group)
         hipLaunchKernelGGL(snappy_compress_group_kernel, g, b, lds, s, a);
     else if (compress)
         hipLaunchKernelGGL(snappy_compress_kernel, g, b, lds, s, a);
+    else if (group == 2)
+        hipLaunchKernelGGL(snappy_uncompress_group_kernel, g, b, lds, s, a);
     else
         hipLaunchKernelGGL(snappy_uncompress_kernel, g, b, lds, s, a);
     return hipGetLastError();

@@ -100,7 +100,7 @@ def encoder_ctxs(torch):
         c.close()
 
 
-@pytest.fixture(params=["1", "0"], ids=["group_encoder", "wave_encoder"])
+@pytest.fixture(params=["1", "0"], ids=["group_codec", "wave_codec"])
 def encoder(request, encoder_ctxs):
     """QGCM_SNAPPY_GROUP (at qgcm_create): 1 = four packets per wave, pipelined miss probes, output
     straight into the slot, the next packets prefetched (the default); 0 = one wave per packet.  Both
@@ -195,7 +195,8 @@ def test_device_compress_failures_untouched(torch, encoder):
         assert np.array_equal(out[i, 4 + len(c):], host[i, 4 + len(c):])  # past the output: untouched
 
 
-def test_device_uncompress_corrupted_streams_vs_host(torch, ctx):
+def test_device_uncompress_corrupted_streams_vs_host(torch, encoder):
+    ctx = encoder
     """Random corruption of valid streams (and truncations, bad varints, offsets before the output):
     the device decoder fails exactly where the host decoder does, and otherwise writes its bytes."""
     rng = np.random.default_rng(0x5EED0052)
@@ -226,7 +227,8 @@ def test_device_uncompress_corrupted_streams_vs_host(torch, ctx):
     assert st[-len(goods):].all()
 
 
-def test_device_uncompress_empty_result_fails(torch, ctx):
+def test_device_uncompress_empty_result_fails(torch, encoder):
+    ctx = encoder
     """b"\\x00" decodes to 0 bytes: golang/snappy's Decode returns a nil slice and compression.go:37-39
     drops the packet, so the device batch fails it (slot and length untouched), as the host slots do."""
     streams = [b"\x00", _host_compress(b"abcabcabc"), b"\x00"]
