@@ -219,7 +219,7 @@ struct SnapArgs {
 // group (compress only): true = snappy_compress_group_kernel, four packets per wave (a.wave_bytes = four
 // packet regions of a.off_sink bytes); false = one wave per packet
 constexpr uint32_t kSnapGroup = 4;
-hipError_t launch_snappy(bool compress, const SnapArgs &a, int waves_per_wg, int grid, hipStream_t s, bool group);
+hipError_t launch_snappy(bool compress, const SnapArgs &a, int waves_per_wg, int grid, hipStream_t s, int group);
 
 // Host worker placement (cpu_topo.cpp): the device's NUMA-local CPUs this process may use (count; 0 when
 // sysfs has no answer), one CPU per physical core ordered preferred-first then least busy over a

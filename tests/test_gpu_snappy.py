@@ -102,10 +102,11 @@ def encoder_ctxs(torch):
 
 @pytest.fixture(params=["1", "0"], ids=["group_codec", "wave_codec"])
 def encoder(request, encoder_ctxs):
-    """QGCM_SNAPPY_GROUP (at qgcm_create): 1 = four packets per wave, pipelined miss probes, output
-    straight into the slot, the next packets prefetched (the default); 0 = one wave per packet.  Both
-    must give the host encoder's (and libsnappy's) bytes, and leave a failing packet's slot untouched.
-    The value is the context built with that setting."""
+    """QGCM_SNAPPY_GROUP (at qgcm_create): 1 = four packets per wave for both directions (the encoder's
+    pipelined miss probes and output straight into the slot, the decoder's header window and
+    branch-free copies, the next packets prefetched; the default); 0 = one wave per packet.  Both must
+    give the host codec's (and libsnappy's) bytes, and leave a failing packet's slot untouched.  The
+    value is the context built with that setting."""
     return encoder_ctxs[request.param]
 
 

@@ -2,8 +2,8 @@
 random, second half a repeated HTTP line, stride 1472): compress, seal, open, uncompress, each timed
 by HIP events; the sealed arena is checked against tests/golden/config5_digest.json and the result
 against the plaintext arena (bench.extra_config5_resident).  The encoders alternate in one process,
-`rounds` times each: QGCM_SNAPPY_GROUP=1, four packets per wave (the default), and 0, one wave per
-packet (SNAP_GROUPS="1,2" compares other settings, e.g. a temporary variant wired to 2 for an A/B).
+`rounds` times each: QGCM_SNAPPY_GROUP=1, four packets per wave in both directions (the default),
+and 0, one wave per packet (SNAP_GROUPS="1,2" compares other settings, e.g. a temporary variant wired to 2 for an A/B).
 
     python3 tools/exp_snappy_dev.py [reps] [rounds]
 """
