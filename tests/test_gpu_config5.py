@@ -134,3 +134,60 @@ def test_config5_device_resident_chain_full_size(torch, c5, gold):
     assert torch.equal(arena.view(N, S)[:, :4 + L], plain.view(N, S)[:, :4 + L])
     del arena, plain
     torch.cuda.empty_cache()
+
+
+def test_config5_host_chain_tampered_packets_device_decoder_matches_host(torch, gold):
+    """Packets whose open fails are left to the caller by the decoder (status_in): 2^16 config-5 slots
+    sealed by the chain, 1 in 61 of them tampered (a ciphertext, tag or nonce byte flipped), then opened
+    and uncompressed with the codec on the host workers and, from the same sealed bytes, on the device
+    (the group decoder by default).  Both must give the same arena, lengths and statuses; the untouched
+    packets come back as plaintext, the tampered ones fail."""
+    from quantum_amd import _lib, batch, workloads as W
+    from quantum_amd.crypto import Context, derive_key
+
+    N, L, S = 1 << 16, W.C5_LEN, W.C5_STRIDE
+    key = derive_key(b"AES256Key-32Characters1234567890", bytes(range(32)))
+    ctx = Context(device=0, max_keys=4)
+    ctx.set_key(0, key)
+    Lb = _lib.lib()
+    a_ptr, n_ptr = Lb.qgcm_host_alloc(N * S), Lb.qgcm_host_alloc(12 * N)
+    try:
+        host = np.frombuffer((C.c_uint8 * (N * S)).from_address(a_ptr), np.uint8).reshape(N, S)
+        nons = np.frombuffer((C.c_uint8 * (12 * N)).from_address(n_ptr), np.uint8)
+        plain = W.config5_packets(N, L, S)
+        host[:] = plain
+        nons[:] = W.config5_nonces(N)
+        lens = np.full(N, L, np.uint32)
+        status = np.zeros(N, np.uint8)
+        assert batch.compress_seal_host(ctx, a_ptr, S, N, lens, 0, n_ptr, threads=16,
+                                        status_ptr=status.ctypes.data) == 0
+        rng = np.random.default_rng(0x5EED0061)
+        bad = np.arange(0, N, 61)
+        for i in bad:  # a byte of the record [4, 4 + lens[i]): ciphertext, tag or nonce
+            j = 4 + int(rng.integers(0, int(lens[i])))
+            host[i, j] ^= 1 + int(rng.integers(0, 255))
+        sealed, sealed_lens = host.copy(), lens.copy()
+        out = {}
+        for mode in (0, 2):
+            host[:] = sealed
+            lens[:] = sealed_lens
+            status[:] = 0
+            prev = batch.chain_codec(ctx, mode)
+            try:
+                failed = batch.open_uncompress_host(ctx, a_ptr, S, N, lens, 0, threads=16,
+                                                    status_ptr=status.ctypes.data)
+            finally:
+                batch.chain_codec(ctx, prev)
+            out[mode] = (failed, host.copy(), lens.copy(), status.copy())
+        f0, h0, l0, s0 = out[0]
+        f2, h2, l2, s2 = out[2]
+        assert f0 == f2 == len(bad)
+        assert np.array_equal(s0, s2) and not s0[bad].any() and int(s0.sum()) == N - len(bad)
+        assert np.array_equal(l0, l2)
+        assert np.array_equal(h0, h2), "device decoder output differs from the host codec's"
+        good = np.setdiff1d(np.arange(N), bad)
+        assert np.array_equal(h0[good, :4 + L], plain[good, :4 + L]) and bool((l0[good] == L).all())
+    finally:
+        Lb.qgcm_host_free(a_ptr)
+        Lb.qgcm_host_free(n_ptr)
+        ctx.close()
