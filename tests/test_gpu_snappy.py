@@ -239,3 +239,54 @@ def test_device_uncompress_empty_result_fails(torch, encoder):
     assert list(st) == [0, 1, 0] and list(ol) == [1, 9, 1]
     assert np.array_equal(out[0], host[0]) and np.array_equal(out[2], host[2])
     assert out[1, 4:13].tobytes() == b"abcabcabc"
+
+
+def test_device_codec_fuzz_vs_host(torch, encoder):
+    """2^15 Payload.Raw slots of random shapes -- the corpus kinds plus two- and four-letter alphabets
+    (hash collisions between consecutive probes, long back-references at short offsets) -- and lengths
+    0..1433: device compress equals the host encoder (bytes, lengths, untouched tails); then a third
+    of the streams get 1-3 random byte flips or a truncation, and the device decoder must agree with
+    the host decoder on every stream (status, length, bytes)."""
+    ctx = encoder
+    n, stride = 1 << 15, 1472
+    rng = np.random.default_rng(0x5EED0071)
+    kinds = SI.KINDS + ["ab", "acgt"]
+    payloads = []
+    for i in range(n):
+        k = kinds[int(rng.integers(0, len(kinds)))]
+        L = int(rng.integers(0, 1434))
+        if k == "ab":
+            payloads.append(bytes(rng.choice(np.frombuffer(b"ab", np.uint8), L)))
+        elif k == "acgt":
+            payloads.append(bytes(rng.choice(np.frombuffer(b"acgt", np.uint8), L)))
+        else:
+            payloads.append(SI.make(k, L, seed=i))
+    host, arena, lens = _arena(torch, payloads, stride)
+    limit = stride - 4 - 28
+    out, ol, st = _run(torch, ctx, True, arena, stride, n, lens, stride - 4, limit)
+    comps = [_host_compress(p) for p in payloads]
+    assert (st == 1).all()
+    assert np.array_equal(ol, np.array([len(c) for c in comps], np.uint32))
+    ref = host.copy()
+    for i, c in enumerate(comps):
+        ref[i, 4:4 + len(c)] = np.frombuffer(c, np.uint8)
+    assert np.array_equal(out, ref)
+    # corrupt a third of the streams in place, then decode on both sides
+    streams = []
+    for i, c in enumerate(comps):
+        b = bytearray(c)
+        if i % 3 == 0 and b:
+            if rng.random() < 0.25:
+                b = b[:int(rng.integers(0, len(b)))]
+            else:
+                for _ in range(int(rng.integers(1, 4))):
+                    b[int(rng.integers(0, len(b)))] = int(rng.integers(0, 256))
+        streams.append(bytes(b))
+    host2, arena2, lens2 = _arena(torch, streams, stride)
+    back, bl, st2 = _run(torch, ctx, False, arena2, stride, n, lens2, stride - 4, stride - 4)
+    for i, s in enumerate(streams):
+        want = _host_uncompress(s, stride - 4)
+        if want is None or len(want) == 0:
+            assert st2[i] == 0 and bl[i] == len(s) and np.array_equal(back[i], host2[i]), i
+        else:
+            assert st2[i] == 1 and bl[i] == len(want) and back[i, 4:4 + len(want)].tobytes() == want, i
