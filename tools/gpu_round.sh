@@ -74,6 +74,9 @@ for s in $STEPS; do
     snapdev)
       timeout -k 10 200 python3 tools/exp_snappy_dev.py 5 > $OUT/snappy_dev.json 2> $OUT/snappy_dev.err
       check snapdev $? ;;
+    snapmix)  # the codec's time by data shape (random, one repeated line, config 5, zeros)
+      timeout -k 10 200 python3 tools/exp_snappy_mix.py 5 > $OUT/snappy_mix.jsonl 2> $OUT/snappy_mix.err
+      check snapmix $? ;;
     profsnap)
       timeout -k 10 900 bash tools/profile_snappy.sh $TAG > $OUT/profile_snappy.log 2>&1
       check profsnap $? ;;
