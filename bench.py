@@ -42,7 +42,7 @@ from quantum_amd.crypto import Context, derive_key  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, MI355X_MICROARCH.md "Chip-level parameters"
 # PMC passes of this command (tools/pmc_traffic.py), newest first
 LAUNCH_CHUNK = 1 << 19  # quantum_amd/csrc/gcm_internal.h kLaunchChunk
-TRAFFIC_JSONS = [os.path.join(ROOT, "profiles", d, "traffic.json") for d in ("r5_s7", "r4_s21", "r4_s3", "r3_s39", "r3_s15", "r3_s1")]
+TRAFFIC_JSONS = [os.path.join(ROOT, "profiles", d, "traffic.json") for d in ("r5_s37", "r5_s7", "r4_s21", "r4_s3", "r3_s39", "r3_s15", "r3_s1")]
 CONFIG4_PACKETS = 64 << 20  # BASELINE config 4: 64 M packets over the node's GPUs
 SECRET = b"AES256Key-32Characters1234567890"
 SALT = bytes(range(32))
