@@ -246,6 +246,8 @@ def cpu_baseline(key: bytes, L: int, threads: int, host: dict, seconds: float = 
             "throttled_ms": round(sum(p["throttled_ms"] or 0 for p in sweep), 1),
             "aes_gcm_only_one_core": round(aes_only, 3),
             "round_trips_per_s_best": best["packets_per_s"], "round_trips_per_s_one_thread": one["packets_per_s"],
+            "best_cpus_busy": best["cpus_busy"],
+            "best_cpu_us_per_pair": round(best["cpus_busy"] / best["packets_per_s"] * 1e6, 3),
             "intact": all(p["intact"] for p in sweep),
             "measured_before_gpu_init": True, "kernel": kernel,
             "sweep": sweep, "host": host,
@@ -730,6 +732,8 @@ def extra_config4_one_gpu(key: bytes, steps: int = 3, warmup: int = 1, settle_ms
     while (time.perf_counter() - t0) * 1e3 < settle_ms:
         step()
         torch.cuda.synchronize()
+    tele = GpuTelemetry(0)
+    tele.start()
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()
@@ -738,6 +742,9 @@ def extra_config4_one_gpu(key: bytes, steps: int = 3, warmup: int = 1, settle_ms
         step()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    tele.stop()
+    clock = tele.summary()
+    tele.close()
     ok = int(status.sum().item()) == N
     del alloc, arena, nonces, status
     ctx.close()
@@ -746,32 +753,154 @@ def extra_config4_one_gpu(key: bytes, steps: int = 3, warmup: int = 1, settle_ms
             "value": round(2 * N * L / (el / steps) / 2**30, 2), "unit": "GiB/s",
             "ms_per_step": round(el * 1e3 / steps, 2), "steps": steps, "packets": N, "slot_stride": stride,
             "arena_GB": round(N * stride / 1e9, 1), "status_ok": ok,
+            "sclk_mhz_mean": clock["sclk_mhz_mean"], "power_w_mean": clock["power_w_mean"],
+            "power_cap_w": clock["power_cap_w"], "gpu_clock_power": clock,
             "use": "N = 1 anchor of the config-4 scaling curve (bench.py --gpus N runs config 4 sharded)"}
 
 
-def headline_digests(ctx, arena, nonces, status, stride: int, N: int, L: int, rank: int, stream,
-                     verify: bool = True) -> dict:
-    """After the timed loop (untimed): the headline arena against tests/golden/headline_digest.json
-    (make_headline_golden.py: the C restatement over every packet, equal to OpenSSL) -- the state the
-    timed steps left (sealed then opened K times: plaintext with each slot's tag || nonce), then one
-    more seal with the same calls (ciphertext, tag, nonce), then the open back.  Only for the layout
-    the golden was made for (config 2 at one GPU); otherwise the fields say why not."""
+def rank_digests(ctx, arena, nonces, status, stride: int, N: int, L: int, rank: int, stream,
+                 verify: bool = True) -> dict:
+    """After the timed loop (untimed), on every rank: the first P slots of this rank's arena against
+    tests/golden/rank_digest.json (make_rank_golden.py: the C restatement over every packet of ranks 0-7,
+    equal to OpenSSL; rank r's fill uses seeds 0x5EED0001 + r / 0x5EED0002 + r, and slot i's bytes depend
+    only on i and the seeds, so one golden covers every N), P the largest of 2^20 / 2^18 / 2^16 that fits.
+    Three states: what the timed steps left (sealed then opened K times: plaintext with each slot's
+    tag || nonce), then one more seal of the prefix with the same calls (ciphertext, tag, nonce), then the
+    open back.  At N = 1 and 2^20 packets the prefix is the whole headline arena (rank 0's 2^20 digests
+    equal tests/golden/headline_digest.json).  Other layouts: the fields say why not."""
     if not verify:
-        return {"sealed_digest_ok": None, "digest_skipped": "--no-verify or N > 1"}
-    gold = json.load(open(os.path.join(ROOT, "tests", "golden", "headline_digest.json")))
-    if (N, L, stride, rank) != (gold["n"], gold["len"], gold["stride"], 0):
+        return {"sealed_digest_ok": None, "digest_skipped": "--no-verify"}
+    gold = json.load(open(os.path.join(ROOT, "tests", "golden", "rank_digest.json")))
+    fits = [p for p in gold["prefixes"] if p <= N]
+    if (L, stride) != (gold["len"], gold["stride"]) or rank >= len(gold["ranks"]) or not fits:
         return {"sealed_digest_ok": None, "digest_skipped": "not the golden's layout"}
-    arena = arena[:N * stride]  # the slots only (the allocation's tail past them is not the golden's)
+    P = max(fits)
+    want = gold["ranks"][rank]["prefixes"][str(P)]
+    a, st = arena[:P * stride], status[:P]  # the prefix's slots only
     torch.cuda.synchronize()
-    timed_ok = _sha256_device(arena) == gold["sha256_opened"]
-    batch.seal_uniform(ctx, arena, stride, N, L, 0, nonces, status=None, stream=stream)
+    timed_ok = _sha256_device(a) == want["sha256_opened"]
+    batch.seal_uniform(ctx, a, stride, P, L, 0, nonces[:12 * P], status=None, stream=stream)
     torch.cuda.synchronize()
-    sealed_ok = _sha256_device(arena) == gold["sha256_sealed"]
-    batch.open_uniform(ctx, arena, stride, N, L + 28, 0, status=status, stream=stream)
+    sealed_ok = _sha256_device(a) == want["sha256_sealed"]
+    batch.open_uniform(ctx, a, stride, P, L + 28, 0, status=st, stream=stream)
     torch.cuda.synchronize()
-    opened_ok = _sha256_device(arena) == gold["sha256_opened"] and int(status.sum().item()) == N
-    return {"sealed_digest_ok": sealed_ok, "opened_digest_ok": opened_ok and timed_ok,
-            "digest_source": "tests/golden/headline_digest.json"}
+    opened_ok = _sha256_device(a) == want["sha256_opened"] and int(st.sum().item()) == P
+    return {"sealed_digest_ok": sealed_ok, "opened_digest_ok": opened_ok and timed_ok, "digest_prefix": P,
+            "digest_source": "tests/golden/rank_digest.json"}
+
+
+class GpuTelemetry:
+    """Clock and power of this rank's GPU while the timed steps run (DESIGN.md s5 "The clock and the power
+    limit"): a background thread reads amdsmi's gpu_metrics of the PCI device torch calls cuda:<dev>
+    every `period_s`, and the power cap once.  Reported: the mean of the per-XCD current GFX clocks, the
+    mean socket power, the cap, and the share of the interval the SMU counted as power- (PPT) or
+    thermally-limited (its residency accumulators, differenced over the interval).  When amdsmi is
+    missing or refuses this process, `summary()` says so instead of a number."""
+
+    def __init__(self, device: int, period_s: float = 0.02):
+        import threading
+
+        self.period, self.samples, self.err, self.h, self.smi = period_s, [], None, None, None
+        self.first = self.last = None
+        self._stop = threading.Event()
+        self._th = None
+        try:
+            import amdsmi
+
+            amdsmi.amdsmi_init()
+            self.smi = amdsmi
+            p = torch.cuda.get_device_properties(device)
+            bdf = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+            for h in amdsmi.amdsmi_get_processor_handles():
+                if amdsmi.amdsmi_get_gpu_device_bdf(h).lower() == bdf.lower():
+                    self.h = h
+            if self.h is None:
+                self.err = f"amdsmi has no device {bdf}"
+        except Exception as e:  # noqa: BLE001 -- reported in the line, never fatal
+            self.err = f"amdsmi: {type(e).__name__}: {e}"
+
+    @staticmethod
+    def _num(v):
+        if isinstance(v, (int, float)) and v not in (0xFFFF, 0xFFFFFFFF, 0xFFFFFFFFFFFFFFFF):
+            return float(v)
+        return None
+
+    def _read(self) -> dict | None:
+        try:
+            m = self.smi.amdsmi_get_gpu_metrics_info(self.h)
+        except Exception as e:  # noqa: BLE001
+            self.err = f"gpu_metrics: {type(e).__name__}: {e}"
+            return None
+        clk = m.get("current_gfxclks")
+        clks = [self._num(c) for c in clk] if isinstance(clk, (list, tuple)) else [self._num(clk)]
+        clks = [c for c in clks if c]
+        if not clks:
+            c = self._num(m.get("current_gfxclk")) or self._num(m.get("average_gfxclk_frequency"))
+            clks = [c] if c else []
+        power = self._num(m.get("current_socket_power")) or self._num(m.get("average_socket_power"))
+        return {"t": time.perf_counter(), "sclk": sum(clks) / len(clks) if clks else None, "power": power,
+                "acc": {k: self._num(m.get(k)) for k in ("accumulation_counter", "ppt_residency_acc",
+                                                           "socket_thm_residency_acc", "prochot_residency_acc")},
+                "throttle": m.get("throttle_status")}
+
+    def _loop(self) -> None:
+        while not self._stop.wait(self.period):
+            s = self._read()
+            if s:
+                self.samples.append(s)
+
+    def start(self) -> None:
+        if self.h is None:
+            return
+        import threading
+
+        self.first = self._read()
+        self._th = threading.Thread(target=self._loop, daemon=True)
+        self._th.start()
+
+    def stop(self) -> None:
+        if self._th is not None:
+            self._stop.set()
+            self._th.join()
+            self.last = self._read()
+
+    def summary(self) -> dict:
+        if self.h is None or not self.samples:
+            return {"sclk_mhz_mean": None, "power_w_mean": None, "power_cap_w": None,
+                    "telemetry": self.err or "no samples"}
+        clk = [s["sclk"] for s in self.samples if s["sclk"]]
+        pw = [s["power"] for s in self.samples if s["power"]]
+        cap = None
+        try:
+            c = self.smi.amdsmi_get_power_cap_info(self.h)
+            cap = self._num(c.get("power_cap"))
+            if cap and cap > 1e5:  # reported in microwatts by this amdsmi
+                cap /= 1e6
+        except Exception as e:  # noqa: BLE001
+            self.err = f"power_cap: {type(e).__name__}: {e}"
+        out = {"sclk_mhz_mean": round(sum(clk) / len(clk), 1) if clk else None,
+               "sclk_mhz_min": min(clk) if clk else None, "sclk_mhz_max": max(clk) if clk else None,
+               "power_w_mean": round(sum(pw) / len(pw), 1) if pw else None, "power_w_max": max(pw) if pw else None,
+               "power_cap_w": cap, "samples": len(self.samples),
+               "telemetry": f"amdsmi gpu_metrics every {self.period * 1e3:.0f} ms over the timed steps"}
+        a0, a1 = (self.first or {}).get("acc", {}), (self.last or {}).get("acc", {})
+        ticks = (a1.get("accumulation_counter") or 0) - (a0.get("accumulation_counter") or 0)
+        if ticks > 0:
+            for k, name in (("ppt_residency_acc", "ppt_limited_frac"), ("socket_thm_residency_acc", "thermal_limited_frac"),
+                            ("prochot_residency_acc", "prochot_frac")):
+                if a0.get(k) is not None and a1.get(k) is not None:
+                    out[name] = round((a1[k] - a0[k]) / ticks, 3)
+        if self.err:
+            out["telemetry_note"] = self.err
+        return out
+
+    def close(self) -> None:
+        self.stop()
+        if self.smi is not None:
+            try:
+                self.smi.amdsmi_shut_down()
+            except Exception:  # noqa: BLE001
+                pass
 
 
 def free_port() -> int:
@@ -818,7 +947,9 @@ def extra_per_packet(seconds: float = 1.5) -> dict:
     """The per-call drop-in (qgcm_seal_one / qgcm_open_one, crypto/aes.go:41-62 from quantum's worker
     threads, worker/outgoing.go:83-93): tools/bin/per_packet_bench (built by __graft_entry__.build()),
     one 1350-B seal+open in flight per thread, through the resident kernel and through a kernel launch
-    per call, 1 and 16 threads.  Run as a child process after the headline."""
+    per call, 1 / 16 / 64 threads, and the resident kernel with every waiting caller asleep on a futex
+    (QGCM_RESIDENT_SPINNERS=0) at 16 and 64.  Each point reports `cpu_us_per_pair`: the process's host CPU
+    time per seal+open pair.  Run as child processes after the headline."""
     import subprocess
 
     exe = os.path.join(ROOT, "tools", "bin", "per_packet_bench")
@@ -826,15 +957,21 @@ def extra_per_packet(seconds: float = 1.5) -> dict:
         return {"skipped": "tools/bin/per_packet_bench not built (python -c 'import __graft_entry__ as g; g.build()')"}
     out = {"workload": "per-packet Encrypt/Decrypt calls, 1350 B, one packet in flight per thread",
            "unit": "seal+open round trips/s"}
-    for threads, mode in ((1, "both"), (16, "both")):
+    for threads, mode, spinners in ((1, "both", None), (16, "both", None), (64, "resident", None),
+                                    (16, "resident", "0"), (64, "resident", "0")):
+        env = dict(os.environ)
+        env.pop("QGCM_RESIDENT_SPINNERS", None)
+        if spinners is not None:
+            env["QGCM_RESIDENT_SPINNERS"] = spinners
         r = subprocess.run([exe, str(threads), "1350", str(seconds), "0", mode], capture_output=True, text=True,
-                           timeout=120)
+                           timeout=120, env=env)
         if r.returncode != 0:
             raise RuntimeError(f"per_packet_bench {threads}: rc {r.returncode}: {r.stderr[-300:]}")
         for ln in r.stdout.splitlines():
             d = json.loads(ln)
-            out[f"{d['path']}_t{threads}"] = {k: d[k] for k in ("round_trips_per_s", "call_pair_p50_us",
-                                                                 "call_pair_p99_us", "failures", "cpus_busy")}
+            name = f"{d['path']}_t{threads}" + ("" if spinners is None else f"_spinners{spinners}")
+            out[name] = {k: d[k] for k in ("round_trips_per_s", "call_pair_p50_us", "call_pair_p99_us", "failures",
+                                           "cpus_busy", "cpu_us_per_pair")}
     return out
 
 
@@ -908,6 +1045,8 @@ def main() -> None:
         settle += 1
         if settle % 8 == 0:
             torch.cuda.synchronize()  # bound the launch queue; the loop keeps the GPU busy
+    tele = GpuTelemetry(local)  # clock and power over the warmup and timed steps (same load)
+    tele.start()
     for _ in range(args.warmup):
         step()
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
@@ -923,6 +1062,9 @@ def main() -> None:
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    tele.stop()
+    clock = tele.summary()
+    tele.close()
     ok = int(status.sum().item()) == N  # the last timed open authenticated every packet
     # max over ranks, AND of the per-rank status (the only cross-rank traffic; no data collective)
     seal_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
@@ -930,8 +1072,19 @@ def main() -> None:
     own_elapsed = elapsed
     coll_dev = dev if args.dist_backend == "nccl" else None
     elapsed, ok = shard.reduce_step_time(elapsed, ok, dist, coll_dev)
+    # every rank checks its own arena against the golden (untimed, before anything else touches it)
+    digests = rank_digests(ctx, arena, nonces, status, stride, N, L, rank, stream, verify=not args.no_verify)
+
+    def flag(v):
+        return -1.0 if v is None else float(bool(v))
+
+    def num(v):
+        return float("nan") if v is None else float(v)
+
     # every rank's own figures (after the timed region): per-GPU rates of the multi-GPU line
-    per_rank = shard.gather_rank_stats([own_elapsed, seal_ms, open_ms, N], dist, coll_dev)
+    per_rank = shard.gather_rank_stats([own_elapsed, seal_ms, open_ms, N, flag(digests["sealed_digest_ok"]),
+                                        flag(digests.get("opened_digest_ok")), num(clock["sclk_mhz_mean"]),
+                                        num(clock["power_w_mean"])], dist, coll_dev)
     ms_step = elapsed * 1e3 / args.steps
     total_packets = CONFIG4_PACKETS if workload == "config4" and not args.packets else world * N
     total_bytes = 2 * total_packets * L  # each payload byte counted once sealed and once unsealed
@@ -946,8 +1099,6 @@ def main() -> None:
     read_pkt = L + 16 if kname == "seal" else L + 32  # the HBM-read-only variant
     achieved_read = N * read_pkt / (kms * 1e-3) / 1e9
     traffic, lds_busy, traffic_src = pmc_traffic(kname, N, L, stride)
-    digests = headline_digests(ctx, arena, nonces, status, stride, N, L, rank, stream,
-                               verify=not args.no_verify and world == 1)  # untimed
     # libqgcm launches a uniform batch in chunks of LAUNCH_CHUNK packets: kms spans them all
     chunk = int(os.environ.get("QGCM_LAUNCH_CHUNK", str(LAUNCH_CHUNK))) // 64 * 64 or N
     launches = -(-N // chunk)
@@ -990,11 +1141,23 @@ def main() -> None:
             "kernels_ms": {"seal": round(seal_ms, 4), "open": round(open_ms, 4)},
             "per_gpu": [{"rank": r, "packets": int(p[3]), "ms_per_step": round(p[0] * 1e3 / args.steps, 4),
                          "GiB_s": round(2 * p[3] * L / (p[0] / args.steps) / 2**30, 2),
-                         "seal_ms": round(p[1], 4), "open_ms": round(p[2], 4)} for r, p in enumerate(per_rank)],
+                         "seal_ms": round(p[1], 4), "open_ms": round(p[2], 4),
+                         "sealed_digest_ok": None if p[4] < 0 else bool(p[4]),
+                         "opened_digest_ok": None if p[5] < 0 else bool(p[5]),
+                         "sclk_mhz_mean": None if p[6] != p[6] else round(p[6], 1),
+                         "power_w_mean": None if p[7] != p[7] else round(p[7], 1)} for r, p in enumerate(per_rank)],
             "dist_backend": args.dist_backend if dist is not None else None,
             "status_ok": ok,
             **digests,
+            "sclk_mhz_mean": clock["sclk_mhz_mean"], "power_w_mean": clock["power_w_mean"],
+            "power_cap_w": clock["power_cap_w"], "gpu_clock_power": clock,
         }
+        # every rank's digests: the line's flags are the AND over ranks (a rank without a golden prefix: None)
+        for k in ("sealed_digest_ok", "opened_digest_ok"):
+            flags = [g[k] for g in line["per_gpu"]]
+            line[k] = False if False in flags else (True if flags and all(flags) else None)
+        if world > 1:
+            line["digest_source"] = "tests/golden/rank_digest.json (each rank's own prefix)"
         rates = [g["GiB_s"] for g in line["per_gpu"]]
         line["per_gpu_GiB_s"] = {"min": min(rates), "max": max(rates), "mean": round(sum(rates) / len(rates), 2),
                                  "aggregate_of_own_times": round(sum(rates), 2),
@@ -1029,7 +1192,16 @@ def main() -> None:
                 # the same work on the CPU chain (one packet sealed and opened = one round trip)
                 extra["per_packet"]["cpu_chain"] = {
                     "round_trips_per_s_best": cpu["round_trips_per_s_best"], "threads": cpu["cores"],
-                    "round_trips_per_s_one_thread": cpu["round_trips_per_s_one_thread"]}
+                    "round_trips_per_s_one_thread": cpu["round_trips_per_s_one_thread"],
+                    "cpus_busy": cpu["best_cpus_busy"], "cpu_us_per_pair": cpu["best_cpu_us_per_pair"]}
+                pts = {k: v for k, v in extra["per_packet"].items() if isinstance(v, dict) and "cpu_us_per_pair" in v
+                       and k != "cpu_chain"}
+                if pts:
+                    best = min(pts, key=lambda k: pts[k]["cpu_us_per_pair"])
+                    extra["per_packet"]["least_host_cpu_per_pair"] = {
+                        "point": best, "cpu_us_per_pair": pts[best]["cpu_us_per_pair"],
+                        "cpu_chain_cpu_us_per_pair": cpu["best_cpu_us_per_pair"],
+                        "below_cpu_chain": pts[best]["cpu_us_per_pair"] < cpu["best_cpu_us_per_pair"]}
             line["extra_configs"] = extra
         print(json.dumps(line), flush=True)
         if any("error" in v for v in line.get("extra_configs", {}).values()):

@@ -275,7 +275,11 @@ func (gg *GPUGroup) NewAES(secret, salt []byte) (*AES, error) {
 	return a, nil
 }
 
+// release marks the slot's key unset on its owner before the slot is reused, so a KeyIndex kept in a
+// batch Desc after its AES was dropped fails that packet's status instead of sealing or opening under
+// whichever peer gets the slot next.
 func (gg *GPUGroup) release(idx uint32) {
+	C.qgcm_group_clear_keys(gg.grp, C.uint32_t(idx), 1)
 	gg.mu.Lock()
 	gg.free = append(gg.free, idx)
 	gg.mu.Unlock()

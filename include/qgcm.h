@@ -92,6 +92,12 @@ int qgcm_derive_keys(const uint8_t *secrets, const uint8_t *salts, uint32_t coun
  * tables on the device for slot key_idx.  Synchronous. */
 int qgcm_set_key(qgcm_ctx *ctx, uint32_t key_idx, const uint8_t key[QGCM_KEY_BYTES]);
 int qgcm_set_keys(qgcm_ctx *ctx, uint32_t first_idx, uint32_t count, const uint8_t *keys);
+/* Marks key slots [first_idx, first_idx + count) unset (the slot's AES was released: go/crypto/aes_gpu.go's
+ * finalizer, crypto::DeviceSet::Release).  Afterwards every call naming one of them fails as for a key never
+ * set (per-packet calls -1 / QGCM_E_KEY, descriptor batches status 0) until qgcm_set_key(s) installs a new
+ * key there, so a stale key index never seals or opens under the slot's next peer.  Synchronous; ends the
+ * resident instance like qgcm_set_keys. */
+int qgcm_clear_keys(qgcm_ctx *ctx, uint32_t first_idx, uint32_t count);
 /* X25519 (crypto/ecdh.go:13-31): pub = X25519(priv, 9); secret = X25519(priv, peer_pub). */
 int qgcm_x25519_base(uint8_t pub[32], const uint8_t priv[32]);
 int qgcm_x25519(uint8_t secret[32], const uint8_t priv[32], const uint8_t peer_pub[32]);
@@ -186,6 +192,8 @@ int qgcm_group_member_cpus(const qgcm_group *g, int member);
 int qgcm_group_shard(const qgcm_group *g, uint32_t key_idx);
 /* Installs keys[i] as key first_idx + i on its owning member only (qgcm_set_keys there). */
 int qgcm_group_set_keys(qgcm_group *g, uint32_t first_idx, uint32_t count, const uint8_t *keys);
+/* qgcm_clear_keys on the owning member of each key index. */
+int qgcm_group_clear_keys(qgcm_group *g, uint32_t first_idx, uint32_t count);
 /* Host batches over the group: packet i is the Raw slot at h_arena + h_descs[i].offset (seal: len = L,
  * capacity 4 + L + 28; open: len = L + 28), any key mix.  Packets are split by owner; one host thread and
  * one stream set per member gathers its packets into pinned staging, copies them to its device, runs the

@@ -103,7 +103,8 @@ class GPUContext {
 // The process-wide device set of the reference-signature NewAES(secret, salt) below, as
 // go/crypto/aes_gpu.go's Devices(): created on first use from QGCM_DEVICES ("0,1,...", default every
 // visible device) and QGCM_MAX_PEERS (default 4096) as a qgcm_group, one member context per device;
-// a key lives on member hash(slot) mod G.  A slot goes back to the set when its AES is destroyed.
+// a key lives on member hash(slot) mod G.  A slot goes back to the set, its key marked unset
+// (qgcm_group_clear_keys), when its AES is destroyed.
 class DeviceSet {
   public:
     static std::pair<std::shared_ptr<DeviceSet>, Error> Get();

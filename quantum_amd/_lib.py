@@ -18,7 +18,7 @@ if os.environ.get("QGCM_AB_LIB"):
 # Every symbol include/qgcm.h declares (checked by tests/test_abi.py).
 EXPORTS = (
     "qgcm_create", "qgcm_destroy", "qgcm_strerror", "qgcm_version", "qgcm_device_count",
-    "qgcm_derive_key", "qgcm_derive_keys", "qgcm_set_key", "qgcm_set_keys",
+    "qgcm_derive_key", "qgcm_derive_keys", "qgcm_set_key", "qgcm_set_keys", "qgcm_clear_keys",
     "qgcm_x25519_base", "qgcm_x25519",
     "qgcm_seal_batch", "qgcm_open_batch", "qgcm_seal_uniform", "qgcm_open_uniform",
     "qgcm_seal_one", "qgcm_open_one", "qgcm_seal_host", "qgcm_open_host",
@@ -32,7 +32,7 @@ EXPORTS = (
     "qgcm_udp_send_slots",
     "qgcm_tun_open", "qgcm_tun_up", "qgcm_tun_read_slots", "qgcm_tun_write_slots", "qgcm_tun_close",
     "qgcm_group_create", "qgcm_group_destroy", "qgcm_group_size", "qgcm_group_ctx", "qgcm_group_shard",
-    "qgcm_group_set_keys", "qgcm_group_seal_host", "qgcm_group_open_host", "qgcm_group_member_cpus",
+    "qgcm_group_set_keys", "qgcm_group_clear_keys", "qgcm_group_seal_host", "qgcm_group_open_host", "qgcm_group_member_cpus",
     "qgcm_group_last_zerocopy", "qgcm_group_last_path", "qgcm_group_order", "qgcm_launch_counts", "qgcm_resident_stop", "qgcm_resident_stats",
 )
 
@@ -74,6 +74,8 @@ def _bind(L: C.CDLL) -> None:
     L.qgcm_derive_keys.argtypes = [u8p, u8p, u32, u8p]
     L.qgcm_set_key.argtypes = [vp, u32, u8p]
     L.qgcm_set_keys.argtypes = [vp, u32, u32, u8p]
+    if hasattr(L, "qgcm_clear_keys"):
+        L.qgcm_clear_keys.argtypes = [vp, u32, u32]
     L.qgcm_x25519_base.argtypes = [u8p, u8p]
     L.qgcm_x25519.argtypes = [u8p, u8p, u8p]
     L.qgcm_seal_batch.argtypes = [vp, vp, vp, u32, vp, u32, vp, vp]
@@ -131,6 +133,8 @@ def _bind(L: C.CDLL) -> None:
         L.qgcm_group_ctx.restype = vp
         L.qgcm_group_shard.argtypes = [vp, u32]
         L.qgcm_group_set_keys.argtypes = [vp, u32, u32, u8p]
+        if hasattr(L, "qgcm_group_clear_keys"):
+            L.qgcm_group_clear_keys.argtypes = [vp, u32, u32]
         L.qgcm_group_seal_host.argtypes = [vp, vp, vp, u32, vp, u32, vp]
         L.qgcm_group_open_host.argtypes = [vp, vp, vp, u32, u32, vp]
         if hasattr(L, "qgcm_group_member_cpus"):

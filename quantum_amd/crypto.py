@@ -103,6 +103,11 @@ class Context:
         _lib.check(_lib.lib().qgcm_set_keys(self.handle, first, len(keys) // keyLength, keys), "qgcm_set_keys")
         self._reserve(first + len(keys) // keyLength)
 
+    def clear_keys(self, first: int, count: int = 1) -> None:
+        """qgcm_clear_keys: slots [first, first + count) unset (their AES was released); calls naming
+        them fail until a key is set there again."""
+        _lib.check(_lib.lib().qgcm_clear_keys(self.handle, first, count), "qgcm_clear_keys")
+
     def close(self) -> None:
         if self.handle and getattr(self, "_owned", True):
             _lib.lib().qgcm_destroy(self.handle)

@@ -1013,6 +1013,20 @@ int qgcm_group_set_keys(qgcm_group *g, uint32_t first_idx, uint32_t count, const
     return QGCM_OK;
 }
 
+int qgcm_group_clear_keys(qgcm_group *g, uint32_t first_idx, uint32_t count) {
+    if (!g) return QGCM_E_ARG;
+    if ((uint64_t)first_idx + count > g->max_keys) return QGCM_E_KEY;
+    for (uint32_t i = 0; i < count;) {
+        const int k = qgcm_group_shard(g, first_idx + i);
+        uint32_t j = i + 1;
+        while (j < count && qgcm_group_shard(g, first_idx + j) == k) ++j;
+        const int rc = qgcm_clear_keys(g->m[k].ctx, first_idx + i, j - i);
+        if (rc != QGCM_OK) return rc;
+        i = j;
+    }
+    return QGCM_OK;
+}
+
 int qgcm_group_seal_host(qgcm_group *g, uint8_t *h_arena, const qgcm_desc *h_descs, uint32_t n,
                          const uint8_t *h_nonces, uint32_t aad_len, uint8_t *h_status) {
     return run_group(g, true, h_arena, h_descs, n, h_nonces, aad_len, h_status);

@@ -63,11 +63,11 @@ struct qgcm_ctx {
     bool snappy_group = true;
     // the chain's host codec workers run one per physical core, the GPU's NUMA-local cores and the least
     // busy first (cpu_topo.cpp; QGCM_CHAIN_PIN=0 at qgcm_create: left to the scheduler).  The core list
-    // comes from a 30-ms sample of the host's load, taken once per device and process in the background
-    // from the first qgcm_create on (codec_cpu_list), and is kept from the context's first chained call.
+    // comes from a 30-ms sample of the host's load, taken per device in the background from the first
+    // qgcm_create on and again once it is older than kCodecCpusMaxAge (codec_cpu_list); a chained call
+    // pins only when the list has a core for every worker, so no two workers share one CPU.
     bool chain_pin = true;
-    std::shared_future<std::vector<int>> codec_cpus_pending;
-    std::once_flag codec_cpus_once;
+    std::mutex codec_cpus_mu;
     std::vector<int> codec_cpus;
     uint32_t *d_rk = nullptr;
     uint4 *d_gh = nullptr;
@@ -519,21 +519,45 @@ struct BigRelease {
 
 }  // namespace
 
-// The chain's codec core list for a device (qgcm_ctx::chain_pin): sampled once per process, off the
-// caller's path -- the first context of a device starts the 30-ms load sample, later ones share it.
+// The chain's codec core list for a device (qgcm_ctx::chain_pin), off the caller's path: the first
+// context of a device starts the 30-ms load sample, later ones share it, and a list older than
+// kCodecCpusMaxAge starts a new sample (a long-running process must not pin by stale load figures).
+// Returns the newest finished list, or the first sample still running.
+static constexpr auto kCodecCpusMaxAge = std::chrono::seconds(60);
 static std::shared_future<std::vector<int>> codec_cpu_list(int device) {
+    struct Lists {
+        std::shared_future<std::vector<int>> ready, next;
+        std::chrono::steady_clock::time_point at;
+    };
     static std::mutex mu;
-    static std::map<int, std::shared_future<std::vector<int>>> lists;
+    static std::map<int, Lists> lists;
+    auto sample = [device] {
+        return std::async(std::launch::async, [device] {
+                   cpu_set_t local;
+                   const bool have = qgcm::gpu_local_cpus(device, &local) > 0;
+                   return qgcm::spread_cpus(have ? &local : nullptr, 30);
+               }).share();
+    };
+    const auto now = std::chrono::steady_clock::now();
     std::lock_guard<std::mutex> g(mu);
     auto it = lists.find(device);
-    if (it != lists.end()) return it->second;
-    auto f = std::async(std::launch::async, [device] {
-                 cpu_set_t local;
-                 const bool have = qgcm::gpu_local_cpus(device, &local) > 0;
-                 return qgcm::spread_cpus(have ? &local : nullptr, 30);
-             }).share();
-    lists.emplace(device, f);
-    return f;
+    if (it == lists.end()) {
+        Lists l;
+        l.next = sample();
+        l.at = now;
+        lists.emplace(device, l);
+        return l.next;
+    }
+    Lists &l = it->second;
+    if (l.next.valid() && l.next.wait_for(std::chrono::seconds(0)) == std::future_status::ready) {
+        l.ready = l.next;
+        l.next = {};
+    }
+    if (!l.next.valid() && now - l.at > kCodecCpusMaxAge) {
+        l.next = sample();
+        l.at = now;
+    }
+    return l.ready.valid() ? l.ready : l.next;
 }
 
 extern "C" {
@@ -668,7 +692,7 @@ qgcm_ctx *qgcm_create(int device, uint32_t max_keys, char *err, int errlen) {
         qgcm_destroy(ctx);
         return nullptr;
     }
-    if (ctx->chain_pin) ctx->codec_cpus_pending = codec_cpu_list(ctx->device);
+    if (ctx->chain_pin) (void)codec_cpu_list(ctx->device);  // starts the first load sample
     return ctx;
 }
 
@@ -742,6 +766,29 @@ int qgcm_set_keys(qgcm_ctx *ctx, uint32_t first_idx, uint32_t count, const uint8
 
 int qgcm_set_key(qgcm_ctx *ctx, uint32_t key_idx, const uint8_t key[QGCM_KEY_BYTES]) {
     return qgcm_set_keys(ctx, key_idx, 1, key);
+}
+
+int qgcm_clear_keys(qgcm_ctx *ctx, uint32_t first_idx, uint32_t count) {
+    if (!ctx) return QGCM_E_ARG;
+    if ((uint64_t)first_idx + count > ctx->max_keys) return QGCM_E_KEY;
+    if (count == 0) return QGCM_OK;
+    if (hipSetDevice(ctx->device) != hipSuccess) return QGCM_E_HIP;
+    std::lock_guard<std::mutex> io(ctx->io_mu);
+    hipStream_t s = ctx->pipe[1];
+    // the host map first (new per-packet calls and uniform batches fail from here on), then the device
+    // map the descriptor batches check; the resident instance caches key-valid bytes, so it ends first
+    std::lock_guard<std::mutex> res_lk(ctx->res_mu);
+    Resident *res = ctx->res.load(std::memory_order_acquire);
+    (void)resident_pause(res);
+    {
+        std::lock_guard<std::mutex> g(ctx->key_mu);
+        for (uint32_t i = 0; i < count; ++i) __atomic_store_n(&ctx->key_set[first_idx + i], (uint8_t)0, __ATOMIC_RELEASE);
+    }
+    int rc = QGCM_OK;
+    if (hipMemsetAsync(ctx->d_key_valid + first_idx, 0, count, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+        rc = QGCM_E_HIP;
+    resident_resume(res);
+    return rc;
 }
 
 int qgcm_seal_batch(qgcm_ctx *ctx, uint8_t *d_arena, const qgcm_desc *d_descs, uint32_t n, const uint8_t *d_nonces,
@@ -1160,14 +1207,17 @@ static int run_host_chain(qgcm_ctx *ctx, bool seal, uint8_t *h_arena, uint64_t s
         }
     };
     const int nt = (seal && dev_ok && dev_mode == 2) ? 0 : std::max(1, std::min(threads, 256));
-    if (ctx->chain_pin && nt > 0)
-        std::call_once(ctx->codec_cpus_once, [ctx] {
-            if (ctx->codec_cpus_pending.valid()) ctx->codec_cpus = ctx->codec_cpus_pending.get();
-        });
-    const std::vector<int> *pin = ctx->chain_pin && !ctx->codec_cpus.empty() ? &ctx->codec_cpus : nullptr;
+    std::vector<int> cores;  // one CPU per worker, or empty: left to the scheduler
+    if (ctx->chain_pin && nt > 0) {
+        std::lock_guard<std::mutex> g(ctx->codec_cpus_mu);
+        const auto f = codec_cpu_list(ctx->device);
+        if (f.valid() && (ctx->codec_cpus.empty() || f.wait_for(std::chrono::seconds(0)) == std::future_status::ready))
+            ctx->codec_cpus = f.get();
+        if ((size_t)nt <= ctx->codec_cpus.size()) cores = ctx->codec_cpus;
+    }
     for (int t = 0; t < nt; ++t)
-        pool.workers.emplace_back([&work, pin, t] {
-            if (pin) qgcm::pin_to_cpu((*pin)[(size_t)t % pin->size()]);
+        pool.workers.emplace_back([&work, cpu = cores.empty() ? -1 : cores[(size_t)t]] {
+            if (cpu >= 0) qgcm::pin_to_cpu(cpu);
             work();
         });
     // seal: the device takes a chunk when fewer than ahead_min compressed host chunks are waiting as a

@@ -754,6 +754,11 @@ __device__ int gdecode(const GDec &w, uint32_t n, uint32_t cap) {
             ip += 4;
         }
         if (off == 0 || off > op || len > total - op) return -1;
+        // the bytes read back were written by OTHER lanes in earlier elements: the wave's LDS ops run in
+        // order, but the compiler must not move these reads above those writes (a cross-lane dependence
+        // it cannot see): a compiler fence (the wave decoder's wave_lds_sync also waits; in-order LDS
+        // needs only the fence)
+        asm volatile("" ::: "memory");
         uint8_t v[4];
 #pragma unroll
         for (uint32_t k = 0; k < 4; ++k) v[k] = w.out[op - off + mod64(w.gl + kGL * k, off)];

@@ -20,8 +20,9 @@
  *   TestAESConcurrentGoroutines 16 threads x 200 packets through one key, 4-B AAD
  *   TestNewAESAcrossMembers 6 peers' keys spread over both members; each seals on its owner, the other
  *                      member (which never got the key) refuses it, a peer's packet fails under another's key
- *   TestSlotsRecycled  4 x QGCM_MAX_PEERS NewAES calls, every earlier AES collected (its finalizer frees
- *                      the slot): the same slots are re-keyed with new keys, each checked against the oracle
+ *   TestSlotsRecycled  4 x QGCM_MAX_PEERS NewAES calls, every earlier AES collected (its finalizer marks the
+ *                      slot's key unset and frees the slot: the stale index then fails both ways): the same
+ *                      slots are re-keyed with new keys, each checked against the oracle
  *   TestGPUGroupBatch  NewGPUGroup({0,0}) + GPUGroup.NewAES / Order / NewArena / SealBatch / OpenBatch:
  *                      600 packets of 8 peers (one key slot never set) in Order's order in a pinned arena;
  *                      sealed against the oracle, opened back, a tampered packet zeroed, the unset key's
@@ -95,7 +96,8 @@ static struct group *new_group(const int *devs, int n, uint32_t max) {
     return gg;
 }
 
-static void release_slot(struct group *gg, uint32_t idx) { /* the AES finalizer */
+static void release_slot(struct group *gg, uint32_t idx) { /* the AES finalizer: GPUGroup.release */
+    qgcm_group_clear_keys(gg->g, idx, 1);
     pthread_mutex_lock(&gg->mu);
     gg->free[gg->nfree++] = idx;
     pthread_mutex_unlock(&gg->mu);
@@ -315,7 +317,15 @@ static void TestSlotsRecycled(void) {
     struct aes prev = {0};
     int have_prev = 0;
     for (uint32_t i = 0; i < 4 * gg->max; ++i) {
-        if (have_prev) release_slot(gg, prev.idx); /* runtime.GC(): the previous AES was collected */
+        if (have_prev) {
+            release_slot(gg, prev.idx); /* runtime.GC(): the previous AES was collected */
+            /* a KeyIndex kept past its AES (a batch Desc) now fails, in both directions, bytes untouched */
+            uint8_t z[64 + 28], zb[64 + 28];
+            for (int j = 0; j < 64 + 28; ++j) z[j] = zb[j] = (uint8_t)(j * 3 + i);
+            CHECK(qgcm_seal_one(prev.ctx, prev.idx, z, 64, NULL, 0, NULL) == -1);
+            CHECK(qgcm_open_one(prev.ctx, prev.idx, z, 64 + 28, NULL, 0) == -1);
+            CHECK(memcmp(z, zb, sizeof z) == 0);
+        }
         uint8_t salt[32];
         memset(salt, (int)(i * 13 + 5), sizeof salt); /* every NewAES a different key */
         struct aes a;

@@ -295,7 +295,20 @@ void TestNewAESSlotsRecycled() {
     uint8_t ip[4] = {10, 0, 0, 7};
     const Slice aad{ip, 4, 4};
     for (int round = 0; round < 3; ++round) {
+        // the slots and owners of the AES objects about to go: a Slot() kept past its AES (a batch
+        // descriptor) must fail once the slot is back in the set, bytes untouched
+        std::vector<std::pair<qgcm_ctx *, uint32_t>> stale;
+        for (const auto &a : live)
+            stale.push_back({qgcm_group_ctx(crypto::DeviceSet::Get().first->handle(),
+                                            qgcm_group_shard(crypto::DeviceSet::Get().first->handle(), a->Slot())),
+                             a->Slot()});
         live.clear();  // every slot back
+        for (const auto &[c, s] : stale) {
+            std::vector<uint8_t> z(92, 0x33), zb = z;
+            if (qgcm_seal_one(c, s, z.data(), 64, nullptr, 0, nullptr) != -1 ||
+                qgcm_open_one(c, s, z.data(), 92, nullptr, 0) != -1 || z != zb)
+                FATAL("a released slot still seals or opens");
+        }
         for (int i = 0; i < 4; ++i) {
             auto [a, err] = crypto::NewAES(MakeSlice(key), MakeSlice(salt));
             if (!err.ok() || !a) FATAL("recycled NewAES: " + err.msg);

@@ -16,6 +16,15 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def _digests_ok(line: dict, prefix: int) -> None:
+    """Every rank hashed its own arena prefix against tests/golden/rank_digest.json after the timed loop
+    (seeds 0x5EED0001 + r): the timed state, one more seal, the open back."""
+    per = line["per_gpu"]
+    assert all(g["sealed_digest_ok"] is True and g["opened_digest_ok"] is True for g in per), per
+    assert line["sealed_digest_ok"] is True and line["opened_digest_ok"] is True
+    assert line["digest_prefix"] == prefix
+
+
 def test_bench_two_ranks_one_device():
     import torch
 
@@ -39,6 +48,7 @@ def test_bench_two_ranks_one_device():
     assert [g["rank"] for g in per] == [0, 1] and all(g["packets"] == 65536 and g["GiB_s"] > 0 for g in per)
     assert line["per_gpu_GiB_s"]["min"] <= line["per_gpu_GiB_s"]["max"]
     assert line["dist_backend"] == "gloo"
+    _digests_ok(line, 1 << 16)
 
 
 def test_bench_config4_two_ranks_one_device():
@@ -62,6 +72,7 @@ def test_bench_config4_two_ranks_one_device():
     assert line["config"]["packets_total"] == 64 << 20 and line["config"]["packets_per_gpu"] == 32 << 20
     assert line["config"]["workload"].startswith("config4")
     assert [g["packets"] for g in line["per_gpu"]] == [32 << 20, 32 << 20]
+    _digests_ok(line, 1 << 20)  # each rank's first 2^20 slots of its 2^25-packet shard
 
 
 def test_bench_rccl_process_group_one_rank():
@@ -84,6 +95,7 @@ def test_bench_rccl_process_group_one_rank():
     line = json.loads(lines[0])
     assert line["dist_backend"] == "nccl" and line["status_ok"] is True and line["n_gpus"] == 1
     assert len(line["per_gpu"]) == 1 and line["per_gpu"][0]["packets"] == 65536
+    _digests_ok(line, 1 << 16)
 
 
 def test_bench_gpus_flag_spawns_ranks():
@@ -129,3 +141,4 @@ def test_bench_eight_ranks_one_device():
     per = line["per_gpu"]
     assert [g["rank"] for g in per] == list(range(8)) and all(g["packets"] == 262144 and g["GiB_s"] > 0 for g in per)
     assert line["value"] > 0 and line["dist_backend"] == "gloo"
+    _digests_ok(line, 1 << 18)  # ranks 0..7, each against its own seeds

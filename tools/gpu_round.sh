@@ -3,7 +3,7 @@
 # reference build, and the config-2 profile (trace + PMC).  Every GPU step has its own time limit;
 # the script stops at the first step that faults, aborts or times out (a plain test failure goes on).
 # Usage: bash tools/gpu_round.sh <tag> [steps...]
-#   steps: stests policy snapdev rtests tests smoke bench ab prof pp prof3 exp_res res_trace ahead barreq align
+#   steps: probe copyab r6tests pp6 stests policy snapdev rtests tests smoke bench ab prof pp prof3 exp_res res_trace ahead barreq align
 #          r4tests abrealign snapab profsnap gtests ftests hostsizes smallwl smalltrace copytrace
 #          (default: tests smoke bench ab prof)
 set -u
@@ -256,6 +256,28 @@ for s in $STEPS; do
       bash tools/profile_snappy.sh ${TAG}_s3 > $OUT/profsnap3.log 2>&1
       check profsnap3 $?
       python3 tools/pmc_kernels.py gpurun_out/prof_snappy_${TAG}_s3 1048576 snappy_compress_group snappy_compress_kernel snappy_uncompress_kernel > $OUT/snappy_pmc_s3.txt 2>&1 ;;
+    probe)  # what GPU telemetry (clock, power, cap) this box gives an unprivileged process
+      timeout -k 10 120 python3 tools/probe_telemetry.py > $OUT/telemetry_probe.jsonl 2> $OUT/telemetry_probe.err
+      check probe $? ;;
+    copyab)  # HBM copy kernel shapes (tools/microbench/copy.hip): the roofline's achievable-copy reference
+      timeout -k 10 120 tools/bin/copy_bench 1.48 10 > $OUT/copy_bench.jsonl 2> $OUT/copy_bench.err
+      check copyab $? ;;
+    r6tests)  # the suites round 6 changed
+      timeout -k 10 900 python3 -u -m pytest tests/test_gpu_parity.py tests/test_cpp_mirror.py tests/test_bench_dist.py tests/test_gpu_snappy.py tests/test_gpu_config5.py -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/r6_tests.txt 2>&1
+      check r6tests $? ;;
+    pp6)  # per-packet host CPU per pair: resident callers spinning (default) vs all asleep (SPINNERS=0), 16 / 64 threads
+      for rep in 1 2; do
+        for sp in default 0; do
+          for t in 16 64; do
+            if [ $sp = default ]; then
+              timeout -k 10 60 tools/bin/per_packet_bench $t 1350 2 0 resident >> $OUT/pp6.jsonl 2>> $OUT/pp6.err
+            else
+              QGCM_RESIDENT_SPINNERS=$sp timeout -k 10 60 tools/bin/per_packet_bench $t 1350 2 0 resident >> $OUT/pp6.jsonl 2>> $OUT/pp6.err
+            fi
+            check pp6_${sp}_$t $?
+          done
+        done
+      done ;;
     snapab)  # device snappy codec: group vs wave encoder, interleaved
       timeout -k 10 300 python3 tools/exp_snappy_dev.py 5 2 > $OUT/snap_ab.jsonl 2> $OUT/snap_ab.err
       check snapab $? ;;

@@ -1,0 +1,152 @@
+// Microbenchmark: achievable HBM copy rate (read + write bytes / s) on gfx950, by kernel shape.
+// libqgcm's stream_copy_kernel (grid-stride, each lane's four 16-B loads a
+// whole grid apart, grid capped at 8 workgroups per CU) read 4.59 TB/s; MI355X_MICROARCH.md quotes
+// 6.29 TB/s for a float4 copy.  Variants:
+//   0  the round-5 library kernel (grid-stride, 4 loads in flight per lane, 8 x 256-thread WG per CU)
+//   1  one tile per workgroup: 256 threads x U 16-B loads, contiguous per workgroup, no loop (U = 4)
+//   2  as 1 with U = 8
+//   3  as 1, non-temporal loads and stores
+//   4  as 2, non-temporal loads and stores
+//   5  persistent: each wave a contiguous run of 1 KiB rows, 4 rows in flight, 16 waves per CU
+//   6  as 5, non-temporal
+// Build: hipcc --offload-arch=gfx950 -O3 copy.hip -o copy      Run: ./copy [GB] [reps]
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#define CK(x)                                                                      \
+    do {                                                                           \
+        hipError_t e_ = (x);                                                       \
+        if (e_ != hipSuccess) {                                                    \
+            fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+            exit(1);                                                               \
+        }                                                                          \
+    } while (0)
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__global__ void __launch_bounds__(256) k_grid_stride(u32x4 *__restrict__ dst, const u32x4 *__restrict__ src,
+                                                     uint64_t n16) {
+    const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + 3 * step < n16; i += 4 * step) {
+        const u32x4 a = src[i], b = src[i + step], c = src[i + 2 * step], d = src[i + 3 * step];
+        dst[i] = a;
+        dst[i + step] = b;
+        dst[i + 2 * step] = c;
+        dst[i + 3 * step] = d;
+    }
+    for (; i < n16; i += step) dst[i] = src[i];
+}
+
+template <int U, bool NT>
+__global__ void __launch_bounds__(256) k_tile(u32x4 *__restrict__ dst, const u32x4 *__restrict__ src, uint64_t n16) {
+    const uint64_t base = (uint64_t)blockIdx.x * (256 * U) + threadIdx.x;
+    u32x4 v[U];
+    if (base + 256 * (U - 1) < n16) {
+#pragma unroll
+        for (int k = 0; k < U; ++k) v[k] = NT ? __builtin_nontemporal_load(src + base + 256 * k) : src[base + 256 * k];
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            if (NT)
+                __builtin_nontemporal_store(v[k], dst + base + 256 * k);
+            else
+                dst[base + 256 * k] = v[k];
+        }
+    } else {
+        for (int k = 0; k < U; ++k)
+            if (base + 256 * k < n16) dst[base + 256 * k] = src[base + 256 * k];
+    }
+}
+
+// each wave copies rows of 64 x 16 B; wave w takes rows w, w + W, ... (W = total waves), 4 in flight
+template <bool NT>
+__global__ void __launch_bounds__(256) k_wave_rows(u32x4 *__restrict__ dst, const u32x4 *__restrict__ src,
+                                                   uint64_t n16) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t waves = (uint64_t)gridDim.x * 4, w = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint64_t rows = n16 / 64;
+    // contiguous runs: wave w owns rows [w * per, (w + 1) * per)
+    const uint64_t per = (rows + waves - 1) / waves;
+    uint64_t r = w * per, end = r + per < rows ? r + per : rows;
+    for (; r + 3 < end; r += 4) {
+        u32x4 v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const u32x4 *p = src + (r + k) * 64 + lane;
+            v[k] = NT ? __builtin_nontemporal_load(p) : *p;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            u32x4 *p = dst + (r + k) * 64 + lane;
+            if (NT)
+                __builtin_nontemporal_store(v[k], p);
+            else
+                *p = v[k];
+        }
+    }
+    for (; r < end; ++r) dst[r * 64 + lane] = src[r * 64 + lane];
+}
+
+static void launch(int var, u32x4 *d, const u32x4 *s, uint64_t n16, int cus) {
+    switch (var) {
+        case 0: {
+            const uint64_t want = (n16 + 255) / 256;
+            const uint32_t g = (uint32_t)(want < (uint64_t)cus * 8 ? want : (uint64_t)cus * 8);
+            hipLaunchKernelGGL(k_grid_stride, dim3(g), dim3(256), 0, 0, d, s, n16);
+            break;
+        }
+        case 1: hipLaunchKernelGGL((k_tile<4, false>), dim3((n16 + 1023) / 1024), dim3(256), 0, 0, d, s, n16); break;
+        case 2: hipLaunchKernelGGL((k_tile<8, false>), dim3((n16 + 2047) / 2048), dim3(256), 0, 0, d, s, n16); break;
+        case 3: hipLaunchKernelGGL((k_tile<4, true>), dim3((n16 + 1023) / 1024), dim3(256), 0, 0, d, s, n16); break;
+        case 4: hipLaunchKernelGGL((k_tile<8, true>), dim3((n16 + 2047) / 2048), dim3(256), 0, 0, d, s, n16); break;
+        case 5: hipLaunchKernelGGL((k_wave_rows<false>), dim3(cus * 4), dim3(256), 0, 0, d, s, n16); break;
+        case 6: hipLaunchKernelGGL((k_wave_rows<true>), dim3(cus * 4), dim3(256), 0, 0, d, s, n16); break;
+    }
+}
+
+int main(int argc, char **argv) {
+    const double gb = argc > 1 ? atof(argv[1]) : 1.48;
+    const int reps = argc > 2 ? atoi(argv[2]) : 10;
+    const uint64_t bytes = (uint64_t)(gb * 1e9) & ~(uint64_t)16383;
+    const uint64_t n16 = bytes / 16;
+    int cus = 0;
+    CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+    u32x4 *s, *d;
+    CK(hipMalloc(&s, bytes));
+    CK(hipMalloc(&d, bytes));
+    CK(hipMemset(s, 0x5a, bytes));
+    CK(hipMemset(d, 0, bytes));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    const int nvar = 7;
+    double best[nvar] = {0};
+    for (int round = 0; round < 3; ++round) {
+        for (int var = 0; var < nvar; ++var) {
+            launch(var, d, s, n16, cus);  // warm
+            CK(hipGetLastError());
+            CK(hipEventRecord(e0, 0));
+            for (int r = 0; r < reps; ++r) launch(var, d, s, n16, cus);
+            CK(hipEventRecord(e1, 0));
+            CK(hipEventSynchronize(e1));
+            float ms = 0;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            const double tbs = 2.0 * bytes * reps / (ms * 1e-3) / 1e12;
+            if (tbs > best[var]) best[var] = tbs;
+            printf("{\"round\": %d, \"variant\": %d, \"bytes\": %llu, \"TB_s\": %.3f}\n", round, var,
+                   (unsigned long long)bytes, tbs);
+            fflush(stdout);
+        }
+    }
+    // check the last variant's copy
+    unsigned char *h = (unsigned char *)malloc(1 << 20);
+    CK(hipMemcpy(h, (char *)d + bytes - (1 << 20), 1 << 20, hipMemcpyDeviceToHost));
+    int bad = 0;
+    for (int i = 0; i < (1 << 20); ++i) bad += h[i] != 0x5a;
+    printf("{\"best_TB_s\": [");
+    for (int v = 0; v < nvar; ++v) printf("%s%.3f", v ? ", " : "", best[v]);
+    printf("], \"tail_bad_bytes\": %d, \"cus\": %d}\n", bad, cus);
+    return bad != 0;
+}

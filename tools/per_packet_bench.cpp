@@ -175,8 +175,14 @@ int main(int argc, char **argv) {
                        g[3] / 100.0 / n, g[4] / 100.0 / n, n, g[7] ? g[6] * 100.0 / g[7] : 0.0);
             }
         }
-        printf(", \"cpus_busy\": %.2f, \"cgroup_throttled\": %llu, \"cgroup_throttled_ms\": %.1f", (c1.cpu_s - c0.cpu_s) / wall,
-               c1.nr_throttled - c0.nr_throttled, (c1.throttled_usec - c0.throttled_usec) / 1000.0);
+        // host CPU time per seal+open pair (the process's CPU seconds over the timed run / pairs served):
+        // what the per-call drop-in costs quantum's host next to the CPU plugin chain's figure
+        const double busy = (c1.cpu_s - c0.cpu_s) / wall;
+        const char *sp = getenv("QGCM_RESIDENT_SPINNERS");
+        printf(", \"cpus_busy\": %.2f, \"cpu_us_per_pair\": %.2f, \"spinners_env\": \"%s\", \"cgroup_throttled\": %llu, "
+               "\"cgroup_throttled_ms\": %.1f",
+               busy, r.rt_per_s > 0 ? busy / r.rt_per_s * 1e6 : 0.0, sp ? sp : "default", c1.nr_throttled - c0.nr_throttled,
+               (c1.throttled_usec - c0.throttled_usec) / 1000.0);
         printf("}\n");
         fflush(stdout);
         if (r.fail) rc = 2;
