@@ -61,6 +61,7 @@ struct qgcm_ctx {
     uint64_t chain_chunk = kPipeChunk;
     int chain_slots = kPipeStreams, chain_dev_ahead = 2, chain_dev_backlog = -1;
     bool snappy_group = true;
+    int snappy_per_cu = 0;  // QGCM_SNAPPY_PER_CU: cap on resident codec waves per CU (0 = as the LDS allows; A/B knob)
     // the chain's host codec workers run one per physical core, the GPU's NUMA-local cores and the least
     // busy first (cpu_topo.cpp; QGCM_CHAIN_PIN=0 at qgcm_create: left to the scheduler).  The core list
     // comes from a 30-ms sample of the host's load, taken per device in the background from the first
@@ -659,6 +660,7 @@ qgcm_ctx *qgcm_create(int device, uint32_t max_keys, char *err, int errlen) {
     ctx->chain_dev_ahead = std::max(1, env_int("QGCM_CHAIN_DEV_AHEAD", 2));
     ctx->chain_dev_backlog = env_int("QGCM_CHAIN_DEV_BACKLOG", -1);
     ctx->snappy_group = env_int("QGCM_SNAPPY_GROUP", 1) != 0;
+    ctx->snappy_per_cu = std::max(0, env_int("QGCM_SNAPPY_PER_CU", 0));
     ctx->chain_pin = env_int("QGCM_CHAIN_PIN", 1) != 0;
     ctx->desc_one_on = !off("QGCM_DESC_ONE");
     ctx->host_direct = !off("QGCM_HOST_DIRECT");
@@ -1425,6 +1427,7 @@ static int run_snappy(qgcm_ctx *ctx, bool compress, uint8_t *d_arena, uint64_t s
     while (waves > 1 && (size_t)waves * a.wave_bytes > 64u * 1024u) --waves;
     int per_cu = (int)((160u * 1024u) / ((uint32_t)waves * a.wave_bytes));
     per_cu = std::max(1, std::min(per_cu, 8));
+    if (ctx->snappy_per_cu) per_cu = std::min(per_cu, std::max(1, ctx->snappy_per_cu / waves));
     const uint64_t need = (n + (uint64_t)waves * per_wave - 1) / ((uint64_t)waves * per_wave);
     const int grid = (int)std::min<uint64_t>(need, (uint64_t)ctx->num_cus * per_cu);
     if (hipSetDevice(ctx->device) != hipSuccess) return QGCM_E_HIP;

@@ -260,8 +260,10 @@ for s in $STEPS; do
       timeout -k 10 120 python3 tools/probe_telemetry.py > $OUT/telemetry_probe.jsonl 2> $OUT/telemetry_probe.err
       check probe $? ;;
     copyab)  # HBM copy kernel shapes (tools/microbench/copy.hip): the roofline's achievable-copy reference
-      timeout -k 10 120 tools/bin/copy_bench 1.48 10 > $OUT/copy_bench.jsonl 2> $OUT/copy_bench.err
-      check copyab $? ;;
+      for gb in ${COPYGB:-1.48}; do
+        timeout -k 10 120 tools/bin/copy_bench $gb 10 > $OUT/copy_bench_$gb.jsonl 2> $OUT/copy_bench.err
+        check copyab_$gb $?
+      done ;;
     r6tests)  # the suites round 6 changed
       timeout -k 10 900 python3 -u -m pytest tests/test_gpu_parity.py tests/test_cpp_mirror.py tests/test_bench_dist.py tests/test_gpu_snappy.py tests/test_gpu_config5.py -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/r6_tests.txt 2>&1
       check r6tests $? ;;
@@ -278,6 +280,9 @@ for s in $STEPS; do
           done
         done
       done ;;
+    snapocc)  # device snappy encoder time vs the waves per CU it may hold (QGCM_SNAPPY_PER_CU), interleaved
+      timeout -k 10 400 python3 tools/exp_snappy_occupancy.py 5 3 > $OUT/snappy_occupancy.jsonl 2> $OUT/snappy_occupancy.err
+      check snapocc $? ;;
     snapab)  # device snappy codec: group vs wave encoder, interleaved
       timeout -k 10 300 python3 tools/exp_snappy_dev.py 5 2 > $OUT/snap_ab.jsonl 2> $OUT/snap_ab.err
       check snapab $? ;;
