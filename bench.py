@@ -40,6 +40,7 @@ from quantum_amd import batch, shard  # noqa: E402
 from quantum_amd.crypto import Context, derive_key  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, MI355X_MICROARCH.md "Chip-level parameters"
+COPY_GUIDE_GBS = 6290.0  # the same table's measured float4 copy (read + write)
 # PMC passes of this command (tools/pmc_traffic.py), newest first
 LAUNCH_CHUNK = 1 << 19  # quantum_amd/csrc/gcm_internal.h kLaunchChunk
 TRAFFIC_JSONS = [os.path.join(ROOT, "profiles", d, "traffic.json") for d in ("r5_s37", "r5_s7", "r4_s21", "r4_s3", "r3_s39", "r3_s15", "r3_s1")]
@@ -265,11 +266,14 @@ def cpu_baseline(key: bytes, L: int, threads: int, host: dict, seconds: float = 
 
 
 def stream_copy_gbs(ctx, nbytes: int, dev, stream, reps: int = 5) -> float:
-    """Achievable HBM copy rate (read + write bytes / s) with libqgcm's in-repo stream kernel."""
+    """Achievable HBM copy rate (read + write bytes / s) with libqgcm's in-repo stream kernel (one 16-B
+    non-temporal load and store per lane, a 4-KiB tile per workgroup: the fastest of the shapes
+    tools/microbench/copy.hip timed, profiles/r6_s2), on random bytes (a constant buffer runs at a
+    higher clock)."""
     from quantum_amd import _lib
 
     nbytes &= ~15
-    src = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    src = torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device=dev)
     dst = torch.empty(nbytes, dtype=torch.uint8, device=dev)
     h = stream.cuda_stream
     _lib.check(_lib.lib().qgcm_stream_copy(ctx.handle, dst.data_ptr(), src.data_ptr(), nbytes, h), "stream_copy")
@@ -1135,9 +1139,15 @@ def main() -> None:
                          "achieved_read_only": round(achieved_read, 1),
                          "read_bytes_per_packet": read_pkt,
                          "copy_achievable": round(copy_gbs, 1),
-                         "frac_of_copy": round(achieved / copy_gbs, 4),
+                         "copy_reference_guide": COPY_GUIDE_GBS,
+                         # against the larger of this run's copy kernel and the guide's measured float4 copy
+                         "frac_of_copy": round(achieved / max(copy_gbs, COPY_GUIDE_GBS), 4),
                          "binding_unit": "LDS (T-table AES + comb GHASH lookups, DESIGN.md 4.1)",
-                         "lds_array_busy": lds_busy},
+                         "lds_array_busy": lds_busy,
+                         # the kernel's cycles per launch at the measured mean GFX clock: the box-independent
+                         # figure (the kernel runs at the chip's power limit, so boxes differ by their clock)
+                         "launch_mcycles_at_mean_sclk": (round(kms / launches * clock["sclk_mhz_mean"] / 1e3, 3)
+                                                         if clock["sclk_mhz_mean"] else None)},
             "kernels_ms": {"seal": round(seal_ms, 4), "open": round(open_ms, 4)},
             "per_gpu": [{"rank": r, "packets": int(p[3]), "ms_per_step": round(p[0] * 1e3 / args.steps, 4),
                          "GiB_s": round(2 * p[3] * L / (p[0] / args.steps) / 2**30, 2),

@@ -22,6 +22,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "gcm_internal.h"
 
 namespace qgcm {
@@ -2263,20 +2265,20 @@ __global__ void fill_uniform_kernel(uint8_t *arena, uint64_t stride, uint32_t n,
         fill_uniform_item(arena, stride, len, groups, aad_word, seed_payload, nonces, seed_nonce, t);
 }
 
-// Streaming copy, 16 B per lane, grid-stride: the achievable-HBM reference the roofline is also
-// quoted against (SURVEY.md §8d "measure the achievable copy bandwidth with an in-repo stream kernel").
+// Streaming copy: the achievable-HBM reference the roofline is also quoted against (SURVEY.md s8d
+// "measure the achievable copy bandwidth with an in-repo stream kernel").  One 16-B non-temporal load and
+// store per lane, one 4-KiB tile per 256-thread workgroup, a grid that covers the buffer (no loop).
+// tools/microbench/copy.hip timed twelve shapes in one process on random data (profiles/r6_s2): this one
+// 6.52 TB/s read + write on a 1.48-GB buffer and 6.47 on 8 GB; the round-5 form (grid-stride, each lane's
+// four loads a grid apart, 8 workgroups per CU) 4.45 / 4.80, the same tile shape with cached accesses
+// 5.73 / 5.61 and with four 16-B pieces per lane 5.87 / 5.75.
 __global__ void __launch_bounds__(256) stream_copy_kernel(uint4 *__restrict__ dst, const uint4 *__restrict__ src,
                                                           uint64_t n16) {
-    const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
-    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    for (; i + 3 * step < n16; i += 4 * step) {  // four 16-B loads in flight per lane
-        const uint4 a = src[i], b = src[i + step], c = src[i + 2 * step], d = src[i + 3 * step];
-        dst[i] = a;
-        dst[i + step] = b;
-        dst[i + 2 * step] = c;
-        dst[i + 3 * step] = d;
-    }
-    for (; i < n16; i += step) dst[i] = src[i];
+    typedef uint32_t v4 __attribute__((ext_vector_type(4)));  // the builtins take native vector types
+    const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (i < n16)
+        __builtin_nontemporal_store(__builtin_nontemporal_load(reinterpret_cast<const v4 *>(src) + i),
+                                    reinterpret_cast<v4 *>(dst) + i);
 }
 
 // Record moves for the group dispatcher's zero-copy path (group.cpp): one wave per record copies
@@ -2321,10 +2323,15 @@ hipError_t launch_move_records(const RecMove *d_moves, uint32_t n, const uint8_t
 hipError_t launch_stream_copy(void *dst, const void *src, uint64_t bytes, int num_cus, hipStream_t s) {
     const uint64_t n16 = bytes / 16;
     if (n16 == 0) return hipSuccess;
-    const uint64_t want = (n16 + 255) / 256;
-    const uint32_t g = (uint32_t)(want < (uint64_t)num_cus * 8 ? want : (uint64_t)num_cus * 8);
-    hipLaunchKernelGGL(stream_copy_kernel, dim3(g), dim3(256), 0, s, static_cast<uint4 *>(dst),
-                       static_cast<const uint4 *>(src), n16);
+    (void)num_cus;
+    // a grid of one 256-lane tile per 4 KiB, launched in pieces of at most 2^30 tiles (4 TiB) each
+    for (uint64_t done = 0; done < n16;) {
+        const uint64_t left = n16 - done, tiles = std::min<uint64_t>((left + 255) / 256, 1ull << 30);
+        const uint64_t cnt = std::min<uint64_t>(left, tiles * 256);
+        hipLaunchKernelGGL(stream_copy_kernel, dim3((uint32_t)tiles), dim3(256), 0, s, static_cast<uint4 *>(dst) + done,
+                           static_cast<const uint4 *>(src) + done, cnt);
+        done += cnt;
+    }
     return hipGetLastError();
 }
 
