@@ -1106,7 +1106,9 @@ def main() -> None:
     # libqgcm launches a uniform batch in chunks of LAUNCH_CHUNK packets: kms spans them all
     chunk = int(os.environ.get("QGCM_LAUNCH_CHUNK", str(LAUNCH_CHUNK))) // 64 * 64 or N
     launches = -(-N // chunk)
-    copy_gbs = stream_copy_gbs(ctx, N * stride, dev, stream)  # after the timed region
+    # after the timed region; an arena-sized buffer up to 4 GiB (past the 256-MiB Infinity Cache the rate
+    # does not depend on the size: 6.52 / 6.47 TB/s at 1.48 / 8 GB, profiles/r6_s2)
+    copy_gbs = stream_copy_gbs(ctx, min(N * stride, 4 << 30), dev, stream)
 
     if rank == 0:
         line = {
