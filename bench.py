@@ -43,7 +43,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, MI355X_MICROARCH.md "Chip-level para
 COPY_GUIDE_GBS = 6290.0  # the same table's measured float4 copy (read + write)
 # PMC passes of this command (tools/pmc_traffic.py), newest first
 LAUNCH_CHUNK = 1 << 19  # quantum_amd/csrc/gcm_internal.h kLaunchChunk
-TRAFFIC_JSONS = [os.path.join(ROOT, "profiles", d, "traffic.json") for d in ("r5_s37", "r5_s7", "r4_s21", "r4_s3", "r3_s39", "r3_s15", "r3_s1")]
+TRAFFIC_JSONS = [os.path.join(ROOT, "profiles", d, "traffic.json") for d in ("r6_s3", "r5_s37", "r5_s7", "r4_s21", "r4_s3", "r3_s39", "r3_s15", "r3_s1")]
 CONFIG4_PACKETS = 64 << 20  # BASELINE config 4: 64 M packets over the node's GPUs
 SECRET = b"AES256Key-32Characters1234567890"
 SALT = bytes(range(32))
@@ -842,7 +842,12 @@ class GpuTelemetry:
             c = self._num(m.get("current_gfxclk")) or self._num(m.get("average_gfxclk_frequency"))
             clks = [c] if c else []
         power = self._num(m.get("current_socket_power")) or self._num(m.get("average_socket_power"))
+        soc = m.get("current_socclks")
+        socs = [self._num(c) for c in soc] if isinstance(soc, (list, tuple)) else [self._num(m.get("current_socclk"))]
+        socs = [c for c in socs if c]
         return {"t": time.perf_counter(), "sclk": sum(clks) / len(clks) if clks else None, "power": power,
+                "uclk": self._num(m.get("current_uclk")), "socclk": sum(socs) / len(socs) if socs else None,
+                "hotspot": self._num(m.get("temperature_hotspot")),
                 "acc": {k: self._num(m.get(k)) for k in ("accumulation_counter", "ppt_residency_acc",
                                                            "socket_thm_residency_acc", "prochot_residency_acc")},
                 "throttle": m.get("throttle_status")}
@@ -886,6 +891,10 @@ class GpuTelemetry:
                "sclk_mhz_min": min(clk) if clk else None, "sclk_mhz_max": max(clk) if clk else None,
                "power_w_mean": round(sum(pw) / len(pw), 1) if pw else None, "power_w_max": max(pw) if pw else None,
                "power_cap_w": cap, "samples": len(self.samples),
+               **{f"{k}_mean": (round(sum(v) / len(v), 1) if v else None)
+                  for k, v in (("uclk_mhz", [x["uclk"] for x in self.samples if x["uclk"]]),
+                               ("socclk_mhz", [x["socclk"] for x in self.samples if x["socclk"]]),
+                               ("hotspot_c", [x["hotspot"] for x in self.samples if x["hotspot"]]))},
                "telemetry": f"amdsmi gpu_metrics every {self.period * 1e3:.0f} ms over the timed steps"}
         a0, a1 = (self.first or {}).get("acc", {}), (self.last or {}).get("acc", {})
         ticks = (a1.get("accumulation_counter") or 0) - (a0.get("accumulation_counter") or 0)
