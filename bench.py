@@ -801,11 +801,13 @@ class GpuTelemetry:
     thermally-limited (its residency accumulators, differenced over the interval).  When amdsmi is
     missing or refuses this process, `summary()` says so instead of a number."""
 
-    def __init__(self, device: int, period_s: float = 0.02):
+    def __init__(self, device: int, period_s: float = 0.01):
         import threading
 
         self.period, self.samples, self.err, self.h, self.smi = period_s, [], None, None, None
         self.first = self.last = None
+        self.span = "the timed steps"
+        self.started = False
         self._stop = threading.Event()
         self._th = None
         try:
@@ -842,11 +844,8 @@ class GpuTelemetry:
             c = self._num(m.get("current_gfxclk")) or self._num(m.get("average_gfxclk_frequency"))
             clks = [c] if c else []
         power = self._num(m.get("current_socket_power")) or self._num(m.get("average_socket_power"))
-        soc = m.get("current_socclks")
-        socs = [self._num(c) for c in soc] if isinstance(soc, (list, tuple)) else [self._num(m.get("current_socclk"))]
-        socs = [c for c in socs if c]
         return {"t": time.perf_counter(), "sclk": sum(clks) / len(clks) if clks else None, "power": power,
-                "uclk": self._num(m.get("current_uclk")), "socclk": sum(socs) / len(socs) if socs else None,
+                "uclk": self._num(m.get("current_uclk")), "socclk": self._num(m.get("current_socclk")),
                 "hotspot": self._num(m.get("temperature_hotspot")),
                 "acc": {k: self._num(m.get(k)) for k in ("accumulation_counter", "ppt_residency_acc",
                                                            "socket_thm_residency_acc", "prochot_residency_acc")},
@@ -859,6 +858,7 @@ class GpuTelemetry:
                 self.samples.append(s)
 
     def start(self) -> None:
+        self.started = True
         if self.h is None:
             return
         import threading
@@ -895,7 +895,7 @@ class GpuTelemetry:
                   for k, v in (("uclk_mhz", [x["uclk"] for x in self.samples if x["uclk"]]),
                                ("socclk_mhz", [x["socclk"] for x in self.samples if x["socclk"]]),
                                ("hotspot_c", [x["hotspot"] for x in self.samples if x["hotspot"]]))},
-               "telemetry": f"amdsmi gpu_metrics every {self.period * 1e3:.0f} ms over the timed steps"}
+               "telemetry": f"amdsmi gpu_metrics every {self.period * 1e3:.0f} ms over {self.span}"}
         a0, a1 = (self.first or {}).get("acc", {}), (self.last or {}).get("acc", {})
         ticks = (a1.get("accumulation_counter") or 0) - (a0.get("accumulation_counter") or 0)
         if ticks > 0:
@@ -1051,6 +1051,11 @@ def main() -> None:
 
     # clock settle: the same step back to back for settle_ms of wall time, so the timed steps run at
     # the clocks the chip holds under this load (not timed, not counted as warmup)
+    # clock and power (GpuTelemetry): sampled from 100 ms into the settle loop (the clocks have come up
+    # by then, DESIGN.md s5 "Clock ramp") through the timed steps -- the same step back to back all along,
+    # so a short timed region (the driver's 20 steps are ~65 ms) still gets a few dozen samples
+    tele = GpuTelemetry(local)
+    tele.span = "the settle loop's last part, the warmup and the timed steps (the same step back to back)"
     settle = 0
     t_settle = time.perf_counter()
     while (time.perf_counter() - t_settle) * 1e3 < args.settle_ms:
@@ -1058,8 +1063,11 @@ def main() -> None:
         settle += 1
         if settle % 8 == 0:
             torch.cuda.synchronize()  # bound the launch queue; the loop keeps the GPU busy
-    tele = GpuTelemetry(local)  # clock and power over the warmup and timed steps (same load)
-    tele.start()
+            if not tele.started and (time.perf_counter() - t_settle) * 1e3 >= min(100.0, args.settle_ms / 2):
+                tele.start()
+    if not tele.started:
+        tele.span = "the warmup and the timed steps"
+        tele.start()
     for _ in range(args.warmup):
         step()
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]

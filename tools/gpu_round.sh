@@ -27,6 +27,9 @@ for s in $STEPS; do
     bench)
       timeout -k 10 600 python3 bench.py > $OUT/bench_line.json 2> $OUT/bench.err
       check bench $? ;;
+    benchdrv)  # the driver's round-end arguments (BENCH_r05: --steps 20 --warmup 5)
+      timeout -k 10 600 python3 bench.py --steps 20 --warmup 5 > $OUT/bench_drv_line.json 2> $OUT/bench_drv.err
+      check benchdrv $? ;;
     ab)
       timeout -k 10 300 python3 tools/ab_libs.py ablib/libqgcm_r2.so quantum_amd/libqgcm.so --rounds 15 > $OUT/ab.txt 2>&1
       check ab $? ;;
