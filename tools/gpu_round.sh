@@ -283,6 +283,9 @@ for s in $STEPS; do
           done
         done
       done ;;
+    streams)  # the headline step in several stream layouts, interleaved (tools/exp_streams.py)
+      timeout -k 10 500 python3 tools/exp_streams.py ${EXP_ROUNDS:-3} 200 > $OUT/streams.jsonl 2> $OUT/streams.err
+      check streams $? ;;
     snapocc)  # device snappy encoder time vs the waves per CU it may hold (QGCM_SNAPPY_PER_CU), interleaved
       timeout -k 10 400 python3 tools/exp_snappy_occupancy.py 5 3 > $OUT/snappy_occupancy.jsonl 2> $OUT/snappy_occupancy.err
       check snapocc $? ;;
