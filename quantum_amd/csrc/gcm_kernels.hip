@@ -730,6 +730,15 @@ __device__ __forceinline__ void quad_packet(const Batch &b, const Eng &eng, uint
 // 8 KiB of LDS), one 12-wave workgroup per CU; it takes the tiles of the keys too short for the
 // segmented kernel (and every tile when QGCM_DESC_VARIANT=13).  Both recombine the four Horner chains
 // once per packet by H^2..H^5 from the global key table (L2-resident), off the LDS pipe.
+// Single-key batches: where a wave's next tile comes from.  0: static, wave w of workgroup g takes tiles
+// g*16 + w + k*gridDim*16 (k = 0, 1, ...).  1: the same set of tiles per workgroup, shared by its 16
+// waves through an LDS counter (index i -> tile g*16 + i%16 + (i/16)*gridDim*16, i ascending), so a wave
+// that runs ahead takes more of its workgroup's tiles instead of idling while slower waves finish.
+#ifndef QGCM_TILE_POOL
+#define QGCM_TILE_POOL 1
+#endif
+constexpr uint32_t kPoolCtr = kG5Bytes + kTeBytes;  // LDS word after the uniform kernel's tables
+
 template <bool kDesc>
 constexpr int quad_waves() { return kDesc ? 12 : 16; }
 template <bool kDesc>
@@ -755,6 +764,9 @@ gcm_quad_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
         lds_st32(kTeBase + 4 * i, b.te[(slot >> 5) * 256u + x]);
     }
     if constexpr (!kDesc) g5_fill(b.gh_table + (size_t)b.uniform_key * kGhEntries + kGhH4, threadIdx.x, kT);
+    if constexpr (!kDesc && QGCM_TILE_POOL) {
+        if (threadIdx.x == 0) lds_st32(kPoolCtr, kW);  // pool indices 0..kW-1: each wave's first tile
+    }
     __syncthreads();
 
     const uint32_t lb = (lane & 31u) << 2;
@@ -822,7 +834,15 @@ gcm_quad_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
                 L -= QGCM_OVERHEAD;
             }
             off = (uint64_t)pkt * b.stride;
-            tile += gridDim.x * kW;
+            if constexpr (QGCM_TILE_POOL) {
+                // the next pool index, taken now so the LDS atomic's latency hides behind this tile
+                uint32_t i = 0;
+                if (lane == 0) i = __atomic_fetch_add((lds_u32 *)(size_t)kPoolCtr, 1u, __ATOMIC_RELAXED);
+                i = __builtin_amdgcn_readfirstlane(i);
+                tile = blockIdx.x * kW + (i % kW) + (i / kW) * gridDim.x * kW;
+            } else {
+                tile += gridDim.x * kW;
+            }
             if (!valid) {
                 if (!kSeal && b.status && pkt < b.n && m == 0) b.status[pkt] = 0;
                 continue;  // the whole quad leaves together
@@ -1975,7 +1995,7 @@ static int variant_slot(int v) {
 hipError_t init_kernels() {
     g_variants[0] = Variant{reinterpret_cast<const void *>(&gcm_quad_kernel<true, false>),
                                           reinterpret_cast<const void *>(&gcm_quad_kernel<false, false>),
-                                          quad_waves<false>(), kG5Bytes + kTeBytes,
+                                          quad_waves<false>(), kG5Bytes + kTeBytes + 16u,
                                           quad_wpe<false>() * 4 / quad_waves<false>(), false, -1};
     g_variants[1] = Variant{reinterpret_cast<const void *>(&gcm_quad_kernel<true, true>),
                                            reinterpret_cast<const void *>(&gcm_quad_kernel<false, true>),

@@ -120,7 +120,7 @@ def main() -> None:
             print(json.dumps({"mode": mode, "round": r, "steps": steps, "GiB_s": round(gib * steps / el, 2),
                               "ms_per_step": round(el * 1e3 / steps, 4), "sclk_mhz_mean": clock["sclk_mhz_mean"],
                               "power_w_mean": clock["power_w_mean"], "ppt_limited_frac": clock.get("ppt_limited_frac"),
-                              "mcycles_per_step": (round(el / steps * clock["sclk_mhz_mean"] / 1e3, 3)
+                              "mcycles_per_step": (round(el / steps * clock["sclk_mhz_mean"], 3)
                                                    if clock["sclk_mhz_mean"] else None),
                               "status_ok": int(status.sum().item()) == N,
                               "digests_ok": bool(d["sealed_digest_ok"] and d["opened_digest_ok"])}), flush=True)
