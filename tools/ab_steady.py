@@ -5,7 +5,10 @@ clock of every timed stretch (bench.GpuTelemetry), so a build's rate and its cyc
 compared.  tools/ab_libs.py times one synchronized pair per round instead.  Every build's sealed arena
 must equal the first build's.
 
-    python3 tools/ab_steady.py lib1.so lib2.so [...] [--rounds R] [--steps K]
+    python3 tools/ab_steady.py lib1.so lib2.so[:ENV=V,ENV2=V2] [...] [--rounds R] [--steps K]
+
+A ":ENV=V,..." suffix sets those environment variables around that entry's qgcm_create (the library's
+knobs are read there), so one build can be compared with itself under other settings.
 """
 import ctypes as C
 import json
@@ -31,7 +34,9 @@ def main() -> None:
     N, L, stride = 1 << 20, 1350, 1408
     vp, u32, u64 = C.c_void_p, C.c_uint32, C.c_uint64
     libs = {}
-    for path in paths:
+    for entry in paths:
+        path, _, envs = entry.partition(":")
+        env = dict(kv.split("=", 1) for kv in envs.split(",") if kv)
         lib = C.CDLL(os.path.abspath(path))
         lib.qgcm_create.restype = vp
         lib.qgcm_create.argtypes = [C.c_int, u32, C.c_char_p, C.c_size_t]
@@ -41,12 +46,19 @@ def main() -> None:
         lib.qgcm_open_uniform.argtypes = [vp, vp, u64, u32, u32, u32, u32, vp, vp]
         lib.qgcm_fill_uniform.argtypes = [vp, u64, u32, u32, u32, u64, vp, u64, vp]
         err = C.create_string_buffer(120)
+        saved = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
         ctx = lib.qgcm_create(0, 4, err, 120)
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
         assert ctx, err.value
         key = C.create_string_buffer(32)
         assert lib.qgcm_derive_key(bench.SECRET, 32, bench.SALT, 32, key) == 0
         assert lib.qgcm_set_key(ctx, 0, key.raw) == 0
-        libs[path] = (lib, ctx)
+        libs[entry] = (lib, ctx)
     alloc = torch.zeros(N * stride + 64, dtype=torch.uint8, device="cuda")
     arena = alloc[60:60 + N * stride]
     nonces = torch.zeros(12 * N, dtype=torch.uint8, device="cuda")
