@@ -56,11 +56,7 @@ struct Batch {
                                 // back and made system-visible (the host polls it instead of the stream)
     const uint4 *pw_table;      // latency engine: [pw_keys][kPwPowers][kPwEntries] kPwBits-bit comb tables of
     uint32_t pw_keys;           // H^1..H^kPwPowers (NULL / 0: the Horner + Estrin GHASH for every packet)
-    uint32_t *tile_queues;      // uniform quad kernel: NULL = each workgroup's tiles through its LDS pool;
-                                // else kTileQueues zeroed counters 64 B apart, one per eighth of the tiles
 };
-constexpr uint32_t kTileQueues = 8;        // one per XCD's share of a uniform launch (tile_queues)
-constexpr uint32_t kTileQueueSlots = 4096; // per-context ring of zeroed counter sets (kTileQueues x 64 B each)
 constexpr uint32_t kPwPowers = 128;    // flat GHASH up to d + 2 = 128 exponents (payloads up to 2016 B)
 constexpr uint32_t kPwBits = 6;                                  // comb window of the flat GHASH tables
 constexpr uint32_t kPwWin = (128 + kPwBits - 1) / kPwBits;       // windows per block (22)

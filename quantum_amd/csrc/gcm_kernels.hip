@@ -734,10 +734,6 @@ __device__ __forceinline__ void quad_packet(const Batch &b, const Eng &eng, uint
 // g*16 + w + k*gridDim*16 (k = 0, 1, ...).  1: the same set of tiles per workgroup, shared by its 16
 // waves through an LDS counter (index i -> tile g*16 + i%16 + (i/16)*gridDim*16, i ascending), so a wave
 // that runs ahead takes more of its workgroup's tiles instead of idling while slower waves finish.
-// With Batch::tile_queues set (QGCM_TILE_MODE=2 at qgcm_create), the tiles come instead from kTileQueues
-// global counters, each over a contiguous eighth of the launch's tiles: a wave draws from its
-// workgroup's queue (blockIdx % 8: the XCD round-robin, so each XCD mostly sweeps its own eighth) and,
-// once that is empty, from the next ones, so the whole grid drains together.
 #ifndef QGCM_TILE_POOL
 #define QGCM_TILE_POOL 1
 #endif
@@ -782,23 +778,6 @@ gcm_quad_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
     const uint32_t ntiles = kDesc ? (b.tile_list ? *b.n_list : b.n_items >> 4) : ((b.n + 15) >> 4);
 
     uint32_t tile = blockIdx.x * kW + wave;
-    // global tile queues (uniform batches, b.tile_queues): queue q holds tiles [ntiles*q/8, ntiles*(q+1)/8)
-    uint32_t tq = blockIdx.x % kTileQueues, tq_left = kTileQueues;
-    auto tq_next = [&]() -> uint32_t {  // the next tile, or ntiles when every queue is empty (wave-uniform)
-        while (tq_left) {
-            const uint32_t lo = (uint32_t)((uint64_t)ntiles * tq / kTileQueues);
-            const uint32_t hi = (uint32_t)((uint64_t)ntiles * (tq + 1) / kTileQueues);
-            uint32_t t = 0;
-            if (lane == 0) t = atomicAdd(b.tile_queues + 16u * tq, 1u);
-            t = __builtin_amdgcn_readfirstlane(t);
-            if (t < hi - lo) return lo + t;
-            --tq_left;
-            tq = (tq + 1) % kTileQueues;
-        }
-        return ntiles;
-    };
-    const bool queued = !kDesc && b.tile_queues != nullptr;
-    if (queued) tile = tq_next();
     if constexpr (kDesc) {  // dynamic tiles: lengths vary by 100x between tiles
         uint32_t t = 0;
         if (lane == 0) t = atomicAdd(b.tile_counter, 1u);
@@ -855,9 +834,7 @@ gcm_quad_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
                 L -= QGCM_OVERHEAD;
             }
             off = (uint64_t)pkt * b.stride;
-            if (queued) {
-                tile = tq_next();  // taken now, so the atomic's latency hides behind this tile
-            } else if constexpr (QGCM_TILE_POOL) {
+            if constexpr (QGCM_TILE_POOL) {
                 // the next pool index, taken now so the LDS atomic's latency hides behind this tile
                 uint32_t i = 0;
                 if (lane == 0) i = __atomic_fetch_add((lds_u32 *)(size_t)kPoolCtr, 1u, __ATOMIC_RELAXED);

@@ -51,11 +51,6 @@ struct qgcm_ctx {
     // streams of the context (QGCM_UNIFORM_STREAMS; the helpers wait for the caller's earlier work and
     // the caller's stream waits for them at the end, so the call stays ordered on its stream)
     int uniform_streams = 1;
-    // QGCM_TILE_MODE: 1 (default) = a uniform launch's workgroups share their tiles through LDS pools;
-    // 2 = global tile queues (Batch::tile_queues), a zeroed counter set per launch from a ring
-    int tile_mode = 1;
-    uint32_t *d_tq = nullptr;
-    std::atomic<uint32_t> tq_next{0};
     std::mutex fork_mu;                    // the helper streams and their fork/join events
     hipStream_t fork_s[3] = {};
     hipEvent_t fork_ev = nullptr, join_ev[3] = {};
@@ -388,10 +383,6 @@ int run_uniform(qgcm_ctx *ctx, bool seal, uint8_t *arena, uint64_t stride, uint3
         c.n = m;
         c.n_items = (uint32_t)(((uint64_t)m + 63) & ~63ull);
         const hipStream_t ls = ns > 1 && k % ns ? ctx->fork_s[k % ns - 1] : s;
-        if (ctx->d_tq) {  // a counter set of the ring, zeroed on the launch's stream just before it
-            c.tile_queues = ctx->d_tq + (size_t)(ctx->tq_next.fetch_add(1) % kTileQueueSlots) * kTileQueues * 16u;
-            if (hipMemsetAsync(c.tile_queues, 0, kTileQueues * 64u, ls) != hipSuccess) return QGCM_E_HIP;
-        }
         if (launch_packets(seal, v, c, grid_for(ctx, c.n_items, v), ls) != hipSuccess) return QGCM_E_HIP;
         ctx->count(QGCM_KERNEL_QUAD);
     }
@@ -676,7 +667,6 @@ qgcm_ctx *qgcm_create(int device, uint32_t max_keys, char *err, int errlen) {
     if (const char *v = getenv("QGCM_LAUNCH_CHUNK"))  // rounded down to whole 64-packet tiles
         ctx->launch_chunk = (uint32_t)std::max(0, atoi(v)) & ~63u;
     ctx->uniform_streams = std::max(1, std::min(4, env_int("QGCM_UNIFORM_STREAMS", 1)));
-    ctx->tile_mode = env_int("QGCM_TILE_MODE", 1) == 2 ? 2 : 1;
     if (const char *v = getenv("QGCM_DESC_CHUNK")) ctx->desc_chunk = (uint32_t)std::max(0, atoi(v));
     if (const char *v = getenv("QGCM_PIPE_CHUNK_MB")) ctx->host_chunk = (uint64_t)std::max(1, atoi(v)) << 20;
     if (const char *v = getenv("QGCM_PIPE_RING_MB")) ctx->host_ring = (uint64_t)std::max(1, atoi(v)) << 20;
@@ -722,8 +712,6 @@ qgcm_ctx *qgcm_create(int device, uint32_t max_keys, char *err, int errlen) {
     }
     for (int k = 0; ok && k < kPipeStreams; ++k)
         ok = hipStreamCreateWithFlags(&ctx->pipe[k], hipStreamNonBlocking) == hipSuccess;
-    if (ok && ctx->tile_mode == 2)
-        ok = hipMalloc(&ctx->d_tq, (size_t)kTileQueueSlots * kTileQueues * 64u) == hipSuccess;
     if (ok && ctx->uniform_streams > 1) {
         ok = hipEventCreateWithFlags(&ctx->fork_ev, hipEventDisableTiming) == hipSuccess;
         for (int i = 0; ok && i < ctx->uniform_streams - 1; ++i)
@@ -750,7 +738,6 @@ void qgcm_destroy(qgcm_ctx *ctx) {
     hipFree(ctx->d_te);
     hipFree(ctx->d_sbox);
     hipFree(ctx->d_key_valid);
-    hipFree(ctx->d_tq);
     hipFree(ctx->d_qws);
     auto free_slot = [](qgcm_ctx::OneSlot &sl) {
         if (sl.h) hipHostFree(sl.h);
