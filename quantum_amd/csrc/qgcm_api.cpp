@@ -47,13 +47,6 @@ struct qgcm_ctx {
                                                 // latency kernel (QGCM_ONE_UNIFORM_MAX, tuning)
     uint32_t launch_chunk = kLaunchChunk;       // uniform batches launch at most this many packets per
                                                 // kernel (QGCM_LAUNCH_CHUNK, tuning; 0 = one launch)
-    // a uniform batch's launches go round-robin over the caller's stream and uniform_streams - 1 helper
-    // streams of the context (QGCM_UNIFORM_STREAMS; the helpers wait for the caller's earlier work and
-    // the caller's stream waits for them at the end, so the call stays ordered on its stream)
-    int uniform_streams = 1;
-    std::mutex fork_mu;                    // the helper streams and their fork/join events
-    hipStream_t fork_s[3] = {};
-    hipEvent_t fork_ev = nullptr, join_ev[3] = {};
     uint32_t desc_chunk = kDescChunk;           // descriptor batches: packets per sorted chunk
                                                 // (QGCM_DESC_CHUNK, tuning; 0 = one launch)
     // A/B switches, read once at qgcm_create like every other knob (a getenv per call would race a
@@ -364,17 +357,7 @@ int run_uniform(qgcm_ctx *ctx, bool seal, uint8_t *arena, uint64_t stride, uint3
     // 2^23-packet launch ran at 768 GiB/s, the same batch as 2^19-packet launches at 827, at 2^20 packets
     // either form 826-829 (tools/exp_chunked.py).
     const uint32_t chunk = ctx->launch_chunk ? ctx->launch_chunk : n;
-    const uint32_t launches = (uint32_t)(((uint64_t)n + chunk - 1) / chunk);
-    const int ns = (int)std::min<uint32_t>((uint32_t)ctx->uniform_streams, launches);
-    std::unique_lock<std::mutex> fork_lk;
-    if (ns > 1) {  // fork: the helpers start after everything queued on s so far
-        fork_lk = std::unique_lock<std::mutex>(ctx->fork_mu);
-        if (hipEventRecord(ctx->fork_ev, s) != hipSuccess) return QGCM_E_HIP;
-        for (int i = 0; i < ns - 1; ++i)
-            if (hipStreamWaitEvent(ctx->fork_s[i], ctx->fork_ev, 0) != hipSuccess) return QGCM_E_HIP;
-    }
-    uint32_t k = 0;
-    for (uint32_t p = 0; p < n; p += chunk, ++k) {
+    for (uint32_t p = 0; p < n; p += chunk) {
         const uint32_t m = std::min(chunk, n - p);
         Batch c = b;
         c.arena = arena + (uint64_t)p * stride;
@@ -382,14 +365,9 @@ int run_uniform(qgcm_ctx *ctx, bool seal, uint8_t *arena, uint64_t stride, uint3
         c.status = status ? status + p : nullptr;
         c.n = m;
         c.n_items = (uint32_t)(((uint64_t)m + 63) & ~63ull);
-        const hipStream_t ls = ns > 1 && k % ns ? ctx->fork_s[k % ns - 1] : s;
-        if (launch_packets(seal, v, c, grid_for(ctx, c.n_items, v), ls) != hipSuccess) return QGCM_E_HIP;
+        if (launch_packets(seal, v, c, grid_for(ctx, c.n_items, v), s) != hipSuccess) return QGCM_E_HIP;
         ctx->count(QGCM_KERNEL_QUAD);
     }
-    for (int i = 0; i < ns - 1; ++i)  // join: s waits for the helpers' launches
-        if (hipEventRecord(ctx->join_ev[i], ctx->fork_s[i]) != hipSuccess ||
-            hipStreamWaitEvent(s, ctx->join_ev[i], 0) != hipSuccess)
-            return QGCM_E_HIP;
     return QGCM_OK;
 }
 
@@ -666,7 +644,6 @@ qgcm_ctx *qgcm_create(int device, uint32_t max_keys, char *err, int errlen) {
     if (const char *v = getenv("QGCM_DIRECT_MAX")) ctx->direct_max = (uint32_t)std::max(0, atoi(v));
     if (const char *v = getenv("QGCM_LAUNCH_CHUNK"))  // rounded down to whole 64-packet tiles
         ctx->launch_chunk = (uint32_t)std::max(0, atoi(v)) & ~63u;
-    ctx->uniform_streams = std::max(1, std::min(4, env_int("QGCM_UNIFORM_STREAMS", 1)));
     if (const char *v = getenv("QGCM_DESC_CHUNK")) ctx->desc_chunk = (uint32_t)std::max(0, atoi(v));
     if (const char *v = getenv("QGCM_PIPE_CHUNK_MB")) ctx->host_chunk = (uint64_t)std::max(1, atoi(v)) << 20;
     if (const char *v = getenv("QGCM_PIPE_RING_MB")) ctx->host_ring = (uint64_t)std::max(1, atoi(v)) << 20;
@@ -712,12 +689,6 @@ qgcm_ctx *qgcm_create(int device, uint32_t max_keys, char *err, int errlen) {
     }
     for (int k = 0; ok && k < kPipeStreams; ++k)
         ok = hipStreamCreateWithFlags(&ctx->pipe[k], hipStreamNonBlocking) == hipSuccess;
-    if (ok && ctx->uniform_streams > 1) {
-        ok = hipEventCreateWithFlags(&ctx->fork_ev, hipEventDisableTiming) == hipSuccess;
-        for (int i = 0; ok && i < ctx->uniform_streams - 1; ++i)
-            ok = hipStreamCreateWithFlags(&ctx->fork_s[i], hipStreamNonBlocking) == hipSuccess &&
-                 hipEventCreateWithFlags(&ctx->join_ev[i], hipEventDisableTiming) == hipSuccess;
-    }
     if (!ok) {
         set_err(err, errlen, "device allocation / kernel setup failed");
         qgcm_destroy(ctx);
@@ -753,11 +724,6 @@ void qgcm_destroy(qgcm_ctx *ctx) {
     for (hipStream_t x : ctx->chain_extra) hipStreamDestroy(x);
     for (hipStream_t p : ctx->pipe)
         if (p) hipStreamDestroy(p);
-    for (int i = 0; i < 3; ++i) {
-        if (ctx->fork_s[i]) hipStreamDestroy(ctx->fork_s[i]);
-        if (ctx->join_ev[i]) hipEventDestroy(ctx->join_ev[i]);
-    }
-    if (ctx->fork_ev) hipEventDestroy(ctx->fork_ev);
     if (ctx->ws_done) hipEventDestroy(ctx->ws_done);
     for (auto *v : {&ctx->ev_in, &ctx->ev_kern, &ctx->ev_out})
         for (hipEvent_t e : *v) hipEventDestroy(e);

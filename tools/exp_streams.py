@@ -12,9 +12,9 @@ interleaved, `rounds` x `steps` steps each, with the telemetry of bench.py:
              split of one call across two streams has to do: the call returns ordered after all its work)
   quarters   four quarters on two streams (q0, q2 on one; q1, q3 on the other), no join
   quarters4  four quarters on four streams, no join
-  lib2       bench.py's step on a context made with QGCM_UNIFORM_STREAMS=2: the library sends every other
-             2^19-packet launch of a call to a helper stream and joins at the end of the call
-  lib2c18    as lib2 with QGCM_LAUNCH_CHUNK=262144 (four launches per call over the two streams)
+
+(profiles/r6_s6 also timed a library-side split of each call across a helper stream, joined at the end
+of the call, QGCM_UNIFORM_STREAMS=2: 828-829 against 833-836 for one stream; it was removed.)
 
 Every layout ends with the arena's digests checked against tests/golden/rank_digest.json (rank 0's
 2^20 prefix = the headline arena) and every status byte 1.
@@ -38,7 +38,7 @@ from quantum_amd.crypto import Context  # noqa: E402
 def main() -> None:
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 3
     steps = int(sys.argv[2]) if len(sys.argv) > 2 else 200
-    modes = os.environ.get("EXP_MODES", "one,halves,halvesj,quarters,quarters4,lib2,lib2c18").split(",")
+    modes = os.environ.get("EXP_MODES", "one,halves,halvesj,quarters,quarters4").split(",")
     N, L = 1 << 20, 1350
     stride = batch.slot_stride(L, align=64)
     key = bench.derive_key(bench.SECRET, bench.SALT)
@@ -50,15 +50,6 @@ def main() -> None:
     status = torch.zeros(N, dtype=torch.uint8, device="cuda")
     batch.fill_uniform(arena, stride, N, L, int.from_bytes(bench.AAD, "little"), 0x5EED0001, nonces, 0x5EED0002)
     main_s = torch.cuda.current_stream()
-    libctx = {}
-    for name, env in (("lib2", {"QGCM_UNIFORM_STREAMS": "2"}),
-                      ("lib2c18", {"QGCM_UNIFORM_STREAMS": "2", "QGCM_LAUNCH_CHUNK": "262144"})):
-        if name in modes:
-            os.environ.update(env)
-            libctx[name] = Context(device=0, max_keys=4)
-            libctx[name].set_key(0, key)
-            for k in env:
-                os.environ.pop(k)
     streams = [torch.cuda.Stream() for _ in range(4)]
 
     def part(k, parts):
@@ -73,10 +64,6 @@ def main() -> None:
     def step(mode):
         if mode == "one":
             pair(main_s, arena[:N * stride], nonces, status, N)
-        elif mode in libctx:
-            c = libctx[mode]
-            batch.seal_uniform(c, arena[:N * stride], stride, N, L, 0, nonces, status=None, stream=main_s)
-            batch.open_uniform(c, arena[:N * stride], stride, N, L + 28, 0, status=status, stream=main_s)
         elif mode in ("halves", "quarters", "quarters4"):
             parts = 2 if mode == "halves" else 4
             ns = 4 if mode == "quarters4" else 2
@@ -124,8 +111,6 @@ def main() -> None:
                                                    if clock["sclk_mhz_mean"] else None),
                               "status_ok": int(status.sum().item()) == N,
                               "digests_ok": bool(d["sealed_digest_ok"] and d["opened_digest_ok"])}), flush=True)
-    for c in libctx.values():
-        c.close()
     ctx.close()
 
 
