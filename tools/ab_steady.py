@@ -5,7 +5,9 @@ clock of every timed stretch (bench.GpuTelemetry), so a build's rate and its cyc
 compared.  tools/ab_libs.py times one synchronized pair per round instead.  Every build's sealed arena
 must equal the first build's.
 
-    python3 tools/ab_steady.py lib1.so lib2.so[:ENV=V,ENV2=V2] [...] [--rounds R] [--steps K]
+    python3 tools/ab_steady.py lib1.so lib2.so[:ENV=V,ENV2=V2] [...] [--rounds R] [--steps K] [--packets N]
+
+(--packets: batch size, default 2^20; the rank-0 layout and fill at any size.)
 
 A ":ENV=V,..." suffix sets those environment variables around that entry's qgcm_create (the library's
 knobs are read there), so one build can be compared with itself under other settings.
@@ -28,10 +30,10 @@ def opt(name, dflt):
 
 
 def main() -> None:
-    rounds, steps = opt("--rounds", 5), opt("--steps", 200)
+    rounds, steps, N = opt("--rounds", 5), opt("--steps", 200), opt("--packets", 1 << 20)
     paths = [a for i, a in enumerate(sys.argv[1:], 1) if not a.startswith("--") and sys.argv[i - 1] not in
-             ("--rounds", "--steps")]
-    N, L, stride = 1 << 20, 1350, 1408
+             ("--rounds", "--steps", "--packets")]
+    L, stride = 1350, 1408
     vp, u32, u64 = C.c_void_p, C.c_uint32, C.c_uint64
     libs = {}
     for entry in paths:
@@ -90,7 +92,7 @@ def main() -> None:
     gib = 2 * N * L / 2**30
     for r in range(rounds):
         for path, (lib, ctx) in libs.items():
-            run(lib, ctx, 50)  # settle at this build's load
+            run(lib, ctx, max(2, 50 * (1 << 20) // N))  # settle at this build's load
             torch.cuda.synchronize()
             tele = bench.GpuTelemetry(0)
             tele.start()
@@ -102,7 +104,7 @@ def main() -> None:
             c = tele.summary()
             tele.close()
             ms = el * 1e3 / steps
-            row = {"lib": path, "round": r, "GiB_s": round(gib / (ms * 1e-3), 2), "ms_per_step": round(ms, 4),
+            row = {"lib": path, "round": r, "packets": N, "GiB_s": round(gib / (ms * 1e-3), 2), "ms_per_step": round(ms, 4),
                    "sclk_mhz_mean": c["sclk_mhz_mean"], "power_w_mean": c["power_w_mean"],
                    "mcycles_per_step": round(ms * c["sclk_mhz_mean"] / 1e3, 3) if c["sclk_mhz_mean"] else None,
                    "status_ok": int(status.sum().item()) == N}

@@ -284,7 +284,7 @@ for s in $STEPS; do
         done
       done ;;
     abst)  # steady-state in-process A/B of the working tree's library against the build(s) in ABLIBS
-      timeout -k 10 600 python3 tools/ab_steady.py quantum_amd/libqgcm.so ${ABLIBS:-sidelib/pool0/libqgcm.so} --rounds ${ABROUNDS:-5} > $OUT/ab_steady.jsonl 2> $OUT/ab_steady.err
+      timeout -k 10 600 python3 tools/ab_steady.py quantum_amd/libqgcm.so ${ABLIBS:-sidelib/pool0/libqgcm.so} --rounds ${ABROUNDS:-5} --steps ${ABSTEPS:-200} --packets ${ABPACKETS:-1048576} > $OUT/ab_steady${ABTAG:-}.jsonl 2> $OUT/ab_steady${ABTAG:-}.err
       check abst $? ;;
     streams)  # the headline step in several stream layouts, interleaved (tools/exp_streams.py)
       timeout -k 10 500 python3 tools/exp_streams.py ${EXP_ROUNDS:-3} 200 > $OUT/streams.jsonl 2> $OUT/streams.err
