@@ -37,3 +37,31 @@ def test_one_device_needs_gloo():
     out = run(["--gpus", "2", "--one-device", "--steps", "1", "--warmup", "0"])
     assert out.returncode != 0
     assert "gloo" in out.stderr
+
+
+def test_telemetry_degrades_to_a_note():
+    """bench.GpuTelemetry without a readable GPU (this CPU box): the clock and power fields are None and
+    the reason is in the line; starting, stopping and closing it never raise."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    t = bench.GpuTelemetry(0)
+    t.start()
+    t.stop()
+    s = t.summary()
+    t.close()
+    assert s["sclk_mhz_mean"] is None and s["power_w_mean"] is None and s["power_cap_w"] is None
+    assert isinstance(s["telemetry"], str) and s["telemetry"]
+
+
+def test_rank_digests_skip_other_layouts():
+    """bench.rank_digests checks only the layout tests/golden/rank_digest.json was made for (L 1350,
+    stride 1408, ranks 0-7, at least 2^16 slots); anything else says why it was skipped (no GPU needed)."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    assert bench.rank_digests(None, None, None, None, 1408, 1 << 20, 1350, 0, None, verify=False)["digest_skipped"]
+    for stride, n, L, rank in ((1472, 1 << 20, 1350, 0), (1408, 1 << 15, 1350, 0), (1408, 1 << 20, 1349, 0),
+                               (1408, 1 << 20, 1350, 8)):
+        d = bench.rank_digests(None, None, None, None, stride, n, L, rank, None)
+        assert d["sealed_digest_ok"] is None and d["digest_skipped"] == "not the golden's layout"
