@@ -42,7 +42,7 @@ from quantum_amd.crypto import Context, derive_key  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, MI355X_MICROARCH.md "Chip-level parameters"
 COPY_GUIDE_GBS = 6290.0  # the same table's measured float4 copy (read + write)
 # PMC passes of this command (tools/pmc_traffic.py), newest first
-LAUNCH_CHUNK = 1 << 19  # quantum_amd/csrc/gcm_internal.h kLaunchChunk
+LAUNCH_CHUNK = 1 << 20  # quantum_amd/csrc/gcm_internal.h kLaunchChunk
 TRAFFIC_JSONS = [os.path.join(ROOT, "profiles", d, "traffic.json") for d in ("r6_s10", "r6_s3", "r5_s37", "r5_s7", "r4_s21", "r4_s3", "r3_s39", "r3_s15", "r3_s1")]
 CONFIG4_PACKETS = 64 << 20  # BASELINE config 4: 64 M packets over the node's GPUs
 SECRET = b"AES256Key-32Characters1234567890"
@@ -770,7 +770,7 @@ def extra_config4_one_gpu(key: bytes, steps: int = 3, warmup: int = 1, settle_ms
     """BASELINE config 4's whole batch on ONE GPU: 64 x 2^20 x 1350 B (94.5 GB of 1408-B slots, one
     MI355X holds it), seal then unseal, so the N-GPU lines (config 4 sharded over N ranks) have a
     same-workload N = 1 anchor: per-GPU efficiency at N = value_N / (N x this value).  One step is the
-    same pair of uniform calls the headline makes (2^19-packet launches), timed between synchronizes."""
+    same pair of uniform calls the headline makes (2^20-packet launches), timed between synchronizes."""
     N, L = CONFIG4_PACKETS, 1350
     stride = batch.slot_stride(L, align=64)
     ctx = Context(device=0, max_keys=4)

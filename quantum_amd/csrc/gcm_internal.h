@@ -167,7 +167,7 @@ constexpr uint32_t kDescOneMax = 8192;
 // r4_s62)
 constexpr uint32_t kDirectMax = 65536;
 constexpr uint64_t kDirectMaxBytes = 128ull << 20;
-constexpr uint32_t kLaunchChunk = 1u << 19;  // packets per quad-kernel launch of a uniform batch
+constexpr uint32_t kLaunchChunk = 1u << 20;  // packets per quad-kernel launch of a uniform batch
 constexpr uint32_t kDescChunk = 0;           // packets per sorted chunk of a descriptor batch (0 = all)
 bool ctx_one_kernel(const qgcm_ctx *ctx);
 // the context's host-pipeline streams (0 copy-in, 1 kernels, 2 copy-out) and the mutex that guards them

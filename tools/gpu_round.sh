@@ -48,7 +48,7 @@ for s in $STEPS; do
       check prof $?
       mkdir -p profiles/$TAG
       python3 tools/trace_summary.py gpurun_out/prof_$TAG > $OUT/kernel_stats_summary.txt 2>&1
-      python3 tools/pmc_traffic.py gpurun_out/prof_$TAG 1048576 1350 1408 524288 > $OUT/traffic_print.txt 2>&1
+      python3 tools/pmc_traffic.py gpurun_out/prof_$TAG 1048576 1350 1408 1048576 > $OUT/traffic_print.txt 2>&1
       cp gpurun_out/prof_$TAG/traffic.json $OUT/ 2>/dev/null ;;
     pp)
       for t in 1 16 64 256; do
