@@ -869,9 +869,9 @@ gcm_quad_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
             } else {
                 tile += gridDim.x * kW;
             }
-            const bool mine = h == 2 || (qd >> 3) == h;  // the other half of a split tile: another wave's
-            if (!valid || !mine) {
-                if (!kSeal && mine && b.status && pkt < b.n && m == 0) b.status[pkt] = 0;
+            if (h != 2 && (qd >> 3) != h) continue;  // the other half of a split tile: another wave's
+            if (!valid) {
+                if (!kSeal && b.status && pkt < b.n && m == 0) b.status[pkt] = 0;
                 continue;  // the whole quad leaves together
             }
         }
