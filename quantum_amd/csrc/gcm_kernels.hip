@@ -734,11 +734,8 @@ __device__ __forceinline__ void quad_packet(const Batch &b, const Eng &eng, uint
 // g*16 + w + k*gridDim*16 (k = 0, 1, ...).  1: the same set of tiles per workgroup, shared by its 16
 // waves through an LDS counter (index i -> tile g*16 + i%16 + (i/16)*gridDim*16, i ascending), so a wave
 // that runs ahead takes more of its workgroup's tiles instead of idling while slower waves finish.
-// 2: as 1, and the workgroup's last 16 tiles are handed out as 32 half tiles (8 packets each, the other
-// half's lanes idle), so the waves that finish first take the work of the drain instead of idling
-// while the last whole tiles finish (the drain is where one stream loses to two).
 #ifndef QGCM_TILE_POOL
-#define QGCM_TILE_POOL 2
+#define QGCM_TILE_POOL 1
 #endif
 constexpr uint32_t kPoolCtr = kG5Bytes + kTeBytes;  // LDS word after the uniform kernel's tables
 
@@ -781,25 +778,6 @@ gcm_quad_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
     const uint32_t ntiles = kDesc ? (b.tile_list ? *b.n_list : b.n_items >> 4) : ((b.n + 15) >> 4);
 
     uint32_t tile = blockIdx.x * kW + wave;
-    // pool index -> tile (and half: 2 = the whole tile, 0 / 1 = its packets 0-7 / 8-15); C = this
-    // workgroup's tiles, indices from `cut` on are half tiles (QGCM_TILE_POOL 2)
-    uint32_t half = 2, C = 0, cut = ~0u;
-    if constexpr (!kDesc && QGCM_TILE_POOL >= 2) {
-        const uint32_t per_round = gridDim.x * kW, rem = ntiles % per_round, first = blockIdx.x * kW;
-        C = ntiles / per_round * kW + (rem > first ? min(rem - first, kW) : 0u);
-        cut = C > kW ? C - kW : 0u;
-    }
-    auto pool_tile = [&](uint32_t i) {
-        uint32_t ti = i;
-        half = 2;
-        if (i >= cut) {
-            ti = cut + ((i - cut) >> 1);
-            half = (i - cut) & 1u;
-            if (ti >= C) return ntiles;
-        }
-        return blockIdx.x * kW + (ti % kW) + (ti / kW) * gridDim.x * kW;
-    };
-    if constexpr (!kDesc && QGCM_TILE_POOL >= 2) tile = pool_tile(wave);
     if constexpr (kDesc) {  // dynamic tiles: lengths vary by 100x between tiles
         uint32_t t = 0;
         if (lane == 0) t = atomicAdd(b.tile_counter, 1u);
@@ -845,7 +823,6 @@ gcm_quad_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
             }
             tile = next;
         } else {
-            const uint32_t h = half;  // this tile's half (the next tile's is set below)
             pkt = tile * 16u + qd;
             L = b.uniform_len;
             // Opaque per tile: stops LICM from hoisting dozens of L-derived values (masks, selectors)
@@ -862,14 +839,10 @@ gcm_quad_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
                 uint32_t i = 0;
                 if (lane == 0) i = __atomic_fetch_add((lds_u32 *)(size_t)kPoolCtr, 1u, __ATOMIC_RELAXED);
                 i = __builtin_amdgcn_readfirstlane(i);
-                if constexpr (QGCM_TILE_POOL >= 2)
-                    tile = pool_tile(i);
-                else
-                    tile = blockIdx.x * kW + (i % kW) + (i / kW) * gridDim.x * kW;
+                tile = blockIdx.x * kW + (i % kW) + (i / kW) * gridDim.x * kW;
             } else {
                 tile += gridDim.x * kW;
             }
-            if (h != 2 && (qd >> 3) != h) continue;  // the other half of a split tile: another wave's
             if (!valid) {
                 if (!kSeal && b.status && pkt < b.n && m == 0) b.status[pkt] = 0;
                 continue;  // the whole quad leaves together
