@@ -734,10 +734,27 @@ __device__ __forceinline__ void quad_packet(const Batch &b, const Eng &eng, uint
 // g*16 + w + k*gridDim*16 (k = 0, 1, ...).  1: the same set of tiles per workgroup, shared by its 16
 // waves through an LDS counter (index i -> tile g*16 + i%16 + (i/16)*gridDim*16, i ascending), so a wave
 // that runs ahead takes more of its workgroup's tiles instead of idling while slower waves finish.
+// 4 (default): mode 1 over the launch's first rows of tiles, then the last QGCM_TAIL_EIGHTHS eighths of
+// its rows through one global counter that every wave of the grid draws from once its workgroup's rows
+// are done (b.pool; NULL: mode 1 for all tiles).  The eight XCDs run at different speeds, so with each
+// workgroup's share fixed the fastest XCD's CUs idled ~4% of a launch while the slowest finished
+// (tools/quad_stats.py, profiles/r6_s18); with the shared tail every XCD ends within ~2%.  Tail of 4
+// eighths: +2.1% at 3.7% fewer cycles per step against mode 1 (3: +1.6%, 5 and 6: +2.0%;
+// tools/ab_steady.py, profiles/r6_s20).
 #ifndef QGCM_TILE_POOL
-#define QGCM_TILE_POOL 1
+#define QGCM_TILE_POOL 4
+#endif
+#ifndef QGCM_TAIL_EIGHTHS
+#define QGCM_TAIL_EIGHTHS 4
 #endif
 constexpr uint32_t kPoolCtr = kG5Bytes + kTeBytes;  // LDS word after the uniform kernel's tables
+
+// QGCM_QUAD_STATS (side builds only, tools/quad_stats.py): per-workgroup timeline of the uniform kernel
+// in a device array (100 MHz clock): [0] start after the table fill, [1] the last wave's end, [2] the
+// sum of the waves' ends, [3] tiles, [4] XCC id, [5] HW_ID, [6] 2^62 - the first wave's end.
+#ifdef QGCM_QUAD_STATS
+__device__ unsigned long long g_quad_stats[4096 * 8];
+#endif
 
 template <bool kDesc>
 constexpr int quad_waves() { return kDesc ? 12 : 16; }
@@ -767,6 +784,11 @@ gcm_quad_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
     if constexpr (!kDesc && QGCM_TILE_POOL) {
         if (threadIdx.x == 0) lds_st32(kPoolCtr, kW);  // pool indices 0..kW-1: each wave's first tile
     }
+#if QGCM_TILE_POOL == 4
+    if constexpr (!kDesc) {
+        if (threadIdx.x == 0) lds_st32(kPoolCtr + 12, 0u);  // waves of this workgroup done
+    }
+#endif
     __syncthreads();
 
     const uint32_t lb = (lane & 31u) << 2;
@@ -777,6 +799,47 @@ gcm_quad_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
     uint32_t cur_key = kDesc ? 0xffffffffu : b.uniform_key;
     const uint32_t ntiles = kDesc ? (b.tile_list ? *b.n_list : b.n_items >> 4) : ((b.n + 15) >> 4);
 
+#ifdef QGCM_QUAD_STATS
+    unsigned long long *qs = g_quad_stats + (size_t)blockIdx.x * 8u;
+    uint32_t qs_tiles = 0;
+    if (!kDesc && threadIdx.x == 0) {
+        qs[0] = wall_clock64();
+        qs[4] = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
+        qs[5] = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID
+    }
+#endif
+#ifdef QGCM_QUAD_STATS
+#define QS_TILE() ++qs_tiles
+#define QS_END()                                                  \
+    do {                                                          \
+        if (!kDesc && lane == 0) {                                \
+            const unsigned long long t_ = wall_clock64();         \
+            atomicMax(&qs[1], t_);                                \
+            atomicAdd(&qs[2], t_);                                \
+            atomicAdd(&qs[3], (unsigned long long)qs_tiles);      \
+            atomicMax(&qs[6], (1ull << 62) - t_);                 \
+        }                                                         \
+    } while (0)
+#else
+#define QS_TILE() do { } while (0)
+#define QS_END() do { } while (0)
+#endif
+#if QGCM_TILE_POOL == 4
+    // The launch's last rows of tiles through one global counter (b.pool, one zeroed set per launch):
+    // each workgroup first takes its own tiles of rows [0, srow) from its LDS counter as in mode 1, then
+    // every wave draws from the shared tail [srow * grid * 16, ntiles), so the XCDs, which run at
+    // different speeds (tools/quad_stats.py), end together instead of idling while the slowest finishes.
+    // QGCM_TAIL_EIGHTHS: eighths of the full rows left to the tail (at least one when there are two).
+    uint32_t sidx = 0xffffffffu, tail0 = 0;
+    if constexpr (!kDesc) {
+        const uint32_t rows = ntiles / (gridDim.x * kW);
+        if (b.pool && rows > 0) {  // (no full row: each wave's first tile is all there is)
+            const uint32_t tail_rows = rows < 2 ? 0u : std::min(rows - 1u, std::max(1u, rows * QGCM_TAIL_EIGHTHS / 8u));
+            sidx = (rows - tail_rows) * kW;
+            tail0 = (rows - tail_rows) * gridDim.x * kW;
+        }
+    }
+#endif
     uint32_t tile = blockIdx.x * kW + wave;
     if constexpr (kDesc) {  // dynamic tiles: lengths vary by 100x between tiles
         uint32_t t = 0;
@@ -840,6 +903,13 @@ gcm_quad_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
                 if (lane == 0) i = __atomic_fetch_add((lds_u32 *)(size_t)kPoolCtr, 1u, __ATOMIC_RELAXED);
                 i = __builtin_amdgcn_readfirstlane(i);
                 tile = blockIdx.x * kW + (i % kW) + (i / kW) * gridDim.x * kW;
+#if QGCM_TILE_POOL == 4
+                if (i >= sidx) {  // this workgroup's rows are done: the launch's tail, shared
+                    uint32_t c = 0;
+                    if (lane == 0) c = atomicAdd(b.pool, 1u);
+                    tile = tail0 + __builtin_amdgcn_readfirstlane(c);
+                }
+#endif
             } else {
                 tile += gridDim.x * kW;
             }
@@ -854,8 +924,41 @@ gcm_quad_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
         } else {
             quad_packet<kSeal>(b, Tab2F{kk, {lb, m8}, mf8}, pkt, off, L, wkey, m, gH4);
         }
+        QS_TILE();
     }
+    QS_END();
+#if QGCM_TILE_POOL == 4
+    // the last wave of the grid zeroes the pool set for the launch that next holds it
+    if constexpr (!kDesc) {
+        if (b.pool) {
+            uint32_t last = 0;
+            if (lane == 0 && __atomic_fetch_add((lds_u32 *)(size_t)(kPoolCtr + 12), 1u, __ATOMIC_RELAXED) == kW - 1) {
+                __threadfence();
+                last = atomicAdd(b.pool + kPoolDoneWord, 1u) == gridDim.x - 1u ? 1u : 0u;
+            }
+            if (lane == 0 && last) {
+                __threadfence();
+                b.pool[0] = 0;
+                b.pool[kPoolDoneWord] = 0;
+            }
+        }
+    }
+#endif
 }
+#undef QS_TILE
+#undef QS_END
+
+#ifdef QGCM_QUAD_STATS
+extern "C" int qgcm_debug_quad_stats(unsigned long long *out, int n, int reset) {
+    if (n > 4096 * 8) n = 4096 * 8;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_quad_stats), (size_t)n * 8) != hipSuccess) return -1;
+    if (reset) {
+        static unsigned long long zero[4096 * 8];
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_quad_stats), zero, sizeof(zero)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
 
 // ---------------------------------------------------------------------------------------------
 // Descriptor batches through the Tab2F engine (BASELINE config 3: any key mix, any lengths):
@@ -2030,6 +2133,7 @@ hipError_t init_kernels() {
     return hipSuccess;
 }
 
+bool quad_pool_global() { return QGCM_TILE_POOL == 4; }
 bool variant_valid(int v) { return variant_slot(v) >= 0 && g_variants[variant_slot(v)].seal != nullptr; }
 int variant_waves(int v) { return g_variants[variant_slot(v)].waves; }
 int variant_wgs_per_cu(int v) { return g_variants[variant_slot(v)].wgs_per_cu; }

@@ -123,6 +123,15 @@ struct qgcm_ctx {
     hipEvent_t ws_done = nullptr;
     bool ws_pending = false;
 
+    // the uniform kernel's shared tail counters (gcm_kernels.hip QGCM_TILE_POOL): a ring of kPoolSets
+    // zeroed sets, one per launch; a set is reused only after the launch that last held it (its event
+    // on the stream that launched it), guarded by pool_mu
+    uint32_t *d_pool = nullptr;
+    hipEvent_t pool_ev[kPoolSets] = {};
+    bool pool_used[kPoolSets] = {};
+    uint32_t pool_next = 0;
+    std::mutex pool_mu;
+
     std::atomic<uint64_t> launches[QGCM_KERNEL_COUNTERS] = {};  // qgcm_launch_counts
     void count(int k, uint64_t v = 1) { launches[k].fetch_add(v, std::memory_order_relaxed); }
 
@@ -365,7 +374,18 @@ int run_uniform(qgcm_ctx *ctx, bool seal, uint8_t *arena, uint64_t stride, uint3
         c.status = status ? status + p : nullptr;
         c.n = m;
         c.n_items = (uint32_t)(((uint64_t)m + 63) & ~63ull);
-        if (launch_packets(seal, v, c, grid_for(ctx, c.n_items, v), s) != hipSuccess) return QGCM_E_HIP;
+        const int grid = grid_for(ctx, c.n_items, v);
+        if (ctx->d_pool) {
+            std::lock_guard<std::mutex> g(ctx->pool_mu);
+            const uint32_t k = ctx->pool_next++ % kPoolSets;
+            if (ctx->pool_used[k] && hipStreamWaitEvent(s, ctx->pool_ev[k], 0) != hipSuccess) return QGCM_E_HIP;
+            c.pool = ctx->d_pool + (size_t)k * kPoolSetWords;
+            if (launch_packets(seal, v, c, grid, s) != hipSuccess) return QGCM_E_HIP;
+            if (hipEventRecord(ctx->pool_ev[k], s) != hipSuccess) return QGCM_E_HIP;
+            ctx->pool_used[k] = true;
+        } else if (launch_packets(seal, v, c, grid, s) != hipSuccess) {
+            return QGCM_E_HIP;
+        }
         ctx->count(QGCM_KERNEL_QUAD);
     }
     return QGCM_OK;
@@ -689,6 +709,12 @@ qgcm_ctx *qgcm_create(int device, uint32_t max_keys, char *err, int errlen) {
     }
     for (int k = 0; ok && k < kPipeStreams; ++k)
         ok = hipStreamCreateWithFlags(&ctx->pipe[k], hipStreamNonBlocking) == hipSuccess;
+    if (ok && quad_pool_global()) {
+        const size_t bytes = (size_t)kPoolSets * kPoolSetWords * 4;
+        ok = hipMalloc(&ctx->d_pool, bytes) == hipSuccess && hipMemset(ctx->d_pool, 0, bytes) == hipSuccess;
+        for (uint32_t k = 0; ok && k < kPoolSets; ++k)
+            ok = hipEventCreateWithFlags(&ctx->pool_ev[k], hipEventDisableTiming) == hipSuccess;
+    }
     if (!ok) {
         set_err(err, errlen, "device allocation / kernel setup failed");
         qgcm_destroy(ctx);
@@ -725,6 +751,9 @@ void qgcm_destroy(qgcm_ctx *ctx) {
     for (hipStream_t p : ctx->pipe)
         if (p) hipStreamDestroy(p);
     if (ctx->ws_done) hipEventDestroy(ctx->ws_done);
+    hipFree(ctx->d_pool);
+    for (hipEvent_t e : ctx->pool_ev)
+        if (e) hipEventDestroy(e);
     for (auto *v : {&ctx->ev_in, &ctx->ev_kern, &ctx->ev_out})
         for (hipEvent_t e : *v) hipEventDestroy(e);
     delete ctx;

@@ -268,7 +268,7 @@ for s in $STEPS; do
         check copyab_$gb $?
       done ;;
     r6tests)  # the suites round 6 changed
-      timeout -k 10 900 python3 -u -m pytest tests/test_gpu_parity.py tests/test_cpp_mirror.py tests/test_bench_dist.py tests/test_gpu_snappy.py tests/test_gpu_config5.py -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/r6_tests.txt 2>&1
+      timeout -k 10 900 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_tail_pool.py tests/test_cpp_mirror.py tests/test_bench_dist.py tests/test_gpu_snappy.py tests/test_gpu_config5.py -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/r6_tests.txt 2>&1
       check r6tests $? ;;
     pp6)  # per-packet host CPU per pair: resident callers spinning (default) vs all asleep (SPINNERS=0), 16 / 64 threads
       for rep in 1 2; do

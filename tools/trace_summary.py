@@ -3,9 +3,9 @@
 Prints, per kernel, calls / mean / min duration (from <prof>/trace/*kernel_stats.csv) and, for the
 packet kernels, the mean over the last `timed` launches in <prof>/trace/*kernel_trace.csv (bench.py
 runs `warmup` untimed steps first) -- the figure bench.py's HIP-event kernel_ms must agree with.
-libqgcm launches a uniform batch as `lpc` back-to-back launches of 2^19 packets (2 for 2^20 packets):
-the per-call figures group consecutive launches of one kind.
-Usage: python tools/trace_summary.py <prof_dir> [timed=100] [lpc=2] > <prof_dir>/kernel_stats_summary.txt
+libqgcm launches a uniform batch as back-to-back launches of up to 2^20 packets (kLaunchChunk; 2^19
+until round 6), `lpc` per call: the per-call figures group consecutive launches of one kind.
+Usage: python tools/trace_summary.py <prof_dir> [timed=100] [lpc=1] > <prof_dir>/kernel_stats_summary.txt
 """
 import csv
 import glob
@@ -17,7 +17,7 @@ import sys
 def main() -> None:
     prof = sys.argv[1]
     timed = int(sys.argv[2]) if len(sys.argv) > 2 else 100
-    lpc = int(sys.argv[3]) if len(sys.argv) > 3 else 2
+    lpc = int(sys.argv[3]) if len(sys.argv) > 3 else 1
     stats = glob.glob(os.path.join(prof, "trace", "*kernel_stats.csv"))[0]
     trace = glob.glob(os.path.join(prof, "trace", "*kernel_trace.csv"))[0]
     print(f"rocprofv3 --kernel-trace --stats -- python3 bench.py (tools/profile.sh), {prof}")
