@@ -1093,15 +1093,16 @@ def main() -> None:
     batch.fill_uniform(arena, stride, N, L, aad_word, 0x5EED0001 + rank, nonces, 0x5EED0002 + rank)
     stream = torch.cuda.current_stream()
 
+    # ev: (after the seal, after the open); the timed loop records one event before its first step, and
+    # each step's last event is the next step's first, so the K steps carry 2K + 1 records (each record is
+    # a packet in the stream between two launches: ~5 us, profiles/r6_s22)
     def step(ev=None):
-        if ev is not None:
-            ev[0].record(stream)
         batch.seal_uniform(ctx, arena, stride, N, L, 0, nonces, status=None, stream=stream)
         if ev is not None:
-            ev[1].record(stream)
+            ev[0].record(stream)
         batch.open_uniform(ctx, arena, stride, N, L + 28, 0, status=status, stream=stream)
         if ev is not None:
-            ev[2].record(stream)
+            ev[1].record(stream)
 
     # clock settle: the same step back to back for settle_ms of wall time, so the timed steps run at
     # the clocks the chip holds under this load (not timed, not counted as warmup)
@@ -1124,15 +1125,16 @@ def main() -> None:
         tele.start()
     for _ in range(args.warmup):
         step()
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(2 * args.steps + 1)]
 
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    evs[0].record(stream)
     for k in range(args.steps):
-        step(evs[k])
+        step((evs[2 * k + 1], evs[2 * k + 2]))
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -1142,8 +1144,8 @@ def main() -> None:
     tele.close()
     ok = int(status.sum().item()) == N  # the last timed open authenticated every packet
     # max over ranks, AND of the per-rank status (the only cross-rank traffic; no data collective)
-    seal_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
-    open_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
+    seal_ms = sum(evs[2 * k].elapsed_time(evs[2 * k + 1]) for k in range(args.steps)) / args.steps
+    open_ms = sum(evs[2 * k + 1].elapsed_time(evs[2 * k + 2]) for k in range(args.steps)) / args.steps
     own_elapsed = elapsed
     coll_dev = dev if args.dist_backend == "nccl" else None
     elapsed, ok = shard.reduce_step_time(elapsed, ok, dist, coll_dev)

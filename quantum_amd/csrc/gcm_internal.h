@@ -58,12 +58,15 @@ struct Batch {
     uint32_t pw_keys;           // H^1..H^kPwPowers (NULL / 0: the Horner + Estrin GHASH for every packet)
     uint32_t *pool;             // uniform kernel (QGCM_TILE_POOL=4, the default): this launch's pool set
                                 // (zeroed; NULL: every tile through the workgroups' LDS counters)
+    uint32_t *pool_done;        // pinned word: the grid's last wave stores pool_gen there once the set is
+    uint32_t pool_gen;          // zeroed again
 };
 // Pool set of the uniform kernel's shared tail (words): [0] the tail's tile counter, [kPoolDoneWord] the
-// grid's finished-workgroup count.  Zero between launches (the grid's last wave zeroes it).
+// grid's finished-workgroup count.  Zero between launches (the grid's last wave zeroes it, then posts
+// the launch's generation to Batch::pool_done).
 constexpr uint32_t kPoolDoneWord = 32;
 constexpr uint32_t kPoolSetWords = 64;
-constexpr uint32_t kPoolSets = 16;  // sets in the ring (a set is reused after the launch that last held it)
+constexpr uint32_t kPoolSets = 16;  // sets per context, each held by one stream at a time
 bool quad_pool_global();            // the uniform kernel takes b.pool (QGCM_TILE_POOL=4)
 constexpr uint32_t kPwPowers = 128;    // flat GHASH up to d + 2 = 128 exponents (payloads up to 2016 B)
 constexpr uint32_t kPwBits = 6;                                  // comb window of the flat GHASH tables

@@ -940,6 +940,9 @@ gcm_quad_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
                 __threadfence();
                 b.pool[0] = 0;
                 b.pool[kPoolDoneWord] = 0;
+                // the set is free for another stream: post this launch's generation to the host word
+                __threadfence_system();
+                __hip_atomic_store(b.pool_done, b.pool_gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
             }
         }
     }

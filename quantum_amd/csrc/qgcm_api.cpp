@@ -123,13 +123,21 @@ struct qgcm_ctx {
     hipEvent_t ws_done = nullptr;
     bool ws_pending = false;
 
-    // the uniform kernel's shared tail counters (gcm_kernels.hip QGCM_TILE_POOL): a ring of kPoolSets
-    // zeroed sets, one per launch; a set is reused only after the launch that last held it (its event
-    // on the stream that launched it), guarded by pool_mu
+    // the uniform kernel's shared tail (gcm_kernels.hip QGCM_TILE_POOL): kPoolSets zeroed counter sets in
+    // device memory, each held by the stream that last launched with it (its handle: HIP keeps a
+    // destroyed stream's object, so its handle, until its queued work has run), so a stream's launches
+    // reuse its set in stream order with nothing in between (an event record between two launches costs
+    // ~3 us, profiles/r6_s23).  The grid's last wave writes the launch's generation to
+    // h_pool_done[k] (pinned) after zeroing the set; another stream takes a set only once that word holds
+    // the set's last generation (read here, or waited for on the new stream: hipStreamWaitValue32).
+    // Guarded by pool_mu.
     uint32_t *d_pool = nullptr;
-    hipEvent_t pool_ev[kPoolSets] = {};
-    bool pool_used[kPoolSets] = {};
-    uint32_t pool_next = 0;
+    uint32_t *h_pool_done = nullptr;
+    hipStream_t pool_owner[kPoolSets] = {};
+    uint32_t pool_gen[kPoolSets] = {};  // 0: never launched with
+    uint64_t pool_tick[kPoolSets] = {};
+    uint64_t pool_clock = 0;
+    uint32_t pool_next_gen = 0;
     std::mutex pool_mu;
 
     std::atomic<uint64_t> launches[QGCM_KERNEL_COUNTERS] = {};  // qgcm_launch_counts
@@ -375,14 +383,37 @@ int run_uniform(qgcm_ctx *ctx, bool seal, uint8_t *arena, uint64_t stride, uint3
         c.n = m;
         c.n_items = (uint32_t)(((uint64_t)m + 63) & ~63ull);
         const int grid = grid_for(ctx, c.n_items, v);
-        if (ctx->d_pool) {
+        // the shared tail needs two full rows of tiles (gcm_kernels.hip); smaller launches go without it
+        const uint64_t rows = ((uint64_t)c.n_items / 16) / ((uint64_t)grid * (uint64_t)variant_waves(v));
+        // (hipStreamPerThread names a different stream in every thread: such launches go without it)
+        const hipStream_t sid = s;
+        if (ctx->d_pool && rows >= 2 && s != hipStreamPerThread) {
             std::lock_guard<std::mutex> g(ctx->pool_mu);
-            const uint32_t k = ctx->pool_next++ % kPoolSets;
-            if (ctx->pool_used[k] && hipStreamWaitEvent(s, ctx->pool_ev[k], 0) != hipSuccess) return QGCM_E_HIP;
+            int k = -1;
+            for (int j = 0; j < (int)kPoolSets && k < 0; ++j)
+                if (ctx->pool_gen[j] && ctx->pool_owner[j] == sid) k = j;  // this stream's own set
+            if (k < 0) {  // a set never used, else the least recently used one
+                for (int j = 0; j < (int)kPoolSets && k < 0; ++j)
+                    if (!ctx->pool_gen[j]) k = j;
+                if (k < 0) {
+                    k = 0;
+                    for (int j = 1; j < (int)kPoolSets; ++j)
+                        if (ctx->pool_tick[j] < ctx->pool_tick[k]) k = j;
+                    // the set's last launch (on another stream) has zeroed it once its generation is posted
+                    if (__atomic_load_n(ctx->h_pool_done + k, __ATOMIC_ACQUIRE) != ctx->pool_gen[k] &&
+                        hipStreamWaitValue32(s, ctx->h_pool_done + k, ctx->pool_gen[k], hipStreamWaitValueEq,
+                                             0xffffffffu) != hipSuccess)
+                        return QGCM_E_HIP;
+                }
+                ctx->pool_owner[k] = sid;
+            }
+            if (++ctx->pool_next_gen == 0) ctx->pool_next_gen = 1;  // generation 0 means "never used"
+            ctx->pool_gen[k] = ctx->pool_next_gen;
+            ctx->pool_tick[k] = ++ctx->pool_clock;
             c.pool = ctx->d_pool + (size_t)k * kPoolSetWords;
+            c.pool_done = ctx->h_pool_done + k;
+            c.pool_gen = ctx->pool_gen[k];
             if (launch_packets(seal, v, c, grid, s) != hipSuccess) return QGCM_E_HIP;
-            if (hipEventRecord(ctx->pool_ev[k], s) != hipSuccess) return QGCM_E_HIP;
-            ctx->pool_used[k] = true;
         } else if (launch_packets(seal, v, c, grid, s) != hipSuccess) {
             return QGCM_E_HIP;
         }
@@ -711,9 +742,10 @@ qgcm_ctx *qgcm_create(int device, uint32_t max_keys, char *err, int errlen) {
         ok = hipStreamCreateWithFlags(&ctx->pipe[k], hipStreamNonBlocking) == hipSuccess;
     if (ok && quad_pool_global()) {
         const size_t bytes = (size_t)kPoolSets * kPoolSetWords * 4;
-        ok = hipMalloc(&ctx->d_pool, bytes) == hipSuccess && hipMemset(ctx->d_pool, 0, bytes) == hipSuccess;
-        for (uint32_t k = 0; ok && k < kPoolSets; ++k)
-            ok = hipEventCreateWithFlags(&ctx->pool_ev[k], hipEventDisableTiming) == hipSuccess;
+        ok = hipMalloc(&ctx->d_pool, bytes) == hipSuccess && hipMemset(ctx->d_pool, 0, bytes) == hipSuccess &&
+             hipHostMalloc(&ctx->h_pool_done, kPoolSets * 4, hipHostMallocCoherent | hipHostMallocMapped) ==
+                 hipSuccess;
+        if (ok) memset(ctx->h_pool_done, 0, kPoolSets * 4);
     }
     if (!ok) {
         set_err(err, errlen, "device allocation / kernel setup failed");
@@ -752,8 +784,7 @@ void qgcm_destroy(qgcm_ctx *ctx) {
         if (p) hipStreamDestroy(p);
     if (ctx->ws_done) hipEventDestroy(ctx->ws_done);
     hipFree(ctx->d_pool);
-    for (hipEvent_t e : ctx->pool_ev)
-        if (e) hipEventDestroy(e);
+    if (ctx->h_pool_done) hipHostFree(ctx->h_pool_done);
     for (auto *v : {&ctx->ev_in, &ctx->ev_kern, &ctx->ev_out})
         for (hipEvent_t e : *v) hipEventDestroy(e);
     delete ctx;

@@ -44,6 +44,21 @@ def test_nm_exports():
     assert set(declared_functions()) <= syms
 
 
+def test_loads_after_torch_hip_runtime():
+    """torch brings its own libamdhip64 (ROCm 7.0): once `import torch` has loaded it, the library binds
+    to that one, so it may only need HIP symbol versions that runtime defines (hipStreamGetId, hip_7.1,
+    did not load on the GPU box, profiles/r6_s24).  A fresh process: torch first, then the library."""
+    import subprocess
+    import sys
+
+    from quantum_amd import _lib
+
+    code = ("import ctypes, torch; L = ctypes.CDLL(%r); L.qgcm_version.restype = ctypes.c_char_p; "
+            "print(L.qgcm_version().decode())" % _lib.LIB_PATH)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and r.stdout.startswith("qgcm"), r.stderr[-2000:]
+
+
 def test_gfx950_code_object_present():
     from quantum_amd import _lib
 

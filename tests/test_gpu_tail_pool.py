@@ -127,3 +127,33 @@ def test_shared_tail_many_launches_on_four_streams(torch, aesgo):
             assert np.array_equal(arena.cpu().numpy(), _oracle(key, plain, n, nonces.cpu().numpy()))
     finally:
         c.close()
+
+
+def test_shared_tail_sets_taken_over_by_more_streams_than_sets(torch, aesgo):
+    """20 streams, more than the context's 16 sets: the later streams take over sets other streams last
+    launched with (each waits, on its own stream, for the generation that set's last launch posts).  Every
+    stream seals its own copy of one arena twice without synchronizing; all must equal the oracle."""
+    from quantum_amd import batch
+
+    key = bytes.fromhex(aesgo["key"])
+    n = 2 * _row_packets(torch) + 333
+    c = _ctx()
+    try:
+        c.set_key(1, key)
+        arena0, nonces = _fill(torch, n, 0x5E750000)
+        plain = arena0.cpu().numpy()
+        want = _oracle(key, plain, n, nonces.cpu().numpy())
+        streams = [torch.cuda.Stream() for _ in range(20)]
+        arenas = [arena0.clone() for _ in streams]
+        torch.cuda.synchronize()
+        for rep in range(2):
+            for a, s in zip(arenas, streams):
+                if rep:
+                    with torch.cuda.stream(s):
+                        a.copy_(arena0)
+                batch.seal_uniform(c, a, STRIDE, n, L, 1, nonces, status=None, stream=s)
+        torch.cuda.synchronize()
+        for a in arenas:
+            assert np.array_equal(a.cpu().numpy(), want)
+    finally:
+        c.close()
