@@ -43,7 +43,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, MI355X_MICROARCH.md "Chip-level para
 COPY_GUIDE_GBS = 6290.0  # the same table's measured float4 copy (read + write)
 # PMC passes of this command (tools/pmc_traffic.py), newest first
 LAUNCH_CHUNK = 1 << 20  # quantum_amd/csrc/gcm_internal.h kLaunchChunk
-TRAFFIC_JSONS = [os.path.join(ROOT, "profiles", d, "traffic.json") for d in ("r6_s22", "r6_s12", "r6_s10", "r6_s3", "r5_s37", "r5_s7", "r4_s21", "r4_s3", "r3_s39", "r3_s15", "r3_s1")]
+TRAFFIC_JSONS = [os.path.join(ROOT, "profiles", d, "traffic.json") for d in ("r6_s26", "r6_s22", "r6_s12", "r6_s10", "r6_s3", "r5_s37", "r5_s7", "r4_s21", "r4_s3", "r3_s39", "r3_s15", "r3_s1")]
 CONFIG4_PACKETS = 64 << 20  # BASELINE config 4: 64 M packets over the node's GPUs
 SECRET = b"AES256Key-32Characters1234567890"
 SALT = bytes(range(32))
