@@ -66,7 +66,7 @@ struct Batch {
 // the launch's generation to Batch::pool_done).
 constexpr uint32_t kPoolDoneWord = 32;
 constexpr uint32_t kPoolSetWords = 64;
-constexpr uint32_t kPoolSets = 16;  // sets per context, each held by one stream at a time
+constexpr uint32_t kPoolSets = 4096;  // sets in a context's ring (1 MiB; QGCM_POOL_SETS at qgcm_create: fewer, for tests)
 bool quad_pool_global();            // the uniform kernel takes b.pool (QGCM_TILE_POOL=4)
 constexpr uint32_t kPwPowers = 128;    // flat GHASH up to d + 2 = 128 exponents (payloads up to 2016 B)
 constexpr uint32_t kPwBits = 6;                                  // comb window of the flat GHASH tables

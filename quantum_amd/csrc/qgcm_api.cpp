@@ -123,21 +123,17 @@ struct qgcm_ctx {
     hipEvent_t ws_done = nullptr;
     bool ws_pending = false;
 
-    // the uniform kernel's shared tail (gcm_kernels.hip QGCM_TILE_POOL): kPoolSets zeroed counter sets in
-    // device memory, each held by the stream that last launched with it (its handle: HIP keeps a
-    // destroyed stream's object, so its handle, until its queued work has run), so a stream's launches
-    // reuse its set in stream order with nothing in between (an event record between two launches costs
-    // ~3 us, profiles/r6_s23).  The grid's last wave writes the launch's generation to
-    // h_pool_done[k] (pinned) after zeroing the set; another stream takes a set only once that word holds
-    // the set's last generation (read here, or waited for on the new stream: hipStreamWaitValue32).
-    // Guarded by pool_mu.
+    // the uniform kernel's shared tail (gcm_kernels.hip QGCM_TILE_POOL): a ring of kPoolSets zeroed
+    // counter sets in device memory, one per launch in turn, whatever its stream, with nothing queued
+    // between launches (an event record there costs ~3 us, profiles/r6_s23).  The grid's last wave
+    // zeroes its set and posts the launch's generation to h_pool_done[k] (pinned); a set comes round
+    // again kPoolSets launches later, and if its last launch has not posted yet the new launch first waits
+    // for it on its own stream (hipStreamWaitValue32).  Guarded by pool_mu.
     uint32_t *d_pool = nullptr;
     uint32_t *h_pool_done = nullptr;
-    hipStream_t pool_owner[kPoolSets] = {};
-    uint32_t pool_gen[kPoolSets] = {};  // 0: never launched with
-    uint64_t pool_tick[kPoolSets] = {};
-    uint64_t pool_clock = 0;
-    uint32_t pool_next_gen = 0;
+    uint32_t pool_gen[kPoolSets] = {};  // generation of each set's last launch (0: none yet)
+    uint32_t pool_launches = 0;
+    uint32_t pool_sets = kPoolSets;  // sets in use (QGCM_POOL_SETS: a short ring, so tests reach the wait)
     std::mutex pool_mu;
 
     std::atomic<uint64_t> launches[QGCM_KERNEL_COUNTERS] = {};  // qgcm_launch_counts
@@ -385,31 +381,15 @@ int run_uniform(qgcm_ctx *ctx, bool seal, uint8_t *arena, uint64_t stride, uint3
         const int grid = grid_for(ctx, c.n_items, v);
         // the shared tail needs two full rows of tiles (gcm_kernels.hip); smaller launches go without it
         const uint64_t rows = ((uint64_t)c.n_items / 16) / ((uint64_t)grid * (uint64_t)variant_waves(v));
-        // (hipStreamPerThread names a different stream in every thread: such launches go without it)
-        const hipStream_t sid = s;
-        if (ctx->d_pool && rows >= 2 && s != hipStreamPerThread) {
+        if (ctx->d_pool && rows >= 2) {
             std::lock_guard<std::mutex> g(ctx->pool_mu);
-            int k = -1;
-            for (int j = 0; j < (int)kPoolSets && k < 0; ++j)
-                if (ctx->pool_gen[j] && ctx->pool_owner[j] == sid) k = j;  // this stream's own set
-            if (k < 0) {  // a set never used, else the least recently used one
-                for (int j = 0; j < (int)kPoolSets && k < 0; ++j)
-                    if (!ctx->pool_gen[j]) k = j;
-                if (k < 0) {
-                    k = 0;
-                    for (int j = 1; j < (int)kPoolSets; ++j)
-                        if (ctx->pool_tick[j] < ctx->pool_tick[k]) k = j;
-                    // the set's last launch (on another stream) has zeroed it once its generation is posted
-                    if (__atomic_load_n(ctx->h_pool_done + k, __ATOMIC_ACQUIRE) != ctx->pool_gen[k] &&
-                        hipStreamWaitValue32(s, ctx->h_pool_done + k, ctx->pool_gen[k], hipStreamWaitValueEq,
-                                             0xffffffffu) != hipSuccess)
-                        return QGCM_E_HIP;
-                }
-                ctx->pool_owner[k] = sid;
-            }
-            if (++ctx->pool_next_gen == 0) ctx->pool_next_gen = 1;  // generation 0 means "never used"
-            ctx->pool_gen[k] = ctx->pool_next_gen;
-            ctx->pool_tick[k] = ++ctx->pool_clock;
+            const uint32_t k = ctx->pool_launches % ctx->pool_sets;
+            if (ctx->pool_gen[k] && __atomic_load_n(ctx->h_pool_done + k, __ATOMIC_ACQUIRE) != ctx->pool_gen[k] &&
+                hipStreamWaitValue32(s, ctx->h_pool_done + k, ctx->pool_gen[k], hipStreamWaitValueEq, 0xffffffffu) !=
+                    hipSuccess)
+                return QGCM_E_HIP;
+            if (++ctx->pool_launches == 0) ctx->pool_launches = 1;
+            ctx->pool_gen[k] = ctx->pool_launches;  // unique among the sets' outstanding generations
             c.pool = ctx->d_pool + (size_t)k * kPoolSetWords;
             c.pool_done = ctx->h_pool_done + k;
             c.pool_gen = ctx->pool_gen[k];
@@ -740,6 +720,7 @@ qgcm_ctx *qgcm_create(int device, uint32_t max_keys, char *err, int errlen) {
     }
     for (int k = 0; ok && k < kPipeStreams; ++k)
         ok = hipStreamCreateWithFlags(&ctx->pipe[k], hipStreamNonBlocking) == hipSuccess;
+    ctx->pool_sets = (uint32_t)std::max(1, std::min((int)kPoolSets, env_int("QGCM_POOL_SETS", (int)kPoolSets)));
     if (ok && quad_pool_global()) {
         const size_t bytes = (size_t)kPoolSets * kPoolSetWords * 4;
         ok = hipMalloc(&ctx->d_pool, bytes) == hipSuccess && hipMemset(ctx->d_pool, 0, bytes) == hipSuccess &&

@@ -1,8 +1,9 @@
 """The uniform kernel's shared tail (gcm_kernels.hip QGCM_TILE_POOL 4): a launch's first rows of tiles go
 through each workgroup's LDS counter, its last rows through one global counter per launch (a ring of
-zeroed sets in the context, each reused only after the launch that last held it).  Checked against the
-oracle: launches with one full row, two, and several plus a ragged row (the tail starts only at two full
-rows), and many launches in flight on four streams at once, more than the ring holds."""
+zeroed counter sets in the context, one per launch in turn; a set that comes round before its last
+launch has posted its generation is waited for on the new launch's stream).  Checked against the
+oracle: launches with one full row, two, and several plus a ragged row (the tail starts only at two
+full rows), many launches in flight on four streams at once, and a ring of two sets under six streams."""
 import os
 import threading
 
@@ -27,19 +28,22 @@ def torch():
     return T
 
 
-def _ctx(chunk=None):
+def _ctx(chunk=None, sets=None):
     from quantum_amd.crypto import Context
 
-    old = os.environ.get("QGCM_LAUNCH_CHUNK")
-    if chunk is not None:
-        os.environ["QGCM_LAUNCH_CHUNK"] = str(chunk)
+    env = {"QGCM_LAUNCH_CHUNK": chunk, "QGCM_POOL_SETS": sets}
+    old = {k: os.environ.get(k) for k in env}
+    for k, v in env.items():
+        if v is not None:
+            os.environ[k] = str(v)
     try:
         return Context(device=0, max_keys=2)
     finally:
-        if old is None:
-            os.environ.pop("QGCM_LAUNCH_CHUNK", None)
-        else:
-            os.environ["QGCM_LAUNCH_CHUNK"] = old
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
 
 
 def _row_packets(torch) -> int:
@@ -88,13 +92,13 @@ def test_shared_tail_rows_vs_oracle(torch, aesgo, rows, extra):
 
 def test_shared_tail_many_launches_on_four_streams(torch, aesgo):
     """Four host threads, each on its own stream, each call cut into 3 launches of 2 rows (the last
-    ragged): seal, open, seal without synchronizing, 36 launches queued against a ring of 16 sets."""
+    ragged): seal, open, seal without synchronizing, 36 launches queued against a ring of 8 sets."""
     from quantum_amd import batch
 
     key = bytes.fromhex(aesgo["key"])
     rp = _row_packets(torch)
     n = 5 * rp + 999
-    c = _ctx(chunk=2 * rp)
+    c = _ctx(chunk=2 * rp, sets=8)
     try:
         c.set_key(1, key)
         jobs = []
@@ -129,21 +133,22 @@ def test_shared_tail_many_launches_on_four_streams(torch, aesgo):
         c.close()
 
 
-def test_shared_tail_sets_taken_over_by_more_streams_than_sets(torch, aesgo):
-    """20 streams, more than the context's 16 sets: the later streams take over sets other streams last
-    launched with (each waits, on its own stream, for the generation that set's last launch posts).  Every
-    stream seals its own copy of one arena twice without synchronizing; all must equal the oracle."""
+def test_shared_tail_short_ring_waits_for_posted_generations(torch, aesgo):
+    """A ring of two counter sets (QGCM_POOL_SETS=2) under six streams, two seals each without
+    synchronizing: nearly every launch finds its set's previous launch (on another stream) still queued or
+    running and waits, on its own stream, for the generation that launch posts.  Every stream seals its
+    own copy of one arena; all must equal the oracle."""
     from quantum_amd import batch
 
     key = bytes.fromhex(aesgo["key"])
     n = 2 * _row_packets(torch) + 333
-    c = _ctx()
+    c = _ctx(sets=2)
     try:
         c.set_key(1, key)
         arena0, nonces = _fill(torch, n, 0x5E750000)
         plain = arena0.cpu().numpy()
         want = _oracle(key, plain, n, nonces.cpu().numpy())
-        streams = [torch.cuda.Stream() for _ in range(20)]
+        streams = [torch.cuda.Stream() for _ in range(6)]
         arenas = [arena0.clone() for _ in streams]
         torch.cuda.synchronize()
         for rep in range(2):
