@@ -389,11 +389,11 @@ int run_uniform(qgcm_ctx *ctx, bool seal, uint8_t *arena, uint64_t stride, uint3
                     hipSuccess)
                 return QGCM_E_HIP;
             if (++ctx->pool_launches == 0) ctx->pool_launches = 1;
-            ctx->pool_gen[k] = ctx->pool_launches;  // unique among the sets' outstanding generations
             c.pool = ctx->d_pool + (size_t)k * kPoolSetWords;
             c.pool_done = ctx->h_pool_done + k;
-            c.pool_gen = ctx->pool_gen[k];
+            c.pool_gen = ctx->pool_launches;  // unique among the sets' outstanding generations
             if (launch_packets(seal, v, c, grid, s) != hipSuccess) return QGCM_E_HIP;
+            ctx->pool_gen[k] = c.pool_gen;  // (a launch that never started posts nothing to wait for)
         } else if (launch_packets(seal, v, c, grid, s) != hipSuccess) {
             return QGCM_E_HIP;
         }
