@@ -1005,11 +1005,11 @@ __device__ __forceinline__ uint32_t wave_lower_bound(uint32_t lo, uint32_t hi, u
 
 // QGCM_SEG_STATS (side builds only, tools/seg_stats.py): per-workgroup counters of the segmented
 // kernel in a device array: phases, tiles, start/end (100 MHz clock), waves' idle and busy time,
-// table fills, wave 0's time finding runs.
+// table fills, wave 0's time finding runs; [8] XCC id, [9] HW_ID (which CU).
 #ifdef QGCM_SEG_STATS
-__device__ unsigned long long g_seg_stats[4096 * 8];
+__device__ unsigned long long g_seg_stats[4096 * 16];
 #define SEG_STAT_ADD(i, v) \
-    do { if (lane == 0) atomicAdd(&g_seg_stats[blockIdx.x * 8u + (i)], (unsigned long long)(v)); } while (0)
+    do { if (lane == 0) atomicAdd(&g_seg_stats[blockIdx.x * 16u + (i)], (unsigned long long)(v)); } while (0)
 #define SEG_NOW() wall_clock64()
 #else
 #define SEG_STAT_ADD(i, v) do { } while (0)
@@ -1120,6 +1120,8 @@ gcm_seg_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
         const uint32_t i = wave_lower_bound(0u, nruns, lane, [&](uint32_t j) { return j == nruns || b.runs[j].x > t; });
         r = i ? i - 1u : 0u;
         SEG_STAT_ADD(6, r);
+        SEG_STAT_ADD(8, __builtin_amdgcn_s_getreg((31 << 11) | 20));  // HW_REG_XCC_ID
+        SEG_STAT_ADD(9, __builtin_amdgcn_s_getreg((31 << 11) | 4));   // HW_REG_HW_ID
     }
     __syncthreads();
     [[maybe_unused]] unsigned long long t_idle = SEG_NOW();
@@ -1172,10 +1174,10 @@ gcm_seg_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
 
 #ifdef QGCM_SEG_STATS
 extern "C" int qgcm_debug_seg_stats(unsigned long long *out, int n, int reset) {
-    if (n > 4096 * 8) n = 4096 * 8;
+    if (n > 4096 * 16) n = 4096 * 16;
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_seg_stats), (size_t)n * 8) != hipSuccess) return -1;
     if (reset) {
-        static unsigned long long zero[4096 * 8];
+        static unsigned long long zero[4096 * 16];
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_seg_stats), zero, sizeof(zero)) != hipSuccess) return -1;
     }
     return 0;

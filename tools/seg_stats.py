@@ -1,5 +1,6 @@
 """Per-workgroup statistics of the segmented descriptor kernel (variant 14) from a side build with
--DQGCM_SEG_STATS: phases, tiles, span, idle/busy wave time, table fills.
+-DQGCM_SEG_STATS: phases, tiles, span, idle/busy wave time, table fills, and the end of each CU (both
+its workgroups done) by XCC.
 Usage: python tools/seg_stats.py path/to/libqgcm_stats.so   (AB_KEYS / AB_LEN as tools/ab_desc.py)
 """
 import ctypes as C
@@ -37,7 +38,7 @@ d_seal = batch.make_descs(offs, lens, kidx, "cuda")
 d_open = batch.make_descs(offs, lens + 28, kidx, "cuda")
 L = _lib.lib()
 L.qgcm_debug_seg_stats.argtypes = [C.c_void_p, C.c_int, C.c_int]
-buf = np.zeros(4096 * 8, dtype=np.uint64)
+buf = np.zeros(4096 * 16, dtype=np.uint64)
 for it in range(6):
     seal = it % 2 == 0
     L.qgcm_debug_seg_stats(buf.ctypes.data, buf.size, 1)
@@ -50,7 +51,7 @@ for it in range(6):
     e[1].record()
     torch.cuda.synchronize()
     L.qgcm_debug_seg_stats(buf.ctypes.data, buf.size, 0)
-    st = buf.reshape(-1, 8).astype(np.int64)
+    st = buf.reshape(-1, 16).astype(np.int64)
     st = st[st[:, 2] > 0]
     span = (st[:, 3] - st[:, 2]) / 100.0  # us (100 MHz)
     t0 = st[:, 2].min()
@@ -66,3 +67,11 @@ for it in range(6):
     print(f"  home runs: {len(np.unique(homes))} distinct, first 8 {homes[:8].tolist()}, max {homes.max()}")
     ends = np.sort((st[:, 3] - t0) / 100)
     print("  WG end times (us) deciles:", [int(x) for x in np.quantile(ends, [0, .1, .25, .5, .75, .9, 1])])
+    xcc = st[:, 8] & 0xF
+    cu = (xcc << 8) | ((st[:, 9] >> 8) & 0xFF)
+    keys, inv = np.unique(cu, return_inverse=True)
+    cend = np.array([st[inv == c, 3].max() for c in range(len(keys))]) - t0
+    cx = np.array([xcc[inv == c][0] for c in range(len(keys))])
+    print(f"  CUs {len(keys)}: CU idle at the end {float((cend.max() - cend).mean() / cend.max()):.4f} of the span; "
+          "mean CU end per XCC (us):", [round(float(cend[cx == x].mean()) / 100) for x in np.unique(cx)],
+          "tiles per XCC:", [int(st[xcc == x, 1].sum()) for x in np.unique(xcc)], flush=True)
