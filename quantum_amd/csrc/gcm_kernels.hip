@@ -1034,6 +1034,11 @@ __device__ unsigned long long g_seg_stats[4096 * 16];
 #ifndef QGCM_SEG_HELP_MIN
 #define QGCM_SEG_HELP_MIN 16
 #endif
+// QGCM_SEG_LAST = n > 0: when no run has QGCM_SEG_HELP_MIN tiles left (the launch's end), a helper joins a
+// run with at least n unclaimed tiles rather than leave: its CU would idle otherwise (profiles/r6_s29).
+#ifndef QGCM_SEG_LAST
+#define QGCM_SEG_LAST 0
+#endif
 __device__ __forceinline__ void seg_next_phase(const Batch &b, uint32_t &r, uint32_t nruns, bool &helping,
                                                uint32_t lane) {
     uint32_t found = kSegDone;
@@ -1052,6 +1057,8 @@ __device__ __forceinline__ void seg_next_phase(const Batch &b, uint32_t &r, uint
             r = (uint32_t)(((uint64_t)(h ^ (h >> 15)) * nruns) >> 32);
         }
         // four runs per lane per step (their loads in flight together): 256 runs per step
+        for (uint32_t pass = 0, need = QGCM_SEG_HELP_MIN; pass < (QGCM_SEG_LAST ? 2u : 1u) && found == kSegDone;
+             ++pass, need = QGCM_SEG_LAST ? QGCM_SEG_LAST : 1u)
         for (uint32_t base = 0; base < nruns; base += 256u) {
             bool left[4];
             uint32_t idx[4];
@@ -1065,7 +1072,7 @@ __device__ __forceinline__ void seg_next_phase(const Batch &b, uint32_t &r, uint
                 if (o < nruns) {
                     const uint2 run = b.runs[i];
                     left[j] = __hip_atomic_load(b.run_next + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) +
-                                  QGCM_SEG_HELP_MIN <= run.y - run.x;
+                                  need <= run.y - run.x;
                 }
             }
 #pragma unroll
