@@ -825,7 +825,8 @@ gcm_quad_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
 #define QS_END() do { } while (0)
 #endif
 #if QGCM_TILE_POOL == 4
-    // The launch's last rows of tiles through one global counter (b.pool, one zeroed set per launch):
+    // The launch's last rows of tiles through one global counter (b.pool, a zeroed set from the context's
+    // ring, one per launch):
     // each workgroup first takes its own tiles of rows [0, srow) from its LDS counter as in mode 1, then
     // every wave draws from the shared tail [srow * grid * 16, ntiles), so the XCDs, which run at
     // different speeds (tools/quad_stats.py), end together instead of idling while the slowest finishes.
@@ -940,7 +941,8 @@ gcm_quad_kernel(Batch b, const uint32_t *__restrict__ rk_table) {
                 __threadfence();
                 b.pool[0] = 0;
                 b.pool[kPoolDoneWord] = 0;
-                // the set is free for another stream: post this launch's generation to the host word
+                // the set is free for the launch that next takes it from the ring: post this launch's
+                // generation to the host word (that launch waits for it if it comes round early)
                 __threadfence_system();
                 __hip_atomic_store(b.pool_done, b.pool_gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
             }
