@@ -899,6 +899,7 @@ class GpuTelemetry:
             clks = [c] if c else []
         power = self._num(m.get("current_socket_power")) or self._num(m.get("average_socket_power"))
         return {"t": time.perf_counter(), "sclk": sum(clks) / len(clks) if clks else None, "power": power,
+                "xcd": clks if isinstance(clk, (list, tuple)) and len(clks) > 1 else None,
                 "uclk": self._num(m.get("current_uclk")), "socclk": self._num(m.get("current_socclk")),
                 "hotspot": self._num(m.get("temperature_hotspot")),
                 "acc": {k: self._num(m.get(k)) for k in ("accumulation_counter", "ppt_residency_acc",
@@ -927,6 +928,12 @@ class GpuTelemetry:
             self._th.join()
             self.last = self._read()
 
+    def _per_xcd(self):
+        xs = [x["xcd"] for x in self.samples if x.get("xcd")]
+        if not xs or len({len(x) for x in xs}) != 1:
+            return None
+        return [round(sum(c) / len(c), 1) for c in zip(*xs)]
+
     def summary(self) -> dict:
         if self.h is None or not self.samples:
             return {"sclk_mhz_mean": None, "power_w_mean": None, "power_cap_w": None,
@@ -945,6 +952,8 @@ class GpuTelemetry:
                "sclk_mhz_min": min(clk) if clk else None, "sclk_mhz_max": max(clk) if clk else None,
                "power_w_mean": round(sum(pw) / len(pw), 1) if pw else None, "power_w_max": max(pw) if pw else None,
                "power_cap_w": cap, "samples": len(self.samples),
+               # per-XCD GFX clocks (the XCDs run at different speeds: DESIGN.md 4.1, the shared tail)
+               "sclk_mhz_mean_per_xcd": self._per_xcd(),
                **{f"{k}_mean": (round(sum(v) / len(v), 1) if v else None)
                   for k, v in (("uclk_mhz", [x["uclk"] for x in self.samples if x["uclk"]]),
                                ("socclk_mhz", [x["socclk"] for x in self.samples if x["socclk"]]),

@@ -42,10 +42,15 @@ def main() -> None:
     lib = _lib.lib()
     lib.qgcm_debug_quad_stats.argtypes = [C.c_void_p, C.c_int, C.c_int]
     buf = np.zeros(4096 * 8, dtype=np.uint64)
+    tele = bench.GpuTelemetry(0)  # per-XCD clocks over the settle loop (the launches below run one at a time)
+    tele.start()
     for _ in range(40):  # settle the clock at this load
         batch.seal_uniform(ctx, arena, stride, N, L, 0, nonces, status=None)
         batch.open_uniform(ctx, arena, stride, N, L + 28, 0, status=status)
     torch.cuda.synchronize()
+    tele.stop()
+    clocks = tele.summary()
+    tele.close()
     rows = []
     for it in range(launches):
         seal = it % 2 == 0
@@ -113,7 +118,10 @@ def main() -> None:
         rows.append(row)
         print(json.dumps(row), flush=True)
     ok = int(status.sum().item()) == N
-    print(json.dumps({"summary": True, "status_ok": ok,
+    print(json.dumps({"summary": True, "status_ok": ok, "sclk_mhz_mean": clocks.get("sclk_mhz_mean"),
+                      "sclk_mhz_mean_per_xcd": clocks.get("sclk_mhz_mean_per_xcd"),
+                      "mean_cu_end_us_per_xcc_all": {x: round(float(np.mean([r["mean_cu_end_us_per_xcc"][x] for r in rows])), 1)
+                                                     for x in rows[0]["mean_cu_end_us_per_xcc"]},
                       "median_cu_idle_frac": float(np.median([r["cu_idle_frac"] for r in rows])),
                       "median_wg_tail_frac": float(np.median([r["wg_tail_frac"] for r in rows])),
                       "median_wave_tail_frac": float(np.median([r["wave_tail_frac"] for r in rows])),
