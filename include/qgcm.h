@@ -342,7 +342,9 @@ int qgcm_tun_close(int fd);
 #define QGCM_KERNEL_RESIDENT 4  /* per-packet calls served by the resident kernel (requests, not launches) */
 #define QGCM_KERNEL_SNAPPY_ENC 5 /* snappy_compress_kernel (device codec; chained calls: one per device chunk) */
 #define QGCM_KERNEL_SNAPPY_DEC 6 /* snappy_uncompress_kernel */
-#define QGCM_KERNEL_COUNTERS 7
+#define QGCM_KERNEL_TAIL_WAITS 7 /* uniform launches that waited, on their stream, for their shared-tail counter
+                                    set's previous launch (the context's ring came round; not a launch) */
+#define QGCM_KERNEL_COUNTERS 8
 int qgcm_launch_counts(const qgcm_ctx *ctx, uint64_t *out, int n);
 
 /* ---- measurement: achievable HBM copy rate (reads + writes bytes) for the roofline ---- */

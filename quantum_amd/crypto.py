@@ -61,7 +61,7 @@ class Context:
 
     def launch_counts(self) -> dict:
         """Kernel launches that served this context's calls so far (qgcm_launch_counts)."""
-        names = ("quad", "segmented", "per_wave", "one", "resident", "snappy_enc", "snappy_dec")
+        names = ("quad", "segmented", "per_wave", "one", "resident", "snappy_enc", "snappy_dec", "tail_waits")
         out = (C.c_uint64 * len(names))()
         _lib.check(_lib.lib().qgcm_launch_counts(self.handle, out, len(names)), "qgcm_launch_counts")
         return dict(zip(names, (int(x) for x in out)))

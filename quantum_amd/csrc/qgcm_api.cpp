@@ -384,10 +384,12 @@ int run_uniform(qgcm_ctx *ctx, bool seal, uint8_t *arena, uint64_t stride, uint3
         if (ctx->d_pool && rows >= 2) {
             std::lock_guard<std::mutex> g(ctx->pool_mu);
             const uint32_t k = ctx->pool_launches % ctx->pool_sets;
-            if (ctx->pool_gen[k] && __atomic_load_n(ctx->h_pool_done + k, __ATOMIC_ACQUIRE) != ctx->pool_gen[k] &&
-                hipStreamWaitValue32(s, ctx->h_pool_done + k, ctx->pool_gen[k], hipStreamWaitValueEq, 0xffffffffu) !=
+            if (ctx->pool_gen[k] && __atomic_load_n(ctx->h_pool_done + k, __ATOMIC_ACQUIRE) != ctx->pool_gen[k]) {
+                if (hipStreamWaitValue32(s, ctx->h_pool_done + k, ctx->pool_gen[k], hipStreamWaitValueEq, 0xffffffffu) !=
                     hipSuccess)
-                return QGCM_E_HIP;
+                    return QGCM_E_HIP;
+                ctx->count(QGCM_KERNEL_TAIL_WAITS);
+            }
             if (++ctx->pool_launches == 0) ctx->pool_launches = 1;
             c.pool = ctx->d_pool + (size_t)k * kPoolSetWords;
             c.pool_done = ctx->h_pool_done + k;

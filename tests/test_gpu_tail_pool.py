@@ -78,7 +78,7 @@ def test_shared_tail_rows_vs_oracle(torch, aesgo, rows, extra):
         arena, nonces = _fill(torch, n, 0x7A110000 + rows)
         plain = arena.cpu().numpy()
         status = torch.zeros(n, dtype=torch.uint8, device="cuda")
-        for _ in range(2):  # the same set of the ring again, after the grid's last wave zeroed it
+        for _ in range(2):  # two launches, each with the next set of the ring
             arena.copy_(torch.from_numpy(plain).cuda())
             batch.seal_uniform(c, arena, STRIDE, n, L, 1, nonces, status=status)
             assert np.array_equal(arena.cpu().numpy(), _oracle(key, plain, n, nonces.cpu().numpy()))
@@ -86,6 +86,7 @@ def test_shared_tail_rows_vs_oracle(torch, aesgo, rows, extra):
         batch.open_uniform(c, arena, STRIDE, n, L + 28, 1, status=status)
         assert int(status.sum()) == n
         assert np.array_equal(arena.cpu().numpy().reshape(n, STRIDE)[:, :4 + L], plain.reshape(n, STRIDE)[:, :4 + L])
+        assert c.launch_counts()["tail_waits"] == 0  # a 4096-set ring never comes round here
     finally:
         c.close()
 
@@ -151,6 +152,7 @@ def test_shared_tail_short_ring_waits_for_posted_generations(torch, aesgo):
         streams = [torch.cuda.Stream() for _ in range(6)]
         arenas = [arena0.clone() for _ in streams]
         torch.cuda.synchronize()
+        w0 = c.launch_counts()["tail_waits"]
         for rep in range(2):
             for a, s in zip(arenas, streams):
                 if rep:
@@ -158,6 +160,7 @@ def test_shared_tail_short_ring_waits_for_posted_generations(torch, aesgo):
                         a.copy_(arena0)
                 batch.seal_uniform(c, a, STRIDE, n, L, 1, nonces, status=None, stream=s)
         torch.cuda.synchronize()
+        assert c.launch_counts()["tail_waits"] > w0  # the ring came round on launches still queued
         for a in arenas:
             assert np.array_equal(a.cpu().numpy(), want)
     finally:
