@@ -51,18 +51,18 @@ def _row_packets(torch) -> int:
     return torch.cuda.get_device_properties(0).multi_processor_count * 2 * 16 * 16
 
 
-def _fill(torch, n, seed):
+def _fill(torch, n, seed, length=L, stride=STRIDE):
     from quantum_amd import batch
 
-    arena = torch.zeros(n * STRIDE, dtype=torch.uint8, device="cuda")
+    arena = torch.zeros(n * stride, dtype=torch.uint8, device="cuda")
     nonces = torch.zeros(12 * n, dtype=torch.uint8, device="cuda")
-    batch.fill_uniform(arena, STRIDE, n, L, AAD_WORD, seed, nonces, seed + 1)
+    batch.fill_uniform(arena, stride, n, length, AAD_WORD, seed, nonces, seed + 1)
     return arena, nonces
 
 
-def _oracle(key, plain, n, nonces):
+def _oracle(key, plain, n, nonces, length=L, stride=STRIDE):
     ref = plain.copy()
-    O.lib().oracle_seal_uniform(key, ref.ctypes.data, STRIDE, n, L, 4, nonces.ctypes.data)
+    O.lib().oracle_seal_uniform(key, ref.ctypes.data, stride, n, length, 4, nonces.ctypes.data)
     return ref
 
 
@@ -143,12 +143,13 @@ def test_shared_tail_short_ring_waits_for_posted_generations(torch, aesgo):
 
     key = bytes.fromhex(aesgo["key"])
     n = 2 * _row_packets(torch) + 333
+    ln, st = 1350, 1408  # ~0.4 ms a launch, far longer than a host call: the ring comes round on launches queued
     c = _ctx(sets=2)
     try:
         c.set_key(1, key)
-        arena0, nonces = _fill(torch, n, 0x5E750000)
+        arena0, nonces = _fill(torch, n, 0x5E750000, ln, st)
         plain = arena0.cpu().numpy()
-        want = _oracle(key, plain, n, nonces.cpu().numpy())
+        want = _oracle(key, plain, n, nonces.cpu().numpy(), ln, st)
         streams = [torch.cuda.Stream() for _ in range(6)]
         arenas = [arena0.clone() for _ in streams]
         torch.cuda.synchronize()
@@ -158,7 +159,7 @@ def test_shared_tail_short_ring_waits_for_posted_generations(torch, aesgo):
                 if rep:
                     with torch.cuda.stream(s):
                         a.copy_(arena0)
-                batch.seal_uniform(c, a, STRIDE, n, L, 1, nonces, status=None, stream=s)
+                batch.seal_uniform(c, a, st, n, ln, 1, nonces, status=None, stream=s)
         torch.cuda.synchronize()
         assert c.launch_counts()["tail_waits"] > w0  # the ring came round on launches still queued
         for a in arenas:
